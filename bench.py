@@ -1,0 +1,315 @@
+#!/usr/bin/env python3
+"""Benchmark of the NConv depth-completion hot path on MI355X.
+
+Headline (BASELINE.json metric, config 2): frames/sec of the unguided NConv U-Net (DNET /
+SETP1_NCONV, models/step1.py:15-94) forward on B=8 synthetic KITTI-shaped 352x1216 sparse depth
+per GPU, fp32, inputs resident in HBM. Also reported (same JSON line): fwd+bwd+AdamW training-step
+frames/sec (config 4b: EnforcePos drift + calculate_loss + backward + AdamW, train_step1.py:59-65),
+per-layer kernel times, the roofline of the dominant kernel, and the CPU baseline (the oracle's
+restatement of the reference, timed on this host's cores).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 8] [--height 352] [--width 1216]
+    torchrun --nproc-per-node N bench.py --gpus N ...      # one process per GPU, RCCL
+
+Multi-GPU: frames are independent units, so each rank runs its own B frames (weak scaling) with
+no collective in the forward; the training step all-reduces gradients over RCCL (one bucket).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md, chip-level parameters (spec)
+FP32_PEAK_TFLOPS = 157.3   # same table: FP32 vector / matrix peak
+LAYERS = ("nconv1", "nconv2", "nconv_down1", "nconv_down2", "nconv_down3", "nconv4", "nconv5", "nconv6", "nconv7")
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--batch", type=int, default=8)
+    p.add_argument("--height", type=int, default=352)
+    p.add_argument("--width", type=int, default=1216)
+    p.add_argument("--train-steps", type=int, default=None, help="timed fwd+bwd steps (default: --steps)")
+    p.add_argument("--no-train", action="store_true")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--graph", type=int, default=1, help="capture the forward in a hipGraph (1) or run eager (0)")
+    return p.parse_args()
+
+
+def sparse_depth(g, B, H, W, device):
+    d = torch.rand(B, 1, H, W, generator=g) * 79 + 1
+    d = d * (torch.rand(B, 1, H, W, generator=g) < 0.05)
+    return d.to(device)
+
+
+# ---- algorithmic per-layer cost --------------------------------------------------
+def layer_costs(B, H, W):
+    """Per fused layer: (bytes, flops) per launch. Bytes: each layer reads its producers' x and c
+    once at their native resolution (glue fused) and writes y and c once; nconv1 reads S only.
+    Flops: 2 convs x 2 flop/FMA x Cin x k^2 x Cout per output pixel, + 4*Cout (div, bias, conf)."""
+    f = 4
+    H2, W2, H4, W4, H8, W8 = H // 2, W // 2, H // 4, W // 4, H // 8, W // 8
+    px = lambda h, w: B * h * w
+    c = {}
+    c["nconv1"] = (px(H, W) * (1 * f + 16 * f), px(H, W) * (2 * 2 * 1 * 25 * 8 + 32))
+    c["nconv2"] = (px(H, W) * (16 * f + 16 * f), px(H, W) * (2 * 2 * 8 * 25 * 8 + 32))
+    c["nconv_down1"] = (px(H, W) * 16 * f + px(H2, W2) * 16 * f, px(H2, W2) * (6400 + 32))
+    c["nconv_down2"] = (px(H2, W2) * 16 * f + px(H4, W4) * 16 * f, px(H4, W4) * (6400 + 32))
+    c["nconv_down3"] = (px(H4, W4) * 16 * f + px(H8, W8) * 16 * f, px(H8, W8) * (6400 + 32))
+    c["nconv4"] = (px(H4, W4) * 16 * f + px(H8, W8) * 16 * f + px(H4, W4) * 16 * f,
+                   px(H4, W4) * (2 * 2 * 16 * 9 * 8 + 32))
+    c["nconv5"] = (px(H2, W2) * 16 * f + px(H4, W4) * 16 * f + px(H2, W2) * 16 * f,
+                   px(H2, W2) * (2 * 2 * 16 * 9 * 8 + 32))
+    c["nconv6"] = (px(H, W) * 16 * f + px(H2, W2) * 16 * f + px(H - 2, W - 2) * 16 * f,
+                   px(H - 2, W - 2) * (2 * 2 * 16 * 9 * 8 + 32))
+    c["nconv7"] = (px(H - 2, W - 2) * 16 * f + px(H + 2, W + 2) * 1 * f, px(H + 2, W + 2) * (2 * 2 * 8 + 4))
+    return c
+
+
+def fused_tail_cost(B, H, W):
+    """nconv6+nconv7 fused launch (inference): reads nconv6's inputs, writes the final output."""
+    H2, W2 = H // 2, W // 2
+    byt = (B * H * W * 16 + B * H2 * W2 * 16 + B * H * W * 1) * 4
+    fl = B * (H - 2) * (W - 2) * (2 * 2 * 16 * 9 * 8 + 32) + B * H * W * (2 * 2 * 8 + 4)
+    return byt, fl
+
+
+def time_layers(m, net, S, reps=20):
+    """Average device time per launch of each forward kernel (HIP events on the launch stream)."""
+    lib = m._lib
+    d = net.d_net
+    layers = [getattr(d, n) for n in LAYERS]
+    wsum = d._prologue(layers, S)
+    specs = [layers[0].spec(lib.THRESH, 0.01), layers[1].spec(), layers[2].spec(lib.POOL2),
+             layers[3].spec(lib.POOL2), layers[4].spec(lib.POOL2), layers[5].spec(lib.UPCAT_SKIP_FIRST),
+             layers[6].spec(lib.UPCAT_SKIP_FIRST), layers[7].spec(lib.UPCAT_UP_FIRST), layers[8].spec()]
+    fwd = m.nconv.layer_forward_raw
+    with torch.no_grad():
+        x1, c1 = fwd(specs[0], S, None, None, None, layers[0].weight, layers[0].bias, wsum[0])
+        x1b, c1b = fwd(specs[1], x1, c1, None, None, layers[1].weight, layers[1].bias, wsum[1])
+        x2, c2 = fwd(specs[2], x1b, c1b, None, None, layers[2].weight, layers[2].bias, wsum[2])
+        x3, c3 = fwd(specs[3], x2, c2, None, None, layers[3].weight, layers[3].bias, wsum[3])
+        x4, c4 = fwd(specs[4], x3, c3, None, None, layers[4].weight, layers[4].bias, wsum[4])
+        x34, c34 = fwd(specs[5], x3, c3, x4, c4, layers[5].weight, layers[5].bias, wsum[5])
+        x23, c23 = fwd(specs[6], x2, c2, x34, c34, layers[6].weight, layers[6].bias, wsum[6])
+        x6, c6 = fwd(specs[7], x1b, c1b, x23, c23, layers[7].weight, layers[7].bias, wsum[7])
+    args = [(S, None, None, None), (x1, c1, None, None), (x1b, c1b, None, None), (x2, c2, None, None),
+            (x3, c3, None, None), (x3, c3, x4, c4), (x2, c2, x34, c34), (x1b, c1b, x23, c23), (x6, c6, None, None)]
+    out = {}
+    H, W = S.shape[2], S.shape[3]
+    oh, ow = m.crop_hw(H, W, d.crop)
+    stream = torch.cuda.current_stream()
+    for name, spec, lay, a, s in zip(LAYERS, specs, layers, args, wsum):
+        with torch.no_grad():
+            fwd(spec, *a, lay.weight, lay.bias, s)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(reps):
+                fwd(spec, *a, lay.weight, lay.bias, s)
+            e1.record(stream)
+        e1.synchronize()
+        out[name] = e0.elapsed_time(e1) / reps * 1e3  # us
+    with torch.no_grad():
+        d._fused_tail(layers[7], layers[8], wsum[7], wsum[8], x1b, c1b, x23, c23, oh, ow)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            d._fused_tail(layers[7], layers[8], wsum[7], wsum[8], x1b, c1b, x23, c23, oh, ow)
+        e1.record(stream)
+    e1.synchronize()
+    out["nconv6+7_tail"] = e0.elapsed_time(e1) / reps * 1e3
+    return out
+
+
+def cpu_baseline(B, H, W, seconds):
+    """The oracle (oracle/nconv_ref.py: the reference's DNET forward restated with the same torch
+    CPU ops; bitwise equal to the reference on the same torch build) timed on this host."""
+    from oracle import nconv_ref as R
+    import nconv_pkg
+    m = nconv_pkg.load()
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    torch.manual_seed(0)
+    net = m.SETP1_NCONV()
+    params = R.dnet_params_from_state_dict({k: R.softplus_pos(v) if k.endswith(".weight") and "bnorm" not in k
+                                            else v for k, v in net.state_dict().items()})
+    g = torch.Generator().manual_seed(0)
+    S = sparse_depth(g, 1, H, W, "cpu")
+    with torch.no_grad():
+        R.dnet_forward(S, params)  # warm-up
+        n, t0 = 0, time.perf_counter()
+        while True:
+            R.dnet_forward(S, params)
+            n += 1
+            el = time.perf_counter() - t0
+            if el >= seconds or n >= 200:
+                break
+    return {"value": n / el, "unit": "frames/sec", "cores": threads, "kind": "port",
+            "sample": f"{n} single-frame {H}x{W} DNET forwards (oracle/nconv_ref.dnet_forward, fp32, "
+                      f"torch CPU, {threads} threads) in {el:.1f} s"}
+
+
+def make_train_step(m, dev, B, H, W, world, rank):
+    """One step-1 training iteration as train_step1.py:59-65: train-mode forward (EnforcePos
+    drift), calculate_loss on element [0] with the gradient loss, backward, (RCCL gradient
+    all-reduce when world > 1), AdamW lr 1e-2 / wd 1e-7 (train_step1.py:16-17, utils.py:55)."""
+    torch.manual_seed(0)
+    net = m.dp.DataParallelRCCL(m.SETP1_NCONV(crop="generalized").to(dev))
+    opt = m.train.get_optimizer(net, "adam", 1e-2, 1e-7)
+    g = torch.Generator().manual_seed(2000 + rank)
+    S = sparse_depth(g, B, H, W, dev)
+    gt = sparse_depth(g, B, H, W, dev)
+    net.train()
+
+    def step():
+        opt.zero_grad()
+        est = net(S)
+        loss = m.train.calculate_loss(est[0, :, :, :], gt[0, :, :, :], True)
+        loss.backward()
+        net.allreduce_grads()
+        opt.step()
+    return step
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    import nconv_pkg
+    m = nconv_pkg.load()
+    B, H, W = a.batch, a.height, a.width
+    torch.manual_seed(0)
+    net = m.SETP1_NCONV(crop="generalized").to(dev)
+    net.train()
+    with torch.no_grad():
+        net(torch.zeros(1, 1, 32, 32, device=dev))  # one EnforcePos: positive (trained-like) weights
+    net.eval()
+    g = torch.Generator().manual_seed(1000 + rank)
+    S = sparse_depth(g, B, H, W, dev)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    # ---- forward (headline) ----
+    graph = None
+    with torch.no_grad():
+        for _ in range(max(a.warmup, 1)):
+            out = net(S)
+        if a.graph:
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                for _ in range(2):
+                    out = net(S)
+            torch.cuda.current_stream().wait_stream(s)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                out = net(S)
+            for _ in range(a.warmup):
+                graph.replay()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    with torch.no_grad():
+        for _ in range(a.steps):
+            if graph is not None:
+                graph.replay()
+            else:
+                out = net(S)
+    torch.cuda.synchronize()
+    barrier()
+    t_fwd = time.perf_counter() - t0
+    t_fwd_max = t_fwd
+    if world > 1:
+        t = torch.tensor([t_fwd], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        t_fwd_max = t.item()
+    fps = world * B * a.steps / t_fwd_max
+
+    # ---- fwd + bwd + AdamW (config 4b) ----
+    train = None
+    if not a.no_train:
+        step = make_train_step(m, dev, B, H, W, world, rank)
+        ks = a.train_steps or a.steps
+        for _ in range(max(a.warmup, 1)):
+            step()
+        torch.cuda.synchronize()
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(ks):
+            step()
+        torch.cuda.synchronize()
+        barrier()
+        tt = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([tt], device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            tt = t.item()
+        train = {"frames_per_sec": world * B * ks / tt, "ms_per_step": tt / ks * 1e3, "steps": ks}
+
+    # ---- per-kernel times, roofline (rank 0) ----
+    result = None
+    if rank == 0:
+        lt = time_layers(m, net, S)
+        costs = layer_costs(B, H, W)
+        dom = max(LAYERS, key=lambda n: lt[n])
+        byt, fl = costs[dom]
+        us = lt[dom]
+        gbs = byt / (us * 1e-6) / 1e9
+        tfl = fl / (us * 1e-6) / 1e12
+        tail_b, tail_f = fused_tail_cost(B, H, W)
+        pass_bytes = 238.44e6 * B if (H, W) == (352, 1216) else None
+        roof = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                "kernel": f"{dom} (fwd_tiled)", "kernel_us": round(us, 2),
+                "algorithmic_bytes_per_launch": byt, "flops_per_launch": fl,
+                "fp32_tflops": round(tfl, 2), "fp32_peak_tflops": FP32_PEAK_TFLOPS,
+                "fp32_frac": round(tfl / FP32_PEAK_TFLOPS, 4),
+                "whole_pass_hbm_frac": round(pass_bytes * a.steps / t_fwd / 1e9 / HBM_PEAK_GBS, 4) if pass_bytes else None}
+        cpu = None
+        if not a.no_cpu_baseline and world == 1:
+            cpu = cpu_baseline(1, H, W, a.cpu_seconds)
+        result = {
+            "metric": "frames/sec (352x1216 sparse depth, DNET NConv U-Net forward, B=8 per GPU)",
+            "value": round(fps, 2), "unit": "frames/sec", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(t_fwd_max / a.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "data": "synthetic (seeded 5%-dense U(1,80) depth, seeded init + one EnforcePos)",
+            "config": {"workload": "config2: SETP1_NCONV/DNET forward, fused HIP NConv kernels",
+                       "global_batch": B * world, "per_gpu_batch": B, "height": H, "width": W,
+                       "crop": "generalized [1:H+1,1:W+1]", "parallelism": f"frame-sharded x{world}",
+                       "hipgraph": bool(graph is not None)},
+            "train_fwd_bwd_adamw": train,
+            "layer_us": {k: round(v, 2) for k, v in lt.items()},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        if cpu:
+            result["speedup_vs_cpu"] = round(fps / cpu["value"], 1)
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

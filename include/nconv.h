@@ -1,0 +1,115 @@
+/*
+ * nconv.h — C ABI of libnconv.so, the MI355X (gfx950) normalized-convolution library.
+ *
+ * The reference (lllllcf/Realtime-Depth-Estimation-Nconv) has no native code: its boundary is the
+ * PyTorch nn.Module API of models/step1.py. Each entry point below replaces a specific group of
+ * PyTorch ops the reference issues on its hot path; the replaced file:line is cited per function.
+ * The Python host layer (realtime-depth-estimation-nconv_amd/) binds these with ctypes; see
+ * INTEGRATION.md for the binding a maintainer of the reference would add.
+ *
+ * Conventions (all entry points):
+ *   - every buffer is a caller-owned device pointer to contiguous fp32 NCHW memory; the library
+ *     never allocates, frees or synchronises;
+ *   - work is enqueued on `stream` (a hipStream_t passed as void*; NULL = the null stream);
+ *   - return 0 on success or a negative errno-style code; nconv_last_error() then describes it
+ *     (thread-local string, valid until the next call on the same thread);
+ *   - stateless and re-entrant; safe to capture into a hipGraph (no host sync inside).
+ */
+#ifndef NCONV_H
+#define NCONV_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NCONV_ABI_VERSION 1
+
+/* How a layer's input (data x, confidence c) is produced from its source tensors. These are the
+ * DNET glue ops fused into the layer's load stage (models/step1.py:53,61-90). */
+enum nconv_load_mode {
+    NCONV_LOAD_PLAIN = 0,            /* x = a.x, c = a.c                                   (step1.py:57,92)    */
+    NCONV_LOAD_THRESH = 1,           /* x = a.x, c = float(a.x > thresh)                    (step1.py:53-56)    */
+    NCONV_LOAD_POOL2 = 2,            /* x = maxpool2x2(a.x), c = maxpool2x2(a.c), independent (step1.py:62-75) */
+    NCONV_LOAD_UPCAT_SKIP_FIRST = 3, /* x = cat(a.x, up(b.x)), c likewise                   (step1.py:78-85)    */
+    NCONV_LOAD_UPCAT_UP_FIRST = 4    /* x = cat(up(b.x), a.x), c likewise                   (step1.py:88-90)    */
+};
+
+/* One source tensor pair (data, confidence), physical shape (B, C, H, W). */
+typedef struct nconv_src {
+    const float* x;
+    const float* c; /* may be NULL for NCONV_LOAD_THRESH */
+    int C, H, W;
+} nconv_src;
+
+/* One NConv2d application (models/step1.py:97-149) plus its fused input glue. */
+typedef struct nconv_layer {
+    int B;
+    int Cin, H, W;     /* logical layer input, after the glue (e.g. H = a.H/2 for POOL2)      */
+    int Cout, Ho, Wo;  /* output: Ho = (H + 2PH - DH(KH-1) - 1)/SH + 1                         */
+    int KH, KW, SH, SW, PH, PW, DH, DW, groups;
+    float eps;         /* NConv2d.eps = 1e-7 (step1.py:103)                                     */
+    int load_mode;     /* enum nconv_load_mode                                                  */
+    float thresh;      /* NCONV_LOAD_THRESH threshold, 0.01 in DNET (step1.py:53)               */
+    nconv_src a;       /* plain / thresholded / pooled / skip source                             */
+    nconv_src b;       /* low-resolution source of the UPCAT modes (unused otherwise)            */
+    const float* weight; /* (Cout, Cin/groups, KH, KW), positive in practice                   */
+    const float* bias;   /* (Cout)                                                              */
+    const float* wsum;   /* (Cout): s[o] = sum of weight[o] (step1.py:141-144), see nconv_weight_prep */
+} nconv_layer;
+
+/* ABI version, for the Python loader's sanity check. */
+int nconv_abi_version(void);
+
+/* Description of the last error on this thread ("" if none). */
+const char* nconv_last_error(void);
+
+/* EnforcePos + confidence-normaliser prologue for n layers in ONE launch.
+ * Replaces EnforcePos.__call__ (models/step1.py:190-193, softplus beta=10 threshold=20 at :206-207,
+ * applied in place when apply_softplus[i] != 0, i.e. module.training) and the per-layer
+ * s = weight.view(Cout,-1).sum(-1) of NConv2d.forward (models/step1.py:141-144).
+ * weights[i] has counts[i] = Cout_i * fan_in_i floats; wsums[i] receives Cout_i floats. */
+int nconv_weight_prep(int n, float* const* weights, const int* couts, const int* fan_ins,
+                      const int* apply_softplus, float* const* wsums, void* stream);
+
+/* Forward of one NConv2d with fused input glue.
+ * Replaces models/step1.py:119-147 (2x F.conv2d, mul, div, bias add, confidence normalisation)
+ * plus the glue op that feeds it (step1.py:53 / 62-75 / 78-90).
+ * y, cout: (B, Cout, Ho, Wo). */
+int nconv_fwd(const nconv_layer* L, float* y, float* cout, void* stream);
+
+/* Inference-only fused tail: the last 3x3 NConv (nconv6, step1.py:88-90) with its 1x1 successor
+ * (nconv7, step1.py:92) evaluated in the epilogue, written straight into the cropped output
+ * (step1.py:94). L6 describes nconv6 (stride 1, no dilation, groups 1). Output pixel (r, c) of
+ * `out` (B, 1, out_h, out_w) is nconv7's output at (r + 1, c + 1) of its (Ho6+2*p7) x (Wo6+2*p7)
+ * grid, i.e. nconv6 pixel (r + 1 - p7, c + 1 - p7); positions in nconv7's zero border get b7.
+ * out_c (nullable) receives the matching output confidence. */
+int nconv_fwd_tail(const nconv_layer* L6, const float* w7, const float* b7, const float* wsum7,
+                   int cin7, int p7, float eps7, float* out, float* out_c, int out_h, int out_w,
+                   void* stream);
+
+/* Workspace needed by nconv_bwd (bytes). */
+size_t nconv_bwd_workspace_bytes(const nconv_layer* L);
+
+/* Backward of nconv_fwd (autograd of models/step1.py:116-149 plus the glue's backward:
+ * max_pool2d routes to the first maximum of each window, nearest-upsample sums, cat splits).
+ * Inputs: y, cout (the forward outputs), gy, gcout (their gradients; gcout may be NULL = 0).
+ * Outputs (any may be NULL if not needed; all are ACCUMULATED into, caller zero-fills):
+ *   gxa, gca : gradients of source a's (x, c)      — same shape as a
+ *   gxb, gcb : gradients of source b's (x, c)      — same shape as b (UPCAT modes)
+ *   gw       : (Cout, Cin/groups, KH, KW) weight gradient, OVERWRITTEN
+ *   gbias    : (Cout) bias gradient, OVERWRITTEN
+ * The closed form: gN = gy/(D+eps), gD = -gy*N/(D+eps)^2 + gcout/s,
+ *   gb = sum gy, gs = -sum gcout*D/s^2, gW = corr(x*c, gN) + corr(c, gD) + gs,
+ *   g(xc) = W^T * gN, gx = g(xc)*c, gc = W^T * gD + g(xc)*x.
+ * D and N/(D+eps) are recovered from the saved outputs as cout*s and y-b. */
+int nconv_bwd(const nconv_layer* L, const float* y, const float* cout, const float* gy,
+              const float* gcout, float* gxa, float* gca, float* gxb, float* gcb, float* gw,
+              float* gbias, void* workspace, size_t workspace_bytes, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NCONV_H */

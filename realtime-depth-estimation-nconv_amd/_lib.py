@@ -1,0 +1,111 @@
+"""ctypes binding of libnconv.so (the C ABI in include/nconv.h).
+
+Loaded lazily on first use, after `import torch`, so the dynamic loader resolves the library's
+libamdhip64.so.7 to the HIP runtime torch already mapped (one HIP runtime per process).
+There is deliberately no fallback: a missing or unloadable library raises.
+"""
+import ctypes
+import os
+import threading
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libnconv.so")
+ABI_VERSION = 1
+
+# enum nconv_load_mode
+PLAIN, THRESH, POOL2, UPCAT_SKIP_FIRST, UPCAT_UP_FIRST = 0, 1, 2, 3, 4
+
+EXPORTED = (
+    "nconv_abi_version",
+    "nconv_last_error",
+    "nconv_weight_prep",
+    "nconv_fwd",
+    "nconv_fwd_tail",
+    "nconv_bwd_workspace_bytes",
+    "nconv_bwd",
+)
+
+
+class NconvSrc(ctypes.Structure):
+    _fields_ = [("x", ctypes.c_void_p), ("c", ctypes.c_void_p), ("C", ctypes.c_int),
+                ("H", ctypes.c_int), ("W", ctypes.c_int)]
+
+
+class NconvLayer(ctypes.Structure):
+    _fields_ = [("B", ctypes.c_int), ("Cin", ctypes.c_int), ("H", ctypes.c_int), ("W", ctypes.c_int),
+                ("Cout", ctypes.c_int), ("Ho", ctypes.c_int), ("Wo", ctypes.c_int),
+                ("KH", ctypes.c_int), ("KW", ctypes.c_int), ("SH", ctypes.c_int), ("SW", ctypes.c_int),
+                ("PH", ctypes.c_int), ("PW", ctypes.c_int), ("DH", ctypes.c_int), ("DW", ctypes.c_int),
+                ("groups", ctypes.c_int), ("eps", ctypes.c_float), ("load_mode", ctypes.c_int),
+                ("thresh", ctypes.c_float), ("a", NconvSrc), ("b", NconvSrc),
+                ("weight", ctypes.c_void_p), ("bias", ctypes.c_void_p), ("wsum", ctypes.c_void_p)]
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+def _declare(lib):
+    P = ctypes.c_void_p
+    lib.nconv_abi_version.restype = ctypes.c_int
+    lib.nconv_abi_version.argtypes = []
+    lib.nconv_last_error.restype = ctypes.c_char_p
+    lib.nconv_last_error.argtypes = []
+    lib.nconv_weight_prep.restype = ctypes.c_int
+    lib.nconv_weight_prep.argtypes = [ctypes.c_int, P, P, P, P, P, P]
+    lib.nconv_fwd.restype = ctypes.c_int
+    lib.nconv_fwd.argtypes = [ctypes.POINTER(NconvLayer), P, P, P]
+    lib.nconv_fwd_tail.restype = ctypes.c_int
+    lib.nconv_fwd_tail.argtypes = [ctypes.POINTER(NconvLayer), P, P, P, ctypes.c_int, ctypes.c_int,
+                                   ctypes.c_float, P, P, ctypes.c_int, ctypes.c_int, P]
+    lib.nconv_bwd_workspace_bytes.restype = ctypes.c_size_t
+    lib.nconv_bwd_workspace_bytes.argtypes = [ctypes.POINTER(NconvLayer)]
+    lib.nconv_bwd.restype = ctypes.c_int
+    lib.nconv_bwd.argtypes = [ctypes.POINTER(NconvLayer), P, P, P, P, P, P, P, P, P, P, P,
+                              ctypes.c_size_t, P]
+
+
+def lib():
+    """The loaded library. Raises RuntimeError if it is missing or incompatible."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise RuntimeError(
+                    f"libnconv.so not found at {LIB_PATH}; build it with "
+                    "`python -c 'import __graft_entry__ as g; g.build()'` (no fallback path exists)")
+            handle = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+            _declare(handle)
+            v = handle.nconv_abi_version()
+            if v != ABI_VERSION:
+                raise RuntimeError(f"libnconv ABI {v} != expected {ABI_VERSION}")
+            _lib = handle
+    return _lib
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = lib().nconv_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what} failed ({rc}): {msg}")
+
+
+def stream_handle(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def src(x, c):
+    """NconvSrc for a (B, C, H, W) pair (c may be None)."""
+    s = NconvSrc()
+    if x is not None:
+        s.x = x.data_ptr()
+        s.c = c.data_ptr() if c is not None else None
+        s.C, s.H, s.W = x.shape[1], x.shape[2], x.shape[3]
+    return s

@@ -1,0 +1,128 @@
+// nconv_capi.hip — the extern "C" boundary of libnconv.so (declared in include/nconv.h).
+// Validates every descriptor on the host before anything is enqueued, so a malformed call
+// returns -EINVAL instead of launching a kernel with out-of-range indexing.
+#include <stdio.h>
+#include <string>
+#include "nconv_internal.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fn, const char* why) {
+    g_err = std::string(fn) + ": " + (why ? why : "error");
+    return code;
+}
+
+const char* validate(const nconv_layer* L, bool need_c) {
+    if (!L) return "null layer descriptor";
+    if (L->B <= 0 || L->Cin <= 0 || L->Cout <= 0 || L->H <= 0 || L->W <= 0) return "non-positive B/Cin/Cout/H/W";
+    if (L->KH <= 0 || L->KW <= 0 || L->SH <= 0 || L->SW <= 0 || L->DH <= 0 || L->DW <= 0) return "non-positive kernel/stride/dilation";
+    if (L->PH < 0 || L->PW < 0) return "negative padding";
+    if (L->groups <= 0 || L->Cin % L->groups || L->Cout % L->groups) return "groups must divide Cin and Cout";
+    const int ho = (L->H + 2 * L->PH - L->DH * (L->KH - 1) - 1) / L->SH + 1;
+    const int wo = (L->W + 2 * L->PW - L->DW * (L->KW - 1) - 1) / L->SW + 1;
+    if (ho <= 0 || wo <= 0) return "empty output";
+    if (ho != L->Ho || wo != L->Wo) return "Ho/Wo inconsistent with H/W/kernel/stride/padding/dilation";
+    if (!L->weight || !L->bias || !L->wsum) return "null weight/bias/wsum";
+    if (!L->a.x) return "null source a.x";
+    switch (L->load_mode) {
+        case NCONV_LOAD_PLAIN:
+            if (!L->a.c && need_c) return "null source a.c";
+            if (L->a.C != L->Cin || L->a.H != L->H || L->a.W != L->W) return "PLAIN: source a must be (Cin, H, W)";
+            break;
+        case NCONV_LOAD_THRESH:
+            if (L->a.C != L->Cin || L->a.H != L->H || L->a.W != L->W) return "THRESH: source a must be (Cin, H, W)";
+            break;
+        case NCONV_LOAD_POOL2:
+            if (!L->a.c && need_c) return "null source a.c";
+            if (L->a.C != L->Cin || L->a.H / 2 != L->H || L->a.W / 2 != L->W) return "POOL2: source a must be (Cin, 2H(+1), 2W(+1))";
+            break;
+        case NCONV_LOAD_UPCAT_SKIP_FIRST:
+        case NCONV_LOAD_UPCAT_UP_FIRST:
+            if (!L->a.c || !L->b.x || !L->b.c) return "UPCAT: null source pointer";
+            if (L->a.C <= 0 || L->b.C <= 0 || L->a.C + L->b.C != L->Cin) return "UPCAT: a.C + b.C must equal Cin";
+            if (L->a.H != L->H || L->a.W != L->W) return "UPCAT: source a must be (Ca, H, W)";
+            if (L->b.H <= 0 || L->b.W <= 0) return "UPCAT: empty source b";
+            break;
+        default:
+            return "unknown load mode";
+    }
+    return nullptr;
+}
+
+LayerDev make_dev(const nconv_layer* L) {
+    LayerDev d;
+    d.L = *L;
+    d.up_scale_h = (L->b.H > 0) ? (float)L->b.H / (float)L->H : 0.f;
+    d.up_scale_w = (L->b.W > 0) ? (float)L->b.W / (float)L->W : 0.f;
+    return d;
+}
+
+}  // namespace
+
+extern "C" {
+
+int nconv_abi_version(void) { return NCONV_ABI_VERSION; }
+
+const char* nconv_last_error(void) { return g_err.c_str(); }
+
+int nconv_weight_prep(int n, float* const* weights, const int* couts, const int* fan_ins,
+                      const int* apply_softplus, float* const* wsums, void* stream) {
+    if (n < 0 || (n > 0 && (!weights || !couts || !fan_ins || !wsums)))
+        return fail(-22, "nconv_weight_prep", "null argument");
+    for (int i = 0; i < n; ++i)
+        if (!weights[i] || !wsums[i] || couts[i] <= 0 || fan_ins[i] <= 0)
+            return fail(-22, "nconv_weight_prep", "bad layer entry");
+    const char* why = nullptr;
+    int rc = nconv::launch_weight_prep(n, weights, couts, fan_ins, apply_softplus, wsums,
+                                       (hipStream_t)stream, &why);
+    return rc ? fail(rc, "nconv_weight_prep", why) : 0;
+}
+
+int nconv_fwd(const nconv_layer* L, float* y, float* cout, void* stream) {
+    if (const char* why = validate(L, true)) return fail(-22, "nconv_fwd", why);
+    if (!y || !cout) return fail(-22, "nconv_fwd", "null output");
+    const char* why = nullptr;
+    int rc = nconv::launch_fwd(make_dev(L), y, cout, (hipStream_t)stream, &why);
+    return rc ? fail(rc, "nconv_fwd", why) : 0;
+}
+
+int nconv_fwd_tail(const nconv_layer* L6, const float* w7, const float* b7, const float* wsum7,
+                   int cin7, int p7, float eps7, float* out, float* out_c, int out_h, int out_w,
+                   void* stream) {
+    if (const char* why = validate(L6, true)) return fail(-22, "nconv_fwd_tail", why);
+    if (!w7 || !b7 || !wsum7 || !out) return fail(-22, "nconv_fwd_tail", "null tail pointer");
+    if (cin7 != L6->Cout) return fail(-22, "nconv_fwd_tail", "nconv7 Cin must equal nconv6 Cout");
+    if (p7 < 0 || out_h < 0 || out_w < 0) return fail(-22, "nconv_fwd_tail", "bad tail geometry");
+    if (out_h > L6->Ho + 2 * p7 - 1 || out_w > L6->Wo + 2 * p7 - 1)
+        return fail(-22, "nconv_fwd_tail", "output crop exceeds nconv7's grid");
+    nconv::TailArgs t{w7, b7, wsum7, eps7, 1 - p7, out_h, out_w, out_c};
+    const char* why = nullptr;
+    int rc = nconv::launch_fwd_tail(make_dev(L6), t, out, (hipStream_t)stream, &why);
+    return rc ? fail(rc, "nconv_fwd_tail", why) : 0;
+}
+
+size_t nconv_bwd_workspace_bytes(const nconv_layer* L) {
+    if (validate(L, true)) return 0;
+    return nconv::bwd_workspace_bytes(make_dev(L));
+}
+
+int nconv_bwd(const nconv_layer* L, const float* y, const float* cout, const float* gy,
+              const float* gcout, float* gxa, float* gca, float* gxb, float* gcb, float* gw,
+              float* gbias, void* workspace, size_t workspace_bytes, void* stream) {
+    if (const char* why = validate(L, true)) return fail(-22, "nconv_bwd", why);
+    if (!y || !cout || !gy) return fail(-22, "nconv_bwd", "null y/cout/gy");
+    const LayerDev d = make_dev(L);
+    const size_t need = nconv::bwd_workspace_bytes(d);
+    if (need && (!workspace || workspace_bytes < need)) return fail(-22, "nconv_bwd", "workspace too small");
+    const int fan = (L->Cin / L->groups) * L->KH * L->KW;
+    if ((long)L->Cout * fan + 2L * L->Cout > 65535)
+        return fail(-22, "nconv_bwd", "weight-gradient path supports at most 65535 weights per layer");
+    nconv::BwdArgs a{y, cout, gy, gcout, gxa, gca, gxb, gcb, gw, gbias, (float*)workspace, workspace_bytes};
+    const char* why = nullptr;
+    int rc = nconv::launch_bwd(d, a, (hipStream_t)stream, &why);
+    return rc ? fail(rc, "nconv_bwd", why) : 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,113 @@
+// nconv_common.h — device-side helpers shared by the forward and backward NConv kernels (gfx950).
+//
+// Reference semantics restated here (all in models/step1.py of the reference):
+//   * threshold confidence c0 = float(S > 0.01)                       step1.py:53
+//   * independent 2x2/s2 max-pooling of data and confidence            step1.py:62-75
+//     (torch max_pool2d: a later element wins iff it is > the running max or is NaN,
+//      so ties keep the FIRST maximum in row-major window order)
+//   * nearest upsampling to a given size (torch: src = dst>>1 when out == 2*in,
+//     else min(floor(dst * (float)in/out), in-1))                       step1.py:78-89
+//   * channel concat, skip first (nconv4/5) or upsampled first (nconv6) step1.py:80,85,90
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "../../include/nconv.h"
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+// Layer descriptor as the kernels see it: the C-ABI struct plus host-derived constants.
+struct LayerDev {
+    nconv_layer L;
+    float up_scale_h;  // (float)b.H / H   (UPCAT modes)
+    float up_scale_w;  // (float)b.W / W
+};
+
+__device__ __forceinline__ int nearest_src(int dst, int in, int out, float scale) {
+    if (out == in) return dst;
+    if (out == 2 * in) return dst >> 1;
+    int s = (int)floorf((float)dst * scale);
+    return s < in - 1 ? s : in - 1;
+}
+
+// torch max_pool2d window scan: (v > m) || isnan(v) replaces; returns the window slot 0..3.
+__device__ __forceinline__ float pool4(float v0, float v1, float v2, float v3, int& arg) {
+    float m = v0;
+    arg = 0;
+    if (v1 > m || v1 != v1) { m = v1; arg = 1; }
+    if (v2 > m || v2 != v2) { m = v2; arg = 2; }
+    if (v3 > m || v3 != v3) { m = v3; arg = 3; }
+    return m;
+}
+
+__device__ __forceinline__ float pool4v(float v0, float v1, float v2, float v3) {
+    int a;
+    return pool4(v0, v1, v2, v3, a);
+}
+
+__device__ __forceinline__ size_t plane_idx(int b, int c, int C, int H, int W, int h, int w) {
+    return (((size_t)b * C + c) * H + h) * (size_t)W + w;
+}
+
+// Layer input (x, c) at logical position (b, ci, ih, iw), which must be in range. The glue op of
+// the layer's load mode is evaluated here, so no glued intermediate tensor ever exists in HBM.
+template <int MODE>
+__device__ __forceinline__ void load_xc(const LayerDev& d, int b, int ci, int ih, int iw, float& x,
+                                        float& c) {
+    const nconv_layer& L = d.L;
+    if constexpr (MODE == NCONV_LOAD_PLAIN) {
+        size_t i = plane_idx(b, ci, L.a.C, L.a.H, L.a.W, ih, iw);
+        x = L.a.x[i];
+        c = L.a.c[i];
+    } else if constexpr (MODE == NCONV_LOAD_THRESH) {
+        x = L.a.x[plane_idx(b, ci, L.a.C, L.a.H, L.a.W, ih, iw)];
+        c = (x > L.thresh) ? 1.0f : 0.0f;
+    } else if constexpr (MODE == NCONV_LOAD_POOL2) {
+        size_t i = plane_idx(b, ci, L.a.C, L.a.H, L.a.W, 2 * ih, 2 * iw);
+        size_t W2 = (size_t)L.a.W;
+        if ((L.a.W & 1) == 0) {  // 8-byte aligned window rows: one dwordx2 per row
+            f2 x0 = *(const f2*)(L.a.x + i), x1 = *(const f2*)(L.a.x + i + W2);
+            f2 c0 = *(const f2*)(L.a.c + i), c1 = *(const f2*)(L.a.c + i + W2);
+            x = pool4v(x0.x, x0.y, x1.x, x1.y);
+            c = pool4v(c0.x, c0.y, c1.x, c1.y);
+        } else {
+            x = pool4v(L.a.x[i], L.a.x[i + 1], L.a.x[i + W2], L.a.x[i + W2 + 1]);
+            c = pool4v(L.a.c[i], L.a.c[i + 1], L.a.c[i + W2], L.a.c[i + W2 + 1]);
+        }
+    } else {
+        const bool skip_first = (MODE == NCONV_LOAD_UPCAT_SKIP_FIRST);
+        const int first_c = skip_first ? L.a.C : L.b.C;
+        const bool from_a = skip_first ? (ci < first_c) : (ci >= first_c);
+        if (from_a) {
+            int ca = skip_first ? ci : ci - first_c;
+            size_t i = plane_idx(b, ca, L.a.C, L.a.H, L.a.W, ih, iw);
+            x = L.a.x[i];
+            c = L.a.c[i];
+        } else {
+            int cb = skip_first ? ci - first_c : ci;
+            int sh = nearest_src(ih, L.b.H, L.H, d.up_scale_h);
+            int sw = nearest_src(iw, L.b.W, L.W, d.up_scale_w);
+            size_t i = plane_idx(b, cb, L.b.C, L.b.H, L.b.W, sh, sw);
+            x = L.b.x[i];
+            c = L.b.c[i];
+        }
+    }
+}
+
+// IEEE-exact epilogue of NConv2d.forward (step1.py:123-147):
+//   y = N / (D + eps) + b,   cout = D / s.
+__device__ __forceinline__ void nconv_epilogue(float N, float D, float eps, float bias, float s,
+                                               float& y, float& co) {
+    y = N / (D + eps) + bias;
+    co = D / s;
+}
+
+// Closed-form gradient of the epilogue w.r.t. N and D, from the saved outputs.
+__device__ __forceinline__ void nconv_grad_nd(float gy, float gco, float y, float co, float eps,
+                                              float bias, float s, float& gN, float& gD) {
+    const float D = co * s;
+    const float den = D + eps;
+    const float r = y - bias;  // = N / (D + eps)
+    gN = gy / den;
+    gD = -(gy * r) / den + gco / s;
+}

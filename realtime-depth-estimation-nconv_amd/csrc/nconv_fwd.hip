@@ -1,0 +1,337 @@
+// nconv_fwd.hip — forward NConv kernels for gfx950 (MI355X).
+//
+// One launch per NConv2d layer computes, for every output pixel and output channel,
+//     N = sum W * (x*c),   D = sum W * c,   y = N/(D+eps) + b,   cout = D/s
+// (reference models/step1.py:116-149). N and D share every weight, so each tap is ONE packed
+// FP32 FMA  {N,D} += {w,w} * {x*c, c}  (v_pk_fma_f32 with the weight broadcast from an SGPR pair,
+// op_sel_hi:[0,1,1]): the weight stream is wave-uniform and rides the scalar cache, the packed
+// {x*c, c} operand is staged once per input element in LDS.
+//
+// Tiling: a 256-thread workgroup owns a 16 x 64 output tile of one image and all Cout channels;
+// each thread owns 4 horizontally adjacent pixels (a sliding window of 4+K-1 staged inputs per
+// kernel row feeds K*4*Cout packed FMAs). Input channels are staged in chunks of CC planes of
+// (16+K-1) x (64+K-1) {x*c, c} pairs, with the layer's glue (threshold / 2x2 max-pool / nearest
+// upsample + concat, step1.py:53-90) evaluated while staging, so glued tensors never hit HBM.
+#include "nconv_internal.h"
+
+namespace nconv {
+
+constexpr int kThreads = 256;
+
+constexpr int pick_cc(int cin, int plane_f2) {
+    int best = 1;
+    for (int cc = 1; cc <= cin; ++cc)
+        if (cin % cc == 0 && cc * plane_f2 * 8 <= 24 * 1024) best = cc;
+    return best;
+}
+
+template <int CIN, int K>
+struct FwdCfg {
+    static constexpr int P = 4, TW = 64, TH = 16;
+    static constexpr int IHT = TH + K - 1, IWT = TW + K - 1;
+    static constexpr int IWP = (IWT + 1) & ~1;  // even pitch keeps the f4 reads 16-B aligned
+    static constexpr int PLANE = IHT * IWP;
+    static constexpr int CC = pick_cc(CIN, PLANE);
+    static constexpr int NV = P + K - 1;  // sliding-window width per kernel row
+};
+
+template <int CIN, int COUT, int K, int MODE, bool TAIL>
+__global__ __launch_bounds__(kThreads) void fwd_tiled(LayerDev d, float* __restrict__ y,
+                                                      float* __restrict__ yc, TailArgs t) {
+    using C = FwdCfg<CIN, K>;
+    __shared__ __attribute__((aligned(16))) f2 tile[C::CC * C::PLANE];
+    const nconv_layer& L = d.L;
+    const float* __restrict__ wgt = L.weight;
+    const int tid = threadIdx.x;
+    const int b = blockIdx.z;
+    const int R0 = blockIdx.y * C::TH, C0 = blockIdx.x * C::TW;  // tile origin in the written grid
+    const int off = TAIL ? t.off : 0;
+    const int oh0 = R0 + off, ow0 = C0 + off;  // tile origin in this layer's output grid
+    const int ih0 = oh0 - L.PH, iw0 = ow0 - L.PW;
+    const int ty = tid >> 4, tx = (tid & 15) * C::P;
+
+    f2 acc[COUT][C::P];
+#pragma unroll
+    for (int o = 0; o < COUT; ++o)
+#pragma unroll
+        for (int j = 0; j < C::P; ++j) acc[o][j] = (f2){0.f, 0.f};
+
+    for (int c0 = 0; c0 < CIN; c0 += C::CC) {
+        if (c0) __syncthreads();
+        // ---- stage CC planes of {x*c, c} over the haloed input tile (glue fused here) ----
+        for (int e = tid; e < C::CC * C::IHT * C::IWT; e += kThreads) {
+            const int cc = e / (C::IHT * C::IWT);
+            const int rem = e - cc * (C::IHT * C::IWT);
+            const int r = rem / C::IWT;
+            const int col = rem - r * C::IWT;
+            const int ih = ih0 + r, iw = iw0 + col;
+            float x = 0.f, c = 0.f;
+            if ((unsigned)ih < (unsigned)L.H && (unsigned)iw < (unsigned)L.W)
+                load_xc<MODE>(d, b, c0 + cc, ih, iw, x, c);
+            tile[cc * C::PLANE + r * C::IWP + col] = (f2){x * c, c};
+        }
+        __syncthreads();
+        // ---- packed-FP32 accumulation: {N, D} += w * {x*c, c} ----
+#pragma unroll
+        for (int cc = 0; cc < C::CC; ++cc) {
+#pragma unroll
+            for (int kh = 0; kh < K; ++kh) {
+                const f2* row = &tile[cc * C::PLANE + (ty + kh) * C::IWP + tx];
+                f2 v[C::NV];
+#pragma unroll
+                for (int m = 0; m < C::NV / 2; ++m) {
+                    f4 q = reinterpret_cast<const f4*>(row)[m];
+                    v[2 * m] = q.xy;
+                    v[2 * m + 1] = q.zw;
+                }
+                if constexpr (C::NV & 1) v[C::NV - 1] = row[C::NV - 1];
+                const float* wr = wgt + ((size_t)(c0 + cc) * K + kh) * K;
+#pragma unroll
+                for (int kw = 0; kw < K; ++kw)
+#pragma unroll
+                    for (int o = 0; o < COUT; ++o) {
+                        const float w = wr[o * CIN * K * K + kw];
+                        const f2 w2 = (f2){w, w};
+#pragma unroll
+                        for (int j = 0; j < C::P; ++j)
+                            acc[o][j] = __builtin_elementwise_fma(w2, v[j + kw], acc[o][j]);
+                    }
+            }
+        }
+    }
+
+    // ---- epilogue ----
+    const int oh = oh0 + ty;
+    if constexpr (!TAIL) {
+        if (oh >= L.Ho) return;
+        const bool vec = (L.Wo & 3) == 0 && (ow0 + tx + 3) < L.Wo;
+#pragma unroll
+        for (int o = 0; o < COUT; ++o) {
+            const float s = L.wsum[o], bo = L.bias[o];
+            float yv[C::P], cv[C::P];
+#pragma unroll
+            for (int j = 0; j < C::P; ++j) nconv_epilogue(acc[o][j].x, acc[o][j].y, L.eps, bo, s, yv[j], cv[j]);
+            const size_t base = plane_idx(b, o, COUT, L.Ho, L.Wo, oh, ow0 + tx);
+            if (vec) {
+                *reinterpret_cast<f4*>(y + base) = (f4){yv[0], yv[1], yv[2], yv[3]};
+                *reinterpret_cast<f4*>(yc + base) = (f4){cv[0], cv[1], cv[2], cv[3]};
+            } else {
+#pragma unroll
+                for (int j = 0; j < C::P; ++j)
+                    if (ow0 + tx + j < L.Wo) {
+                        y[base + j] = yv[j];
+                        yc[base + j] = cv[j];
+                    }
+            }
+        }
+    } else {
+        // nconv6 outputs -> nconv7 (1x1, COUT -> 1) -> cropped final output.
+        const int r = R0 + ty;
+        if (r >= t.out_h) return;
+        float s6[COUT], b6[COUT], w7[COUT];
+#pragma unroll
+        for (int o = 0; o < COUT; ++o) {
+            s6[o] = L.wsum[o];
+            b6[o] = L.bias[o];
+            w7[o] = t.w7[o];
+        }
+        const float b7 = t.b7[0], s7 = t.s7[0];
+        float ov[C::P], oc[C::P];
+#pragma unroll
+        for (int j = 0; j < C::P; ++j) {
+            const int ow = ow0 + tx + j;
+            float N7 = 0.f, D7 = 0.f;
+            if ((unsigned)oh < (unsigned)L.Ho && (unsigned)ow < (unsigned)L.Wo) {
+#pragma unroll
+                for (int o = 0; o < COUT; ++o) {
+                    float y6, c6;
+                    nconv_epilogue(acc[o][j].x, acc[o][j].y, L.eps, b6[o], s6[o], y6, c6);
+                    N7 = fmaf(w7[o], y6 * c6, N7);
+                    D7 = fmaf(w7[o], c6, D7);
+                }
+            }
+            nconv_epilogue(N7, D7, t.eps7, b7, s7, ov[j], oc[j]);
+        }
+        const size_t base = ((size_t)b * t.out_h + r) * t.out_w + C0 + tx;
+#pragma unroll
+        for (int j = 0; j < C::P; ++j)
+            if (C0 + tx + j < t.out_w) {
+                y[base + j] = ov[j];
+                if (t.out_c) t.out_c[base + j] = oc[j];
+            }
+    }
+}
+
+// Any NConv2d configuration (stride, dilation, groups, odd kernels): one thread per output element.
+template <int MODE>
+__global__ __launch_bounds__(kThreads) void fwd_generic(LayerDev d, float* __restrict__ y,
+                                                        float* __restrict__ yc) {
+    const nconv_layer& L = d.L;
+    const size_t n = (size_t)L.B * L.Cout * L.Ho * L.Wo;
+    const int cpg_in = L.Cin / L.groups, cpg_out = L.Cout / L.groups;
+    for (size_t idx = (size_t)blockIdx.x * kThreads + threadIdx.x; idx < n;
+         idx += (size_t)gridDim.x * kThreads) {
+        const int ow = (int)(idx % L.Wo);
+        const int oh = (int)((idx / L.Wo) % L.Ho);
+        const int o = (int)((idx / ((size_t)L.Wo * L.Ho)) % L.Cout);
+        const int b = (int)(idx / ((size_t)L.Wo * L.Ho * L.Cout));
+        const int g = o / cpg_out;
+        float N = 0.f, D = 0.f;
+        for (int cl = 0; cl < cpg_in; ++cl) {
+            const int ci = g * cpg_in + cl;
+            for (int kh = 0; kh < L.KH; ++kh) {
+                const int ih = oh * L.SH - L.PH + kh * L.DH;
+                if ((unsigned)ih >= (unsigned)L.H) continue;
+                for (int kw = 0; kw < L.KW; ++kw) {
+                    const int iw = ow * L.SW - L.PW + kw * L.DW;
+                    if ((unsigned)iw >= (unsigned)L.W) continue;
+                    float x, c;
+                    load_xc<MODE>(d, b, ci, ih, iw, x, c);
+                    const float w = L.weight[(((size_t)o * cpg_in + cl) * L.KH + kh) * L.KW + kw];
+                    N = fmaf(w, x * c, N);
+                    D = fmaf(w, c, D);
+                }
+            }
+        }
+        float yv, cv;
+        nconv_epilogue(N, D, L.eps, L.bias[o], L.wsum[o], yv, cv);
+        y[idx] = yv;
+        yc[idx] = cv;
+    }
+}
+
+// EnforcePos (softplus, beta=10, threshold=20; step1.py:190-207) in place + s[o] = sum W[o].
+struct PrepArgs {
+    static constexpr int kMax = 32;
+    float* w[kMax];
+    float* s[kMax];
+    int cout[kMax];
+    int fan_in[kMax];
+    int softplus[kMax];
+};
+
+__global__ __launch_bounds__(kThreads) void weight_prep(PrepArgs a) {
+    const int l = blockIdx.x;
+    float* w = a.w[l];
+    const int n = a.cout[l] * a.fan_in[l];
+    if (a.softplus[l]) {
+        for (int i = threadIdx.x; i < n; i += kThreads) {
+            const float v = w[i];
+            const float bv = v * 10.0f;
+            w[i] = (bv > 20.0f) ? v : log1pf(expf(bv)) / 10.0f;
+        }
+        __syncthreads();
+        __threadfence_block();
+    }
+    for (int o = threadIdx.x; o < a.cout[l]; o += kThreads) {
+        float s = 0.f;
+        const float* wr = w + (size_t)o * a.fan_in[l];
+        for (int i = 0; i < a.fan_in[l]; ++i) s += wr[i];
+        a.s[l][o] = s;
+    }
+}
+
+}  // namespace nconv
+
+// ------------------------------------------------------------------------------------------------
+// Launchers
+// ------------------------------------------------------------------------------------------------
+namespace nconv {
+
+static int last_launch(const char** why) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        *why = hipGetErrorString(e);
+        return -5;  // EIO
+    }
+    return 0;
+}
+
+static bool simple_geometry(const nconv_layer& L) {
+    return L.SH == 1 && L.SW == 1 && L.DH == 1 && L.DW == 1 && L.groups == 1 && L.KH == L.KW;
+}
+
+template <int CIN, int COUT, int K, int MODE, bool TAIL>
+static void go_tiled(const LayerDev& d, float* y, float* yc, const TailArgs& t, int gh, int gw,
+                     hipStream_t st) {
+    using C = FwdCfg<CIN, K>;
+    dim3 grid((gw + C::TW - 1) / C::TW, (gh + C::TH - 1) / C::TH, d.L.B);
+    hipLaunchKernelGGL((fwd_tiled<CIN, COUT, K, MODE, TAIL>), grid, dim3(kThreads), 0, st, d, y, yc, t);
+}
+
+int launch_fwd(const LayerDev& d, float* y, float* yc, hipStream_t st, const char** why) {
+    const nconv_layer& L = d.L;
+    const TailArgs t{};
+    if (simple_geometry(L)) {
+#define NCONV_TRY(CIN, COUT, K, MODE)                                                       \
+    if (L.Cin == CIN && L.Cout == COUT && L.KH == K && L.load_mode == MODE) {               \
+        go_tiled<CIN, COUT, K, MODE, false>(d, y, yc, t, L.Ho, L.Wo, st);                   \
+        return last_launch(why);                                                             \
+    }
+        NCONV_TRY(1, 8, 5, NCONV_LOAD_THRESH)
+        NCONV_TRY(8, 8, 5, NCONV_LOAD_PLAIN)
+        NCONV_TRY(8, 8, 5, NCONV_LOAD_POOL2)
+        NCONV_TRY(16, 8, 3, NCONV_LOAD_UPCAT_SKIP_FIRST)
+        NCONV_TRY(16, 8, 3, NCONV_LOAD_UPCAT_UP_FIRST)
+        NCONV_TRY(8, 1, 1, NCONV_LOAD_PLAIN)
+#undef NCONV_TRY
+    }
+    const size_t n = (size_t)L.B * L.Cout * L.Ho * L.Wo;
+    size_t blocks = (n + kThreads - 1) / kThreads;
+    if (blocks > (1u << 20)) blocks = 1u << 20;
+    if (blocks == 0) return 0;
+    switch (L.load_mode) {
+        case NCONV_LOAD_PLAIN:
+            hipLaunchKernelGGL(fwd_generic<NCONV_LOAD_PLAIN>, dim3(blocks), dim3(kThreads), 0, st, d, y, yc);
+            break;
+        case NCONV_LOAD_THRESH:
+            hipLaunchKernelGGL(fwd_generic<NCONV_LOAD_THRESH>, dim3(blocks), dim3(kThreads), 0, st, d, y, yc);
+            break;
+        case NCONV_LOAD_POOL2:
+            hipLaunchKernelGGL(fwd_generic<NCONV_LOAD_POOL2>, dim3(blocks), dim3(kThreads), 0, st, d, y, yc);
+            break;
+        case NCONV_LOAD_UPCAT_SKIP_FIRST:
+            hipLaunchKernelGGL(fwd_generic<NCONV_LOAD_UPCAT_SKIP_FIRST>, dim3(blocks), dim3(kThreads), 0, st, d, y, yc);
+            break;
+        case NCONV_LOAD_UPCAT_UP_FIRST:
+            hipLaunchKernelGGL(fwd_generic<NCONV_LOAD_UPCAT_UP_FIRST>, dim3(blocks), dim3(kThreads), 0, st, d, y, yc);
+            break;
+        default:
+            *why = "unknown load mode";
+            return -22;
+    }
+    return last_launch(why);
+}
+
+int launch_fwd_tail(const LayerDev& d, const TailArgs& t, float* out, hipStream_t st, const char** why) {
+    const nconv_layer& L = d.L;
+    if (!(simple_geometry(L) && L.Cin == 16 && L.Cout == 8 && L.KH == 3 &&
+          L.load_mode == NCONV_LOAD_UPCAT_UP_FIRST)) {
+        *why = "fused tail is only built for nconv6's geometry (16->8, 3x3, stride 1, upsample-first concat)";
+        return -95;  // EOPNOTSUPP
+    }
+    if (t.out_h <= 0 || t.out_w <= 0) return 0;
+    go_tiled<16, 8, 3, NCONV_LOAD_UPCAT_UP_FIRST, true>(d, out, nullptr, t, t.out_h, t.out_w, st);
+    return last_launch(why);
+}
+
+int launch_weight_prep(int n, float* const* w, const int* cout, const int* fan_in, const int* sp,
+                       float* const* s, hipStream_t st, const char** why) {
+    if (n <= 0) return 0;
+    if (n > PrepArgs::kMax) {
+        *why = "too many layers for one weight_prep launch (max 32)";
+        return -22;
+    }
+    PrepArgs a{};
+    for (int i = 0; i < n; ++i) {
+        a.w[i] = w[i];
+        a.s[i] = s[i];
+        a.cout[i] = cout[i];
+        a.fan_in[i] = fan_in[i];
+        a.softplus[i] = sp ? sp[i] : 0;
+    }
+    hipLaunchKernelGGL(weight_prep, dim3(n), dim3(kThreads), 0, st, a);
+    return last_launch(why);
+}
+
+}  // namespace nconv

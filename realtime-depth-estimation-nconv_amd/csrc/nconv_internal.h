@@ -1,0 +1,43 @@
+// nconv_internal.h — launcher interface between the C-ABI layer (nconv_capi.hip) and the kernel
+// translation units. Not part of the public ABI.
+#pragma once
+#include "nconv_common.h"
+
+namespace nconv {
+
+struct TailArgs {
+    const float* w7;
+    const float* b7;
+    const float* s7;
+    float eps7;
+    int off;
+    int out_h, out_w;
+    float* out_c;
+};
+
+struct BwdArgs {
+    const float* y;
+    const float* co;
+    const float* gy;
+    const float* gco;  // may be null (= 0)
+    float* gxa;
+    float* gca;
+    float* gxb;
+    float* gcb;
+    float* gw;
+    float* gb;
+    float* ws;  // workspace
+    size_t ws_bytes;
+};
+
+// Forward. Return 0, or a negative errno with *why set.
+int launch_fwd(const LayerDev& d, float* y, float* yc, hipStream_t st, const char** why);
+int launch_fwd_tail(const LayerDev& d, const TailArgs& t, float* out, hipStream_t st, const char** why);
+int launch_weight_prep(int n, float* const* w, const int* cout, const int* fan_in, const int* sp,
+                       float* const* s, hipStream_t st, const char** why);
+
+// Backward.
+size_t bwd_workspace_bytes(const LayerDev& d);
+int launch_bwd(const LayerDev& d, const BwdArgs& a, hipStream_t st, const char** why);
+
+}  // namespace nconv

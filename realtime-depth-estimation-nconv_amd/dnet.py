@@ -1,0 +1,148 @@
+"""DNET / SETP1_NCONV — drop-in for the reference's unguided NConv U-Net (models/step1.py:15-94).
+
+The 9-layer graph (step1.py:51-94) runs as one libnconv launch per layer with the glue fused
+into each layer's load stage:
+
+    nconv1   THRESH      c0 = (S > 0.01), x0 = S                     step1.py:53-56
+    nconv2   PLAIN                                                  step1.py:57
+    down1-3  POOL2       independent 2x2 max-pool of x and c         step1.py:62-75
+    nconv4/5 UPCAT_SKIP  cat(skip, nearest-up(low))                  step1.py:78-85
+    nconv6   UPCAT_UP    cat(nearest-up(low), skip), padding 0       step1.py:88-90
+    nconv7   PLAIN       1x1, default padding 2                      step1.py:92
+    crop     [1:481, 1:641] (literal, default) or [1:H+1, 1:W+1]     step1.py:94
+
+Without autograd (inference) nconv6 and nconv7 are fused into one launch that writes the cropped
+output directly. EnforcePos pre-hooks of all nine layers are applied in one launch in training
+mode, before any layer runs (the reference applies each right before its layer; the layers share
+no weights, so the results are identical).
+"""
+import torch
+import torch.nn as nn
+
+from . import _lib
+from .nconv import EnforcePos, NConv2d, layer_forward_raw, nconv_layer, weight_prep, _require_device
+
+LAYERS = ("nconv1", "nconv2", "nconv_down1", "nconv_down2", "nconv_down3", "nconv4", "nconv5",
+          "nconv6", "nconv7")
+
+
+def crop_hw(H, W, crop):
+    """Output size after nconv7 (grid (H+2) x (W+2)) and the crop of step1.py:94."""
+    if crop == "literal":
+        return max(0, min(481, H + 2) - 1), max(0, min(641, W + 2) - 1)
+    if crop == "generalized":
+        return H, W
+    raise ValueError(f"crop must be 'literal' or 'generalized', got {crop!r}")
+
+
+class DNET(nn.Module):
+    """NConv U-Net (step1.py:30-94). `out_ch` is accepted and ignored like the reference (:19,31,36).
+
+    crop='literal' reproduces xout[:, :, 1:481, 1:641] (e.g. 353x640 at 352x1216 input);
+    crop='generalized' returns [1:H+1, 1:W+1], identical to literal at 480x640.
+    """
+
+    def __init__(self, out_ch, crop="literal"):
+        super().__init__()
+        pos_fn = "softplus"
+        num_channels = 8
+        self.crop = crop
+        self.nconv1 = NConv2d(1, num_channels, (5, 5), pos_fn, "p", padding=(2, 2))
+        self.nconv2 = NConv2d(num_channels, num_channels, (5, 5), pos_fn, "p", padding=(2, 2))
+        self.nconv_down1 = NConv2d(num_channels, num_channels, (5, 5), pos_fn, "p", padding=(2, 2))
+        self.nconv_down2 = NConv2d(num_channels, num_channels, (5, 5), pos_fn, "p", padding=(2, 2))
+        self.nconv_down3 = NConv2d(num_channels, num_channels, (5, 5), pos_fn, "p", padding=(2, 2))
+        self.nconv4 = NConv2d(2 * num_channels, num_channels, (3, 3), pos_fn, "p", padding=(1, 1))
+        self.nconv5 = NConv2d(2 * num_channels, num_channels, (3, 3), pos_fn, "p", padding=(1, 1))
+        self.nconv6 = NConv2d(2 * num_channels, num_channels, (3, 3), pos_fn, "p", padding=(0, 0))
+        self.nconv7 = NConv2d(num_channels, 1, (1, 1), pos_fn, "k")
+        # Set to a dict to receive the (x, c) inputs of the three pooling stages on the next
+        # forward (diagnostics / tests); None in normal use.
+        self.capture = None
+
+    # -- hooks ----------------------------------------------------------------------------------
+    def _prologue(self, layers, S):
+        """Run each layer's forward pre-hooks (EnforcePos) and compute s[o] for every layer."""
+        batched_sp, weights, wsums = [], [], []
+        for m in layers:
+            hooks = list(m._forward_pre_hooks.values())
+            ours = len(hooks) == 1 and isinstance(hooks[0], EnforcePos) and hooks[0].name == "weight" \
+                and hooks[0].pos_fn.lower() == "softplus"
+            if not ours:
+                for h in hooks:
+                    h(m, (S,))
+            w = m.weight
+            if not (w.is_cuda and w.dtype == torch.float32 and w.is_contiguous()):
+                raise RuntimeError(f"{type(m).__name__}.weight must be a contiguous fp32 device tensor")
+            weights.append(w.data)
+            batched_sp.append(ours and m.training)
+        buf = torch.empty(sum(w.shape[0] for w in weights), device=S.device, dtype=torch.float32)
+        off = 0
+        for w in weights:
+            wsums.append(buf[off:off + w.shape[0]])
+            off += w.shape[0]
+        weight_prep(weights, batched_sp, wsums)
+        return wsums
+
+    # -- forward ----------------------------------------------------------------------------------
+    def forward(self, S):
+        _require_device(S, "DNET.forward")
+        if S.dim() != 4 or S.shape[1] != 1:
+            raise ValueError(f"DNET expects (B, 1, H, W) sparse depth, got {tuple(S.shape)}")
+        S = S.contiguous()
+        layers = [getattr(self, n) for n in LAYERS]
+        wsum = self._prologue(layers, S)
+        (l1, l2, d1, d2, d3, l4, l5, l6, l7) = layers
+        (s1, s2, sd1, sd2, sd3, s4, s5, s6, s7) = wsum
+        grad = torch.is_grad_enabled() and (S.requires_grad or any(p.requires_grad for p in self.parameters()))
+        H, W = S.shape[2], S.shape[3]
+        out_h, out_w = crop_hw(H, W, self.crop)
+        f = nconv_layer if grad else (lambda spec, *a: layer_forward_raw(spec, *a))
+
+        x1, c1 = f(l1.spec(_lib.THRESH, 0.01), S, None, None, None, l1.weight, l1.bias, s1)
+        x1, c1 = f(l2.spec(), x1, c1, None, None, l2.weight, l2.bias, s2)
+        x2, c2 = f(d1.spec(_lib.POOL2), x1, c1, None, None, d1.weight, d1.bias, sd1)
+        x3, c3 = f(d2.spec(_lib.POOL2), x2, c2, None, None, d2.weight, d2.bias, sd2)
+        x4, c4 = f(d3.spec(_lib.POOL2), x3, c3, None, None, d3.weight, d3.bias, sd3)
+        if self.capture is not None:
+            self.capture.update(down1=(x1.detach(), c1.detach()), down2=(x2.detach(), c2.detach()),
+                                down3=(x3.detach(), c3.detach()))
+        x34, c34 = f(l4.spec(_lib.UPCAT_SKIP_FIRST), x3, c3, x4, c4, l4.weight, l4.bias, s4)
+        x23, c23 = f(l5.spec(_lib.UPCAT_SKIP_FIRST), x2, c2, x34, c34, l5.weight, l5.bias, s5)
+        if grad:
+            xo, co = f(l6.spec(_lib.UPCAT_UP_FIRST), x1, c1, x23, c23, l6.weight, l6.bias, s6)
+            xo, co = f(l7.spec(), xo, co, None, None, l7.weight, l7.bias, s7)
+            return xo[:, :, 1:1 + out_h, 1:1 + out_w]
+        return self._fused_tail(l6, l7, s6, s7, x1, c1, x23, c23, out_h, out_w)
+
+    def _fused_tail(self, l6, l7, s6, s7, x1, c1, x23, c23, out_h, out_w):
+        B = x1.shape[0]
+        out = torch.empty((B, 1, out_h, out_w), device=x1.device, dtype=torch.float32)
+        if out_h == 0 or out_w == 0:
+            return out
+        L = l6.spec(_lib.UPCAT_UP_FIRST).descriptor(x1, c1, x23, c23, l6.weight, l6.bias, s6)
+        if tuple(l7.kernel_size) != (1, 1) or l7.padding[0] != l7.padding[1] or tuple(l7.stride) != (1, 1):
+            raise RuntimeError("fused tail needs nconv7 = 1x1, stride 1, square padding")
+        rc = _lib.lib().nconv_fwd_tail(
+            _lib.ctypes.byref(L), _lib.ptr(l7.weight), _lib.ptr(l7.bias), _lib.ptr(s7), l7.in_channels,
+            l7.padding[0], l7.eps, _lib.ptr(out), None, out_h, out_w, _lib.stream_handle(x1.device))
+        _lib.check(rc, "nconv_fwd_tail")
+        return out
+
+
+class SETP1_NCONV(nn.Module):
+    """Unguided depth network wrapper (step1.py:15-27); state_dict prefix `d_net.`.
+
+    forward(S) -> d_net(S). Also accepts forward(depth0, depth1, ...) and runs DNET on their
+    batch concatenation: the call the guided model makes (models/step2.py:62,107), which the
+    reference's one-argument forward rejects with a TypeError.
+    """
+
+    def __init__(self, crop="literal"):
+        super().__init__()
+        self.d_net = DNET(32, crop=crop)
+
+    def forward(self, x0_d, *more):
+        if more:
+            x0_d = torch.cat((x0_d,) + tuple(more), dim=0)
+        return self.d_net(x0_d)

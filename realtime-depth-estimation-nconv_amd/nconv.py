@@ -1,0 +1,246 @@
+"""NConv2d / EnforcePos — drop-in for the reference's models/step1.py:97-212, computed by libnconv.
+
+`NConv2d` keeps the reference's constructor signature, parameter names, RNG consumption and
+state_dict layout (weight, bias, and the unused-but-saved bnorm.*), and its forward(data, conf)
+returns (nconv, cout) like step1.py:116-149. The arithmetic runs in hand-written gfx950 kernels
+through the C ABI (include/nconv.h); there is no PyTorch or CPU fallback for it.
+"""
+from dataclasses import dataclass
+from typing import Optional, Tuple
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+from torch.nn.modules.conv import _ConvNd
+from torch.nn.modules.utils import _pair
+
+from . import _lib
+
+
+def _require_device(t: torch.Tensor, what: str):
+    if not t.is_cuda:
+        raise RuntimeError(
+            f"{what}: nconv_amd computes on ROCm devices only (got a {t.device} tensor); "
+            "move the module and inputs to the GPU")
+    if t.dtype != torch.float32:
+        raise TypeError(f"{what}: expected float32, got {t.dtype} (the reference is fp32-only, step1.py:53)")
+
+
+@dataclass(frozen=True)
+class LayerSpec:
+    """Geometry + glue of one fused NConv application (mirrors struct nconv_layer)."""
+    cin: int
+    cout: int
+    kernel: Tuple[int, int]
+    stride: Tuple[int, int] = (1, 1)
+    padding: Tuple[int, int] = (0, 0)
+    dilation: Tuple[int, int] = (1, 1)
+    groups: int = 1
+    eps: float = 1e-7
+    mode: int = _lib.PLAIN
+    thresh: float = 0.01
+
+    def in_hw(self, a_shape, b_shape=None):
+        H, W = a_shape[2], a_shape[3]
+        if self.mode == _lib.POOL2:
+            return H // 2, W // 2
+        return H, W
+
+    def out_hw(self, H, W):
+        kh, kw = self.kernel
+        ho = (H + 2 * self.padding[0] - self.dilation[0] * (kh - 1) - 1) // self.stride[0] + 1
+        wo = (W + 2 * self.padding[1] - self.dilation[1] * (kw - 1) - 1) // self.stride[1] + 1
+        return ho, wo
+
+    def descriptor(self, xa, ca, xb, cb, weight, bias, wsum):
+        H, W = self.in_hw(xa.shape)
+        Ho, Wo = self.out_hw(H, W)
+        L = _lib.NconvLayer()
+        L.B, L.Cin, L.H, L.W = xa.shape[0], self.cin, H, W
+        L.Cout, L.Ho, L.Wo = self.cout, Ho, Wo
+        L.KH, L.KW = self.kernel
+        L.SH, L.SW = self.stride
+        L.PH, L.PW = self.padding
+        L.DH, L.DW = self.dilation
+        L.groups = self.groups
+        L.eps = self.eps
+        L.load_mode = self.mode
+        L.thresh = self.thresh
+        L.a = _lib.src(xa, ca)
+        L.b = _lib.src(xb, cb)
+        L.weight, L.bias, L.wsum = weight.data_ptr(), bias.data_ptr(), wsum.data_ptr()
+        return L
+
+
+def weight_prep(weights, softplus_flags, wsums):
+    """One launch: optional in-place softplus (EnforcePos) + s[o] = sum(W[o]) for each layer."""
+    n = len(weights)
+    if n == 0:
+        return
+    dev = weights[0].device
+    ptrs = _lib.ctypes.c_void_p * n
+    ints = _lib.ctypes.c_int * n
+    wp = ptrs(*[w.data_ptr() for w in weights])
+    sp = ptrs(*[s.data_ptr() for s in wsums])
+    couts = ints(*[w.shape[0] for w in weights])
+    fans = ints(*[w[0].numel() for w in weights])
+    flags = ints(*[1 if f else 0 for f in softplus_flags])
+    rc = _lib.lib().nconv_weight_prep(n, wp, couts, fans, flags, sp, _lib.stream_handle(dev))
+    _lib.check(rc, "nconv_weight_prep")
+
+
+def layer_forward_raw(spec: LayerSpec, xa, ca, xb, cb, weight, bias, wsum):
+    """Enqueue nconv_fwd; returns (y, cout). No autograd."""
+    L = spec.descriptor(xa, ca, xb, cb, weight, bias, wsum)
+    y = torch.empty((L.B, L.Cout, L.Ho, L.Wo), device=xa.device, dtype=torch.float32)
+    co = torch.empty_like(y)
+    rc = _lib.lib().nconv_fwd(_lib.ctypes.byref(L), _lib.ptr(y), _lib.ptr(co), _lib.stream_handle(xa.device))
+    _lib.check(rc, "nconv_fwd")
+    return y, co
+
+
+class NConvLayerFn(torch.autograd.Function):
+    """Autograd node of one fused NConv layer (glue + NConv2d.forward), kernels in libnconv."""
+
+    @staticmethod
+    def forward(ctx, spec, xa, ca, xb, cb, weight, bias, wsum):
+        y, co = layer_forward_raw(spec, xa, ca, xb, cb, weight, bias, wsum)
+        ctx.spec = spec
+        ctx.save_for_backward(xa, ca, xb, cb, weight, bias, wsum, y, co)
+        return y, co
+
+    @staticmethod
+    def backward(ctx, gy, gco):
+        spec = ctx.spec
+        xa, ca, xb, cb, weight, bias, wsum, y, co = ctx.saved_tensors
+        need = ctx.needs_input_grad  # (spec, xa, ca, xb, cb, weight, bias, wsum)
+        dev = y.device
+        if gy is None:
+            gy = torch.zeros_like(y)
+        gy = gy.contiguous()
+        gco = gco.contiguous() if gco is not None else None
+        z = lambda t, n: torch.zeros_like(t) if (t is not None and n) else None
+        gxa, gca, gxb, gcb = z(xa, need[1]), z(ca, need[2]), z(xb, need[3]), z(cb, need[4])
+        gw = torch.empty_like(weight) if need[5] else None
+        gb = torch.empty_like(bias) if need[6] else None
+        L = spec.descriptor(xa, ca, xb, cb, weight, bias, wsum)
+        lib = _lib.lib()
+        ws_bytes = lib.nconv_bwd_workspace_bytes(_lib.ctypes.byref(L))
+        ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+        rc = lib.nconv_bwd(_lib.ctypes.byref(L), _lib.ptr(y), _lib.ptr(co), _lib.ptr(gy), _lib.ptr(gco),
+                           _lib.ptr(gxa), _lib.ptr(gca), _lib.ptr(gxb), _lib.ptr(gcb), _lib.ptr(gw),
+                           _lib.ptr(gb), _lib.ptr(ws), ws_bytes, _lib.stream_handle(dev))
+        _lib.check(rc, "nconv_bwd")
+        return None, gxa, gca, gxb, gcb, gw, gb, None
+
+
+def nconv_layer(spec: LayerSpec, xa, ca, xb, cb, weight, bias, wsum):
+    """Differentiable fused layer. Inputs must be contiguous fp32 device tensors."""
+    return NConvLayerFn.apply(spec, xa, ca, xb, cb, weight, bias, wsum)
+
+
+# ------------------------------------------------------------------------------------------------
+# EnforcePos (models/step1.py:176-212)
+# ------------------------------------------------------------------------------------------------
+class EnforcePos(object):
+    """Non-negativity enforcement as a forward pre-hook: in training mode, before every forward,
+    weight.data <- pos_fn(weight) (step1.py:190-193). Not idempotent: softplus grows the weights
+    on every training forward, exactly like the reference."""
+
+    def __init__(self, pos_fn, name):
+        self.name = name
+        self.pos_fn = pos_fn
+
+    @staticmethod
+    def apply(module, name, pos_fn):
+        fn = EnforcePos(pos_fn, name)
+        module.register_forward_pre_hook(fn)
+        return fn
+
+    def __call__(self, module, inputs):
+        if module.training:
+            weight = getattr(module, self.name)
+            if self.pos_fn.lower() == "softplus" and weight.is_cuda and weight.dtype == torch.float32 \
+                    and weight.is_contiguous():
+                wsum = torch.empty(weight.shape[0], device=weight.device, dtype=torch.float32)
+                weight_prep([weight.data], [True], [wsum])
+            else:
+                weight.data = self._pos(weight).data
+
+    def _pos(self, p):
+        pos_fn = self.pos_fn.lower()
+        if pos_fn == "softmax":
+            p_sz = p.size()
+            return F.softmax(p.view(p_sz[0], p_sz[1], -1), -1).view(p_sz)
+        if pos_fn == "exp":
+            return torch.exp(p)
+        if pos_fn == "softplus":
+            return F.softplus(p, beta=10)
+        if pos_fn == "sigmoid":
+            return torch.sigmoid(p)
+        print("Undefined positive function!")
+        return None
+
+
+def _poisson_kernel(k):
+    """Outer product of the Poisson(k/2) pmf over 0..k-1 (step1.py:159-163), float64."""
+    from scipy.stats import poisson
+    y = poisson(k / 2).pmf(np.arange(0, k))
+    return np.outer(y, y)
+
+
+class NConv2d(_ConvNd):
+    """Normalized convolution layer (reference models/step1.py:97-172).
+
+    forward(data, conf) -> (nconv, cout) with nconv = conv(data*conf, W)/(conv(conf, W)+eps) + b and
+    cout = conv(conf, W) / sum(W[o]). The unused bnorm/relu submodules are kept for state_dict
+    compatibility (step1.py:110-111).
+    """
+
+    def __init__(self, in_channels, out_channels, kernel_size, pos_fn="softplus", init_method="k",
+                 stride=(1, 1), padding=(2, 2), dilation=(1, 1), groups=1, bias=True):
+        super().__init__(in_channels, out_channels, _pair(kernel_size), _pair(stride), _pair(padding),
+                         _pair(dilation), False, output_padding=(0, 0), groups=groups, bias=bias,
+                         padding_mode="zeros")
+        self.eps = 1e-7
+        self.pos_fn = pos_fn
+        self.init_method = init_method
+        self.init_parameters()
+        self.bnorm = nn.BatchNorm2d(out_channels)
+        self.relu = nn.ReLU()
+        if self.pos_fn is not None:
+            EnforcePos.apply(self, "weight", pos_fn)
+
+    def init_parameters(self):
+        # Same RNG consumption as the reference (after _ConvNd.reset_parameters): 'x' xavier,
+        # 'k' kaiming, 'p' Poisson outer product + torch.rand; bias replaced by zeros + 0.01.
+        if self.init_method == "x":
+            torch.nn.init.xavier_uniform_(self.weight)
+        elif self.init_method == "k":
+            torch.nn.init.kaiming_uniform_(self.weight)
+        elif self.init_method == "p":
+            w = torch.tensor(_poisson_kernel(self.kernel_size[0]), dtype=torch.float32).type_as(self.weight)
+            w = w[None, None].repeat(self.out_channels, 1, 1, 1).repeat(1, self.in_channels, 1, 1)
+            self.weight.data = w + torch.rand(w.shape)
+        self.bias = torch.nn.Parameter(torch.zeros(self.out_channels) + 0.01)
+
+    def spec(self, mode=_lib.PLAIN, thresh=0.01):
+        return LayerSpec(self.in_channels, self.out_channels, tuple(self.kernel_size), tuple(self.stride),
+                         tuple(self.padding), tuple(self.dilation), self.groups, self.eps, mode, thresh)
+
+    def weight_sum(self):
+        """s[o] = sum(W[o]) computed on device (no autograd; its gradient is folded into gW)."""
+        w = self.weight.detach()
+        wsum = torch.empty(w.shape[0], device=w.device, dtype=torch.float32)
+        weight_prep([w], [False], [wsum])
+        return wsum
+
+    def forward(self, data, conf):
+        _require_device(data, "NConv2d.forward")
+        _require_device(conf, "NConv2d.forward")
+        if data.shape != conf.shape:
+            raise ValueError(f"data {tuple(data.shape)} and conf {tuple(conf.shape)} differ")
+        w = self.weight if self.weight.is_contiguous() else self.weight.contiguous()
+        return nconv_layer(self.spec(), data.contiguous(), conf.contiguous(), None, None, w, self.bias,
+                           self.weight_sum())

@@ -1,0 +1,237 @@
+"""Generate the golden fixtures under tests/golden/ by running the REFERENCE implementation.
+
+Run in the build container (where /root/reference exists), never on the GPU box:
+
+    python tests/golden/make_golden.py [/root/reference]
+
+The reference's models/step1.py and models/step2.py are imported from the read-only checkout.
+Three third-party imports they make but never use on this path (cv2 at step1.py:7/step2.py:10,
+timm via models/utils.py:11, torchvision at step2.py:8-9) are absent from the image; they are
+satisfied by empty placeholder modules that provide no function the path calls. Everything
+computed below is the reference's own code on torch CPU (fp32 unless stated).
+
+Fixtures written (small .npz, float32 unless noted):
+  f1_layers.npz   per-layer NConv2d forward + autograd backward, 5 DNET layer geometries
+  f2_dnet.npz     DNET eval forward (literal crop), B=2 at 64x96 and 50x70, + weights
+  f3_train.npz    two DNET training steps (EnforcePos drift + calculate_loss + AdamW)
+  f4_masks.npz    c0 threshold masks and max_pool2d argmax with ties / NaN (uint8 / int64)
+  f5_guided.npz   SETP2_BP_TRAIN 4-scale + EXPORT outputs, 1+1 frames at 480x640 (step-1 call shim)
+  f6_init.npz     torch.manual_seed(0) initial parameters of SETP1_NCONV, SETP2 param sums
+"""
+import os
+import sys
+import tempfile
+import types
+
+import numpy as np
+import torch
+
+OUT = os.path.dirname(os.path.abspath(__file__))
+REF = sys.argv[1] if len(sys.argv) > 1 else "/root/reference"
+
+
+def import_reference():
+    sys.dont_write_bytecode = True
+    for name in ("cv2", "timm", "timm.models", "timm.models.layers", "torchvision",
+                 "torchvision.transforms", "torchvision.transforms.functional"):
+        sys.modules.setdefault(name, types.ModuleType(name))
+    sys.modules["timm.models.layers"].DropPath = object
+    sys.path.insert(0, REF)
+    import models.step1 as step1  # noqa: E402
+    import models.step2 as step2  # noqa: E402
+    return step1, step2
+
+
+def np32(t):
+    return t.detach().cpu().float().numpy().copy()  # copy: .numpy() of a CPU tensor shares storage
+
+
+def layer_fixtures(step1):
+    """F1: one NConv2d per DNET geometry, positive weights, fwd + autograd bwd."""
+    out = {}
+    geos = [("nconv1", 1, 8, (5, 5), (2, 2), "p"), ("nconv2", 8, 8, (5, 5), (2, 2), "p"),
+            ("nconv4", 16, 8, (3, 3), (1, 1), "p"), ("nconv6", 16, 8, (3, 3), (0, 0), "p"),
+            ("nconv7", 8, 1, (1, 1), (2, 2), "k")]
+    g = torch.Generator().manual_seed(2024)
+    for name, cin, cout, k, pad, init in geos:
+        torch.manual_seed(7)
+        layer = step1.NConv2d(cin, cout, k, "softplus", init, padding=pad)
+        layer.train()
+        B, H, W = 2, 16, 24
+        x = torch.rand(B, cin, H, W, generator=g) * 10
+        if name == "nconv1":
+            x = x * (torch.rand(B, cin, H, W, generator=g) < 0.3)
+            c = (x > 0.01).float()
+        else:
+            c = torch.rand(B, cin, H, W, generator=g) * (torch.rand(B, cin, H, W, generator=g) < 0.7)
+        w0 = layer.weight.detach().clone()
+        x.requires_grad_(True)
+        c.requires_grad_(True)
+        y, co = layer(x, c)  # train mode: EnforcePos softplus runs first
+        gy = torch.randn(y.shape, generator=g)
+        gc = torch.randn(co.shape, generator=g)
+        (y * gy + co * gc).sum().backward()
+        p = f"{name}_"
+        out.update({p + "w_init": np32(w0), p + "w": np32(layer.weight), p + "b": np32(layer.bias),
+                    p + "x": np32(x), p + "c": np32(c), p + "y": np32(y), p + "cout": np32(co),
+                    p + "gy": np32(gy), p + "gcout": np32(gc), p + "gx": np32(x.grad), p + "gc": np32(c.grad),
+                    p + "gw": np32(layer.weight.grad), p + "gb": np32(layer.bias.grad),
+                    p + "pad": np.array(pad, np.int64)})
+    np.savez_compressed(os.path.join(OUT, "f1_layers.npz"), **out)
+
+
+def positive_setp1(step1):
+    torch.manual_seed(0)
+    net = step1.SETP1_NCONV()
+    net.train()
+    with torch.no_grad():
+        net(torch.zeros(1, 1, 32, 32))  # EnforcePos once -> positive weights
+    net.eval()
+    return net
+
+
+def dnet_fixtures(step1):
+    """F2: eval forward, literal crop (the reference's only crop)."""
+    net = positive_setp1(step1)
+    out = {k: np32(v) for k, v in net.state_dict().items() if v.dtype == torch.float32}
+    g = torch.Generator().manual_seed(5)
+    for (B, H, W) in [(2, 64, 96), (2, 50, 70)]:
+        S = (torch.rand(B, 1, H, W, generator=g) * 79 + 1) * (torch.rand(B, 1, H, W, generator=g) < 0.05)
+        with torch.no_grad():
+            y = net(S)
+        out[f"S_{H}x{W}"] = np32(S)
+        out[f"out_{H}x{W}"] = np32(y)
+    np.savez_compressed(os.path.join(OUT, "f2_dnet.npz"), **out)
+
+
+def _ref_calculate_loss():
+    """The reference's utils.calculate_loss pulls dataset/kittiloader (cv2, PIL) at import; load
+    utils.py's source with those two module-level imports satisfied by placeholders."""
+    for name in ("PIL", "PIL.Image"):
+        sys.modules.setdefault(name, types.ModuleType(name))
+    sys.modules["PIL"].Image = sys.modules["PIL.Image"]
+    import utils as ref_utils  # noqa: E402  (/root/reference/utils.py)
+    return ref_utils
+
+
+def train_fixtures(step1):
+    """F3: two training steps, train_step1.py:59-65 semantics (AdamW lr 1e-2, wd 1e-7)."""
+    ref_utils = _ref_calculate_loss()
+    torch.manual_seed(0)
+    net = step1.SETP1_NCONV()
+    out = {"init_" + k: np32(v) for k, v in net.state_dict().items() if v.dtype == torch.float32}
+    opt = torch.optim.AdamW(net.parameters(), lr=1e-2, weight_decay=1e-7)
+    g = torch.Generator().manual_seed(9)
+    B, H, W = 2, 64, 96
+    for step in range(2):
+        S = (torch.rand(B, 1, H, W, generator=g) * 79 + 1) * (torch.rand(B, 1, H, W, generator=g) < 0.05)
+        gt = (torch.rand(B, 1, H + 1, W + 1, generator=g) * 79 + 1) * (torch.rand(B, 1, H + 1, W + 1, generator=g) < 0.3)
+        net.train()
+        opt.zero_grad()
+        est = net(S)
+        loss = ref_utils.calculate_loss(est[0, :, :, :], gt[0, :, :, :], True)
+        loss.requires_grad_().backward()
+        out[f"step{step}_S"], out[f"step{step}_gt"] = np32(S), np32(gt)
+        out[f"step{step}_loss"] = np.array(loss.item(), np.float64)
+        for k, p in net.named_parameters():
+            if p.grad is not None:
+                out[f"step{step}_grad_{k}"] = np32(p.grad)
+            out[f"step{step}_used_{k}"] = np32(p)  # weights as used (after softplus)
+        opt.step()
+        for k, p in net.named_parameters():
+            out[f"step{step}_after_{k}"] = np32(p)
+    np.savez_compressed(os.path.join(OUT, "f3_train.npz"), **out)
+
+
+def mask_fixtures():
+    """F4: c0 = (S > 0.01) and max_pool2d argmax (first max wins on ties, NaN propagates)."""
+    import torch.nn.functional as F
+    g = torch.Generator().manual_seed(3)
+    S = torch.rand(2, 1, 30, 40, generator=g) * 0.03  # straddles the 0.01 threshold
+    S[0, 0, 0, :5] = torch.tensor([0.01, 0.0100001, 0.0099999, 0.0, -1.0])
+    x = torch.randint(0, 3, (2, 8, 30, 40), generator=g).float()  # many ties
+    x[1, 3, 4, 6] = float("nan")
+    v, idx = F.max_pool2d(x, 2, 2, return_indices=True)
+    np.savez_compressed(os.path.join(OUT, "f4_masks.npz"), S=np32(S), c0=(S > 0.01).numpy().astype(np.uint8),
+                        x=np32(x), pooled=np32(v), argmax=idx.numpy().astype(np.int64))
+
+
+def guided_fixtures(step1, step2):
+    """F5: SETP2_BP_TRAIN / SETP2_BP_EXPORT forward, 1+1 frames at 480x640 (the only size where the
+    reference's literal step-1 crop, step1.py:94, matches the RGB branch), eval mode. The reference's
+    step-1 call self.step1(depth0, depth1) raises TypeError (step1.py:22 takes one tensor); the shim
+    runs d_net on the batch concatenation, the intended semantics of step2.py:62-63.
+    Weights are not stored: torch.manual_seed(1) before SETP2_BP_TRAIN(...) regenerates them; the
+    per-tensor sums below pin that regeneration."""
+    net1 = positive_setp1(step1)
+    with tempfile.TemporaryDirectory() as tmp:
+        os.makedirs(os.path.join(tmp, "checkpoints"))
+        torch.save({"epoch": 0, "state_dict": {"module." + k: v for k, v in net1.state_dict().items()},
+                    "stats": None}, os.path.join(tmp, "checkpoints", "s1.pth.tar"))
+        cwd = os.getcwd()
+        os.chdir(tmp)
+        try:
+            torch.manual_seed(1)
+            model = step2.SETP2_BP_TRAIN("s1")
+        finally:
+            os.chdir(cwd)
+    shim = lambda d0, d1: model.step1.d_net(torch.cat((d0, d1), 0))
+    model.step1.forward = shim
+    model.eval()
+    g = torch.Generator().manual_seed(8)
+    H, W = 480, 640
+    rgb0, rgb1 = torch.rand(1, 3, H, W, generator=g) * 255, torch.rand(1, 3, H, W, generator=g) * 255
+    d0 = (torch.rand(1, 1, H, W, generator=g) * 79 + 1) * (torch.rand(1, 1, H, W, generator=g) < 0.05)
+    d1 = (torch.rand(1, 1, H, W, generator=g) * 79 + 1) * (torch.rand(1, 1, H, W, generator=g) < 0.05)
+    with torch.no_grad():
+        o0, o1 = model(rgb0, d0, rgb1, d1)
+    out = {"sum_" + k: np.array(v.double().sum().item(), np.float64) for k, v in model.state_dict().items()
+           if v.dtype == torch.float32}
+    # inputs are regenerated from torch.Generator().manual_seed(8) (same draw order); sums pin them
+    for k, v in (("rgb0", rgb0), ("rgb1", rgb1), ("d0", d0), ("d1", d1)):
+        out[k + "_sum"] = np.array(v.double().sum().item(), np.float64)
+    for i in range(4):
+        for tag, o in (("out0", o0[i]), ("out1", o1[i])):
+            full = o[0, 0]
+            out[f"{tag}_{i}"] = np32(full if i < 2 else full[::4, ::4])
+            out[f"{tag}_{i}_sum"] = np.array(full.double().sum().item(), np.float64)
+    exp = step2.SETP2_BP_EXPORT()
+    exp.load_state_dict(model.state_dict(), strict=False)
+    exp.step1.forward = lambda d0, d1: exp.step1.d_net(torch.cat((d0, d1), 0))
+    exp.eval()
+    with torch.no_grad():
+        e0, e1 = exp(rgb0, d0, rgb1, d1)
+    out["export0"], out["export1"] = np32(e0[0, 0, ::4, ::4]), np32(e1[0, 0, ::4, ::4])
+    out["export0_sum"] = np.array(e0.double().sum().item(), np.float64)
+    np.savez_compressed(os.path.join(OUT, "f5_guided.npz"), **out)
+
+
+def init_fixtures(step1, step2):
+    """F6: seeded-initialisation known answers (RNG-consumption parity)."""
+    torch.manual_seed(0)
+    net = step1.SETP1_NCONV()
+    out = {"setp1_" + k: np32(v) for k, v in net.state_dict().items() if v.dtype == torch.float32}
+    torch.manual_seed(0)
+    m = step2.SETP2_BP_EXPORT()
+    for k, v in m.state_dict().items():
+        if v.dtype == torch.float32:
+            out["setp2_sum_" + k] = np.array(v.double().sum().item(), np.float64)
+    np.savez_compressed(os.path.join(OUT, "f6_init.npz"), **out)
+
+
+def main():
+    torch.set_num_threads(1)  # reproducible oneDNN reduction order for the fixtures
+    step1, step2 = import_reference()
+    layer_fixtures(step1)
+    dnet_fixtures(step1)
+    train_fixtures(step1)
+    mask_fixtures()
+    guided_fixtures(step1, step2)
+    init_fixtures(step1, step2)
+    for f in sorted(os.listdir(OUT)):
+        if f.endswith(".npz"):
+            print(f, os.path.getsize(os.path.join(OUT, f)))
+
+
+if __name__ == "__main__":
+    main()

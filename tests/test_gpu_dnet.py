@@ -1,0 +1,121 @@
+"""GPU parity of the whole DNET / SETP1_NCONV path against the oracle (dnet_forward = restated
+models/step1.py:51-94) — forward at several sizes and both crops, training-mode EnforcePos drift,
+and the fwd+bwd gradients of a step-1 training loss.
+
+Tolerances: forward elementwise |gpu-ref| <= 1e-4*|ref| + 1e-4 (fp32 kernels vs fp64 oracle; the
+absolute term covers outputs near 0); gradients normwise max|gpu-ref|/max|ref| <= 1e-3.
+"""
+import pytest
+import torch
+
+from oracle import nconv_ref as R
+
+pytestmark = pytest.mark.gpu
+
+
+def sparse_depth(g, B, H, W, density=0.05, dtype=torch.float32):
+    d = torch.rand(B, 1, H, W, generator=g, dtype=dtype) * 79 + 1
+    return d * (torch.rand(B, 1, H, W, generator=g, dtype=dtype) < density)
+
+
+def make_net(nconv_amd, crop, dev):
+    torch.manual_seed(0)
+    net = nconv_amd.SETP1_NCONV(crop=crop).to(dev)
+    # one training-mode forward: EnforcePos makes the weights positive (what training produces)
+    net.train()
+    with torch.no_grad():
+        net(torch.zeros(1, 1, 32, 32, device=dev))
+    net.eval()
+    return net
+
+
+def oracle_params(net):
+    sd = {k: v.detach().double().cpu() for k, v in net.state_dict().items()}
+    return R.dnet_params_from_state_dict(sd)
+
+
+@pytest.mark.parametrize("crop", ["literal", "generalized"])
+@pytest.mark.parametrize("B,H,W", [(2, 64, 96), (2, 50, 70), (1, 33, 47), (1, 352, 1216)])
+def test_dnet_eval_forward(nconv_amd, gpu, crop, B, H, W):
+    net = make_net(nconv_amd, crop, gpu)
+    g = torch.Generator().manual_seed(H * 1000 + W)
+    S = sparse_depth(g, B, H, W)
+    with torch.no_grad():
+        out = net(S.to(gpu)).double().cpu()
+    ref = R.dnet_forward(S.double(), oracle_params(net), crop)
+    assert out.shape == ref.shape, (out.shape, ref.shape)
+    err = (out - ref).abs()
+    bound = 1e-4 * ref.abs() + 1e-4
+    assert (err <= bound).all(), f"max err {err.max():.3e} ratio {(err / bound).max():.3f}"
+
+
+def test_dnet_grad_path_matches_fused_tail(nconv_amd, gpu):
+    """The autograd path (separate nconv6 / nconv7 + slicing) equals the fused inference tail."""
+    net = make_net(nconv_amd, "literal", gpu)
+    g = torch.Generator().manual_seed(7)
+    S = sparse_depth(g, 2, 64, 96).to(gpu)
+    with torch.no_grad():
+        a = net(S)
+    b = net(S.clone().requires_grad_(True)).detach()
+    torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-5)
+
+
+def test_enforcepos_drift(nconv_amd, gpu):
+    """Training-mode forward applies softplus(beta=10) to every layer's weight, once per forward."""
+    torch.manual_seed(0)
+    net = nconv_amd.SETP1_NCONV().to(gpu)
+    before = {k: v.detach().double().cpu().clone() for k, v in net.named_parameters() if k.endswith("weight")
+              and "bnorm" not in k}
+    net.train()
+    net(torch.zeros(1, 1, 16, 16, device=gpu))
+    for k, w0 in before.items():
+        w1 = dict(net.named_parameters())[k].detach().double().cpu()
+        torch.testing.assert_close(w1, R.softplus_pos(w0), rtol=2e-6, atol=2e-7)
+    net.eval()
+    w_eval = {k: v.detach().clone() for k, v in net.named_parameters()}
+    net(torch.zeros(1, 1, 16, 16, device=gpu))
+    for k, v in net.named_parameters():
+        assert torch.equal(v.detach(), w_eval[k]), "eval mode must not touch the weights"
+
+
+@pytest.mark.parametrize("H,W", [(64, 96), (45, 67)])
+def test_dnet_train_gradients(nconv_amd, gpu, H, W):
+    """Step-1 training gradients (EnforcePos + calculate_loss on [0] + backward) vs the fp64 oracle.
+
+    Near an isolated depth sample every window holds the same single sample, so neighbouring
+    outputs equal that depth up to rounding and the 2x2 max-pool winner is decided by rounding
+    noise (any two fp32 implementations, e.g. the reference on CPU and on GPU, disagree there).
+    The max-pool gradient is discontinuous in exactly those places, so the fp64 oracle is run on
+    the branch the GPU took: its pool winners are forced to the GPU's (computed by torch's own
+    max_pool2d on the GPU's activations). Tie-breaking itself is tested bit-exactly elsewhere
+    (test_gpu_layers, integer-valued pooling cases). Tolerance: normwise 1e-3 per tensor."""
+    net = make_net(nconv_amd, "literal", gpu)
+    net.train()
+    g = torch.Generator().manual_seed(11)
+    S = sparse_depth(g, 2, H, W)
+    params0 = oracle_params(net)  # the forward below applies EnforcePos once more
+    net.d_net.capture = {}
+    out = net(S.to(gpu))
+    cap, net.d_net.capture = net.d_net.capture, None
+    idx = {k: tuple(torch.nn.functional.max_pool2d(t, 2, 2, return_indices=True)[1].cpu() for t in v)
+           for k, v in cap.items()}
+
+    params = {n: (R.softplus_pos(w).detach().requires_grad_(True), b.detach().requires_grad_(True))
+              for n, (w, b) in params0.items()}
+    ref = R.dnet_forward(S.double(), params, "literal", pool_idx=idx)
+    gt = torch.rand(ref.shape, generator=g, dtype=torch.float64) * 80
+    gt = gt * (torch.rand(ref.shape, generator=g, dtype=torch.float64) < 0.3)
+    R.calculate_loss(ref[0], gt[0], True).backward()
+    R.calculate_loss(out[0], gt[0].to(gpu, torch.float32), True).backward()
+    torch.cuda.synchronize()
+    named = dict(net.named_parameters())
+    report = []
+    for n, (w, b) in params.items():
+        for lab, ref_t in (("weight", w), ("bias", b)):
+            got = named[f"d_net.{n}.{lab}"].grad.double().cpu()
+            rel = ((got - ref_t.grad).abs().max() / ref_t.grad.abs().max().clamp_min(1e-30)).item()
+            report.append(f"{n}.{lab}: {rel:.2e}" + ("" if rel <= 1e-3 else "  <-- FAIL"))
+        torch.testing.assert_close(named[f"d_net.{n}.weight"].detach().double().cpu(), w.detach(),
+                                   rtol=2e-6, atol=2e-7)
+    print("\n".join(report))
+    assert not any(r.endswith("FAIL") for r in report), "\n".join(report)

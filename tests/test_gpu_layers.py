@@ -1,0 +1,92 @@
+"""GPU parity of single fused NConv layers (all load modes, tiled and generic paths) against the
+oracle (tests/nconv_cases.oracle_layer = reference glue + models/step1.py:116-149) in float64.
+
+Tolerances (written here, from BASELINE.json's north star and SURVEY.md 8(c)):
+  forward  : elementwise |gpu - ref| <= 1e-4 * |ref| + 1e-5          (fp32 kernel vs fp64 oracle)
+  backward : max|gpu - ref| / max|ref| <= 1e-3 per gradient tensor     
+"""
+import pytest
+import torch
+
+from nconv_cases import LAYER_CASES, THRESH, oracle_layer, rand_pair, rand_weight
+
+pytestmark = pytest.mark.gpu
+
+
+def _build(case, seed):
+    name, mode, cin, cout, k, pad, stride, dil, groups, a_shape, b_shape = case
+    g = torch.Generator().manual_seed(seed)
+    xa, ca = rand_pair(g, 2, *a_shape, dtype=torch.float64)
+    if mode == THRESH:
+        xa = xa * (torch.rand(xa.shape, generator=g, dtype=torch.float64) < 0.3)
+        ca = None
+    if name.endswith("_ties"):  # small integer values and a 3-level confidence: many exact ties
+        xa = torch.randint(0, 3, xa.shape, generator=g).double()
+        ca = torch.randint(0, 3, ca.shape, generator=g).double() * 0.5
+    xb = cb = None
+    if b_shape is not None:
+        xb, cb = rand_pair(g, 2, *b_shape, dtype=torch.float64)
+    w = rand_weight(g, cout, cin // groups, k, k, torch.float64)
+    b = torch.rand(cout, generator=g, dtype=torch.float64) * 0.1
+    return xa, ca, xb, cb, w, b
+
+
+def _spec(nconv_amd, case):
+    name, mode, cin, cout, k, pad, stride, dil, groups, a_shape, b_shape = case
+    return nconv_amd.LayerSpec(cin, cout, (k, k), (stride, stride), (pad, pad), (dil, dil), groups, 1e-7, mode, 0.01)
+
+
+def _gpu(t, dev, grad=False):
+    if t is None:
+        return None
+    return t.to(dev, torch.float32).contiguous().requires_grad_(grad)
+
+
+def _wsum(nconv_amd, w):
+    s = torch.empty(w.shape[0], device=w.device, dtype=torch.float32)
+    nconv_amd.weight_prep([w.detach()], [False], [s])
+    return s
+
+
+@pytest.mark.parametrize("case", LAYER_CASES, ids=[c[0] for c in LAYER_CASES])
+def test_layer_forward(nconv_amd, gpu, case):
+    xa, ca, xb, cb, w, b = _build(case, 1234)
+    name, mode, *_ = case
+    _, _, cin, cout, k, pad, stride, dil, groups, *_ = case
+    ry, rc = oracle_layer(mode, xa, ca, xb, cb, w, b, (stride, stride), (pad, pad), (dil, dil), groups)
+    gw = _gpu(w, gpu)
+    y, c = nconv_amd.nconv_layer(_spec(nconv_amd, case), _gpu(xa, gpu), _gpu(ca, gpu), _gpu(xb, gpu),
+                                 _gpu(cb, gpu), gw, _gpu(b, gpu), _wsum(nconv_amd, gw))
+    torch.cuda.synchronize()
+    assert y.shape == ry.shape and c.shape == rc.shape
+    for got, ref in ((y, ry), (c, rc)):
+        got = got.double().cpu()
+        err = (got - ref).abs()
+        bound = 1e-4 * ref.abs() + 1e-5
+        assert torch.isfinite(got).all()
+        assert (err <= bound).all(), f"{name}: max err {err.max():.3e}, worst ratio {(err / bound).max():.3f}"
+
+
+@pytest.mark.parametrize("case", LAYER_CASES, ids=[c[0] for c in LAYER_CASES])
+def test_layer_backward(nconv_amd, gpu, case):
+    xa, ca, xb, cb, w, b = _build(case, 4321)
+    name, mode, cin, cout, k, pad, stride, dil, groups, *_ = case
+    leaves = [t.clone().requires_grad_(True) if t is not None else None for t in (xa, ca, xb, cb, w, b)]
+    ry, rc = oracle_layer(mode, *leaves, (stride, stride), (pad, pad), (dil, dil), groups)
+    g = torch.Generator().manual_seed(99)
+    gy = torch.randn(ry.shape, generator=g, dtype=torch.float64)
+    gc = torch.randn(rc.shape, generator=g, dtype=torch.float64)
+    (ry * gy + rc * gc).sum().backward()
+
+    gl = [_gpu(t, gpu, grad=True) for t in (xa, ca, xb, cb, w, b)]
+    y, c = nconv_amd.nconv_layer(_spec(nconv_amd, case), *gl[:4], gl[4], gl[5], _wsum(nconv_amd, gl[4]))
+    (y * gy.to(gpu, torch.float32) + c * gc.to(gpu, torch.float32)).sum().backward()
+    torch.cuda.synchronize()
+    labels = ("g_xa", "g_ca", "g_xb", "g_cb", "g_w", "g_b")
+    for lab, ref_leaf, got_leaf in zip(labels, leaves, gl):
+        if ref_leaf is None or ref_leaf.grad is None:
+            continue
+        ref = ref_leaf.grad
+        got = got_leaf.grad.double().cpu()
+        rel = ((got - ref).abs().max() / ref.abs().max().clamp_min(1e-30)).item()
+        assert rel <= 1e-3, f"{name} {lab}: normwise rel err {rel:.3e}"
