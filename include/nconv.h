@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define NCONV_ABI_VERSION 1
+#define NCONV_ABI_VERSION 2
 
 /* How a layer's input (data x, confidence c) is produced from its source tensors. These are the
  * DNET glue ops fused into the layer's load stage (models/step1.py:53,61-90). */
@@ -95,18 +95,22 @@ size_t nconv_bwd_workspace_bytes(const nconv_layer* L);
 /* Backward of nconv_fwd (autograd of models/step1.py:116-149 plus the glue's backward:
  * max_pool2d routes to the first maximum of each window, nearest-upsample sums, cat splits).
  * Inputs: y, cout (the forward outputs), gy, gcout (their gradients; gcout may be NULL = 0).
- * Outputs (any may be NULL if not needed; all are ACCUMULATED into, caller zero-fills):
+ * Outputs (any may be NULL if not needed):
  *   gxa, gca : gradients of source a's (x, c)      — same shape as a
  *   gxb, gcb : gradients of source b's (x, c)      — same shape as b (UPCAT modes)
+ *              with (flags & NCONV_BWD_ACCUMULATE) these four are added into; otherwise every
+ *              element is overwritten (no zero-fill needed)
  *   gw       : (Cout, Cin/groups, KH, KW) weight gradient, OVERWRITTEN
  *   gbias    : (Cout) bias gradient, OVERWRITTEN
  * The closed form: gN = gy/(D+eps), gD = -gy*N/(D+eps)^2 + gcout/s,
  *   gb = sum gy, gs = -sum gcout*D/s^2, gW = corr(x*c, gN) + corr(c, gD) + gs,
  *   g(xc) = W^T * gN, gx = g(xc)*c, gc = W^T * gD + g(xc)*x.
  * D and N/(D+eps) are recovered from the saved outputs as cout*s and y-b. */
+#define NCONV_BWD_ACCUMULATE 1u
+
 int nconv_bwd(const nconv_layer* L, const float* y, const float* cout, const float* gy,
               const float* gcout, float* gxa, float* gca, float* gxb, float* gcb, float* gw,
-              float* gbias, void* workspace, size_t workspace_bytes, void* stream);
+              float* gbias, void* workspace, size_t workspace_bytes, unsigned flags, void* stream);
 
 #ifdef __cplusplus
 }

@@ -12,7 +12,8 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libnconv.so")
-ABI_VERSION = 1
+ABI_VERSION = 2
+BWD_ACCUMULATE = 1
 
 # enum nconv_load_mode
 PLAIN, THRESH, POOL2, UPCAT_SKIP_FIRST, UPCAT_UP_FIRST = 0, 1, 2, 3, 4
@@ -64,7 +65,7 @@ def _declare(lib):
     lib.nconv_bwd_workspace_bytes.argtypes = [ctypes.POINTER(NconvLayer)]
     lib.nconv_bwd.restype = ctypes.c_int
     lib.nconv_bwd.argtypes = [ctypes.POINTER(NconvLayer), P, P, P, P, P, P, P, P, P, P, P,
-                              ctypes.c_size_t, P]
+                              ctypes.c_size_t, ctypes.c_uint, P]
 
 
 def lib():

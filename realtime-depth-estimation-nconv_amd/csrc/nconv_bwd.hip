@@ -27,21 +27,29 @@ constexpr int pick_chunk(int n, int plane_f2, int budget) {
 }
 
 // ---- gradient routing from a layer-input pixel to the producer tensors --------------------------
+// a.accumulate != 0: += into the outputs; == 0: overwrite (every element of every requested output
+// is written exactly once, so the caller need not zero-fill; see pool_zero_leftovers).
+__device__ __forceinline__ void put(float* p, size_t i, float v, bool acc) {
+    if (acc) p[i] += v;
+    else p[i] = v;
+}
+
 template <int MODE>
 __device__ __forceinline__ void route_grad(const LayerDev& d, const BwdArgs& a, int b, int ci, int ih,
                                            int iw, float gxc, float gc_direct, float* tmp_x,
                                            float* tmp_c) {
     const nconv_layer& L = d.L;
+    const bool acc = a.accumulate != 0;
     if constexpr (MODE == NCONV_LOAD_PLAIN) {
         const size_t i = plane_idx(b, ci, L.a.C, L.a.H, L.a.W, ih, iw);
         const float x = L.a.x[i], c = L.a.c[i];
-        if (a.gxa) a.gxa[i] += gxc * c;
-        if (a.gca) a.gca[i] += gc_direct + gxc * x;
+        if (a.gxa) put(a.gxa, i, gxc * c, acc);
+        if (a.gca) put(a.gca, i, gc_direct + gxc * x, acc);
     } else if constexpr (MODE == NCONV_LOAD_THRESH) {
         const size_t i = plane_idx(b, ci, L.a.C, L.a.H, L.a.W, ih, iw);
         const float x = L.a.x[i];
         const float c = (x > L.thresh) ? 1.0f : 0.0f;
-        if (a.gxa) a.gxa[i] += gxc * c;  // c = (S > thr) carries no gradient
+        if (a.gxa) put(a.gxa, i, gxc * c, acc);  // c = (S > thr) carries no gradient
     } else if constexpr (MODE == NCONV_LOAD_POOL2) {
         const size_t i0 = plane_idx(b, ci, L.a.C, L.a.H, L.a.W, 2 * ih, 2 * iw);
         const size_t W2 = (size_t)L.a.W;
@@ -49,8 +57,17 @@ __device__ __forceinline__ void route_grad(const LayerDev& d, const BwdArgs& a, 
         int ax, ac;
         const float x = pool4(L.a.x[i0], L.a.x[i0 + 1], L.a.x[i0 + W2], L.a.x[i0 + W2 + 1], ax);
         const float c = pool4(L.a.c[i0], L.a.c[i0 + 1], L.a.c[i0 + W2], L.a.c[i0 + W2 + 1], ac);
-        if (a.gxa) a.gxa[i0 + off[ax]] += gxc * c;
-        if (a.gca) a.gca[i0 + off[ac]] += gc_direct + gxc * x;
+        const float gx = gxc * c, gc = gc_direct + gxc * x;
+        if (acc) {
+            if (a.gxa) a.gxa[i0 + off[ax]] += gx;
+            if (a.gca) a.gca[i0 + off[ac]] += gc;
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (a.gxa) a.gxa[i0 + off[k]] = (k == ax) ? gx : 0.f;
+                if (a.gca) a.gca[i0 + off[k]] = (k == ac) ? gc : 0.f;
+            }
+        }
     } else {
         const bool skip_first = (MODE == NCONV_LOAD_UPCAT_SKIP_FIRST);
         const int first_c = skip_first ? L.a.C : L.b.C;
@@ -61,8 +78,8 @@ __device__ __forceinline__ void route_grad(const LayerDev& d, const BwdArgs& a, 
         if (from_a) {
             const int ca = skip_first ? ci : ci - first_c;
             const size_t i = plane_idx(b, ca, L.a.C, L.a.H, L.a.W, ih, iw);
-            if (a.gxa) a.gxa[i] += gx;
-            if (a.gca) a.gca[i] += gc;
+            if (a.gxa) put(a.gxa, i, gx, acc);
+            if (a.gca) put(a.gca, i, gc, acc);
         } else {
             const int cb = skip_first ? ci - first_c : ci;
             const size_t i = plane_idx(b, cb, L.b.C, L.H, L.W, ih, iw);
@@ -72,9 +89,57 @@ __device__ __forceinline__ void route_grad(const LayerDev& d, const BwdArgs& a, 
     }
 }
 
-template <int MODE>
-__device__ __forceinline__ bool mode_has_tmp() {
-    return MODE == NCONV_LOAD_UPCAT_SKIP_FIRST || MODE == NCONV_LOAD_UPCAT_UP_FIRST;
+// Overwrite mode, POOL2: source rows/cols that no 2x2 window covers (odd source H or W) get 0.
+__device__ __forceinline__ void pool_zero_leftovers(const LayerDev& d, const BwdArgs& a, int b, int ci, int ih,
+                                                    int iw) {
+    const nconv_layer& L = d.L;
+    const bool oddh = (L.a.H & 1) && ih == L.H - 1, oddw = (L.a.W & 1) && iw == L.W - 1;
+    if (!(oddh || oddw)) return;
+    const size_t base = plane_idx(b, ci, L.a.C, L.a.H, L.a.W, 0, 0);
+    auto z = [&](int h, int w) {
+        if (a.gxa) a.gxa[base + (size_t)h * L.a.W + w] = 0.f;
+        if (a.gca) a.gca[base + (size_t)h * L.a.W + w] = 0.f;
+    };
+    if (oddh) { z(L.a.H - 1, 2 * iw); z(L.a.H - 1, 2 * iw + 1); }
+    if (oddw) { z(2 * ih, L.a.W - 1); z(2 * ih + 1, L.a.W - 1); }
+    if (oddh && oddw) z(L.a.H - 1, L.a.W - 1);
+}
+
+// Stage one output-side plane {gN, gD} (channel o) over an OHT x OWT halo (origin oh0, ow0):
+// lanes -> columns, waves -> rows; all loads issued before use (clamped), zero outside.
+template <int OHT, int OWT, int OWP>
+__device__ __forceinline__ void stage_gplane(const LayerDev& d, const BwdArgs& a, int b, int o, f2* t, int oh0,
+                                             int ow0, int tid) {
+    static_assert(OWT >= 64, "lanes map to columns");
+    constexpr int NR = (OHT + 3) / 4;
+    const nconv_layer& L = d.L;
+    const size_t off = ((size_t)b * L.Cout + o) * (size_t)L.Ho * L.Wo;
+    const float *gy = a.gy + off, *y = a.y + off, *co = a.co + off;
+    const float* gco = a.gco ? a.gco + off : nullptr;
+    const float bo = L.bias[o], so = L.wsum[o];
+    auto elem = [&](int r, int col, bool valid) {
+        const int oh = oh0 + r, ow = ow0 + col;
+        const bool ok = valid && (unsigned)oh < (unsigned)L.Ho && (unsigned)ow < (unsigned)L.Wo;
+        const int ohc = oh < 0 ? 0 : (oh >= L.Ho ? L.Ho - 1 : oh);
+        const int owc = ow < 0 ? 0 : (ow >= L.Wo ? L.Wo - 1 : ow);
+        const int i = ohc * L.Wo + owc;
+        float gN, gD;
+        nconv_grad_nd(gy[i], gco ? gco[i] : 0.f, y[i], co[i], L.eps, bo, so, gN, gD);
+        return ok ? (f2){gN, gD} : (f2){0.f, 0.f};
+    };
+    const int col = tid & 63, r0 = tid >> 6;
+    f2 v[NR];
+#pragma unroll
+    for (int k = 0; k < NR; ++k) v[k] = elem(r0 + 4 * k, col, true);
+#pragma unroll
+    for (int k = 0; k < NR; ++k) t[(r0 + 4 * k) * OWP + col] = v[k];
+    if constexpr (OWT > 64) {
+        constexpr int EX = OWT - 64;
+        static_assert(EX * OHT <= 256, "one pass for the extra halo columns");
+        const int r = tid / EX, cx = 64 + tid % EX;
+        const f2 g = elem(r, cx, tid < EX * OHT);
+        if (tid < EX * OHT) t[r * OWP + cx] = g;
+    }
 }
 
 // ---- dgrad: tiled, stride 1 ------------------------------------------------------------------------
@@ -84,13 +149,21 @@ struct DgCfg {
     static constexpr int TW = 64, TPR = TW / P, TH = kT / TPR;
     static constexpr int OHT = TH + K - 1, OWT = TW + K - 1;
     static constexpr int OWP = (OWT + 1) & ~1;
-    static constexpr int PLANE = OHT * OWP;
+    static constexpr int PLANE = ((OHT + 3) / 4 * 4) * OWP;  // stage_gplane writes whole 4-row groups
     static constexpr int NV = P + K - 1;
 };
+
+template <int P>
+struct VecOf;
+template <>
+struct VecOf<4> { typedef f4 T; };
+template <>
+struct VecOf<2> { typedef f2 T; };
 
 template <int CIN, int COUT, int K, int MODE>
 __global__ __launch_bounds__(kT) void dgrad_tiled(LayerDev d, BwdArgs a, float* tmp_x, float* tmp_c) {
     using C = DgCfg<CIN, K>;
+    constexpr int P = C::P;
     constexpr int OC = pick_chunk(COUT, C::PLANE, 24 * 1024);
     __shared__ __attribute__((aligned(16))) f2 tile[OC * C::PLANE];
     const nconv_layer& L = d.L;
@@ -98,67 +171,123 @@ __global__ __launch_bounds__(kT) void dgrad_tiled(LayerDev d, BwdArgs a, float* 
     const int tid = threadIdx.x, b = blockIdx.z;
     const int ih0 = blockIdx.y * C::TH, iw0 = blockIdx.x * C::TW;
     const int oh0 = ih0 + L.PH - (K - 1), ow0 = iw0 + L.PW - (K - 1);
-    const int ty = tid / C::TPR, tx = (tid % C::TPR) * C::P;
+    const int ty = tid / C::TPR, tx = (tid % C::TPR) * P;
 
-    f2 acc[CIN][C::P];
+    f2 acc[CIN][P];
 #pragma unroll
     for (int i = 0; i < CIN; ++i)
 #pragma unroll
-        for (int j = 0; j < C::P; ++j) acc[i][j] = (f2){0.f, 0.f};
+        for (int j = 0; j < P; ++j) acc[i][j] = (f2){0.f, 0.f};
 
     for (int o0 = 0; o0 < COUT; o0 += OC) {
         if (o0) __syncthreads();
-        for (int e = tid; e < OC * C::OHT * C::OWT; e += kT) {
-            const int oc = e / (C::OHT * C::OWT);
-            const int rem = e - oc * (C::OHT * C::OWT);
-            const int r = rem / C::OWT, col = rem - r * C::OWT;
-            const int oh = oh0 + r, ow = ow0 + col, o = o0 + oc;
-            float gN = 0.f, gD = 0.f;
-            if ((unsigned)oh < (unsigned)L.Ho && (unsigned)ow < (unsigned)L.Wo) {
-                const size_t i = plane_idx(b, o, COUT, L.Ho, L.Wo, oh, ow);
-                const float gco = a.gco ? a.gco[i] : 0.f;
-                nconv_grad_nd(a.gy[i], gco, a.y[i], a.co[i], L.eps, L.bias[o], L.wsum[o], gN, gD);
-            }
-            tile[oc * C::PLANE + r * C::OWP + col] = (f2){gN, gD};
-        }
+        for (int oc = 0; oc < OC; ++oc)
+            stage_gplane<C::OHT, C::OWT, C::OWP>(d, a, b, o0 + oc, tile + oc * C::PLANE, oh0, ow0, tid);
         __syncthreads();
-#pragma unroll
-        for (int oc = 0; oc < OC; ++oc) {
-#pragma unroll
-            for (int kh = 0; kh < K; ++kh) {
-                const f2* row = &tile[oc * C::PLANE + (ty + K - 1 - kh) * C::OWP + tx];
-                f2 v[C::NV];
-#pragma unroll
-                for (int m = 0; m < C::NV / 2; ++m) {
-                    f4 q = reinterpret_cast<const f4*>(row)[m];
-                    v[2 * m] = q.xy;
-                    v[2 * m + 1] = q.zw;
-                }
-                if constexpr (C::NV & 1) v[C::NV - 1] = row[C::NV - 1];
-                const float* wr = wgt + (size_t)(o0 + oc) * CIN * K * K + kh * K;
-#pragma unroll
-                for (int kw = 0; kw < K; ++kw)
-#pragma unroll
-                    for (int i = 0; i < CIN; ++i) {
-                        const float w = wr[i * K * K + kw];
-                        const f2 w2 = (f2){w, w};
-#pragma unroll
-                        for (int j = 0; j < C::P; ++j)
-                            acc[i][j] = __builtin_elementwise_fma(w2, v[j + K - 1 - kw], acc[i][j]);
-                    }
+        // one (output channel, kernel row) per iteration, not unrolled: its Cin*K weights go to SGPRs
+        const f2* row = &tile[(ty + K - 1) * C::OWP + tx];
+        const float* wr = wgt + (size_t)o0 * CIN * K * K;
+#pragma unroll 1
+        for (int q = 0; q < OC * K; ++q, row -= C::OWP, wr += K) {
+            if (q && q % K == 0) {
+                row += C::PLANE + K * C::OWP;
+                wr += CIN * K * K - K * K;
             }
+            f2 v[C::NV];
+#pragma unroll
+            for (int m = 0; m < C::NV / 2; ++m) {
+                f4 qv = reinterpret_cast<const f4*>(row)[m];
+                v[2 * m] = qv.xy;
+                v[2 * m + 1] = qv.zw;
+            }
+            if constexpr (C::NV & 1) v[C::NV - 1] = row[C::NV - 1];
+#pragma unroll
+            for (int kw = 0; kw < K; ++kw)
+#pragma unroll
+                for (int i = 0; i < CIN; ++i) {
+                    const float w = wr[i * K * K + kw];
+                    const f2 w2 = (f2){w, w};
+#pragma unroll
+                    for (int j = 0; j < P; ++j)
+                        acc[i][j] = __builtin_elementwise_fma(w2, v[j + K - 1 - kw], acc[i][j]);
+                }
         }
     }
 
+    // ---- epilogue: gx = G_xc*c, gc = G_c + G_xc*x, routed through the glue's backward ----
     const int ih = ih0 + ty;
     if (ih >= L.H) return;
+    const int iwb = iw0 + tx;
+    const bool full = (L.W % P) == 0 && iwb + P <= L.W;  // P-aligned, fully in range
+    const bool accm = a.accumulate != 0;
+    typedef typename VecOf<P>::T V;
 #pragma unroll
-    for (int i = 0; i < CIN; ++i)
+    for (int i = 0; i < CIN; ++i) {
+        if constexpr (MODE == NCONV_LOAD_POOL2) {
 #pragma unroll
-        for (int j = 0; j < C::P; ++j) {
-            const int iw = iw0 + tx + j;
-            if (iw < L.W) route_grad<MODE>(d, a, b, i, ih, iw, acc[i][j].x, acc[i][j].y, tmp_x, tmp_c);
+            for (int j = 0; j < P; ++j)
+                if (iwb + j < L.W) {
+                    route_grad<MODE>(d, a, b, i, ih, iwb + j, acc[i][j].x, acc[i][j].y, tmp_x, tmp_c);
+                    if (!accm) pool_zero_leftovers(d, a, b, i, ih, iwb + j);
+                }
+        } else {
+            const ChanSrc s = chan_src<MODE>(d, b, i);
+            if (!full) {
+#pragma unroll
+                for (int j = 0; j < P; ++j)
+                    if (iwb + j < L.W) route_grad<MODE>(d, a, b, i, ih, iwb + j, acc[i][j].x, acc[i][j].y, tmp_x, tmp_c);
+                continue;
+            }
+            // vector path: P consecutive pixels of one row
+            float x[P], c[P];
+            if (s.kind == kUp) {
+#pragma unroll
+                for (int j = 0; j < P; ++j) load_chan(d, s, ih, iwb + j, x[j], c[j]);
+            } else {
+                const V xv = *reinterpret_cast<const V*>(s.x + ih * s.W + iwb);
+#pragma unroll
+                for (int j = 0; j < P; ++j) x[j] = xv[j];
+                if (s.kind == kThresh) {
+#pragma unroll
+                    for (int j = 0; j < P; ++j) c[j] = (x[j] > L.thresh) ? 1.0f : 0.0f;
+                } else {
+                    const V cv = *reinterpret_cast<const V*>(s.c + ih * s.W + iwb);
+#pragma unroll
+                    for (int j = 0; j < P; ++j) c[j] = cv[j];
+                }
+            }
+            V gxv, gcv;
+#pragma unroll
+            for (int j = 0; j < P; ++j) {
+                gxv[j] = acc[i][j].x * c[j];
+                gcv[j] = acc[i][j].y + acc[i][j].x * x[j];
+            }
+            float *gxp, *gcp;
+            size_t off;
+            bool acc_here = accm;
+            if (s.kind == kUp) {  // upsampled channel: stage for upsample_bwd_gather
+                const bool skip_first = (MODE == NCONV_LOAD_UPCAT_SKIP_FIRST);
+                const int cb = skip_first ? i - L.a.C : i;
+                off = plane_idx(b, cb, L.b.C, L.H, L.W, ih, iwb);
+                gxp = tmp_x;
+                gcp = tmp_c;
+                acc_here = false;
+            } else {
+                const int ca = (MODE == NCONV_LOAD_UPCAT_UP_FIRST) ? i - L.b.C : i;
+                off = plane_idx(b, ca, L.a.C, L.a.H, L.a.W, ih, iwb);
+                gxp = a.gxa;
+                gcp = (s.kind == kThresh) ? nullptr : a.gca;
+            }
+            if (gxp) {
+                V* p = reinterpret_cast<V*>(gxp + off);
+                *p = acc_here ? *p + gxv : gxv;
+            }
+            if (gcp) {
+                V* p = reinterpret_cast<V*>(gcp + off);
+                *p = acc_here ? *p + gcv : gcv;
+            }
         }
+    }
 }
 
 // ---- dgrad: generic (any stride / dilation / groups) ------------------------------------------------
@@ -197,6 +326,7 @@ __global__ __launch_bounds__(kT) void dgrad_generic(LayerDev d, BwdArgs a, float
             }
         }
         route_grad<MODE>(d, a, b, ci, ih, iw, Gxc, Gc, tmp_x, tmp_c);
+        if (MODE == NCONV_LOAD_POOL2 && !a.accumulate) pool_zero_leftovers(d, a, b, ci, ih, iw);
     }
 }
 
@@ -213,7 +343,7 @@ __device__ __forceinline__ void up_range(int u, int in, int out, float scale, in
 }
 
 __global__ __launch_bounds__(kT) void upsample_bwd_gather(LayerDev d, const float* tmp_x, const float* tmp_c,
-                                                          float* gxb, float* gcb) {
+                                                          float* gxb, float* gcb, int accumulate) {
     const nconv_layer& L = d.L;
     const int Cb = L.b.C, Hb = L.b.H, Wb = L.b.W;
     const size_t n = (size_t)L.B * Cb * Hb * Wb;
@@ -231,22 +361,42 @@ __global__ __launch_bounds__(kT) void upsample_bwd_gather(LayerDev d, const floa
                 sx += tmp_x[i];
                 sc += tmp_c[i];
             }
-        if (gxb) gxb[idx] += sx;
-        if (gcb) gcb[idx] += sc;
+        if (accumulate) {
+            if (gxb) gxb[idx] += sx;
+            if (gcb) gcb[idx] += sc;
+        } else {
+            if (gxb) gxb[idx] = sx;
+            if (gcb) gcb[idx] = sc;
+        }
     }
 }
 
 // ---- wgrad: tiled partial sums, stride 1 ------------------------------------------------------------
+// A thread owns one (o, i) weight pair with all K*K taps in registers and a subset ("sub") of each
+// 4 x 64 output tile: rows, or for small Cin*Cout also column segments, so all 256 threads work
+// for every layer shape. Per output pixel it reads g = {gN, gD} once and, for each kernel row, one
+// new input {x*c, c} into a sliding window: K+1 LDS reads per K*K packed FMAs
+// {sum x*c*gN, sum c*gD} += {x*c, c} * {gN, gD}.
+constexpr int pow2ceil(int n) {
+    int p = 1;
+    while (p < n) p <<= 1;
+    return p;
+}
+
 template <int CIN, int COUT, int K>
 struct WgCfg {
     static constexpr int TH = 4, TW = 64;  // TH*TW == kT: one output pixel per thread while staging
-    static constexpr int IHT = TH + K - 1, IWT = TW + K - 1;
-    // plane strides = 1 (mod 32) f2 so that the 8 distinct channel planes a wave reads hit 8
+    static constexpr int IHT = TH + K - 1, IHTP = (IHT + 3) / 4 * 4, IWT = TW + K - 1;
+    // plane strides = 1 (mod 32) f2 so that the distinct channel planes a wave reads hit
     // different bank pairs (bank = dword % 64).
-    static constexpr int IPL = ((IHT * IWT + 31) / 32) * 32 + 1;
+    static constexpr int IPL = ((IHTP * IWT + 31) / 32) * 32 + 1;
     static constexpr int GPL = TH * TW + 1;
-    static constexpr int NCB = COUT * CIN * K;  // (kh, o, i) combos, kw kept in registers
-    static constexpr int NPASS = (NCB + kT - 1) / kT;
+    static constexpr int NCB = COUT * CIN;  // (o, i) pairs
+    static constexpr int NCBP = pow2ceil(NCB);
+    static_assert(NCBP <= kT, "wgrad_tiled: Cin*Cout must be <= 256");
+    static constexpr int NSUB = kT / NCBP;
+    static constexpr int NSEG = NSUB > TH ? NSUB / TH : 1;  // column segments per row
+    static constexpr int SEGW = TW / NSEG;
     static constexpr int LDS_F2 = CIN * IPL + COUT * GPL;
 };
 
@@ -260,98 +410,103 @@ __global__ __launch_bounds__(kT) void wgrad_tiled(LayerDev d, BwdArgs a, float* 
     const nconv_layer& L = d.L;
     const int tid = threadIdx.x;
     const int ntiles = ntile_w * ntile_h * L.B;
+    const int cb = tid % C::NCBP, sub = tid / C::NCBP;
+    const bool active = cb < C::NCB;
+    const int i = active ? cb % CIN : 0, o = active ? cb / CIN : 0;
+    // rows / column segment of this thread's sub
+    const int r_first = (C::NSUB > C::TH) ? sub % C::TH : sub;
+    const int r_step = (C::NSUB > C::TH) ? C::TH : C::NSUB;
+    const int c_first = (C::NSUB > C::TH) ? (sub / C::TH) * C::SEGW : 0;
 
-    f2 acc[C::NPASS][K];
+    f2 acc[K][K];
 #pragma unroll
-    for (int p = 0; p < C::NPASS; ++p)
+    for (int kh = 0; kh < K; ++kh)
 #pragma unroll
-        for (int k = 0; k < K; ++k) acc[p][k] = (f2){0.f, 0.f};
+        for (int kw = 0; kw < K; ++kw) acc[kh][kw] = (f2){0.f, 0.f};
     float gb_acc[COUT], gs_acc[COUT];
 #pragma unroll
-    for (int o = 0; o < COUT; ++o) gb_acc[o] = gs_acc[o] = 0.f;
+    for (int oo = 0; oo < COUT; ++oo) gb_acc[oo] = gs_acc[oo] = 0.f;
 
     for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const int tw = t % ntile_w, th = (t / ntile_w) % ntile_h, b = t / (ntile_w * ntile_h);
         const int oh0 = th * C::TH, ow0 = tw * C::TW;
         const int ih0 = oh0 - L.PH, iw0 = ow0 - L.PW;
         __syncthreads();
-        {
+        {   // g plane: one output pixel per thread per channel; loads clamped and issued up front
             const int r = tid / C::TW, col = tid % C::TW;
             const int oh = oh0 + r, ow = ow0 + col;
             const bool in = (oh < L.Ho) && (ow < L.Wo);
+            const int ohc = oh < L.Ho ? oh : L.Ho - 1, owc = ow < L.Wo ? ow : L.Wo - 1;
 #pragma unroll
-            for (int o = 0; o < COUT; ++o) {
-                float gN = 0.f, gD = 0.f;
-                if (in) {
-                    const size_t i = plane_idx(b, o, COUT, L.Ho, L.Wo, oh, ow);
-                    const float gy = a.gy[i], co = a.co[i];
-                    const float gco = a.gco ? a.gco[i] : 0.f;
-                    nconv_grad_nd(gy, gco, a.y[i], co, L.eps, L.bias[o], L.wsum[o], gN, gD);
-                    gb_acc[o] += gy;
-                    gs_acc[o] = fmaf(gco, co, gs_acc[o]);
-                }
-                sg[o * C::GPL + tid] = (f2){gN, gD};
+            for (int oo = 0; oo < COUT; ++oo) {
+                const size_t gi = plane_idx(b, oo, COUT, L.Ho, L.Wo, ohc, owc);
+                const float gy = a.gy[gi], co = a.co[gi], yv = a.y[gi];
+                const float gco = a.gco ? a.gco[gi] : 0.f;
+                float gN, gD;
+                nconv_grad_nd(gy, gco, yv, co, L.eps, L.bias[oo], L.wsum[oo], gN, gD);
+                gb_acc[oo] += in ? gy : 0.f;
+                gs_acc[oo] = in ? fmaf(gco, co, gs_acc[oo]) : gs_acc[oo];
+                sg[oo * C::GPL + tid] = in ? (f2){gN, gD} : (f2){0.f, 0.f};
             }
         }
-        for (int e = tid; e < CIN * C::IHT * C::IWT; e += kT) {
-            const int ci = e / (C::IHT * C::IWT);
-            const int rem = e - ci * (C::IHT * C::IWT);
-            const int r = rem / C::IWT, col = rem - r * C::IWT;
-            const int ih = ih0 + r, iw = iw0 + col;
-            float x = 0.f, c = 0.f;
-            if ((unsigned)ih < (unsigned)L.H && (unsigned)iw < (unsigned)L.W) load_xc<MODE>(d, b, ci, ih, iw, x, c);
-            sin[ci * C::IPL + r * C::IWT + col] = (f2){x * c, c};
-        }
+        for (int ci = 0; ci < CIN; ++ci)
+            stage_plane<C::IHT, C::IWT, C::IWT>(d, chan_src<MODE>(d, b, ci), sin + ci * C::IPL, ih0, iw0, tid);
         __syncthreads();
+        if (active) {
+            for (int r = r_first; r < C::TH; r += r_step) {
+                const f2* gr = sg + o * C::GPL + r * C::TW;
+                const f2* ir = sin + i * C::IPL + r * C::IWT;
+                f2 win[K][K];
 #pragma unroll
-        for (int p = 0; p < C::NPASS; ++p) {
-            const int cb = tid + p * kT;
-            if (cb < C::NCB) {
-                const int i = cb % CIN, o = (cb / CIN) % COUT, kh = cb / (CIN * COUT);
-                for (int r = 0; r < C::TH; ++r) {
-                    const f2* ir = sin + i * C::IPL + (r + kh) * C::IWT;
-                    const f2* gr = sg + o * C::GPL + r * C::TW;
-                    f2 win[K];
+                for (int kh = 0; kh < K; ++kh)
 #pragma unroll
-                    for (int k = 0; k < K - 1; ++k) win[k] = ir[k];
-#pragma unroll 16
-                    for (int col = 0; col < C::TW; ++col) {
-                        win[K - 1] = ir[col + K - 1];
-                        const f2 g = gr[col];
+                    for (int kw = 0; kw < K - 1; ++kw) win[kh][kw] = ir[kh * C::IWT + c_first + kw];
+#pragma unroll 4
+                for (int col = c_first; col < c_first + C::SEGW; ++col) {
+                    const f2 g = gr[col];
 #pragma unroll
-                        for (int k = 0; k < K; ++k) acc[p][k] = __builtin_elementwise_fma(win[k], g, acc[p][k]);
+                    for (int kh = 0; kh < K; ++kh) {
+                        win[kh][K - 1] = ir[kh * C::IWT + col + K - 1];
 #pragma unroll
-                        for (int k = 0; k < K - 1; ++k) win[k] = win[k + 1];
+                        for (int kw = 0; kw < K; ++kw)
+                            acc[kh][kw] = __builtin_elementwise_fma(win[kh][kw], g, acc[kh][kw]);
+#pragma unroll
+                        for (int kw = 0; kw < K - 1; ++kw) win[kh][kw] = win[kh][kw + 1];
                     }
                 }
             }
         }
     }
 
+    // ---- combine the subs in a fixed order, then the gb / gs sums; write the partial row ----
     // partial[blk] = { gW-partial[COUT*CIN*K*K], sum gy[COUT], sum gco*cout[COUT] }
-    float* out = part + (size_t)blockIdx.x * (COUT * CIN * K * K + 2 * COUT);
-#pragma unroll
-    for (int p = 0; p < C::NPASS; ++p) {
-        const int cb = tid + p * kT;
-        if (cb < C::NCB) {
-            const int i = cb % CIN, o = (cb / CIN) % COUT, kh = cb / (CIN * COUT);
-#pragma unroll
-            for (int k = 0; k < K; ++k) out[((o * CIN + i) * K + kh) * K + k] = acc[p][k].x + acc[p][k].y;
-        }
-    }
-    // block reduction of gb / gs in a fixed order
-    __syncthreads();
+    constexpr int NW = COUT * CIN * K * K;
+    float* out = part + (size_t)blockIdx.x * (NW + 2 * COUT);
     float* red = reinterpret_cast<float*>(smem);
+    __syncthreads();
+    if (active) {
 #pragma unroll
-    for (int o = 0; o < COUT; ++o) {
-        red[o * kT + tid] = gb_acc[o];
-        red[(COUT + o) * kT + tid] = gs_acc[o];
+        for (int kh = 0; kh < K; ++kh)
+#pragma unroll
+            for (int kw = 0; kw < K; ++kw) red[(sub * C::NCB + cb) * K * K + kh * K + kw] = acc[kh][kw].x + acc[kh][kw].y;
+    }
+    __syncthreads();
+    for (int w = tid; w < NW; w += kT) {  // w = ((o*CIN + i)*K + kh)*K + kw = cb*K*K + tap
+        float sum = 0.f;
+        for (int sb = 0; sb < C::NSUB; ++sb) sum += red[sb * NW + w];
+        out[w] = sum;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int oo = 0; oo < COUT; ++oo) {
+        red[oo * kT + tid] = gb_acc[oo];
+        red[(COUT + oo) * kT + tid] = gs_acc[oo];
     }
     __syncthreads();
     if (tid < 2 * COUT) {
-        float s = 0.f;
-        for (int k = 0; k < kT; ++k) s += red[tid * kT + k];
-        out[COUT * CIN * K * K + tid] = s;
+        float sum = 0.f;
+        for (int k = 0; k < kT; ++k) sum += red[tid * kT + k];
+        out[NW + tid] = sum;
     }
 }
 
@@ -412,27 +567,50 @@ __global__ __launch_bounds__(kT) void wgrad_generic(LayerDev d, BwdArgs a, float
 }
 
 // ---- wgrad: fixed-order reduction of the per-block partials ----------------------------------------
-__global__ __launch_bounds__(kT) void wgrad_reduce(const float* part, int nblk, int nw, int cout, int fan,
-                                                   const float* wsum, float* gw, float* gb) {
-    const int stride = nw + 2 * cout;
+// Stage 1: tot[e] = sum_k part[k][e] for every entry e of a partial row (weights, sum gy, sum
+// gco*cout). A 256-thread block owns 64 consecutive entries; its 4 waves sum interleaved subsets of
+// the partial rows (coalesced 256-B rows, 8 independent loads in flight per lane) and combine the
+// 4 subtotals in LDS in a fixed order — deterministic, no atomics.
+__global__ __launch_bounds__(kT) void wgrad_reduce_sum(const float* part, int nblk, int stride, float* tot) {
+    __shared__ float red[kT];
+    const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
+    const int e = blockIdx.x * 64 + lane;
+    float s = 0.f;
+    if (e < stride) {
+        int k = grp;
+        for (; k + 28 < nblk; k += 32) {
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = part[(size_t)(k + 4 * u) * stride + e];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) s += v[u];
+        }
+        for (; k < nblk; k += 4) s += part[(size_t)k * stride + e];
+    }
+    red[threadIdx.x] = s;
+    __syncthreads();
+    if (grp == 0 && e < stride) tot[e] = ((red[lane] + red[64 + lane]) + red[128 + lane]) + red[192 + lane];
+}
+
+// Stage 2: gW[w] = tot[w] + gs[o(w)] with gs = -(sum gco*cout)/s (d cout / d s, cout = D/s), gb = sum gy.
+__global__ __launch_bounds__(kT) void wgrad_finish(const float* tot, int nw, int cout, int fan, const float* wsum,
+                                                   float* gw, float* gb) {
     for (int w = blockIdx.x * kT + threadIdx.x; w < nw + cout; w += gridDim.x * kT) {
         if (w < nw) {
             const int o = w / fan;
-            float s = 0.f, gsum = 0.f;
-            for (int k = 0; k < nblk; ++k) {
-                s += part[(size_t)k * stride + w];
-                gsum += part[(size_t)k * stride + nw + cout + o];
-            }
-            const float so = wsum[o];
-            const float gs = -gsum / so;  // d/ds of cout = D/s, summed: -sum gco*D/s^2 = -sum(gco*cout)/s
-            if (gw) gw[w] = s + gs;
-        } else {
-            const int o = w - nw;
-            float s = 0.f;
-            for (int k = 0; k < nblk; ++k) s += part[(size_t)k * stride + nw + o];
-            if (gb) gb[o] = s;
+            if (gw) gw[w] = tot[w] + (-tot[nw + cout + o] / wsum[o]);
+        } else if (gb) {
+            gb[w - nw] = tot[w];
         }
     }
+}
+
+static void launch_wgrad_reduce(const float* part, int nblk, int nw, int cout, int fan, const float* wsum,
+                                float* gw, float* gb, float* tot, hipStream_t st) {
+    const int stride = nw + 2 * cout;
+    hipLaunchKernelGGL(wgrad_reduce_sum, dim3((stride + 63) / 64), dim3(kT), 0, st, part, nblk, stride, tot);
+    hipLaunchKernelGGL(wgrad_finish, dim3((nw + cout + kT - 1) / kT), dim3(kT), 0, st, tot, nw, cout, fan, wsum,
+                       gw, gb);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -485,7 +663,7 @@ size_t bwd_workspace_bytes(const LayerDev& d) {
     const int fan = (L.Cin / L.groups) * L.KH * L.KW;
     const size_t stride = (size_t)L.Cout * fan + 2 * L.Cout;
     const size_t nblk = pick_path(L) == kTiled ? wg_blocks(L) : (size_t)generic_chunks(L);
-    size_t bytes = nblk * stride * sizeof(float);
+    size_t bytes = (nblk + 1) * stride * sizeof(float);  // partial rows + the reduced row
     bytes = (bytes + 255) & ~(size_t)255;
     if (L.load_mode == NCONV_LOAD_UPCAT_SKIP_FIRST || L.load_mode == NCONV_LOAD_UPCAT_UP_FIRST)
         bytes += 2 * (size_t)L.B * L.b.C * L.H * L.W * sizeof(float);
@@ -506,12 +684,14 @@ static void go_bwd_tiled(const LayerDev& d, const BwdArgs& a, float* part, float
         const int ntw = (L.Wo + W::TW - 1) / W::TW, nth = (L.Ho + W::TH - 1) / W::TH;
         const int nblk = (int)wg_blocks(L);
         size_t lds = (size_t)W::LDS_F2 * sizeof(f2);
-        const size_t red = (size_t)2 * COUT * kT * sizeof(float);
+        size_t red = (size_t)2 * COUT * kT * sizeof(float);
+        const size_t red2 = (size_t)W::NSUB * COUT * CIN * K * K * sizeof(float);
+        if (red2 > red) red = red2;
         if (red > lds) lds = red;
         hipLaunchKernelGGL((wgrad_tiled<CIN, COUT, K, MODE>), dim3(nblk), dim3(kT), lds, st, d, a, part, ntw, nth);
         const int nw = COUT * CIN * K * K;
-        hipLaunchKernelGGL(wgrad_reduce, dim3((nw + COUT + kT - 1) / kT), dim3(kT), 0, st, part, nblk, nw, COUT,
-                           CIN * K * K, L.wsum, a.gw, a.gb);
+        launch_wgrad_reduce(part, nblk, nw, COUT, CIN * K * K, L.wsum, a.gw, a.gb,
+                            part + (size_t)nblk * (nw + 2 * COUT), st);
     }
 }
 
@@ -530,8 +710,8 @@ static void go_bwd_generic(const LayerDev& d, const BwdArgs& a, float* part, flo
         const int nw = L.Cout * fan;
         const int nchunk = generic_chunks(L);
         hipLaunchKernelGGL(wgrad_generic<MODE>, dim3(nchunk, nw + 2 * L.Cout), dim3(kT), 0, st, d, a, part, nchunk);
-        hipLaunchKernelGGL(wgrad_reduce, dim3((nw + L.Cout + kT - 1) / kT), dim3(kT), 0, st, part, nchunk, nw,
-                           L.Cout, fan, L.wsum, a.gw, a.gb);
+        launch_wgrad_reduce(part, nchunk, nw, L.Cout, fan, L.wsum, a.gw, a.gb,
+                            part + (size_t)nchunk * (nw + 2 * L.Cout), st);
     }
 }
 
@@ -546,7 +726,7 @@ int launch_bwd(const LayerDev& d, const BwdArgs& a, hipStream_t st, const char**
     const Path path = pick_path(L);
     const size_t nblk = path == kTiled ? wg_blocks(L) : (size_t)generic_chunks(L);
     float* part = a.ws;
-    float* tx = a.ws + (((nblk * stride * sizeof(float)) + 255) & ~(size_t)255) / sizeof(float);
+    float* tx = a.ws + ((((nblk + 1) * stride * sizeof(float)) + 255) & ~(size_t)255) / sizeof(float);
     float* tc = tx + (size_t)L.B * L.b.C * L.H * L.W;
     const bool up = L.load_mode == NCONV_LOAD_UPCAT_SKIP_FIRST || L.load_mode == NCONV_LOAD_UPCAT_UP_FIRST;
 
@@ -572,7 +752,8 @@ int launch_bwd(const LayerDev& d, const BwdArgs& a, hipStream_t st, const char**
         const size_t n = (size_t)L.B * L.b.C * L.b.H * L.b.W;
         size_t blocks = (n + kT - 1) / kT;
         if (blocks > (1u << 20)) blocks = 1u << 20;
-        if (blocks) hipLaunchKernelGGL(upsample_bwd_gather, dim3(blocks), dim3(kT), 0, st, d, tx, tc, a.gxb, a.gcb);
+        if (blocks) hipLaunchKernelGGL(upsample_bwd_gather, dim3(blocks), dim3(kT), 0, st, d, tx, tc, a.gxb, a.gcb,
+                                      a.accumulate);
     }
     return last_err(why);
 }

@@ -110,7 +110,7 @@ size_t nconv_bwd_workspace_bytes(const nconv_layer* L) {
 
 int nconv_bwd(const nconv_layer* L, const float* y, const float* cout, const float* gy,
               const float* gcout, float* gxa, float* gca, float* gxb, float* gcb, float* gw,
-              float* gbias, void* workspace, size_t workspace_bytes, void* stream) {
+              float* gbias, void* workspace, size_t workspace_bytes, unsigned flags, void* stream) {
     if (const char* why = validate(L, true)) return fail(-22, "nconv_bwd", why);
     if (!y || !cout || !gy) return fail(-22, "nconv_bwd", "null y/cout/gy");
     const LayerDev d = make_dev(L);
@@ -119,7 +119,8 @@ int nconv_bwd(const nconv_layer* L, const float* y, const float* cout, const flo
     const int fan = (L->Cin / L->groups) * L->KH * L->KW;
     if ((long)L->Cout * fan + 2L * L->Cout > 65535)
         return fail(-22, "nconv_bwd", "weight-gradient path supports at most 65535 weights per layer");
-    nconv::BwdArgs a{y, cout, gy, gcout, gxa, gca, gxb, gcb, gw, gbias, (float*)workspace, workspace_bytes};
+    nconv::BwdArgs a{y, cout, gy, gcout, gxa, gca, gxb, gcb, gw, gbias, (float*)workspace, workspace_bytes,
+                     (flags & NCONV_BWD_ACCUMULATE) ? 1 : 0};
     const char* why = nullptr;
     int rc = nconv::launch_bwd(d, a, (hipStream_t)stream, &why);
     return rc ? fail(rc, "nconv_bwd", why) : 0;

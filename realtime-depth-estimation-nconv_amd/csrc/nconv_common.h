@@ -111,3 +111,128 @@ __device__ __forceinline__ void nconv_grad_nd(float gy, float gco, float y, floa
     gN = gy / den;
     gD = -(gy * r) / den + gco / s;
 }
+
+// ------------------------------------------------------------------------------------------------
+// Tile staging. A layer-input channel's source is resolved once per (image, channel) — a
+// wave-uniform decision — so the per-element work is one bounds test, 32-bit plane offsets,
+// the glue's loads and one ds_write_b64.
+// ------------------------------------------------------------------------------------------------
+enum ChanKind { kDirect = 0, kThresh = 1, kPool = 2, kUp = 3 };
+
+struct ChanSrc {
+    const float* x;
+    const float* c;
+    int W;     // row pitch of the source plane
+    int kind;  // ChanKind
+};
+
+template <int MODE>
+__device__ __forceinline__ ChanSrc chan_src(const LayerDev& d, int b, int ci) {
+    const nconv_layer& L = d.L;
+    ChanSrc s;
+    if constexpr (MODE == NCONV_LOAD_PLAIN || MODE == NCONV_LOAD_THRESH || MODE == NCONV_LOAD_POOL2) {
+        const size_t off = ((size_t)b * L.a.C + ci) * (size_t)L.a.H * L.a.W;
+        s.x = L.a.x + off;
+        s.c = (MODE == NCONV_LOAD_THRESH) ? nullptr : L.a.c + off;
+        s.W = L.a.W;
+        s.kind = (MODE == NCONV_LOAD_PLAIN) ? kDirect : (MODE == NCONV_LOAD_THRESH) ? kThresh : kPool;
+    } else {
+        const bool skip_first = (MODE == NCONV_LOAD_UPCAT_SKIP_FIRST);
+        const int first_c = skip_first ? L.a.C : L.b.C;
+        const bool from_a = skip_first ? (ci < first_c) : (ci >= first_c);
+        if (from_a) {
+            const int ca = skip_first ? ci : ci - first_c;
+            const size_t off = ((size_t)b * L.a.C + ca) * (size_t)L.a.H * L.a.W;
+            s.x = L.a.x + off;
+            s.c = L.a.c + off;
+            s.W = L.a.W;
+            s.kind = kDirect;
+        } else {
+            const int cb = skip_first ? ci - first_c : ci;
+            const size_t off = ((size_t)b * L.b.C + cb) * (size_t)L.b.H * L.b.W;
+            s.x = L.b.x + off;
+            s.c = L.b.c + off;
+            s.W = L.b.W;
+            s.kind = kUp;
+        }
+    }
+    return s;
+}
+
+// (x, c) of the layer input at (ih, iw), in range, from a resolved channel source.
+__device__ __forceinline__ void load_chan(const LayerDev& d, const ChanSrc& s, int ih, int iw, float& x,
+                                          float& c) {
+    if (s.kind == kDirect) {
+        const int i = ih * s.W + iw;
+        x = s.x[i];
+        c = s.c[i];
+    } else if (s.kind == kThresh) {
+        x = s.x[ih * s.W + iw];
+        c = (x > d.L.thresh) ? 1.0f : 0.0f;
+    } else if (s.kind == kPool) {
+        const int i = (2 * ih) * s.W + 2 * iw;
+        if ((s.W & 1) == 0) {
+            const f2 x0 = *(const f2*)(s.x + i), x1 = *(const f2*)(s.x + i + s.W);
+            const f2 c0 = *(const f2*)(s.c + i), c1 = *(const f2*)(s.c + i + s.W);
+            x = pool4v(x0.x, x0.y, x1.x, x1.y);
+            c = pool4v(c0.x, c0.y, c1.x, c1.y);
+        } else {
+            x = pool4v(s.x[i], s.x[i + 1], s.x[i + s.W], s.x[i + s.W + 1]);
+            c = pool4v(s.c[i], s.c[i + 1], s.c[i + s.W], s.c[i + s.W + 1]);
+        }
+    } else {
+        const int sh = nearest_src(ih, d.L.b.H, d.L.H, d.up_scale_h);
+        const int sw = nearest_src(iw, d.L.b.W, d.L.W, d.up_scale_w);
+        const int i = sh * s.W + sw;
+        x = s.x[i];
+        c = s.c[i];
+    }
+}
+
+// Stage one channel plane of {x*c, c} over an IHT x IWT halo tile (origin ih0, iw0) into t
+// (row pitch IWP; the plane must hold round_up(IHT, 4) rows: the last row group is written
+// unconditionally). 256 threads; IWT >= 64: lanes map to columns, waves to rows. Every load of a
+// thread is issued before the first is consumed (addresses clamped into the plane, out-of-range
+// elements zeroed afterwards), so a thread has all its row loads in flight at once instead of
+// one branch-guarded load per element.
+template <int IHT, int IWT, int IWP>
+__device__ __forceinline__ void stage_plane(const LayerDev& d, const ChanSrc& s, f2* t, int ih0, int iw0,
+                                            int tid) {
+    static_assert(IWT >= 64, "stage_plane maps 64 lanes to columns");
+    constexpr int NR = (IHT + 3) / 4;
+    const int H = d.L.H, W = d.L.W;
+    const int col = tid & 63, r0 = tid >> 6;
+    const int iw = iw0 + col;
+    const bool wok = (unsigned)iw < (unsigned)W;
+    const int iwc = iw < 0 ? 0 : (iw >= W ? W - 1 : iw);
+    float xs[NR], cs[NR];
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+        const int ih = ih0 + r0 + 4 * k;
+        const int ihc = ih < 0 ? 0 : (ih >= H ? H - 1 : ih);
+        load_chan(d, s, ihc, iwc, xs[k], cs[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {  // rows >= IHT land in the plane's padding rows (see IHTP)
+        const int r = r0 + 4 * k;
+        const int ih = ih0 + r;
+        const bool ok = wok && (unsigned)ih < (unsigned)H;
+        const float x = ok ? xs[k] : 0.f, c = ok ? cs[k] : 0.f;
+        t[r * IWP + col] = (f2){x * c, c};
+    }
+    if constexpr (IWT > 64) {
+        constexpr int EX = IWT - 64;
+        static_assert(EX * IHT <= 256, "one pass for the extra halo columns");
+        const int e = tid;
+        const int r = e / EX, cx = 64 + e % EX;
+        const int ih = ih0 + r, iw2 = iw0 + cx;
+        const bool ok = e < EX * IHT && (unsigned)ih < (unsigned)H && (unsigned)iw2 < (unsigned)W;
+        const int ihc = ih < 0 ? 0 : (ih >= H ? H - 1 : ih);
+        const int iwc2 = iw2 < 0 ? 0 : (iw2 >= W ? W - 1 : iw2);
+        float x, c;
+        load_chan(d, s, ihc, iwc2, x, c);
+        x = ok ? x : 0.f;
+        c = ok ? c : 0.f;
+        if (e < EX * IHT) t[r * IWP + cx] = (f2){x * c, c};
+    }
+}

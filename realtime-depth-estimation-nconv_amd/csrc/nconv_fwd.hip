@@ -30,7 +30,7 @@ struct FwdCfg {
     static constexpr int P = 4, TW = 64, TH = 16;
     static constexpr int IHT = TH + K - 1, IWT = TW + K - 1;
     static constexpr int IWP = (IWT + 1) & ~1;  // even pitch keeps the f4 reads 16-B aligned
-    static constexpr int PLANE = IHT * IWP;
+    static constexpr int PLANE = ((IHT + 3) / 4 * 4) * IWP;  // stage_plane writes whole 4-row groups
     static constexpr int CC = pick_cc(CIN, PLANE);
     static constexpr int NV = P + K - 1;  // sliding-window width per kernel row
 };
@@ -59,44 +59,37 @@ __global__ __launch_bounds__(kThreads) void fwd_tiled(LayerDev d, float* __restr
     for (int c0 = 0; c0 < CIN; c0 += C::CC) {
         if (c0) __syncthreads();
         // ---- stage CC planes of {x*c, c} over the haloed input tile (glue fused here) ----
-        for (int e = tid; e < C::CC * C::IHT * C::IWT; e += kThreads) {
-            const int cc = e / (C::IHT * C::IWT);
-            const int rem = e - cc * (C::IHT * C::IWT);
-            const int r = rem / C::IWT;
-            const int col = rem - r * C::IWT;
-            const int ih = ih0 + r, iw = iw0 + col;
-            float x = 0.f, c = 0.f;
-            if ((unsigned)ih < (unsigned)L.H && (unsigned)iw < (unsigned)L.W)
-                load_xc<MODE>(d, b, c0 + cc, ih, iw, x, c);
-            tile[cc * C::PLANE + r * C::IWP + col] = (f2){x * c, c};
-        }
+        for (int cc = 0; cc < C::CC; ++cc)
+            stage_plane<C::IHT, C::IWT, C::IWP>(d, chan_src<MODE>(d, b, c0 + cc), tile + cc * C::PLANE, ih0,
+                                                iw0, tid);
         __syncthreads();
         // ---- packed-FP32 accumulation: {N, D} += w * {x*c, c} ----
+        // One (channel, kernel-row) pair per iteration, deliberately not unrolled: its K*Cout
+        // weights are loaded into SGPRs (s_load) right before use. Unrolling lets the compiler
+        // hoist every weight of the chunk into SGPRs, which spills them through v_writelane.
+        const f2* row = &tile[ty * C::IWP + tx];
+        const float* wr = wgt + (size_t)c0 * K * K;  // weights of (c0+cc, kh) are K contiguous floats
+#pragma unroll 1
+        for (int q = 0; q < C::CC * K; ++q, row += C::IWP, wr += K) {
+            if (q && q % K == 0) row += C::PLANE - K * C::IWP;  // next staged channel plane
+            f2 v[C::NV];
 #pragma unroll
-        for (int cc = 0; cc < C::CC; ++cc) {
-#pragma unroll
-            for (int kh = 0; kh < K; ++kh) {
-                const f2* row = &tile[cc * C::PLANE + (ty + kh) * C::IWP + tx];
-                f2 v[C::NV];
-#pragma unroll
-                for (int m = 0; m < C::NV / 2; ++m) {
-                    f4 q = reinterpret_cast<const f4*>(row)[m];
-                    v[2 * m] = q.xy;
-                    v[2 * m + 1] = q.zw;
-                }
-                if constexpr (C::NV & 1) v[C::NV - 1] = row[C::NV - 1];
-                const float* wr = wgt + ((size_t)(c0 + cc) * K + kh) * K;
-#pragma unroll
-                for (int kw = 0; kw < K; ++kw)
-#pragma unroll
-                    for (int o = 0; o < COUT; ++o) {
-                        const float w = wr[o * CIN * K * K + kw];
-                        const f2 w2 = (f2){w, w};
-#pragma unroll
-                        for (int j = 0; j < C::P; ++j)
-                            acc[o][j] = __builtin_elementwise_fma(w2, v[j + kw], acc[o][j]);
-                    }
+            for (int m = 0; m < C::NV / 2; ++m) {
+                f4 qv = reinterpret_cast<const f4*>(row)[m];
+                v[2 * m] = qv.xy;
+                v[2 * m + 1] = qv.zw;
             }
+            if constexpr (C::NV & 1) v[C::NV - 1] = row[C::NV - 1];
+#pragma unroll
+            for (int kw = 0; kw < K; ++kw)
+#pragma unroll
+                for (int o = 0; o < COUT; ++o) {
+                    const float w = wr[o * CIN * K * K + kw];
+                    const f2 w2 = (f2){w, w};
+#pragma unroll
+                    for (int j = 0; j < C::P; ++j)
+                        acc[o][j] = __builtin_elementwise_fma(w2, v[j + kw], acc[o][j]);
+                }
         }
     }
 

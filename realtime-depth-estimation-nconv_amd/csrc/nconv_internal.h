@@ -28,6 +28,7 @@ struct BwdArgs {
     float* gb;
     float* ws;  // workspace
     size_t ws_bytes;
+    int accumulate;  // 1: += into gxa/gca/gxb/gcb; 0: overwrite every element
 };
 
 // Forward. Return 0, or a negative errno with *why set.

@@ -120,7 +120,8 @@ class NConvLayerFn(torch.autograd.Function):
             gy = torch.zeros_like(y)
         gy = gy.contiguous()
         gco = gco.contiguous() if gco is not None else None
-        z = lambda t, n: torch.zeros_like(t) if (t is not None and n) else None
+        # the kernels overwrite every element of the input gradients (no zero-fill)
+        z = lambda t, n: torch.empty_like(t) if (t is not None and n) else None
         gxa, gca, gxb, gcb = z(xa, need[1]), z(ca, need[2]), z(xb, need[3]), z(cb, need[4])
         gw = torch.empty_like(weight) if need[5] else None
         gb = torch.empty_like(bias) if need[6] else None
@@ -130,7 +131,7 @@ class NConvLayerFn(torch.autograd.Function):
         ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
         rc = lib.nconv_bwd(_lib.ctypes.byref(L), _lib.ptr(y), _lib.ptr(co), _lib.ptr(gy), _lib.ptr(gco),
                            _lib.ptr(gxa), _lib.ptr(gca), _lib.ptr(gxb), _lib.ptr(gcb), _lib.ptr(gw),
-                           _lib.ptr(gb), _lib.ptr(ws), ws_bytes, _lib.stream_handle(dev))
+                           _lib.ptr(gb), _lib.ptr(ws), ws_bytes, 0, _lib.stream_handle(dev))
         _lib.check(rc, "nconv_bwd")
         return None, gxa, gca, gxb, gcb, gw, gb, None
 
