@@ -461,8 +461,10 @@ __global__ __launch_bounds__(kT) void wgrad_tiled(LayerDev d, BwdArgs a, float* 
                 for (int kh = 0; kh < K; ++kh)
 #pragma unroll
                     for (int kw = 0; kw < K - 1; ++kw) win[kh][kw] = ir[kh * C::IWT + c_first + kw];
-#pragma unroll 4
-                for (int col = c_first; col < c_first + C::SEGW; ++col) {
+                // fully unrolled: the window shifts below become register renames
+#pragma unroll
+                for (int cc = 0; cc < C::SEGW; ++cc) {
+                    const int col = c_first + cc;
                     const f2 g = gr[col];
 #pragma unroll
                     for (int kh = 0; kh < K; ++kh) {

@@ -14,19 +14,26 @@ import torch.nn.functional as F
 import torch.optim as optimizer
 
 
-def _sobel(img, rows):
+def _padded(img):
     if img.dim() == 3:
         img = img.unsqueeze(0)
-    k = torch.tensor([[rows]], dtype=img.dtype, device=img.device)
-    return F.conv2d(img, k, padding=1).squeeze(0)
+    return F.pad(img, (1, 1, 1, 1)), img.shape[-2], img.shape[-1]
 
 
 def gradient_x(img):
-    return _sobel(img, [[1, 0, -1], [2, 0, -2], [1, 0, -1]])
+    """F.conv2d(img, [[1,0,-1],[2,0,-2],[1,0,-1]], padding=1) (utils.py:95-106) as shifted
+    differences: a 1-channel 3x3 correlation is a poor fit for a library conv (MIOpen picks a naive
+    fp64-accumulating kernel for this shape)."""
+    p, H, W = _padded(img)
+    d = p[..., :, 0:W] - p[..., :, 2:W + 2]
+    return (d[..., 0:H, :] + 2 * d[..., 1:H + 1, :] + d[..., 2:H + 2, :]).squeeze(0)
 
 
 def gradient_y(img):
-    return _sobel(img, [[1, 2, 1], [0, 0, 0], [-1, -2, -1]])
+    """F.conv2d(img, [[1,2,1],[0,0,0],[-1,-2,-1]], padding=1) (utils.py:109-122)."""
+    p, H, W = _padded(img)
+    d = p[..., 0:H, :] - p[..., 2:H + 2, :]
+    return (d[..., :, 0:W] + 2 * d[..., :, 1:W + 1] + d[..., :, 2:W + 2]).squeeze(0)
 
 
 def gradient_loss(input_img, predicted_img):

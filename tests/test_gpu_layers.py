@@ -90,3 +90,68 @@ def test_layer_backward(nconv_amd, gpu, case):
         got = got_leaf.grad.double().cpu()
         rel = ((got - ref).abs().max() / ref.abs().max().clamp_min(1e-30)).item()
         assert rel <= 1e-3, f"{name} {lab}: normwise rel err {rel:.3e}"
+
+
+@pytest.mark.parametrize("case", [c for c in LAYER_CASES if c[0] in ("nconv2_plain", "down_pool_odd",
+                                                                      "nconv5_upcat_inexact", "generic_stride2")],
+                         ids=lambda c: c[0])
+def test_bwd_accumulate_flag(nconv_amd, gpu, case):
+    """NCONV_BWD_ACCUMULATE adds into pre-filled input-gradient buffers; without it every element
+    is overwritten (garbage-filled buffers must come out identical to zero-filled ones)."""
+    import ctypes
+    lib = nconv_amd._lib
+    xa, ca, xb, cb, w, b = _build(case, 77)
+    spec = _spec(nconv_amd, case)
+    t = [_gpu(v, gpu) for v in (xa, ca, xb, cb, w, b)]
+    wsum = _wsum(nconv_amd, t[4])
+    y, co = nconv_amd.nconv.layer_forward_raw(spec, *t[:4], t[4], t[5], wsum)
+    gy, gc = torch.randn_like(y), torch.randn_like(co)
+    L = spec.descriptor(*t[:4], t[4], t[5], wsum)
+    ws_bytes = lib.lib().nconv_bwd_workspace_bytes(ctypes.byref(L))
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=gpu)
+
+    def run(fill, flags):
+        outs = [torch.full_like(v, fill) if v is not None else None for v in t[:4]]
+        gw, gb = torch.empty_like(t[4]), torch.empty_like(t[5])
+        rc = lib.lib().nconv_bwd(ctypes.byref(L), lib.ptr(y), lib.ptr(co), lib.ptr(gy), lib.ptr(gc),
+                                 *[lib.ptr(o) for o in outs], lib.ptr(gw), lib.ptr(gb), lib.ptr(ws), ws_bytes,
+                                 flags, lib.stream_handle(gpu))
+        lib.check(rc, "nconv_bwd")
+        torch.cuda.synchronize()
+        return outs, gw, gb
+
+    o0, gw0, gb0 = run(0.0, 0)
+    o1, gw1, gb1 = run(float("nan"), 0)
+    o2, gw2, gb2 = run(1.5, lib.BWD_ACCUMULATE)
+    for a0, a1, a2 in zip(o0, o1, o2):
+        if a0 is None:
+            continue
+        assert torch.equal(a0, a1), "overwrite mode left unwritten elements"
+        torch.testing.assert_close(a2, a0 + 1.5, rtol=1e-6, atol=1e-6)
+    assert torch.equal(gw0, gw1) and torch.equal(gw0, gw2) and torch.equal(gb0, gb2)
+
+
+def test_nconv2d_module_train_step(nconv_amd, gpu):
+    """Standalone NConv2d (the reference's layer API): EnforcePos pre-hook + forward + backward."""
+    from oracle import nconv_ref as R
+    torch.manual_seed(3)
+    layer = nconv_amd.NConv2d(8, 8, (5, 5), "softplus", "p", padding=(2, 2)).to(gpu)
+    w0 = layer.weight.detach().double().cpu().clone()
+    g = torch.Generator().manual_seed(5)
+    x, c = rand_pair(g, 2, 8, 30, 44, dtype=torch.float64)
+    layer.train()
+    xg, cg = _gpu(x, gpu, True), _gpu(c, gpu, True)
+    y, co = layer(xg, cg)
+    wr = R.softplus_pos(w0).requires_grad_(True)
+    br = layer.bias.detach().double().cpu().clone().requires_grad_(True)
+    xr, cr = x.clone().requires_grad_(True), c.clone().requires_grad_(True)
+    ry, rc = R.nconv2d(xr, cr, wr, br, (1, 1), (2, 2))
+    torch.testing.assert_close(layer.weight.detach().double().cpu(), wr.detach(), rtol=2e-6, atol=2e-7)
+    torch.testing.assert_close(y.double().cpu(), ry, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(co.double().cpu(), rc, rtol=1e-4, atol=1e-6)
+    gy = torch.randn(ry.shape, generator=g, dtype=torch.float64)
+    (ry * gy + rc).sum().backward()
+    (y * gy.to(gpu, torch.float32) + co).sum().backward()
+    for got, ref in ((xg.grad, xr.grad), (cg.grad, cr.grad), (layer.weight.grad, wr.grad), (layer.bias.grad, br.grad)):
+        rel = ((got.double().cpu() - ref).abs().max() / ref.abs().max()).item()
+        assert rel <= 1e-3, rel
