@@ -132,6 +132,24 @@ def time_layers(m, net, S, reps=20):
     return out
 
 
+def pmc_traffic(kernel, B, H, W):
+    """HBM bytes per launch of `kernel` from the committed PMC summary (profiles/pmc_traffic.json,
+    written by tools/pmc_traffic.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes,
+    FETCH_SIZE doubled per MI355X_MICROARCH.md's gfx950 correction), or None if not measured for
+    this configuration."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        d = json.load(open(path))
+        e = d.get("kernels", {}).get(kernel)
+        if e and tuple(d.get("config", ())) == (B, H, W):
+            return e["hbm_bytes_per_launch"]
+    except (ValueError, KeyError, TypeError):
+        return None
+    return None
+
+
 def cpu_baseline(B, H, W, seconds):
     """The oracle (oracle/nconv_ref.py: the reference's DNET forward restated with the same torch
     CPU ops; bitwise equal to the reference on the same torch build) timed on this host."""
@@ -272,15 +290,19 @@ def main():
     if rank == 0:
         lt = time_layers(m, net, S)
         costs = layer_costs(B, H, W)
-        dom = max(LAYERS, key=lambda n: lt[n])
+        costs["nconv6+7_tail"] = fused_tail_cost(B, H, W)
+        # kernels of the timed inference pass: nconv1..5 + the fused nconv6+7 tail
+        infer = [n for n in LAYERS if n not in ("nconv6", "nconv7")] + ["nconv6+7_tail"]
+        dom = max(infer, key=lambda n: lt[n])
         byt, fl = costs[dom]
         us = lt[dom]
+        traffic = pmc_traffic(dom, B, H, W)
         gbs = byt / (us * 1e-6) / 1e9
         tfl = fl / (us * 1e-6) / 1e12
         tail_b, tail_f = fused_tail_cost(B, H, W)
         pass_bytes = 238.44e6 * B if (H, W) == (352, 1216) else None
         roof = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "kernel": f"{dom} (fwd_tiled)", "kernel_us": round(us, 2),
                 "algorithmic_bytes_per_launch": byt, "flops_per_launch": fl,
                 "fp32_tflops": round(tfl, 2), "fp32_peak_tflops": FP32_PEAK_TFLOPS,

@@ -168,8 +168,9 @@ __global__ __launch_bounds__(kT) void dgrad_tiled(LayerDev d, BwdArgs a, float* 
     __shared__ __attribute__((aligned(16))) f2 tile[OC * C::PLANE];
     const nconv_layer& L = d.L;
     const float* __restrict__ wgt = L.weight;
-    const int tid = threadIdx.x, b = blockIdx.z;
-    const int ih0 = blockIdx.y * C::TH, iw0 = blockIdx.x * C::TW;
+    const TileCoord tcd = xcd_tile((L.W + C::TW - 1) / C::TW, (L.H + C::TH - 1) / C::TH, L.B);
+    const int tid = threadIdx.x, b = tcd.b;
+    const int ih0 = tcd.ty * C::TH, iw0 = tcd.tx * C::TW;
     const int oh0 = ih0 + L.PH - (K - 1), ow0 = iw0 + L.PW - (K - 1);
     const int ty = tid / C::TPR, tx = (tid % C::TPR) * P;
 
@@ -427,7 +428,10 @@ __global__ __launch_bounds__(kT) void wgrad_tiled(LayerDev d, BwdArgs a, float* 
 #pragma unroll
     for (int oo = 0; oo < COUT; ++oo) gb_acc[oo] = gs_acc[oo] = 0.f;
 
-    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    // a contiguous run of row-major tiles per block: neighbouring tiles' halos hit the same L2
+    const int per_blk = (ntiles + gridDim.x - 1) / gridDim.x;
+    const int t_end = min(ntiles, ((int)blockIdx.x + 1) * per_blk);
+    for (int t = blockIdx.x * per_blk; t < t_end; ++t) {
         const int tw = t % ntile_w, th = (t / ntile_w) % ntile_h, b = t / (ntile_w * ntile_h);
         const int oh0 = th * C::TH, ow0 = tw * C::TW;
         const int ih0 = oh0 - L.PH, iw0 = ow0 - L.PW;
@@ -678,7 +682,7 @@ static void go_bwd_tiled(const LayerDev& d, const BwdArgs& a, float* part, float
     const nconv_layer& L = d.L;
     using D = DgCfg<CIN, K>;
     if (a.gxa || a.gca || a.gxb || a.gcb) {
-        dim3 g((L.W + D::TW - 1) / D::TW, (L.H + D::TH - 1) / D::TH, L.B);
+        dim3 g(((L.W + D::TW - 1) / D::TW) * ((L.H + D::TH - 1) / D::TH) * L.B);  // see xcd_tile
         hipLaunchKernelGGL((dgrad_tiled<CIN, COUT, K, MODE>), g, dim3(kT), 0, st, d, a, tx, tc);
     }
     if (a.gw || a.gb) {

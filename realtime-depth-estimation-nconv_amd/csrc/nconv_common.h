@@ -94,6 +94,25 @@ __device__ __forceinline__ void load_xc(const LayerDev& d, int b, int ci, int ih
     }
 }
 
+// XCD-aware tile order (MI355X: 8 XCDs, each with its own L2; workgroups are dealt round-robin,
+// so blocks b and b+8 share an XCD). Launch a 1-D grid of ntx*nty*nb blocks; this bijection gives
+// each XCD group a contiguous run of row-major tiles, so the halo rows and columns neighbouring
+// tiles share are fetched into one L2 instead of two or three (speed only, never correctness).
+struct TileCoord {
+    int tx, ty, b;
+};
+__device__ __forceinline__ TileCoord xcd_tile(int ntx, int nty, int nb) {
+    const int total = ntx * nty * nb;
+    const int bid = blockIdx.x;
+    const int q = total / 8, r = total % 8, xcd = bid % 8, loc = bid / 8;
+    const int t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+    TileCoord c;
+    c.tx = t % ntx;
+    c.ty = (t / ntx) % nty;
+    c.b = t / (ntx * nty);
+    return c;
+}
+
 // IEEE-exact epilogue of NConv2d.forward (step1.py:123-147):
 //   y = N / (D + eps) + b,   cout = D / s.
 __device__ __forceinline__ void nconv_epilogue(float N, float D, float eps, float bias, float s,

@@ -43,8 +43,10 @@ __global__ __launch_bounds__(kThreads) void fwd_tiled(LayerDev d, float* __restr
     const nconv_layer& L = d.L;
     const float* __restrict__ wgt = L.weight;
     const int tid = threadIdx.x;
-    const int b = blockIdx.z;
-    const int R0 = blockIdx.y * C::TH, C0 = blockIdx.x * C::TW;  // tile origin in the written grid
+    const int gh = TAIL ? t.out_h : L.Ho, gw = TAIL ? t.out_w : L.Wo;  // the written grid
+    const TileCoord tc = xcd_tile((gw + C::TW - 1) / C::TW, (gh + C::TH - 1) / C::TH, L.B);
+    const int b = tc.b;
+    const int R0 = tc.ty * C::TH, C0 = tc.tx * C::TW;  // tile origin in the written grid
     const int off = TAIL ? t.off : 0;
     const int oh0 = R0 + off, ow0 = C0 + off;  // tile origin in this layer's output grid
     const int ih0 = oh0 - L.PH, iw0 = ow0 - L.PW;
@@ -248,7 +250,7 @@ template <int CIN, int COUT, int K, int MODE, bool TAIL>
 static void go_tiled(const LayerDev& d, float* y, float* yc, const TailArgs& t, int gh, int gw,
                      hipStream_t st) {
     using C = FwdCfg<CIN, K>;
-    dim3 grid((gw + C::TW - 1) / C::TW, (gh + C::TH - 1) / C::TH, d.L.B);
+    dim3 grid(((gw + C::TW - 1) / C::TW) * ((gh + C::TH - 1) / C::TH) * d.L.B);  // see xcd_tile
     hipLaunchKernelGGL((fwd_tiled<CIN, COUT, K, MODE, TAIL>), grid, dim3(kThreads), 0, st, d, y, yc, t);
 }
 
