@@ -384,6 +384,37 @@ constexpr int pow2ceil(int n) {
     return p;
 }
 
+// One kernel row of the weight-gradient correlation over SEGW output columns:
+// acc[kw] += in[c + kw] * g[c]  ({x*c, c} * {gN, gD} elementwise). Circular window: input column
+// c lives in slot c % K; stepping K columns at a time keeps every slot index a compile-time
+// constant, so the window never moves between registers.
+template <int K, int SEGW>
+__device__ __forceinline__ void wgrad_row(const f2* ir, const f2* gr, f2 (&acc)[K]) {
+    f2 win[K];
+#pragma unroll
+    for (int kw = 0; kw < K - 1; ++kw) win[kw] = ir[kw];
+    constexpr int NSTEP = SEGW / K, REM = SEGW % K;
+#pragma unroll 2
+    for (int st = 0; st < NSTEP; ++st) {
+        const int cc = st * K;
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            const f2 g = gr[cc + j];
+            win[(j + K - 1) % K] = ir[cc + j + K - 1];
+#pragma unroll
+            for (int kw = 0; kw < K; ++kw) acc[kw] = __builtin_elementwise_fma(win[(j + kw) % K], g, acc[kw]);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < REM; ++j) {
+        const int cc = NSTEP * K;
+        const f2 g = gr[cc + j];
+        win[(j + K - 1) % K] = ir[cc + j + K - 1];
+#pragma unroll
+        for (int kw = 0; kw < K; ++kw) acc[kw] = __builtin_elementwise_fma(win[(j + kw) % K], g, acc[kw]);
+    }
+}
+
 template <int CIN, int COUT, int K>
 struct WgCfg {
     static constexpr int TH = 4, TW = 64;  // TH*TW == kT: one output pixel per thread while staging
@@ -392,13 +423,17 @@ struct WgCfg {
     // different bank pairs (bank = dword % 64).
     static constexpr int IPL = ((IHTP * IWT + 31) / 32) * 32 + 1;
     static constexpr int GPL = TH * TW + 1;
-    static constexpr int NCB = COUT * CIN;  // (o, i) pairs
+    static constexpr int CW = CIN < 8 ? CIN : 8;  // input channels staged per chunk
+    static_assert(CIN % CW == 0, "input channel chunking");
+    static constexpr int NCH = CIN / CW;
+    static constexpr int NCB = COUT * CW;  // (o, i) pairs of one chunk
     static constexpr int NCBP = pow2ceil(NCB);
-    static_assert(NCBP <= kT, "wgrad_tiled: Cin*Cout must be <= 256");
+    static_assert(NCBP <= kT, "wgrad_tiled: Cout*min(Cin,8) must be <= 256");
+    static_assert(K <= 7, "wgrad_tiled: kernel rows dispatched through a switch of 7 cases");
     static constexpr int NSUB = kT / NCBP;
     static constexpr int NSEG = NSUB > TH ? NSUB / TH : 1;  // column segments per row
     static constexpr int SEGW = TW / NSEG;
-    static constexpr int LDS_F2 = CIN * IPL + COUT * GPL;
+    static constexpr int LDS_F2 = CW * IPL + COUT * GPL;
 };
 
 template <int CIN, int COUT, int K, int MODE>
@@ -407,23 +442,25 @@ __global__ __launch_bounds__(kT) void wgrad_tiled(LayerDev d, BwdArgs a, float* 
     using C = WgCfg<CIN, COUT, K>;
     extern __shared__ __attribute__((aligned(16))) f2 smem[];
     f2* sin = smem;
-    f2* sg = smem + CIN * C::IPL;
+    f2* sg = smem + C::CW * C::IPL;
     const nconv_layer& L = d.L;
     const int tid = threadIdx.x;
     const int ntiles = ntile_w * ntile_h * L.B;
     const int cb = tid % C::NCBP, sub = tid / C::NCBP;
     const bool active = cb < C::NCB;
-    const int i = active ? cb % CIN : 0, o = active ? cb / CIN : 0;
+    const int il = active ? cb % C::CW : 0, o = active ? cb / C::CW : 0;
     // rows / column segment of this thread's sub
     const int r_first = (C::NSUB > C::TH) ? sub % C::TH : sub;
     const int r_step = (C::NSUB > C::TH) ? C::TH : C::NSUB;
     const int c_first = (C::NSUB > C::TH) ? (sub / C::TH) * C::SEGW : 0;
 
-    f2 acc[K][K];
+    f2 acc[C::NCH][K][K];
 #pragma unroll
-    for (int kh = 0; kh < K; ++kh)
+    for (int ch = 0; ch < C::NCH; ++ch)
 #pragma unroll
-        for (int kw = 0; kw < K; ++kw) acc[kh][kw] = (f2){0.f, 0.f};
+        for (int kh = 0; kh < K; ++kh)
+#pragma unroll
+            for (int kw = 0; kw < K; ++kw) acc[ch][kh][kw] = (f2){0.f, 0.f};
     float gb_acc[COUT], gs_acc[COUT];
 #pragma unroll
     for (int oo = 0; oo < COUT; ++oo) gb_acc[oo] = gs_acc[oo] = 0.f;
@@ -453,31 +490,36 @@ __global__ __launch_bounds__(kT) void wgrad_tiled(LayerDev d, BwdArgs a, float* 
                 sg[oo * C::GPL + tid] = in ? (f2){gN, gD} : (f2){0.f, 0.f};
             }
         }
-        for (int ci = 0; ci < CIN; ++ci)
-            stage_plane<C::IHT, C::IWT, C::IWT>(d, chan_src<MODE>(d, b, ci), sin + ci * C::IPL, ih0, iw0, tid);
-        __syncthreads();
-        if (active) {
-            for (int r = r_first; r < C::TH; r += r_step) {
-                const f2* gr = sg + o * C::GPL + r * C::TW;
-                const f2* ir = sin + i * C::IPL + r * C::IWT;
-                f2 win[K][K];
 #pragma unroll
-                for (int kh = 0; kh < K; ++kh)
-#pragma unroll
-                    for (int kw = 0; kw < K - 1; ++kw) win[kh][kw] = ir[kh * C::IWT + c_first + kw];
-                // fully unrolled: the window shifts below become register renames
-#pragma unroll
-                for (int cc = 0; cc < C::SEGW; ++cc) {
-                    const int col = c_first + cc;
-                    const f2 g = gr[col];
-#pragma unroll
+        for (int ch = 0; ch < C::NCH; ++ch) {
+            if (ch) __syncthreads();
+            for (int ci = 0; ci < C::CW; ++ci)
+                stage_plane<C::IHT, C::IWT, C::IWT>(d, chan_src<MODE>(d, b, ch * C::CW + ci), sin + ci * C::IPL, ih0,
+                                                    iw0, tid);
+            __syncthreads();
+            if (active) {
+                for (int r = r_first; r < C::TH; r += r_step) {
+                    const f2* gr = sg + o * C::GPL + r * C::TW + c_first;
+                    // kernel rows one at a time (a runtime loop over a compile-time switch keeps
+                    // acc statically indexed without letting the scheduler hoist every row's
+                    // LDS reads into registers at once)
+#pragma unroll 1
                     for (int kh = 0; kh < K; ++kh) {
-                        win[kh][K - 1] = ir[kh * C::IWT + col + K - 1];
-#pragma unroll
-                        for (int kw = 0; kw < K; ++kw)
-                            acc[kh][kw] = __builtin_elementwise_fma(win[kh][kw], g, acc[kh][kw]);
-#pragma unroll
-                        for (int kw = 0; kw < K - 1; ++kw) win[kh][kw] = win[kh][kw + 1];
+                        const f2* ir = sin + il * C::IPL + (r + kh) * C::IWT + c_first;
+                        switch (kh) {
+#define NCONV_WG_ROW(KH) \
+    case KH:             \
+        if constexpr (KH < K) wgrad_row<K, C::SEGW>(ir, gr, acc[ch][KH]); \
+        break;
+                            NCONV_WG_ROW(0)
+                            NCONV_WG_ROW(1)
+                            NCONV_WG_ROW(2)
+                            NCONV_WG_ROW(3)
+                            NCONV_WG_ROW(4)
+                            NCONV_WG_ROW(5)
+                            NCONV_WG_ROW(6)
+#undef NCONV_WG_ROW
+                        }
                     }
                 }
             }
@@ -492,12 +534,17 @@ __global__ __launch_bounds__(kT) void wgrad_tiled(LayerDev d, BwdArgs a, float* 
     __syncthreads();
     if (active) {
 #pragma unroll
-        for (int kh = 0; kh < K; ++kh)
+        for (int ch = 0; ch < C::NCH; ++ch) {
+            const int i = ch * C::CW + il;
 #pragma unroll
-            for (int kw = 0; kw < K; ++kw) red[(sub * C::NCB + cb) * K * K + kh * K + kw] = acc[kh][kw].x + acc[kh][kw].y;
+            for (int kh = 0; kh < K; ++kh)
+#pragma unroll
+                for (int kw = 0; kw < K; ++kw)
+                    red[sub * NW + ((o * CIN + i) * K + kh) * K + kw] = acc[ch][kh][kw].x + acc[ch][kh][kw].y;
+        }
     }
     __syncthreads();
-    for (int w = tid; w < NW; w += kT) {  // w = ((o*CIN + i)*K + kh)*K + kw = cb*K*K + tap
+    for (int w = tid; w < NW; w += kT) {
         float sum = 0.f;
         for (int sb = 0; sb < C::NSUB; ++sb) sum += red[sb * NW + w];
         out[w] = sum;
