@@ -10,6 +10,7 @@ The directory name is not a Python identifier; import it through the repo-root h
 from . import _lib, dp, train
 from .nconv import EnforcePos, LayerSpec, NConv2d, NConvLayerFn, nconv_layer, weight_prep
 from .dnet import DNET, SETP1_NCONV, crop_hw
+from .guided import SETP2_BP_EXPORT, SETP2_BP_TRAIN, RGBEncoder
 
 __all__ = ["EnforcePos", "LayerSpec", "NConv2d", "NConvLayerFn", "nconv_layer", "weight_prep", "DNET",
-           "SETP1_NCONV", "crop_hw"]
+           "SETP1_NCONV", "crop_hw", "SETP2_BP_EXPORT", "SETP2_BP_TRAIN", "RGBEncoder"]

@@ -1,0 +1,222 @@
+"""RGB-guided depth refinement — drop-in for the reference's models/step2.py:22-297.
+
+SETP2_BP_TRAIN / SETP2_BP_EXPORT keep the reference's constructors, forward(rgb0, depth0, rgb1,
+depth1), submodule names (hence state_dict keys, including the unused rgb_encoder4 of the TRAIN
+variant, step2.py:46) and RNG consumption order. Step 1 is this package's SETP1_NCONV (libnconv
+kernels); it is called as step1(depth0, depth1), which the reference intends (step2.py:62-63) but
+its one-argument SETP1_NCONV.forward rejects. The dense convolutions of the RGB
+encoder and the fusion decoder are PyTorch-ROCm convolutions (MIOpen).
+"""
+from collections import OrderedDict
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .dnet import SETP1_NCONV
+
+
+def Conv1x1(in_planes, out_planes, stride, bias=False, groups=1, dilation=1, padding_mode="zeros"):
+    """1x1 projection shortcut (step2.py:130-132)."""
+    return nn.Conv2d(in_planes, out_planes, kernel_size=1, stride=stride, bias=bias)
+
+
+def Conv3x3(in_planes, stride=1, groups=1, dilation=1, padding_mode="zeros", bias=False):
+    """3x3 residual head producing one depth channel (step2.py:156-158)."""
+    return nn.Conv2d(in_planes, 1, kernel_size=3, stride=stride, padding=dilation, padding_mode=padding_mode,
+                     groups=groups, bias=bias, dilation=dilation)
+
+
+class RGBEncoder(nn.Module):
+    """ReLU(BN(conv3x3_s(x))) + conv1x1_s(x) (step2.py:134-154)."""
+
+    def __init__(self, in_channel, out_channel, stride):
+        super().__init__()
+        self.stride = stride
+        self.encoder = nn.Sequential(
+            nn.Conv2d(in_channels=in_channel, out_channels=out_channel, kernel_size=3, stride=stride, padding=1),
+            nn.BatchNorm2d(out_channel),
+            nn.ReLU(inplace=True))
+        self.downsample = nn.Sequential(Conv1x1(in_channel, out_channel, stride))
+
+    def forward(self, x):
+        return self.encoder(x) + self.downsample(x)
+
+
+class Basic2d(nn.Module):
+    """conv (+BN when norm_layer, then no conv bias) + activation (step2.py:178-195)."""
+
+    def __init__(self, in_channels, out_channels, norm_layer=None, kernel_size=3, padding=1, padding_mode="zeros",
+                 act=nn.ReLU, stride=1):
+        super().__init__()
+        conv = nn.Conv2d(in_channels=in_channels, out_channels=out_channels, kernel_size=kernel_size,
+                         stride=stride, padding=padding, bias=not norm_layer, padding_mode=padding_mode)
+        self.conv = nn.Sequential(OrderedDict([("conv", conv)]))
+        if norm_layer:
+            self.conv.add_module("bn", norm_layer(out_channels))
+        self.conv.add_module("relu", act())
+
+    def forward(self, x):
+        return self.conv(x)
+
+
+class Basic2dTrans(nn.Module):
+    """ConvTranspose 4x4 / stride 2 / padding 1 + BN + activation (step2.py:197-214)."""
+
+    def __init__(self, in_channels, out_channels, norm_layer=None, act=nn.ReLU):
+        super().__init__()
+        bias = norm_layer is None
+        self.conv = nn.ConvTranspose2d(in_channels=in_channels, out_channels=out_channels, kernel_size=4, stride=2,
+                                       padding=1, bias=bias)
+        self.bn = (norm_layer or nn.Identity)(out_channels)
+        self.relu = act()
+
+    def forward(self, x):
+        return self.relu(self.bn(self.conv(x.contiguous())))
+
+
+class UpCat(nn.Module):
+    """Upsample cat(x, d) by the transposed conv, then fuse with the skip y (step2.py:160-176)."""
+
+    def __init__(self, in_channels, out_channels, norm_layer=nn.BatchNorm2d, kernel_size=3, padding=1,
+                 padding_mode="zeros", act=nn.ReLU):
+        super().__init__()
+        self.upf = Basic2dTrans(in_channels + 1, out_channels, norm_layer=norm_layer, act=act)
+        self.conv = Basic2d(out_channels * 2, out_channels, norm_layer=norm_layer, kernel_size=kernel_size,
+                            padding=padding, padding_mode=padding_mode, act=act)
+
+    def forward(self, y, x, d):
+        up = self.upf(torch.cat([x, d], dim=1))
+        return self.conv(torch.cat([up, y], dim=1))
+
+
+class ConvBlock(nn.Module):
+    """3x3 conv (bias) + ReLU (step2.py:290-297)."""
+
+    def __init__(self, in_channels, out_channels, kernel_size=3, stride=1, padding=1):
+        super().__init__()
+        self.conv = nn.Conv2d(in_channels, out_channels, kernel_size, stride, padding)
+        self.relu = nn.ReLU()
+
+    def forward(self, x):
+        return self.relu(self.conv(x))
+
+
+class NewFusionBlock(nn.Module):
+    """rgb / depth branches, concat, three fusing convs (step2.py:216-236)."""
+
+    def __init__(self, rgb_channels, out_channels):
+        super().__init__()
+        self.rgb_conv = ConvBlock(rgb_channels, rgb_channels)
+        self.depth_conv = ConvBlock(1, rgb_channels)
+        self.fuse_conv1 = ConvBlock(rgb_channels * 2, rgb_channels)
+        self.fuse_conv2 = ConvBlock(rgb_channels, out_channels)
+        self.fuse_conv3 = ConvBlock(out_channels, out_channels)
+
+    def forward(self, rgb, depth):
+        fused = torch.cat((self.rgb_conv(rgb), self.depth_conv(depth)), 1)
+        return self.fuse_conv3(self.fuse_conv2(self.fuse_conv1(fused)))
+
+
+class FusionResolutionBlock(nn.Module):
+    """One decoder scale: UpCat, bilinear depth downsample (align_corners=True), fusion, residual
+    depth head (step2.py:238-259)."""
+
+    def __init__(self, in_channel, out_channel, downsample_factor):
+        super().__init__()
+        self.upcat = UpCat(in_channel, in_channel)
+        self.fuse = NewFusionBlock(in_channel, out_channel)
+        self.conv = Conv3x3(out_channel, 1)
+        self.downsample_factor = downsample_factor
+
+    def forward(self, rgb, depth, depth_last_step, fusion_festure):
+        fout = self.upcat(rgb, fusion_festure, depth_last_step)
+        depth = F.interpolate(depth, scale_factor=1 / self.downsample_factor, mode="bilinear", align_corners=True)
+        fout = self.fuse(fout, depth)
+        return fout, depth + self.conv(fout)
+
+
+class FusionResolution0(nn.Module):
+    """Coarsest decoder scale (step2.py:262-278)."""
+
+    def __init__(self, in_channel, downsample_factor):
+        super().__init__()
+        self.fuse = NewFusionBlock(in_channel, in_channel)
+        self.conv = Conv3x3(in_channel, 1)
+        self.downsample_factor = downsample_factor
+
+    def forward(self, rgb, depth):
+        depth = F.interpolate(depth, scale_factor=1 / self.downsample_factor, mode="bilinear", align_corners=True)
+        fout = self.fuse(rgb, depth)
+        return fout, depth + self.conv(fout)
+
+
+def _encoders_and_decoder(m, first_set):
+    """Submodule construction in the reference's order (RNG consumption parity)."""
+    if first_set:  # SETP2_BP_TRAIN builds a first encoder set and overwrites 0-3 (step2.py:42-51)
+        m.rgb_encoder0 = RGBEncoder(3, 32, 1)
+        m.rgb_encoder1 = RGBEncoder(32, 32, 2)
+        m.rgb_encoder2 = RGBEncoder(32, 64, 2)
+        m.rgb_encoder3 = RGBEncoder(64, 64, 2)
+        m.rgb_encoder4 = RGBEncoder(64, 64, 2)  # never used in forward; kept for state_dict keys
+    m.rgb_encoder0 = RGBEncoder(3, 32, 1)
+    m.rgb_encoder1 = RGBEncoder(32, 64, 2)
+    m.rgb_encoder2 = RGBEncoder(64, 64, 2)
+    m.rgb_encoder3 = RGBEncoder(64, 64, 2)
+    m.fuse0 = FusionResolution0(64, 8)
+    m.fuse1 = FusionResolutionBlock(64, 64, 4)
+    m.fuse2 = FusionResolutionBlock(64, 32, 2)
+    m.fuse3 = FusionResolutionBlock(32, 32, 1)
+
+
+def _guided_forward(m, rgb0, depth0, rgb1, depth1):
+    sparse = m.step1(depth0, depth1)
+    rgb = torch.cat((rgb0, rgb1), dim=0)
+    e0 = m.rgb_encoder0(rgb)
+    e1 = m.rgb_encoder1(e0)
+    e2 = m.rgb_encoder2(e1)
+    e3 = m.rgb_encoder3(e2)
+    # the reference passes (features, depth) into the (depth_last_step, fusion_festure) slots
+    # (step2.py:72-74 vs :248), so UpCat concatenates [depth, features]; kept as is
+    f0, d0 = m.fuse0(e3, sparse)
+    f1, d1 = m.fuse1(e2, sparse, f0, d0)
+    f2, d2 = m.fuse2(e1, sparse, f1, d1)
+    f3, d3 = m.fuse3(e0, sparse, f2, d2)
+    return d0, d1, d2, d3
+
+
+class SETP2_BP_TRAIN(nn.Module):
+    """Guided training model (step2.py:22-77). Loads ./checkpoints/<name>.pth.tar into step 1
+    (weights-only load, `module.` prefix stripped, strict=False) and freezes it. forward returns the
+    four scales of frame pair 0 and of frame pair 1 (batch slices [0:1] and [1:2])."""
+
+    def __init__(self, step1_checkpoint_name, step1_crop="literal", checkpoint_dir="./checkpoints"):
+        super().__init__()
+        self.step1 = SETP1_NCONV(crop=step1_crop)
+        if step1_checkpoint_name is not None:
+            from .train import load_checkpoint
+            load_checkpoint(self.step1, f"{checkpoint_dir}/{step1_checkpoint_name}.pth.tar", strict=False)
+        for p in self.step1.parameters():
+            p.requires_grad = False
+        _encoders_and_decoder(self, first_set=True)
+
+    def forward(self, rgb0, depth0, rgb1, depth1):
+        d = _guided_forward(self, rgb0, depth0, rgb1, depth1)
+        return [x[0:1] for x in d], [x[1:2] for x in d]
+
+
+class SETP2_BP_EXPORT(nn.Module):
+    """Guided export model (step2.py:80-126): finest scale only, with 45 rows top and bottom and
+    20 columns on the left zeroed; returns (frame 0, frame 1)."""
+
+    def __init__(self, step1_crop="literal"):
+        super().__init__()
+        self.step1 = SETP1_NCONV(crop=step1_crop)
+        _encoders_and_decoder(self, first_set=False)
+
+    def forward(self, rgb0, depth0, rgb1, depth1):
+        d3 = _guided_forward(self, rgb0, depth0, rgb1, depth1)[3]
+        d3[:, :, :45, :] = 0
+        d3[:, :, -45:, :] = 0
+        d3[:, :, :, :20] = 0
+        return d3[0:1], d3[1:2]
