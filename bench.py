@@ -55,8 +55,10 @@ def sparse_depth(g, B, H, W, device):
 
 # ---- algorithmic per-layer cost --------------------------------------------------
 def layer_costs(B, H, W):
-    """Per fused layer: (bytes, flops) per launch. Bytes: each layer reads its producers' x and c
-    once at their native resolution (glue fused) and writes y and c once; nconv1 reads S only.
+    """Per fused layer: (bytes, flops) per launch, SURVEY.md 8(d)'s algorithmic count. Bytes: each
+    layer reads its producers' x and c once at their native resolution (glue fused) and writes y
+    and c once; nconv1 reads S only. (The inference path's pooled copies change the down layers'
+    actual reads; the algorithmic count is kept as the common yardstick.)
     Flops: 2 convs x 2 flop/FMA x Cin x k^2 x Cout per output pixel, + 4*Cout (div, bias, conf)."""
     f = 4
     H2, W2, H4, W4, H8, W8 = H // 2, W // 2, H // 4, W // 4, H // 8, W // 8
@@ -86,49 +88,48 @@ def fused_tail_cost(B, H, W):
 
 
 def time_layers(m, net, S, reps=20):
-    """Average device time per launch of each forward kernel (HIP events on the launch stream)."""
+    """Average device time per launch of each kernel of the inference forward (HIP events on the
+    launch stream): nconv1, nconv2 (+pooled copy), down1..3 (reading the pooled copies), nconv4/5,
+    and the fused nconv6+7 tail."""
     lib = m._lib
     d = net.d_net
     layers = [getattr(d, n) for n in LAYERS]
     wsum = d._prologue(layers, S)
-    specs = [layers[0].spec(lib.THRESH, 0.01), layers[1].spec(), layers[2].spec(lib.POOL2),
-             layers[3].spec(lib.POOL2), layers[4].spec(lib.POOL2), layers[5].spec(lib.UPCAT_SKIP_FIRST),
-             layers[6].spec(lib.UPCAT_SKIP_FIRST), layers[7].spec(lib.UPCAT_UP_FIRST), layers[8].spec()]
-    fwd = m.nconv.layer_forward_raw
-    with torch.no_grad():
-        x1, c1 = fwd(specs[0], S, None, None, None, layers[0].weight, layers[0].bias, wsum[0])
-        x1b, c1b = fwd(specs[1], x1, c1, None, None, layers[1].weight, layers[1].bias, wsum[1])
-        x2, c2 = fwd(specs[2], x1b, c1b, None, None, layers[2].weight, layers[2].bias, wsum[2])
-        x3, c3 = fwd(specs[3], x2, c2, None, None, layers[3].weight, layers[3].bias, wsum[3])
-        x4, c4 = fwd(specs[4], x3, c3, None, None, layers[4].weight, layers[4].bias, wsum[4])
-        x34, c34 = fwd(specs[5], x3, c3, x4, c4, layers[5].weight, layers[5].bias, wsum[5])
-        x23, c23 = fwd(specs[6], x2, c2, x34, c34, layers[6].weight, layers[6].bias, wsum[6])
-        x6, c6 = fwd(specs[7], x1b, c1b, x23, c23, layers[7].weight, layers[7].bias, wsum[7])
-    args = [(S, None, None, None), (x1, c1, None, None), (x1b, c1b, None, None), (x2, c2, None, None),
-            (x3, c3, None, None), (x3, c3, x4, c4), (x2, c2, x34, c34), (x1b, c1b, x23, c23), (x6, c6, None, None)]
-    out = {}
+    l1, l2, d1, d2, d3, l4, l5, l6, l7 = layers
+    s1, s2, sd1, sd2, sd3, s4, s5, s6, s7 = wsum
+    fwd, fpool = m.nconv.layer_forward_raw, m.nconv.layer_forward_pooled
     H, W = S.shape[2], S.shape[3]
     oh, ow = m.crop_hw(H, W, d.crop)
+    with torch.no_grad():
+        x1, c1 = fwd(l1.spec(lib.THRESH, 0.01), S, None, None, None, l1.weight, l1.bias, s1)
+        x1b, c1b, p1, q1 = fpool(l2.spec(), x1, c1, None, None, l2.weight, l2.bias, s2)
+        x2, c2, p2, q2 = fpool(d1.spec(), p1, q1, None, None, d1.weight, d1.bias, sd1)
+        x3, c3, p3, q3 = fpool(d2.spec(), p2, q2, None, None, d2.weight, d2.bias, sd2)
+        x4, c4 = fwd(d3.spec(), p3, q3, None, None, d3.weight, d3.bias, sd3)
+        x34, c34 = fwd(l4.spec(lib.UPCAT_SKIP_FIRST), x3, c3, x4, c4, l4.weight, l4.bias, s4)
+        x23, c23 = fwd(l5.spec(lib.UPCAT_SKIP_FIRST), x2, c2, x34, c34, l5.weight, l5.bias, s5)
+    calls = {
+        "nconv1": lambda: fwd(l1.spec(lib.THRESH, 0.01), S, None, None, None, l1.weight, l1.bias, s1),
+        "nconv2": lambda: fpool(l2.spec(), x1, c1, None, None, l2.weight, l2.bias, s2),
+        "nconv_down1": lambda: fpool(d1.spec(), p1, q1, None, None, d1.weight, d1.bias, sd1),
+        "nconv_down2": lambda: fpool(d2.spec(), p2, q2, None, None, d2.weight, d2.bias, sd2),
+        "nconv_down3": lambda: fwd(d3.spec(), p3, q3, None, None, d3.weight, d3.bias, sd3),
+        "nconv4": lambda: fwd(l4.spec(lib.UPCAT_SKIP_FIRST), x3, c3, x4, c4, l4.weight, l4.bias, s4),
+        "nconv5": lambda: fwd(l5.spec(lib.UPCAT_SKIP_FIRST), x2, c2, x34, c34, l5.weight, l5.bias, s5),
+        "nconv6+7_tail": lambda: d._fused_tail(l6, l7, s6, s7, x1b, c1b, x23, c23, oh, ow),
+    }
+    out = {}
     stream = torch.cuda.current_stream()
-    for name, spec, lay, a, s in zip(LAYERS, specs, layers, args, wsum):
-        with torch.no_grad():
-            fwd(spec, *a, lay.weight, lay.bias, s)
+    with torch.no_grad():
+        for name, fn in calls.items():
+            fn()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
             for _ in range(reps):
-                fwd(spec, *a, lay.weight, lay.bias, s)
+                fn()
             e1.record(stream)
-        e1.synchronize()
-        out[name] = e0.elapsed_time(e1) / reps * 1e3  # us
-    with torch.no_grad():
-        d._fused_tail(layers[7], layers[8], wsum[7], wsum[8], x1b, c1b, x23, c23, oh, ow)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        for _ in range(reps):
-            d._fused_tail(layers[7], layers[8], wsum[7], wsum[8], x1b, c1b, x23, c23, oh, ow)
-        e1.record(stream)
-    e1.synchronize()
-    out["nconv6+7_tail"] = e0.elapsed_time(e1) / reps * 1e3
+            e1.synchronize()
+            out[name] = e0.elapsed_time(e1) / reps * 1e3  # us
     return out
 
 
@@ -291,9 +292,7 @@ def main():
         lt = time_layers(m, net, S)
         costs = layer_costs(B, H, W)
         costs["nconv6+7_tail"] = fused_tail_cost(B, H, W)
-        # kernels of the timed inference pass: nconv1..5 + the fused nconv6+7 tail
-        infer = [n for n in LAYERS if n not in ("nconv6", "nconv7")] + ["nconv6+7_tail"]
-        dom = max(infer, key=lambda n: lt[n])
+        dom = max(lt, key=lambda n: lt[n])  # kernels of the timed inference pass
         byt, fl = costs[dom]
         us = lt[dom]
         traffic = pmc_traffic(dom, B, H, W)

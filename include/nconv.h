@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define NCONV_ABI_VERSION 2
+#define NCONV_ABI_VERSION 3
 
 /* How a layer's input (data x, confidence c) is produced from its source tensors. These are the
  * DNET glue ops fused into the layer's load stage (models/step1.py:53,61-90). */
@@ -78,6 +78,14 @@ int nconv_weight_prep(int n, float* const* weights, const int* couts, const int*
  * plus the glue op that feeds it (step1.py:53 / 62-75 / 78-90).
  * y, cout: (B, Cout, Ho, Wo). */
 int nconv_fwd(const nconv_layer* L, float* y, float* cout, void* stream);
+
+/* nconv_fwd plus, in the same launch, the 2x2/s2 max-pool of both outputs (torch semantics:
+ * first maximum wins, NaN propagates) into y_pool, cout_pool (B, Cout, Ho/2, Wo/2): the input of
+ * the next down layer (models/step1.py:62-75), which then loads it with NCONV_LOAD_PLAIN instead
+ * of re-reading and pooling the full-resolution tensors. Built for the tiled DNET layer shapes
+ * (returns -EOPNOTSUPP otherwise). */
+int nconv_fwd_pooled(const nconv_layer* L, float* y, float* cout, float* y_pool, float* cout_pool,
+                     void* stream);
 
 /* Inference-only fused tail: the last 3x3 NConv (nconv6, step1.py:88-90) with its 1x1 successor
  * (nconv7, step1.py:92) evaluated in the epilogue, written straight into the cropped output

@@ -12,7 +12,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libnconv.so")
-ABI_VERSION = 2
+ABI_VERSION = 3
 BWD_ACCUMULATE = 1
 
 # enum nconv_load_mode
@@ -23,6 +23,7 @@ EXPORTED = (
     "nconv_last_error",
     "nconv_weight_prep",
     "nconv_fwd",
+    "nconv_fwd_pooled",
     "nconv_fwd_tail",
     "nconv_bwd_workspace_bytes",
     "nconv_bwd",
@@ -58,6 +59,8 @@ def _declare(lib):
     lib.nconv_weight_prep.argtypes = [ctypes.c_int, P, P, P, P, P, P]
     lib.nconv_fwd.restype = ctypes.c_int
     lib.nconv_fwd.argtypes = [ctypes.POINTER(NconvLayer), P, P, P]
+    lib.nconv_fwd_pooled.restype = ctypes.c_int
+    lib.nconv_fwd_pooled.argtypes = [ctypes.POINTER(NconvLayer), P, P, P, P, P]
     lib.nconv_fwd_tail.restype = ctypes.c_int
     lib.nconv_fwd_tail.argtypes = [ctypes.POINTER(NconvLayer), P, P, P, ctypes.c_int, ctypes.c_int,
                                    ctypes.c_float, P, P, ctypes.c_int, ctypes.c_int, P]

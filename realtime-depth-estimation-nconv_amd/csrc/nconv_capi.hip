@@ -84,8 +84,18 @@ int nconv_fwd(const nconv_layer* L, float* y, float* cout, void* stream) {
     if (const char* why = validate(L, true)) return fail(-22, "nconv_fwd", why);
     if (!y || !cout) return fail(-22, "nconv_fwd", "null output");
     const char* why = nullptr;
-    int rc = nconv::launch_fwd(make_dev(L), y, cout, (hipStream_t)stream, &why);
+    int rc = nconv::launch_fwd(make_dev(L), y, cout, nullptr, nullptr, (hipStream_t)stream, &why);
     return rc ? fail(rc, "nconv_fwd", why) : 0;
+}
+
+int nconv_fwd_pooled(const nconv_layer* L, float* y, float* cout, float* y_pool, float* cout_pool,
+                     void* stream) {
+    if (const char* why = validate(L, true)) return fail(-22, "nconv_fwd_pooled", why);
+    if (!y || !cout || !y_pool || !cout_pool) return fail(-22, "nconv_fwd_pooled", "null output");
+    if (L->Ho < 2 || L->Wo < 2) return fail(-22, "nconv_fwd_pooled", "output too small to pool");
+    const char* why = nullptr;
+    int rc = nconv::launch_fwd(make_dev(L), y, cout, y_pool, cout_pool, (hipStream_t)stream, &why);
+    return rc ? fail(rc, "nconv_fwd_pooled", why) : 0;
 }
 
 int nconv_fwd_tail(const nconv_layer* L6, const float* w7, const float* b7, const float* wsum7,

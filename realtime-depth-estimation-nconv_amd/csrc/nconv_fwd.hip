@@ -98,14 +98,37 @@ __global__ __launch_bounds__(kThreads) void fwd_tiled(LayerDev d, float* __restr
     // ---- epilogue ----
     const int oh = oh0 + ty;
     if constexpr (!TAIL) {
-        if (oh >= L.Ho) return;
         const bool vec = (L.Wo & 3) == 0 && (ow0 + tx + 3) < L.Wo;
+        // optional fused 2x2 max-pool of the outputs (the next down layer's input, step1.py:62-75):
+        // rows oh and oh^1 sit in lanes l and l^16 of one wave (ty = tid >> 4, tile origin even)
+        const bool pool = t.py != nullptr;
+        const int Hp = L.Ho >> 1, Wp = L.Wo >> 1;
+        const int pr = oh >> 1, pc0 = (ow0 + tx) >> 1;
+        const bool pool_row = pool && ((ty & 1) == 0) && pr < Hp;
 #pragma unroll
         for (int o = 0; o < COUT; ++o) {
             const float s = L.wsum[o], bo = L.bias[o];
             float yv[C::P], cv[C::P];
 #pragma unroll
             for (int j = 0; j < C::P; ++j) nconv_epilogue(acc[o][j].x, acc[o][j].y, L.eps, bo, s, yv[j], cv[j]);
+            if (pool) {  // every lane joins the shuffles
+                float yb[C::P], cb[C::P];
+#pragma unroll
+                for (int j = 0; j < C::P; ++j) {
+                    yb[j] = __shfl_xor(yv[j], 16);
+                    cb[j] = __shfl_xor(cv[j], 16);
+                }
+                if (pool_row) {
+                    const size_t pbase = plane_idx(b, o, COUT, Hp, Wp, pr, pc0);
+#pragma unroll
+                    for (int h = 0; h < C::P / 2; ++h)
+                        if (pc0 + h < Wp) {
+                            t.py[pbase + h] = pool4v(yv[2 * h], yv[2 * h + 1], yb[2 * h], yb[2 * h + 1]);
+                            t.pc[pbase + h] = pool4v(cv[2 * h], cv[2 * h + 1], cb[2 * h], cb[2 * h + 1]);
+                        }
+                }
+            }
+            if (oh >= L.Ho) continue;
             const size_t base = plane_idx(b, o, COUT, L.Ho, L.Wo, oh, ow0 + tx);
             if (vec) {
                 *reinterpret_cast<f4*>(y + base) = (f4){yv[0], yv[1], yv[2], yv[3]};
@@ -254,9 +277,11 @@ static void go_tiled(const LayerDev& d, float* y, float* yc, const TailArgs& t, 
     hipLaunchKernelGGL((fwd_tiled<CIN, COUT, K, MODE, TAIL>), grid, dim3(kThreads), 0, st, d, y, yc, t);
 }
 
-int launch_fwd(const LayerDev& d, float* y, float* yc, hipStream_t st, const char** why) {
+int launch_fwd(const LayerDev& d, float* y, float* yc, float* py, float* pc, hipStream_t st, const char** why) {
     const nconv_layer& L = d.L;
-    const TailArgs t{};
+    TailArgs t{};
+    t.py = py;
+    t.pc = pc;
     if (simple_geometry(L)) {
 #define NCONV_TRY(CIN, COUT, K, MODE)                                                       \
     if (L.Cin == CIN && L.Cout == COUT && L.KH == K && L.load_mode == MODE) {               \
@@ -270,6 +295,10 @@ int launch_fwd(const LayerDev& d, float* y, float* yc, hipStream_t st, const cha
         NCONV_TRY(16, 8, 3, NCONV_LOAD_UPCAT_UP_FIRST)
         NCONV_TRY(8, 1, 1, NCONV_LOAD_PLAIN)
 #undef NCONV_TRY
+    }
+    if (py) {
+        *why = "fused output pooling is only built for the tiled DNET layer shapes";
+        return -95;  // EOPNOTSUPP
     }
     const size_t n = (size_t)L.B * L.Cout * L.Ho * L.Wo;
     size_t blocks = (n + kThreads - 1) / kThreads;

@@ -13,6 +13,8 @@ struct TailArgs {
     int off;
     int out_h, out_w;
     float* out_c;
+    float* py;  // optional 2x2 max-pooled copies of y / cout (non-tail launches), (B,Cout,Ho/2,Wo/2)
+    float* pc;
 };
 
 struct BwdArgs {
@@ -32,7 +34,7 @@ struct BwdArgs {
 };
 
 // Forward. Return 0, or a negative errno with *why set.
-int launch_fwd(const LayerDev& d, float* y, float* yc, hipStream_t st, const char** why);
+int launch_fwd(const LayerDev& d, float* y, float* yc, float* py, float* pc, hipStream_t st, const char** why);
 int launch_fwd_tail(const LayerDev& d, const TailArgs& t, float* out, hipStream_t st, const char** why);
 int launch_weight_prep(int n, float* const* w, const int* cout, const int* fan_in, const int* sp,
                        float* const* s, hipStream_t st, const char** why);

@@ -20,7 +20,8 @@ import torch
 import torch.nn as nn
 
 from . import _lib
-from .nconv import EnforcePos, NConv2d, layer_forward_raw, nconv_layer, weight_prep, _require_device
+from .nconv import (EnforcePos, NConv2d, _require_device, layer_forward_pooled, layer_forward_raw, nconv_layer,
+                    weight_prep)
 
 LAYERS = ("nconv1", "nconv2", "nconv_down1", "nconv_down2", "nconv_down3", "nconv4", "nconv5",
           "nconv6", "nconv7")
@@ -100,10 +101,17 @@ class DNET(nn.Module):
         f = nconv_layer if grad else (lambda spec, *a: layer_forward_raw(spec, *a))
 
         x1, c1 = f(l1.spec(_lib.THRESH, 0.01), S, None, None, None, l1.weight, l1.bias, s1)
-        x1, c1 = f(l2.spec(), x1, c1, None, None, l2.weight, l2.bias, s2)
-        x2, c2 = f(d1.spec(_lib.POOL2), x1, c1, None, None, d1.weight, d1.bias, sd1)
-        x3, c3 = f(d2.spec(_lib.POOL2), x2, c2, None, None, d2.weight, d2.bias, sd2)
-        x4, c4 = f(d3.spec(_lib.POOL2), x3, c3, None, None, d3.weight, d3.bias, sd3)
+        if grad or min(H, W) < 16:
+            x1, c1 = f(l2.spec(), x1, c1, None, None, l2.weight, l2.bias, s2)
+            x2, c2 = f(d1.spec(_lib.POOL2), x1, c1, None, None, d1.weight, d1.bias, sd1)
+            x3, c3 = f(d2.spec(_lib.POOL2), x2, c2, None, None, d2.weight, d2.bias, sd2)
+            x4, c4 = f(d3.spec(_lib.POOL2), x3, c3, None, None, d3.weight, d3.bias, sd3)
+        else:  # inference: each producer also writes the pooled input of the next down layer
+            fp = layer_forward_pooled
+            x1, c1, p1, q1 = fp(l2.spec(), x1, c1, None, None, l2.weight, l2.bias, s2)
+            x2, c2, p2, q2 = fp(d1.spec(), p1, q1, None, None, d1.weight, d1.bias, sd1)
+            x3, c3, p3, q3 = fp(d2.spec(), p2, q2, None, None, d2.weight, d2.bias, sd2)
+            x4, c4 = f(d3.spec(), p3, q3, None, None, d3.weight, d3.bias, sd3)
         if self.capture is not None:
             self.capture.update(down1=(x1.detach(), c1.detach()), down2=(x2.detach(), c2.detach()),
                                 down3=(x3.detach(), c3.detach()))

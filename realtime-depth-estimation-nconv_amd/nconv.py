@@ -100,6 +100,19 @@ def layer_forward_raw(spec: LayerSpec, xa, ca, xb, cb, weight, bias, wsum):
     return y, co
 
 
+def layer_forward_pooled(spec: LayerSpec, xa, ca, xb, cb, weight, bias, wsum):
+    """nconv_fwd_pooled: (y, cout, maxpool2x2(y), maxpool2x2(cout)) in one launch. No autograd."""
+    L = spec.descriptor(xa, ca, xb, cb, weight, bias, wsum)
+    y = torch.empty((L.B, L.Cout, L.Ho, L.Wo), device=xa.device, dtype=torch.float32)
+    co = torch.empty_like(y)
+    py = torch.empty((L.B, L.Cout, L.Ho // 2, L.Wo // 2), device=xa.device, dtype=torch.float32)
+    pc = torch.empty_like(py)
+    rc = _lib.lib().nconv_fwd_pooled(_lib.ctypes.byref(L), _lib.ptr(y), _lib.ptr(co), _lib.ptr(py), _lib.ptr(pc),
+                                     _lib.stream_handle(xa.device))
+    _lib.check(rc, "nconv_fwd_pooled")
+    return y, co, py, pc
+
+
 class NConvLayerFn(torch.autograd.Function):
     """Autograd node of one fused NConv layer (glue + NConv2d.forward), kernels in libnconv."""
 

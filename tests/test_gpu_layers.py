@@ -155,3 +155,23 @@ def test_nconv2d_module_train_step(nconv_amd, gpu):
     for got, ref in ((xg.grad, xr.grad), (cg.grad, cr.grad), (layer.weight.grad, wr.grad), (layer.bias.grad, br.grad)):
         rel = ((got.double().cpu() - ref).abs().max() / ref.abs().max()).item()
         assert rel <= 1e-3, rel
+
+
+@pytest.mark.parametrize("shape", [(2, 8, 48, 128), (2, 8, 37, 71), (1, 8, 20, 66)])
+def test_fwd_pooled_outputs(nconv_amd, gpu, shape):
+    """nconv_fwd_pooled: identical y/cout to nconv_fwd, and pooled copies bit-equal to torch's
+    max_pool2d of them (first maximum, floor mode; integer data makes ties frequent)."""
+    g = torch.Generator().manual_seed(sum(shape))
+    x = torch.randint(0, 3, shape, generator=g).float()
+    c = torch.randint(0, 3, shape, generator=g).float() * 0.5
+    spec = nconv_amd.LayerSpec(8, 8, (5, 5), (1, 1), (2, 2))
+    w = _gpu(rand_weight(g, 8, 8, 5, 5), gpu)
+    b = _gpu(torch.rand(8, generator=g) * 0.1, gpu)
+    ws = _wsum(nconv_amd, w)
+    xg, cg = x.to(gpu), c.to(gpu)
+    y0, c0 = nconv_amd.nconv.layer_forward_raw(spec, xg, cg, None, None, w, b, ws)
+    y1, c1, py, pc = nconv_amd.nconv.layer_forward_pooled(spec, xg, cg, None, None, w, b, ws)
+    torch.cuda.synchronize()
+    assert torch.equal(y0, y1) and torch.equal(c0, c1)
+    assert torch.equal(py, torch.nn.functional.max_pool2d(y1, 2, 2))
+    assert torch.equal(pc, torch.nn.functional.max_pool2d(c1, 2, 2))
