@@ -208,50 +208,75 @@ __device__ __forceinline__ void load_chan(const LayerDev& d, const ChanSrc& s, i
     }
 }
 
-// Stage one channel plane of {x*c, c} over an IHT x IWT halo tile (origin ih0, iw0) into t
-// (row pitch IWP; the plane must hold round_up(IHT, 4) rows: the last row group is written
-// unconditionally). 256 threads; IWT >= 64: lanes map to columns, waves to rows. Every load of a
-// thread is issued before the first is consumed (addresses clamped into the plane, out-of-range
-// elements zeroed afterwards), so a thread has all its row loads in flight at once instead of
-// one branch-guarded load per element.
+// One channel plane of {x*c, c} over an IHT x IWT halo tile (origin ih0, iw0), split into a load
+// phase (global -> registers) and a store phase (registers -> LDS, row pitch IWP). Between the two
+// a kernel can compute on the previous plane, so the loads' latency hides behind packed FMAs
+// (register-staged software pipeline). 256 threads, IWT >= 64: lanes map to columns, waves to
+// rows; every address is clamped into the source plane so all of a thread's loads are issued
+// before the first is consumed, and out-of-range elements are zeroed at store time. The plane
+// must hold round_up(IHT, 4) rows: the last row group is written unconditionally.
+template <int IHT, int IWT, int IWP>
+struct PlaneRegs {
+    static_assert(IWT >= 64, "lanes map to columns");
+    static constexpr int NR = (IHT + 3) / 4;  // rows per thread (waves stride 4 rows)
+    static constexpr int NCH = IWT / 64;      // full 64-column chunks
+    static constexpr int EX = IWT % 64;       // remaining halo columns, one pass over EX x IHT
+    static_assert(EX * IHT <= 256, "one pass for the remaining halo columns");
+    float x[NCH][NR], c[NCH][NR];
+    float ex, ec;
+
+    __device__ __forceinline__ void load(const LayerDev& d, const ChanSrc& s, int ih0, int iw0, int tid) {
+        const int H = d.L.H, W = d.L.W;
+        const int lane = tid & 63, r0 = tid >> 6;
+#pragma unroll
+        for (int ch = 0; ch < NCH; ++ch) {
+            const int iw = iw0 + ch * 64 + lane;
+            const int iwc = iw < 0 ? 0 : (iw >= W ? W - 1 : iw);
+#pragma unroll
+            for (int k = 0; k < NR; ++k) {
+                const int ih = ih0 + r0 + 4 * k;
+                const int ihc = ih < 0 ? 0 : (ih >= H ? H - 1 : ih);
+                load_chan(d, s, ihc, iwc, x[ch][k], c[ch][k]);
+            }
+        }
+        if constexpr (EX != 0) {
+            const int r = tid / EX, iw = iw0 + NCH * 64 + tid % EX;
+            int ih = ih0 + (r < IHT ? r : IHT - 1);
+            ih = ih < 0 ? 0 : (ih >= H ? H - 1 : ih);
+            const int iwc = iw < 0 ? 0 : (iw >= W ? W - 1 : iw);
+            load_chan(d, s, ih, iwc, ex, ec);
+        }
+    }
+
+    __device__ __forceinline__ void store(const LayerDev& d, f2* t, int ih0, int iw0, int tid) const {
+        const int H = d.L.H, W = d.L.W;
+        const int lane = tid & 63, r0 = tid >> 6;
+#pragma unroll
+        for (int ch = 0; ch < NCH; ++ch) {
+            const int col = ch * 64 + lane;
+            const bool wok = (unsigned)(iw0 + col) < (unsigned)W;
+#pragma unroll
+            for (int k = 0; k < NR; ++k) {  // rows >= IHT land in the plane's padding rows
+                const int r = r0 + 4 * k;
+                const bool ok = wok && (unsigned)(ih0 + r) < (unsigned)H;
+                const float xv = ok ? x[ch][k] : 0.f, cv = ok ? c[ch][k] : 0.f;
+                t[r * IWP + col] = (f2){xv * cv, cv};
+            }
+        }
+        if constexpr (EX != 0) {
+            const int r = tid / EX, cx = NCH * 64 + tid % EX;
+            const bool ok = (unsigned)(ih0 + r) < (unsigned)H && (unsigned)(iw0 + cx) < (unsigned)W;
+            const float xv = ok ? ex : 0.f, cv = ok ? ec : 0.f;
+            if (tid < EX * IHT) t[r * IWP + cx] = (f2){xv * cv, cv};
+        }
+    }
+};
+
+// Load and store back to back (no pipelining): one staged plane.
 template <int IHT, int IWT, int IWP>
 __device__ __forceinline__ void stage_plane(const LayerDev& d, const ChanSrc& s, f2* t, int ih0, int iw0,
                                             int tid) {
-    static_assert(IWT >= 64, "stage_plane maps 64 lanes to columns");
-    constexpr int NR = (IHT + 3) / 4;
-    const int H = d.L.H, W = d.L.W;
-    const int col = tid & 63, r0 = tid >> 6;
-    const int iw = iw0 + col;
-    const bool wok = (unsigned)iw < (unsigned)W;
-    const int iwc = iw < 0 ? 0 : (iw >= W ? W - 1 : iw);
-    float xs[NR], cs[NR];
-#pragma unroll
-    for (int k = 0; k < NR; ++k) {
-        const int ih = ih0 + r0 + 4 * k;
-        const int ihc = ih < 0 ? 0 : (ih >= H ? H - 1 : ih);
-        load_chan(d, s, ihc, iwc, xs[k], cs[k]);
-    }
-#pragma unroll
-    for (int k = 0; k < NR; ++k) {  // rows >= IHT land in the plane's padding rows (see IHTP)
-        const int r = r0 + 4 * k;
-        const int ih = ih0 + r;
-        const bool ok = wok && (unsigned)ih < (unsigned)H;
-        const float x = ok ? xs[k] : 0.f, c = ok ? cs[k] : 0.f;
-        t[r * IWP + col] = (f2){x * c, c};
-    }
-    if constexpr (IWT > 64) {
-        constexpr int EX = IWT - 64;
-        static_assert(EX * IHT <= 256, "one pass for the extra halo columns");
-        const int e = tid;
-        const int r = e / EX, cx = 64 + e % EX;
-        const int ih = ih0 + r, iw2 = iw0 + cx;
-        const bool ok = e < EX * IHT && (unsigned)ih < (unsigned)H && (unsigned)iw2 < (unsigned)W;
-        const int ihc = ih < 0 ? 0 : (ih >= H ? H - 1 : ih);
-        const int iwc2 = iw2 < 0 ? 0 : (iw2 >= W ? W - 1 : iw2);
-        float x, c;
-        load_chan(d, s, ihc, iwc2, x, c);
-        x = ok ? x : 0.f;
-        c = ok ? c : 0.f;
-        if (e < EX * IHT) t[r * IWP + cx] = (f2){x * c, c};
-    }
+    PlaneRegs<IHT, IWT, IWP> r;
+    r.load(d, s, ih0, iw0, tid);
+    r.store(d, t, ih0, iw0, tid);
 }

@@ -9,29 +9,24 @@
 //
 // Tiling: a 256-thread workgroup owns a 16 x 64 output tile of one image and all Cout channels;
 // each thread owns 4 horizontally adjacent pixels (a sliding window of 4+K-1 staged inputs per
-// kernel row feeds K*4*Cout packed FMAs). Input channels are staged in chunks of CC planes of
-// (16+K-1) x (64+K-1) {x*c, c} pairs, with the layer's glue (threshold / 2x2 max-pool / nearest
-// upsample + concat, step1.py:53-90) evaluated while staging, so glued tensors never hit HBM.
+// kernel row feeds K*4*Cout packed FMAs). Input channels are staged one plane of
+// (16+K-1) x (64+K-1) {x*c, c} pairs at a time into two LDS buffers (register-staged software
+// pipeline), with the layer's glue (threshold / 2x2 max-pool / nearest upsample + concat,
+// step1.py:53-90) evaluated while staging, so glued tensors never hit HBM.
 #include "nconv_internal.h"
 
 namespace nconv {
 
 constexpr int kThreads = 256;
 
-constexpr int pick_cc(int cin, int plane_f2) {
-    int best = 1;
-    for (int cc = 1; cc <= cin; ++cc)
-        if (cin % cc == 0 && cc * plane_f2 * 8 <= 24 * 1024) best = cc;
-    return best;
-}
-
 template <int CIN, int K>
 struct FwdCfg {
-    static constexpr int P = 4, TW = 64, TH = 16;
+    // 4 pixels per thread, 16 threads per tile row, 16 rows (P = 8 for the 3x3 layers measured
+    // slower: 187 VGPRs -> 2 waves/SIMD)
+    static constexpr int P = 4, TW = 16 * P, TH = 16;
     static constexpr int IHT = TH + K - 1, IWT = TW + K - 1;
     static constexpr int IWP = (IWT + 1) & ~1;  // even pitch keeps the f4 reads 16-B aligned
     static constexpr int PLANE = ((IHT + 3) / 4 * 4) * IWP;  // stage_plane writes whole 4-row groups
-    static constexpr int CC = pick_cc(CIN, PLANE);
     static constexpr int NV = P + K - 1;  // sliding-window width per kernel row
 };
 
@@ -39,7 +34,7 @@ template <int CIN, int COUT, int K, int MODE, bool TAIL>
 __global__ __launch_bounds__(kThreads) void fwd_tiled(LayerDev d, float* __restrict__ y,
                                                       float* __restrict__ yc, TailArgs t) {
     using C = FwdCfg<CIN, K>;
-    __shared__ __attribute__((aligned(16))) f2 tile[C::CC * C::PLANE];
+    __shared__ __attribute__((aligned(16))) f2 tile[2 * C::PLANE];
     const nconv_layer& L = d.L;
     const float* __restrict__ wgt = L.weight;
     const int tid = threadIdx.x;
@@ -58,22 +53,27 @@ __global__ __launch_bounds__(kThreads) void fwd_tiled(LayerDev d, float* __restr
 #pragma unroll
         for (int j = 0; j < C::P; ++j) acc[o][j] = (f2){0.f, 0.f};
 
-    for (int c0 = 0; c0 < CIN; c0 += C::CC) {
-        if (c0) __syncthreads();
-        // ---- stage CC planes of {x*c, c} over the haloed input tile (glue fused here) ----
-        for (int cc = 0; cc < C::CC; ++cc)
-            stage_plane<C::IHT, C::IWT, C::IWP>(d, chan_src<MODE>(d, b, c0 + cc), tile + cc * C::PLANE, ih0,
-                                                iw0, tid);
-        __syncthreads();
-        // ---- packed-FP32 accumulation: {N, D} += w * {x*c, c} ----
-        // One (channel, kernel-row) pair per iteration, deliberately not unrolled: its K*Cout
-        // weights are loaded into SGPRs (s_load) right before use. Unrolling lets the compiler
-        // hoist every weight of the chunk into SGPRs, which spills them through v_writelane.
-        const f2* row = &tile[ty * C::IWP + tx];
-        const float* wr = wgt + (size_t)c0 * K * K;  // weights of (c0+cc, kh) are K contiguous floats
+    // Software pipeline over input channels, one staged plane per step, two LDS buffers: the
+    // global loads of plane ci+1 are issued into registers before the FMAs on plane ci and land
+    // in the other buffer after them, so one barrier per channel separates writer and readers
+    // (a buffer is rewritten two steps after it was read, with a barrier in between).
+    PlaneRegs<C::IHT, C::IWT, C::IWP> pr;
+    pr.load(d, chan_src<MODE>(d, b, 0), ih0, iw0, tid);
+    const f2* rowbase = &tile[ty * C::IWP + tx];
 #pragma unroll 1
-        for (int q = 0; q < C::CC * K; ++q, row += C::IWP, wr += K) {
-            if (q && q % K == 0) row += C::PLANE - K * C::IWP;  // next staged channel plane
+    for (int ci = 0; ci < CIN; ++ci) {
+        f2* buf = tile + (ci & 1) * C::PLANE;
+        pr.store(d, buf, ih0, iw0, tid);
+        __syncthreads();
+        if (ci + 1 < CIN) pr.load(d, chan_src<MODE>(d, b, ci + 1), ih0, iw0, tid);
+        // ---- packed-FP32 accumulation: {N, D} += w * {x*c, c} ----
+        // One kernel row per iteration, deliberately not unrolled: its K*Cout weights are loaded
+        // into SGPRs (s_load) right before use. Unrolling lets the compiler hoist every weight of
+        // the plane into SGPRs, which spills them through v_writelane.
+        const f2* row = rowbase + (ci & 1) * C::PLANE;
+        const float* wr = wgt + (size_t)ci * K * K;  // weights of (ci, kh) are K contiguous floats
+#pragma unroll 1
+        for (int q = 0; q < K; ++q, row += C::IWP, wr += K) {
             f2 v[C::NV];
 #pragma unroll
             for (int m = 0; m < C::NV / 2; ++m) {
@@ -98,7 +98,7 @@ __global__ __launch_bounds__(kThreads) void fwd_tiled(LayerDev d, float* __restr
     // ---- epilogue ----
     const int oh = oh0 + ty;
     if constexpr (!TAIL) {
-        const bool vec = (L.Wo & 3) == 0 && (ow0 + tx + 3) < L.Wo;
+        const bool vec = (L.Wo & 3) == 0 && (ow0 + tx + C::P - 1) < L.Wo;
         // optional fused 2x2 max-pool of the outputs (the next down layer's input, step1.py:62-75):
         // rows oh and oh^1 sit in lanes l and l^16 of one wave (ty = tid >> 4, tile origin even)
         const bool pool = t.py != nullptr;
@@ -131,8 +131,11 @@ __global__ __launch_bounds__(kThreads) void fwd_tiled(LayerDev d, float* __restr
             if (oh >= L.Ho) continue;
             const size_t base = plane_idx(b, o, COUT, L.Ho, L.Wo, oh, ow0 + tx);
             if (vec) {
-                *reinterpret_cast<f4*>(y + base) = (f4){yv[0], yv[1], yv[2], yv[3]};
-                *reinterpret_cast<f4*>(yc + base) = (f4){cv[0], cv[1], cv[2], cv[3]};
+#pragma unroll
+                for (int q = 0; q < C::P; q += 4) {
+                    *reinterpret_cast<f4*>(y + base + q) = (f4){yv[q], yv[q + 1], yv[q + 2], yv[q + 3]};
+                    *reinterpret_cast<f4*>(yc + base + q) = (f4){cv[q], cv[q + 1], cv[q + 2], cv[q + 3]};
+                }
             } else {
 #pragma unroll
                 for (int j = 0; j < C::P; ++j)
