@@ -11,6 +11,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <type_traits>
 #include "../../include/nconv.h"
 
 typedef float f2 __attribute__((ext_vector_type(2)));
@@ -271,6 +272,45 @@ struct PlaneRegs {
         }
     }
 };
+
+// The same for tiles narrower than a wave (IWT < 64): elements are dealt to the 256 threads in
+// row-major order (e = tid + 256 k), so consecutive lanes still read consecutive columns.
+template <int IHT, int IWT, int IWP>
+struct PlaneRegsLin {
+    static constexpr int NT = IHT * IWT;
+    static constexpr int NE = (NT + 255) / 256;
+    float x[NE], c[NE];
+
+    __device__ __forceinline__ void load(const LayerDev& d, const ChanSrc& s, int ih0, int iw0, int tid) {
+        const int H = d.L.H, W = d.L.W;
+#pragma unroll
+        for (int k = 0; k < NE; ++k) {
+            int e = tid + 256 * k;
+            e = e < NT ? e : NT - 1;
+            const int r = e / IWT, col = e - r * IWT;
+            const int ih = ih0 + r, iw = iw0 + col;
+            const int ihc = ih < 0 ? 0 : (ih >= H ? H - 1 : ih);
+            const int iwc = iw < 0 ? 0 : (iw >= W ? W - 1 : iw);
+            load_chan(d, s, ihc, iwc, x[k], c[k]);
+        }
+    }
+
+    __device__ __forceinline__ void store(const LayerDev& d, f2* t, int ih0, int iw0, int tid) const {
+        const int H = d.L.H, W = d.L.W;
+#pragma unroll
+        for (int k = 0; k < NE; ++k) {
+            const int e = tid + 256 * k;
+            const int r = e / IWT, col = e - r * IWT;
+            const bool ok = (unsigned)(ih0 + r) < (unsigned)H && (unsigned)(iw0 + col) < (unsigned)W;
+            const float xv = ok ? x[k] : 0.f, cv = ok ? c[k] : 0.f;
+            if (NE * 256 == NT || e < NT) t[r * IWP + col] = (f2){xv * cv, cv};
+        }
+    }
+};
+
+template <int IHT, int IWT, int IWP>
+using PlaneStage = typename std::conditional<(IWT >= 64), PlaneRegs<IHT, IWT, IWP>,
+                                             PlaneRegsLin<IHT, IWT, IWP>>::type;
 
 // Load and store back to back (no pipelining): one staged plane.
 template <int IHT, int IWT, int IWP>

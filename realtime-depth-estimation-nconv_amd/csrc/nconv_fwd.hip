@@ -21,9 +21,8 @@ constexpr int kThreads = 256;
 
 template <int CIN, int K>
 struct FwdCfg {
-    // 4 pixels per thread, 16 threads per tile row, 16 rows (P = 8 for the 3x3 layers measured
-    // slower: 187 VGPRs -> 2 waves/SIMD)
-    static constexpr int P = 4, TW = 16 * P, TH = 16;
+    // P pixels per thread, 16 threads per tile row, 16 rows
+    static constexpr int P = K == 1 ? 4 : 2, TW = 16 * P, TH = 16;
     static constexpr int IHT = TH + K - 1, IWT = TW + K - 1;
     static constexpr int IWP = (IWT + 1) & ~1;  // even pitch keeps the f4 reads 16-B aligned
     static constexpr int PLANE = ((IHT + 3) / 4 * 4) * IWP;  // stage_plane writes whole 4-row groups
@@ -57,7 +56,7 @@ __global__ __launch_bounds__(kThreads) void fwd_tiled(LayerDev d, float* __restr
     // global loads of plane ci+1 are issued into registers before the FMAs on plane ci and land
     // in the other buffer after them, so one barrier per channel separates writer and readers
     // (a buffer is rewritten two steps after it was read, with a barrier in between).
-    PlaneRegs<C::IHT, C::IWT, C::IWP> pr;
+    PlaneStage<C::IHT, C::IWT, C::IWP> pr;
     pr.load(d, chan_src<MODE>(d, b, 0), ih0, iw0, tid);
     const f2* rowbase = &tile[ty * C::IWP + tx];
 #pragma unroll 1
@@ -98,7 +97,8 @@ __global__ __launch_bounds__(kThreads) void fwd_tiled(LayerDev d, float* __restr
     // ---- epilogue ----
     const int oh = oh0 + ty;
     if constexpr (!TAIL) {
-        const bool vec = (L.Wo & 3) == 0 && (ow0 + tx + C::P - 1) < L.Wo;
+        constexpr int VW = C::P % 4 == 0 ? 4 : 2;  // vector store width
+        const bool vec = (L.Wo % VW) == 0 && (ow0 + tx + C::P - 1) < L.Wo;
         // optional fused 2x2 max-pool of the outputs (the next down layer's input, step1.py:62-75):
         // rows oh and oh^1 sit in lanes l and l^16 of one wave (ty = tid >> 4, tile origin even)
         const bool pool = t.py != nullptr;
@@ -132,9 +132,14 @@ __global__ __launch_bounds__(kThreads) void fwd_tiled(LayerDev d, float* __restr
             const size_t base = plane_idx(b, o, COUT, L.Ho, L.Wo, oh, ow0 + tx);
             if (vec) {
 #pragma unroll
-                for (int q = 0; q < C::P; q += 4) {
-                    *reinterpret_cast<f4*>(y + base + q) = (f4){yv[q], yv[q + 1], yv[q + 2], yv[q + 3]};
-                    *reinterpret_cast<f4*>(yc + base + q) = (f4){cv[q], cv[q + 1], cv[q + 2], cv[q + 3]};
+                for (int q = 0; q < C::P; q += VW) {
+                    if constexpr (VW == 4) {
+                        *reinterpret_cast<f4*>(y + base + q) = (f4){yv[q], yv[q + 1], yv[q + 2], yv[q + 3]};
+                        *reinterpret_cast<f4*>(yc + base + q) = (f4){cv[q], cv[q + 1], cv[q + 2], cv[q + 3]};
+                    } else {
+                        *reinterpret_cast<f2*>(y + base + q) = (f2){yv[q], yv[q + 1]};
+                        *reinterpret_cast<f2*>(yc + base + q) = (f2){cv[q], cv[q + 1]};
+                    }
                 }
             } else {
 #pragma unroll
