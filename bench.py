@@ -44,6 +44,7 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--graph", type=int, default=1, help="capture the forward in a hipGraph (1) or run eager (0)")
+    p.add_argument("--streams", type=int, default=2, help="HIP streams the inference batch is split over")
     return p.parse_args()
 
 
@@ -108,6 +109,7 @@ def time_layers(m, net, S, reps=20):
         x4, c4 = fwd(d3.spec(), p3, q3, None, None, d3.weight, d3.bias, sd3)
         x34, c34 = fwd(l4.spec(lib.UPCAT_SKIP_FIRST), x3, c3, x4, c4, l4.weight, l4.bias, s4)
         x23, c23 = fwd(l5.spec(lib.UPCAT_SKIP_FIRST), x2, c2, x34, c34, l5.weight, l5.bias, s5)
+    tail_out = torch.empty((S.shape[0], 1, oh, ow), device=S.device, dtype=torch.float32)
     calls = {
         "nconv1": lambda: fwd(l1.spec(lib.THRESH, 0.01), S, None, None, None, l1.weight, l1.bias, s1),
         "nconv2": lambda: fpool(l2.spec(), x1, c1, None, None, l2.weight, l2.bias, s2),
@@ -116,7 +118,7 @@ def time_layers(m, net, S, reps=20):
         "nconv_down3": lambda: fwd(d3.spec(), p3, q3, None, None, d3.weight, d3.bias, sd3),
         "nconv4": lambda: fwd(l4.spec(lib.UPCAT_SKIP_FIRST), x3, c3, x4, c4, l4.weight, l4.bias, s4),
         "nconv5": lambda: fwd(l5.spec(lib.UPCAT_SKIP_FIRST), x2, c2, x34, c34, l5.weight, l5.bias, s5),
-        "nconv6+7_tail": lambda: d._fused_tail(l6, l7, s6, s7, x1b, c1b, x23, c23, oh, ow),
+        "nconv6+7_tail": lambda: d._fused_tail(l6, l7, s6, s7, x1b, c1b, x23, c23, tail_out),
     }
     out = {}
     stream = torch.cuda.current_stream()
@@ -220,6 +222,7 @@ def main():
     with torch.no_grad():
         net(torch.zeros(1, 1, 32, 32, device=dev))  # one EnforcePos: positive (trained-like) weights
     net.eval()
+    net.d_net.inference_streams = a.streams
     g = torch.Generator().manual_seed(1000 + rank)
     S = sparse_depth(g, B, H, W, dev)
 
@@ -319,7 +322,7 @@ def main():
             "config": {"workload": "config2: SETP1_NCONV/DNET forward, fused HIP NConv kernels",
                        "global_batch": B * world, "per_gpu_batch": B, "height": H, "width": W,
                        "crop": "generalized [1:H+1,1:W+1]", "parallelism": f"frame-sharded x{world}",
-                       "hipgraph": bool(graph is not None)},
+                       "hipgraph": bool(graph is not None), "streams": a.streams},
             "train_fwd_bwd_adamw": train,
             "layer_us": {k: round(v, 2) for k, v in lt.items()},
             "roofline": roof,

@@ -15,24 +15,26 @@
 // step1.py:53-90) evaluated while staging, so glued tensors never hit HBM.
 #include "nconv_internal.h"
 
+#include <stdlib.h>
+
 namespace nconv {
 
 constexpr int kThreads = 256;
 
-template <int CIN, int K>
+template <int CIN, int K, int P_>
 struct FwdCfg {
     // P pixels per thread, 16 threads per tile row, 16 rows
-    static constexpr int P = K == 1 ? 4 : 2, TW = 16 * P, TH = 16;
+    static constexpr int P = P_, TW = 16 * P, TH = 16;
     static constexpr int IHT = TH + K - 1, IWT = TW + K - 1;
     static constexpr int IWP = (IWT + 1) & ~1;  // even pitch keeps the f4 reads 16-B aligned
     static constexpr int PLANE = ((IHT + 3) / 4 * 4) * IWP;  // stage_plane writes whole 4-row groups
     static constexpr int NV = P + K - 1;  // sliding-window width per kernel row
 };
 
-template <int CIN, int COUT, int K, int MODE, bool TAIL>
+template <int CIN, int COUT, int K, int MODE, bool TAIL, int P>
 __global__ __launch_bounds__(kThreads) void fwd_tiled(LayerDev d, float* __restrict__ y,
                                                       float* __restrict__ yc, TailArgs t) {
-    using C = FwdCfg<CIN, K>;
+    using C = FwdCfg<CIN, K, P>;
     __shared__ __attribute__((aligned(16))) f2 tile[2 * C::PLANE];
     const nconv_layer& L = d.L;
     const float* __restrict__ wgt = L.weight;
@@ -74,13 +76,18 @@ __global__ __launch_bounds__(kThreads) void fwd_tiled(LayerDev d, float* __restr
 #pragma unroll 1
         for (int q = 0; q < K; ++q, row += C::IWP, wr += K) {
             f2 v[C::NV];
+            if constexpr (C::P % 2 == 0) {  // even pixel offset: 16-B aligned ds_read_b128
 #pragma unroll
-            for (int m = 0; m < C::NV / 2; ++m) {
-                f4 qv = reinterpret_cast<const f4*>(row)[m];
-                v[2 * m] = qv.xy;
-                v[2 * m + 1] = qv.zw;
+                for (int m = 0; m < C::NV / 2; ++m) {
+                    f4 qv = reinterpret_cast<const f4*>(row)[m];
+                    v[2 * m] = qv.xy;
+                    v[2 * m + 1] = qv.zw;
+                }
+                if constexpr (C::NV & 1) v[C::NV - 1] = row[C::NV - 1];
+            } else {
+#pragma unroll
+                for (int m = 0; m < C::NV; ++m) v[m] = row[m];
             }
-            if constexpr (C::NV & 1) v[C::NV - 1] = row[C::NV - 1];
 #pragma unroll
             for (int kw = 0; kw < K; ++kw)
 #pragma unroll
@@ -97,7 +104,7 @@ __global__ __launch_bounds__(kThreads) void fwd_tiled(LayerDev d, float* __restr
     // ---- epilogue ----
     const int oh = oh0 + ty;
     if constexpr (!TAIL) {
-        constexpr int VW = C::P % 4 == 0 ? 4 : 2;  // vector store width
+        constexpr int VW = C::P % 4 == 0 ? 4 : C::P % 2 == 0 ? 2 : 1;  // vector store width
         const bool vec = (L.Wo % VW) == 0 && (ow0 + tx + C::P - 1) < L.Wo;
         // optional fused 2x2 max-pool of the outputs (the next down layer's input, step1.py:62-75):
         // rows oh and oh^1 sit in lanes l and l^16 of one wave (ty = tid >> 4, tile origin even)
@@ -118,7 +125,15 @@ __global__ __launch_bounds__(kThreads) void fwd_tiled(LayerDev d, float* __restr
                     yb[j] = __shfl_xor(yv[j], 16);
                     cb[j] = __shfl_xor(cv[j], 16);
                 }
-                if (pool_row) {
+                if constexpr (C::P == 1) {  // the window's right column sits in lane l^1
+                    const float ya = __shfl_xor(yv[0], 1), ca = __shfl_xor(cv[0], 1);
+                    const float yd = __shfl_xor(yb[0], 1), cd = __shfl_xor(cb[0], 1);
+                    if (pool_row && (tid & 1) == 0 && pc0 < Wp) {
+                        const size_t pi = plane_idx(b, o, COUT, Hp, Wp, pr, pc0);
+                        t.py[pi] = pool4v(yv[0], ya, yb[0], yd);
+                        t.pc[pi] = pool4v(cv[0], ca, cb[0], cd);
+                    }
+                } else if (pool_row) {
                     const size_t pbase = plane_idx(b, o, COUT, Hp, Wp, pr, pc0);
 #pragma unroll
                     for (int h = 0; h < C::P / 2; ++h)
@@ -136,9 +151,12 @@ __global__ __launch_bounds__(kThreads) void fwd_tiled(LayerDev d, float* __restr
                     if constexpr (VW == 4) {
                         *reinterpret_cast<f4*>(y + base + q) = (f4){yv[q], yv[q + 1], yv[q + 2], yv[q + 3]};
                         *reinterpret_cast<f4*>(yc + base + q) = (f4){cv[q], cv[q + 1], cv[q + 2], cv[q + 3]};
-                    } else {
+                    } else if constexpr (VW == 2) {
                         *reinterpret_cast<f2*>(y + base + q) = (f2){yv[q], yv[q + 1]};
                         *reinterpret_cast<f2*>(yc + base + q) = (f2){cv[q], cv[q + 1]};
+                    } else {
+                        y[base + q] = yv[q];
+                        yc[base + q] = cv[q];
                     }
                 }
             } else {
@@ -277,12 +295,32 @@ static bool simple_geometry(const nconv_layer& L) {
     return L.SH == 1 && L.SW == 1 && L.DH == 1 && L.DW == 1 && L.groups == 1 && L.KH == L.KW;
 }
 
+template <int CIN, int COUT, int K, int MODE, bool TAIL, int P>
+static void go_tiled_p(const LayerDev& d, float* y, float* yc, const TailArgs& t, int gh, int gw,
+                       hipStream_t st) {
+    using C = FwdCfg<CIN, K, P>;
+    dim3 grid(((gw + C::TW - 1) / C::TW) * ((gh + C::TH - 1) / C::TH) * d.L.B);  // see xcd_tile
+    hipLaunchKernelGGL((fwd_tiled<CIN, COUT, K, MODE, TAIL, P>), grid, dim3(kThreads), 0, st, d, y, yc, t);
+}
+
+// Pixels per thread of a tiled launch (NCONV_FWD_P overrides, for tuning).
+static int fwd_pixels(int K) {
+    static int env = [] {
+        const char* e = getenv("NCONV_FWD_P");
+        return e ? atoi(e) : 0;
+    }();
+    if (K == 1) return 4;
+    return (env == 1 || env == 2 || env == 4) ? env : 2;
+}
+
 template <int CIN, int COUT, int K, int MODE, bool TAIL>
 static void go_tiled(const LayerDev& d, float* y, float* yc, const TailArgs& t, int gh, int gw,
                      hipStream_t st) {
-    using C = FwdCfg<CIN, K>;
-    dim3 grid(((gw + C::TW - 1) / C::TW) * ((gh + C::TH - 1) / C::TH) * d.L.B);  // see xcd_tile
-    hipLaunchKernelGGL((fwd_tiled<CIN, COUT, K, MODE, TAIL>), grid, dim3(kThreads), 0, st, d, y, yc, t);
+    switch (fwd_pixels(K)) {
+        case 1: go_tiled_p<CIN, COUT, K, MODE, TAIL, 1>(d, y, yc, t, gh, gw, st); break;
+        case 4: go_tiled_p<CIN, COUT, K, MODE, TAIL, 4>(d, y, yc, t, gh, gw, st); break;
+        default: go_tiled_p<CIN, COUT, K, MODE, TAIL, 2>(d, y, yc, t, gh, gw, st); break;
+    }
 }
 
 int launch_fwd(const LayerDev& d, float* y, float* yc, float* py, float* pc, hipStream_t st, const char** why) {

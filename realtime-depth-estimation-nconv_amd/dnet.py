@@ -100,33 +100,76 @@ class DNET(nn.Module):
         out_h, out_w = crop_hw(H, W, self.crop)
         f = nconv_layer if grad else (lambda spec, *a: layer_forward_raw(spec, *a))
 
+        if not grad and min(H, W) >= 16:
+            out = torch.empty((S.shape[0], 1, out_h, out_w), device=S.device, dtype=torch.float32)
+            self._infer_split(S, layers, wsum, out)
+            return out
+
         x1, c1 = f(l1.spec(_lib.THRESH, 0.01), S, None, None, None, l1.weight, l1.bias, s1)
-        if grad or min(H, W) < 16:
-            x1, c1 = f(l2.spec(), x1, c1, None, None, l2.weight, l2.bias, s2)
-            x2, c2 = f(d1.spec(_lib.POOL2), x1, c1, None, None, d1.weight, d1.bias, sd1)
-            x3, c3 = f(d2.spec(_lib.POOL2), x2, c2, None, None, d2.weight, d2.bias, sd2)
-            x4, c4 = f(d3.spec(_lib.POOL2), x3, c3, None, None, d3.weight, d3.bias, sd3)
-        else:  # inference: each producer also writes the pooled input of the next down layer
-            fp = layer_forward_pooled
-            x1, c1, p1, q1 = fp(l2.spec(), x1, c1, None, None, l2.weight, l2.bias, s2)
-            x2, c2, p2, q2 = fp(d1.spec(), p1, q1, None, None, d1.weight, d1.bias, sd1)
-            x3, c3, p3, q3 = fp(d2.spec(), p2, q2, None, None, d2.weight, d2.bias, sd2)
-            x4, c4 = f(d3.spec(), p3, q3, None, None, d3.weight, d3.bias, sd3)
+        x1, c1 = f(l2.spec(), x1, c1, None, None, l2.weight, l2.bias, s2)
+        x2, c2 = f(d1.spec(_lib.POOL2), x1, c1, None, None, d1.weight, d1.bias, sd1)
+        x3, c3 = f(d2.spec(_lib.POOL2), x2, c2, None, None, d2.weight, d2.bias, sd2)
+        x4, c4 = f(d3.spec(_lib.POOL2), x3, c3, None, None, d3.weight, d3.bias, sd3)
         if self.capture is not None:
             self.capture.update(down1=(x1.detach(), c1.detach()), down2=(x2.detach(), c2.detach()),
                                 down3=(x3.detach(), c3.detach()))
         x34, c34 = f(l4.spec(_lib.UPCAT_SKIP_FIRST), x3, c3, x4, c4, l4.weight, l4.bias, s4)
         x23, c23 = f(l5.spec(_lib.UPCAT_SKIP_FIRST), x2, c2, x34, c34, l5.weight, l5.bias, s5)
-        if grad:
-            xo, co = f(l6.spec(_lib.UPCAT_UP_FIRST), x1, c1, x23, c23, l6.weight, l6.bias, s6)
-            xo, co = f(l7.spec(), xo, co, None, None, l7.weight, l7.bias, s7)
-            return xo[:, :, 1:1 + out_h, 1:1 + out_w]
-        return self._fused_tail(l6, l7, s6, s7, x1, c1, x23, c23, out_h, out_w)
+        xo, co = f(l6.spec(_lib.UPCAT_UP_FIRST), x1, c1, x23, c23, l6.weight, l6.bias, s6)
+        xo, co = f(l7.spec(), xo, co, None, None, l7.weight, l7.bias, s7)
+        return xo[:, :, 1:1 + out_h, 1:1 + out_w]
 
-    def _fused_tail(self, l6, l7, s6, s7, x1, c1, x23, c23, out_h, out_w):
-        B = x1.shape[0]
-        out = torch.empty((B, 1, out_h, out_w), device=x1.device, dtype=torch.float32)
-        if out_h == 0 or out_w == 0:
+    # -- inference ------------------------------------------------------------------------------
+    # Frames are independent, so the batch is split over `inference_streams` HIP streams, each
+    # running the whole layer chain on its share: the streams' kernels overlap, so the partial
+    # last round of one layer's workgroups and the drain/fill gap between dependent launches are
+    # filled with the other stream's work (the chain itself is strictly sequential).
+    inference_streams = 2
+
+    def _side_streams(self, device, n):
+        key = (device.index, n)
+        cache = self.__dict__.setdefault("_stream_cache", {})
+        if key not in cache:
+            cache[key] = [torch.cuda.Stream(device=device) for _ in range(n)]
+        return cache[key]
+
+    def _infer_split(self, S, layers, wsum, out):
+        B = S.shape[0]
+        n = max(1, min(int(self.inference_streams), B))
+        if n == 1:
+            self._infer(S, layers, wsum, out)
+            return
+        cur = torch.cuda.current_stream(S.device)
+        side = self._side_streams(S.device, n - 1)
+        bounds = [B * k // n for k in range(n + 1)]
+        for st in side:
+            st.wait_stream(cur)
+        for k, st in enumerate([cur] + side):
+            with torch.cuda.stream(st):
+                self._infer(S[bounds[k]:bounds[k + 1]], layers, wsum, out[bounds[k]:bounds[k + 1]])
+        for st in side:
+            cur.wait_stream(st)
+
+    def _infer(self, S, layers, wsum, out):
+        """The inference chain on the current stream: each producer also writes the pooled input
+        of the next down layer, and nconv6+nconv7+crop run as one launch writing `out`."""
+        (l1, l2, d1, d2, d3, l4, l5, l6, l7) = layers
+        (s1, s2, sd1, sd2, sd3, s4, s5, s6, s7) = wsum
+        f, fp = layer_forward_raw, layer_forward_pooled
+        x1, c1 = f(l1.spec(_lib.THRESH, 0.01), S, None, None, None, l1.weight, l1.bias, s1)
+        x1, c1, p1, q1 = fp(l2.spec(), x1, c1, None, None, l2.weight, l2.bias, s2)
+        x2, c2, p2, q2 = fp(d1.spec(), p1, q1, None, None, d1.weight, d1.bias, sd1)
+        x3, c3, p3, q3 = fp(d2.spec(), p2, q2, None, None, d2.weight, d2.bias, sd2)
+        x4, c4 = f(d3.spec(), p3, q3, None, None, d3.weight, d3.bias, sd3)
+        if self.capture is not None:
+            self.capture.update(down1=(x1, c1), down2=(x2, c2), down3=(x3, c3))
+        x34, c34 = f(l4.spec(_lib.UPCAT_SKIP_FIRST), x3, c3, x4, c4, l4.weight, l4.bias, s4)
+        x23, c23 = f(l5.spec(_lib.UPCAT_SKIP_FIRST), x2, c2, x34, c34, l5.weight, l5.bias, s5)
+        self._fused_tail(l6, l7, s6, s7, x1, c1, x23, c23, out)
+
+    def _fused_tail(self, l6, l7, s6, s7, x1, c1, x23, c23, out):
+        out_h, out_w = out.shape[2], out.shape[3]
+        if out_h == 0 or out_w == 0 or out.shape[0] == 0:
             return out
         L = l6.spec(_lib.UPCAT_UP_FIRST).descriptor(x1, c1, x23, c23, l6.weight, l6.bias, s6)
         if tuple(l7.kernel_size) != (1, 1) or l7.padding[0] != l7.padding[1] or tuple(l7.stride) != (1, 1):
