@@ -11,7 +11,8 @@ import threading
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libnconv.so")
+# NCONV_LIB: an alternative build of the same library (kernel-tuning experiments)
+LIB_PATH = os.environ.get("NCONV_LIB") or os.path.join(_HERE, "libnconv.so")
 ABI_VERSION = 3
 BWD_ACCUMULATE = 1
 

@@ -35,7 +35,10 @@ template <int CIN, int COUT, int K, int MODE, bool TAIL, int P>
 __global__ __launch_bounds__(kThreads) void fwd_tiled(LayerDev d, float* __restrict__ y,
                                                       float* __restrict__ yc, TailArgs t) {
     using C = FwdCfg<CIN, K, P>;
-    __shared__ __attribute__((aligned(16))) f2 tile[2 * C::PLANE];
+    using TS = TileStager<C::IHT, C::IWT, C::IWP, MODE>;
+    constexpr bool kBufStage = C::IWT < 64;  // buffer-load stager (narrow tiles)
+    constexpr int kStride = kBufStage ? TS::PLANE_STRIDE : C::PLANE;  // f2 per plane buffer
+    __shared__ __attribute__((aligned(16))) f2 tile[2 * kStride];
     const nconv_layer& L = d.L;
     const float* __restrict__ wgt = L.weight;
     const int tid = threadIdx.x;
@@ -54,24 +57,13 @@ __global__ __launch_bounds__(kThreads) void fwd_tiled(LayerDev d, float* __restr
 #pragma unroll
         for (int j = 0; j < C::P; ++j) acc[o][j] = (f2){0.f, 0.f};
 
-    // Software pipeline over input channels, one staged plane per step, two LDS buffers: the
-    // global loads of plane ci+1 are issued into registers before the FMAs on plane ci and land
-    // in the other buffer after them, so one barrier per channel separates writer and readers
-    // (a buffer is rewritten two steps after it was read, with a barrier in between).
-    PlaneStage<C::IHT, C::IWT, C::IWP> pr;
-    pr.load(d, chan_src<MODE>(d, b, 0), ih0, iw0, tid);
+    // ---- packed-FP32 accumulation of one staged plane: {N, D} += w * {x*c, c} ----
+    // One kernel row per iteration, deliberately not unrolled: its K*Cout weights are loaded into
+    // SGPRs (s_load) right before use. Unrolling lets the compiler hoist every weight of the plane
+    // into SGPRs, which spills them through v_writelane.
     const f2* rowbase = &tile[ty * C::IWP + tx];
-#pragma unroll 1
-    for (int ci = 0; ci < CIN; ++ci) {
-        f2* buf = tile + (ci & 1) * C::PLANE;
-        pr.store(d, buf, ih0, iw0, tid);
-        __syncthreads();
-        if (ci + 1 < CIN) pr.load(d, chan_src<MODE>(d, b, ci + 1), ih0, iw0, tid);
-        // ---- packed-FP32 accumulation: {N, D} += w * {x*c, c} ----
-        // One kernel row per iteration, deliberately not unrolled: its K*Cout weights are loaded
-        // into SGPRs (s_load) right before use. Unrolling lets the compiler hoist every weight of
-        // the plane into SGPRs, which spills them through v_writelane.
-        const f2* row = rowbase + (ci & 1) * C::PLANE;
+    auto fma_plane = [&](int ci, int bufi) {
+        const f2* row = rowbase + bufi * kStride;
         const float* wr = wgt + (size_t)ci * K * K;  // weights of (ci, kh) are K contiguous floats
 #pragma unroll 1
         for (int q = 0; q < K; ++q, row += C::IWP, wr += K) {
@@ -88,16 +80,60 @@ __global__ __launch_bounds__(kThreads) void fwd_tiled(LayerDev d, float* __restr
 #pragma unroll
                 for (int m = 0; m < C::NV; ++m) v[m] = row[m];
             }
+#ifndef NCONV_FMA_REPEAT
+#define NCONV_FMA_REPEAT 1
+#endif
 #pragma unroll
-            for (int kw = 0; kw < K; ++kw)
+            for (int rep = 0; rep < NCONV_FMA_REPEAT; ++rep)
 #pragma unroll
-                for (int o = 0; o < COUT; ++o) {
-                    const float w = wr[o * CIN * K * K + kw];
-                    const f2 w2 = (f2){w, w};
+                for (int kw = 0; kw < K; ++kw)
 #pragma unroll
-                    for (int j = 0; j < C::P; ++j)
-                        acc[o][j] = __builtin_elementwise_fma(w2, v[j + kw], acc[o][j]);
-                }
+                    for (int o = 0; o < COUT; ++o) {
+                        const float w = wr[o * CIN * K * K + kw];
+                        const f2 w2 = (f2){w, w};
+#pragma unroll
+                        for (int j = 0; j < C::P; ++j)
+                            acc[o][j] = __builtin_elementwise_fma(w2, v[j + kw], acc[o][j]);
+                    }
+        }
+    };
+
+    // Software pipeline over input channels with two LDS plane buffers and one barrier per
+    // channel (a buffer is rewritten two steps after it was read, with a barrier in between).
+    if constexpr (kBufStage) {
+        // Loads run two planes ahead: plane ci+2's buffer loads are issued right after plane ci
+        // is stored, so each has two planes of FMAs to land.
+        TS ts;
+        ts.init(d, ih0, iw0, tid);
+        float xa[TS::NE], ca[TS::NE], xb[TS::NE], cb[TS::NE];
+        ts.load(chan_src<MODE>(d, b, 0), xa, ca);
+        if (CIN > 1) ts.load(chan_src<MODE>(d, b, 1), xb, cb);
+        // The prefetches are unconditional (past the last channel they re-read it, L2-resident):
+        // a branch around them would make the wait before each store conservatively drain the
+        // other set's loads too.
+#pragma unroll 1
+        for (int ci = 0; ci < CIN; ci += 2) {
+            ts.store(tile, xa, ca, L.thresh);
+            __syncthreads();
+            ts.load(chan_src<MODE>(d, b, ci + 2 < CIN ? ci + 2 : CIN - 1), xa, ca);
+            fma_plane(ci, 0);
+            if (ci + 1 < CIN) {
+                ts.store(tile + kStride, xb, cb, L.thresh);
+                __syncthreads();
+                ts.load(chan_src<MODE>(d, b, ci + 3 < CIN ? ci + 3 : CIN - 1), xb, cb);
+                fma_plane(ci + 1, 1);
+            }
+        }
+    } else {
+        // wide tiles: loads one plane ahead through the column-mapped register stage
+        PlaneStage<C::IHT, C::IWT, C::IWP> pr;
+        pr.load(d, chan_src<MODE>(d, b, 0), ih0, iw0, tid);
+#pragma unroll 1
+        for (int ci = 0; ci < CIN; ++ci) {
+            pr.store(d, tile + (ci & 1) * kStride, ih0, iw0, tid);
+            __syncthreads();
+            if (ci + 1 < CIN) pr.load(d, chan_src<MODE>(d, b, ci + 1), ih0, iw0, tid);
+            fma_plane(ci, ci & 1);
         }
     }
 
@@ -143,6 +179,9 @@ __global__ __launch_bounds__(kThreads) void fwd_tiled(LayerDev d, float* __restr
                         }
                 }
             }
+#ifdef NCONV_EXP_NO_STORES
+            if (yv[0] != 1234.5f) continue;
+#endif
             if (oh >= L.Ho) continue;
             const size_t base = plane_idx(b, o, COUT, L.Ho, L.Wo, oh, ow0 + tx);
             if (vec) {
