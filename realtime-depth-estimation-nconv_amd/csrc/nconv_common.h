@@ -418,8 +418,13 @@ struct TileStager {
 #pragma unroll
             for (int k = 0; k < NE; ++k) {
                 const unsigned o = UP ? (up ? gb[UP ? k : 0] : ga[k]) : ga[k];
+#ifdef NCONV_EXP_NO_LOADS
+                x[k] = (float)(o & 255);
+                c[k] = 1.f;
+#else
                 x[k] = ld_f32(rx, o);
                 c[k] = ld_f32(rc, o);
+#endif
             }
         }
     }

@@ -31,8 +31,13 @@ struct FwdCfg {
     static constexpr int NV = P + K - 1;  // sliding-window width per kernel row
 };
 
+#ifdef NCONV_EXP_WAVES
+#define NCONV_FWD_ATTR __attribute__((amdgpu_waves_per_eu(NCONV_EXP_WAVES, NCONV_EXP_WAVES)))
+#else
+#define NCONV_FWD_ATTR
+#endif
 template <int CIN, int COUT, int K, int MODE, bool TAIL, int P>
-__global__ __launch_bounds__(kThreads) void fwd_tiled(LayerDev d, float* __restrict__ y,
+__global__ __launch_bounds__(kThreads) NCONV_FWD_ATTR void fwd_tiled(LayerDev d, float* __restrict__ y,
                                                       float* __restrict__ yc, TailArgs t) {
     using C = FwdCfg<CIN, K, P>;
     using TS = TileStager<C::IHT, C::IWT, C::IWP, MODE>;

@@ -30,6 +30,9 @@ def main(dirs, min_grid):
         for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_SMEM", "SQ_INSTS_LDS", "SQ_LDS_BANK_CONFLICT"):
             if c in m:
                 line += f" {c[3:].lower()}/w {m[c]/w:.0f}"
+        for c, val in sorted(m.items()):  # any other counter: mean per dispatch
+            if not c.startswith("SQ_"):
+                line += f" {c}={val:.4g}"
         print(line)
 
 
