@@ -42,6 +42,7 @@ def parse():
     p.add_argument("--train-steps", type=int, default=None, help="timed fwd+bwd steps (default: --steps)")
     p.add_argument("--no-train", action="store_true")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-guided", action="store_true", help="skip the config-3 guided forward measurement")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--graph", type=int, default=1, help="capture the forward in a hipGraph (1) or run eager (0)")
     p.add_argument("--streams", type=int, default=2, help="HIP streams the inference batch is split over")
@@ -181,6 +182,40 @@ def cpu_baseline(B, H, W, seconds):
                       f"torch CPU, {threads} threads) in {el:.1f} s"}
 
 
+def guided_forward(m, dev, B, H, W, steps, warmup, rank):
+    """Config 3: SETP2 (RGB-guided, models/step2.py:80-126) forward on B/2 + B/2 frames (rgb0/depth0,
+    rgb1/depth1) per GPU, eval, hipGraph-captured; step 1 runs on the libnconv kernels, the RGB
+    encoder and fusion decoder convolutions on PyTorch-ROCm. Returns frames/sec of this rank."""
+    torch.manual_seed(1)
+    net = m.SETP2_BP_EXPORT(step1_crop="generalized").to(dev).eval()
+    g = torch.Generator().manual_seed(3000 + rank)
+    h = B // 2
+    rgb0 = (torch.rand(h, 3, H, W, generator=g) * 255).to(dev)
+    rgb1 = (torch.rand(h, 3, H, W, generator=g) * 255).to(dev)
+    d0 = sparse_depth(g, h, H, W, dev)
+    d1 = sparse_depth(g, h, H, W, dev)
+    with torch.no_grad():
+        for _ in range(max(warmup, 1)):
+            net(rgb0, d0, rgb1, d1)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                net(rgb0, d0, rgb1, d1)
+        torch.cuda.current_stream().wait_stream(s)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            net(rgb0, d0, rgb1, d1)
+        graph.replay()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            graph.replay()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+    return el
+
+
 def make_train_step(m, dev, B, H, W, world, rank):
     """One step-1 training iteration as train_step1.py:59-65: train-mode forward (EnforcePos
     drift), calculate_loss on element [0] with the gradient loss, backward, (RCCL gradient
@@ -289,6 +324,20 @@ def main():
             tt = t.item()
         train = {"frames_per_sec": world * B * ks / tt, "ms_per_step": tt / ks * 1e3, "steps": ks}
 
+    # ---- config 3: guided forward ----
+    guided = None
+    if not a.no_guided:
+        gsteps = max(5, a.steps // 5)
+        el = guided_forward(m, dev, B, H, W, gsteps, min(a.warmup, 3), rank)
+        barrier()
+        if world > 1:
+            t = torch.tensor([el], device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = t.item()
+        guided = {"frames_per_sec": round(world * B * gsteps / el, 2), "ms_per_step": round(el / gsteps * 1e3, 3),
+                  "steps": gsteps, "frames_per_step": B * world,
+                  "workload": "config3: SETP2_BP_EXPORT forward, B/2+B/2 frames per GPU, hipGraph"}
+
     # ---- per-kernel times, roofline (rank 0) ----
     result = None
     if rank == 0:
@@ -324,6 +373,7 @@ def main():
                        "crop": "generalized [1:H+1,1:W+1]", "parallelism": f"frame-sharded x{world}",
                        "hipgraph": bool(graph is not None), "streams": a.streams},
             "train_fwd_bwd_adamw": train,
+            "guided_fwd": guided,
             "layer_us": {k: round(v, 2) for k, v in lt.items()},
             "roofline": roof,
             "cpu_baseline": cpu,

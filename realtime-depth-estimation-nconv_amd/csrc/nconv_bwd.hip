@@ -666,6 +666,286 @@ static void launch_wgrad_reduce(const float* part, int nblk, int nw, int cout, i
                        gw, gb);
 }
 
+// ---- wgrad on the matrix cores (fp32 MFMA 16x16x4, exact f32 products) -----------------------------
+// For a 3x3 / 5x5 stride-1 layer the weight gradient is, per output row oh, a GEMM over the
+// column index q = ow + kw:
+//     gW[o][i][kh][kw] += sum_q  XC[i][oh+kh-PH][q-PW] * gN[o][oh][q-kw]
+//                              +  C[i][oh+kh-PH][q-PW] * gD[o][oh][q-kw]
+// with rows M = (kh, i) (i fastest) and columns N = (kw, o) (o fastest), K = q: the kernel-row
+// shift lives in the A operand (which staged input row) and the kernel-column shift in the B
+// operand (which g column), so neither operand is replicated per tap. A workgroup owns a 64-wide
+// q strip of one image and walks a segment of output rows: a ring of K+1 staged input rows (one
+// new row per output row, no halo re-staging) and a double-buffered {gN, gD} row with a K-1
+// column left halo, one barrier per row, the next row's global loads issued before the current
+// row's MFMAs. Each wave takes 16 of the 64 columns (4 MFMA k-steps per operand pair) and keeps the
+// whole (M x N) tile in accumulators; the four waves' tiles are summed in a fixed order at the end
+// into the block's partial row (then wgrad_reduce_sum / wgrad_finish, as for wgrad_tiled).
+typedef float f4acc __attribute__((ext_vector_type(4)));
+
+template <int CIN, int COUT, int K>
+struct WmCfg {
+    static constexpr int TW = 64;
+    static constexpr int M = CIN * K, N = COUT * K;
+    static constexpr int MT = (M + 15) / 16, NT = (N + 15) / 16;
+    static constexpr int XP = TW + 4;  // staged row pitch: channel rows 4 banks apart
+    static constexpr int SLOTS = K + 1;
+    // slot stride == 4*CIN (mod 64) for CIN < 16, so a 16-row A tile spanning several kernel rows
+    // (consecutive ring slots) still covers 64 distinct banks; 0 for CIN >= 16 (one kh per tile)
+    static constexpr int SKEW = CIN * 4 < 64 ? CIN * 4 : 0;
+    static constexpr int SLOT = CIN * XP + (((SKEW - CIN * XP) % 64) + 64) % 64;
+    static constexpr int GW = TW + K - 1;  // g row incl. the left halo
+    static constexpr int GP = 72;          // == 8 (mod 64): the 8 channels of a B tile 8 banks apart
+    static_assert(GW <= GP, "g row pitch");
+    static_assert(COUT % 4 == 0, "g rows are staged four output channels per pass");
+    static constexpr int C_OFF = SLOTS * SLOT;
+    static constexpr int G_OFF = 2 * SLOTS * SLOT;  // [buf][part][o][GP]
+    static constexpr int GBUF = 2 * COUT * GP;
+    static constexpr int Z_OFF = G_OFF + 2 * GBUF;  // a zero row for padded M / N lanes
+    static constexpr int STAGE = Z_OFF + GP;
+    static constexpr int RED = 4 * MT * NT * 256;
+    static constexpr int LDS = STAGE > RED ? STAGE : RED;
+    static constexpr int CPW = (CIN + 3) / 4, OPW = COUT / 4;  // channels staged per wave
+};
+
+// (x, c) of layer-input pixel (ih, iw) of a resolved channel, zero outside the image (buffer
+// loads: out-of-range offsets read 0). THRESH leaves c to the caller.
+template <int MODE>
+__device__ __forceinline__ void load_px(const LayerDev& d, const ChanSrc& s, int ih, int iw, float& x, float& c) {
+    const nconv_layer& L = d.L;
+    const bool in = (unsigned)ih < (unsigned)L.H && (unsigned)iw < (unsigned)L.W;
+    constexpr unsigned OOB = 0x80000000u;
+    const __amdgpu_buffer_rsrc_t rx = plane_rsrc(s.x, s.bytes);
+    if constexpr (MODE == NCONV_LOAD_THRESH) {
+        x = ld_f32(rx, in ? (unsigned)(ih * s.W + iw) * 4u : OOB);
+        c = 0.f;
+    } else if constexpr (MODE == NCONV_LOAD_POOL2) {
+        const __amdgpu_buffer_rsrc_t rc = plane_rsrc(s.c, s.bytes);
+        const unsigned o1 = in ? (unsigned)((2 * ih) * s.W + 2 * iw) * 4u : OOB;
+        const unsigned o2 = in ? o1 + (unsigned)s.W * 4u : OOB;
+        const f2 x0 = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rx, o1, 0, 0));
+        const f2 x1 = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rx, o2, 0, 0));
+        const f2 c0 = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rc, o1, 0, 0));
+        const f2 c1 = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rc, o2, 0, 0));
+        x = pool4v(x0.x, x0.y, x1.x, x1.y);
+        c = pool4v(c0.x, c0.y, c1.x, c1.y);
+    } else {
+        const __amdgpu_buffer_rsrc_t rc = plane_rsrc(s.c, s.bytes);
+        unsigned off;
+        if (s.kind == kUp) {
+            const int sh = nearest_src(in ? ih : 0, L.b.H, L.H, d.up_scale_h);
+            const int sw = nearest_src(in ? iw : 0, L.b.W, L.W, d.up_scale_w);
+            off = in ? (unsigned)(sh * s.W + sw) * 4u : OOB;
+        } else {
+            off = in ? (unsigned)(ih * s.W + iw) * 4u : OOB;
+        }
+        x = ld_f32(rx, off);
+        c = ld_f32(rc, off);
+    }
+}
+
+template <int CIN, int COUT, int K, int MODE>
+__global__ __launch_bounds__(kT) void wgrad_mfma(LayerDev d, BwdArgs a, float* part, int nstrip, int nseg,
+                                                 int seg_rows) {
+    using C = WmCfg<CIN, COUT, K>;
+    __shared__ __attribute__((aligned(16))) float lds[C::LDS];
+    const nconv_layer& L = d.L;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    int blk = blockIdx.x;
+    const int strip = blk % nstrip;
+    blk /= nstrip;
+    const int seg = blk % nseg, b = blk / nseg;
+    const int ow0 = strip * C::TW;
+    const int r0 = seg * seg_rows, r1 = min(L.Ho, r0 + seg_rows);
+    constexpr unsigned OOB = 0x80000000u;
+
+    for (int e = tid; e < C::GP; e += kT) lds[C::Z_OFF + e] = 0.f;
+
+    // per-lane MFMA operand coordinates (A[m = lane&15][k = lane>>4], B[k = lane>>4][n = lane&15])
+    const int kq = lane >> 4, ml = lane & 15;
+    int a_kh[C::MT], a_ik[C::MT], b_off[C::NT];
+#pragma unroll
+    for (int t = 0; t < C::MT; ++t) {
+        const int m = 16 * t + ml;
+        a_kh[t] = m < C::M ? m / CIN : -1;
+        a_ik[t] = (m % CIN) * C::XP + kq;
+    }
+#pragma unroll
+    for (int u = 0; u < C::NT; ++u) {
+        const int n = 16 * u + ml;
+        b_off[u] = n < C::N ? (n % COUT) * C::GP + (K - 1) - n / COUT + kq : -1;
+    }
+
+    // ---- staging: one input row (CIN x 64 columns) and one g row (COUT x (64+K-1) columns) ----
+    float px[C::CPW], pc[C::CPW];
+    float gq[C::OPW][2][4];
+    float gb_acc[C::OPW], gs_acc[C::OPW];
+#pragma unroll
+    for (int kk = 0; kk < C::OPW; ++kk) gb_acc[kk] = gs_acc[kk] = 0.f;
+
+    auto load_in = [&](int ih) {
+#pragma unroll
+        for (int kk = 0; kk < C::CPW; ++kk) {
+            const int i = w + 4 * kk;
+            px[kk] = pc[kk] = 0.f;
+            if (i < CIN) load_px<MODE>(d, chan_src<MODE>(d, b, i), ih, ow0 - L.PW + lane, px[kk], pc[kk]);
+        }
+    };
+    auto store_in = [&](int ih) {
+        const int slot = ((ih % C::SLOTS) + C::SLOTS) % C::SLOTS;
+#pragma unroll
+        for (int kk = 0; kk < C::CPW; ++kk) {
+            const int i = w + 4 * kk;
+            if (i < CIN) {
+                const float cv = (MODE == NCONV_LOAD_THRESH) ? (px[kk] > L.thresh ? 1.0f : 0.0f) : pc[kk];
+                lds[slot * C::SLOT + i * C::XP + lane] = px[kk] * cv;
+                lds[C::C_OFF + slot * C::SLOT + i * C::XP + lane] = cv;
+            }
+        }
+    };
+    const int plane = L.Ho * L.Wo;
+    auto load_g = [&](int oh) {
+#pragma unroll
+        for (int kk = 0; kk < C::OPW; ++kk) {
+            const int o = w + 4 * kk;
+            const size_t base = ((size_t)b * COUT + o) * plane;
+            const __amdgpu_buffer_rsrc_t rgy = plane_rsrc(a.gy + base, plane * 4);
+            const __amdgpu_buffer_rsrc_t rco = plane_rsrc(a.co + base, plane * 4);
+            const __amdgpu_buffer_rsrc_t ry = plane_rsrc(a.y + base, plane * 4);
+#pragma unroll
+            for (int p = 0; p < 2; ++p) {
+                const int ow = ow0 - (K - 1) + p * 64 + lane;
+                const bool in = (p == 0 || lane < K - 1) && (unsigned)oh < (unsigned)L.Ho &&
+                                (unsigned)ow < (unsigned)L.Wo;
+                const unsigned off = in ? (unsigned)(oh * L.Wo + ow) * 4u : OOB;
+                gq[kk][p][0] = ld_f32(rgy, off);
+                gq[kk][p][1] = ld_f32(rco, off);
+                gq[kk][p][2] = ld_f32(ry, off);
+                gq[kk][p][3] = a.gco ? ld_f32(plane_rsrc(a.gco + base, plane * 4), off) : 0.f;
+            }
+        }
+    };
+    auto store_g = [&](int buf) {
+#pragma unroll
+        for (int kk = 0; kk < C::OPW; ++kk) {
+            const int o = w + 4 * kk;
+            const float bo = L.bias[o], so = L.wsum[o];
+#pragma unroll
+            for (int p = 0; p < 2; ++p) {
+                const int col = p * 64 + lane;
+                if (p == 1 && lane >= K - 1) continue;
+                float gN, gD;
+                nconv_grad_nd(gq[kk][p][0], gq[kk][p][3], gq[kk][p][2], gq[kk][p][1], L.eps, bo, so, gN, gD);
+                float* g = lds + C::G_OFF + buf * C::GBUF + o * C::GP + col;
+                g[0] = gN;
+                g[COUT * C::GP] = gD;
+                if (col >= K - 1) {  // this strip's own columns: the bias / wsum gradient sums
+                    gb_acc[kk] += gq[kk][p][0];
+                    gs_acc[kk] = fmaf(gq[kk][p][3], gq[kk][p][1], gs_acc[kk]);
+                }
+            }
+        }
+    };
+
+    f4acc acc[C::MT][C::NT];
+#pragma unroll
+    for (int t = 0; t < C::MT; ++t)
+#pragma unroll
+        for (int u = 0; u < C::NT; ++u) acc[t][u] = (f4acc){0.f, 0.f, 0.f, 0.f};
+
+    if (r0 < r1) {
+        for (int kh = 0; kh < K - 1; ++kh) {  // prologue: the segment's first K-1 input rows
+            load_in(r0 - L.PH + kh);
+            store_in(r0 - L.PH + kh);
+        }
+        load_in(r0 - L.PH + K - 1);
+        load_g(r0);
+    }
+#pragma unroll 1
+    for (int oh = r0; oh < r1; ++oh) {
+        const int buf = (oh - r0) & 1;
+        store_in(oh - L.PH + K - 1);
+        store_g(buf);
+        __syncthreads();
+        {   // next row's loads in flight during this row's MFMAs (re-reads the last row at the end)
+            const int nx = oh + 1 < r1 ? oh + 1 : oh;
+            load_in(nx - L.PH + K - 1);
+            load_g(nx);
+        }
+        int ax[C::MT], ac[C::MT], bn[C::NT], bd[C::NT];
+#pragma unroll
+        for (int t = 0; t < C::MT; ++t) {
+            const int ih = oh - L.PH + a_kh[t];
+            const int slot = ((ih % C::SLOTS) + C::SLOTS) % C::SLOTS;
+            ax[t] = a_kh[t] < 0 ? C::Z_OFF + kq : slot * C::SLOT + a_ik[t];
+            ac[t] = a_kh[t] < 0 ? C::Z_OFF + kq : C::C_OFF + slot * C::SLOT + a_ik[t];
+        }
+#pragma unroll
+        for (int u = 0; u < C::NT; ++u) {
+            bn[u] = b_off[u] < 0 ? C::Z_OFF + kq : C::G_OFF + buf * C::GBUF + b_off[u];
+            bd[u] = b_off[u] < 0 ? C::Z_OFF + kq : C::G_OFF + buf * C::GBUF + COUT * C::GP + b_off[u];
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const int q0 = 16 * w + 4 * s;
+            float va[C::MT], vb[C::NT];
+#pragma unroll
+            for (int t = 0; t < C::MT; ++t) va[t] = lds[ax[t] + q0];
+#pragma unroll
+            for (int u = 0; u < C::NT; ++u) vb[u] = lds[bn[u] + q0];
+#pragma unroll
+            for (int t = 0; t < C::MT; ++t)
+#pragma unroll
+                for (int u = 0; u < C::NT; ++u)
+                    acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(va[t], vb[u], acc[t][u], 0, 0, 0);
+#pragma unroll
+            for (int t = 0; t < C::MT; ++t) va[t] = lds[ac[t] + q0];
+#pragma unroll
+            for (int u = 0; u < C::NT; ++u) vb[u] = lds[bd[u] + q0];
+#pragma unroll
+            for (int t = 0; t < C::MT; ++t)
+#pragma unroll
+                for (int u = 0; u < C::NT; ++u)
+                    acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(va[t], vb[u], acc[t][u], 0, 0, 0);
+        }
+    }
+
+    // ---- the four waves' tiles summed in a fixed order -> this block's partial row ----
+    constexpr int NW = COUT * CIN * K * K;
+    constexpr int NE = C::MT * C::NT * 256;
+    float* out = part + (size_t)blockIdx.x * (NW + 2 * COUT);
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < C::MT; ++t)
+#pragma unroll
+        for (int u = 0; u < C::NT; ++u)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) lds[w * NE + (t * C::NT + u) * 256 + r * 64 + lane] = acc[t][u][r];
+    __syncthreads();
+    for (int e = tid; e < NE; e += kT) {
+        const float v = ((lds[e] + lds[NE + e]) + lds[2 * NE + e]) + lds[3 * NE + e];
+        const int l = e & 63, r = (e >> 6) & 3, tu = e >> 8;
+        const int u = tu % C::NT, t = tu / C::NT;
+        const int m = 16 * t + (l >> 4) * 4 + r, n = 16 * u + (l & 15);
+        if (m < C::M && n < C::N) {
+            const int kh = m / CIN, i = m % CIN, kw = n / COUT, o = n % COUT;
+            out[((o * CIN + i) * K + kh) * K + kw] = v;
+        }
+    }
+#pragma unroll
+    for (int kk = 0; kk < C::OPW; ++kk) {
+        float sb = gb_acc[kk], ss = gs_acc[kk];
+#pragma unroll
+        for (int sh = 32; sh > 0; sh >>= 1) {
+            sb += __shfl_xor(sb, sh);
+            ss += __shfl_xor(ss, sh);
+        }
+        if (lane == 0) {
+            out[NW + w + 4 * kk] = sb;
+            out[NW + COUT + w + 4 * kk] = ss;
+        }
+    }
+}
+
 // ------------------------------------------------------------------------------------------------
 // Launchers
 // ------------------------------------------------------------------------------------------------
@@ -711,11 +991,35 @@ static size_t wg_blocks(const nconv_layer& L) {
     return nt < kMaxWgBlocks ? nt : kMaxWgBlocks;
 }
 
+// wgrad_mfma grid: 64-wide q strips (q = ow + kw spans Wo + K - 1 columns) x row segments x images,
+// about kMfmaBlocks workgroups.
+constexpr int kMfmaBlocks = 2048;
+struct WmGrid {
+    int nstrip, nseg, seg_rows;
+    size_t nblk;
+};
+static WmGrid wm_grid(const nconv_layer& L) {
+    WmGrid g;
+    g.nstrip = (L.Wo + L.KW - 1 + 63) / 64;
+    const int per_img = g.nstrip * L.B;
+    int nseg = (kMfmaBlocks + per_img - 1) / per_img;
+    nseg = nseg < 1 ? 1 : (nseg > L.Ho ? L.Ho : nseg);
+    g.seg_rows = (L.Ho + nseg - 1) / nseg;
+    if (g.seg_rows < 1) g.seg_rows = 1;
+    g.nseg = (L.Ho + g.seg_rows - 1) / g.seg_rows;
+    if (g.nseg < 1) g.nseg = 1;
+    g.nblk = (size_t)g.nstrip * g.nseg * L.B;
+    return g;
+}
+static bool wgrad_on_mfma(const nconv_layer& L) { return L.KH > 1; }  // tiled 3x3 / 5x5 layers
+
 size_t bwd_workspace_bytes(const LayerDev& d) {
     const nconv_layer& L = d.L;
     const int fan = (L.Cin / L.groups) * L.KH * L.KW;
     const size_t stride = (size_t)L.Cout * fan + 2 * L.Cout;
-    const size_t nblk = pick_path(L) == kTiled ? wg_blocks(L) : (size_t)generic_chunks(L);
+    const Path path = pick_path(L);
+    const size_t nblk = path == kTiled ? (wgrad_on_mfma(L) ? wm_grid(L).nblk : wg_blocks(L))
+                                       : (size_t)generic_chunks(L);
     size_t bytes = (nblk + 1) * stride * sizeof(float);  // partial rows + the reduced row
     bytes = (bytes + 255) & ~(size_t)255;
     if (L.load_mode == NCONV_LOAD_UPCAT_SKIP_FIRST || L.load_mode == NCONV_LOAD_UPCAT_UP_FIRST)
@@ -732,7 +1036,16 @@ static void go_bwd_tiled(const LayerDev& d, const BwdArgs& a, float* part, float
         dim3 g(((L.W + D::TW - 1) / D::TW) * ((L.H + D::TH - 1) / D::TH) * L.B);  // see xcd_tile
         hipLaunchKernelGGL((dgrad_tiled<CIN, COUT, K, MODE>), g, dim3(kT), 0, st, d, a, tx, tc);
     }
-    if (a.gw || a.gb) {
+    if constexpr (K > 1) {
+        if (a.gw || a.gb) {
+            const WmGrid g = wm_grid(L);
+            hipLaunchKernelGGL((wgrad_mfma<CIN, COUT, K, MODE>), dim3(g.nblk), dim3(kT), 0, st, d, a, part,
+                               g.nstrip, g.nseg, g.seg_rows);
+            const int nw = COUT * CIN * K * K;
+            launch_wgrad_reduce(part, (int)g.nblk, nw, COUT, CIN * K * K, L.wsum, a.gw, a.gb,
+                                part + g.nblk * (nw + 2 * COUT), st);
+        }
+    } else if (a.gw || a.gb) {
         using W = WgCfg<CIN, COUT, K>;
         const int ntw = (L.Wo + W::TW - 1) / W::TW, nth = (L.Ho + W::TH - 1) / W::TH;
         const int nblk = (int)wg_blocks(L);
@@ -777,7 +1090,8 @@ int launch_bwd(const LayerDev& d, const BwdArgs& a, hipStream_t st, const char**
     const int fan = (L.Cin / L.groups) * L.KH * L.KW;
     const size_t stride = (size_t)L.Cout * fan + 2 * L.Cout;
     const Path path = pick_path(L);
-    const size_t nblk = path == kTiled ? wg_blocks(L) : (size_t)generic_chunks(L);
+    const size_t nblk = path == kTiled ? (wgrad_on_mfma(L) ? wm_grid(L).nblk : wg_blocks(L))
+                                       : (size_t)generic_chunks(L);
     float* part = a.ws;
     float* tx = a.ws + ((((nblk + 1) * stride * sizeof(float)) + 255) & ~(size_t)255) / sizeof(float);
     float* tc = tx + (size_t)L.B * L.b.C * L.H * L.W;
