@@ -46,6 +46,7 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--graph", type=int, default=1, help="capture the forward in a hipGraph (1) or run eager (0)")
     p.add_argument("--streams", type=int, default=2, help="HIP streams the inference batch is split over")
+    p.add_argument("--train-graph", type=int, default=1, help="replay the training step from a hipGraph (1) or eager (0)")
     return p.parse_args()
 
 
@@ -216,22 +217,30 @@ def guided_forward(m, dev, B, H, W, steps, warmup, rank):
     return el
 
 
-def make_train_step(m, dev, B, H, W, world, rank):
+def make_train_step(m, dev, B, H, W, world, rank, graph=True):
     """One step-1 training iteration as train_step1.py:59-65: train-mode forward (EnforcePos
     drift), calculate_loss on element [0] with the gradient loss, backward, (RCCL gradient
-    all-reduce when world > 1), AdamW lr 1e-2 / wd 1e-7 (train_step1.py:16-17, utils.py:55)."""
+    all-reduce when world > 1), AdamW lr 1e-2 / wd 1e-7 (train_step1.py:16-17, utils.py:55).
+    graph=True replays the whole iteration from a hipGraph (m.train.GraphedTrainStep)."""
     torch.manual_seed(0)
     net = m.dp.DataParallelRCCL(m.SETP1_NCONV(crop="generalized").to(dev))
-    opt = m.train.get_optimizer(net, "adam", 1e-2, 1e-7)
+    opt = m.train.get_optimizer(net, "adam", 1e-2, 1e-7, capturable=graph)
     g = torch.Generator().manual_seed(2000 + rank)
     S = sparse_depth(g, B, H, W, dev)
     gt = sparse_depth(g, B, H, W, dev)
     net.train()
 
+    def loss_fn(model, S, gt):
+        est = model(S)
+        return m.train.calculate_loss(est[0, :, :, :], gt[0, :, :, :], True)
+
+    if graph:
+        gstep = m.train.GraphedTrainStep(net, opt, loss_fn, (S, gt))
+        return lambda: gstep()
+
     def step():
         opt.zero_grad()
-        est = net(S)
-        loss = m.train.calculate_loss(est[0, :, :, :], gt[0, :, :, :], True)
+        loss = loss_fn(net, S, gt)
         loss.backward()
         net.allreduce_grads()
         opt.step()
@@ -305,7 +314,7 @@ def main():
     # ---- fwd + bwd + AdamW (config 4b) ----
     train = None
     if not a.no_train:
-        step = make_train_step(m, dev, B, H, W, world, rank)
+        step = make_train_step(m, dev, B, H, W, world, rank, graph=bool(a.train_graph))
         ks = a.train_steps or a.steps
         for _ in range(max(a.warmup, 1)):
             step()
@@ -322,7 +331,8 @@ def main():
             t = torch.tensor([tt], device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             tt = t.item()
-        train = {"frames_per_sec": world * B * ks / tt, "ms_per_step": tt / ks * 1e3, "steps": ks}
+        train = {"frames_per_sec": round(world * B * ks / tt, 2), "ms_per_step": round(tt / ks * 1e3, 4), "steps": ks,
+                 "hipgraph": bool(a.train_graph)}
 
     # ---- config 3: guided forward ----
     guided = None

@@ -105,51 +105,75 @@ __device__ __forceinline__ void pool_zero_leftovers(const LayerDev& d, const Bwd
     if (oddh && oddw) z(L.a.H - 1, L.a.W - 1);
 }
 
-// Stage one output-side plane {gN, gD} (channel o) over an OHT x OWT halo (origin oh0, ow0):
-// lanes -> columns, waves -> rows; all loads issued before use (clamped), zero outside.
+// Staging of output-side planes {gN, gD} over an OHT x OWT halo tile (origin oh0, ow0) for the
+// dgrad: the element map (LDS slot, byte offset in an output plane, or past-the-end for the zero
+// padding) is computed once per workgroup; per output channel the four saved planes (gy, gcout,
+// y, cout) are read with buffer loads and {gN, gD} are formed at store time. Elements are dealt
+// to the 256 threads row-major; slots past the tile go to a dump slot after the plane.
 template <int OHT, int OWT, int OWP>
-__device__ __forceinline__ void stage_gplane(const LayerDev& d, const BwdArgs& a, int b, int o, f2* t, int oh0,
-                                             int ow0, int tid) {
-    static_assert(OWT >= 64, "lanes map to columns");
-    constexpr int NR = (OHT + 3) / 4;
-    const nconv_layer& L = d.L;
-    const size_t off = ((size_t)b * L.Cout + o) * (size_t)L.Ho * L.Wo;
-    const float *gy = a.gy + off, *y = a.y + off, *co = a.co + off;
-    const float* gco = a.gco ? a.gco + off : nullptr;
-    const float bo = L.bias[o], so = L.wsum[o];
-    auto elem = [&](int r, int col, bool valid) {
-        const int oh = oh0 + r, ow = ow0 + col;
-        const bool ok = valid && (unsigned)oh < (unsigned)L.Ho && (unsigned)ow < (unsigned)L.Wo;
-        const int ohc = oh < 0 ? 0 : (oh >= L.Ho ? L.Ho - 1 : oh);
-        const int owc = ow < 0 ? 0 : (ow >= L.Wo ? L.Wo - 1 : ow);
-        const int i = ohc * L.Wo + owc;
-        float gN, gD;
-        nconv_grad_nd(gy[i], gco ? gco[i] : 0.f, y[i], co[i], L.eps, bo, so, gN, gD);
-        return ok ? (f2){gN, gD} : (f2){0.f, 0.f};
-    };
-    const int col = tid & 63, r0 = tid >> 6;
-    f2 v[NR];
+struct GTileStager {
+    static constexpr int NT = OHT * OWT;
+    static constexpr int NE = (NT + 255) / 256;
+    static constexpr int PLANE = OHT * OWP;
+    static constexpr int PLANE_STRIDE = PLANE + 2;
+    static constexpr unsigned OOB = 0x80000000u;
+    unsigned lofs[NE];
+    unsigned go[NE];
+
+    __device__ __forceinline__ void init(const nconv_layer& L, int oh0, int ow0, int tid) {
 #pragma unroll
-    for (int k = 0; k < NR; ++k) v[k] = elem(r0 + 4 * k, col, true);
-#pragma unroll
-    for (int k = 0; k < NR; ++k) t[(r0 + 4 * k) * OWP + col] = v[k];
-    if constexpr (OWT > 64) {
-        constexpr int EX = OWT - 64;
-        static_assert(EX * OHT <= 256, "one pass for the extra halo columns");
-        const int r = tid / EX, cx = 64 + tid % EX;
-        const f2 g = elem(r, cx, tid < EX * OHT);
-        if (tid < EX * OHT) t[r * OWP + cx] = g;
+        for (int k = 0; k < NE; ++k) {
+            const int e = tid + 256 * k;
+            const int r = e / OWT, col = e - r * OWT;
+            const int oh = oh0 + r, ow = ow0 + col;
+            const bool in = e < NT && (unsigned)oh < (unsigned)L.Ho && (unsigned)ow < (unsigned)L.Wo;
+            lofs[k] = e < NT ? r * OWP + col : PLANE;
+            go[k] = in ? (unsigned)(oh * L.Wo + ow) * 4u : OOB;
+        }
     }
-}
+
+    // raw (gy, gcout, y, cout) of output channel o of image b, no wait
+    __device__ __forceinline__ void load(const nconv_layer& L, const BwdArgs& a, int b, int o,
+                                         float (&v)[4][NE]) const {
+        const int plane = L.Ho * L.Wo;
+        const size_t base = ((size_t)b * L.Cout + o) * plane;
+        const __amdgpu_buffer_rsrc_t rgy = plane_rsrc(a.gy + base, plane * 4);
+        const __amdgpu_buffer_rsrc_t ry = plane_rsrc(a.y + base, plane * 4);
+        const __amdgpu_buffer_rsrc_t rco = plane_rsrc(a.co + base, plane * 4);
+#pragma unroll
+        for (int k = 0; k < NE; ++k) {
+            v[0][k] = ld_f32(rgy, go[k]);
+            v[2][k] = ld_f32(ry, go[k]);
+            v[3][k] = ld_f32(rco, go[k]);
+        }
+        if (a.gco) {
+            const __amdgpu_buffer_rsrc_t rgc = plane_rsrc(a.gco + base, plane * 4);
+#pragma unroll
+            for (int k = 0; k < NE; ++k) v[1][k] = ld_f32(rgc, go[k]);
+        } else {
+#pragma unroll
+            for (int k = 0; k < NE; ++k) v[1][k] = 0.f;
+        }
+    }
+
+    __device__ __forceinline__ void store(const nconv_layer& L, int o, const float (&v)[4][NE], f2* t) const {
+        const float bo = L.bias[o], so = L.wsum[o];
+#pragma unroll
+        for (int k = 0; k < NE; ++k) {
+            float gN, gD;  // zero padding: gy = gcout = y = cout = 0 gives gN = gD = 0
+            nconv_grad_nd(v[0][k], v[1][k], v[2][k], v[3][k], L.eps, bo, so, gN, gD);
+            t[lofs[k]] = (f2){gN, gD};
+        }
+    }
+};
 
 // ---- dgrad: tiled, stride 1 ------------------------------------------------------------------------
 template <int CIN, int K>
 struct DgCfg {
-    static constexpr int P = (CIN >= 16) ? 2 : 4;
-    static constexpr int TW = 64, TPR = TW / P, TH = kT / TPR;
+    static constexpr int P = 2;  // input pixels per thread (f2 epilogue: any even width stays vectorized)
+    static constexpr int TPR = 16, TW = TPR * P, TH = kT / TPR;
     static constexpr int OHT = TH + K - 1, OWT = TW + K - 1;
-    static constexpr int OWP = (OWT + 1) & ~1;
-    static constexpr int PLANE = ((OHT + 3) / 4 * 4) * OWP;  // stage_gplane writes whole 4-row groups
+    static constexpr int OWP = (OWT + 1) & ~1;  // even pitch: 16-B aligned window reads
     static constexpr int NV = P + K - 1;
 };
 
@@ -160,12 +184,15 @@ struct VecOf<4> { typedef f4 T; };
 template <>
 struct VecOf<2> { typedef f2 T; };
 
+// One (output channel o, kernel row kh) step per iteration of the inner loop, not unrolled: its
+// Cin*K weights ride SGPRs. The {gN, gD} planes of the output channels are staged one at a time
+// into two LDS buffers, the loads two channels ahead (as the forward's input planes).
 template <int CIN, int COUT, int K, int MODE>
 __global__ __launch_bounds__(kT) void dgrad_tiled(LayerDev d, BwdArgs a, float* tmp_x, float* tmp_c) {
     using C = DgCfg<CIN, K>;
+    using GS = GTileStager<C::OHT, C::OWT, C::OWP>;
     constexpr int P = C::P;
-    constexpr int OC = pick_chunk(COUT, C::PLANE, 24 * 1024);
-    __shared__ __attribute__((aligned(16))) f2 tile[OC * C::PLANE];
+    __shared__ __attribute__((aligned(16))) f2 tile[2 * GS::PLANE_STRIDE];
     const nconv_layer& L = d.L;
     const float* __restrict__ wgt = L.weight;
     const TileCoord tcd = xcd_tile((L.W + C::TW - 1) / C::TW, (L.H + C::TH - 1) / C::TH, L.B);
@@ -180,20 +207,11 @@ __global__ __launch_bounds__(kT) void dgrad_tiled(LayerDev d, BwdArgs a, float* 
 #pragma unroll
         for (int j = 0; j < P; ++j) acc[i][j] = (f2){0.f, 0.f};
 
-    for (int o0 = 0; o0 < COUT; o0 += OC) {
-        if (o0) __syncthreads();
-        for (int oc = 0; oc < OC; ++oc)
-            stage_gplane<C::OHT, C::OWT, C::OWP>(d, a, b, o0 + oc, tile + oc * C::PLANE, oh0, ow0, tid);
-        __syncthreads();
-        // one (output channel, kernel row) per iteration, not unrolled: its Cin*K weights go to SGPRs
-        const f2* row = &tile[(ty + K - 1) * C::OWP + tx];
-        const float* wr = wgt + (size_t)o0 * CIN * K * K;
+    auto fma_plane = [&](int o, int bufi) {
+        const f2* row = &tile[bufi * GS::PLANE_STRIDE + (ty + K - 1) * C::OWP + tx];
+        const float* wr = wgt + (size_t)o * CIN * K * K;
 #pragma unroll 1
-        for (int q = 0; q < OC * K; ++q, row -= C::OWP, wr += K) {
-            if (q && q % K == 0) {
-                row += C::PLANE + K * C::OWP;
-                wr += CIN * K * K - K * K;
-            }
+        for (int kh = 0; kh < K; ++kh, row -= C::OWP, wr += K) {
             f2 v[C::NV];
 #pragma unroll
             for (int m = 0; m < C::NV / 2; ++m) {
@@ -212,6 +230,25 @@ __global__ __launch_bounds__(kT) void dgrad_tiled(LayerDev d, BwdArgs a, float* 
                     for (int j = 0; j < P; ++j)
                         acc[i][j] = __builtin_elementwise_fma(w2, v[j + K - 1 - kw], acc[i][j]);
                 }
+        }
+    };
+
+    GS gs;
+    gs.init(L, oh0, ow0, tid);
+    float va[4][GS::NE], vb[4][GS::NE];
+    gs.load(L, a, b, 0, va);
+    if (COUT > 1) gs.load(L, a, b, 1, vb);
+#pragma unroll 1
+    for (int o = 0; o < COUT; o += 2) {
+        gs.store(L, o, va, tile);
+        __syncthreads();
+        gs.load(L, a, b, o + 2 < COUT ? o + 2 : COUT - 1, va);  // unconditional (see fwd_tiled)
+        fma_plane(o, 0);
+        if (o + 1 < COUT) {
+            gs.store(L, o + 1, vb, tile + GS::PLANE_STRIDE);
+            __syncthreads();
+            gs.load(L, a, b, o + 3 < COUT ? o + 3 : COUT - 1, vb);
+            fma_plane(o + 1, 1);
         }
     }
 
@@ -620,49 +657,66 @@ __global__ __launch_bounds__(kT) void wgrad_generic(LayerDev d, BwdArgs a, float
 }
 
 // ---- wgrad: fixed-order reduction of the per-block partials ----------------------------------------
-// Stage 1: tot[e] = sum_k part[k][e] for every entry e of a partial row (weights, sum gy, sum
-// gco*cout). A 256-thread block owns 64 consecutive entries; its 4 waves sum interleaved subsets of
-// the partial rows (coalesced 256-B rows, 8 independent loads in flight per lane) and combine the
-// 4 subtotals in LDS in a fixed order — deterministic, no atomics.
-__global__ __launch_bounds__(kT) void wgrad_reduce_sum(const float* part, int nblk, int stride, float* tot) {
+// Stage 1: sub[y][e] = sum of part[k][e] over the y-th of kReduceSplit contiguous slices of the
+// partial rows, for every entry e of a row (weights, sum gy, sum gco*cout). A 256-thread block owns
+// 64 consecutive entries of one slice; its 4 waves sum interleaved rows (coalesced 256-B rows,
+// 8 independent loads in flight per lane) and combine the 4 subtotals in LDS in a fixed order.
+// Stage 2 (wgrad_finish) adds the kReduceSplit slice sums in order — deterministic, no atomics.
+constexpr int kReduceSplit = 16;
+
+__global__ __launch_bounds__(kT) void wgrad_reduce_sum(const float* part, int nblk, int stride, float* sub) {
     __shared__ float red[kT];
     const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
     const int e = blockIdx.x * 64 + lane;
+    const int per = (nblk + kReduceSplit - 1) / kReduceSplit;
+    const int k0 = blockIdx.y * per, k1 = min(nblk, k0 + per);
     float s = 0.f;
     if (e < stride) {
-        int k = grp;
-        for (; k + 28 < nblk; k += 32) {
+        int k = k0 + grp;
+        for (; k + 28 < k1; k += 32) {
             float v[8];
 #pragma unroll
             for (int u = 0; u < 8; ++u) v[u] = part[(size_t)(k + 4 * u) * stride + e];
 #pragma unroll
             for (int u = 0; u < 8; ++u) s += v[u];
         }
-        for (; k < nblk; k += 4) s += part[(size_t)k * stride + e];
+        for (; k < k1; k += 4) s += part[(size_t)k * stride + e];
     }
     red[threadIdx.x] = s;
     __syncthreads();
-    if (grp == 0 && e < stride) tot[e] = ((red[lane] + red[64 + lane]) + red[128 + lane]) + red[192 + lane];
+    if (grp == 0 && e < stride)
+        sub[(size_t)blockIdx.y * stride + e] = ((red[lane] + red[64 + lane]) + red[128 + lane]) + red[192 + lane];
 }
 
-// Stage 2: gW[w] = tot[w] + gs[o(w)] with gs = -(sum gco*cout)/s (d cout / d s, cout = D/s), gb = sum gy.
-__global__ __launch_bounds__(kT) void wgrad_finish(const float* tot, int nw, int cout, int fan, const float* wsum,
+// Stage 2: tot = sum of the slice sums; gW[w] = tot[w] + gs[o(w)] with gs = -(sum gco*cout)/s
+// (d cout / d s, cout = D/s), gb = sum gy.
+__device__ __forceinline__ float slice_total(const float* sub, int stride, int e) {
+    float t = 0.f;
+#pragma unroll
+    for (int y = 0; y < kReduceSplit; ++y) t += sub[(size_t)y * stride + e];
+    return t;
+}
+
+__global__ __launch_bounds__(kT) void wgrad_finish(const float* sub, int nw, int cout, int fan, const float* wsum,
                                                    float* gw, float* gb) {
+    const int stride = nw + 2 * cout;
     for (int w = blockIdx.x * kT + threadIdx.x; w < nw + cout; w += gridDim.x * kT) {
         if (w < nw) {
             const int o = w / fan;
-            if (gw) gw[w] = tot[w] + (-tot[nw + cout + o] / wsum[o]);
+            if (gw) gw[w] = slice_total(sub, stride, w) + (-slice_total(sub, stride, nw + cout + o) / wsum[o]);
         } else if (gb) {
-            gb[w - nw] = tot[w];
+            gb[w - nw] = slice_total(sub, stride, w);
         }
     }
 }
 
+// part: nblk partial rows followed by kReduceSplit rows of slice sums (see bwd_workspace_bytes)
 static void launch_wgrad_reduce(const float* part, int nblk, int nw, int cout, int fan, const float* wsum,
-                                float* gw, float* gb, float* tot, hipStream_t st) {
+                                float* gw, float* gb, float* sub, hipStream_t st) {
     const int stride = nw + 2 * cout;
-    hipLaunchKernelGGL(wgrad_reduce_sum, dim3((stride + 63) / 64), dim3(kT), 0, st, part, nblk, stride, tot);
-    hipLaunchKernelGGL(wgrad_finish, dim3((nw + cout + kT - 1) / kT), dim3(kT), 0, st, tot, nw, cout, fan, wsum,
+    hipLaunchKernelGGL(wgrad_reduce_sum, dim3((stride + 63) / 64, kReduceSplit), dim3(kT), 0, st, part, nblk,
+                       stride, sub);
+    hipLaunchKernelGGL(wgrad_finish, dim3((nw + cout + kT - 1) / kT), dim3(kT), 0, st, sub, nw, cout, fan, wsum,
                        gw, gb);
 }
 
@@ -697,11 +751,15 @@ struct WmCfg {
     static constexpr int GP = 72;          // == 8 (mod 64): the 8 channels of a B tile 8 banks apart
     static_assert(GW <= GP, "g row pitch");
     static_assert(COUT % 4 == 0, "g rows are staged four output channels per pass");
-    static constexpr int C_OFF = SLOTS * SLOT;
-    static constexpr int G_OFF = 2 * SLOTS * SLOT;  // [buf][part][o][GP]
-    static constexpr int GBUF = 2 * COUT * GP;
-    static constexpr int Z_OFF = G_OFF + 2 * GBUF;  // a zero row for padded M / N lanes
-    static constexpr int STAGE = Z_OFF + GP;
+    // LDS (floats): xc ring + its zero row | c ring + its zero row | g [buf][part][COUT + 1 rows][GP]
+    // (row COUT of each g part is zero). Padded M / N lanes read the zero rows, whose offsets from
+    // the xc / gN data equal the c / gD part offsets, so one address per operand serves both parts.
+    static constexpr int XR = SLOTS * SLOT;             // the zero row of the xc ring
+    static constexpr int C_OFF = XR + GP;               // c ring (its zero row at C_OFF + XR)
+    static constexpr int G_OFF = 2 * C_OFF;
+    static constexpr int GPART = (COUT + 1) * GP;       // one part of one g buffer
+    static constexpr int GBUF = 2 * GPART;
+    static constexpr int STAGE = G_OFF + 2 * GBUF;
     static constexpr int RED = 4 * MT * NT * 256;
     static constexpr int LDS = STAGE > RED ? STAGE : RED;
     static constexpr int CPW = (CIN + 3) / 4, OPW = COUT / 4;  // channels staged per wave
@@ -743,13 +801,18 @@ __device__ __forceinline__ void load_px(const LayerDev& d, const ChanSrc& s, int
     }
 }
 
+#ifndef NCONV_WM_WAVES
+#define NCONV_WM_WAVES 3
+#endif
+#define NCONV_WM_ATTR __attribute__((amdgpu_waves_per_eu(NCONV_WM_WAVES, 8)))
 template <int CIN, int COUT, int K, int MODE>
-__global__ __launch_bounds__(kT) void wgrad_mfma(LayerDev d, BwdArgs a, float* part, int nstrip, int nseg,
+__global__ __launch_bounds__(kT) NCONV_WM_ATTR void wgrad_mfma(LayerDev d, BwdArgs a, float* part, int nstrip, int nseg,
                                                  int seg_rows) {
     using C = WmCfg<CIN, COUT, K>;
     __shared__ __attribute__((aligned(16))) float lds[C::LDS];
     const nconv_layer& L = d.L;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: channel sources stay in SGPRs
     int blk = blockIdx.x;
     const int strip = blk % nstrip;
     blk /= nstrip;
@@ -758,7 +821,12 @@ __global__ __launch_bounds__(kT) void wgrad_mfma(LayerDev d, BwdArgs a, float* p
     const int r0 = seg * seg_rows, r1 = min(L.Ho, r0 + seg_rows);
     constexpr unsigned OOB = 0x80000000u;
 
-    for (int e = tid; e < C::GP; e += kT) lds[C::Z_OFF + e] = 0.f;
+    for (int e = tid; e < C::GP; e += kT) {
+        lds[C::XR + e] = 0.f;
+        lds[C::C_OFF + C::XR + e] = 0.f;
+#pragma unroll
+        for (int z = 0; z < 4; ++z) lds[C::G_OFF + z * C::GPART + COUT * C::GP + e] = 0.f;
+    }
 
     // per-lane MFMA operand coordinates (A[m = lane&15][k = lane>>4], B[k = lane>>4][n = lane&15])
     const int kq = lane >> 4, ml = lane & 15;
@@ -772,7 +840,7 @@ __global__ __launch_bounds__(kT) void wgrad_mfma(LayerDev d, BwdArgs a, float* p
 #pragma unroll
     for (int u = 0; u < C::NT; ++u) {
         const int n = 16 * u + ml;
-        b_off[u] = n < C::N ? (n % COUT) * C::GP + (K - 1) - n / COUT + kq : -1;
+        b_off[u] = n < C::N ? (n % COUT) * C::GP + (K - 1) - n / COUT + kq : COUT * C::GP + kq;
     }
 
     // ---- staging: one input row (CIN x 64 columns) and one g row (COUT x (64+K-1) columns) ----
@@ -837,7 +905,7 @@ __global__ __launch_bounds__(kT) void wgrad_mfma(LayerDev d, BwdArgs a, float* p
                 nconv_grad_nd(gq[kk][p][0], gq[kk][p][3], gq[kk][p][2], gq[kk][p][1], L.eps, bo, so, gN, gD);
                 float* g = lds + C::G_OFF + buf * C::GBUF + o * C::GP + col;
                 g[0] = gN;
-                g[COUT * C::GP] = gD;
+                g[C::GPART] = gD;
                 if (col >= K - 1) {  // this strip's own columns: the bias / wsum gradient sums
                     gb_acc[kk] += gq[kk][p][0];
                     gs_acc[kk] = fmaf(gq[kk][p][3], gq[kk][p][1], gs_acc[kk]);
@@ -871,41 +939,31 @@ __global__ __launch_bounds__(kT) void wgrad_mfma(LayerDev d, BwdArgs a, float* p
             load_in(nx - L.PH + K - 1);
             load_g(nx);
         }
-        int ax[C::MT], ac[C::MT], bn[C::NT], bd[C::NT];
+        int ax[C::MT], bn[C::NT];
 #pragma unroll
         for (int t = 0; t < C::MT; ++t) {
             const int ih = oh - L.PH + a_kh[t];
             const int slot = ((ih % C::SLOTS) + C::SLOTS) % C::SLOTS;
-            ax[t] = a_kh[t] < 0 ? C::Z_OFF + kq : slot * C::SLOT + a_ik[t];
-            ac[t] = a_kh[t] < 0 ? C::Z_OFF + kq : C::C_OFF + slot * C::SLOT + a_ik[t];
+            ax[t] = a_kh[t] < 0 ? C::XR + kq : slot * C::SLOT + a_ik[t];
         }
 #pragma unroll
-        for (int u = 0; u < C::NT; ++u) {
-            bn[u] = b_off[u] < 0 ? C::Z_OFF + kq : C::G_OFF + buf * C::GBUF + b_off[u];
-            bd[u] = b_off[u] < 0 ? C::Z_OFF + kq : C::G_OFF + buf * C::GBUF + COUT * C::GP + b_off[u];
-        }
+        for (int u = 0; u < C::NT; ++u) bn[u] = C::G_OFF + buf * C::GBUF + b_off[u];
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
             const int q0 = 16 * w + 4 * s;
-            float va[C::MT], vb[C::NT];
 #pragma unroll
-            for (int t = 0; t < C::MT; ++t) va[t] = lds[ax[t] + q0];
+            for (int part = 0; part < 2; ++part) {  // {x*c, gN} then {c, gD}
+                float va[C::MT], vb[C::NT];
 #pragma unroll
-            for (int u = 0; u < C::NT; ++u) vb[u] = lds[bn[u] + q0];
+                for (int t = 0; t < C::MT; ++t) va[t] = lds[ax[t] + part * C::C_OFF + q0];
 #pragma unroll
-            for (int t = 0; t < C::MT; ++t)
+                for (int u = 0; u < C::NT; ++u) vb[u] = lds[bn[u] + part * C::GPART + q0];
 #pragma unroll
-                for (int u = 0; u < C::NT; ++u)
-                    acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(va[t], vb[u], acc[t][u], 0, 0, 0);
+                for (int t = 0; t < C::MT; ++t)
 #pragma unroll
-            for (int t = 0; t < C::MT; ++t) va[t] = lds[ac[t] + q0];
-#pragma unroll
-            for (int u = 0; u < C::NT; ++u) vb[u] = lds[bd[u] + q0];
-#pragma unroll
-            for (int t = 0; t < C::MT; ++t)
-#pragma unroll
-                for (int u = 0; u < C::NT; ++u)
-                    acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(va[t], vb[u], acc[t][u], 0, 0, 0);
+                    for (int u = 0; u < C::NT; ++u)
+                        acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(va[t], vb[u], acc[t][u], 0, 0, 0);
+            }
         }
     }
 
@@ -1011,7 +1069,9 @@ static WmGrid wm_grid(const nconv_layer& L) {
     g.nblk = (size_t)g.nstrip * g.nseg * L.B;
     return g;
 }
-static bool wgrad_on_mfma(const nconv_layer& L) { return L.KH > 1; }  // tiled 3x3 / 5x5 layers
+// tiled 3x3 / 5x5 layers with several input channels (Cin = 1 has a single-row A tile and stays
+// on wgrad_tiled, which reads each g plane once per 4 x 64 tile instead of once per row segment)
+static bool wgrad_on_mfma(const nconv_layer& L) { return L.KH > 1 && L.Cin > 1; }
 
 size_t bwd_workspace_bytes(const LayerDev& d) {
     const nconv_layer& L = d.L;
@@ -1020,7 +1080,7 @@ size_t bwd_workspace_bytes(const LayerDev& d) {
     const Path path = pick_path(L);
     const size_t nblk = path == kTiled ? (wgrad_on_mfma(L) ? wm_grid(L).nblk : wg_blocks(L))
                                        : (size_t)generic_chunks(L);
-    size_t bytes = (nblk + 1) * stride * sizeof(float);  // partial rows + the reduced row
+    size_t bytes = (nblk + kReduceSplit) * stride * sizeof(float);  // partial rows + slice sums
     bytes = (bytes + 255) & ~(size_t)255;
     if (L.load_mode == NCONV_LOAD_UPCAT_SKIP_FIRST || L.load_mode == NCONV_LOAD_UPCAT_UP_FIRST)
         bytes += 2 * (size_t)L.B * L.b.C * L.H * L.W * sizeof(float);
@@ -1036,7 +1096,7 @@ static void go_bwd_tiled(const LayerDev& d, const BwdArgs& a, float* part, float
         dim3 g(((L.W + D::TW - 1) / D::TW) * ((L.H + D::TH - 1) / D::TH) * L.B);  // see xcd_tile
         hipLaunchKernelGGL((dgrad_tiled<CIN, COUT, K, MODE>), g, dim3(kT), 0, st, d, a, tx, tc);
     }
-    if constexpr (K > 1) {
+    if constexpr (K > 1 && CIN > 1) {
         if (a.gw || a.gb) {
             const WmGrid g = wm_grid(L);
             hipLaunchKernelGGL((wgrad_mfma<CIN, COUT, K, MODE>), dim3(g.nblk), dim3(kT), 0, st, d, a, part,
@@ -1093,7 +1153,7 @@ int launch_bwd(const LayerDev& d, const BwdArgs& a, hipStream_t st, const char**
     const size_t nblk = path == kTiled ? (wgrad_on_mfma(L) ? wm_grid(L).nblk : wg_blocks(L))
                                        : (size_t)generic_chunks(L);
     float* part = a.ws;
-    float* tx = a.ws + ((((nblk + 1) * stride * sizeof(float)) + 255) & ~(size_t)255) / sizeof(float);
+    float* tx = a.ws + ((((nblk + kReduceSplit) * stride * sizeof(float)) + 255) & ~(size_t)255) / sizeof(float);
     float* tc = tx + (size_t)L.B * L.b.C * L.H * L.W;
     const bool up = L.load_mode == NCONV_LOAD_UPCAT_SKIP_FIRST || L.load_mode == NCONV_LOAD_UPCAT_UP_FIRST;
 

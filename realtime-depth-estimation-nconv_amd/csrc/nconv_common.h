@@ -131,13 +131,20 @@ __device__ __forceinline__ void nconv_epilogue(float N, float D, float eps, floa
 }
 
 // Closed-form gradient of the epilogue w.r.t. N and D, from the saved outputs.
+// Reciprocal-based like nconv_epilogue (<= 2 ulp from IEEE division; -DNCONV_IEEE_DIV restores it).
 __device__ __forceinline__ void nconv_grad_nd(float gy, float gco, float y, float co, float eps,
                                               float bias, float s, float& gN, float& gD) {
     const float D = co * s;
     const float den = D + eps;
     const float r = y - bias;  // = N / (D + eps)
+#ifdef NCONV_IEEE_DIV
     gN = gy / den;
     gD = -(gy * r) / den + gco / s;
+#else
+    const float rd = __builtin_amdgcn_rcpf(den);
+    gN = gy * rd;
+    gD = fmaf(-(gy * r), rd, gco * __builtin_amdgcn_rcpf(s));
+#endif
 }
 
 // ------------------------------------------------------------------------------------------------

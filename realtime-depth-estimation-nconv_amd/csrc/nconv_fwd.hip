@@ -15,8 +15,6 @@
 // step1.py:53-90) evaluated while staging, so glued tensors never hit HBM.
 #include "nconv_internal.h"
 
-#include <stdlib.h>
-
 namespace nconv {
 
 constexpr int kThreads = 256;
@@ -347,24 +345,12 @@ static void go_tiled_p(const LayerDev& d, float* y, float* yc, const TailArgs& t
     hipLaunchKernelGGL((fwd_tiled<CIN, COUT, K, MODE, TAIL, P>), grid, dim3(kThreads), 0, st, d, y, yc, t);
 }
 
-// Pixels per thread of a tiled launch (NCONV_FWD_P overrides, for tuning).
-static int fwd_pixels(int K) {
-    static int env = [] {
-        const char* e = getenv("NCONV_FWD_P");
-        return e ? atoi(e) : 0;
-    }();
-    if (K == 1) return 4;
-    return (env == 1 || env == 2 || env == 4) ? env : 2;
-}
-
+// 2 pixels per thread: 32 x 16 tiles (measured against P = 1 and P = 4: 4 pixels needs 105-125
+// VGPRs, 4 waves/SIMD; 1 pixel doubles the LDS reads per FMA)
 template <int CIN, int COUT, int K, int MODE, bool TAIL>
 static void go_tiled(const LayerDev& d, float* y, float* yc, const TailArgs& t, int gh, int gw,
                      hipStream_t st) {
-    switch (fwd_pixels(K)) {
-        case 1: go_tiled_p<CIN, COUT, K, MODE, TAIL, 1>(d, y, yc, t, gh, gw, st); break;
-        case 4: go_tiled_p<CIN, COUT, K, MODE, TAIL, 4>(d, y, yc, t, gh, gw, st); break;
-        default: go_tiled_p<CIN, COUT, K, MODE, TAIL, 2>(d, y, yc, t, gh, gw, st); break;
-    }
+    go_tiled_p<CIN, COUT, K, MODE, TAIL, 2>(d, y, yc, t, gh, gw, st);
 }
 
 int launch_fwd(const LayerDev& d, float* y, float* yc, float* py, float* pc, hipStream_t st, const char** why) {

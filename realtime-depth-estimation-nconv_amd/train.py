@@ -6,6 +6,8 @@ These are cheap elementwise/reduction ops around the NConv path; they run as PyT
   calculate_loss_multi_resolution   utils.py:63-71     each scale bilinear-resized to 480x640, [0] only
   get_optimizer                     utils.py:53-61     AdamW / SGD / RMSprop
   save_checkpoint / load_state_dict_compat  utils.py:42-51, models/step2.py:29-36
+  GraphedTrainStep                  one training iteration (train_step1.py:59-65) captured in a
+                                    hipGraph and replayed: removes the per-kernel host launch cost
 """
 import os
 
@@ -56,9 +58,10 @@ def calculate_loss_multi_resolution(reconstructed_img, target_img, use_gradient_
     return total / len(reconstructed_img)
 
 
-def get_optimizer(net, optim_type, lr, weight_decay):
+def get_optimizer(net, optim_type, lr, weight_decay, capturable=False):
+    """utils.py:53-61; capturable=True keeps AdamW's step count on the device (GraphedTrainStep)."""
     if optim_type == "adam":
-        return optimizer.AdamW(net.parameters(), lr=lr, weight_decay=weight_decay)
+        return optimizer.AdamW(net.parameters(), lr=lr, weight_decay=weight_decay, capturable=capturable)
     if optim_type == "sgd":
         return optimizer.SGD(net.parameters(), lr=lr, weight_decay=weight_decay, momentum=0.9)
     if optim_type == "rmsprop":
@@ -82,3 +85,61 @@ def load_checkpoint(model, path, strict=False, map_location="cpu"):
     ck = torch.load(path, map_location=map_location, weights_only=True)
     sd = ck["state_dict"] if isinstance(ck, dict) and "state_dict" in ck else ck
     return model.load_state_dict(strip_module_prefix(sd), strict=strict)
+
+
+class GraphedTrainStep:
+    """One training iteration — zero_grad, forward (EnforcePos drift included), loss, backward,
+    the data-parallel gradient all-reduce (DataParallelRCCL.allreduce_grads, if the model has it)
+    and the optimizer step — captured once in a hipGraph and replayed per call.
+
+    loss_fn(model, *inputs) -> scalar loss tensor. The optimizer must keep its state on the device
+    and update it without host synchronisation (torch AdamW / Adam with capturable=True). Inputs
+    are copied into static buffers on every call (pass the same tensors to skip the copy). The
+    warm-up iterations needed before capture run on a snapshot: parameters, buffers and optimizer
+    state are restored in place afterwards, so constructing the step does not train the model.
+    """
+
+    def __init__(self, model, optimizer, loss_fn, example_inputs, warmup=3):
+        self.model, self.optimizer, self.loss_fn = model, optimizer, loss_fn
+        self.static_inputs = [x.detach().clone() for x in example_inputs]
+        tensors = [t for t in list(model.parameters()) + list(model.buffers())]
+        tensors += [v for st in optimizer.state.values() for v in st.values() if torch.is_tensor(v)]
+        snap = [t.detach().clone() for t in tensors]
+        cur = torch.cuda.current_stream()
+        side = torch.cuda.Stream()
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            for _ in range(max(1, warmup)):
+                self._body()
+        cur.wait_stream(side)
+        # optimizer state created during warm-up (first step) is part of the captured graph too
+        new_state = [v for st in optimizer.state.values() for v in st.values() if torch.is_tensor(v)]
+        self.graph = torch.cuda.CUDAGraph()
+        optimizer.zero_grad(set_to_none=True)
+        with torch.cuda.graph(self.graph):
+            self.static_loss = self._body(zero=False)
+        with torch.no_grad():
+            for t, v in zip(tensors, snap):
+                t.copy_(v)
+            known = {id(t) for t in tensors}
+            for v in new_state:  # state that did not exist before the warm-up starts from zero
+                if id(v) not in known:
+                    v.zero_()
+        torch.cuda.synchronize()
+
+    def _body(self, zero=True):
+        if zero:
+            self.optimizer.zero_grad(set_to_none=True)
+        loss = self.loss_fn(self.model, *self.static_inputs)
+        loss.backward()
+        if hasattr(self.model, "allreduce_grads"):
+            self.model.allreduce_grads()
+        self.optimizer.step()
+        return loss
+
+    def __call__(self, *inputs):
+        for dst, src in zip(self.static_inputs, inputs):
+            if src is not dst and src.data_ptr() != dst.data_ptr():
+                dst.copy_(src)
+        self.graph.replay()
+        return self.static_loss

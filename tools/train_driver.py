@@ -14,7 +14,7 @@ def main(steps):
     import nconv_pkg
     m = nconv_pkg.load()
     dev = torch.device("cuda:0")
-    step = bench.make_train_step(m, dev, 8, 352, 1216, 1, 0)
+    step = bench.make_train_step(m, dev, 8, 352, 1216, 1, 0, graph=len(sys.argv) < 3 or sys.argv[2] != "eager")
     for _ in range(steps):
         step()
     torch.cuda.synchronize()
