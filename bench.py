@@ -127,13 +127,13 @@ def time_layers(m, net, S, reps=20):
     with torch.no_grad():
         for name, fn in calls.items():
             fn()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-            for _ in range(reps):
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+            for e0, e1 in ev:  # one event pair per launch: device time of the kernel alone
+                e0.record(stream)
                 fn()
-            e1.record(stream)
-            e1.synchronize()
-            out[name] = e0.elapsed_time(e1) / reps * 1e3  # us
+                e1.record(stream)
+            ev[-1][1].synchronize()
+            out[name] = sum(e0.elapsed_time(e1) for e0, e1 in ev) / reps * 1e3  # us
     return out
 
 

@@ -39,6 +39,7 @@ def run():
     with torch.no_grad():
         net(torch.zeros(1, 1, 32, 32, device=dev))
     net.eval()
+    net.d_net.inference_streams = 1  # full-batch launches, as bench.time_layers times them
     S = bench.sparse_depth(torch.Generator().manual_seed(1000), B, H, W, dev)
     with torch.no_grad():
         for _ in range(REPS):
@@ -52,17 +53,18 @@ def _layer_of(name, grid, grids_by_name):
     sig = name.split("(")[0]
     order = sorted(grids_by_name[sig], reverse=True)  # the warm-up call's small grids sort last
     pick = lambda names: names[order.index(grid)] if order.index(grid) < len(names) else None
-    if grid != order[0] and ("fwd_tiled<1, 8, 5, 1" in sig or "true>" in sig):
+    # template arguments <CIN, COUT, K, MODE, TAIL, P>
+    if grid != order[0] and ("fwd_tiled<1, 8, 5, 1," in sig or ", true," in sig):
         return None
-    if "fwd_tiled<1, 8, 5, 1, false>" in sig:
+    if "fwd_tiled<1, 8, 5, 1, false," in sig:
         return "nconv1"
-    if "fwd_tiled<8, 8, 5, 0, false>" in sig:  # nconv2 and the down layers (pooled-copy inputs)
+    if "fwd_tiled<8, 8, 5, 0, false," in sig:  # nconv2 and the down layers (pooled-copy inputs)
         return pick(["nconv2", "nconv_down1", "nconv_down2", "nconv_down3"])
-    if "fwd_tiled<8, 8, 5, 2, false>" in sig:  # down layers pooling on load (training path)
+    if "fwd_tiled<8, 8, 5, 2, false," in sig:  # down layers pooling on load (training path)
         return pick(["nconv_down1", "nconv_down2", "nconv_down3"])
-    if "fwd_tiled<16, 8, 3, 3, false>" in sig:
+    if "fwd_tiled<16, 8, 3, 3, false," in sig:
         return pick(["nconv5", "nconv4"])
-    if "fwd_tiled<16, 8, 3, 4, true>" in sig:
+    if "fwd_tiled<16, 8, 3, 4, true," in sig:
         return "nconv6+7_tail"
     return None
 
