@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define NCONV_ABI_VERSION 3
+#define NCONV_ABI_VERSION 4
 
 /* How a layer's input (data x, confidence c) is produced from its source tensors. These are the
  * DNET glue ops fused into the layer's load stage (models/step1.py:53,61-90). */
@@ -119,6 +119,52 @@ size_t nconv_bwd_workspace_bytes(const nconv_layer* L);
 int nconv_bwd(const nconv_layer* L, const float* y, const float* cout, const float* gy,
               const float* gcout, float* gxa, float* gca, float* gxb, float* gcb, float* gw,
               float* gbias, void* workspace, size_t workspace_bytes, unsigned flags, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Dense convolutions of the RGB-guided model on the matrix cores (fp32 MFMA, exact f32 products).
+ * Replace the nn.Conv2d / nn.ConvTranspose2d (+ eval BatchNorm + ReLU + residual add + torch.cat)
+ * sequences of models/step2.py: RGBEncoder (:134-154), ConvBlock (:290-297), Basic2d (:178-195),
+ * Basic2dTrans (:197-214), UpCat / NewFusionBlock cat (:173-175, :229-231), Conv3x3 heads (:156-158,
+ * :259, :278). Inference (eval) semantics: BatchNorm uses its running statistics, folded into
+ * the packed weights (scale) and the bias.
+ * ------------------------------------------------------------------------------------------ */
+enum nconv_dense_kind {
+    NCONV_DENSE_3X3 = 0,            /* Conv2d 3x3, padding 1, stride 1 or 2                      */
+    NCONV_DENSE_1X1 = 1,            /* Conv2d 1x1, padding 0, stride 1 or 2                      */
+    NCONV_DENSE_TRANSPOSED_4X4 = 2  /* ConvTranspose2d 4x4, stride 2, padding 1 (Ho = 2H)        */
+};
+
+typedef struct nconv_dense_conv {
+    int B;
+    const float* x0; int C0;   /* input = cat(x0, x1) along channels: x0 (B, C0, H, W)          */
+    const float* x1; int C1;   /* x1 (B, C1, H, W), or NULL / 0                                   */
+    int H, W;
+    int Cout, Ho, Wo;          /* Cout in {32, 64}                                                */
+    int kind, stride;
+    const float* wpack;        /* nconv_dense_pack output                                         */
+    const float* bias;         /* (Cout) or NULL                                                   */
+    int relu;                  /* 1: max(., 0) after the bias                                      */
+    const float* wshort;       /* optional packed 1x1 shortcut (same stride) added after the ReLU  */
+    float* out;                /* output channels [out_c0, out_c0 + Cout) of (B, out_C, Ho, Wo)    */
+    int out_C, out_c0;
+} nconv_dense_conv;
+
+/* Floats of a packed weight buffer for (kind, Cin, Cout). */
+size_t nconv_dense_packed_floats(int kind, int Cin, int Cout);
+
+/* Pack w — Conv2d (Cout, Cin, k, k) or ConvTranspose2d (Cin, Cout, 4, 4) — into the kernel's
+ * layout, multiplying output channel o by scale[o] if scale != NULL (eval BatchNorm folding). */
+int nconv_dense_pack(int kind, int Cin, int Cout, const float* w, const float* scale, float* wpack,
+                     void* stream);
+
+/* out[:, out_c0:out_c0+Cout] = [relu](conv(cat(x0, x1)) + bias) [+ conv1x1_shortcut(cat(x0, x1))] */
+int nconv_dense_conv_fwd(const nconv_dense_conv* c, void* stream);
+
+/* 3x3 (padding 1, stride 1) convolution to one output channel plus a residual:
+ * out = conv3x3(x; w (1, Cin, 3, 3)) + res, all (B, ., H, W); res may be NULL
+ * (the depth heads `depth + Conv3x3(fout)`, models/step2.py:259,278). */
+int nconv_conv3x3_c1(const float* x, int B, int Cin, int H, int W, const float* w, const float* res,
+                     float* out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -13,11 +13,13 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # NCONV_LIB: an alternative build of the same library (kernel-tuning experiments)
 LIB_PATH = os.environ.get("NCONV_LIB") or os.path.join(_HERE, "libnconv.so")
-ABI_VERSION = 3
+ABI_VERSION = 4
 BWD_ACCUMULATE = 1
 
 # enum nconv_load_mode
 PLAIN, THRESH, POOL2, UPCAT_SKIP_FIRST, UPCAT_UP_FIRST = 0, 1, 2, 3, 4
+# enum nconv_dense_kind
+DENSE_3X3, DENSE_1X1, DENSE_TRANSPOSED_4X4 = 0, 1, 2
 
 EXPORTED = (
     "nconv_abi_version",
@@ -28,6 +30,10 @@ EXPORTED = (
     "nconv_fwd_tail",
     "nconv_bwd_workspace_bytes",
     "nconv_bwd",
+    "nconv_dense_packed_floats",
+    "nconv_dense_pack",
+    "nconv_dense_conv_fwd",
+    "nconv_conv3x3_c1",
 )
 
 
@@ -44,6 +50,15 @@ class NconvLayer(ctypes.Structure):
                 ("groups", ctypes.c_int), ("eps", ctypes.c_float), ("load_mode", ctypes.c_int),
                 ("thresh", ctypes.c_float), ("a", NconvSrc), ("b", NconvSrc),
                 ("weight", ctypes.c_void_p), ("bias", ctypes.c_void_p), ("wsum", ctypes.c_void_p)]
+
+
+class NconvDenseConv(ctypes.Structure):
+    _fields_ = [("B", ctypes.c_int), ("x0", ctypes.c_void_p), ("C0", ctypes.c_int),
+                ("x1", ctypes.c_void_p), ("C1", ctypes.c_int), ("H", ctypes.c_int), ("W", ctypes.c_int),
+                ("Cout", ctypes.c_int), ("Ho", ctypes.c_int), ("Wo", ctypes.c_int),
+                ("kind", ctypes.c_int), ("stride", ctypes.c_int), ("wpack", ctypes.c_void_p),
+                ("bias", ctypes.c_void_p), ("relu", ctypes.c_int), ("wshort", ctypes.c_void_p),
+                ("out", ctypes.c_void_p), ("out_C", ctypes.c_int), ("out_c0", ctypes.c_int)]
 
 
 _lib = None
@@ -70,6 +85,15 @@ def _declare(lib):
     lib.nconv_bwd.restype = ctypes.c_int
     lib.nconv_bwd.argtypes = [ctypes.POINTER(NconvLayer), P, P, P, P, P, P, P, P, P, P, P,
                               ctypes.c_size_t, ctypes.c_uint, P]
+    I = ctypes.c_int
+    lib.nconv_dense_packed_floats.restype = ctypes.c_size_t
+    lib.nconv_dense_packed_floats.argtypes = [I, I, I]
+    lib.nconv_dense_pack.restype = I
+    lib.nconv_dense_pack.argtypes = [I, I, I, P, P, P, P]
+    lib.nconv_dense_conv_fwd.restype = I
+    lib.nconv_dense_conv_fwd.argtypes = [ctypes.POINTER(NconvDenseConv), P]
+    lib.nconv_conv3x3_c1.restype = I
+    lib.nconv_conv3x3_c1.argtypes = [P, I, I, I, I, P, P, P, P]
 
 
 def lib():

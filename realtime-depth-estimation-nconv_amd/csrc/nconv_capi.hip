@@ -136,4 +136,64 @@ int nconv_bwd(const nconv_layer* L, const float* y, const float* cout, const flo
     return rc ? fail(rc, "nconv_bwd", why) : 0;
 }
 
+size_t nconv_dense_packed_floats(int kind, int Cin, int Cout) {
+    if (kind < NCONV_DENSE_3X3 || kind > NCONV_DENSE_TRANSPOSED_4X4 || Cin <= 0 || Cout <= 0) return 0;
+    return nconv::dense_packed_floats(kind, Cin, Cout);
+}
+
+int nconv_dense_pack(int kind, int Cin, int Cout, const float* w, const float* scale, float* wpack, void* stream) {
+    if (kind < NCONV_DENSE_3X3 || kind > NCONV_DENSE_TRANSPOSED_4X4) return fail(-22, "nconv_dense_pack", "unknown kind");
+    if (Cin <= 0 || Cout <= 0) return fail(-22, "nconv_dense_pack", "non-positive Cin/Cout");
+    if (!w || !wpack) return fail(-22, "nconv_dense_pack", "null weight pointer");
+    const char* why = nullptr;
+    int rc = nconv::launch_dense_pack(kind, Cin, Cout, w, scale, wpack, (hipStream_t)stream, &why);
+    return rc ? fail(rc, "nconv_dense_pack", why) : 0;
+}
+
+int nconv_dense_conv_fwd(const nconv_dense_conv* c, void* stream) {
+    const char* fn = "nconv_dense_conv_fwd";
+    if (!c) return fail(-22, fn, "null descriptor");
+    if (c->B <= 0 || c->H <= 0 || c->W <= 0 || c->C0 <= 0 || c->C1 < 0) return fail(-22, fn, "non-positive B/H/W/C0");
+    if (!c->x0 || (c->C1 > 0 && !c->x1)) return fail(-22, fn, "null input pointer");
+    if (c->Cout != 32 && c->Cout != 64) return fail(-95, fn, "Cout must be 32 or 64");
+    if (!c->wpack || !c->out) return fail(-22, fn, "null weight / output pointer");
+    if (c->out_c0 < 0 || c->out_c0 + c->Cout > c->out_C) return fail(-22, fn, "output channel range exceeds out_C");
+    int ho, wo;
+    switch (c->kind) {
+        case NCONV_DENSE_3X3:
+            if (c->stride != 1 && c->stride != 2) return fail(-22, fn, "3x3 stride must be 1 or 2");
+            ho = (c->H - 1) / c->stride + 1;
+            wo = (c->W - 1) / c->stride + 1;
+            break;
+        case NCONV_DENSE_1X1:
+            if (c->stride != 1 && c->stride != 2) return fail(-22, fn, "1x1 stride must be 1 or 2");
+            ho = (c->H - 1) / c->stride + 1;
+            wo = (c->W - 1) / c->stride + 1;
+            if (c->wshort) return fail(-22, fn, "shortcut only with a 3x3 main convolution");
+            break;
+        case NCONV_DENSE_TRANSPOSED_4X4:
+            if (c->stride != 2) return fail(-22, fn, "transposed 4x4 has stride 2");
+            if (c->wshort) return fail(-22, fn, "no shortcut for the transposed convolution");
+            ho = 2 * c->H;
+            wo = 2 * c->W;
+            break;
+        default:
+            return fail(-22, fn, "unknown kind");
+    }
+    if (ho != c->Ho || wo != c->Wo) return fail(-22, fn, "Ho/Wo inconsistent with kind/stride/H/W");
+    const char* why = nullptr;
+    int rc = nconv::launch_dense_conv(*c, (hipStream_t)stream, &why);
+    return rc ? fail(rc, fn, why) : 0;
+}
+
+int nconv_conv3x3_c1(const float* x, int B, int Cin, int H, int W, const float* w, const float* res, float* out,
+                     void* stream) {
+    const char* fn = "nconv_conv3x3_c1";
+    if (!x || !w || !out) return fail(-22, fn, "null pointer");
+    if (B <= 0 || Cin <= 0 || H <= 0 || W <= 0) return fail(-22, fn, "non-positive B/Cin/H/W");
+    const char* why = nullptr;
+    int rc = nconv::launch_conv3x3_c1(x, B, Cin, H, W, w, res, out, (hipStream_t)stream, &why);
+    return rc ? fail(rc, fn, why) : 0;
+}
+
 }  // extern "C"

@@ -43,4 +43,12 @@ int launch_weight_prep(int n, float* const* w, const int* cout, const int* fan_i
 size_t bwd_workspace_bytes(const LayerDev& d);
 int launch_bwd(const LayerDev& d, const BwdArgs& a, hipStream_t st, const char** why);
 
+// Dense convolutions (RGB-guided model).
+size_t dense_packed_floats(int kind, int Cin, int Cout);
+int launch_dense_pack(int kind, int Cin, int Cout, const float* w, const float* scale, float* wp, hipStream_t st,
+                      const char** why);
+int launch_dense_conv(const nconv_dense_conv& p, hipStream_t st, const char** why);
+int launch_conv3x3_c1(const float* x, int B, int Cin, int H, int W, const float* w, const float* res, float* out,
+                      hipStream_t st, const char** why);
+
 }  // namespace nconv

@@ -4,8 +4,13 @@ SETP2_BP_TRAIN / SETP2_BP_EXPORT keep the reference's constructors, forward(rgb0
 depth1), submodule names (hence state_dict keys, including the unused rgb_encoder4 of the TRAIN
 variant, step2.py:46) and RNG consumption order. Step 1 is this package's SETP1_NCONV (libnconv
 kernels); it is called as step1(depth0, depth1), which the reference intends (step2.py:62-63) but
-its one-argument SETP1_NCONV.forward rejects. The dense convolutions of the RGB
-encoder and the fusion decoder are PyTorch-ROCm convolutions (MIOpen).
+its one-argument SETP1_NCONV.forward rejects.
+
+Inference (eval mode, no autograd): every dense convolution of the RGB encoder and the fusion
+decoder runs on libnconv's fp32-MFMA kernels (dense.py, nconv_dense_conv_fwd) with eval
+BatchNorm folded into the packed weights, bias + ReLU + the RGBEncoder shortcut fused into the
+epilogue, and each torch.cat replaced by two-source loads / channel-offset stores. Training mode
+(BatchNorm batch statistics, autograd) uses the PyTorch-ROCm modules below.
 """
 from collections import OrderedDict
 
@@ -13,6 +18,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from . import dense as D
 from .dnet import SETP1_NCONV
 
 
@@ -42,6 +48,17 @@ class RGBEncoder(nn.Module):
     def forward(self, x):
         return self.encoder(x) + self.downsample(x)
 
+    def dense_forward(self, x):
+        conv, bn, sc = self.encoder[0], self.encoder[1], self.downsample[0]
+
+        def build():
+            scale, shift = D.bn_fold(bn, conv.bias)
+            return (D.pack(D.DENSE_3X3, conv.weight, conv.in_channels, conv.out_channels, scale), shift,
+                    D.pack(D.DENSE_1X1, sc.weight, sc.in_channels, sc.out_channels))
+        wp, bias, ws = D.cached(self, "enc", [conv.weight, conv.bias, bn.weight, bn.bias, bn.running_mean,
+                                              bn.running_var, sc.weight], build)
+        return D.conv(x, D.DENSE_3X3, conv.stride[0], wp, bias, True, conv.out_channels, wshort=ws)
+
 
 class Basic2d(nn.Module):
     """conv (+BN when norm_layer, then no conv bias) + activation (step2.py:178-195)."""
@@ -59,6 +76,24 @@ class Basic2d(nn.Module):
     def forward(self, x):
         return self.conv(x)
 
+    def dense_forward(self, x0, x1=None, out=None, out_c0=0):
+        conv = self.conv.conv
+        bn = getattr(self.conv, "bn", None)
+        if conv.kernel_size != (3, 3) or conv.padding != (1, 1) or not isinstance(self.conv.relu, nn.ReLU):
+            raise NotImplementedError("dense path: 3x3 / padding 1 / ReLU Basic2d only")
+
+        def build():
+            if bn is not None:
+                scale, shift = D.bn_fold(bn, conv.bias)
+            else:
+                scale, shift = None, conv.bias.detach().contiguous()
+            return D.pack(D.DENSE_3X3, conv.weight, conv.in_channels, conv.out_channels, scale), shift
+        ts = [conv.weight] + ([conv.bias] if conv.bias is not None else []) + \
+            ([bn.weight, bn.bias, bn.running_mean, bn.running_var] if bn is not None else [])
+        wp, bias = D.cached(self, "conv", ts, build)
+        return D.conv(x0, D.DENSE_3X3, conv.stride[0], wp, bias, True, conv.out_channels, x1=x1, out=out,
+                      out_c0=out_c0)
+
 
 class Basic2dTrans(nn.Module):
     """ConvTranspose 4x4 / stride 2 / padding 1 + BN + activation (step2.py:197-214)."""
@@ -73,6 +108,22 @@ class Basic2dTrans(nn.Module):
 
     def forward(self, x):
         return self.relu(self.bn(self.conv(x.contiguous())))
+
+    def dense_forward(self, x0, x1=None):
+        conv, bn = self.conv, self.bn
+
+        def build():
+            if isinstance(bn, nn.BatchNorm2d):
+                scale, shift = D.bn_fold(bn, conv.bias)
+            else:
+                scale = None
+                shift = conv.bias.detach().contiguous() if conv.bias is not None else None
+            return D.pack(D.DENSE_TRANSPOSED_4X4, conv.weight, conv.in_channels, conv.out_channels, scale), shift
+        ts = [conv.weight] + ([conv.bias] if conv.bias is not None else []) + \
+            ([bn.weight, bn.bias, bn.running_mean, bn.running_var] if isinstance(bn, nn.BatchNorm2d) else [])
+        wp, bias = D.cached(self, "convT", ts, build)
+        return D.conv(x0, D.DENSE_TRANSPOSED_4X4, 2, wp, bias, isinstance(self.relu, nn.ReLU),
+                      conv.out_channels, x1=x1)
 
 
 class UpCat(nn.Module):
@@ -89,6 +140,10 @@ class UpCat(nn.Module):
         up = self.upf(torch.cat([x, d], dim=1))
         return self.conv(torch.cat([up, y], dim=1))
 
+    def dense_forward(self, y, x, d):
+        up = self.upf.dense_forward(x, d)
+        return self.conv.dense_forward(up, y)
+
 
 class ConvBlock(nn.Module):
     """3x3 conv (bias) + ReLU (step2.py:290-297)."""
@@ -100,6 +155,14 @@ class ConvBlock(nn.Module):
 
     def forward(self, x):
         return self.relu(self.conv(x))
+
+    def dense_forward(self, x, out=None, out_c0=0):
+        conv = self.conv
+
+        def build():
+            return D.pack(D.DENSE_3X3, conv.weight, conv.in_channels, conv.out_channels), conv.bias.detach().contiguous()
+        wp, bias = D.cached(self, "conv", [conv.weight, conv.bias], build)
+        return D.conv(x, D.DENSE_3X3, conv.stride[0], wp, bias, True, conv.out_channels, out=out, out_c0=out_c0)
 
 
 class NewFusionBlock(nn.Module):
@@ -116,6 +179,14 @@ class NewFusionBlock(nn.Module):
     def forward(self, rgb, depth):
         fused = torch.cat((self.rgb_conv(rgb), self.depth_conv(depth)), 1)
         return self.fuse_conv3(self.fuse_conv2(self.fuse_conv1(fused)))
+
+    def dense_forward(self, rgb, depth):
+        C = self.rgb_conv.conv.out_channels
+        B, _, H, W = rgb.shape
+        fused = torch.empty((B, 2 * C, H, W), device=rgb.device, dtype=torch.float32)
+        self.rgb_conv.dense_forward(rgb, out=fused, out_c0=0)      # the cat, written in place
+        self.depth_conv.dense_forward(depth, out=fused, out_c0=C)
+        return self.fuse_conv3.dense_forward(self.fuse_conv2.dense_forward(self.fuse_conv1.dense_forward(fused)))
 
 
 class FusionResolutionBlock(nn.Module):
@@ -135,6 +206,13 @@ class FusionResolutionBlock(nn.Module):
         fout = self.fuse(fout, depth)
         return fout, depth + self.conv(fout)
 
+    def dense_forward(self, rgb, depth, depth_last_step, fusion_festure):
+        fout = self.upcat.dense_forward(rgb, fusion_festure, depth_last_step)
+        depth = F.interpolate(depth, scale_factor=1 / self.downsample_factor, mode="bilinear",
+                              align_corners=True).contiguous()
+        fout = self.fuse.dense_forward(fout, depth)
+        return fout, D.conv3x3_c1(fout, self.conv.weight, depth)
+
 
 class FusionResolution0(nn.Module):
     """Coarsest decoder scale (step2.py:262-278)."""
@@ -149,6 +227,12 @@ class FusionResolution0(nn.Module):
         depth = F.interpolate(depth, scale_factor=1 / self.downsample_factor, mode="bilinear", align_corners=True)
         fout = self.fuse(rgb, depth)
         return fout, depth + self.conv(fout)
+
+    def dense_forward(self, rgb, depth):
+        depth = F.interpolate(depth, scale_factor=1 / self.downsample_factor, mode="bilinear",
+                              align_corners=True).contiguous()
+        fout = self.fuse.dense_forward(rgb, depth)
+        return fout, D.conv3x3_c1(fout, self.conv.weight, depth)
 
 
 def _encoders_and_decoder(m, first_set):
@@ -169,7 +253,30 @@ def _encoders_and_decoder(m, first_set):
     m.fuse3 = FusionResolutionBlock(32, 32, 1)
 
 
+def _use_dense(m, x):
+    """libnconv's MFMA kernels for the dense convolutions: eval mode, device tensors, no autograd."""
+    if m.training or not x.is_cuda or not getattr(m, "dense_kernels", True):
+        return False
+    return not (torch.is_grad_enabled() and any(p.requires_grad for p in m.parameters()))
+
+
+def _guided_forward_dense(m, rgb0, depth0, rgb1, depth1):
+    sparse = m.step1(depth0, depth1).contiguous()
+    rgb = torch.cat((rgb0, rgb1), dim=0).contiguous()
+    e0 = m.rgb_encoder0.dense_forward(rgb)
+    e1 = m.rgb_encoder1.dense_forward(e0)
+    e2 = m.rgb_encoder2.dense_forward(e1)
+    e3 = m.rgb_encoder3.dense_forward(e2)
+    f0, d0 = m.fuse0.dense_forward(e3, sparse)
+    f1, d1 = m.fuse1.dense_forward(e2, sparse, f0, d0)
+    f2, d2 = m.fuse2.dense_forward(e1, sparse, f1, d1)
+    f3, d3 = m.fuse3.dense_forward(e0, sparse, f2, d2)
+    return d0, d1, d2, d3
+
+
 def _guided_forward(m, rgb0, depth0, rgb1, depth1):
+    if _use_dense(m, rgb0):
+        return _guided_forward_dense(m, rgb0, depth0, rgb1, depth1)
     sparse = m.step1(depth0, depth1)
     rgb = torch.cat((rgb0, rgb1), dim=0)
     e0 = m.rgb_encoder0(rgb)

@@ -1,0 +1,109 @@
+"""GPU parity of the matrix-core dense convolutions (dense_conv.hip via dense.py) against float64
+PyTorch CPU references of the same modules (torch.nn.functional conv2d / conv_transpose2d, eval
+BatchNorm): every kind / stride / output width, two-source (concatenated) inputs, channel-offset
+outputs, the RGBEncoder shortcut, ragged sizes. Tolerance: max|gpu - ref| <= 2e-5 * max|ref| per
+tensor (fp32 products are exact on MFMA; only the summation order differs)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _close(got, ref, what):
+    got = got.double().cpu()
+    err = (got - ref).abs().max().item()
+    scale = ref.abs().max().item()
+    assert err <= 2e-5 * scale + 1e-12, f"{what}: max err {err:.3e} (ref max {scale:.3e})"
+
+
+def _rand(g, *shape):
+    return torch.randn(*shape, generator=g, dtype=torch.float64)
+
+
+@pytest.mark.parametrize("kind,stride,cout,c0,c1,H,W", [
+    (0, 1, 32, 5, 3, 13, 37),     # 3x3 s1, two sources, partial chunk, ragged tile edges
+    (0, 1, 64, 64, 64, 20, 70),   # 3x3 s1 128 -> 64 (UpCat conv)
+    (0, 1, 32, 1, 0, 9, 33),      # depth_conv (1 input channel)
+    (0, 2, 64, 32, 0, 15, 41),    # 3x3 s2 (encoder), odd sizes
+    (1, 1, 32, 8, 0, 11, 35),     # 1x1
+    (1, 2, 64, 16, 0, 12, 40),    # 1x1 s2
+    (2, 2, 32, 32, 1, 7, 19),     # ConvTranspose 4x4 s2 from cat(features, depth)
+    (2, 2, 64, 1, 64, 6, 40),     # ConvTranspose with the 1-channel source first
+])
+def test_dense_conv_kinds(nconv_amd, gpu, kind, stride, cout, c0, c1, H, W):
+    D = nconv_amd.dense
+    g = torch.Generator().manual_seed(7 + kind * 10 + stride)
+    B, cin = 2, c0 + c1
+    x0, x1 = _rand(g, B, c0, H, W), (_rand(g, B, c1, H, W) if c1 else None)
+    x = torch.cat([x0, x1], 1) if c1 else x0
+    if kind == 2:
+        w = _rand(g, cin, cout, 4, 4) * 0.1
+        ref = F.conv_transpose2d(x, w, stride=2, padding=1)
+    else:
+        k = 3 if kind == 0 else 1
+        w = _rand(g, cout, cin, k, k) * 0.1
+        ref = F.conv2d(x, w, stride=stride, padding=k // 2)
+    bias = _rand(g, cout)
+    scale = torch.rand(cout, generator=g, dtype=torch.float64) + 0.5
+    ref = torch.relu(ref * scale.view(1, -1, 1, 1) + bias.view(1, -1, 1, 1))
+    f = lambda t: None if t is None else t.to(gpu, torch.float32).contiguous()
+    wp = D.pack(kind, f(w), cin, cout, f(scale))
+    out_full = torch.full((B, cout + 8, ref.shape[2], ref.shape[3]), 7.0, device=gpu)
+    D.conv(f(x0), kind, stride, wp, f(bias), True, cout, x1=f(x1), out=out_full, out_c0=8)
+    torch.cuda.synchronize()
+    assert torch.equal(out_full[:, :8].cpu(), torch.full((B, 8) + tuple(ref.shape[2:]), 7.0)), "wrote outside its channel range"
+    _close(out_full[:, 8:], ref, f"kind {kind} stride {stride} cout {cout}")
+
+
+@pytest.mark.parametrize("stride,cin,cout", [(1, 3, 32), (2, 32, 64), (2, 64, 64)])
+def test_rgb_encoder_dense_matches_module(nconv_amd, gpu, stride, cin, cout):
+    """RGBEncoder (step2.py:134-154) in eval mode with non-trivial BatchNorm statistics."""
+    torch.manual_seed(stride * 100 + cin)
+    enc = nconv_amd.guided.RGBEncoder(cin, cout, stride).double().eval()
+    bn = enc.encoder[1]
+    with torch.no_grad():
+        bn.running_mean.uniform_(-0.5, 0.5)
+        bn.running_var.uniform_(0.5, 2.0)
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.2, 0.2)
+    x = torch.randn(2, cin, 17, 45, dtype=torch.float64) * 50
+    with torch.no_grad():
+        ref = enc(x)
+        got = enc.float().to(gpu).dense_forward(x.float().to(gpu))
+    torch.cuda.synchronize()
+    _close(got, ref, "RGBEncoder")
+
+
+def test_conv3x3_c1_residual(nconv_amd, gpu):
+    g = torch.Generator().manual_seed(3)
+    x, w, res = _rand(g, 2, 64, 21, 70), _rand(g, 1, 64, 3, 3) * 0.1, _rand(g, 2, 1, 21, 70)
+    ref = F.conv2d(x, w, padding=1) + res
+    f = lambda t: t.to(gpu, torch.float32).contiguous()
+    got = nconv_amd.dense.conv3x3_c1(f(x), f(w), f(res))
+    torch.cuda.synchronize()
+    _close(got, ref, "conv3x3_c1")
+
+
+@pytest.mark.parametrize("H,W", [(64, 96), (96, 320)])
+def test_guided_dense_path_matches_torch_modules(nconv_amd, gpu, H, W):
+    """The whole SETP2 eval forward: dense kernels vs the PyTorch modules (same weights, BN with
+    non-trivial running statistics), fp32 on the GPU both ways. Tolerance 1e-4 relative to the
+    largest magnitude per scale (the torch path runs MIOpen's Winograd kernels)."""
+    from guided_cases import f5_inputs
+    torch.manual_seed(4)
+    model = nconv_amd.SETP2_BP_EXPORT(step1_crop="generalized")
+    with torch.no_grad():
+        for mod in model.modules():
+            if isinstance(mod, torch.nn.BatchNorm2d):
+                mod.running_mean.uniform_(-0.1, 0.1)
+                mod.running_var.uniform_(0.5, 1.5)
+    model = model.to(gpu).eval()
+    ins = [t.to(gpu) for t in f5_inputs(H, W)]
+    with torch.no_grad():
+        got = nconv_amd.guided._guided_forward(model, *ins)
+        model.dense_kernels = False
+        ref = nconv_amd.guided._guided_forward(model, *ins)
+    for i, (a, b) in enumerate(zip(got, ref)):
+        err = (a - b).abs().max().item()
+        assert err <= 1e-4 * b.abs().max().item() + 1e-5, f"scale {i}: max err {err:.3e}"
