@@ -46,7 +46,9 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--graph", type=int, default=1, help="capture the forward in a hipGraph (1) or run eager (0)")
     p.add_argument("--streams", type=int, default=2, help="HIP streams the inference batch is split over")
-    p.add_argument("--train-graph", type=int, default=1, help="replay the training step from a hipGraph (1) or eager (0)")
+    p.add_argument("--train-graph", type=int, default=-1,
+                   help="replay the training step from a hipGraph (1) or eager (0); default: 1 on one GPU, 0 with "
+                        "several (the RCCL all-reduce stays outside graph capture)")
     return p.parse_args()
 
 
@@ -314,7 +316,8 @@ def main():
     # ---- fwd + bwd + AdamW (config 4b) ----
     train = None
     if not a.no_train:
-        step = make_train_step(m, dev, B, H, W, world, rank, graph=bool(a.train_graph))
+        tg = (world == 1) if a.train_graph < 0 else bool(a.train_graph)
+        step = make_train_step(m, dev, B, H, W, world, rank, graph=tg)
         ks = a.train_steps or a.steps
         for _ in range(max(a.warmup, 1)):
             step()
@@ -332,7 +335,7 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             tt = t.item()
         train = {"frames_per_sec": round(world * B * ks / tt, 2), "ms_per_step": round(tt / ks * 1e3, 4), "steps": ks,
-                 "hipgraph": bool(a.train_graph)}
+                 "hipgraph": tg}
 
     # ---- config 3: guided forward ----
     guided = None
