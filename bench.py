@@ -43,6 +43,9 @@ def parse():
     p.add_argument("--no-train", action="store_true")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-guided", action="store_true", help="skip the config-3 guided forward measurement")
+    p.add_argument("--no-guided-train", action="store_true", help="skip the config-4 guided training step")
+    p.add_argument("--guided-train-torch", action="store_true",
+                   help="also time the config-4 step on the PyTorch-ROCm modules (MIOpen), for comparison")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--graph", type=int, default=1, help="capture the forward in a hipGraph (1) or run eager (0)")
     p.add_argument("--streams", type=int, default=2, help="HIP streams the inference batch is split over")
@@ -219,6 +222,59 @@ def guided_forward(m, dev, B, H, W, steps, warmup, rank):
     return el
 
 
+def make_guided_train_step(m, dev, B, H, W, rank, kernels=True):
+    """Config 4 per GPU: one SETP2_BP_TRAIN iteration as train_step2.py:60-66 — train mode (frozen
+    step 1, still EnforcePos-drifted; BatchNorm batch statistics), forward on B/2 + B/2 frames,
+    calculate_loss_multi_resolution over the four scales of pair 0 (utils.py:63-71; MSE:
+    use_gradient_loss = False, train_step2.py:21), backward, RCCL all-reduce of the present
+    gradients when several ranks run, AdamW lr 1e-4 / wd 1e-7 (train_step2.py:17-18).
+    kernels=False runs the same step on the PyTorch-ROCm modules (MIOpen) for comparison."""
+    torch.manual_seed(1)
+    model = m.SETP2_BP_TRAIN(None, step1_crop="generalized").to(dev)
+    model.dense_kernels = kernels
+    net = m.dp.DataParallelRCCL(model)
+    opt = m.train.get_optimizer(net, "adam", 1e-4, 1e-7)
+    g = torch.Generator().manual_seed(4000 + rank)
+    h = B // 2
+    rgb0 = (torch.rand(h, 3, H, W, generator=g) * 255).to(dev)
+    rgb1 = (torch.rand(h, 3, H, W, generator=g) * 255).to(dev)
+    d0 = sparse_depth(g, h, H, W, dev)
+    d1 = sparse_depth(g, h, H, W, dev)
+    gt = sparse_depth(g, h, 480, 640, dev)  # the loss resizes every scale to 480x640 (utils.py:67)
+    net.train()
+
+    def step():
+        opt.zero_grad()
+        est, _ = net(rgb0, d0, rgb1, d1)
+        loss = m.train.calculate_loss_multi_resolution(est, gt, False)
+        loss.backward()
+        net.allreduce_grads()
+        opt.step()
+    return step
+
+
+def timed_steps(step, steps, warmup, world, dev, barrier):
+    for i in range(max(warmup, 1)):
+        t0 = time.perf_counter()
+        step()
+        torch.cuda.synchronize()
+        log(f"  warm-up step {i}: {time.perf_counter() - t0:.3f} s")
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    tt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([tt], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        tt = t.item()
+    return tt
+
+
 def make_train_step(m, dev, B, H, W, world, rank, graph=True):
     """One step-1 training iteration as train_step1.py:59-65: train-mode forward (EnforcePos
     drift), calculate_loss on element [0] with the gradient loss, backward, (RCCL gradient
@@ -249,6 +305,11 @@ def make_train_step(m, dev, B, H, W, world, rank, graph=True):
     return step
 
 
+def log(*msg):
+    """Progress on stderr (a long silent run looks hung to the GPU harness)."""
+    print("[bench]", *msg, file=sys.stderr, flush=True)
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -277,6 +338,7 @@ def main():
             dist.barrier()
 
     # ---- forward (headline) ----
+    log("config 2 forward")
     graph = None
     with torch.no_grad():
         for _ in range(max(a.warmup, 1)):
@@ -314,6 +376,7 @@ def main():
     fps = world * B * a.steps / t_fwd_max
 
     # ---- fwd + bwd + AdamW (config 4b) ----
+    log("config 2 forward done:", round(fps, 1), "frames/s; config 4b training step")
     train = None
     if not a.no_train:
         tg = (world == 1) if a.train_graph < 0 else bool(a.train_graph)
@@ -338,6 +401,7 @@ def main():
                  "hipgraph": tg}
 
     # ---- config 3: guided forward ----
+    log("config 3 guided forward")
     guided = None
     if not a.no_guided:
         gsteps = max(5, a.steps // 5)
@@ -351,9 +415,28 @@ def main():
                   "steps": gsteps, "frames_per_step": B * world,
                   "workload": "config3: SETP2_BP_EXPORT forward, B/2+B/2 frames per GPU, hipGraph"}
 
+    # ---- config 4: guided training step (per GPU B/2 + B/2 frames) ----
+    log("config 4 guided training step")
+    guided_train = None
+    if not a.no_guided_train:
+        gts = max(3, a.steps // 10)
+        tt = timed_steps(make_guided_train_step(m, dev, B, H, W, rank), gts, min(a.warmup, 2), world, dev, barrier)
+        guided_train = {"frames_per_sec": round(world * B * gts / tt, 2), "ms_per_step": round(tt / gts * 1e3, 3),
+                        "steps": gts, "frames_per_step": B * world,
+                        "workload": "config4: SETP2_BP_TRAIN fwd+bwd+AdamW, B/2+B/2 frames per GPU, dense convs "
+                                    "on libnconv MFMA kernels, eager"}
+        log("config 4 done:", guided_train["frames_per_sec"], "frames/s")
+        if a.guided_train_torch:
+            log("config 4 on the PyTorch-ROCm modules")
+            tt = timed_steps(make_guided_train_step(m, dev, B, H, W, rank, kernels=False), gts, min(a.warmup, 2),
+                             world, dev, barrier)
+            guided_train["torch_modules_frames_per_sec"] = round(world * B * gts / tt, 2)
+        torch.cuda.empty_cache()
+
     # ---- per-kernel times, roofline (rank 0) ----
     result = None
     if rank == 0:
+        log("per-layer kernel times")
         lt = time_layers(m, net, S)
         costs = layer_costs(B, H, W)
         costs["nconv6+7_tail"] = fused_tail_cost(B, H, W)
@@ -374,6 +457,7 @@ def main():
                 "whole_pass_hbm_frac": round(pass_bytes * a.steps / t_fwd / 1e9 / HBM_PEAK_GBS, 4) if pass_bytes else None}
         cpu = None
         if not a.no_cpu_baseline and world == 1:
+            log("CPU baseline")
             cpu = cpu_baseline(1, H, W, a.cpu_seconds)
         result = {
             "metric": "frames/sec (352x1216 sparse depth, DNET NConv U-Net forward, B=8 per GPU)",
@@ -387,6 +471,7 @@ def main():
                        "hipgraph": bool(graph is not None), "streams": a.streams},
             "train_fwd_bwd_adamw": train,
             "guided_fwd": guided,
+            "guided_train_fwd_bwd_adamw": guided_train,
             "layer_us": {k: round(v, 2) for k, v in lt.items()},
             "roofline": roof,
             "cpu_baseline": cpu,

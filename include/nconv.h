@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define NCONV_ABI_VERSION 4
+#define NCONV_ABI_VERSION 5
 
 /* How a layer's input (data x, confidence c) is produced from its source tensors. These are the
  * DNET glue ops fused into the layer's load stage (models/step1.py:53,61-90). */
@@ -131,7 +131,10 @@ int nconv_bwd(const nconv_layer* L, const float* y, const float* cout, const flo
 enum nconv_dense_kind {
     NCONV_DENSE_3X3 = 0,            /* Conv2d 3x3, padding 1, stride 1 or 2                      */
     NCONV_DENSE_1X1 = 1,            /* Conv2d 1x1, padding 0, stride 1 or 2                      */
-    NCONV_DENSE_TRANSPOSED_4X4 = 2  /* ConvTranspose2d 4x4, stride 2, padding 1 (Ho = 2H)        */
+    NCONV_DENSE_TRANSPOSED_4X4 = 2, /* ConvTranspose2d 4x4, stride 2, padding 1 (Ho = 2H, or the
+                                       cropped 2H - 1)                                           */
+    NCONV_DENSE_CONV4X4_S2 = 3      /* Conv2d 4x4, stride 2, padding 1, Ho = (H - 1) / 2 + 1: the
+                                       input gradient of the transposed convolution              */
 };
 
 typedef struct nconv_dense_conv {
@@ -139,7 +142,7 @@ typedef struct nconv_dense_conv {
     const float* x0; int C0;   /* input = cat(x0, x1) along channels: x0 (B, C0, H, W)          */
     const float* x1; int C1;   /* x1 (B, C1, H, W), or NULL / 0                                   */
     int H, W;
-    int Cout, Ho, Wo;          /* Cout in {32, 64}                                                */
+    int Cout, Ho, Wo;          /* any Cout >= 1 (tiled by 32 or 64 output channels)               */
     int kind, stride;
     const float* wpack;        /* nconv_dense_pack output                                         */
     const float* bias;         /* (Cout) or NULL                                                   */
@@ -153,7 +156,8 @@ typedef struct nconv_dense_conv {
 size_t nconv_dense_packed_floats(int kind, int Cin, int Cout);
 
 /* Pack w — Conv2d (Cout, Cin, k, k) or ConvTranspose2d (Cin, Cout, 4, 4) — into the kernel's
- * layout, multiplying output channel o by scale[o] if scale != NULL (eval BatchNorm folding). */
+ * layout, multiplying output channel o by scale[o] if scale != NULL (eval BatchNorm folding).
+ * The layout depends on (kind, Cin, Cout) only: a pack is valid for every call with those. */
 int nconv_dense_pack(int kind, int Cin, int Cout, const float* w, const float* scale, float* wpack,
                      void* stream);
 
@@ -165,6 +169,35 @@ int nconv_dense_conv_fwd(const nconv_dense_conv* c, void* stream);
  * (the depth heads `depth + Conv3x3(fout)`, models/step2.py:259,278). */
 int nconv_conv3x3_c1(const float* x, int B, int Cin, int H, int W, const float* w, const float* res,
                      float* out, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Training of the guided model: the weight gradient of a dense convolution.
+ * Replaces the autograd of nn.Conv2d / nn.ConvTranspose2d (convolution_backward, weight part) for
+ * the layers of models/step2.py listed above. The input gradient of a convolution is another
+ * convolution of dL/dy and runs on nconv_dense_conv_fwd with re-arranged weights (3x3 / 1x1
+ * stride 1: transposed, flipped; stride 2: NCONV_DENSE_TRANSPOSED_4X4 with the 3x3 / 1x1 kernel
+ * embedded, output cropped to H x W; transposed 4x4: NCONV_DENSE_CONV4X4_S2, same weights).
+ * The bias gradient is the sum of dL/dy over images and pixels.
+ * ------------------------------------------------------------------------------------------ */
+typedef struct nconv_dense_wgrad {
+    int B;
+    int kind, stride;          /* the forward convolution: NCONV_DENSE_3X3 / _1X1 (stride 1|2),
+                                  NCONV_DENSE_TRANSPOSED_4X4 (stride 2)                           */
+    const float* x0; int C0;   /* forward input = cat(x0, x1) along channels, (B, C0 + C1, H, W)  */
+    const float* x1; int C1;   /* NULL / 0 for one source                                         */
+    int H, W;
+    const float* gy;           /* dL/dy, (B, Cout, Ho, Wo)                                        */
+    int Cout, Ho, Wo;
+    float* gw;                 /* OVERWRITTEN: Conv2d (Cout, Cin, k, k) / ConvTranspose2d
+                                  (Cin, Cout, 4, 4). Limits: Cout <= 96 (conv), Cin <= 96
+                                  (transposed), Cin <= 64 (1x1)                                   */
+} nconv_dense_wgrad;
+
+/* Workspace of nconv_dense_conv_wgrad in bytes (0 if the descriptor is invalid). */
+size_t nconv_dense_wgrad_workspace_bytes(const nconv_dense_wgrad* g);
+
+/* gw = dL/dW: deterministic (fixed-order reduction of per-workgroup partial sums). */
+int nconv_dense_conv_wgrad(const nconv_dense_wgrad* g, void* workspace, size_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -13,13 +13,13 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # NCONV_LIB: an alternative build of the same library (kernel-tuning experiments)
 LIB_PATH = os.environ.get("NCONV_LIB") or os.path.join(_HERE, "libnconv.so")
-ABI_VERSION = 4
+ABI_VERSION = 5
 BWD_ACCUMULATE = 1
 
 # enum nconv_load_mode
 PLAIN, THRESH, POOL2, UPCAT_SKIP_FIRST, UPCAT_UP_FIRST = 0, 1, 2, 3, 4
 # enum nconv_dense_kind
-DENSE_3X3, DENSE_1X1, DENSE_TRANSPOSED_4X4 = 0, 1, 2
+DENSE_3X3, DENSE_1X1, DENSE_TRANSPOSED_4X4, DENSE_CONV4X4_S2 = 0, 1, 2, 3
 
 EXPORTED = (
     "nconv_abi_version",
@@ -34,6 +34,8 @@ EXPORTED = (
     "nconv_dense_pack",
     "nconv_dense_conv_fwd",
     "nconv_conv3x3_c1",
+    "nconv_dense_wgrad_workspace_bytes",
+    "nconv_dense_conv_wgrad",
 )
 
 
@@ -59,6 +61,13 @@ class NconvDenseConv(ctypes.Structure):
                 ("kind", ctypes.c_int), ("stride", ctypes.c_int), ("wpack", ctypes.c_void_p),
                 ("bias", ctypes.c_void_p), ("relu", ctypes.c_int), ("wshort", ctypes.c_void_p),
                 ("out", ctypes.c_void_p), ("out_C", ctypes.c_int), ("out_c0", ctypes.c_int)]
+
+
+class NconvDenseWgrad(ctypes.Structure):
+    _fields_ = [("B", ctypes.c_int), ("kind", ctypes.c_int), ("stride", ctypes.c_int),
+                ("x0", ctypes.c_void_p), ("C0", ctypes.c_int), ("x1", ctypes.c_void_p), ("C1", ctypes.c_int),
+                ("H", ctypes.c_int), ("W", ctypes.c_int), ("gy", ctypes.c_void_p), ("Cout", ctypes.c_int),
+                ("Ho", ctypes.c_int), ("Wo", ctypes.c_int), ("gw", ctypes.c_void_p)]
 
 
 _lib = None
@@ -94,6 +103,10 @@ def _declare(lib):
     lib.nconv_dense_conv_fwd.argtypes = [ctypes.POINTER(NconvDenseConv), P]
     lib.nconv_conv3x3_c1.restype = I
     lib.nconv_conv3x3_c1.argtypes = [P, I, I, I, I, P, P, P, P]
+    lib.nconv_dense_wgrad_workspace_bytes.restype = ctypes.c_size_t
+    lib.nconv_dense_wgrad_workspace_bytes.argtypes = [ctypes.POINTER(NconvDenseWgrad)]
+    lib.nconv_dense_conv_wgrad.restype = I
+    lib.nconv_dense_conv_wgrad.argtypes = [ctypes.POINTER(NconvDenseWgrad), P, ctypes.c_size_t, P]
 
 
 def lib():

@@ -3,21 +3,28 @@
 // The RGB encoder (models/step2.py:134-154) and the fusion decoder (step2.py:156-297) are plain
 // K x C x R x S contractions, so they run as implicit GEMMs on v_mfma_f32_32x32x2_f32 (fp32 in,
 // fp32 accumulate: exact f32 products, the precision of the reference's fp32 convolutions):
-//   A = weights  [Cout][k]        (M = output channels, 32 per tile)
+//   A = weights  [Cout][k]        (M = output channels, 32 or 64 per tile)
 //   B = im2col   [k][pixel]       (N = 32 output columns of one output row)
 //   k = (tap, input channel)      (K, input channels staged 8 at a time)
-// A workgroup (4 waves) owns an output tile of TH rows x 32 columns x all Cout of one image; each
-// wave owns TH/4 rows. Per 8-channel chunk the input patch (with halo) and the chunk's packed
-// weights are staged in LDS (loads for the next chunk issued before this chunk's MFMAs); an MFMA
-// k-step pairs two input channels (lane half kk = lane >> 5 takes channel 2p + kk), so every
-// operand read is one ds_read_b32 at a compile-time offset from a per-lane base. The epilogue
-// applies bias (eval BatchNorm folded in by nconv_dense_pack), ReLU and the RGBEncoder 1x1
-// shortcut (computed from the centre tap of the same patch) and writes a channel range of the
+// A workgroup (4 waves) owns an output tile of TH rows x 32 columns x one output-channel tile of
+// one image; each wave owns TH/4 rows. Per 8-channel chunk the input patch (with halo) and the
+// chunk's packed weights are staged in LDS (loads for the next chunk issued before this chunk's
+// MFMAs); an MFMA k-step pairs two input channels (lane half kk = lane >> 5 takes channel 2p + kk),
+// so every operand read is one ds_read_b32 at a compile-time offset from a per-lane base. The
+// epilogue applies bias (eval BatchNorm folded in by nconv_dense_pack), ReLU and the RGBEncoder
+// 1x1 shortcut (computed from the centre tap of the same patch) and writes a channel range of the
 // output tensor, so torch.cat of the decoder never materialises: convolutions write their half
 // of the concatenated tensor and the next one reads two sources.
 //
 // Kinds: 3x3 pad 1 stride 1|2; 1x1 stride 1|2; ConvTranspose 4x4 stride 2 pad 1 as four
-// output-parity classes, each a 2x2 gather over the input's 3x3 neighbourhood.
+// output-parity classes, each a 2x2 gather over the input's 3x3 neighbourhood (output 2H or,
+// cropped, 2H-1); Conv 4x4 stride 2 pad 1. Output channels are tiled by 32 or 64
+// (dense_cout_tile), one tile per workgroup, so any Cout runs.
+//
+// Training (dense.py's autograd functions): the input gradient of every kind is this same kernel
+// on re-arranged weights — 3x3 / 1x1 stride 1: transposed (+ flipped) kernel; stride 2: the
+// transposed 4x4 convolution with the 3x3 / 1x1 kernel embedded; ConvTranspose 4x4: the 4x4 s2
+// convolution with the same weights — and the weight gradient is dense_wgrad_mfma below.
 #include "nconv_internal.h"
 
 namespace nconv {
@@ -29,12 +36,23 @@ constexpr int round_mod64(int n, int target) {  // smallest m >= n with m % 64 =
     return n + (((target - n) % 64) + 64) % 64;
 }
 
+__host__ __device__ constexpr int dense_taps(int kind) {
+    return kind == NCONV_DENSE_3X3 ? 9 : kind == NCONV_DENSE_1X1 ? 1 : kind == NCONV_DENSE_TRANSPOSED_4X4 ? 4 : 16;
+}
+
+int dense_cout_tile(int Cout) {
+    if (Cout <= 32) return 32;
+    const int p32 = (Cout + 31) / 32 * 32, p64 = (Cout + 63) / 64 * 64;
+    return p32 < p64 ? 32 : 64;  // less padding; ties: 64 (the patch is staged once, not twice)
+}
+
 template <int COUT, int KIND, int S>
 struct DcCfg {
     static constexpr bool TR = KIND == NCONV_DENSE_TRANSPOSED_4X4;
-    static constexpr int TAPS = KIND == NCONV_DENSE_3X3 ? 9 : (KIND == NCONV_DENSE_1X1 ? 1 : 4);
+    static constexpr int TAPS = dense_taps(KIND);
     static constexpr int SP = TR ? 1 : S;                 // patch stride
-    static constexpr int KS = KIND == NCONV_DENSE_1X1 ? 1 : 3;
+    static constexpr int KS = KIND == NCONV_DENSE_1X1 ? 1 : (KIND == NCONV_DENSE_CONV4X4_S2 ? 4 : 3);
+    static constexpr int PAD = KIND == NCONV_DENSE_1X1 ? 0 : 1;
     static constexpr int TH = SP == 1 ? 8 : 4, RW = TH / 4, TW = 32;
     static constexpr int PR = (TH - 1) * SP + KS, PC = (TW - 1) * SP + KS;
     static constexpr int ROW = PC;
@@ -55,7 +73,7 @@ struct DcCfg {
 typedef float f16v __attribute__((ext_vector_type(16)));
 
 template <int COUT, int KIND, int S, bool SC>
-__global__ __launch_bounds__(kDT) void dense_conv_mfma(nconv_dense_conv p, int ntx, int nty) {
+__global__ __launch_bounds__(kDT) void dense_conv_mfma(nconv_dense_conv p, int ntx, int nty, int ncot) {
     using C = DcCfg<COUT, KIND, S>;
     __shared__ __attribute__((aligned(16))) float lds[C::LDS];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -65,12 +83,13 @@ __global__ __launch_bounds__(kDT) void dense_conv_mfma(nconv_dense_conv p, int n
     blk /= ntx;
     const int ty = blk % nty;
     blk /= nty;
+    const int cot = blk % ncot;  // output-channel tile
+    blk /= ncot;
     const int cls = C::TR ? blk % 4 : 0;  // output parity class (transposed)
     const int b = C::TR ? blk / 4 : blk;
     const int pa = cls >> 1, pb = cls & 1;
     const int oy0 = ty * C::TH, ox0 = tx * C::TW;  // tile origin (output grid, or class grid)
-    const int pad = C::TR ? 1 : (C::KS / 2);
-    const int iy0 = oy0 * C::SP - pad, ix0 = ox0 * C::SP - pad;  // patch origin in the input
+    const int iy0 = oy0 * C::SP - C::PAD, ix0 = ox0 * C::SP - C::PAD;  // patch origin in the input
     const int Cin = p.C0 + p.C1;
     const int nchunk = (Cin + kCK - 1) / kCK;
     const int HW = p.H * p.W;
@@ -91,14 +110,15 @@ __global__ __launch_bounds__(kDT) void dense_conv_mfma(nconv_dense_conv p, int n
                                          : p.x1 + ((size_t)b * p.C1 + (gc - p.C0)) * HW;
             pv[k] = in ? src[iy * p.W + ix] : 0.f;
         }
-        const f4* wg = reinterpret_cast<const f4*>(p.wpack + ((size_t)cls * nchunk + ch) * C::TAPS * kCK * COUT);
+        const f4* wg = reinterpret_cast<const f4*>(
+            p.wpack + (((size_t)cls * ncot + cot) * nchunk + ch) * C::TAPS * kCK * COUT);
 #pragma unroll
         for (int k = 0; k < C::NW4; ++k) {
             const int e = tid + kDT * k;
             if (e < C::TAPS * kCK * COUT / 4) wv[k] = wg[e];
         }
         if constexpr (SC) {
-            const f4* sg = reinterpret_cast<const f4*>(p.wshort + (size_t)ch * kCK * COUT);
+            const f4* sg = reinterpret_cast<const f4*>(p.wshort + ((size_t)cot * nchunk + ch) * kCK * COUT);
 #pragma unroll
             for (int k = 0; k < C::NS4; ++k) {
                 const int e = tid + kDT * k;
@@ -162,10 +182,10 @@ __global__ __launch_bounds__(kDT) void dense_conv_mfma(nconv_dense_conv p, int n
         // hoist every operand read of the chunk into registers); the 4 channel pairs unrolled
 #pragma unroll 1
         for (int t = 0; t < C::TAPS; ++t) {
-            // patch offset of this tap: 3x3 / 1x1 (kh, kw); transposed: the parity class picks
-            // rows (1 - tr) + pa and columns (1 - tc) + pb (pa, pb folded into bbase)
-            const int dr = C::TR ? 1 - t / 2 : (C::KS == 3 ? t / 3 : 0);
-            const int dc = C::TR ? 1 - t % 2 : (C::KS == 3 ? t % 3 : 0);
+            // patch offset of this tap: (kh, kw); transposed: the parity class picks rows
+            // (1 - tr) + pa and columns (1 - tc) + pb (pa, pb folded into bbase)
+            const int dr = C::TR ? 1 - t / 2 : t / C::KS;
+            const int dc = C::TR ? 1 - t % 2 : t % C::KS;
             const float* ap = lds + abase + t * kCK * C::COP;
             const float* bp = lds + bbase + dr * C::ROW + dc;
 #pragma unroll
@@ -197,18 +217,19 @@ __global__ __launch_bounds__(kDT) void dense_conv_mfma(nconv_dense_conv p, int n
 
     // ---- epilogue: bias, ReLU, shortcut; C[row = co][col = pixel]: col = lane & 31,
     //      row = (q & 3) + 8 (q >> 2) + 4 (lane >> 5) for register q ----
-    const int Hc = C::TR ? p.Ho / 2 : p.Ho, Wc = C::TR ? p.Wo / 2 : p.Wo;  // (class) grid
+    const int Hc = C::TR ? p.H : p.Ho, Wc = C::TR ? p.W : p.Wo;  // (class) grid
     const int ox = ox0 + li;
 #pragma unroll
     for (int r = 0; r < C::RW; ++r) {
         const int oy = oy0 + w * C::RW + r;
         if (oy >= Hc || ox >= Wc) continue;
         const int oyo = C::TR ? 2 * oy + pa : oy, oxo = C::TR ? 2 * ox + pb : ox;
+        if (C::TR && (oyo >= p.Ho || oxo >= p.Wo)) continue;  // cropped transposed output
 #pragma unroll
         for (int m = 0; m < C::MT; ++m)
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
-                const int co = 32 * m + (q & 3) + 8 * (q >> 2) + 4 * kk;
+                const int co = cot * COUT + 32 * m + (q & 3) + 8 * (q >> 2) + 4 * kk;
                 if (co >= p.Cout) continue;
                 float v = acc[m][r][q] + (p.bias ? p.bias[co] : 0.f);
                 if (p.relu) v = fmaxf(v, 0.f);
@@ -219,29 +240,35 @@ __global__ __launch_bounds__(kDT) void dense_conv_mfma(nconv_dense_conv p, int n
 }
 
 // ---- weight packing: (Cout, Cin, kh, kw) [conv] / (Cin, Cout, 4, 4) [transposed] ->
-//      [class][chunk][tap][ci 8][Cout], times an optional per-Cout scale (eval BatchNorm) --------
-__global__ __launch_bounds__(kDT) void dense_pack(int kind, int Cin, int Cout, const float* w, const float* scale,
-                                                  float* wp) {
-    const int taps = kind == NCONV_DENSE_3X3 ? 9 : (kind == NCONV_DENSE_1X1 ? 1 : 4);
+//      [class][cout tile][chunk][tap][ci 8][T], times an optional per-Cout scale (eval
+//      BatchNorm); channels past Cin / Cout are zero ----------------------------------------------
+__global__ __launch_bounds__(kDT) void dense_pack(int kind, int Cin, int Cout, int T, const float* w,
+                                                  const float* scale, float* wp) {
+    const int taps = dense_taps(kind);
     const int ncls = kind == NCONV_DENSE_TRANSPOSED_4X4 ? 4 : 1;
     const int nchunk = (Cin + kCK - 1) / kCK;
-    const size_t n = (size_t)ncls * nchunk * taps * kCK * Cout;
+    const int ncot = (Cout + T - 1) / T;
+    const size_t n = (size_t)ncls * ncot * nchunk * taps * kCK * T;
     for (size_t e = (size_t)blockIdx.x * kDT + threadIdx.x; e < n; e += (size_t)gridDim.x * kDT) {
-        const int co = (int)(e % Cout);
-        size_t r = e / Cout;
+        const int col = (int)(e % T);
+        size_t r = e / T;
         const int cil = (int)(r % kCK);
         r /= kCK;
         const int t = (int)(r % taps);
         r /= taps;
         const int ch = (int)(r % nchunk);
-        const int cls = (int)(r / nchunk);
-        const int ci = ch * kCK + cil;
+        r /= nchunk;
+        const int cot = (int)(r % ncot);
+        const int cls = (int)(r / ncot);
+        const int ci = ch * kCK + cil, co = cot * T + col;
         float v = 0.f;
-        if (ci < Cin) {
+        if (ci < Cin && co < Cout) {
             if (kind == NCONV_DENSE_3X3) {
                 v = w[((size_t)co * Cin + ci) * 9 + t];
             } else if (kind == NCONV_DENSE_1X1) {
                 v = w[(size_t)co * Cin + ci];
+            } else if (kind == NCONV_DENSE_CONV4X4_S2) {
+                v = w[((size_t)co * Cin + ci) * 16 + t];
             } else {  // ConvTranspose2d weight (Cin, Cout, 4, 4): class (pa, pb), tap (tr, tc)
                 const int pa = cls >> 1, pb = cls & 1, tr = t >> 1, tc = t & 1;
                 const int kh = 1 - pa + 2 * tr, kw = 1 - pb + 2 * tc;
@@ -317,12 +344,214 @@ __global__ __launch_bounds__(kDT) void conv3x3_c1(const float* __restrict__ x, i
 }
 
 // ------------------------------------------------------------------------------------------------
+// Weight gradients (training):  gW[m][n] = sum over images and pixels p of
+//     D[m][p] * P[n / TAPS][patch(p, n % TAPS)]
+//   Conv2d 3x3 pad 1 / 1x1, stride S:  pixels = output grid, D = dL/dy (m = co),
+//       P = the input x (n = ci*TAPS + kh*KS + kw) at (oy*S + kh - PAD, ox*S + kw - PAD);
+//   ConvTranspose2d 4x4 s2 p1:         pixels = input grid, D = the input x (m = ci),
+//       P = dL/dy (n = co*16 + kh*4 + kw) at (2 iy - 1 + kh, 2 ix - 1 + kw)
+// so gW's own layout (Conv2d (Cout, Cin, k, k) / ConvTranspose2d (Cin, Cout, 4, 4)) is [m][n].
+// Implicit GEMM on v_mfma_f32_32x32x2_f32: M = m (MT tiles of 32), N = n (NTW tiles of 32 per
+// wave, 4 waves), K = pixels (2 per MFMA). A block owns one group of NCOLS columns and a
+// contiguous range of 4 x 32 pixel tiles: per tile, D (MT*32 rows x 128 pixels) and the patch
+// planes of the channels its columns touch are staged in LDS (the next tile's loads in flight
+// during the MFMAs); pixel q = 2j + kk of k-step j of a tile row sits at a compile-time offset
+// from each lane's base. Each block writes its partial [M][N] to its K slice; dense_wgrad_reduce
+// adds the slices in a fixed order (deterministic, no float atomics).
+// ------------------------------------------------------------------------------------------------
+constexpr int wgd_ntw(int kind, int s) { return (kind == NCONV_DENSE_3X3 && s == 1) ? 2 : 1; }
+constexpr int wgd_ncols(int kind, int s) { return 4 * 32 * wgd_ntw(kind, s); }
+
+template <int KIND, int S, int MT>
+struct WgdCfg {
+    static constexpr bool TR = KIND == NCONV_DENSE_TRANSPOSED_4X4;
+    static constexpr int TAPS = KIND == NCONV_DENSE_3X3 ? 9 : (KIND == NCONV_DENSE_1X1 ? 1 : 16);
+    static constexpr int KS = KIND == NCONV_DENSE_3X3 ? 3 : (KIND == NCONV_DENSE_1X1 ? 1 : 4);
+    static constexpr int NTW = wgd_ntw(KIND, S);
+    static constexpr int NCOLS = wgd_ncols(KIND, S);
+    static constexpr int TH = 4, TW = 32, NPX = TH * TW;
+    // patch geometry: LDS step between neighbouring pixels (1x1 stages only the sampled
+    // positions), global step between neighbouring LDS columns, patch origin = pixel * OS - PAD
+    static constexpr int LS = KIND == NCONV_DENSE_1X1 ? 1 : (TR ? 2 : S);
+    static constexpr int GS = KIND == NCONV_DENSE_1X1 ? S : 1;
+    static constexpr int OS = TR ? 2 : S;
+    static constexpr int PAD = KIND == NCONV_DENSE_1X1 ? 0 : 1;
+    static constexpr int PR = (TH - 1) * LS + KS, PC = (TW - 1) * LS + KS;
+    static constexpr int PPLANE = PR * PC;
+    static constexpr int CPB0 = (NCOLS - 1) / TAPS + 2;
+    static constexpr int CPB = CPB0 < 64 ? CPB0 : 64;  // patch channels staged per block
+    static constexpr int DP = NPX + 2;                 // D row pitch: rows m, m+1 two banks apart
+    static constexpr int D_OFF = (CPB * PPLANE + 3) & ~3;
+    static constexpr int LDS = D_OFF + MT * 32 * DP;
+    static constexpr int NDE = MT * 32 * NPX / kDT;    // D elements per thread
+    static constexpr int NPE = (CPB * PPLANE + kDT - 1) / kDT;
+};
+
+struct WgdArgs {
+    const float* d0;
+    const float* d1;
+    int dC0, dC1;  // direct operand: M = dC0 + dC1 channels on the pixel grid
+    int Hp, Wp;    // pixel grid
+    const float* p0;
+    const float* p1;
+    int pC0, pC1;  // patch operand channels
+    int Hs, Ws;    // patch source planes
+    int M, N;      // N = (pC0 + pC1) * TAPS
+    int ntx, nty, nng, nks;
+    long long ntiles;
+};
+
+template <int KIND, int S, int MT>
+__global__ __launch_bounds__(kDT) void dense_wgrad_mfma(WgdArgs a, float* __restrict__ part) {
+    using C = WgdCfg<KIND, S, MT>;
+    __shared__ __attribute__((aligned(16))) float lds[C::LDS];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int ng = blockIdx.x % a.nng, ks = blockIdx.x / a.nng;
+    const int n0 = ng * C::NCOLS;
+    const int Cp = a.pC0 + a.pC1;
+    const int c_lo = n0 / C::TAPS;
+    int c_hi = (n0 + C::NCOLS - 1) / C::TAPS + 1;
+    c_hi = c_hi < Cp ? c_hi : Cp;
+    const long long t0 = a.ntiles * ks / a.nks, t1 = a.ntiles * (ks + 1) / a.nks;
+    const size_t HWp = (size_t)a.Hp * a.Wp, HWs = (size_t)a.Hs * a.Ws;
+
+    // per-lane operand bases (A: row m = mt*32 + li, B: column n of this wave's tile u)
+    const int kk = lane >> 5, li = lane & 31;
+    const int abase = C::D_OFF + li * C::DP + kk;
+    int bbase[C::NTW];
+#pragma unroll
+    for (int u = 0; u < C::NTW; ++u) {
+        const int n = n0 + (w * C::NTW + u) * 32 + li;
+        if (n < a.N) {
+            const int ci = n / C::TAPS - c_lo, tap = n % C::TAPS;
+            const int kh = tap / C::KS, kw = tap % C::KS;
+            bbase[u] = ci * C::PPLANE + kh * C::PC + kw + kk * C::LS;
+        } else {
+            bbase[u] = kk * C::LS;  // any in-range address: the column is never written
+        }
+    }
+
+    f16v acc[MT][C::NTW];
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int u = 0; u < C::NTW; ++u) acc[m][u] = (f16v){};
+
+    float dv[C::NDE], pv[C::NPE];
+    auto load = [&](long long t) {
+        // the per-element coordinates below are recomputed per tile (tid made opaque): hoisted
+        // out of the tile loop they would pin ~4 registers per staged element
+        int tq = tid;
+        asm volatile("" : "+v"(tq));
+        const int tx = (int)(t % a.ntx);
+        const long long rr = t / a.ntx;
+        const int ty = (int)(rr % a.nty), b = (int)(rr / a.nty);
+        const int py0 = ty * C::TH, px0 = tx * C::TW;
+#pragma unroll
+        for (int k = 0; k < C::NDE; ++k) {
+            const int e = tq + kDT * k;
+            const int m = e / C::NPX, q = e % C::NPX;  // m is wave-uniform
+            const int py = py0 + q / C::TW, px = px0 + q % C::TW;
+            const bool ok = m < a.M && py < a.Hp && px < a.Wp;
+            const float* src = m < a.dC0 ? a.d0 + ((size_t)b * a.dC0 + m) * HWp
+                                         : a.d1 + ((size_t)b * a.dC1 + (m - a.dC0)) * HWp;
+            dv[k] = ok ? src[(size_t)py * a.Wp + px] : 0.f;
+        }
+        const int iy0 = py0 * C::OS - C::PAD, ix0 = px0 * C::OS - C::PAD;
+#pragma unroll
+        for (int k = 0; k < C::NPE; ++k) {
+            const int e = tq + kDT * k;
+            const int ci = e / C::PPLANE, rem = e % C::PPLANE;
+            const int r = rem / C::PC, c = rem % C::PC;
+            const int gc = c_lo + ci, iy = iy0 + r * C::GS, ix = ix0 + c * C::GS;
+            const bool ok = e < C::CPB * C::PPLANE && gc < c_hi && (unsigned)iy < (unsigned)a.Hs &&
+                            (unsigned)ix < (unsigned)a.Ws;
+            const float* src = gc < a.pC0 ? a.p0 + ((size_t)b * a.pC0 + gc) * HWs
+                                          : a.p1 + ((size_t)b * a.pC1 + (gc - a.pC0)) * HWs;
+            pv[k] = ok ? src[(size_t)iy * a.Ws + ix] : 0.f;
+        }
+    };
+    auto store = [&]() {
+#pragma unroll
+        for (int k = 0; k < C::NDE; ++k) {
+            const int e = tid + kDT * k;
+            lds[C::D_OFF + (e / C::NPX) * C::DP + e % C::NPX] = dv[k];
+        }
+#pragma unroll
+        for (int k = 0; k < C::NPE; ++k) {
+            const int e = tid + kDT * k;
+            if (e < C::CPB * C::PPLANE) lds[e] = pv[k];
+        }
+    };
+
+    if (t0 < t1) load(t0);
+#pragma unroll 1
+    for (long long t = t0; t < t1; ++t) {
+        __syncthreads();  // the previous tile's MFMAs are done with the LDS
+        store();
+        __syncthreads();
+        if (t + 1 < t1) load(t + 1);
+#pragma unroll 1
+        for (int r = 0; r < C::TH; ++r) {
+            const float* ap = lds + abase + r * C::TW;
+            const int boff = r * C::LS * C::PC;
+#pragma unroll
+            for (int j = 0; j < C::TW / 2; ++j) {
+                float av[MT], bv[C::NTW];
+#pragma unroll
+                for (int m = 0; m < MT; ++m) av[m] = ap[m * 32 * C::DP + 2 * j];
+#pragma unroll
+                for (int u = 0; u < C::NTW; ++u) bv[u] = lds[bbase[u] + boff + 2 * j * C::LS];
+#pragma unroll
+                for (int m = 0; m < MT; ++m)
+#pragma unroll
+                    for (int u = 0; u < C::NTW; ++u)
+                        acc[m][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[m], bv[u], acc[m][u], 0, 0, 0);
+            }
+        }
+    }
+
+    // ---- partial [M][N] of this K slice: C[row = m][col = n] ----
+    float* out = part + (size_t)ks * a.M * a.N;
+#pragma unroll
+    for (int u = 0; u < C::NTW; ++u) {
+        const int n = n0 + (w * C::NTW + u) * 32 + li;
+        if (n >= a.N) continue;
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int row = 32 * m + (q & 3) + 8 * (q >> 2) + 4 * kk;
+                if (row < a.M) out[(size_t)row * a.N + n] = acc[m][u][q];
+            }
+    }
+}
+
+// gw[e] = sum over the nks slices of part[slice][e]: 64 elements x 4 slice phases per block,
+// each phase summing every 4th slice in order, the phases combined in a fixed order.
+__global__ __launch_bounds__(kDT) void dense_wgrad_reduce(const float* __restrict__ part, int nks, int mn,
+                                                          float* __restrict__ gw) {
+    __shared__ float red[4][64];
+    const int col = threadIdx.x & 63, ph = threadIdx.x >> 6;
+    const int e = blockIdx.x * 64 + col;
+    float s = 0.f;
+    if (e < mn) {
+#pragma unroll 8
+        for (int k = ph; k < nks; k += 4) s += part[(size_t)k * mn + e];
+    }
+    red[ph][col] = s;
+    __syncthreads();
+    if (ph == 0 && e < mn) gw[e] = ((red[0][col] + red[1][col]) + red[2][col]) + red[3][col];
+}
+
+// ------------------------------------------------------------------------------------------------
 // Launchers
 // ------------------------------------------------------------------------------------------------
 size_t dense_packed_floats(int kind, int Cin, int Cout) {
-    const int taps = kind == NCONV_DENSE_3X3 ? 9 : (kind == NCONV_DENSE_1X1 ? 1 : 4);
     const int ncls = kind == NCONV_DENSE_TRANSPOSED_4X4 ? 4 : 1;
-    return (size_t)ncls * ((Cin + kCK - 1) / kCK) * taps * kCK * Cout;
+    const int T = dense_cout_tile(Cout);
+    return (size_t)ncls * ((Cout + T - 1) / T) * ((Cin + kCK - 1) / kCK) * dense_taps(kind) * kCK * T;
 }
 
 int launch_dense_pack(int kind, int Cin, int Cout, const float* w, const float* scale, float* wp, hipStream_t st,
@@ -330,7 +559,9 @@ int launch_dense_pack(int kind, int Cin, int Cout, const float* w, const float* 
     const size_t n = dense_packed_floats(kind, Cin, Cout);
     size_t blocks = (n + kDT - 1) / kDT;
     if (blocks > 4096) blocks = 4096;
-    if (blocks) hipLaunchKernelGGL(dense_pack, dim3(blocks), dim3(kDT), 0, st, kind, Cin, Cout, w, scale, wp);
+    if (blocks)
+        hipLaunchKernelGGL(dense_pack, dim3(blocks), dim3(kDT), 0, st, kind, Cin, Cout, dense_cout_tile(Cout), w,
+                           scale, wp);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         *why = hipGetErrorString(e);
@@ -342,15 +573,16 @@ int launch_dense_pack(int kind, int Cin, int Cout, const float* w, const float* 
 template <int COUT, int KIND, int S, bool SC>
 static void go_dense(const nconv_dense_conv& p, hipStream_t st) {
     using C = DcCfg<COUT, KIND, S>;
-    const int Hc = C::TR ? p.Ho / 2 : p.Ho, Wc = C::TR ? p.Wo / 2 : p.Wo;
+    const int Hc = C::TR ? p.H : p.Ho, Wc = C::TR ? p.W : p.Wo;
     const int ntx = (Wc + C::TW - 1) / C::TW, nty = (Hc + C::TH - 1) / C::TH;
-    const int blocks = ntx * nty * p.B * (C::TR ? 4 : 1);
-    hipLaunchKernelGGL((dense_conv_mfma<COUT, KIND, S, SC>), dim3(blocks), dim3(kDT), 0, st, p, ntx, nty);
+    const int ncot = (p.Cout + COUT - 1) / COUT;
+    const int blocks = ntx * nty * ncot * p.B * (C::TR ? 4 : 1);
+    hipLaunchKernelGGL((dense_conv_mfma<COUT, KIND, S, SC>), dim3(blocks), dim3(kDT), 0, st, p, ntx, nty, ncot);
 }
 
 int launch_dense_conv(const nconv_dense_conv& p, hipStream_t st, const char** why) {
     const bool sc = p.wshort != nullptr;
-    const int co = p.Cout <= 32 ? 32 : 64;
+    const int co = dense_cout_tile(p.Cout);
 #define NCONV_DC(COUT_, KIND_, S_, SC_)                                                   \
     if (co == COUT_ && p.kind == KIND_ && p.stride == S_ && sc == SC_) {                  \
         go_dense<COUT_, KIND_, S_, SC_>(p, st);                                             \
@@ -375,8 +607,10 @@ int launch_dense_conv(const nconv_dense_conv& p, hipStream_t st, const char** wh
     NCONV_DC(64, NCONV_DENSE_1X1, 2, false)
     NCONV_DC(32, NCONV_DENSE_TRANSPOSED_4X4, 2, false)
     NCONV_DC(64, NCONV_DENSE_TRANSPOSED_4X4, 2, false)
+    NCONV_DC(32, NCONV_DENSE_CONV4X4_S2, 2, false)
+    NCONV_DC(64, NCONV_DENSE_CONV4X4_S2, 2, false)
 #undef NCONV_DC
-    *why = "no dense-conv kernel for this (Cout, kind, stride, shortcut) combination";
+    *why = "no dense-conv kernel for this (kind, stride, shortcut) combination";
     return -95;
 }
 
@@ -384,6 +618,102 @@ int launch_conv3x3_c1(const float* x, int B, int Cin, int H, int W, const float*
                       hipStream_t st, const char** why) {
     const int ntx = (W + 63) / 64, nty = (H + 15) / 16;
     hipLaunchKernelGGL(conv3x3_c1, dim3(ntx * nty * B), dim3(kDT), 0, st, x, Cin, H, W, w, res, out, ntx, nty);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        *why = hipGetErrorString(e);
+        return -5;
+    }
+    return 0;
+}
+
+// ---- weight gradient ----
+constexpr int kWgdTargetBlocks = 512;  // two 4-wave blocks per CU (LDS 58-75 KB each): one round
+
+static WgdArgs wgrad_args(const nconv_dense_wgrad& g) {
+    WgdArgs a{};
+    const int cin = g.C0 + g.C1;
+    if (g.kind != NCONV_DENSE_TRANSPOSED_4X4) {  // Conv2d: D = dL/dy, patch = x
+        a.d0 = g.gy;
+        a.d1 = nullptr;
+        a.dC0 = g.Cout;
+        a.dC1 = 0;
+        a.Hp = g.Ho;
+        a.Wp = g.Wo;
+        a.p0 = g.x0;
+        a.p1 = g.x1;
+        a.pC0 = g.C0;
+        a.pC1 = g.C1;
+        a.Hs = g.H;
+        a.Ws = g.W;
+        a.M = g.Cout;
+        a.N = cin * dense_taps(g.kind);
+    } else {  // ConvTranspose2d: D = x, patch = dL/dy
+        a.d0 = g.x0;
+        a.d1 = g.x1;
+        a.dC0 = g.C0;
+        a.dC1 = g.C1;
+        a.Hp = g.H;
+        a.Wp = g.W;
+        a.p0 = g.gy;
+        a.p1 = nullptr;
+        a.pC0 = g.Cout;
+        a.pC1 = 0;
+        a.Hs = g.Ho;
+        a.Ws = g.Wo;
+        a.M = cin;
+        a.N = g.Cout * 16;
+    }
+    a.ntx = (a.Wp + 31) / 32;
+    a.nty = (a.Hp + 3) / 4;
+    a.ntiles = (long long)g.B * a.ntx * a.nty;
+    const int ncols = wgd_ncols(g.kind, g.stride);
+    a.nng = (a.N + ncols - 1) / ncols;
+    long long nks = kWgdTargetBlocks / a.nng;
+    if (nks < 1) nks = 1;
+    if (nks > a.ntiles) nks = a.ntiles;
+    a.nks = (int)nks;
+    return a;
+}
+
+size_t dense_wgrad_workspace_bytes(const nconv_dense_wgrad& g) {
+    const WgdArgs a = wgrad_args(g);
+    return (size_t)a.nks * a.M * a.N * sizeof(float);
+}
+
+template <int KIND, int S>
+static void go_wgrad(const WgdArgs& a, float* part, hipStream_t st) {
+    const dim3 grid(a.nng * a.nks), blk(kDT);
+    const int mt = (a.M + 31) / 32;
+    if (mt == 1)
+        hipLaunchKernelGGL((dense_wgrad_mfma<KIND, S, 1>), grid, blk, 0, st, a, part);
+    else if (mt == 2)
+        hipLaunchKernelGGL((dense_wgrad_mfma<KIND, S, 2>), grid, blk, 0, st, a, part);
+    else
+        hipLaunchKernelGGL((dense_wgrad_mfma<KIND, S, 3>), grid, blk, 0, st, a, part);
+}
+
+int launch_dense_wgrad(const nconv_dense_wgrad& g, float* ws, size_t ws_bytes, hipStream_t st, const char** why) {
+    const WgdArgs a = wgrad_args(g);
+    if (ws_bytes < (size_t)a.nks * a.M * a.N * sizeof(float)) {
+        *why = "workspace too small (see nconv_dense_wgrad_workspace_bytes)";
+        return -22;
+    }
+    if (g.kind == NCONV_DENSE_3X3 && g.stride == 1)
+        go_wgrad<NCONV_DENSE_3X3, 1>(a, ws, st);
+    else if (g.kind == NCONV_DENSE_3X3 && g.stride == 2)
+        go_wgrad<NCONV_DENSE_3X3, 2>(a, ws, st);
+    else if (g.kind == NCONV_DENSE_1X1 && g.stride == 1)
+        go_wgrad<NCONV_DENSE_1X1, 1>(a, ws, st);
+    else if (g.kind == NCONV_DENSE_1X1 && g.stride == 2)
+        go_wgrad<NCONV_DENSE_1X1, 2>(a, ws, st);
+    else if (g.kind == NCONV_DENSE_TRANSPOSED_4X4 && g.stride == 2)
+        go_wgrad<NCONV_DENSE_TRANSPOSED_4X4, 2>(a, ws, st);
+    else {
+        *why = "no weight-gradient kernel for this (kind, stride)";
+        return -95;
+    }
+    const int mn = a.M * a.N;
+    hipLaunchKernelGGL(dense_wgrad_reduce, dim3((mn + 63) / 64), dim3(kDT), 0, st, ws, a.nks, mn, g.gw);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         *why = hipGetErrorString(e);

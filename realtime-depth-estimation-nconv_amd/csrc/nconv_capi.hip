@@ -51,6 +51,33 @@ const char* validate(const nconv_layer* L, bool need_c) {
     return nullptr;
 }
 
+const char* validate_wgrad(const nconv_dense_wgrad* g) {
+    if (!g) return "null descriptor";
+    if (g->B <= 0 || g->C0 <= 0 || g->C1 < 0 || g->H <= 0 || g->W <= 0 || g->Cout <= 0)
+        return "non-positive B/C0/H/W/Cout";
+    if (!g->x0 || (g->C1 > 0 && !g->x1) || !g->gy || !g->gw) return "null pointer";
+    const int cin = g->C0 + g->C1;
+    switch (g->kind) {
+        case NCONV_DENSE_3X3:
+        case NCONV_DENSE_1X1:
+            if (g->stride != 1 && g->stride != 2) return "stride must be 1 or 2";
+            if (g->Ho != (g->H - 1) / g->stride + 1 || g->Wo != (g->W - 1) / g->stride + 1)
+                return "Ho/Wo inconsistent with kind/stride/H/W";
+            if (g->Cout > 96) return "weight gradient supports at most 96 output channels";
+            if (g->kind == NCONV_DENSE_1X1 && cin > 64) return "1x1 weight gradient supports at most 64 input channels";
+            break;
+        case NCONV_DENSE_TRANSPOSED_4X4:
+            if (g->stride != 2) return "transposed 4x4 has stride 2";
+            if ((g->Ho != 2 * g->H && g->Ho != 2 * g->H - 1) || (g->Wo != 2 * g->W && g->Wo != 2 * g->W - 1))
+                return "Ho/Wo inconsistent with kind/stride/H/W";
+            if (cin > 96) return "transposed weight gradient supports at most 96 input channels";
+            break;
+        default:
+            return "unknown kind (weight gradients: 3x3, 1x1, transposed 4x4)";
+    }
+    return nullptr;
+}
+
 LayerDev make_dev(const nconv_layer* L) {
     LayerDev d;
     d.L = *L;
@@ -137,12 +164,12 @@ int nconv_bwd(const nconv_layer* L, const float* y, const float* cout, const flo
 }
 
 size_t nconv_dense_packed_floats(int kind, int Cin, int Cout) {
-    if (kind < NCONV_DENSE_3X3 || kind > NCONV_DENSE_TRANSPOSED_4X4 || Cin <= 0 || Cout <= 0) return 0;
+    if (kind < NCONV_DENSE_3X3 || kind > NCONV_DENSE_CONV4X4_S2 || Cin <= 0 || Cout <= 0) return 0;
     return nconv::dense_packed_floats(kind, Cin, Cout);
 }
 
 int nconv_dense_pack(int kind, int Cin, int Cout, const float* w, const float* scale, float* wpack, void* stream) {
-    if (kind < NCONV_DENSE_3X3 || kind > NCONV_DENSE_TRANSPOSED_4X4) return fail(-22, "nconv_dense_pack", "unknown kind");
+    if (kind < NCONV_DENSE_3X3 || kind > NCONV_DENSE_CONV4X4_S2) return fail(-22, "nconv_dense_pack", "unknown kind");
     if (Cin <= 0 || Cout <= 0) return fail(-22, "nconv_dense_pack", "non-positive Cin/Cout");
     if (!w || !wpack) return fail(-22, "nconv_dense_pack", "null weight pointer");
     const char* why = nullptr;
@@ -155,7 +182,7 @@ int nconv_dense_conv_fwd(const nconv_dense_conv* c, void* stream) {
     if (!c) return fail(-22, fn, "null descriptor");
     if (c->B <= 0 || c->H <= 0 || c->W <= 0 || c->C0 <= 0 || c->C1 < 0) return fail(-22, fn, "non-positive B/H/W/C0");
     if (!c->x0 || (c->C1 > 0 && !c->x1)) return fail(-22, fn, "null input pointer");
-    if (c->Cout != 32 && c->Cout != 64) return fail(-95, fn, "Cout must be 32 or 64");
+    if (c->Cout <= 0) return fail(-22, fn, "non-positive Cout");
     if (!c->wpack || !c->out) return fail(-22, fn, "null weight / output pointer");
     if (c->out_c0 < 0 || c->out_c0 + c->Cout > c->out_C) return fail(-22, fn, "output channel range exceeds out_C");
     int ho, wo;
@@ -174,8 +201,16 @@ int nconv_dense_conv_fwd(const nconv_dense_conv* c, void* stream) {
         case NCONV_DENSE_TRANSPOSED_4X4:
             if (c->stride != 2) return fail(-22, fn, "transposed 4x4 has stride 2");
             if (c->wshort) return fail(-22, fn, "no shortcut for the transposed convolution");
-            ho = 2 * c->H;
-            wo = 2 * c->W;
+            // 2H x 2W, or cropped by one row / column (the input gradient of a stride-2 conv of
+            // an odd-sized input)
+            ho = (c->Ho == 2 * c->H - 1) ? c->Ho : 2 * c->H;
+            wo = (c->Wo == 2 * c->W - 1) ? c->Wo : 2 * c->W;
+            break;
+        case NCONV_DENSE_CONV4X4_S2:
+            if (c->stride != 2) return fail(-22, fn, "conv 4x4 has stride 2");
+            if (c->wshort) return fail(-22, fn, "shortcut only with a 3x3 main convolution");
+            ho = (c->H - 1) / 2 + 1;
+            wo = (c->W - 1) / 2 + 1;
             break;
         default:
             return fail(-22, fn, "unknown kind");
@@ -183,6 +218,21 @@ int nconv_dense_conv_fwd(const nconv_dense_conv* c, void* stream) {
     if (ho != c->Ho || wo != c->Wo) return fail(-22, fn, "Ho/Wo inconsistent with kind/stride/H/W");
     const char* why = nullptr;
     int rc = nconv::launch_dense_conv(*c, (hipStream_t)stream, &why);
+    return rc ? fail(rc, fn, why) : 0;
+}
+
+size_t nconv_dense_wgrad_workspace_bytes(const nconv_dense_wgrad* g) {
+    if (validate_wgrad(g)) return 0;
+    return nconv::dense_wgrad_workspace_bytes(*g);
+}
+
+int nconv_dense_conv_wgrad(const nconv_dense_wgrad* g, void* workspace, size_t workspace_bytes, void* stream) {
+    const char* fn = "nconv_dense_conv_wgrad";
+    if (const char* why = validate_wgrad(g)) return fail(-22, fn, why);
+    const size_t need = nconv::dense_wgrad_workspace_bytes(*g);
+    if (need && (!workspace || workspace_bytes < need)) return fail(-22, fn, "workspace too small");
+    const char* why = nullptr;
+    int rc = nconv::launch_dense_wgrad(*g, (float*)workspace, workspace_bytes, (hipStream_t)stream, &why);
     return rc ? fail(rc, fn, why) : 0;
 }
 

@@ -44,11 +44,14 @@ size_t bwd_workspace_bytes(const LayerDev& d);
 int launch_bwd(const LayerDev& d, const BwdArgs& a, hipStream_t st, const char** why);
 
 // Dense convolutions (RGB-guided model).
+int dense_cout_tile(int Cout);
 size_t dense_packed_floats(int kind, int Cin, int Cout);
 int launch_dense_pack(int kind, int Cin, int Cout, const float* w, const float* scale, float* wp, hipStream_t st,
                       const char** why);
 int launch_dense_conv(const nconv_dense_conv& p, hipStream_t st, const char** why);
 int launch_conv3x3_c1(const float* x, int B, int Cin, int H, int W, const float* w, const float* res, float* out,
                       hipStream_t st, const char** why);
+size_t dense_wgrad_workspace_bytes(const nconv_dense_wgrad& g);
+int launch_dense_wgrad(const nconv_dense_wgrad& g, float* ws, size_t ws_bytes, hipStream_t st, const char** why);
 
 }  // namespace nconv

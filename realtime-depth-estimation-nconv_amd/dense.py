@@ -1,16 +1,21 @@
-"""Dense convolutions of the RGB-guided model on libnconv's matrix-core kernels (eval mode).
+"""Dense convolutions of the RGB-guided model on libnconv's matrix-core kernels.
 
-Host side of nconv_dense_conv_fwd / nconv_dense_pack / nconv_conv3x3_c1 (include/nconv.h): weight
-packing with eval-BatchNorm folding, cached per module and rebuilt when a weight / BN tensor
-changes (torch's in-place version counters), and the launch wrappers. Used by guided.py's
-inference path; training keeps the PyTorch modules (BatchNorm batch statistics, autograd).
+Host side of nconv_dense_conv_fwd / nconv_dense_pack / nconv_conv3x3_c1 / nconv_dense_conv_wgrad
+(include/nconv.h):
+  * inference (guided.py's eval path): weight packing with eval-BatchNorm folding, cached per
+    module and rebuilt when a weight / BN tensor changes (torch's in-place version counters);
+  * training (guided.py's train path): autograd functions for Conv2d 3x3 / 1x1 and
+    ConvTranspose2d 4x4 s2 (+ bias, + fused ReLU, two-source input = the reference's torch.cat)
+    and for the 3x3 -> 1 depth heads. Backward: the input gradient is the forward kernel on
+    re-arranged weights (_dgrad_plan), the weight gradient nconv_dense_conv_wgrad, the bias
+    gradient a reduction; BatchNorm (batch statistics) stays a PyTorch-ROCm op between them.
 """
 import ctypes
 
 import torch
 
 from . import _lib
-from ._lib import DENSE_1X1, DENSE_3X3, DENSE_TRANSPOSED_4X4  # noqa: F401  (re-exported)
+from ._lib import DENSE_1X1, DENSE_3X3, DENSE_CONV4X4_S2, DENSE_TRANSPOSED_4X4  # noqa: F401  (re-exported)
 
 
 def bn_fold(bn, conv_bias=None):
@@ -47,7 +52,9 @@ def conv(x0, kind, stride, wpack, bias, relu, cout, x1=None, wshort=None, out=No
     """[relu](conv(cat(x0, x1)) + bias) [+ shortcut]; written to out[:, out_c0:out_c0+cout] if out is given."""
     B, C0, H, W = x0.shape
     C1 = 0 if x1 is None else x1.shape[1]
-    if kind == DENSE_TRANSPOSED_4X4:
+    if out is not None:  # (a transposed convolution may write a cropped 2H-1 x 2W-1 output)
+        Ho, Wo = out.shape[2], out.shape[3]
+    elif kind == DENSE_TRANSPOSED_4X4:
         Ho, Wo = 2 * H, 2 * W
     else:
         Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
@@ -76,3 +83,128 @@ def conv3x3_c1(x, w, res=None):
     _lib.check(_lib.lib().nconv_conv3x3_c1(_lib.ptr(x), B, C, H, W, _lib.ptr(w), _lib.ptr(res), _lib.ptr(out),
                                            _lib.stream_handle(x.device)), "nconv_conv3x3_c1")
     return out
+
+
+# ------------------------------------------------------------------------------------------------
+# Training: autograd functions
+# ------------------------------------------------------------------------------------------------
+def _dgrad_plan(weight, kind, stride):
+    """The input gradient of conv(x; weight) as another convolution of dL/dy on the same kernels:
+    (kind', stride', weight' in kind's layout, Cin', Cout').
+      3x3 / 1x1 stride 1: the transposed, flipped kernel (Ci, Co, k, k), same geometry;
+      3x3 / 1x1 stride 2: ConvTranspose 4x4 s2 p1 whose (Co, Ci, 4, 4) kernel embeds the 3x3
+                          kernel at [0:3, 0:3] (the 1x1 at [1, 1]), output cropped to H x W;
+      ConvTranspose 4x4 s2 p1 (Ci, Co, 4, 4): Conv 4x4 s2 p1 with the same tensor read as a
+                          (Cout' = Ci, Cin' = Co) Conv2d weight."""
+    w = weight.detach()
+    if kind == DENSE_TRANSPOSED_4X4:
+        return DENSE_CONV4X4_S2, 2, w.contiguous(), w.shape[1], w.shape[0]
+    co, ci = w.shape[0], w.shape[1]
+    if stride == 1:
+        return kind, 1, w.transpose(0, 1).flip(2, 3).contiguous(), co, ci
+    w4 = w.new_zeros((co, ci, 4, 4))
+    if kind == DENSE_3X3:
+        w4[:, :, :3, :3] = w
+    else:
+        w4[:, :, 1, 1] = w[:, :, 0, 0]
+    return DENSE_TRANSPOSED_4X4, 2, w4, co, ci
+
+
+def dgrad(g, weight, kind, stride, in_shape):
+    """dL/dx (B, Cin, H, W) of conv(x; weight) from g = dL/dy (contiguous)."""
+    k2, s2, w2, cin2, cout2 = _dgrad_plan(weight, kind, stride)
+    B, _, H, W = in_shape
+    out = torch.empty((B, cout2, H, W), device=g.device, dtype=torch.float32)
+    return conv(g, k2, s2, pack(k2, w2, cin2, cout2), None, False, cout2, out=out)
+
+
+def wgrad(x0, x1, g, kind, stride, wshape):
+    """dL/dW of conv(cat(x0, x1); W) from g = dL/dy (nconv_dense_conv_wgrad; deterministic)."""
+    L = _lib.lib()
+    d = _lib.NconvDenseWgrad()
+    d.B, d.kind, d.stride = x0.shape[0], kind, stride
+    d.x0, d.C0 = x0.data_ptr(), x0.shape[1]
+    d.x1, d.C1 = (x1.data_ptr(), x1.shape[1]) if x1 is not None else (None, 0)
+    d.H, d.W = x0.shape[2], x0.shape[3]
+    d.gy, d.Cout, d.Ho, d.Wo = g.data_ptr(), g.shape[1], g.shape[2], g.shape[3]
+    gw = torch.empty(wshape, device=x0.device, dtype=torch.float32)
+    d.gw = gw.data_ptr()
+    nbytes = L.nconv_dense_wgrad_workspace_bytes(ctypes.byref(d))
+    ws = torch.empty(max(nbytes, 4) // 4, device=x0.device, dtype=torch.float32)
+    _lib.check(L.nconv_dense_conv_wgrad(ctypes.byref(d), _lib.ptr(ws), nbytes, _lib.stream_handle(x0.device)),
+               "nconv_dense_conv_wgrad")
+    return gw
+
+
+class DenseConvFn(torch.autograd.Function):
+    """y = [relu](conv(cat(x0, x1); weight) + bias) for Conv2d 3x3 pad 1 / 1x1 (stride 1 | 2) and
+    ConvTranspose2d 4x4 s2 p1 — nn.Conv2d / nn.ConvTranspose2d (+ ReLU, + the torch.cat before
+    them) of models/step2.py — forward and backward on libnconv's MFMA kernels."""
+
+    @staticmethod
+    def forward(ctx, x0, x1, weight, bias, kind, stride, relu):
+        x0 = x0.contiguous()
+        x1 = x1.contiguous() if x1 is not None else None
+        cin = x0.shape[1] + (0 if x1 is None else x1.shape[1])
+        cout = weight.shape[1] if kind == DENSE_TRANSPOSED_4X4 else weight.shape[0]
+        wp = pack(kind, weight, cin, cout)
+        b = bias.detach().contiguous() if bias is not None else None
+        out = conv(x0, kind, stride, wp, b, relu, cout, x1=x1)
+        ctx.kind, ctx.stride, ctx.relu, ctx.c0 = kind, stride, relu, x0.shape[1]
+        ctx.has_bias = bias is not None
+        ctx.save_for_backward(x0, x1, weight, out if relu else None)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        x0, x1, weight, out = ctx.saved_tensors
+        g = g.contiguous()
+        if ctx.relu:  # ReLU backward: gradient where the output is positive
+            g = g.masked_fill(out <= 0, 0.0)
+        need = ctx.needs_input_grad
+        gx0 = gx1 = gw = gb = None
+        if need[0] or need[1]:
+            cin = x0.shape[1] + (0 if x1 is None else x1.shape[1])
+            gx = dgrad(g, weight, ctx.kind, ctx.stride, (x0.shape[0], cin, x0.shape[2], x0.shape[3]))
+            if x1 is None:
+                gx0 = gx
+            else:
+                gx0, gx1 = gx[:, :ctx.c0], gx[:, ctx.c0:]
+        if need[2]:
+            gw = wgrad(x0, x1, g, ctx.kind, ctx.stride, weight.shape)
+        if ctx.has_bias and need[3]:
+            gb = g.sum(dim=(0, 2, 3))
+        return gx0, gx1, gw, gb, None, None, None
+
+
+def conv_fn(x0, weight, bias, kind, stride, relu=False, x1=None):
+    """Differentiable [relu](conv(cat(x0, x1)) + bias) (see DenseConvFn)."""
+    if not x0.is_cuda:
+        raise RuntimeError("nconv_amd dense convolutions compute on ROCm devices only")
+    return DenseConvFn.apply(x0, x1, weight, bias, kind, stride, relu)
+
+
+class HeadFn(torch.autograd.Function):
+    """res + conv3x3(x; w (1, Cin, 3, 3), pad 1) — the depth heads `dout = depth + self.conv(fout)`
+    (models/step2.py:255-257, 274-276); backward on the dense kernels (dgrad: 3x3 kernel with
+    Cout' = Cin; wgrad: M = 1)."""
+
+    @staticmethod
+    def forward(ctx, x, w, res):
+        x = x.contiguous()
+        out = conv3x3_c1(x, w, res.contiguous())
+        ctx.save_for_backward(x, w)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w = ctx.saved_tensors
+        g = g.contiguous()
+        need = ctx.needs_input_grad
+        gx = dgrad(g, w, DENSE_3X3, 1, x.shape) if need[0] else None
+        gw = wgrad(x, None, g, DENSE_3X3, 1, w.shape) if need[1] else None
+        return gx, gw, (g if need[2] else None)
+
+
+def head_fn(x, w, res):
+    return HeadFn.apply(x, w, res)

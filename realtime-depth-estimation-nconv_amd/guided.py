@@ -9,8 +9,13 @@ its one-argument SETP1_NCONV.forward rejects.
 Inference (eval mode, no autograd): every dense convolution of the RGB encoder and the fusion
 decoder runs on libnconv's fp32-MFMA kernels (dense.py, nconv_dense_conv_fwd) with eval
 BatchNorm folded into the packed weights, bias + ReLU + the RGBEncoder shortcut fused into the
-epilogue, and each torch.cat replaced by two-source loads / channel-offset stores. Training mode
-(BatchNorm batch statistics, autograd) uses the PyTorch-ROCm modules below.
+epilogue, and each torch.cat replaced by two-source loads / channel-offset stores.
+
+Training (or any forward that records autograd) on the device: every convolution is a
+dense.DenseConvFn / dense.HeadFn — forward, input gradient and weight gradient on the same MFMA
+kernels, ReLU after a bias-only convolution fused, torch.cat replaced by two-source loads —
+while BatchNorm (batch statistics, running-stat updates) and the bilinear depth downsampling stay
+PyTorch-ROCm ops. `model.dense_kernels = False` selects the plain PyTorch modules instead.
 """
 from collections import OrderedDict
 
@@ -59,6 +64,11 @@ class RGBEncoder(nn.Module):
                                               bn.running_var, sc.weight], build)
         return D.conv(x, D.DENSE_3X3, conv.stride[0], wp, bias, True, conv.out_channels, wshort=ws)
 
+    def train_forward(self, x):
+        conv, bn, act, sc = self.encoder[0], self.encoder[1], self.encoder[2], self.downsample[0]
+        y = act(bn(D.conv_fn(x, conv.weight, conv.bias, D.DENSE_3X3, conv.stride[0])))
+        return y + D.conv_fn(x, sc.weight, None, D.DENSE_1X1, sc.stride[0])
+
 
 class Basic2d(nn.Module):
     """conv (+BN when norm_layer, then no conv bias) + activation (step2.py:178-195)."""
@@ -94,6 +104,16 @@ class Basic2d(nn.Module):
         return D.conv(x0, D.DENSE_3X3, conv.stride[0], wp, bias, True, conv.out_channels, x1=x1, out=out,
                       out_c0=out_c0)
 
+    def train_forward(self, x0, x1=None):
+        conv, bn, act = self.conv.conv, getattr(self.conv, "bn", None), self.conv.relu
+        if conv.kernel_size != (3, 3) or conv.padding != (1, 1):
+            raise NotImplementedError("dense path: 3x3 / padding 1 Basic2d only")
+        fuse = bn is None and isinstance(act, nn.ReLU)  # conv + bias + ReLU in one kernel
+        y = D.conv_fn(x0, conv.weight, conv.bias, D.DENSE_3X3, conv.stride[0], relu=fuse, x1=x1)
+        if bn is not None:
+            y = bn(y)
+        return y if fuse else act(y)
+
 
 class Basic2dTrans(nn.Module):
     """ConvTranspose 4x4 / stride 2 / padding 1 + BN + activation (step2.py:197-214)."""
@@ -125,6 +145,10 @@ class Basic2dTrans(nn.Module):
         return D.conv(x0, D.DENSE_TRANSPOSED_4X4, 2, wp, bias, isinstance(self.relu, nn.ReLU),
                       conv.out_channels, x1=x1)
 
+    def train_forward(self, x0, x1=None):
+        y = D.conv_fn(x0, self.conv.weight, self.conv.bias, D.DENSE_TRANSPOSED_4X4, 2, x1=x1)
+        return self.relu(self.bn(y))
+
 
 class UpCat(nn.Module):
     """Upsample cat(x, d) by the transposed conv, then fuse with the skip y (step2.py:160-176)."""
@@ -143,6 +167,9 @@ class UpCat(nn.Module):
     def dense_forward(self, y, x, d):
         up = self.upf.dense_forward(x, d)
         return self.conv.dense_forward(up, y)
+
+    def train_forward(self, y, x, d):
+        return self.conv.train_forward(self.upf.train_forward(x, d), y)
 
 
 class ConvBlock(nn.Module):
@@ -163,6 +190,10 @@ class ConvBlock(nn.Module):
             return D.pack(D.DENSE_3X3, conv.weight, conv.in_channels, conv.out_channels), conv.bias.detach().contiguous()
         wp, bias = D.cached(self, "conv", [conv.weight, conv.bias], build)
         return D.conv(x, D.DENSE_3X3, conv.stride[0], wp, bias, True, conv.out_channels, out=out, out_c0=out_c0)
+
+    def train_forward(self, x0, x1=None):
+        conv = self.conv
+        return D.conv_fn(x0, conv.weight, conv.bias, D.DENSE_3X3, conv.stride[0], relu=True, x1=x1)
 
 
 class NewFusionBlock(nn.Module):
@@ -187,6 +218,11 @@ class NewFusionBlock(nn.Module):
         self.rgb_conv.dense_forward(rgb, out=fused, out_c0=0)      # the cat, written in place
         self.depth_conv.dense_forward(depth, out=fused, out_c0=C)
         return self.fuse_conv3.dense_forward(self.fuse_conv2.dense_forward(self.fuse_conv1.dense_forward(fused)))
+
+    def train_forward(self, rgb, depth):
+        # the torch.cat of step2.py:232 becomes fuse_conv1's two-source input
+        f = self.fuse_conv1.train_forward(self.rgb_conv.train_forward(rgb), self.depth_conv.train_forward(depth))
+        return self.fuse_conv3.train_forward(self.fuse_conv2.train_forward(f))
 
 
 class FusionResolutionBlock(nn.Module):
@@ -213,6 +249,12 @@ class FusionResolutionBlock(nn.Module):
         fout = self.fuse.dense_forward(fout, depth)
         return fout, D.conv3x3_c1(fout, self.conv.weight, depth)
 
+    def train_forward(self, rgb, depth, depth_last_step, fusion_festure):
+        fout = self.upcat.train_forward(rgb, fusion_festure, depth_last_step)
+        depth = F.interpolate(depth, scale_factor=1 / self.downsample_factor, mode="bilinear", align_corners=True)
+        fout = self.fuse.train_forward(fout, depth)
+        return fout, D.head_fn(fout, self.conv.weight, depth)
+
 
 class FusionResolution0(nn.Module):
     """Coarsest decoder scale (step2.py:262-278)."""
@@ -233,6 +275,11 @@ class FusionResolution0(nn.Module):
                               align_corners=True).contiguous()
         fout = self.fuse.dense_forward(rgb, depth)
         return fout, D.conv3x3_c1(fout, self.conv.weight, depth)
+
+    def train_forward(self, rgb, depth):
+        depth = F.interpolate(depth, scale_factor=1 / self.downsample_factor, mode="bilinear", align_corners=True)
+        fout = self.fuse.train_forward(rgb, depth)
+        return fout, D.head_fn(fout, self.conv.weight, depth)
 
 
 def _encoders_and_decoder(m, first_set):
@@ -274,9 +321,26 @@ def _guided_forward_dense(m, rgb0, depth0, rgb1, depth1):
     return d0, d1, d2, d3
 
 
+def _guided_forward_train(m, rgb0, depth0, rgb1, depth1):
+    """Autograd-recording forward with every convolution on the MFMA kernels (dense.conv_fn)."""
+    sparse = m.step1(depth0, depth1)
+    rgb = torch.cat((rgb0, rgb1), dim=0)
+    e0 = m.rgb_encoder0.train_forward(rgb)
+    e1 = m.rgb_encoder1.train_forward(e0)
+    e2 = m.rgb_encoder2.train_forward(e1)
+    e3 = m.rgb_encoder3.train_forward(e2)
+    f0, d0 = m.fuse0.train_forward(e3, sparse)
+    f1, d1 = m.fuse1.train_forward(e2, sparse, f0, d0)
+    f2, d2 = m.fuse2.train_forward(e1, sparse, f1, d1)
+    f3, d3 = m.fuse3.train_forward(e0, sparse, f2, d2)
+    return d0, d1, d2, d3
+
+
 def _guided_forward(m, rgb0, depth0, rgb1, depth1):
     if _use_dense(m, rgb0):
         return _guided_forward_dense(m, rgb0, depth0, rgb1, depth1)
+    if rgb0.is_cuda and getattr(m, "dense_kernels", True):
+        return _guided_forward_train(m, rgb0, depth0, rgb1, depth1)
     sparse = m.step1(depth0, depth1)
     rgb = torch.cat((rgb0, rgb1), dim=0)
     e0 = m.rgb_encoder0(rgb)

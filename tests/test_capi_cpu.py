@@ -80,3 +80,60 @@ def test_product_path_refuses_cpu_tensors(nconv_amd):
     layer = nconv_amd.NConv2d(8, 8, (5, 5))
     with pytest.raises(RuntimeError, match="ROCm devices only"):
         layer(torch.zeros(1, 8, 8, 8), torch.zeros(1, 8, 8, 8))
+
+
+def _wgrad_desc(nconv_amd, **kw):
+    d = nconv_amd._lib.NconvDenseWgrad()
+    fake = 0x1000  # never dereferenced
+    d.B, d.kind, d.stride = 1, nconv_amd._lib.DENSE_3X3, 1
+    d.x0, d.C0, d.x1, d.C1 = fake, 8, None, 0
+    d.H = d.W = 16
+    d.gy, d.Cout, d.Ho, d.Wo, d.gw = fake, 32, 16, 16, fake
+    for k, v in kw.items():
+        setattr(d, k, v)
+    return d
+
+
+@pytest.mark.parametrize("bad,msg", [
+    (dict(kind=7), "unknown kind"),
+    (dict(Ho=15), "Ho/Wo inconsistent"),
+    (dict(stride=3), "stride"),
+    (dict(kind=1, C0=65), "at most 64 input channels"),
+    (dict(Cout=97), "at most 96 output channels"),
+    (dict(kind=2, stride=2, Ho=33, Wo=32), "Ho/Wo inconsistent"),
+    (dict(kind=2, stride=2, C0=97, Ho=32, Wo=32), "at most 96 input channels"),
+    (dict(gw=None), "null pointer"),
+])
+def test_dense_wgrad_rejects_bad_descriptors(nconv_amd, bad, msg):
+    lib = nconv_amd._lib.lib()
+    d = _wgrad_desc(nconv_amd, **bad)
+    assert lib.nconv_dense_wgrad_workspace_bytes(ctypes.byref(d)) == 0
+    rc = lib.nconv_dense_conv_wgrad(ctypes.byref(d), None, 0, None)
+    assert rc == -22
+    assert msg in lib.nconv_last_error().decode()
+
+
+def test_dense_wgrad_workspace_query_is_host_only(nconv_amd):
+    lib = nconv_amd._lib.lib()
+    for kw in (dict(), dict(stride=2, Ho=8, Wo=8), dict(kind=1), dict(kind=2, stride=2, C0=1, C1=64, Ho=31, Wo=32)):
+        d = _wgrad_desc(nconv_amd, **kw)
+        if kw.get("C1"):
+            d.x1 = 0x2000
+        assert lib.nconv_dense_wgrad_workspace_bytes(ctypes.byref(d)) > 0, kw
+
+
+def test_dense_fwd_geometry_validation(nconv_amd):
+    """Transposed output 2H or 2H-1 only; conv 4x4 s2 output ceil(H/2); any Cout >= 1."""
+    L = nconv_amd._lib
+    lib = L.lib()
+    d = L.NconvDenseConv()
+    d.B, d.x0, d.C0, d.x1, d.C1, d.H, d.W = 1, 0x1000, 8, None, 0, 10, 10
+    d.Cout, d.kind, d.stride, d.wpack, d.out, d.out_C, d.out_c0 = 5, L.DENSE_TRANSPOSED_4X4, 2, 0x1000, 0x1000, 5, 0
+    d.Ho, d.Wo = 21, 20
+    assert lib.nconv_dense_conv_fwd(ctypes.byref(d), None) == -22
+    assert "Ho/Wo inconsistent" in lib.nconv_last_error().decode()
+    d.kind, d.Ho, d.Wo = L.DENSE_CONV4X4_S2, 6, 5
+    assert lib.nconv_dense_conv_fwd(ctypes.byref(d), None) == -22
+    d.Cout = 0
+    assert lib.nconv_dense_conv_fwd(ctypes.byref(d), None) == -22
+    assert "Cout" in lib.nconv_last_error().decode()
