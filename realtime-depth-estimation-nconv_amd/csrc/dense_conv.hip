@@ -351,25 +351,34 @@ __global__ __launch_bounds__(kDT) void conv3x3_c1(const float* __restrict__ x, i
 //   ConvTranspose2d 4x4 s2 p1:         pixels = input grid, D = the input x (m = ci),
 //       P = dL/dy (n = co*16 + kh*4 + kw) at (2 iy - 1 + kh, 2 ix - 1 + kw)
 // so gW's own layout (Conv2d (Cout, Cin, k, k) / ConvTranspose2d (Cin, Cout, 4, 4)) is [m][n].
-// Implicit GEMM on v_mfma_f32_32x32x2_f32: M = m (MT tiles of 32), N = n (NTW tiles of 32 per
-// wave, 4 waves), K = pixels (2 per MFMA). A block owns one group of NCOLS columns and a
-// contiguous range of 4 x 32 pixel tiles: per tile, D (MT*32 rows x 128 pixels) and the patch
-// planes of the channels its columns touch are staged in LDS (the next tile's loads in flight
-// during the MFMAs); pixel q = 2j + kk of k-step j of a tile row sits at a compile-time offset
-// from each lane's base. Each block writes its partial [M][N] to its K slice; dense_wgrad_reduce
-// adds the slices in a fixed order (deterministic, no float atomics).
+// Implicit GEMM on v_mfma_f32_32x32x2_f32: M = 32 rows m per workgroup, N = NTB tiles of 32
+// columns n (whole input channels: 32 x 9 taps, 16 x 16 taps, 64 x 1), K = pixels (2 per MFMA).
+// A workgroup walks a contiguous range of 4-row x 32-column pixel tiles: per tile, D (32 rows x
+// 128 pixels) and the patch planes of its channels are staged in LDS (the next tile's loads in
+// flight during the MFMAs); wave w takes pixel row w of the tile against ALL NTB column tiles, so
+// the waves split K (equal work, no idle column tiles) and each owns its own partial [32][NCOLS].
+// Pixel q = 2j + kk of k-step j sits at a compile-time offset from each lane's base. Partials
+// go to part[slice = kslice * 4 + wave][M][N]; dense_wgrad_reduce adds the slices in a fixed
+// order (deterministic, no float atomics).
 // ------------------------------------------------------------------------------------------------
-constexpr int wgd_ntw(int kind, int s) { return (kind == NCONV_DENSE_3X3 && s == 1) ? 2 : 1; }
-constexpr int wgd_ncols(int kind, int s) { return 4 * 32 * wgd_ntw(kind, s); }
+__host__ __device__ constexpr int wgd_ntb(int kind) {
+    return kind == NCONV_DENSE_3X3 ? 9 : (kind == NCONV_DENSE_1X1 ? 2 : 8);
+}
+// column tiles per workgroup for a GEMM of N columns: wgd_ntb, or 1 when N fits one tile
+// (the 1- and 3-channel inputs of depth_conv / rgb_encoder0, a 1x1 of <= 32 channels)
+constexpr int wgd_nt(int kind, int N) { return N <= 32 ? 1 : wgd_ntb(kind); }
 
-template <int KIND, int S, int MT>
+template <int KIND, int S, int NT>
 struct WgdCfg {
     static constexpr bool TR = KIND == NCONV_DENSE_TRANSPOSED_4X4;
     static constexpr int TAPS = KIND == NCONV_DENSE_3X3 ? 9 : (KIND == NCONV_DENSE_1X1 ? 1 : 16);
     static constexpr int KS = KIND == NCONV_DENSE_3X3 ? 3 : (KIND == NCONV_DENSE_1X1 ? 1 : 4);
-    static constexpr int NTW = wgd_ntw(KIND, S);
-    static constexpr int NCOLS = wgd_ncols(KIND, S);
-    static constexpr int TH = 4, TW = 32, NPX = TH * TW;
+    static constexpr int NTB = NT;                        // column tiles per workgroup
+    static constexpr int NCOLS = 32 * NTB;
+    // patch channels staged per workgroup: whole channels per column group (wgd_ntb), or every
+    // channel a one-tile group (N <= 32) may touch
+    static constexpr int CPB = NCOLS % TAPS == 0 ? NCOLS / TAPS : (NCOLS - 1) / TAPS + 2;
+    static constexpr int TH = 4, TW = 32, NPX = TH * TW;  // pixel tile: one row per wave
     // patch geometry: LDS step between neighbouring pixels (1x1 stages only the sampled
     // positions), global step between neighbouring LDS columns, patch origin = pixel * OS - PAD
     static constexpr int LS = KIND == NCONV_DENSE_1X1 ? 1 : (TR ? 2 : S);
@@ -378,12 +387,10 @@ struct WgdCfg {
     static constexpr int PAD = KIND == NCONV_DENSE_1X1 ? 0 : 1;
     static constexpr int PR = (TH - 1) * LS + KS, PC = (TW - 1) * LS + KS;
     static constexpr int PPLANE = PR * PC;
-    static constexpr int CPB0 = (NCOLS - 1) / TAPS + 2;
-    static constexpr int CPB = CPB0 < 64 ? CPB0 : 64;  // patch channels staged per block
     static constexpr int DP = NPX + 2;                 // D row pitch: rows m, m+1 two banks apart
     static constexpr int D_OFF = (CPB * PPLANE + 3) & ~3;
-    static constexpr int LDS = D_OFF + MT * 32 * DP;
-    static constexpr int NDE = MT * 32 * NPX / kDT;    // D elements per thread
+    static constexpr int LDS = D_OFF + 32 * DP;
+    static constexpr int NDE = 32 * NPX / kDT;         // D elements per thread
     static constexpr int NPE = (CPB * PPLANE + kDT - 1) / kDT;
 };
 
@@ -397,48 +404,54 @@ struct WgdArgs {
     int pC0, pC1;  // patch operand channels
     int Hs, Ws;    // patch source planes
     int M, N;      // N = (pC0 + pC1) * TAPS
-    int ntx, nty, nng, nks;
+    int ntx, nty, nmg, nng, nks;
     long long ntiles;
 };
 
-template <int KIND, int S, int MT>
+template <int KIND, int S, int NT>
 __global__ __launch_bounds__(kDT) void dense_wgrad_mfma(WgdArgs a, float* __restrict__ part) {
-    using C = WgdCfg<KIND, S, MT>;
+    using C = WgdCfg<KIND, S, NT>;
     __shared__ __attribute__((aligned(16))) float lds[C::LDS];
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int ng = blockIdx.x % a.nng, ks = blockIdx.x / a.nng;
-    const int n0 = ng * C::NCOLS;
+    int blk = blockIdx.x;
+    const int ng = blk % a.nng;
+    blk /= a.nng;
+    const int mg = blk % a.nmg, ks = blk / a.nmg;
+    const int n0 = ng * C::NCOLS, m0 = mg * 32;
     const int Cp = a.pC0 + a.pC1;
     const int c_lo = n0 / C::TAPS;
-    int c_hi = (n0 + C::NCOLS - 1) / C::TAPS + 1;
-    c_hi = c_hi < Cp ? c_hi : Cp;
     const long long t0 = a.ntiles * ks / a.nks, t1 = a.ntiles * (ks + 1) / a.nks;
     const size_t HWp = (size_t)a.Hp * a.Wp, HWs = (size_t)a.Hs * a.Ws;
 
-    // per-lane operand bases (A: row m = mt*32 + li, B: column n of this wave's tile u)
+    // per-lane operand bases (A: row m0 + li of D, pixel row w; B: column n0 + 32u + li)
     const int kk = lane >> 5, li = lane & 31;
-    const int abase = C::D_OFF + li * C::DP + kk;
-    int bbase[C::NTW];
+    const int abase = C::D_OFF + li * C::DP + w * C::TW + kk;
+    const int bb = li * 0;  // (keeps the B bases below in VGPRs)
+    int bbase[C::NTB];
 #pragma unroll
-    for (int u = 0; u < C::NTW; ++u) {
-        const int n = n0 + (w * C::NTW + u) * 32 + li;
-        if (n < a.N) {
-            const int ci = n / C::TAPS - c_lo, tap = n % C::TAPS;
-            const int kh = tap / C::KS, kw = tap % C::KS;
-            bbase[u] = ci * C::PPLANE + kh * C::PC + kw + kk * C::LS;
-        } else {
-            bbase[u] = kk * C::LS;  // any in-range address: the column is never written
-        }
+    for (int u = 0; u < C::NTB; ++u) {
+        const int nl = 32 * u + li;  // column within the group
+        const int ci = nl / C::TAPS, tap = nl % C::TAPS;
+        const int kh = tap / C::KS, kw = tap % C::KS;
+        bbase[u] = bb + ci * C::PPLANE + (w * C::LS + kh) * C::PC + kw + kk * C::LS;
     }
 
-    f16v acc[MT][C::NTW];
+    f16v acc[C::NTB];
 #pragma unroll
-    for (int m = 0; m < MT; ++m)
-#pragma unroll
-        for (int u = 0; u < C::NTW; ++u) acc[m][u] = (f16v){};
+    for (int u = 0; u < C::NTB; ++u) acc[u] = (f16v){};
 
-    float dv[C::NDE], pv[C::NPE];
+    // Staging loads are buffer loads: the image's planes sit behind one SGPR resource per
+    // source, elements outside the image / channel range carry an offset past it and read 0
+    // (no per-element masks or 64-bit addresses live across the load latency). A column group's
+    // channels lie in one source when the concatenation boundary is a multiple of CPB (every
+    // concatenation of the guided model); otherwise each element is read from both sources,
+    // one of them out of range.
+    constexpr unsigned OOB = 0x80000000u;
+    const int Cp_hi = c_lo + C::CPB < Cp ? c_lo + C::CPB : Cp;
+    const bool p_split = a.p1 != nullptr && c_lo < a.pC0 && Cp_hi > a.pC0;  // wave-uniform
+    const bool p_hi = a.p1 != nullptr && c_lo >= a.pC0;                     // all from source 1
+    float dv[C::NDE], pv[C::NPE], pv1[C::NPE];
     auto load = [&](long long t) {
         // the per-element coordinates below are recomputed per tile (tid made opaque): hoisted
         // out of the tile loop they would pin ~4 registers per staged element
@@ -448,28 +461,44 @@ __global__ __launch_bounds__(kDT) void dense_wgrad_mfma(WgdArgs a, float* __rest
         const long long rr = t / a.ntx;
         const int ty = (int)(rr % a.nty), b = (int)(rr / a.nty);
         const int py0 = ty * C::TH, px0 = tx * C::TW;
-#pragma unroll
-        for (int k = 0; k < C::NDE; ++k) {
-            const int e = tq + kDT * k;
-            const int m = e / C::NPX, q = e % C::NPX;  // m is wave-uniform
+        // D: element k of a thread is row m0 + (tid >> 7) + 2k (wave-uniform), pixel tid & 127
+        {
+            const int q = tq % C::NPX;
             const int py = py0 + q / C::TW, px = px0 + q % C::TW;
-            const bool ok = m < a.M && py < a.Hp && px < a.Wp;
-            const float* src = m < a.dC0 ? a.d0 + ((size_t)b * a.dC0 + m) * HWp
-                                         : a.d1 + ((size_t)b * a.dC1 + (m - a.dC0)) * HWp;
-            dv[k] = ok ? src[(size_t)py * a.Wp + px] : 0.f;
+            const unsigned ob = (py < a.Hp && px < a.Wp) ? (unsigned)(py * a.Wp + px) * 4u : OOB;
+            const __amdgpu_buffer_rsrc_t rd0 = plane_rsrc(a.d0 + (size_t)b * a.dC0 * HWp, (int)(a.dC0 * HWp * 4));
+            const __amdgpu_buffer_rsrc_t rd1 =
+                plane_rsrc(a.d1 ? a.d1 + (size_t)b * a.dC1 * HWp : a.d0, (int)((a.d1 ? a.dC1 : 0) * HWp * 4));
+            const int mw = __builtin_amdgcn_readfirstlane(m0 + tid / C::NPX);  // NPX >= 64: per wave
+#pragma unroll
+            for (int k = 0; k < C::NDE; ++k) {
+                const int m = mw + (kDT / C::NPX) * k;
+                const bool s1 = m >= a.dC0;
+                const int mm = s1 ? m - a.dC0 : m;
+                const unsigned off = (m < a.M && ob != OOB) ? (unsigned)(mm * HWp) * 4u + ob : OOB;
+                dv[k] = ld_f32(s1 ? rd1 : rd0, off);
+            }
         }
         const int iy0 = py0 * C::OS - C::PAD, ix0 = px0 * C::OS - C::PAD;
+        const __amdgpu_buffer_rsrc_t rp0 = plane_rsrc(a.p0 + (size_t)b * a.pC0 * HWs, (int)(a.pC0 * HWs * 4));
+        const __amdgpu_buffer_rsrc_t rp1 =
+            plane_rsrc(a.p1 ? a.p1 + (size_t)b * a.pC1 * HWs : a.p0, (int)((a.p1 ? a.pC1 : 0) * HWs * 4));
+        const int cb = p_hi ? a.pC0 : 0;  // first channel of the block's source
 #pragma unroll
         for (int k = 0; k < C::NPE; ++k) {
             const int e = tq + kDT * k;
             const int ci = e / C::PPLANE, rem = e % C::PPLANE;
             const int r = rem / C::PC, c = rem % C::PC;
             const int gc = c_lo + ci, iy = iy0 + r * C::GS, ix = ix0 + c * C::GS;
-            const bool ok = e < C::CPB * C::PPLANE && gc < c_hi && (unsigned)iy < (unsigned)a.Hs &&
+            const bool ok = e < C::CPB * C::PPLANE && gc < Cp_hi && (unsigned)iy < (unsigned)a.Hs &&
                             (unsigned)ix < (unsigned)a.Ws;
-            const float* src = gc < a.pC0 ? a.p0 + ((size_t)b * a.pC0 + gc) * HWs
-                                          : a.p1 + ((size_t)b * a.pC1 + (gc - a.pC0)) * HWs;
-            pv[k] = ok ? src[(size_t)iy * a.Ws + ix] : 0.f;
+            const unsigned pix = (unsigned)(iy * a.Ws + ix);
+            if (!p_split) {
+                pv[k] = ld_f32(p_hi ? rp1 : rp0, ok ? ((unsigned)(gc - cb) * (unsigned)HWs + pix) * 4u : OOB);
+            } else {
+                pv[k] = ld_f32(rp0, ok && gc < a.pC0 ? ((unsigned)gc * (unsigned)HWs + pix) * 4u : OOB);
+                pv1[k] = ld_f32(rp1, ok && gc >= a.pC0 ? ((unsigned)(gc - a.pC0) * (unsigned)HWs + pix) * 4u : OOB);
+            }
         }
     };
     auto store = [&]() {
@@ -481,7 +510,7 @@ __global__ __launch_bounds__(kDT) void dense_wgrad_mfma(WgdArgs a, float* __rest
 #pragma unroll
         for (int k = 0; k < C::NPE; ++k) {
             const int e = tid + kDT * k;
-            if (e < C::CPB * C::PPLANE) lds[e] = pv[k];
+            if (e < C::CPB * C::PPLANE) lds[e] = p_split ? pv[k] + pv1[k] : pv[k];
         }
     };
 
@@ -492,45 +521,36 @@ __global__ __launch_bounds__(kDT) void dense_wgrad_mfma(WgdArgs a, float* __rest
         store();
         __syncthreads();
         if (t + 1 < t1) load(t + 1);
-#pragma unroll 1
-        for (int r = 0; r < C::TH; ++r) {
-            const float* ap = lds + abase + r * C::TW;
-            const int boff = r * C::LS * C::PC;
+        // k-steps two at a time: fully unrolled, the scheduler hoists all 16 x NTB operand
+        // reads of the tile into registers (~300 VGPRs)
+#pragma unroll 2
+        for (int j = 0; j < C::TW / 2; ++j) {
+            const float av = lds[abase + 2 * j];
 #pragma unroll
-            for (int j = 0; j < C::TW / 2; ++j) {
-                float av[MT], bv[C::NTW];
-#pragma unroll
-                for (int m = 0; m < MT; ++m) av[m] = ap[m * 32 * C::DP + 2 * j];
-#pragma unroll
-                for (int u = 0; u < C::NTW; ++u) bv[u] = lds[bbase[u] + boff + 2 * j * C::LS];
-#pragma unroll
-                for (int m = 0; m < MT; ++m)
-#pragma unroll
-                    for (int u = 0; u < C::NTW; ++u)
-                        acc[m][u] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[m], bv[u], acc[m][u], 0, 0, 0);
+            for (int u = 0; u < C::NTB; ++u) {
+                const float bv = lds[bbase[u] + 2 * j * C::LS];
+                acc[u] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[u], 0, 0, 0);
             }
         }
     }
 
-    // ---- partial [M][N] of this K slice: C[row = m][col = n] ----
-    float* out = part + (size_t)ks * a.M * a.N;
+    // ---- this wave's partial [32][NCOLS] -> slice ks * 4 + w: C[row = m][col = n] ----
+    float* out = part + ((size_t)ks * 4 + w) * a.M * a.N;
 #pragma unroll
-    for (int u = 0; u < C::NTW; ++u) {
-        const int n = n0 + (w * C::NTW + u) * 32 + li;
+    for (int u = 0; u < C::NTB; ++u) {
+        const int n = n0 + 32 * u + li;
         if (n >= a.N) continue;
 #pragma unroll
-        for (int m = 0; m < MT; ++m)
-#pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                const int row = 32 * m + (q & 3) + 8 * (q >> 2) + 4 * kk;
-                if (row < a.M) out[(size_t)row * a.N + n] = acc[m][u][q];
-            }
+        for (int q = 0; q < 16; ++q) {
+            const int m = m0 + (q & 3) + 8 * (q >> 2) + 4 * kk;
+            if (m < a.M) out[(size_t)m * a.N + n] = acc[u][q];
+        }
     }
 }
 
-// gw[e] = sum over the nks slices of part[slice][e]: 64 elements x 4 slice phases per block,
+// gw[e] = sum over the nsl slices of part[slice][e]: 64 elements x 4 slice phases per block,
 // each phase summing every 4th slice in order, the phases combined in a fixed order.
-__global__ __launch_bounds__(kDT) void dense_wgrad_reduce(const float* __restrict__ part, int nks, int mn,
+__global__ __launch_bounds__(kDT) void dense_wgrad_reduce(const float* __restrict__ part, int nsl, int mn,
                                                           float* __restrict__ gw) {
     __shared__ float red[4][64];
     const int col = threadIdx.x & 63, ph = threadIdx.x >> 6;
@@ -538,7 +558,7 @@ __global__ __launch_bounds__(kDT) void dense_wgrad_reduce(const float* __restric
     float s = 0.f;
     if (e < mn) {
 #pragma unroll 8
-        for (int k = ph; k < nks; k += 4) s += part[(size_t)k * mn + e];
+        for (int k = ph; k < nsl; k += 4) s += part[(size_t)k * mn + e];
     }
     red[ph][col] = s;
     __syncthreads();
@@ -627,7 +647,7 @@ int launch_conv3x3_c1(const float* x, int B, int Cin, int H, int W, const float*
 }
 
 // ---- weight gradient ----
-constexpr int kWgdTargetBlocks = 512;  // two 4-wave blocks per CU (LDS 58-75 KB each): one round
+constexpr int kWgdTargetBlocks = 512;  // two 4-wave workgroups per CU: one round
 
 static WgdArgs wgrad_args(const nconv_dense_wgrad& g) {
     WgdArgs a{};
@@ -666,9 +686,10 @@ static WgdArgs wgrad_args(const nconv_dense_wgrad& g) {
     a.ntx = (a.Wp + 31) / 32;
     a.nty = (a.Hp + 3) / 4;
     a.ntiles = (long long)g.B * a.ntx * a.nty;
-    const int ncols = wgd_ncols(g.kind, g.stride);
+    const int ncols = 32 * wgd_nt(g.kind, a.N);
     a.nng = (a.N + ncols - 1) / ncols;
-    long long nks = kWgdTargetBlocks / a.nng;
+    a.nmg = (a.M + 31) / 32;
+    long long nks = kWgdTargetBlocks / (a.nng * a.nmg);
     if (nks < 1) nks = 1;
     if (nks > a.ntiles) nks = a.ntiles;
     a.nks = (int)nks;
@@ -677,43 +698,35 @@ static WgdArgs wgrad_args(const nconv_dense_wgrad& g) {
 
 size_t dense_wgrad_workspace_bytes(const nconv_dense_wgrad& g) {
     const WgdArgs a = wgrad_args(g);
-    return (size_t)a.nks * a.M * a.N * sizeof(float);
-}
-
-template <int KIND, int S>
-static void go_wgrad(const WgdArgs& a, float* part, hipStream_t st) {
-    const dim3 grid(a.nng * a.nks), blk(kDT);
-    const int mt = (a.M + 31) / 32;
-    if (mt == 1)
-        hipLaunchKernelGGL((dense_wgrad_mfma<KIND, S, 1>), grid, blk, 0, st, a, part);
-    else if (mt == 2)
-        hipLaunchKernelGGL((dense_wgrad_mfma<KIND, S, 2>), grid, blk, 0, st, a, part);
-    else
-        hipLaunchKernelGGL((dense_wgrad_mfma<KIND, S, 3>), grid, blk, 0, st, a, part);
+    return (size_t)a.nks * 4 * a.M * a.N * sizeof(float);
 }
 
 int launch_dense_wgrad(const nconv_dense_wgrad& g, float* ws, size_t ws_bytes, hipStream_t st, const char** why) {
     const WgdArgs a = wgrad_args(g);
-    if (ws_bytes < (size_t)a.nks * a.M * a.N * sizeof(float)) {
+    if (ws_bytes < dense_wgrad_workspace_bytes(g)) {
         *why = "workspace too small (see nconv_dense_wgrad_workspace_bytes)";
         return -22;
     }
-    if (g.kind == NCONV_DENSE_3X3 && g.stride == 1)
-        go_wgrad<NCONV_DENSE_3X3, 1>(a, ws, st);
-    else if (g.kind == NCONV_DENSE_3X3 && g.stride == 2)
-        go_wgrad<NCONV_DENSE_3X3, 2>(a, ws, st);
-    else if (g.kind == NCONV_DENSE_1X1 && g.stride == 1)
-        go_wgrad<NCONV_DENSE_1X1, 1>(a, ws, st);
-    else if (g.kind == NCONV_DENSE_1X1 && g.stride == 2)
-        go_wgrad<NCONV_DENSE_1X1, 2>(a, ws, st);
-    else if (g.kind == NCONV_DENSE_TRANSPOSED_4X4 && g.stride == 2)
-        go_wgrad<NCONV_DENSE_TRANSPOSED_4X4, 2>(a, ws, st);
-    else {
+    const dim3 grid(a.nng * a.nmg * a.nks), blk(kDT);
+    const bool one = a.N <= 32;
+#define NCONV_WG(KIND_, S_)                                                                                  \
+    if (g.kind == KIND_ && g.stride == S_) {                                                                \
+        if (one)                                                                                             \
+            hipLaunchKernelGGL((dense_wgrad_mfma<KIND_, S_, 1>), grid, blk, 0, st, a, ws);                  \
+        else                                                                                                 \
+            hipLaunchKernelGGL((dense_wgrad_mfma<KIND_, S_, wgd_ntb(KIND_)>), grid, blk, 0, st, a, ws);     \
+    } else
+    NCONV_WG(NCONV_DENSE_3X3, 1)
+    NCONV_WG(NCONV_DENSE_3X3, 2)
+    NCONV_WG(NCONV_DENSE_1X1, 1)
+    NCONV_WG(NCONV_DENSE_1X1, 2)
+    NCONV_WG(NCONV_DENSE_TRANSPOSED_4X4, 2) {
         *why = "no weight-gradient kernel for this (kind, stride)";
         return -95;
     }
+#undef NCONV_WG
     const int mn = a.M * a.N;
-    hipLaunchKernelGGL(dense_wgrad_reduce, dim3((mn + 63) / 64), dim3(kDT), 0, st, ws, a.nks, mn, g.gw);
+    hipLaunchKernelGGL(dense_wgrad_reduce, dim3((mn + 63) / 64), dim3(kDT), 0, st, ws, a.nks * 4, mn, g.gw);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         *why = hipGetErrorString(e);
