@@ -351,34 +351,37 @@ __global__ __launch_bounds__(kDT) void conv3x3_c1(const float* __restrict__ x, i
 //   ConvTranspose2d 4x4 s2 p1:         pixels = input grid, D = the input x (m = ci),
 //       P = dL/dy (n = co*16 + kh*4 + kw) at (2 iy - 1 + kh, 2 ix - 1 + kw)
 // so gW's own layout (Conv2d (Cout, Cin, k, k) / ConvTranspose2d (Cin, Cout, 4, 4)) is [m][n].
-// Implicit GEMM on v_mfma_f32_32x32x2_f32: M = 32 rows m per workgroup, N = NTB tiles of 32
-// columns n (whole input channels: 32 x 9 taps, 16 x 16 taps, 64 x 1), K = pixels (2 per MFMA).
-// A workgroup walks a contiguous range of 4-row x 32-column pixel tiles: per tile, D (32 rows x
-// 128 pixels) and the patch planes of its channels are staged in LDS (the next tile's loads in
-// flight during the MFMAs); wave w takes pixel row w of the tile against ALL NTB column tiles, so
-// the waves split K (equal work, no idle column tiles) and each owns its own partial [32][NCOLS].
-// Pixel q = 2j + kk of k-step j sits at a compile-time offset from each lane's base. Partials
-// go to part[slice = kslice * 4 + wave][M][N]; dense_wgrad_reduce adds the slices in a fixed
-// order (deterministic, no float atomics).
+// Implicit GEMM on v_mfma_f32_32x32x2_f32 with K = pixels (2 per MFMA). The (M, N) plane is cut
+// into groups of one 32-row m-tile x NT 32-column n-tiles (NT x 32 columns = whole input
+// channels: 32 x 9 taps, 16 x 16 taps, 64 x 1); a workgroup owns GM x GN groups (D rows and
+// patch channels staged once for all of them) and walks a contiguous range of TH x 32 pixel
+// tiles. Wave w takes group w % (GM GN) on the pixels of its row share (1/4, 1/2 or all of the
+// tile), so every wave does the same MFMA work and every loaded byte feeds up to 4 waves. Per
+// tile, D and the patch planes are staged in LDS with buffer loads (the next tile's loads in
+// flight during the MFMAs); pixel q = q0 + 2j + kk of k-step j sits at a compile-time offset
+// from a per-wave base. Each wave writes its partial [32][NT*32] to slice ks * RG + row-group;
+// dense_wgrad_reduce adds the slices in a fixed order (deterministic, no float atomics).
 // ------------------------------------------------------------------------------------------------
 __host__ __device__ constexpr int wgd_ntb(int kind) {
     return kind == NCONV_DENSE_3X3 ? 9 : (kind == NCONV_DENSE_1X1 ? 2 : 8);
 }
-// column tiles per workgroup for a GEMM of N columns: wgd_ntb, or 1 when N fits one tile
+// column tiles per group for a GEMM of N columns: wgd_ntb, or 1 when N fits one tile
 // (the 1- and 3-channel inputs of depth_conv / rgb_encoder0, a 1x1 of <= 32 channels)
 constexpr int wgd_nt(int kind, int N) { return N <= 32 ? 1 : wgd_ntb(kind); }
 
-template <int KIND, int S, int NT>
+template <int KIND, int S, int NT, int GM, int GN>
 struct WgdCfg {
     static constexpr bool TR = KIND == NCONV_DENSE_TRANSPOSED_4X4;
     static constexpr int TAPS = KIND == NCONV_DENSE_3X3 ? 9 : (KIND == NCONV_DENSE_1X1 ? 1 : 16);
     static constexpr int KS = KIND == NCONV_DENSE_3X3 ? 3 : (KIND == NCONV_DENSE_1X1 ? 1 : 4);
-    static constexpr int NTB = NT;                        // column tiles per workgroup
-    static constexpr int NCOLS = 32 * NTB;
-    // patch channels staged per workgroup: whole channels per column group (wgd_ntb), or every
-    // channel a one-tile group (N <= 32) may touch
-    static constexpr int CPB = NCOLS % TAPS == 0 ? NCOLS / TAPS : (NCOLS - 1) / TAPS + 2;
-    static constexpr int TH = 4, TW = 32, NPX = TH * TW;  // pixel tile: one row per wave
+    static constexpr int NCOLS = 32 * NT;  // columns per group
+    // patch channels per group: whole channels (wgd_ntb), or every channel a one-tile group may touch
+    static constexpr int CPG = NCOLS % TAPS == 0 ? NCOLS / TAPS : (NCOLS - 1) / TAPS + 2;
+    static constexpr int CPB = GN * CPG;   // patch channels staged per workgroup
+    static constexpr int GB = GM * GN, RG = 4 / GB;  // groups per workgroup, row-groups (waves per group)
+    // pixel tile: 4 x 32 (2 x 32 where the strided patch is tall: 3x3 s2, transposed)
+    static constexpr int TH = (TR || (KIND == NCONV_DENSE_3X3 && S == 2)) ? 2 : 4, TW = 32, NPX = TH * TW;
+    static constexpr int PPW = NPX / RG;   // pixels per wave per tile (a multiple of 16)
     // patch geometry: LDS step between neighbouring pixels (1x1 stages only the sampled
     // positions), global step between neighbouring LDS columns, patch origin = pixel * OS - PAD
     static constexpr int LS = KIND == NCONV_DENSE_1X1 ? 1 : (TR ? 2 : S);
@@ -387,11 +390,12 @@ struct WgdCfg {
     static constexpr int PAD = KIND == NCONV_DENSE_1X1 ? 0 : 1;
     static constexpr int PR = (TH - 1) * LS + KS, PC = (TW - 1) * LS + KS;
     static constexpr int PPLANE = PR * PC;
-    static constexpr int DP = NPX + 2;                 // D row pitch: rows m, m+1 two banks apart
+    static constexpr int DP = NPX + 2;     // D row pitch: rows m, m+1 two banks apart
     static constexpr int D_OFF = (CPB * PPLANE + 3) & ~3;
-    static constexpr int LDS = D_OFF + 32 * DP;
-    static constexpr int NDE = 32 * NPX / kDT;         // D elements per thread
-    static constexpr int NPE = (CPB * PPLANE + kDT - 1) / kDT;
+    static constexpr int LDS = D_OFF + GM * 32 * DP;
+    static constexpr int NDE = GM * 32 * NPX / kDT;  // D elements per thread
+    static constexpr int NPG = (CPG * PPLANE + kDT - 1) / kDT;  // patch elements per thread and group
+    static_assert(PPW % 16 == 0 && (GM * 32 * NPX) % kDT == 0, "wave / thread shares");
 };
 
 struct WgdArgs {
@@ -404,54 +408,55 @@ struct WgdArgs {
     int pC0, pC1;  // patch operand channels
     int Hs, Ws;    // patch source planes
     int M, N;      // N = (pC0 + pC1) * TAPS
-    int ntx, nty, nmg, nng, nks;
+    int ntx, nty, nbm, nbn, nks;  // tiles; workgroup groups along M and N; K slices
     long long ntiles;
 };
 
-template <int KIND, int S, int NT>
+template <int KIND, int S, int NT, int GM, int GN>
 __global__ __launch_bounds__(kDT) void dense_wgrad_mfma(WgdArgs a, float* __restrict__ part) {
-    using C = WgdCfg<KIND, S, NT>;
+    using C = WgdCfg<KIND, S, NT, GM, GN>;
     __shared__ __attribute__((aligned(16))) float lds[C::LDS];
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     int blk = blockIdx.x;
-    const int ng = blk % a.nng;
-    blk /= a.nng;
-    const int mg = blk % a.nmg, ks = blk / a.nmg;
-    const int n0 = ng * C::NCOLS, m0 = mg * 32;
+    const int bn = blk % a.nbn;
+    blk /= a.nbn;
+    const int bm = blk % a.nbm, ks = blk / a.nbm;
+    const int m0 = bm * GM * 32, n0 = bn * GN * C::NCOLS;  // the workgroup's first row / column
     const int Cp = a.pC0 + a.pC1;
     const int c_lo = n0 / C::TAPS;
     const long long t0 = a.ntiles * ks / a.nks, t1 = a.ntiles * (ks + 1) / a.nks;
     const size_t HWp = (size_t)a.Hp * a.Wp, HWs = (size_t)a.Hs * a.Ws;
+    static_assert(GN == 1 || C::NCOLS % C::TAPS == 0, "groups of whole channels");
 
-    // per-lane operand bases (A: row m0 + li of D, pixel row w; B: column n0 + 32u + li)
+    // this wave's group (m-tile gmi, n-group gni) and pixel share [q0, q0 + PPW) of each tile
+    const int gi = w % C::GB, rg = w / C::GB;
+    const int gmi = gi % GM, gni = gi / GM;
+    const int q0 = rg * C::PPW;
     const int kk = lane >> 5, li = lane & 31;
-    const int abase = C::D_OFF + li * C::DP + w * C::TW + kk;
-    const int bb = li * 0;  // (keeps the B bases below in VGPRs)
-    int bbase[C::NTB];
+    const int abase = C::D_OFF + (gmi * 32 + li) * C::DP + kk;  // + q
+    int bbase[NT];
 #pragma unroll
-    for (int u = 0; u < C::NTB; ++u) {
-        const int nl = 32 * u + li;  // column within the group
+    for (int u = 0; u < NT; ++u) {
+        const int nl = gni * C::NCOLS + 32 * u + li;  // column within the workgroup
         const int ci = nl / C::TAPS, tap = nl % C::TAPS;
         const int kh = tap / C::KS, kw = tap % C::KS;
-        bbase[u] = bb + ci * C::PPLANE + (w * C::LS + kh) * C::PC + kw + kk * C::LS;
+        bbase[u] = ci * C::PPLANE + kh * C::PC + kw + kk * C::LS;  // + r*LS*PC + c*LS
     }
 
-    f16v acc[C::NTB];
+    f16v acc[NT];
 #pragma unroll
-    for (int u = 0; u < C::NTB; ++u) acc[u] = (f16v){};
+    for (int u = 0; u < NT; ++u) acc[u] = (f16v){};
 
     // Staging loads are buffer loads: the image's planes sit behind one SGPR resource per
     // source, elements outside the image / channel range carry an offset past it and read 0
-    // (no per-element masks or 64-bit addresses live across the load latency). A column group's
-    // channels lie in one source when the concatenation boundary is a multiple of CPB (every
-    // concatenation of the guided model); otherwise each element is read from both sources,
-    // one of them out of range.
+    // (no per-element masks or 64-bit addresses live across the load latency). The patch is
+    // staged group by group, so the source of a group's channels is wave-uniform whenever the
+    // concatenation boundary is a multiple of 32 channels (16 for the transposed kernel) — every
+    // concatenation of the guided model; otherwise that group reads each element from both
+    // sources (one out of range) and adds them.
     constexpr unsigned OOB = 0x80000000u;
-    const int Cp_hi = c_lo + C::CPB < Cp ? c_lo + C::CPB : Cp;
-    const bool p_split = a.p1 != nullptr && c_lo < a.pC0 && Cp_hi > a.pC0;  // wave-uniform
-    const bool p_hi = a.p1 != nullptr && c_lo >= a.pC0;                     // all from source 1
-    float dv[C::NDE], pv[C::NPE], pv1[C::NPE];
+    float dv[C::NDE], pv[GN][C::NPG];
     auto load = [&](long long t) {
         // the per-element coordinates below are recomputed per tile (tid made opaque): hoisted
         // out of the tile loop they would pin ~4 registers per staged element
@@ -461,8 +466,7 @@ __global__ __launch_bounds__(kDT) void dense_wgrad_mfma(WgdArgs a, float* __rest
         const long long rr = t / a.ntx;
         const int ty = (int)(rr % a.nty), b = (int)(rr / a.nty);
         const int py0 = ty * C::TH, px0 = tx * C::TW;
-        // D: element k of a thread is row m0 + (tid >> 7) + 2k (wave-uniform), pixel tid & 127
-        {
+        {   // D: element k of a thread is row m0 + tid / NPX + k * (256 / NPX), pixel tid % NPX
             const int q = tq % C::NPX;
             const int py = py0 + q / C::TW, px = px0 + q % C::TW;
             const unsigned ob = (py < a.Hp && px < a.Wp) ? (unsigned)(py * a.Wp + px) * 4u : OOB;
@@ -483,21 +487,28 @@ __global__ __launch_bounds__(kDT) void dense_wgrad_mfma(WgdArgs a, float* __rest
         const __amdgpu_buffer_rsrc_t rp0 = plane_rsrc(a.p0 + (size_t)b * a.pC0 * HWs, (int)(a.pC0 * HWs * 4));
         const __amdgpu_buffer_rsrc_t rp1 =
             plane_rsrc(a.p1 ? a.p1 + (size_t)b * a.pC1 * HWs : a.p0, (int)((a.p1 ? a.pC1 : 0) * HWs * 4));
-        const int cb = p_hi ? a.pC0 : 0;  // first channel of the block's source
 #pragma unroll
-        for (int k = 0; k < C::NPE; ++k) {
-            const int e = tq + kDT * k;
-            const int ci = e / C::PPLANE, rem = e % C::PPLANE;
-            const int r = rem / C::PC, c = rem % C::PC;
-            const int gc = c_lo + ci, iy = iy0 + r * C::GS, ix = ix0 + c * C::GS;
-            const bool ok = e < C::CPB * C::PPLANE && gc < Cp_hi && (unsigned)iy < (unsigned)a.Hs &&
-                            (unsigned)ix < (unsigned)a.Ws;
-            const unsigned pix = (unsigned)(iy * a.Ws + ix);
-            if (!p_split) {
-                pv[k] = ld_f32(p_hi ? rp1 : rp0, ok ? ((unsigned)(gc - cb) * (unsigned)HWs + pix) * 4u : OOB);
-            } else {
-                pv[k] = ld_f32(rp0, ok && gc < a.pC0 ? ((unsigned)gc * (unsigned)HWs + pix) * 4u : OOB);
-                pv1[k] = ld_f32(rp1, ok && gc >= a.pC0 ? ((unsigned)(gc - a.pC0) * (unsigned)HWs + pix) * 4u : OOB);
+        for (int g = 0; g < GN; ++g) {
+            const int gc0 = c_lo + g * C::CPG;  // the group's first channel
+            const bool hi = a.p1 != nullptr && gc0 >= a.pC0;
+            const bool straddle = a.p1 != nullptr && gc0 < a.pC0 && gc0 + C::CPG > a.pC0;
+            const int cb = hi ? a.pC0 : 0;
+#pragma unroll
+            for (int k = 0; k < C::NPG; ++k) {
+                const int e = tq + kDT * k;
+                const int ci = e / C::PPLANE, rem = e % C::PPLANE;
+                const int r = rem / C::PC, c = rem % C::PC;
+                const int gc = gc0 + ci, iy = iy0 + r * C::GS, ix = ix0 + c * C::GS;
+                const bool ok = e < C::CPG * C::PPLANE && gc < Cp && (unsigned)iy < (unsigned)a.Hs &&
+                                (unsigned)ix < (unsigned)a.Ws;
+                const unsigned pix = (unsigned)(iy * a.Ws + ix);
+                if (!straddle) {
+                    pv[g][k] = ld_f32(hi ? rp1 : rp0, ok ? ((unsigned)(gc - cb) * (unsigned)HWs + pix) * 4u : OOB);
+                } else {
+                    pv[g][k] = ld_f32(rp0, ok && gc < a.pC0 ? ((unsigned)gc * (unsigned)HWs + pix) * 4u : OOB) +
+                               ld_f32(rp1, ok && gc >= a.pC0 ? ((unsigned)(gc - a.pC0) * (unsigned)HWs + pix) * 4u
+                                                              : OOB);
+                }
             }
         }
     };
@@ -508,10 +519,12 @@ __global__ __launch_bounds__(kDT) void dense_wgrad_mfma(WgdArgs a, float* __rest
             lds[C::D_OFF + (e / C::NPX) * C::DP + e % C::NPX] = dv[k];
         }
 #pragma unroll
-        for (int k = 0; k < C::NPE; ++k) {
-            const int e = tid + kDT * k;
-            if (e < C::CPB * C::PPLANE) lds[e] = p_split ? pv[k] + pv1[k] : pv[k];
-        }
+        for (int g = 0; g < GN; ++g)
+#pragma unroll
+            for (int k = 0; k < C::NPG; ++k) {
+                const int e = tid + kDT * k;
+                if (e < C::CPG * C::PPLANE) lds[g * C::CPG * C::PPLANE + e] = pv[g][k];
+            }
     };
 
     if (t0 < t1) load(t0);
@@ -521,28 +534,32 @@ __global__ __launch_bounds__(kDT) void dense_wgrad_mfma(WgdArgs a, float* __rest
         store();
         __syncthreads();
         if (t + 1 < t1) load(t + 1);
-        // k-steps two at a time: fully unrolled, the scheduler hoists all 16 x NTB operand
-        // reads of the tile into registers (~300 VGPRs)
+        // the wave's pixels in segments of 16 (8 k-steps) inside one tile row
+#pragma unroll 1
+        for (int sg = 0; sg < C::PPW / 16; ++sg) {
+            const int q = q0 + 16 * sg, r = q / C::TW, c = q % C::TW;
+            const int aoff = abase + q, boff = r * C::LS * C::PC + c * C::LS;
 #pragma unroll 2
-        for (int j = 0; j < C::TW / 2; ++j) {
-            const float av = lds[abase + 2 * j];
+            for (int j = 0; j < 8; ++j) {
+                const float av = lds[aoff + 2 * j];
 #pragma unroll
-            for (int u = 0; u < C::NTB; ++u) {
-                const float bv = lds[bbase[u] + 2 * j * C::LS];
-                acc[u] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[u], 0, 0, 0);
+                for (int u = 0; u < NT; ++u) {
+                    const float bv = lds[bbase[u] + boff + 2 * j * C::LS];
+                    acc[u] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[u], 0, 0, 0);
+                }
             }
         }
     }
 
-    // ---- this wave's partial [32][NCOLS] -> slice ks * 4 + w: C[row = m][col = n] ----
-    float* out = part + ((size_t)ks * 4 + w) * a.M * a.N;
+    // ---- this wave's partial [32][NT*32] -> slice ks * RG + rg: C[row = m][col = n] ----
+    float* out = part + ((size_t)ks * C::RG + rg) * a.M * a.N;
 #pragma unroll
-    for (int u = 0; u < C::NTB; ++u) {
-        const int n = n0 + 32 * u + li;
+    for (int u = 0; u < NT; ++u) {
+        const int n = n0 + gni * C::NCOLS + 32 * u + li;
         if (n >= a.N) continue;
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
-            const int m = m0 + (q & 3) + 8 * (q >> 2) + 4 * kk;
+            const int m = m0 + gmi * 32 + (q & 3) + 8 * (q >> 2) + 4 * kk;
             if (m < a.M) out[(size_t)m * a.N + n] = acc[u][q];
         }
     }
@@ -647,12 +664,17 @@ int launch_conv3x3_c1(const float* x, int B, int Cin, int H, int W, const float*
 }
 
 // ---- weight gradient ----
-constexpr int kWgdTargetBlocks = 512;  // two 4-wave workgroups per CU: one round
+struct WgdPlan {
+    WgdArgs a;
+    int nt, gm, gn, rg;
+};
 
-static WgdArgs wgrad_args(const nconv_dense_wgrad& g) {
-    WgdArgs a{};
+static WgdPlan wgrad_plan(const nconv_dense_wgrad& g) {
+    WgdPlan pl{};
+    WgdArgs& a = pl.a;
     const int cin = g.C0 + g.C1;
-    if (g.kind != NCONV_DENSE_TRANSPOSED_4X4) {  // Conv2d: D = dL/dy, patch = x
+    const bool tr = g.kind == NCONV_DENSE_TRANSPOSED_4X4;
+    if (!tr) {  // Conv2d: D = dL/dy, patch = x
         a.d0 = g.gy;
         a.d1 = nullptr;
         a.dC0 = g.Cout;
@@ -683,50 +705,75 @@ static WgdArgs wgrad_args(const nconv_dense_wgrad& g) {
         a.M = cin;
         a.N = g.Cout * 16;
     }
+    pl.nt = wgd_nt(g.kind, a.N);
+    const int nmg = (a.M + 31) / 32, nng = (a.N + 32 * pl.nt - 1) / (32 * pl.nt);
+    // groups per workgroup: pairs along M and N where they divide evenly; the strided 3x3
+    // stages tall patches, so it pairs along M only
+    pl.gm = (pl.nt > 1 && nmg % 2 == 0) ? 2 : 1;
+    pl.gn = (pl.nt > 1 && nng % 2 == 0 && !(g.kind == NCONV_DENSE_3X3 && g.stride == 2)) ? 2 : 1;
+    pl.rg = 4 / (pl.gm * pl.gn);
+    const int th = (tr || (g.kind == NCONV_DENSE_3X3 && g.stride == 2)) ? 2 : 4;
     a.ntx = (a.Wp + 31) / 32;
-    a.nty = (a.Hp + 3) / 4;
+    a.nty = (a.Hp + th - 1) / th;
     a.ntiles = (long long)g.B * a.ntx * a.nty;
-    const int ncols = 32 * wgd_nt(g.kind, a.N);
-    a.nng = (a.N + ncols - 1) / ncols;
-    a.nmg = (a.M + 31) / 32;
-    long long nks = kWgdTargetBlocks / (a.nng * a.nmg);
+    a.nbm = nmg / pl.gm;
+    a.nbn = nng / pl.gn;
+    long long nks = 512 / (a.nbm * a.nbn);  // about two workgroups per CU
     if (nks < 1) nks = 1;
     if (nks > a.ntiles) nks = a.ntiles;
     a.nks = (int)nks;
-    return a;
+    return pl;
 }
 
 size_t dense_wgrad_workspace_bytes(const nconv_dense_wgrad& g) {
-    const WgdArgs a = wgrad_args(g);
-    return (size_t)a.nks * 4 * a.M * a.N * sizeof(float);
+    const WgdPlan pl = wgrad_plan(g);
+    return (size_t)pl.a.nks * pl.rg * pl.a.M * pl.a.N * sizeof(float);
+}
+
+template <int KIND, int S, int NT>
+static bool go_wgrad(const WgdPlan& pl, float* ws, hipStream_t st) {
+    const dim3 grid(pl.a.nbm * pl.a.nbn * pl.a.nks), blk(kDT);
+    if (pl.gm == 1 && pl.gn == 1)
+        hipLaunchKernelGGL((dense_wgrad_mfma<KIND, S, NT, 1, 1>), grid, blk, 0, st, pl.a, ws);
+    else if constexpr (NT > 1) {
+        if (pl.gm == 2 && pl.gn == 1)
+            hipLaunchKernelGGL((dense_wgrad_mfma<KIND, S, NT, 2, 1>), grid, blk, 0, st, pl.a, ws);
+        else if constexpr (!(KIND == NCONV_DENSE_3X3 && S == 2) && KIND != NCONV_DENSE_1X1) {
+            if (pl.gm == 1 && pl.gn == 2)
+                hipLaunchKernelGGL((dense_wgrad_mfma<KIND, S, NT, 1, 2>), grid, blk, 0, st, pl.a, ws);
+            else
+                hipLaunchKernelGGL((dense_wgrad_mfma<KIND, S, NT, 2, 2>), grid, blk, 0, st, pl.a, ws);
+        } else {
+            return false;
+        }
+    } else {
+        return false;
+    }
+    return true;
 }
 
 int launch_dense_wgrad(const nconv_dense_wgrad& g, float* ws, size_t ws_bytes, hipStream_t st, const char** why) {
-    const WgdArgs a = wgrad_args(g);
+    const WgdPlan pl = wgrad_plan(g);
     if (ws_bytes < dense_wgrad_workspace_bytes(g)) {
         *why = "workspace too small (see nconv_dense_wgrad_workspace_bytes)";
         return -22;
     }
-    const dim3 grid(a.nng * a.nmg * a.nks), blk(kDT);
-    const bool one = a.N <= 32;
-#define NCONV_WG(KIND_, S_)                                                                                  \
-    if (g.kind == KIND_ && g.stride == S_) {                                                                \
-        if (one)                                                                                             \
-            hipLaunchKernelGGL((dense_wgrad_mfma<KIND_, S_, 1>), grid, blk, 0, st, a, ws);                  \
-        else                                                                                                 \
-            hipLaunchKernelGGL((dense_wgrad_mfma<KIND_, S_, wgd_ntb(KIND_)>), grid, blk, 0, st, a, ws);     \
-    } else
+    bool ok = false;
+#define NCONV_WG(KIND_, S_)                                                                     \
+    if (g.kind == KIND_ && g.stride == S_)                                                     \
+        ok = pl.nt == 1 ? go_wgrad<KIND_, S_, 1>(pl, ws, st) : go_wgrad<KIND_, S_, wgd_ntb(KIND_)>(pl, ws, st);
     NCONV_WG(NCONV_DENSE_3X3, 1)
     NCONV_WG(NCONV_DENSE_3X3, 2)
     NCONV_WG(NCONV_DENSE_1X1, 1)
     NCONV_WG(NCONV_DENSE_1X1, 2)
-    NCONV_WG(NCONV_DENSE_TRANSPOSED_4X4, 2) {
-        *why = "no weight-gradient kernel for this (kind, stride)";
+    NCONV_WG(NCONV_DENSE_TRANSPOSED_4X4, 2)
+#undef NCONV_WG
+    if (!ok) {
+        *why = "no weight-gradient kernel for this (kind, stride, grouping)";
         return -95;
     }
-#undef NCONV_WG
-    const int mn = a.M * a.N;
-    hipLaunchKernelGGL(dense_wgrad_reduce, dim3((mn + 63) / 64), dim3(kDT), 0, st, ws, a.nks * 4, mn, g.gw);
+    const int mn = pl.a.M * pl.a.N;
+    hipLaunchKernelGGL(dense_wgrad_reduce, dim3((mn + 63) / 64), dim3(kDT), 0, st, ws, pl.a.nks * pl.rg, mn, g.gw);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         *why = hipGetErrorString(e);
