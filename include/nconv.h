@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define NCONV_ABI_VERSION 5
+#define NCONV_ABI_VERSION 6
 
 /* How a layer's input (data x, confidence c) is produced from its source tensors. These are the
  * DNET glue ops fused into the layer's load stage (models/step1.py:53,61-90). */
@@ -198,6 +198,36 @@ size_t nconv_dense_wgrad_workspace_bytes(const nconv_dense_wgrad* g);
 
 /* gw = dL/dW: deterministic (fixed-order reduction of per-workgroup partial sums). */
 int nconv_dense_conv_wgrad(const nconv_dense_wgrad* g, void* workspace, size_t workspace_bytes, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Training-mode BatchNorm2d + optional ReLU: batch statistics, running statistics updated in
+ * place (momentum, unbiased running variance) — the nn.BatchNorm2d(train) -> nn.ReLU pairs of
+ * models/step2.py:139-143 (RGBEncoder), :189-191 (Basic2d), :207-213 (Basic2dTrans) — and its
+ * backward (the ReLU mask recomputed from x). Deterministic (fixed-order reductions).
+ * ------------------------------------------------------------------------------------------ */
+typedef struct nconv_bn_train {
+    int B, C, H, W;
+    const float* x;            /* (B, C, H, W) input                                              */
+    const float* gamma;        /* (C) or NULL (= 1)                                               */
+    const float* beta;         /* (C) or NULL (= 0)                                               */
+    float* running_mean;       /* (C) updated by the forward, or NULL                             */
+    float* running_var;        /* (C) updated by the forward (unbiased variance), or NULL         */
+    float momentum, eps;
+    int relu;                  /* 1: y = max(BN(x), 0)                                            */
+    float* y;                  /* (B, C, H, W) forward output                                     */
+    float* mean;               /* (C) batch mean: written by the forward, read by the backward    */
+    float* invstd;             /* (C) 1/sqrt(biased batch variance + eps): likewise               */
+} nconv_bn_train;
+
+/* Workspace of nconv_bn_train_fwd / _bwd in bytes (0 if the descriptor is invalid). */
+size_t nconv_bn_workspace_bytes(const nconv_bn_train* p);
+
+int nconv_bn_train_fwd(const nconv_bn_train* p, void* workspace, size_t workspace_bytes, void* stream);
+
+/* gx = dL/dx (NULL: skip), ggamma / gbeta = dL/dgamma, dL/dbeta (OVERWRITTEN; NULL: skip),
+ * from gy = dL/dy and the forward's x, mean, invstd. */
+int nconv_bn_train_bwd(const nconv_bn_train* p, const float* gy, float* gx, float* ggamma, float* gbeta,
+                       void* workspace, size_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -13,7 +13,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # NCONV_LIB: an alternative build of the same library (kernel-tuning experiments)
 LIB_PATH = os.environ.get("NCONV_LIB") or os.path.join(_HERE, "libnconv.so")
-ABI_VERSION = 5
+ABI_VERSION = 6
 BWD_ACCUMULATE = 1
 
 # enum nconv_load_mode
@@ -36,6 +36,9 @@ EXPORTED = (
     "nconv_conv3x3_c1",
     "nconv_dense_wgrad_workspace_bytes",
     "nconv_dense_conv_wgrad",
+    "nconv_bn_workspace_bytes",
+    "nconv_bn_train_fwd",
+    "nconv_bn_train_bwd",
 )
 
 
@@ -68,6 +71,14 @@ class NconvDenseWgrad(ctypes.Structure):
                 ("x0", ctypes.c_void_p), ("C0", ctypes.c_int), ("x1", ctypes.c_void_p), ("C1", ctypes.c_int),
                 ("H", ctypes.c_int), ("W", ctypes.c_int), ("gy", ctypes.c_void_p), ("Cout", ctypes.c_int),
                 ("Ho", ctypes.c_int), ("Wo", ctypes.c_int), ("gw", ctypes.c_void_p)]
+
+
+class NconvBnTrain(ctypes.Structure):
+    _fields_ = [("B", ctypes.c_int), ("C", ctypes.c_int), ("H", ctypes.c_int), ("W", ctypes.c_int),
+                ("x", ctypes.c_void_p), ("gamma", ctypes.c_void_p), ("beta", ctypes.c_void_p),
+                ("running_mean", ctypes.c_void_p), ("running_var", ctypes.c_void_p),
+                ("momentum", ctypes.c_float), ("eps", ctypes.c_float), ("relu", ctypes.c_int),
+                ("y", ctypes.c_void_p), ("mean", ctypes.c_void_p), ("invstd", ctypes.c_void_p)]
 
 
 _lib = None
@@ -107,6 +118,12 @@ def _declare(lib):
     lib.nconv_dense_wgrad_workspace_bytes.argtypes = [ctypes.POINTER(NconvDenseWgrad)]
     lib.nconv_dense_conv_wgrad.restype = I
     lib.nconv_dense_conv_wgrad.argtypes = [ctypes.POINTER(NconvDenseWgrad), P, ctypes.c_size_t, P]
+    lib.nconv_bn_workspace_bytes.restype = ctypes.c_size_t
+    lib.nconv_bn_workspace_bytes.argtypes = [ctypes.POINTER(NconvBnTrain)]
+    lib.nconv_bn_train_fwd.restype = I
+    lib.nconv_bn_train_fwd.argtypes = [ctypes.POINTER(NconvBnTrain), P, ctypes.c_size_t, P]
+    lib.nconv_bn_train_bwd.restype = I
+    lib.nconv_bn_train_bwd.argtypes = [ctypes.POINTER(NconvBnTrain), P, P, P, P, P, ctypes.c_size_t, P]
 
 
 def lib():

@@ -1,0 +1,257 @@
+// batchnorm.hip — training-mode BatchNorm2d (+ ReLU) of the RGB-guided model on gfx950.
+//
+// Replaces nn.BatchNorm2d in training mode (batch statistics, running-stat update) followed by
+// nn.ReLU — RGBEncoder (models/step2.py:139-143), Basic2d (:189-191), Basic2dTrans (:207-213) —
+// and the autograd of both. HBM-bound passes over NCHW fp32:
+//   forward : bn_stats (1 read: per-chunk count / mean / M2, Welford-style), bn_finalize (per
+//             channel, chunks combined in a fixed order with Chan's formula: deterministic,
+//             no E[x^2] - E[x]^2 cancellation; running mean / unbiased running var updated),
+//             bn_apply (1 read + 1 write: y = [relu](gamma (x - mean) invstd + beta));
+//   backward: bn_bwd_stats (2 reads: sum g' and sum g' xhat per chunk, g' = g masked by the
+//             recomputed ReLU), bn_bwd_finalize (fixed order), bn_bwd_apply (2 reads + 1 write:
+//             gx = gamma invstd (g' - sum g' / N - xhat sum g' xhat / N)).
+// A chunk is kChunk consecutive elements of one (image, channel) plane, 16 per thread (float4
+// loads when the plane size is a multiple of 4).
+#include "nconv_internal.h"
+
+namespace nconv {
+
+constexpr int kBT = 256;
+constexpr int kChunk = 4096;
+constexpr int kPer = kChunk / kBT;  // elements per thread
+
+__device__ __forceinline__ float block_sum(float v, float* red) {
+#pragma unroll
+    for (int s = 32; s > 0; s >>= 1) v += __shfl_xor(v, s);
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    __syncthreads();  // red is reused between calls
+    if (lane == 0) red[w] = v;
+    __syncthreads();
+    return ((red[0] + red[1]) + red[2]) + red[3];
+}
+
+// Loads the thread's kPer elements of chunk j of plane (b, c): element i = j*kChunk + 4*tid + k
+// (+ kBT*4 per float4 group); out-of-plane elements are flagged invalid.
+__device__ __forceinline__ void load_chunk(const float* plane, int hw, int j, bool vec, float (&v)[kPer],
+                                           bool (&ok)[kPer]) {
+    const int base = j * kChunk;
+#pragma unroll
+    for (int g = 0; g < kPer / 4; ++g) {
+        const int i0 = base + (g * kBT + threadIdx.x) * 4;
+        if (vec && i0 + 3 < hw) {
+            const f4 q = *reinterpret_cast<const f4*>(plane + i0);
+            v[4 * g] = q.x;
+            v[4 * g + 1] = q.y;
+            v[4 * g + 2] = q.z;
+            v[4 * g + 3] = q.w;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) ok[4 * g + k] = true;
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                ok[4 * g + k] = i0 + k < hw;
+                v[4 * g + k] = ok[4 * g + k] ? plane[i0 + k] : 0.f;
+            }
+        }
+    }
+}
+
+// part[(c * nparts + b * ncp + j) * 3 + {0,1,2}] = (count, mean, M2) of chunk j of plane (b, c)
+__global__ __launch_bounds__(kBT) void bn_stats(const float* __restrict__ x, int C, int hw, int ncp, int nparts,
+                                                int vec, float* __restrict__ part) {
+    __shared__ float red[4];
+    const int j = blockIdx.x, c = blockIdx.y, b = blockIdx.z;
+    const float* plane = x + ((size_t)b * C + c) * hw;
+    float v[kPer];
+    bool ok[kPer];
+    load_chunk(plane, hw, j, vec != 0, v, ok);
+    const int n = min(kChunk, hw - j * kChunk);
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) s += v[k];  // invalid elements are 0
+    const float mean = block_sum(s, red) / (float)n;
+    float m2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const float d = ok[k] ? v[k] - mean : 0.f;
+        m2 = fmaf(d, d, m2);
+    }
+    m2 = block_sum(m2, red);
+    if (threadIdx.x == 0) {
+        float* o = part + ((size_t)c * nparts + (size_t)b * ncp + j) * 3;
+        o[0] = (float)n;
+        o[1] = mean;
+        o[2] = m2;
+    }
+}
+
+// One thread per channel: Chan's parallel combination of the chunks in a fixed order.
+__global__ __launch_bounds__(kBT) void bn_finalize(const float* __restrict__ part, int C, int nparts, float momentum,
+                                                   float eps, float* __restrict__ rmean, float* __restrict__ rvar,
+                                                   float* __restrict__ mean_out, float* __restrict__ invstd_out) {
+    const int c = blockIdx.x * kBT + threadIdx.x;
+    if (c >= C) return;
+    const float* p = part + (size_t)c * nparts * 3;
+    double n = 0.0, mean = 0.0, m2 = 0.0;  // 418+ chunks per channel: combine in double
+    for (int k = 0; k < nparts; ++k) {
+        const double nb = p[3 * k], mb = p[3 * k + 1], m2b = p[3 * k + 2];
+        const double nn = n + nb, d = mb - mean;
+        mean += d * nb / nn;
+        m2 += m2b + d * d * n * nb / nn;
+        n = nn;
+    }
+    const double var = m2 / n;
+    mean_out[c] = (float)mean;
+    invstd_out[c] = (float)(1.0 / sqrt(var + (double)eps));
+    if (rmean) rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * mean);
+    if (rvar) rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * (n > 1.0 ? m2 / (n - 1.0) : var));
+}
+
+__device__ __forceinline__ float bn_y(float x, float mu, float is, float g, float bt, bool relu) {
+    const float y = fmaf((x - mu) * is, g, bt);
+    return relu ? fmaxf(y, 0.f) : y;
+}
+
+__global__ __launch_bounds__(kBT) void bn_apply(const float* __restrict__ x, float* __restrict__ y, int C, int hw,
+                                                size_t n4, const float* __restrict__ mean,
+                                                const float* __restrict__ invstd, const float* __restrict__ gamma,
+                                                const float* __restrict__ beta, int relu) {
+    // hw % 4 == 0: float4 over the whole tensor (a float4 never crosses a plane)
+    for (size_t i = (size_t)blockIdx.x * kBT + threadIdx.x; i < n4; i += (size_t)gridDim.x * kBT) {
+        const int c = (int)((i * 4 / hw) % C);
+        const float mu = mean[c], is = invstd[c], g = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+        const f4 q = reinterpret_cast<const f4*>(x)[i];
+        reinterpret_cast<f4*>(y)[i] = (f4){bn_y(q.x, mu, is, g, bt, relu), bn_y(q.y, mu, is, g, bt, relu),
+                                           bn_y(q.z, mu, is, g, bt, relu), bn_y(q.w, mu, is, g, bt, relu)};
+    }
+}
+
+__global__ __launch_bounds__(kBT) void bn_apply_scalar(const float* __restrict__ x, float* __restrict__ y, int C,
+                                                       int hw, size_t n, const float* __restrict__ mean,
+                                                       const float* __restrict__ invstd,
+                                                       const float* __restrict__ gamma,
+                                                       const float* __restrict__ beta, int relu) {
+    for (size_t i = (size_t)blockIdx.x * kBT + threadIdx.x; i < n; i += (size_t)gridDim.x * kBT) {
+        const int c = (int)((i / hw) % C);
+        y[i] = bn_y(x[i], mean[c], invstd[c], gamma ? gamma[c] : 1.f, beta ? beta[c] : 0.f, relu);
+    }
+}
+
+// part[(c * nparts + b * ncp + j) * 2 + {0,1}] = (sum g', sum g' xhat) of chunk j of plane (b, c)
+__global__ __launch_bounds__(kBT) void bn_bwd_stats(const float* __restrict__ gy, const float* __restrict__ x, int C,
+                                                    int hw, int ncp, int nparts, int vec,
+                                                    const float* __restrict__ mean, const float* __restrict__ invstd,
+                                                    const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                    int relu, float* __restrict__ part) {
+    __shared__ float red[4];
+    const int j = blockIdx.x, c = blockIdx.y, b = blockIdx.z;
+    const size_t off = ((size_t)b * C + c) * hw;
+    float g[kPer], v[kPer];
+    bool ok[kPer];
+    load_chunk(gy + off, hw, j, vec != 0, g, ok);
+    load_chunk(x + off, hw, j, vec != 0, v, ok);
+    const float mu = mean[c], is = invstd[c], ga = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+    float s = 0.f, sx = 0.f;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const float xh = (v[k] - mu) * is;
+        const float gg = (relu && !(fmaf(xh, ga, bt) > 0.f)) ? 0.f : g[k];  // invalid: g = 0
+        s += gg;
+        sx = fmaf(gg, xh, sx);
+    }
+    s = block_sum(s, red);
+    sx = block_sum(sx, red);
+    if (threadIdx.x == 0) {
+        float* o = part + ((size_t)c * nparts + (size_t)b * ncp + j) * 2;
+        o[0] = s;
+        o[1] = sx;
+    }
+}
+
+__global__ __launch_bounds__(kBT) void bn_bwd_finalize(const float* __restrict__ part, int C, int nparts,
+                                                       float* __restrict__ sums, float* __restrict__ ggamma,
+                                                       float* __restrict__ gbeta) {
+    const int c = blockIdx.x * kBT + threadIdx.x;
+    if (c >= C) return;
+    const float* p = part + (size_t)c * nparts * 2;
+    double s = 0.0, sx = 0.0;
+    for (int k = 0; k < nparts; ++k) {
+        s += p[2 * k];
+        sx += p[2 * k + 1];
+    }
+    sums[2 * c] = (float)s;
+    sums[2 * c + 1] = (float)sx;
+    if (gbeta) gbeta[c] = (float)s;
+    if (ggamma) ggamma[c] = (float)sx;
+}
+
+__global__ __launch_bounds__(kBT) void bn_bwd_apply(const float* __restrict__ gy, const float* __restrict__ x,
+                                                    float* __restrict__ gx, int C, int hw, size_t n, float inv_n,
+                                                    const float* __restrict__ mean, const float* __restrict__ invstd,
+                                                    const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                    int relu, const float* __restrict__ sums) {
+    for (size_t i = (size_t)blockIdx.x * kBT + threadIdx.x; i < n; i += (size_t)gridDim.x * kBT) {
+        const int c = (int)((i / hw) % C);
+        const float mu = mean[c], is = invstd[c], ga = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+        const float xh = (x[i] - mu) * is;
+        const float gg = (relu && !(fmaf(xh, ga, bt) > 0.f)) ? 0.f : gy[i];
+        gx[i] = ga * is * (gg - sums[2 * c] * inv_n - xh * (sums[2 * c + 1] * inv_n));
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+static int bn_ncp(const nconv_bn_train& p) { return (p.H * p.W + kChunk - 1) / kChunk; }
+
+size_t bn_workspace_bytes(const nconv_bn_train& p) {
+    const size_t nparts = (size_t)p.B * bn_ncp(p);
+    return (nparts * p.C * 3 + 2 * (size_t)p.C) * sizeof(float);
+}
+
+static unsigned elem_blocks(size_t n) {
+    size_t b = (n + kBT - 1) / kBT;
+    return (unsigned)(b > 8192 ? 8192 : (b ? b : 1));
+}
+
+int launch_bn_train_fwd(const nconv_bn_train& p, float* ws, hipStream_t st, const char** why) {
+    const int hw = p.H * p.W, ncp = bn_ncp(p), nparts = p.B * ncp;
+    const int vec = (hw % 4 == 0) && ((uintptr_t)p.x % 16 == 0);
+    hipLaunchKernelGGL(bn_stats, dim3(ncp, p.C, p.B), dim3(kBT), 0, st, p.x, p.C, hw, ncp, nparts, vec, ws);
+    hipLaunchKernelGGL(bn_finalize, dim3((p.C + kBT - 1) / kBT), dim3(kBT), 0, st, ws, p.C, nparts, p.momentum, p.eps,
+                       p.running_mean, p.running_var, p.mean, p.invstd);
+    const size_t n = (size_t)p.B * p.C * hw;
+    if (vec && ((uintptr_t)p.y % 16 == 0))
+        hipLaunchKernelGGL(bn_apply, dim3(elem_blocks(n / 4)), dim3(kBT), 0, st, p.x, p.y, p.C, hw, n / 4, p.mean,
+                           p.invstd, p.gamma, p.beta, p.relu);
+    else
+        hipLaunchKernelGGL(bn_apply_scalar, dim3(elem_blocks(n)), dim3(kBT), 0, st, p.x, p.y, p.C, hw, n, p.mean,
+                           p.invstd, p.gamma, p.beta, p.relu);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        *why = hipGetErrorString(e);
+        return -5;
+    }
+    return 0;
+}
+
+int launch_bn_train_bwd(const nconv_bn_train& p, const float* gy, float* gx, float* ggamma, float* gbeta, float* ws,
+                        hipStream_t st, const char** why) {
+    const int hw = p.H * p.W, ncp = bn_ncp(p), nparts = p.B * ncp;
+    const int vec = (hw % 4 == 0) && ((uintptr_t)p.x % 16 == 0) && ((uintptr_t)gy % 16 == 0);
+    float* sums = ws + (size_t)nparts * p.C * 3;
+    hipLaunchKernelGGL(bn_bwd_stats, dim3(ncp, p.C, p.B), dim3(kBT), 0, st, gy, p.x, p.C, hw, ncp, nparts, vec, p.mean,
+                       p.invstd, p.gamma, p.beta, p.relu, ws);
+    hipLaunchKernelGGL(bn_bwd_finalize, dim3((p.C + kBT - 1) / kBT), dim3(kBT), 0, st, ws, p.C, nparts, sums, ggamma,
+                       gbeta);
+    const size_t n = (size_t)p.B * p.C * hw;
+    if (gx)
+        hipLaunchKernelGGL(bn_bwd_apply, dim3(elem_blocks(n)), dim3(kBT), 0, st, gy, p.x, gx, p.C, hw, n,
+                           1.f / (float)((size_t)p.B * hw), p.mean, p.invstd, p.gamma, p.beta, p.relu, sums);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        *why = hipGetErrorString(e);
+        return -5;
+    }
+    return 0;
+}
+
+}  // namespace nconv

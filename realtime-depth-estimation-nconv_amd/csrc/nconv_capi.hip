@@ -78,6 +78,15 @@ const char* validate_wgrad(const nconv_dense_wgrad* g) {
     return nullptr;
 }
 
+const char* validate_bn(const nconv_bn_train* p) {
+    if (!p) return "null descriptor";
+    if (p->B <= 0 || p->C <= 0 || p->H <= 0 || p->W <= 0) return "non-positive B/C/H/W";
+    if ((long long)p->H * p->W > (1LL << 30)) return "plane too large";
+    if (!p->x || !p->mean || !p->invstd) return "null x / mean / invstd";
+    if (!(p->eps > 0.f) || p->momentum < 0.f || p->momentum > 1.f) return "eps must be > 0 and momentum in [0, 1]";
+    return nullptr;
+}
+
 LayerDev make_dev(const nconv_layer* L) {
     LayerDev d;
     d.L = *L;
@@ -233,6 +242,32 @@ int nconv_dense_conv_wgrad(const nconv_dense_wgrad* g, void* workspace, size_t w
     if (need && (!workspace || workspace_bytes < need)) return fail(-22, fn, "workspace too small");
     const char* why = nullptr;
     int rc = nconv::launch_dense_wgrad(*g, (float*)workspace, workspace_bytes, (hipStream_t)stream, &why);
+    return rc ? fail(rc, fn, why) : 0;
+}
+
+size_t nconv_bn_workspace_bytes(const nconv_bn_train* p) {
+    if (validate_bn(p)) return 0;
+    return nconv::bn_workspace_bytes(*p);
+}
+
+int nconv_bn_train_fwd(const nconv_bn_train* p, void* workspace, size_t workspace_bytes, void* stream) {
+    const char* fn = "nconv_bn_train_fwd";
+    if (const char* why = validate_bn(p)) return fail(-22, fn, why);
+    if (!p->y) return fail(-22, fn, "null y");
+    if (!workspace || workspace_bytes < nconv::bn_workspace_bytes(*p)) return fail(-22, fn, "workspace too small");
+    const char* why = nullptr;
+    int rc = nconv::launch_bn_train_fwd(*p, (float*)workspace, (hipStream_t)stream, &why);
+    return rc ? fail(rc, fn, why) : 0;
+}
+
+int nconv_bn_train_bwd(const nconv_bn_train* p, const float* gy, float* gx, float* ggamma, float* gbeta,
+                       void* workspace, size_t workspace_bytes, void* stream) {
+    const char* fn = "nconv_bn_train_bwd";
+    if (const char* why = validate_bn(p)) return fail(-22, fn, why);
+    if (!gy) return fail(-22, fn, "null gy");
+    if (!workspace || workspace_bytes < nconv::bn_workspace_bytes(*p)) return fail(-22, fn, "workspace too small");
+    const char* why = nullptr;
+    int rc = nconv::launch_bn_train_bwd(*p, gy, gx, ggamma, gbeta, (float*)workspace, (hipStream_t)stream, &why);
     return rc ? fail(rc, fn, why) : 0;
 }
 

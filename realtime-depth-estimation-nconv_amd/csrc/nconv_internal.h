@@ -54,4 +54,10 @@ int launch_conv3x3_c1(const float* x, int B, int Cin, int H, int W, const float*
 size_t dense_wgrad_workspace_bytes(const nconv_dense_wgrad& g);
 int launch_dense_wgrad(const nconv_dense_wgrad& g, float* ws, size_t ws_bytes, hipStream_t st, const char** why);
 
+// Training-mode BatchNorm (+ ReLU).
+size_t bn_workspace_bytes(const nconv_bn_train& p);
+int launch_bn_train_fwd(const nconv_bn_train& p, float* ws, hipStream_t st, const char** why);
+int launch_bn_train_bwd(const nconv_bn_train& p, const float* gy, float* gx, float* ggamma, float* gbeta, float* ws,
+                        hipStream_t st, const char** why);
+
 }  // namespace nconv

@@ -208,3 +208,75 @@ class HeadFn(torch.autograd.Function):
 
 def head_fn(x, w, res):
     return HeadFn.apply(x, w, res)
+
+
+# ------------------------------------------------------------------------------------------------
+# Training-mode BatchNorm2d + ReLU (nconv_bn_train_fwd / _bwd)
+# ------------------------------------------------------------------------------------------------
+def _bn_desc(x, bn, relu, y=None, mean=None, invstd=None, update=True):
+    d = _lib.NconvBnTrain()
+    d.B, d.C, d.H, d.W = x.shape
+    d.x = x.data_ptr()
+    d.gamma = bn.weight.data_ptr() if bn.weight is not None else None
+    d.beta = bn.bias.data_ptr() if bn.bias is not None else None
+    track = update and bn.track_running_stats and bn.running_mean is not None
+    d.running_mean = bn.running_mean.data_ptr() if track else None
+    d.running_var = bn.running_var.data_ptr() if track else None
+    if bn.momentum is None:  # cumulative moving average (num_batches_tracked already incremented)
+        d.momentum = 1.0 / float(bn.num_batches_tracked.item()) if track else 0.0
+    else:
+        d.momentum = bn.momentum
+    d.eps = bn.eps
+    d.relu = 1 if relu else 0
+    d.y = y.data_ptr() if y is not None else None
+    d.mean, d.invstd = mean.data_ptr(), invstd.data_ptr()
+    return d
+
+
+class BatchNormReLUFn(torch.autograd.Function):
+    """[relu](BatchNorm2d(x)) with batch statistics (module in training mode): the forward
+    updates bn.running_mean / running_var / num_batches_tracked like nn.BatchNorm2d."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, bn, relu):
+        x = x.contiguous()
+        C = x.shape[1]
+        mean = torch.empty(C, device=x.device, dtype=torch.float32)
+        invstd = torch.empty_like(mean)
+        y = torch.empty_like(x)
+        if bn.track_running_stats and bn.num_batches_tracked is not None:
+            bn.num_batches_tracked.add_(1)
+        d = _bn_desc(x, bn, relu, y, mean, invstd)
+        L = _lib.lib()
+        nb = L.nconv_bn_workspace_bytes(ctypes.byref(d))
+        ws = torch.empty(max(nb, 4) // 4, device=x.device, dtype=torch.float32)
+        _lib.check(L.nconv_bn_train_fwd(ctypes.byref(d), _lib.ptr(ws), nb, _lib.stream_handle(x.device)),
+                   "nconv_bn_train_fwd")
+        ctx.bn, ctx.relu = bn, relu
+        ctx.save_for_backward(x, weight, bias, mean, invstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        x, weight, bias, mean, invstd = ctx.saved_tensors
+        g = g.contiguous()
+        need = ctx.needs_input_grad
+        gx = torch.empty_like(x) if need[0] else None
+        gw = torch.empty_like(weight) if (weight is not None and need[1]) else None
+        gb = torch.empty_like(bias) if (bias is not None and need[2]) else None
+        d = _bn_desc(x, ctx.bn, ctx.relu, None, mean, invstd, update=False)
+        L = _lib.lib()
+        nb = L.nconv_bn_workspace_bytes(ctypes.byref(d))
+        ws = torch.empty(max(nb, 4) // 4, device=x.device, dtype=torch.float32)
+        _lib.check(L.nconv_bn_train_bwd(ctypes.byref(d), _lib.ptr(g), _lib.ptr(gx), _lib.ptr(gw), _lib.ptr(gb),
+                                        _lib.ptr(ws), nb, _lib.stream_handle(x.device)), "nconv_bn_train_bwd")
+        return gx, gw, gb, None, None
+
+
+def bn_relu(x, bn, relu):
+    """[relu](bn(x)) for an nn.BatchNorm2d: libnconv kernels in training mode (batch statistics),
+    the module itself (running statistics) otherwise."""
+    if bn.training or not bn.track_running_stats:
+        return BatchNormReLUFn.apply(x, bn.weight, bn.bias, bn, relu)
+    y = bn(x)
+    return torch.relu(y) if relu else y

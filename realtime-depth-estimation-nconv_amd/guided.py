@@ -27,6 +27,13 @@ from . import dense as D
 from .dnet import SETP1_NCONV
 
 
+def _bn_act(y, bn, act):
+    """act(bn(y)): BatchNorm (+ ReLU) on libnconv's kernels (dense.bn_relu)."""
+    if isinstance(act, nn.ReLU):
+        return D.bn_relu(y, bn, True)
+    return act(D.bn_relu(y, bn, False))
+
+
 def Conv1x1(in_planes, out_planes, stride, bias=False, groups=1, dilation=1, padding_mode="zeros"):
     """1x1 projection shortcut (step2.py:130-132)."""
     return nn.Conv2d(in_planes, out_planes, kernel_size=1, stride=stride, bias=bias)
@@ -66,7 +73,7 @@ class RGBEncoder(nn.Module):
 
     def train_forward(self, x):
         conv, bn, act, sc = self.encoder[0], self.encoder[1], self.encoder[2], self.downsample[0]
-        y = act(bn(D.conv_fn(x, conv.weight, conv.bias, D.DENSE_3X3, conv.stride[0])))
+        y = _bn_act(D.conv_fn(x, conv.weight, conv.bias, D.DENSE_3X3, conv.stride[0]), bn, act)
         return y + D.conv_fn(x, sc.weight, None, D.DENSE_1X1, sc.stride[0])
 
 
@@ -110,9 +117,7 @@ class Basic2d(nn.Module):
             raise NotImplementedError("dense path: 3x3 / padding 1 Basic2d only")
         fuse = bn is None and isinstance(act, nn.ReLU)  # conv + bias + ReLU in one kernel
         y = D.conv_fn(x0, conv.weight, conv.bias, D.DENSE_3X3, conv.stride[0], relu=fuse, x1=x1)
-        if bn is not None:
-            y = bn(y)
-        return y if fuse else act(y)
+        return y if fuse else (_bn_act(y, bn, act) if bn is not None else act(y))
 
 
 class Basic2dTrans(nn.Module):
@@ -147,7 +152,7 @@ class Basic2dTrans(nn.Module):
 
     def train_forward(self, x0, x1=None):
         y = D.conv_fn(x0, self.conv.weight, self.conv.bias, D.DENSE_TRANSPOSED_4X4, 2, x1=x1)
-        return self.relu(self.bn(y))
+        return _bn_act(y, self.bn, self.relu) if isinstance(self.bn, nn.BatchNorm2d) else self.relu(self.bn(y))
 
 
 class UpCat(nn.Module):

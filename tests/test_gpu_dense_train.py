@@ -181,3 +181,40 @@ def test_guided_training_step_matches_oracle(nconv_amd, gpu, H, W):
             bad.append(f"{k}: {rel:.2e}")
     assert not bad, "\n".join(bad)
     assert named["rgb_encoder4.encoder.0.weight"].grad is None  # unused in forward (step2.py:46)
+
+
+@pytest.mark.parametrize("B,C,H,W,relu", [(2, 32, 19, 45, True), (3, 64, 8, 10, False), (1, 33, 100, 130, True)])
+def test_batchnorm_relu_train(nconv_amd, gpu, B, C, H, W, relu):
+    """Training-mode BatchNorm2d (+ ReLU) against nn.BatchNorm2d in float64: output, running-stat
+    update (momentum 0.1, unbiased variance), num_batches_tracked, and the three gradients."""
+    D = nconv_amd.dense
+    g = torch.Generator().manual_seed(B * 100 + C)
+    x = torch.randn(B, C, H, W, generator=g, dtype=torch.float64) * 3 + 1.5
+    ref_bn = torch.nn.BatchNorm2d(C).double()
+    with torch.no_grad():
+        ref_bn.weight.uniform_(0.5, 1.5, generator=g)
+        ref_bn.bias.uniform_(-0.5, 0.5, generator=g)
+        ref_bn.running_mean.uniform_(-1, 1, generator=g)
+        ref_bn.running_var.uniform_(0.5, 2, generator=g)
+    bn = torch.nn.BatchNorm2d(C).to(gpu)
+    bn.load_state_dict({k: v.float() if v.is_floating_point() else v for k, v in ref_bn.state_dict().items()})
+    bn.train()
+    ref_bn.train()
+    xg = x.to(gpu, torch.float32).requires_grad_(True)
+    y = D.bn_relu(xg, bn, relu)
+    xr = x.clone().requires_grad_(True)
+    yr = ref_bn(xr)
+    yr = torch.relu(yr) if relu else yr
+    if relu:  # the ReLU mask the GPU took
+        yr = yr * (y.detach().double().cpu() > 0)
+    gy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    y.backward(gy.to(gpu, torch.float32))
+    yr.backward(gy)
+    torch.cuda.synchronize()
+    _close(y.detach(), yr.detach(), "forward", 1e-5)
+    _close(bn.running_mean, ref_bn.running_mean, "running_mean", 1e-5)
+    _close(bn.running_var, ref_bn.running_var, "running_var", 1e-5)
+    assert int(bn.num_batches_tracked) == int(ref_bn.num_batches_tracked) == 1
+    _close(xg.grad, xr.grad, "grad x", 1e-4)
+    _close(bn.weight.grad, ref_bn.weight.grad, "grad weight", 1e-4)
+    _close(bn.bias.grad, ref_bn.bias.grad, "grad bias", 1e-4)
