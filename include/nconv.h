@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define NCONV_ABI_VERSION 6
+#define NCONV_ABI_VERSION 7
 
 /* How a layer's input (data x, confidence c) is produced from its source tensors. These are the
  * DNET glue ops fused into the layer's load stage (models/step1.py:53,61-90). */
@@ -228,6 +228,14 @@ int nconv_bn_train_fwd(const nconv_bn_train* p, void* workspace, size_t workspac
  * from gy = dL/dy and the forward's x, mean, invstd. */
 int nconv_bn_train_bwd(const nconv_bn_train* p, const float* gy, float* gx, float* ggamma, float* gbeta,
                        void* workspace, size_t workspace_bytes, void* stream);
+
+/* Backward of the ReLU after a biased convolution and its bias gradient (ConvBlock, step2.py:
+ * 290-297, bias + ReLU fused in nconv_dense_conv_fwd): g_masked = g * (out > 0) (out = the
+ * forward's ReLU output; out == NULL: no ReLU, g_masked unused), gbias[c] = sum over images and
+ * pixels of the masked gradient (NULL: skip). All (B, C, H, W) except gbias (C). */
+size_t nconv_relu_bias_bwd_workspace_bytes(int B, int C, int H, int W);
+int nconv_relu_bias_bwd(int B, int C, int H, int W, const float* g, const float* out, float* g_masked,
+                        float* gbias, void* workspace, size_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -13,7 +13,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # NCONV_LIB: an alternative build of the same library (kernel-tuning experiments)
 LIB_PATH = os.environ.get("NCONV_LIB") or os.path.join(_HERE, "libnconv.so")
-ABI_VERSION = 6
+ABI_VERSION = 7
 BWD_ACCUMULATE = 1
 
 # enum nconv_load_mode
@@ -39,6 +39,8 @@ EXPORTED = (
     "nconv_bn_workspace_bytes",
     "nconv_bn_train_fwd",
     "nconv_bn_train_bwd",
+    "nconv_relu_bias_bwd_workspace_bytes",
+    "nconv_relu_bias_bwd",
 )
 
 
@@ -124,6 +126,10 @@ def _declare(lib):
     lib.nconv_bn_train_fwd.argtypes = [ctypes.POINTER(NconvBnTrain), P, ctypes.c_size_t, P]
     lib.nconv_bn_train_bwd.restype = I
     lib.nconv_bn_train_bwd.argtypes = [ctypes.POINTER(NconvBnTrain), P, P, P, P, P, ctypes.c_size_t, P]
+    lib.nconv_relu_bias_bwd_workspace_bytes.restype = ctypes.c_size_t
+    lib.nconv_relu_bias_bwd_workspace_bytes.argtypes = [I, I, I, I]
+    lib.nconv_relu_bias_bwd.restype = I
+    lib.nconv_relu_bias_bwd.argtypes = [I, I, I, I, P, P, P, P, P, ctypes.c_size_t, P]
 
 
 def lib():

@@ -199,6 +199,72 @@ __global__ __launch_bounds__(kBT) void bn_bwd_apply(const float* __restrict__ gy
     }
 }
 
+// ---- ReLU backward + bias gradient of a convolution (the ConvBlock / bias-only layers):
+//      g' = g * (out > 0) (when out is given), gbias = sum of g' over images and pixels ----
+__global__ __launch_bounds__(kBT) void relu_bias_stats(const float* __restrict__ g, const float* __restrict__ out,
+                                                       float* __restrict__ gm, int C, int hw, int ncp, int nparts,
+                                                       int vec, float* __restrict__ part) {
+    __shared__ float red[4];
+    const int j = blockIdx.x, c = blockIdx.y, b = blockIdx.z;
+    const size_t off = ((size_t)b * C + c) * hw;
+    float v[kPer], o[kPer];
+    bool ok[kPer];
+    load_chunk(g + off, hw, j, vec != 0, v, ok);
+    if (out) {
+        load_chunk(out + off, hw, j, vec != 0, o, ok);
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) v[k] = o[k] > 0.f ? v[k] : 0.f;
+        if (gm) {
+            const int base = j * kChunk;
+#pragma unroll
+            for (int q = 0; q < kPer / 4; ++q) {
+                const int i0 = base + (q * kBT + threadIdx.x) * 4;
+                if (vec && i0 + 3 < hw) {
+                    *reinterpret_cast<f4*>(gm + off + i0) = (f4){v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
+                } else {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        if (i0 + k < hw) gm[off + i0 + k] = v[4 * q + k];
+                }
+            }
+        }
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) s += v[k];
+    s = block_sum(s, red);
+    if (threadIdx.x == 0) part[(size_t)c * nparts + (size_t)b * ncp + j] = s;
+}
+
+__global__ __launch_bounds__(kBT) void channel_sum_finalize(const float* __restrict__ part, int C, int nparts,
+                                                            float* __restrict__ out) {
+    const int c = blockIdx.x * kBT + threadIdx.x;
+    if (c >= C) return;
+    double s = 0.0;
+    for (int k = 0; k < nparts; ++k) s += part[(size_t)c * nparts + k];
+    out[c] = (float)s;
+}
+
+size_t relu_bias_workspace_bytes(int B, int C, int H, int W) {
+    return (size_t)B * ((H * W + kChunk - 1) / kChunk) * C * sizeof(float);
+}
+
+int launch_relu_bias_bwd(int B, int C, int H, int W, const float* g, const float* out, float* gm, float* gbias,
+                         float* ws, hipStream_t st, const char** why) {
+    const int hw = H * W, ncp = (hw + kChunk - 1) / kChunk, nparts = B * ncp;
+    const int vec = (hw % 4 == 0) && ((uintptr_t)g % 16 == 0) && (!out || (uintptr_t)out % 16 == 0) &&
+                    (!gm || (uintptr_t)gm % 16 == 0);
+    hipLaunchKernelGGL(relu_bias_stats, dim3(ncp, C, B), dim3(kBT), 0, st, g, out, gm, C, hw, ncp, nparts, vec, ws);
+    if (gbias)
+        hipLaunchKernelGGL(channel_sum_finalize, dim3((C + kBT - 1) / kBT), dim3(kBT), 0, st, ws, C, nparts, gbias);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        *why = hipGetErrorString(e);
+        return -5;
+    }
+    return 0;
+}
+
 // ------------------------------------------------------------------------------------------------
 static int bn_ncp(const nconv_bn_train& p) { return (p.H * p.W + kChunk - 1) / kChunk; }
 

@@ -53,7 +53,8 @@ struct DcCfg {
     static constexpr int SP = TR ? 1 : S;                 // patch stride
     static constexpr int KS = KIND == NCONV_DENSE_1X1 ? 1 : (KIND == NCONV_DENSE_CONV4X4_S2 ? 4 : 3);
     static constexpr int PAD = KIND == NCONV_DENSE_1X1 ? 0 : 1;
-    static constexpr int TH = SP == 1 ? 8 : 4, RW = TH / 4, TW = 32;
+    // rows per wave: 4 (2 strided) with 32 output channels, 2 (1) with 64: 4 MFMAs per 4-5 LDS reads
+    static constexpr int TH = (SP == 1 ? 8 : 4) * (COUT == 32 ? 2 : 1), RW = TH / 4, TW = 32;
     static constexpr int PR = (TH - 1) * SP + KS, PC = (TW - 1) * SP + KS;
     static constexpr int ROW = PC;
     // B reads: 32 lanes on the columns of one patch row, lane half kk on the channel plane:

@@ -271,6 +271,25 @@ int nconv_bn_train_bwd(const nconv_bn_train* p, const float* gy, float* gx, floa
     return rc ? fail(rc, fn, why) : 0;
 }
 
+size_t nconv_relu_bias_bwd_workspace_bytes(int B, int C, int H, int W) {
+    if (B <= 0 || C <= 0 || H <= 0 || W <= 0) return 0;
+    return nconv::relu_bias_workspace_bytes(B, C, H, W);
+}
+
+int nconv_relu_bias_bwd(int B, int C, int H, int W, const float* g, const float* out, float* g_masked,
+                        float* gbias, void* workspace, size_t workspace_bytes, void* stream) {
+    const char* fn = "nconv_relu_bias_bwd";
+    if (B <= 0 || C <= 0 || H <= 0 || W <= 0) return fail(-22, fn, "non-positive B/C/H/W");
+    if ((long long)H * W > (1LL << 30)) return fail(-22, fn, "plane too large");
+    if (!g) return fail(-22, fn, "null g");
+    if (!workspace || workspace_bytes < nconv::relu_bias_workspace_bytes(B, C, H, W))
+        return fail(-22, fn, "workspace too small");
+    const char* why = nullptr;
+    int rc = nconv::launch_relu_bias_bwd(B, C, H, W, g, out, g_masked, gbias, (float*)workspace, (hipStream_t)stream,
+                                         &why);
+    return rc ? fail(rc, fn, why) : 0;
+}
+
 int nconv_conv3x3_c1(const float* x, int B, int Cin, int H, int W, const float* w, const float* res, float* out,
                      void* stream) {
     const char* fn = "nconv_conv3x3_c1";

@@ -57,6 +57,9 @@ int launch_dense_wgrad(const nconv_dense_wgrad& g, float* ws, size_t ws_bytes, h
 // Training-mode BatchNorm (+ ReLU).
 size_t bn_workspace_bytes(const nconv_bn_train& p);
 int launch_bn_train_fwd(const nconv_bn_train& p, float* ws, hipStream_t st, const char** why);
+size_t relu_bias_workspace_bytes(int B, int C, int H, int W);
+int launch_relu_bias_bwd(int B, int C, int H, int W, const float* g, const float* out, float* gm, float* gbias,
+                         float* ws, hipStream_t st, const char** why);
 int launch_bn_train_bwd(const nconv_bn_train& p, const float* gy, float* gx, float* ggamma, float* gbeta, float* ws,
                         hipStream_t st, const char** why);
 

@@ -136,6 +136,16 @@ def wgrad(x0, x1, g, kind, stride, wshape):
     return gw
 
 
+def relu_bias_bwd(g, out, g_masked, gbias):
+    """g_masked = g * (out > 0) (out given), gbias = sum of the (masked) gradient per channel."""
+    B, C, H, W = g.shape
+    L = _lib.lib()
+    nb = L.nconv_relu_bias_bwd_workspace_bytes(B, C, H, W)
+    ws = torch.empty(max(nb, 4) // 4, device=g.device, dtype=torch.float32)
+    _lib.check(L.nconv_relu_bias_bwd(B, C, H, W, _lib.ptr(g), _lib.ptr(out), _lib.ptr(g_masked), _lib.ptr(gbias),
+                                     _lib.ptr(ws), nb, _lib.stream_handle(g.device)), "nconv_relu_bias_bwd")
+
+
 class DenseConvFn(torch.autograd.Function):
     """y = [relu](conv(cat(x0, x1); weight) + bias) for Conv2d 3x3 pad 1 / 1x1 (stride 1 | 2) and
     ConvTranspose2d 4x4 s2 p1 — nn.Conv2d / nn.ConvTranspose2d (+ ReLU, + the torch.cat before
@@ -159,21 +169,26 @@ class DenseConvFn(torch.autograd.Function):
     def backward(ctx, g):
         x0, x1, weight, out = ctx.saved_tensors
         g = g.contiguous()
-        if ctx.relu:  # ReLU backward: gradient where the output is positive
-            g = g.masked_fill(out <= 0, 0.0)
         need = ctx.needs_input_grad
         gx0 = gx1 = gw = gb = None
-        if need[0] or need[1]:
-            cin = x0.shape[1] + (0 if x1 is None else x1.shape[1])
-            gx = dgrad(g, weight, ctx.kind, ctx.stride, (x0.shape[0], cin, x0.shape[2], x0.shape[3]))
-            if x1 is None:
-                gx0 = gx
-            else:
-                gx0, gx1 = gx[:, :ctx.c0], gx[:, ctx.c0:]
+        if ctx.relu or (ctx.has_bias and need[3]):
+            # ReLU backward (gradient where the output is positive) and the bias gradient, one pass
+            gb = torch.empty(g.shape[1], device=g.device, dtype=torch.float32) if ctx.has_bias and need[3] else None
+            gm = torch.empty_like(g) if ctx.relu else None
+            relu_bias_bwd(g, out if ctx.relu else None, gm, gb)
+            g = gm if ctx.relu else g
+        # input gradient per source: the forward weight's input-channel slice of each source, so
+        # each gradient is written contiguous (no split / copy of a concatenated gradient)
+        co = ctx.c0
+        tr = ctx.kind == DENSE_TRANSPOSED_4X4
+        w = weight.detach()
+        if need[0]:
+            w0 = w if x1 is None else (w[:co] if tr else w[:, :co])
+            gx0 = dgrad(g, w0, ctx.kind, ctx.stride, x0.shape)
+        if x1 is not None and need[1]:
+            gx1 = dgrad(g, w[co:] if tr else w[:, co:], ctx.kind, ctx.stride, x1.shape)
         if need[2]:
             gw = wgrad(x0, x1, g, ctx.kind, ctx.stride, weight.shape)
-        if ctx.has_bias and need[3]:
-            gb = g.sum(dim=(0, 2, 3))
         return gx0, gx1, gw, gb, None, None, None
 
 

@@ -218,3 +218,22 @@ def test_batchnorm_relu_train(nconv_amd, gpu, B, C, H, W, relu):
     _close(xg.grad, xr.grad, "grad x", 1e-4)
     _close(bn.weight.grad, ref_bn.weight.grad, "grad weight", 1e-4)
     _close(bn.bias.grad, ref_bn.bias.grad, "grad bias", 1e-4)
+
+
+@pytest.mark.parametrize("B,C,H,W,relu", [(2, 32, 19, 45, True), (3, 64, 8, 10, False), (1, 5, 3, 7, True)])
+def test_relu_bias_bwd(nconv_amd, gpu, B, C, H, W, relu):
+    """nconv_relu_bias_bwd: g * (out > 0) bit-exact, per-channel sum of the masked gradient within
+    1e-5 normwise of float64."""
+    D = nconv_amd.dense
+    g = torch.Generator().manual_seed(B * 7 + C)
+    gy = torch.randn(B, C, H, W, generator=g)
+    out = torch.randn(B, C, H, W, generator=g).clamp_min(0)
+    gg, og = gy.to(gpu), out.to(gpu)
+    gm = torch.empty_like(gg) if relu else None
+    gb = torch.empty(C, device=gpu)
+    D.relu_bias_bwd(gg, og if relu else None, gm, gb)
+    torch.cuda.synchronize()
+    ref = gy.masked_fill(out <= 0, 0.0) if relu else gy
+    if relu:
+        assert torch.equal(gm.cpu(), ref)
+    _close(gb, ref.double().sum(dim=(0, 2, 3)), "gbias", 1e-5)
