@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define NCONV_ABI_VERSION 7
+#define NCONV_ABI_VERSION 8
 
 /* How a layer's input (data x, confidence c) is produced from its source tensors. These are the
  * DNET glue ops fused into the layer's load stage (models/step1.py:53,61-90). */
@@ -34,6 +34,14 @@ enum nconv_load_mode {
     NCONV_LOAD_POOL2 = 2,            /* x = maxpool2x2(a.x), c = maxpool2x2(a.c), independent (step1.py:62-75) */
     NCONV_LOAD_UPCAT_SKIP_FIRST = 3, /* x = cat(a.x, up(b.x)), c likewise                   (step1.py:78-85)    */
     NCONV_LOAD_UPCAT_UP_FIRST = 4    /* x = cat(up(b.x), a.x), c likewise                   (step1.py:88-90)    */
+};
+
+/* Arithmetic of the NConv forward sums N = W*(x*c), D = W*c (nconv_layer.math). */
+enum nconv_math {
+    NCONV_MATH_BF16X3 = 0, /* default: bf16 matrix cores on split operands, v = hi + lo, products
+                              hi*hi + lo*hi + hi*lo in fp32 (<= ~1.1e-5 relative per product), for
+                              the 8-output-channel 5x5 (8 in) / 3x3 (16 in) layers; others FP32 */
+    NCONV_MATH_FP32 = 1    /* exact fp32 products on the vector ALU (packed FP32 FMA) */
 };
 
 /* One source tensor pair (data, confidence), physical shape (B, C, H, W). */
@@ -57,6 +65,7 @@ typedef struct nconv_layer {
     const float* weight; /* (Cout, Cin/groups, KH, KW), positive in practice                   */
     const float* bias;   /* (Cout)                                                              */
     const float* wsum;   /* (Cout): s[o] = sum of weight[o] (step1.py:141-144), see nconv_weight_prep */
+    int math;            /* enum nconv_math (forward only; 0 = default)                         */
 } nconv_layer;
 
 /* ABI version, for the Python loader's sanity check. */

@@ -13,11 +13,13 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # NCONV_LIB: an alternative build of the same library (kernel-tuning experiments)
 LIB_PATH = os.environ.get("NCONV_LIB") or os.path.join(_HERE, "libnconv.so")
-ABI_VERSION = 7
+ABI_VERSION = 8
 BWD_ACCUMULATE = 1
 
 # enum nconv_load_mode
 PLAIN, THRESH, POOL2, UPCAT_SKIP_FIRST, UPCAT_UP_FIRST = 0, 1, 2, 3, 4
+# enum nconv_math
+MATH_BF16X3, MATH_FP32 = 0, 1
 # enum nconv_dense_kind
 DENSE_3X3, DENSE_1X1, DENSE_TRANSPOSED_4X4, DENSE_CONV4X4_S2 = 0, 1, 2, 3
 
@@ -56,7 +58,8 @@ class NconvLayer(ctypes.Structure):
                 ("PH", ctypes.c_int), ("PW", ctypes.c_int), ("DH", ctypes.c_int), ("DW", ctypes.c_int),
                 ("groups", ctypes.c_int), ("eps", ctypes.c_float), ("load_mode", ctypes.c_int),
                 ("thresh", ctypes.c_float), ("a", NconvSrc), ("b", NconvSrc),
-                ("weight", ctypes.c_void_p), ("bias", ctypes.c_void_p), ("wsum", ctypes.c_void_p)]
+                ("weight", ctypes.c_void_p), ("bias", ctypes.c_void_p), ("wsum", ctypes.c_void_p),
+                ("math", ctypes.c_int)]
 
 
 class NconvDenseConv(ctypes.Structure):

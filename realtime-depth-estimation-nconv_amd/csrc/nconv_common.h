@@ -102,9 +102,8 @@ __device__ __forceinline__ void load_xc(const LayerDev& d, int b, int ci, int ih
 struct TileCoord {
     int tx, ty, b;
 };
-__device__ __forceinline__ TileCoord xcd_tile(int ntx, int nty, int nb) {
+__device__ __forceinline__ TileCoord xcd_tile(int ntx, int nty, int nb, int bid) {
     const int total = ntx * nty * nb;
-    const int bid = blockIdx.x;
     const int q = total / 8, r = total % 8, xcd = bid % 8, loc = bid / 8;
     const int t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
     TileCoord c;
@@ -113,6 +112,9 @@ __device__ __forceinline__ TileCoord xcd_tile(int ntx, int nty, int nb) {
     c.b = t / (ntx * nty);
     return c;
 }
+__device__ __forceinline__ TileCoord xcd_tile(int ntx, int nty, int nb) { return xcd_tile(ntx, nty, nb, blockIdx.x); }
+// Persistent grids: a workgroup walks the virtual ids blockIdx.x + i * gridDim.x; with gridDim.x a
+// multiple of 8 these stay on the workgroup's own XCD, so xcd_tile's mapping still holds.
 
 // Epilogue of NConv2d.forward (step1.py:123-147):  y = N / (D + eps) + b,   cout = D / s.
 // The quotients use v_rcp_f32 (1 ulp) and a multiply instead of the ~10-instruction IEEE division

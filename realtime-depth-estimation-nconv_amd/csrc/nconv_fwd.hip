@@ -358,6 +358,7 @@ int launch_fwd(const LayerDev& d, float* y, float* yc, float* py, float* pc, hip
     TailArgs t{};
     t.py = py;
     t.pc = pc;
+    if (launch_fwd_mfma(d, y, yc, t, false, st)) return last_launch(why);
     if (simple_geometry(L)) {
 #define NCONV_TRY(CIN, COUT, K, MODE)                                                       \
     if (L.Cin == CIN && L.Cout == COUT && L.KH == K && L.load_mode == MODE) {               \
@@ -411,6 +412,7 @@ int launch_fwd_tail(const LayerDev& d, const TailArgs& t, float* out, hipStream_
         return -95;  // EOPNOTSUPP
     }
     if (t.out_h <= 0 || t.out_w <= 0) return 0;
+    if (launch_fwd_mfma(d, out, nullptr, t, true, st)) return last_launch(why);
     go_tiled<16, 8, 3, NCONV_LOAD_UPCAT_UP_FIRST, true>(d, out, nullptr, t, t.out_h, t.out_w, st);
     return last_launch(why);
 }

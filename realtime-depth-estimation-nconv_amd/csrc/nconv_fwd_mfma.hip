@@ -1,0 +1,603 @@
+// nconv_fwd_mfma.hip — NConv forward on the bf16 matrix cores, split-bf16 ("bf16x3") arithmetic.
+//
+// The 8-output-channel NConv layers of DNET (step1.py:39-46: 8->8 5x5, 16->8 3x3) are
+// FP32-compute bound on the vector ALU (arithmetic intensity 32-50 flop/B against a ridge of
+// 19.7). gfx950 has no reduced-precision f32 MFMA (no xf32), but its bf16 MFMA runs at 16x the
+// FP32 rate, so each fp32 operand v is split into v = hi + lo (hi = bf16(v), lo = bf16(v - hi))
+// and every product is formed as  a_hi*b_hi + a_lo*b_hi + a_hi*b_lo  with fp32 accumulation.
+// The dropped a_lo*b_lo and the split residuals are <= 2^-18 |a*b| each, so a product carries a
+// relative error <= ~1.1e-5 and — every term of N and D being a product of a positive weight and
+// a non-negative confidence (times the data for N) — so do the sums: inside the 1e-4 forward
+// tolerance with two orders of magnitude to spare in practice (errors are
+// unbiased; tests/test_gpu_layers.py measures them). NCONV_MATH_FP32 keeps the exact VALU path.
+//
+// GEMM shape (v_mfma_f32_16x16x32_bf16): a 16x16 output tile is 16 adjacent output columns (the
+// A rows, u) x (8 output channels o, 2 output rows s) (the B columns). The row shift s lives in
+// the weights: with k = (kh' in [0, K], kw, 8 input channels), B[k][(o, s)] = W[o][ci][kh'-s][kw]
+// (0 outside the kernel), A[u][k] = input[ci][row0 + kh'][col0 + u + kw], so one A fragment feeds
+// both output rows and all 8 output channels and no B column is wasted (8 channels alone would
+// fill half of a 16-wide tile). N and D share B and accumulate in separate tiles.
+//
+// Data flow per 256-thread workgroup (TH x 32 output pixels, all 8 channels): the layer's input
+// glue (2x2 max-pool / nearest-upsample + concat, step1.py:62-90) is evaluated while staging the
+// (TH+K-1) x (32+K-1) halo tile; each position's 8-channel vectors {x*c, c} are split and stored
+// as four bf16x8 planes (x*c hi/lo, c hi/lo), so every A fragment is one conflict-free
+// ds_read_b128 (16 lanes read 256 contiguous bytes). The weights' B fragments are built once per
+// workgroup into registers. Epilogue per lane: 4 adjacent pixels of one (channel, row):
+// y = N/(D+eps)+b, cout = D/s, 16-B stores, optionally the fused 2x2 max-pooled copies (rows s=0/1
+// of a pixel pair sit in lanes l, l^8) or nconv7 (1x1 over the 8 channels = lanes l^1, l^2, l^4)
+// with the crop, as the VALU kernels of nconv_fwd.hip do.
+#include <cstdlib>
+#include "nconv_internal.h"
+
+namespace nconv {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+namespace {
+
+constexpr int kMfThreads = 256;
+
+enum MfEpi { kEpiPlain = 0, kEpiPool = 1, kEpiTail = 2 };
+
+template <int CIN, int K, int TH>
+struct MfCfg {
+    static constexpr int G = CIN / 8;  // 8-channel groups (one bf16x8 per position and part)
+    static constexpr int TW = 32;      // two 16-column MFMA tiles
+    static constexpr int IH = TH + K - 1, IW = TW + K - 1;
+    static constexpr int NPOS = IH * IW;
+    static constexpr int NE = (NPOS + kMfThreads - 1) / kMfThreads;  // positions per thread
+    static constexpr int PSTRIDE = NPOS * 16;                        // bytes of one plane
+    static constexpr int LDS_IN = 4 * G * PSTRIDE;                   // [g][part][pos] bf16x8
+    static constexpr int NKP = (K + 1) * K * G;                      // k positions (kh', kw, g)
+    static constexpr int NT = (NKP + 3) / 4;                         // k-steps (4 positions each)
+    static constexpr int NRP = TH / 2;                               // row pairs, NRP / 4 per wave
+    static_assert(CIN % 8 == 0 && NRP % 4 == 0, "tile shape");
+};
+
+constexpr unsigned kOOB = 0x80000000u;
+constexpr int kOutPitch = 36;  // floats per row of a wave's output-transpose region  // buffer offset past any resource: access dropped
+
+__device__ __forceinline__ void st_f32(__amdgpu_buffer_rsrc_t r, unsigned off, float v) {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, (int)off, 0, 0);
+}
+__device__ __forceinline__ void st_f4(__amdgpu_buffer_rsrc_t r, unsigned off, f4 v) {
+    typedef unsigned u4 __attribute__((ext_vector_type(4)));
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, v), r, (int)off, 0, 0);
+}
+
+__device__ __forceinline__ void split8(const float (&v)[8], bf16x8& hi, bf16x8& lo) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const __bf16 h = (__bf16)v[j];
+        hi[j] = h;
+        lo[j] = (__bf16)(v[j] - (float)h);
+    }
+}
+
+// Staging of one tile's halo: per thread NE positions x CIN channels of {x, c}, loaded into
+// registers (load: glue evaluated, no wait) and later split into the four bf16x8 planes (store).
+template <int CIN, int K, int MODE, int TH>
+struct MfStage {
+    using C = MfCfg<CIN, K, TH>;
+    static constexpr bool UP = MODE == NCONV_LOAD_UPCAT_SKIP_FIRST || MODE == NCONV_LOAD_UPCAT_UP_FIRST;
+    static constexpr unsigned OOB = 0x80000000u;
+    float xv[C::NE][CIN], cv[C::NE][CIN];
+
+    __device__ __forceinline__ void load(const LayerDev& d, int b, int ih0, int iw0, int tid) {
+        const nconv_layer& L = d.L;
+        unsigned ga[C::NE], gb[UP ? C::NE : 1];
+#pragma unroll
+        for (int k = 0; k < C::NE; ++k) {
+            const int e = tid + kMfThreads * k;
+            const int r = e / C::IW, col = e - r * C::IW;
+            const int ih = ih0 + r, iw = iw0 + col;
+            const bool in = e < C::NPOS && (unsigned)ih < (unsigned)L.H && (unsigned)iw < (unsigned)L.W;
+            if constexpr (MODE == NCONV_LOAD_POOL2)
+                ga[k] = in ? (unsigned)((2 * ih) * L.a.W + 2 * iw) * 4u : OOB;
+            else
+                ga[k] = in ? (unsigned)(ih * L.a.W + iw) * 4u : OOB;
+            if constexpr (UP) {
+                const int sh = nearest_src(ih, L.b.H, L.H, d.up_scale_h);
+                const int sw = nearest_src(iw, L.b.W, L.W, d.up_scale_w);
+                gb[k] = in ? (unsigned)(sh * L.b.W + sw) * 4u : OOB;
+            }
+        }
+#pragma unroll
+        for (int ci = 0; ci < CIN; ++ci) {
+            const ChanSrc s = chan_src<MODE>(d, b, ci);  // wave-uniform
+            const __amdgpu_buffer_rsrc_t rx = plane_rsrc(s.x, s.bytes), rc = plane_rsrc(s.c, s.bytes);
+            if constexpr (MODE == NCONV_LOAD_POOL2) {
+                const unsigned row = (unsigned)s.W * 4u;
+#pragma unroll
+                for (int k = 0; k < C::NE; ++k) {
+                    const unsigned o2 = ga[k] == OOB ? OOB : ga[k] + row;
+                    const f2 x0 = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rx, ga[k], 0, 0));
+                    const f2 x1 = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rx, o2, 0, 0));
+                    const f2 c0 = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rc, ga[k], 0, 0));
+                    const f2 c1 = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rc, o2, 0, 0));
+                    xv[k][ci] = pool4v(x0.x, x0.y, x1.x, x1.y);
+                    cv[k][ci] = pool4v(c0.x, c0.y, c1.x, c1.y);
+                }
+            } else {
+                const bool up = UP && s.kind == kUp;
+#pragma unroll
+                for (int k = 0; k < C::NE; ++k) {
+                    const unsigned o = UP ? (up ? gb[UP ? k : 0] : ga[k]) : ga[k];
+#ifdef NCONV_EXP_MF_NOLOAD
+                    xv[k][ci] = (float)(o & 255);
+                    cv[k][ci] = 0.5f;
+#else
+                    xv[k][ci] = ld_f32(rx, o);
+                    cv[k][ci] = ld_f32(rc, o);
+#endif
+                }
+            }
+        }
+    }
+
+    static constexpr int BYTES = 0;  // no LDS of its own
+    __device__ __forceinline__ void issue(const LayerDev& d, int b, int ih0, int iw0, unsigned char*, int tid) {
+        load(d, b, ih0, iw0, tid);
+    }
+    __device__ __forceinline__ void to_planes(const LayerDev&, int, int, unsigned char* lds, const unsigned char*,
+                                              int tid) const {
+        store(lds, tid);
+    }
+
+    __device__ __forceinline__ void store(unsigned char* lds, int tid) const {
+#pragma unroll
+        for (int k = 0; k < C::NE; ++k) {
+            const int e = tid + kMfThreads * k;
+            if (C::NE * kMfThreads != C::NPOS && e >= C::NPOS) continue;
+#pragma unroll
+            for (int g = 0; g < C::G; ++g) {
+                float p[8], q[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    q[j] = cv[k][8 * g + j];
+                    p[j] = xv[k][8 * g + j] * q[j];
+                }
+                bf16x8 h, l;
+                unsigned char* base = lds + g * 4 * C::PSTRIDE + e * 16;
+                split8(p, h, l);
+                *reinterpret_cast<bf16x8*>(base) = h;
+                *reinterpret_cast<bf16x8*>(base + C::PSTRIDE) = l;
+                split8(q, h, l);
+                *reinterpret_cast<bf16x8*>(base + 2 * C::PSTRIDE) = h;
+                *reinterpret_cast<bf16x8*>(base + 3 * C::PSTRIDE) = l;
+            }
+        }
+    }
+};
+
+__device__ __forceinline__ int floor_div4(int v) { return v >> 2; }  // arithmetic shift: floor
+
+// Staging through LDS-DMA (buffer_load_dwordx4 ... lds): no registers hold the halo in flight and
+// one wave-instruction moves 1 KiB, four times the bytes of a dword load. The fp32 source rows are
+// copied as aligned 16-byte vectors (row width a multiple of 4 floats, so a vector is wholly in or
+// out of the image; out-of-image vectors carry an offset past the resource and land as zeros, the
+// convolution's padding): source a at the layer's resolution (IH rows x 10 vectors per channel),
+// and for the upsample-concat modes source b at its own half resolution (IH/2+1 rows x 6 vectors),
+// the exact 2x nearest upsampling being applied when the planes are formed. Sections (a.x, a.c,
+// b.x, b.c) are padded to whole 1-KiB pieces; LDS is lane-linear within a piece.
+template <int CIN, int K, int MODE, int TH>
+struct DmaStage {
+    using C = MfCfg<CIN, K, TH>;
+    static constexpr bool UP = MODE == NCONV_LOAD_UPCAT_SKIP_FIRST || MODE == NCONV_LOAD_UPCAT_UP_FIRST;
+    static constexpr int CA = UP ? CIN / 2 : CIN, CB = UP ? CIN / 2 : 0;
+    static constexpr int NVA = 10, SRA = C::IH;            // source a: vectors per row, rows
+    static constexpr int NVB = 6, SRB = C::IH / 2 + 1;     // source b (half resolution)
+    static constexpr int PA = (CA * SRA * NVA + 63) / 64;  // 1-KiB pieces per tensor of source a
+    static constexpr int PB = UP ? (CB * SRB * NVB + 63) / 64 : 0;
+    static constexpr int NP = 2 * PA + 2 * PB;
+    static constexpr int BYTES = NP * 1024;
+    static_assert(4 * NVA >= C::IW + 3 && 4 * NVB >= (C::IW + 1) / 2 + 4, "staged columns cover the halo");
+
+    __device__ __forceinline__ void issue(const LayerDev& d, int b, int ih0, int iw0, unsigned char* stage,
+                                          int tid) const {
+        const nconv_layer& L = d.L;
+        const int wave = tid >> 6, lane = tid & 63;
+#pragma unroll 1
+        for (int j = wave; j < NP; j += 4) {  // wave-uniform piece index
+            const int sec = j < 2 * PA ? j / PA : 2 + (j - 2 * PA) / PB;
+            const int jj = sec < 2 ? j - sec * PA : j - 2 * PA - (sec - 2) * PB;
+            const bool a = sec < 2;
+            const nconv_src& sr = a ? L.a : L.b;
+            const int Cs = a ? CA : CB, SR = a ? SRA : SRB, NV = a ? NVA : NVB;
+            const int r0 = a ? ih0 : (ih0 >> 1), c0 = 4 * floor_div4(a ? iw0 : (iw0 >> 1));
+            const float* base = ((sec & 1) ? sr.c : sr.x) + (size_t)b * Cs * sr.H * sr.W;
+            const __amdgpu_buffer_rsrc_t rs = plane_rsrc(base, Cs * sr.H * sr.W * 4);
+            const int f = jj * 64 + lane;
+            const int ch = f / (SR * NV), rem = f - ch * (SR * NV), row = rem / NV, vec = rem - row * NV;
+            const int gr = r0 + row, gc = c0 + 4 * vec;
+            const bool ok = ch < Cs && (unsigned)gr < (unsigned)sr.H && (unsigned)gc < (unsigned)sr.W;
+            const unsigned go = ok ? (unsigned)((ch * sr.H + gr) * sr.W + gc) * 4u : kOOB;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                rs, (__attribute__((address_space(3))) void*)(stage + j * 1024), 16, (int)go, 0, 0, 0);
+        }
+    }
+
+    // Wait for this wave's pieces, then (all pieces landed) form the bf16 planes.
+    __device__ __forceinline__ void to_planes(const LayerDev& d, int ih0, int iw0, unsigned char* lds,
+                                              const unsigned char* stage, int tid) const {
+        __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) expcnt(0) lgkmcnt(0)
+        __syncthreads();
+        const float* S = reinterpret_cast<const float*>(stage);
+        const int sha = iw0 - 4 * floor_div4(iw0);                   // column shift in source a rows
+        const int rb0 = ih0 >> 1, cb0 = 4 * floor_div4(iw0 >> 1);  // source b origin
+#pragma unroll
+        for (int k = 0; k < C::NE; ++k) {
+            const int e = tid + kMfThreads * k;
+            if (C::NE * kMfThreads != C::NPOS && e >= C::NPOS) continue;
+            const int r = e / C::IW, col = e - r * C::IW;
+            const int ia = r * (NVA * 4) + col + sha;
+            const int ib = (((ih0 + r) >> 1) - rb0) * (NVB * 4) + ((iw0 + col) >> 1) - cb0;
+#pragma unroll
+            for (int g = 0; g < C::G; ++g) {
+                float p[8], q[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int ci = 8 * g + j;
+                    bool from_a = true;
+                    int cs = ci;
+                    if constexpr (MODE == NCONV_LOAD_UPCAT_SKIP_FIRST) {
+                        from_a = ci < CA;
+                        cs = from_a ? ci : ci - CA;
+                    } else if constexpr (MODE == NCONV_LOAD_UPCAT_UP_FIRST) {
+                        from_a = ci >= CB;
+                        cs = from_a ? ci - CB : ci;
+                    }
+                    float xv, cv;
+                    if (from_a) {
+                        xv = S[cs * SRA * NVA * 4 + ia];
+                        cv = S[PA * 256 + cs * SRA * NVA * 4 + ia];
+                    } else {
+                        xv = S[2 * PA * 256 + cs * SRB * NVB * 4 + ib];
+                        cv = S[(2 * PA + PB) * 256 + cs * SRB * NVB * 4 + ib];
+                    }
+                    q[j] = cv;
+                    p[j] = xv * cv;
+                }
+                bf16x8 hh, ll;
+                unsigned char* base = lds + g * 4 * C::PSTRIDE + e * 16;
+                split8(p, hh, ll);
+                *reinterpret_cast<bf16x8*>(base) = hh;
+                *reinterpret_cast<bf16x8*>(base + C::PSTRIDE) = ll;
+                split8(q, hh, ll);
+                *reinterpret_cast<bf16x8*>(base + 2 * C::PSTRIDE) = hh;
+                *reinterpret_cast<bf16x8*>(base + 3 * C::PSTRIDE) = ll;
+            }
+        }
+    }
+};
+
+// Persistent: gridDim.x (a multiple of 8) workgroups walk the tiles; the next tile's halo loads
+// are in flight while the current one's MFMAs and epilogue run.
+#ifndef NCONV_MFMA_WAVES
+#define NCONV_MFMA_WAVES 3  // waves per SIMD: 168 VGPRs (3 workgroups per CU) without spilling
+#endif
+// POOL2 staging holds four values per element before pooling: 2 waves per SIMD (no spills)
+template <int MODE, bool DMA>
+constexpr int mf_waves() { return DMA || MODE == NCONV_LOAD_POOL2 ? 2 : NCONV_MFMA_WAVES; }
+template <int CIN, int K, int MODE, int EPI, int TH>
+constexpr int mf_lds_bytes(bool dma) {
+    return MfCfg<CIN, K, TH>::LDS_IN + (EPI == kEpiTail ? 0 : 4 * 2 * 16 * kOutPitch * 4) +
+           (dma ? DmaStage<CIN, K, MODE, TH>::BYTES : 0);
+}
+template <int CIN, int K, int MODE, int EPI, int TH, bool VEC, bool DMA>
+__global__ __launch_bounds__(kMfThreads) __attribute__((amdgpu_waves_per_eu(mf_waves<MODE, DMA>(), mf_waves<MODE, DMA>()))) void fwd_mfma(LayerDev d, float* __restrict__ y, float* __restrict__ yc,
+                                                       TailArgs t) {
+    using C = MfCfg<CIN, K, TH>;
+    using Stage = typename std::conditional<DMA, DmaStage<CIN, K, MODE, TH>, MfStage<CIN, K, MODE, TH>>::type;
+    // input planes, (non-tail) four waves' output-transpose regions (y and cout), DMA staging
+    __shared__ __attribute__((aligned(16))) unsigned char lds[mf_lds_bytes<CIN, K, MODE, EPI, TH>(DMA)];
+    unsigned char* const stage = lds + mf_lds_bytes<CIN, K, MODE, EPI, TH>(false);
+    const nconv_layer& L = d.L;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const bool tail = EPI == kEpiTail;
+    const int gh = tail ? t.out_h : L.Ho, gw = tail ? t.out_w : L.Wo;  // the written grid
+    const int ntx = (gw + C::TW - 1) / C::TW, nty = (gh + TH - 1) / TH;
+    const int ntiles = ntx * nty * L.B;
+    const int off = tail ? t.off : 0;
+
+    Stage st;
+    int v = blockIdx.x;
+    {  // loads are unconditional (a block without tiles loads the last one and never uses it)
+        const TileCoord tc = xcd_tile(ntx, nty, L.B, v < ntiles ? v : ntiles - 1);
+        st.issue(d, tc.b, tc.ty * TH + off - L.PH, tc.tx * C::TW + off - L.PW, stage, tid);
+    }
+
+    // ---- B fragments (weights, once per workgroup) and per-lane A offsets ----
+    const int u = lane & 15, h = lane >> 4;
+    const int o = lane & 7, s = (lane >> 3) & 1;  // this lane's B / C column (o, s)
+    bf16x8 bh[C::NT], bl[C::NT];
+    int aoff[C::NT];
+#pragma unroll
+    for (int q = 0; q < C::NT; ++q) {
+        const int pos = 4 * q + h;
+        float w[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) w[j] = 0.f;
+        int a = (1 * C::IW) * 16;  // padding positions read (kh'=1, kw=0): inside both rows' windows
+        if (pos < C::NKP) {
+            const int g = pos % C::G, qq = pos / C::G, kw = qq % K, khp = qq / K, kh = khp - s;
+            a = g * 4 * C::PSTRIDE + (khp * C::IW + kw) * 16;
+            if (kh >= 0 && kh < K) {
+                const float* wp = L.weight + ((size_t)(o * CIN + g * 8) * K + kh) * K + kw;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) w[j] = wp[j * K * K];
+            }
+        }
+        split8(w, bh[q], bl[q]);
+        aoff[q] = a + u * 16;
+    }
+    const float eps = L.eps, bo = L.bias[o];
+    const float rcp_s = __builtin_amdgcn_rcpf(L.wsum[o]);
+
+#pragma unroll 1
+    for (; v < ntiles; v += gridDim.x) {
+        const TileCoord tc = xcd_tile(ntx, nty, L.B, v);
+        const int b = tc.b;
+        const int R0 = tc.ty * TH, C0 = tc.tx * C::TW;  // tile origin in the written grid
+        const int oh0 = R0 + off, ow0 = C0 + off;         // ... in this layer's output grid
+        st.to_planes(d, oh0 - L.PH, ow0 - L.PW, lds, stage, tid);
+        __syncthreads();
+        {  // next tile's loads fly during this tile's MFMAs (the last tile re-loads itself)
+            const int vn = v + (int)gridDim.x < ntiles ? v + (int)gridDim.x : v;
+            const TileCoord tn = xcd_tile(ntx, nty, L.B, vn);
+            st.issue(d, tn.b, tn.ty * TH + off - L.PH, tn.tx * C::TW + off - L.PW, stage, tid);
+        }
+
+        // ---- MFMAs: wave w takes the row pairs rp = w, w+4, ..., both 16-column halves ct ----
+        typedef float f4_ __attribute__((ext_vector_type(4)));
+#pragma unroll 1
+        for (int rpi = 0; rpi < C::NRP / 4; ++rpi) {
+            const int rp = wave + 4 * rpi;
+            f4_ accN[2], accD[2];
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct) {
+                const unsigned char* tb = lds + (2 * rp * C::IW + 16 * ct) * 16;
+                f4_ n = {0.f, 0.f, 0.f, 0.f}, dd = {0.f, 0.f, 0.f, 0.f};
+#ifdef NCONV_EXP_MF_NOMFMA
+                n[0] = tb[aoff[0]];
+#else
+#pragma unroll
+                for (int q = 0; q < C::NT; ++q) {
+                    const unsigned char* p = tb + aoff[q];
+                    const bf16x8 nh = *reinterpret_cast<const bf16x8*>(p);
+                    const bf16x8 nl = *reinterpret_cast<const bf16x8*>(p + C::PSTRIDE);
+                    const bf16x8 dh = *reinterpret_cast<const bf16x8*>(p + 2 * C::PSTRIDE);
+                    const bf16x8 dl = *reinterpret_cast<const bf16x8*>(p + 3 * C::PSTRIDE);
+                    n = __builtin_amdgcn_mfma_f32_16x16x32_bf16(nl, bh[q], n, 0, 0, 0);
+                    dd = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dl, bh[q], dd, 0, 0, 0);
+                    n = __builtin_amdgcn_mfma_f32_16x16x32_bf16(nh, bl[q], n, 0, 0, 0);
+                    dd = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dh, bl[q], dd, 0, 0, 0);
+                    n = __builtin_amdgcn_mfma_f32_16x16x32_bf16(nh, bh[q], n, 0, 0, 0);
+                    dd = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dh, bh[q], dd, 0, 0, 0);
+                }
+#endif
+                accN[ct] = n;
+                accD[ct] = dd;
+            }
+
+            // ---- epilogue: this lane holds (o, row oh, columns 16 ct + 4 h .. +3) per half ct ----
+            // Every global store is an unconditional buffer store; lanes with nothing to write carry
+            // an offset past the resource (dropped by the hardware). The number of stores per tile is
+            // thus static, so the wait for the next tile's loads (issued before these stores) does not
+            // also wait for the stores to complete.
+            float yv[2][4], cv[2][4];
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    yv[ct][r] = accN[ct][r] * __builtin_amdgcn_rcpf(accD[ct][r] + eps) + bo;
+                    cv[ct][r] = accD[ct][r] * rcp_s;
+                }
+            if constexpr (EPI != kEpiTail) {
+                // Transpose the row pair through this wave's LDS region ([o + 8 s][32 columns], pitch
+                // 36 floats: conflict-free f4 writes), so that each global store instruction writes
+                // eight whole 128-byte rows (lane: channel l>>3, columns 4 (l&7) .. +3) instead of
+                // sixteen 64-byte pieces.
+                float* wy = reinterpret_cast<float*>(lds + C::LDS_IN) + wave * (2 * 16 * kOutPitch);
+                float* wc = wy + 16 * kOutPitch;
+#pragma unroll
+                for (int ct = 0; ct < 2; ++ct) {
+                    const int lo = (o + 8 * s) * kOutPitch + 16 * ct + 4 * h;
+                    *reinterpret_cast<f4*>(wy + lo) = (f4){yv[ct][0], yv[ct][1], yv[ct][2], yv[ct][3]};
+                    *reinterpret_cast<f4*>(wc + lo) = (f4){cv[ct][0], cv[ct][1], cv[ct][2], cv[ct][3]};
+                }
+                __builtin_amdgcn_wave_barrier();  // DS operations of one wave execute in order
+                const int o8 = lane >> 3, qc = 4 * (lane & 7);
+                f4 ry[2], rcv[2];
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    ry[i] = *reinterpret_cast<const f4*>(wy + (o8 + 8 * i) * kOutPitch + qc);
+                    rcv[i] = *reinterpret_cast<const f4*>(wc + (o8 + 8 * i) * kOutPitch + qc);
+                }
+                __builtin_amdgcn_wave_barrier();
+                const int row0 = oh0 + 2 * rp, col = ow0 + qc;
+                const unsigned obytes = (unsigned)(8 * L.Ho * L.Wo) * 4u;
+                const __amdgpu_buffer_rsrc_t rsy = plane_rsrc(y + (size_t)b * 8 * L.Ho * L.Wo, obytes);
+                const __amdgpu_buffer_rsrc_t rsc = plane_rsrc(yc + (size_t)b * 8 * L.Ho * L.Wo, obytes);
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    const unsigned rowoff = (unsigned)((o8 * L.Ho + row0 + i) * L.Wo) * 4u;
+                    const bool rok = row0 + i < L.Ho;
+                    if constexpr (VEC) {  // Wo % 4 == 0: the 4 columns are all in or all out
+                        const unsigned so = rok && col < L.Wo ? rowoff + (unsigned)col * 4u : kOOB;
+                        st_f4(rsy, so, ry[i]);
+                        st_f4(rsc, so, rcv[i]);
+                    } else {
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const unsigned so = rok && col + r < L.Wo ? rowoff + (unsigned)(col + r) * 4u : kOOB;
+                            st_f32(rsy, so, ry[i][r]);
+                            st_f32(rsc, so, rcv[i][r]);
+                        }
+                    }
+                }
+                if constexpr (EPI == kEpiPool) {  // 2x2 max-pool of the row pair, both rows in this lane
+                    const int Hp = L.Ho >> 1, Wp = L.Wo >> 1, pr = row0 >> 1, pc0 = col >> 1;
+                    const unsigned pbytes = (unsigned)(8 * Hp * Wp) * 4u;
+                    const __amdgpu_buffer_rsrc_t rpy = plane_rsrc(t.py + (size_t)b * 8 * Hp * Wp, pbytes);
+                    const __amdgpu_buffer_rsrc_t rpc = plane_rsrc(t.pc + (size_t)b * 8 * Hp * Wp, pbytes);
+#pragma unroll
+                    for (int hh = 0; hh < 2; ++hh) {
+                        const unsigned po = pr < Hp && pc0 + hh < Wp ? (unsigned)((o8 * Hp + pr) * Wp + pc0 + hh) * 4u : kOOB;
+                        st_f32(rpy, po, pool4v(ry[0][2 * hh], ry[0][2 * hh + 1], ry[1][2 * hh], ry[1][2 * hh + 1]));
+                        st_f32(rpc, po, pool4v(rcv[0][2 * hh], rcv[0][2 * hh + 1], rcv[1][2 * hh], rcv[1][2 * hh + 1]));
+                    }
+                }
+            } else {
+                // nconv7 (1x1, 8 -> 1) over the 8 channels in lanes l^1, l^2, l^4, then the crop
+                const int oh = oh0 + 2 * rp + s;
+                const float w7 = t.w7[o];
+                const float b7 = t.b7[0], s7 = t.s7[0];
+                const unsigned obytes = (unsigned)(t.out_h * t.out_w) * 4u;
+                const __amdgpu_buffer_rsrc_t ro = plane_rsrc(y + (size_t)b * t.out_h * t.out_w, obytes);
+                const __amdgpu_buffer_rsrc_t rc = plane_rsrc(t.out_c ? t.out_c + (size_t)b * t.out_h * t.out_w : y,
+                                                             t.out_c ? obytes : 0);
+                const int orow = R0 + 2 * rp + s;
+                const bool wr = o == 0 && orow < t.out_h;
+                const unsigned rowoff = (unsigned)(orow * t.out_w) * 4u;
+#pragma unroll
+                for (int ct = 0; ct < 2; ++ct) {
+                    const int ow = ow0 + 16 * ct + 4 * h, ocol = C0 + 16 * ct + 4 * h;
+                    float n7[4], d7[4];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const bool ok = (unsigned)oh < (unsigned)L.Ho && (unsigned)(ow + r) < (unsigned)L.Wo;
+                        n7[r] = ok ? w7 * (yv[ct][r] * cv[ct][r]) : 0.f;
+                        d7[r] = ok ? w7 * cv[ct][r] : 0.f;
+                    }
+#pragma unroll
+                    for (int m = 1; m < 8; m <<= 1)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            n7[r] += __shfl_xor(n7[r], m);
+                            d7[r] += __shfl_xor(d7[r], m);
+                        }
+                    float ov[4], oc[4];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) nconv_epilogue(n7[r], d7[r], t.eps7, b7, s7, ov[r], oc[r]);
+                    if constexpr (VEC) {  // out_w % 4 == 0
+                        const unsigned so = wr && ocol < t.out_w ? rowoff + (unsigned)ocol * 4u : kOOB;
+                        st_f4(ro, so, (f4){ov[0], ov[1], ov[2], ov[3]});
+                        st_f4(rc, so, (f4){oc[0], oc[1], oc[2], oc[3]});
+                    } else {
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const unsigned so = wr && ocol + r < t.out_w ? rowoff + (unsigned)(ocol + r) * 4u : kOOB;
+                            st_f32(ro, so, ov[r]);
+                            st_f32(rc, so, oc[r]);
+                        }
+                    }
+                }
+            }
+        }
+        // every wave is done reading the planes before the next tile's are formed (DmaStage's own
+        // barrier, after its wait, does this there; a __syncthreads here would drain the DMA)
+        if constexpr (!DMA) __syncthreads();
+    }
+}
+
+// Persistent grid: resident workgroups per CU (by waves per SIMD and LDS) x CUs, a multiple of 8
+// (one XCD per blockIdx % 8).
+int mfma_grid_blocks(int waves, int lds_bytes) {
+    static int cus = 0;
+    if (cus == 0) {
+        int dev = 0, n = 256;
+        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+        cus = n;
+    }
+    int per_cu = waves < (160 * 1024) / lds_bytes ? waves : (160 * 1024) / lds_bytes;
+    if (const char* e = getenv("NCONV_MFMA_WG_PER_CU")) per_cu = atoi(e);
+    return (cus * (per_cu > 0 ? per_cu : 1) + 7) / 8 * 8;
+}
+
+template <int CIN, int K, int MODE, int EPI, int TH, bool DMA>
+void go_mfma(const LayerDev& d, float* y, float* yc, const TailArgs& t, int gh, int gw, hipStream_t st) {
+    using C = MfCfg<CIN, K, TH>;
+    const int ntiles = ((gw + C::TW - 1) / C::TW) * ((gh + TH - 1) / TH) * d.L.B;
+    int grid = mfma_grid_blocks(mf_waves<MODE, DMA>(), mf_lds_bytes<CIN, K, MODE, EPI, TH>(DMA));
+    if (ntiles < grid) grid = (ntiles + 7) / 8 * 8;
+    if (gw % 4 == 0)
+        hipLaunchKernelGGL((fwd_mfma<CIN, K, MODE, EPI, TH, true, DMA>), grid, dim3(kMfThreads), 0, st, d, y, yc, t);
+    else
+        hipLaunchKernelGGL((fwd_mfma<CIN, K, MODE, EPI, TH, false, DMA>), grid, dim3(kMfThreads), 0, st, d, y, yc, t);
+}
+
+// LDS-DMA staging: rows of every source a multiple of 4 floats (16-B vectors never straddle a row
+// end), exact 2x upsampling of source b with 8 + 8 channels, per-image sources below 2 GiB.
+// Measured slower than register staging at two workgroups per CU (nconv2 198 vs 179 us, the tail
+// 272 vs 169 us at B=8 352x1216): opt-in with NCONV_MFMA_DMA=1 while it is being tuned.
+bool dma_ok(const nconv_layer& L, int cin) {
+    static const bool on = [] {
+        const char* e = getenv("NCONV_MFMA_DMA");
+        return e && atoi(e) != 0;
+    }();
+    if (!on) return false;
+    if (L.load_mode != NCONV_LOAD_PLAIN && L.load_mode != NCONV_LOAD_UPCAT_SKIP_FIRST &&
+        L.load_mode != NCONV_LOAD_UPCAT_UP_FIRST)
+        return false;
+    const bool up = L.load_mode != NCONV_LOAD_PLAIN;
+    auto fine = [](const nconv_src& s) {
+        return s.W % 4 == 0 && ((uintptr_t)s.x % 16) == 0 && ((uintptr_t)s.c % 16) == 0 &&
+               (long long)s.C * s.H * s.W * 4 < (1LL << 31);
+    };
+    if (!fine(L.a)) return false;
+    if (!up) return L.a.C == cin && L.a.H == L.H && L.a.W == L.W;
+    return fine(L.b) && L.a.C == cin / 2 && L.b.C == cin / 2 && L.a.H == L.H && L.a.W == L.W && L.H == 2 * L.b.H &&
+           L.W == 2 * L.b.W;
+}
+
+template <int CIN, int K, int MODE, int EPI, int TH>
+void go_mfma_any(const LayerDev& d, float* y, float* yc, const TailArgs& t, int gh, int gw, hipStream_t st) {
+    if constexpr (MODE == NCONV_LOAD_POOL2)
+        go_mfma<CIN, K, MODE, EPI, TH, false>(d, y, yc, t, gh, gw, st);
+    else if (dma_ok(d.L, CIN))
+        go_mfma<CIN, K, MODE, EPI, TH, true>(d, y, yc, t, gh, gw, st);
+    else
+        go_mfma<CIN, K, MODE, EPI, TH, false>(d, y, yc, t, gh, gw, st);
+}
+
+}  // namespace
+
+// Returns true (and launches) when the layer has a matrix-core kernel: 8 output channels,
+// 8 input channels with a 5x5 kernel or 16 with a 3x3, stride 1, no dilation / groups.
+bool launch_fwd_mfma(const LayerDev& d, float* y, float* yc, const TailArgs& t, bool tail, hipStream_t st) {
+    const nconv_layer& L = d.L;
+    if (L.math != NCONV_MATH_BF16X3 || L.Cout != 8 || L.KH != L.KW || L.SH != 1 || L.SW != 1 || L.DH != 1 ||
+        L.DW != 1 || L.groups != 1)
+        return false;
+    const bool pool = !tail && t.py != nullptr;
+    const int gh = tail ? t.out_h : L.Ho, gw = tail ? t.out_w : L.Wo;
+    if (L.Cin == 8 && L.KH == 5 && L.load_mode == NCONV_LOAD_PLAIN && !tail) {
+        if (pool)
+            go_mfma_any<8, 5, NCONV_LOAD_PLAIN, kEpiPool, 8>(d, y, yc, t, gh, gw, st);
+        else
+            go_mfma_any<8, 5, NCONV_LOAD_PLAIN, kEpiPlain, 8>(d, y, yc, t, gh, gw, st);
+        return true;
+    }
+    if (L.Cin == 8 && L.KH == 5 && L.load_mode == NCONV_LOAD_POOL2 && !tail && !pool) {
+        go_mfma_any<8, 5, NCONV_LOAD_POOL2, kEpiPlain, 8>(d, y, yc, t, gh, gw, st);
+        return true;
+    }
+    if (L.Cin == 16 && L.KH == 3 && !pool) {
+        if (L.load_mode == NCONV_LOAD_UPCAT_SKIP_FIRST && !tail) {
+            go_mfma_any<16, 3, NCONV_LOAD_UPCAT_SKIP_FIRST, kEpiPlain, 8>(d, y, yc, t, gh, gw, st);
+            return true;
+        }
+        if (L.load_mode == NCONV_LOAD_UPCAT_UP_FIRST) {
+            if (tail)
+                go_mfma_any<16, 3, NCONV_LOAD_UPCAT_UP_FIRST, kEpiTail, 8>(d, y, nullptr, t, gh, gw, st);
+            else
+                go_mfma_any<16, 3, NCONV_LOAD_UPCAT_UP_FIRST, kEpiPlain, 8>(d, y, yc, t, gh, gw, st);
+            return true;
+        }
+    }
+    return false;
+}
+
+}  // namespace nconv

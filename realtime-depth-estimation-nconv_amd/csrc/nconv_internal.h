@@ -35,6 +35,7 @@ struct BwdArgs {
 
 // Forward. Return 0, or a negative errno with *why set.
 int launch_fwd(const LayerDev& d, float* y, float* yc, float* py, float* pc, hipStream_t st, const char** why);
+bool launch_fwd_mfma(const LayerDev& d, float* y, float* yc, const TailArgs& t, bool tail, hipStream_t st);
 int launch_fwd_tail(const LayerDev& d, const TailArgs& t, float* out, hipStream_t st, const char** why);
 int launch_weight_prep(int n, float* const* w, const int* cout, const int* fan_in, const int* sp,
                        float* const* s, hipStream_t st, const char** why);

@@ -5,6 +5,7 @@ state_dict layout (weight, bias, and the unused-but-saved bnorm.*), and its forw
 returns (nconv, cout) like step1.py:116-149. The arithmetic runs in hand-written gfx950 kernels
 through the C ABI (include/nconv.h); there is no PyTorch or CPU fallback for it.
 """
+import os
 from dataclasses import dataclass
 from typing import Optional, Tuple
 
@@ -16,6 +17,13 @@ from torch.nn.modules.conv import _ConvNd
 from torch.nn.modules.utils import _pair
 
 from . import _lib
+
+
+# Arithmetic of the forward sums N = W*(x*c), D = W*c (include/nconv.h enum nconv_math): "bf16x3"
+# (default: split-bf16 products on the matrix cores, <= ~1.1e-5 relative per product) or "fp32"
+# (exact fp32 products on the vector ALU). NCONV_FWD_MATH selects it; tests switch this global.
+_MATH_NAMES = {"bf16x3": _lib.MATH_BF16X3, "fp32": _lib.MATH_FP32}
+FORWARD_MATH = _MATH_NAMES[os.environ.get("NCONV_FWD_MATH", "bf16x3")]
 
 
 def _require_device(t: torch.Tensor, what: str):
@@ -70,6 +78,7 @@ class LayerSpec:
         L.a = _lib.src(xa, ca)
         L.b = _lib.src(xb, cb)
         L.weight, L.bias, L.wsum = weight.data_ptr(), bias.data_ptr(), wsum.data_ptr()
+        L.math = FORWARD_MATH
         return L
 
 

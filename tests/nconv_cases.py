@@ -48,6 +48,10 @@ LAYER_CASES = [
     ("nconv5_upcat_inexact", UPCAT_SKIP_FIRST, 16, 8, 3, 1, 1, 1, 1, (8, 25, 71), (8, 12, 35)),
     ("nconv6_upfirst_p0", UPCAT_UP_FIRST, 16, 8, 3, 0, 1, 1, 1, (8, 37, 70), (8, 18, 35)),
     ("nconv7_1x1_p2", PLAIN, 8, 1, 1, 2, 1, 1, 1, (8, 35, 68), None),
+    # widths a multiple of 4: the 16-byte store (and LDS-DMA staging) paths of the MFMA kernels
+    ("nconv2_w4", PLAIN, 8, 8, 5, 2, 1, 1, 1, (8, 21, 68), None),
+    ("nconv5_upcat_w4", UPCAT_SKIP_FIRST, 16, 8, 3, 1, 1, 1, 1, (8, 26, 72), (8, 13, 36)),
+    ("nconv6_upfirst_w4", UPCAT_UP_FIRST, 16, 8, 3, 0, 1, 1, 1, (8, 34, 72), (8, 17, 36)),
     ("generic_3x3_plain", PLAIN, 8, 8, 3, 1, 1, 1, 1, (8, 29, 41), None),
     ("generic_stride2", PLAIN, 4, 6, 3, 1, 2, 1, 1, (4, 29, 41), None),
     ("generic_dil2_groups2", PLAIN, 4, 6, 3, 2, 1, 2, 2, (4, 29, 41), None),

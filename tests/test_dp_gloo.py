@@ -39,8 +39,10 @@ def _worker(rank, world, port, q):
     loss = net.module.a(x[2 * rank:2 * rank + 2]).pow(2).mean()
     loss.backward()
     net.allreduce_grads()
-    q.put((rank, {k: v.detach().clone() for k, v in net.module.state_dict().items()},
-           net.module.a.weight.grad.clone(), net.module.unused.weight.grad))
+    # numpy arrays travel by value: torch tensors would be passed as shared-memory handles that
+    # vanish when this process exits before the parent has received them
+    q.put((rank, {k: v.detach().numpy().copy() for k, v in net.module.state_dict().items()},
+           net.module.a.weight.grad.numpy().copy(), net.module.unused.weight.grad))
     dist.destroy_process_group()
 
 
@@ -53,6 +55,7 @@ def test_allreduce_matches_mean_loss_gradient():
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda t: t[0])
+    res = [(r, {k: torch.from_numpy(v) for k, v in sd.items()}, torch.from_numpy(g), u) for r, sd, g, u in res]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0

@@ -48,8 +48,15 @@ def _wsum(nconv_amd, w):
     return s
 
 
+@pytest.fixture(params=["bf16x3", "fp32"])
+def fwd_math(request, nconv_amd, monkeypatch):
+    """Both forward arithmetics (include/nconv.h enum nconv_math)."""
+    monkeypatch.setattr(nconv_amd.nconv, "FORWARD_MATH", {"bf16x3": 0, "fp32": 1}[request.param])
+    return request.param
+
+
 @pytest.mark.parametrize("case", LAYER_CASES, ids=[c[0] for c in LAYER_CASES])
-def test_layer_forward(nconv_amd, gpu, case):
+def test_layer_forward(nconv_amd, gpu, case, fwd_math):
     xa, ca, xb, cb, w, b = _build(case, 1234)
     name, mode, *_ = case
     _, _, cin, cout, k, pad, stride, dil, groups, *_ = case
@@ -65,6 +72,7 @@ def test_layer_forward(nconv_amd, gpu, case):
         bound = 1e-4 * ref.abs() + 1e-5
         assert torch.isfinite(got).all()
         assert (err <= bound).all(), f"{name}: max err {err.max():.3e}, worst ratio {(err / bound).max():.3f}"
+        print(f"{name} [{fwd_math}]: max rel err {(err / (ref.abs() + 1e-30)).max():.2e}")
 
 
 @pytest.mark.parametrize("case", LAYER_CASES, ids=[c[0] for c in LAYER_CASES])
