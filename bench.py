@@ -27,6 +27,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md, chip-level parameters (spec)
+MFMA_BF16_PEAK_TFLOPS = 2500.0  # dense bf16 matrix peak (no sparsity), MI355X_MICROARCH.md
 FP32_PEAK_TFLOPS = 157.3   # same table: FP32 vector / matrix peak
 LAYERS = ("nconv1", "nconv2", "nconv_down1", "nconv_down2", "nconv_down3", "nconv4", "nconv5", "nconv6", "nconv7")
 
@@ -48,7 +49,8 @@ def parse():
                    help="also time the config-4 step on the PyTorch-ROCm modules (MIOpen), for comparison")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--graph", type=int, default=1, help="capture the forward in a hipGraph (1) or run eager (0)")
-    p.add_argument("--streams", type=int, default=2, help="HIP streams the inference batch is split over")
+    p.add_argument("--streams", type=int, default=1, help="HIP streams the inference batch is split over")
+    p.add_argument("--fused-head", type=int, default=1, help="nconv1 inside nconv2's kernel (nconv_fwd_head)")
     p.add_argument("--train-graph", type=int, default=-1,
                    help="replay the training step from a hipGraph (1) or eager (0); default: 1 on one GPU, 0 with "
                         "several (the RCCL all-reduce stays outside graph capture)")
@@ -140,6 +142,23 @@ def time_layers(m, net, S, reps=20):
             ev[-1][1].synchronize()
             out[name] = sum(e0.elapsed_time(e1) for e0, e1 in ev) / reps * 1e3  # us
     return out
+
+
+# Layers on the bf16x3 matrix-core kernel (fwd_mfma, include/nconv.h NCONV_MATH_BF16X3): output
+# rows per tile, k-steps (4 positions x 8 channels each) and the grid each launch writes.
+MFMA_LAYERS = {"nconv2": (8, 8, 1), "nconv_down1": (8, 8, 2), "nconv_down2": (8, 8, 4), "nconv_down3": (8, 8, 8),
+               "nconv4": (8, 6, 4), "nconv5": (8, 6, 2), "nconv6+7_tail": (8, 6, 1)}
+
+
+def mfma_issued_flops(layer, B, H, W):
+    """bf16 MFMA flops one fwd_mfma launch issues: per 8x32-pixel tile, 4 row pairs x 2 column
+    halves x NT k-steps x 6 v_mfma_f32_16x16x32_bf16 (3 split products x {N, D}) of 16384 flops."""
+    if layer not in MFMA_LAYERS:
+        return None
+    th, nt, div = MFMA_LAYERS[layer]
+    h, w = H // div, W // div
+    tiles = -(-h // th) * -(-w // 32) * B
+    return tiles * (th // 2) * 2 * nt * 6 * 16384
 
 
 def pmc_traffic(kernel, B, H, W):
@@ -330,6 +349,7 @@ def main():
         net(torch.zeros(1, 1, 32, 32, device=dev))  # one EnforcePos: positive (trained-like) weights
     net.eval()
     net.d_net.inference_streams = a.streams
+    net.d_net.fused_head = bool(a.fused_head)
     g = torch.Generator().manual_seed(1000 + rank)
     S = sparse_depth(g, B, H, W, dev)
 
@@ -448,12 +468,18 @@ def main():
         tfl = fl / (us * 1e-6) / 1e12
         tail_b, tail_f = fused_tail_cost(B, H, W)
         pass_bytes = 238.44e6 * B if (H, W) == (352, 1216) else None
+        on_mfma = m.nconv.FORWARD_MATH == m._lib.MATH_BF16X3 and dom in MFMA_LAYERS
+        issued = mfma_issued_flops(dom, B, H, W) if on_mfma else None
         roof = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": f"{dom} (fwd_tiled)", "kernel_us": round(us, 2),
+                "kernel": f"{dom} ({'fwd_mfma, bf16x3 matrix cores' if on_mfma else 'fwd_tiled, packed FP32'})",
+                "kernel_us": round(us, 2),
                 "algorithmic_bytes_per_launch": byt, "flops_per_launch": fl,
-                "fp32_tflops": round(tfl, 2), "fp32_peak_tflops": FP32_PEAK_TFLOPS,
-                "fp32_frac": round(tfl / FP32_PEAK_TFLOPS, 4),
+                "useful_tflops": round(tfl, 2),
+                "mfma_issued_tflops": round(issued / (us * 1e-6) / 1e12, 2) if issued else None,
+                "mfma_bf16_dense_peak_tflops": MFMA_BF16_PEAK_TFLOPS if issued else None,
+                "mfma_frac": round(issued / (us * 1e-6) / 1e12 / MFMA_BF16_PEAK_TFLOPS, 4) if issued else None,
+                "fp32_vector_peak_tflops": FP32_PEAK_TFLOPS,
                 "whole_pass_hbm_frac": round(pass_bytes * a.steps / t_fwd / 1e9 / HBM_PEAK_GBS, 4) if pass_bytes else None}
         cpu = None
         if not a.no_cpu_baseline and world == 1:
@@ -468,7 +494,8 @@ def main():
             "config": {"workload": "config2: SETP1_NCONV/DNET forward, fused HIP NConv kernels",
                        "global_batch": B * world, "per_gpu_batch": B, "height": H, "width": W,
                        "crop": "generalized [1:H+1,1:W+1]", "parallelism": f"frame-sharded x{world}",
-                       "hipgraph": bool(graph is not None), "streams": a.streams},
+                       "hipgraph": bool(graph is not None), "streams": a.streams,
+                       "fused_head": bool(a.fused_head)},
             "train_fwd_bwd_adamw": train,
             "guided_fwd": guided,
             "guided_train_fwd_bwd_adamw": guided_train,

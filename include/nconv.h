@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define NCONV_ABI_VERSION 8
+#define NCONV_ABI_VERSION 9
 
 /* How a layer's input (data x, confidence c) is produced from its source tensors. These are the
  * DNET glue ops fused into the layer's load stage (models/step1.py:53,61-90). */
@@ -95,6 +95,15 @@ int nconv_fwd(const nconv_layer* L, float* y, float* cout, void* stream);
  * (returns -EOPNOTSUPP otherwise). */
 int nconv_fwd_pooled(const nconv_layer* L, float* y, float* cout, float* y_pool, float* cout_pool,
                      void* stream);
+
+/* Inference-only fused head: nconv1 on the thresholded sparse depth (models/step1.py:53-57;
+ * L1: Cin 1, Cout 8, 5x5, padding 2, NCONV_LOAD_THRESH) is evaluated while staging nconv2's input
+ * tile (step1.py:58; L2: 8 -> 8, 5x5, padding 2, stride 1; its sources are not read), so nconv1's
+ * 8-channel output never reaches HBM. Writes nconv2's y, cout (B, 8, H, W) and their 2x2 max-pooled
+ * copies (B, 8, H/2, W/2) like nconv_fwd_pooled. Matrix-core math only (L2->math ==
+ * NCONV_MATH_BF16X3; nconv1 itself is exact fp32); -EOPNOTSUPP otherwise. */
+int nconv_fwd_head(const nconv_layer* L1, const nconv_layer* L2, float* y, float* cout, float* y_pool,
+                   float* cout_pool, void* stream);
 
 /* Inference-only fused tail: the last 3x3 NConv (nconv6, step1.py:88-90) with its 1x1 successor
  * (nconv7, step1.py:92) evaluated in the epilogue, written straight into the cropped output

@@ -13,7 +13,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # NCONV_LIB: an alternative build of the same library (kernel-tuning experiments)
 LIB_PATH = os.environ.get("NCONV_LIB") or os.path.join(_HERE, "libnconv.so")
-ABI_VERSION = 8
+ABI_VERSION = 9
 BWD_ACCUMULATE = 1
 
 # enum nconv_load_mode
@@ -30,6 +30,7 @@ EXPORTED = (
     "nconv_fwd",
     "nconv_fwd_pooled",
     "nconv_fwd_tail",
+    "nconv_fwd_head",
     "nconv_bwd_workspace_bytes",
     "nconv_bwd",
     "nconv_dense_packed_floats",
@@ -102,6 +103,8 @@ def _declare(lib):
     lib.nconv_fwd.argtypes = [ctypes.POINTER(NconvLayer), P, P, P]
     lib.nconv_fwd_pooled.restype = ctypes.c_int
     lib.nconv_fwd_pooled.argtypes = [ctypes.POINTER(NconvLayer), P, P, P, P, P]
+    lib.nconv_fwd_head.restype = ctypes.c_int
+    lib.nconv_fwd_head.argtypes = [ctypes.POINTER(NconvLayer), ctypes.POINTER(NconvLayer), P, P, P, P, P]
     lib.nconv_fwd_tail.restype = ctypes.c_int
     lib.nconv_fwd_tail.argtypes = [ctypes.POINTER(NconvLayer), P, P, P, ctypes.c_int, ctypes.c_int,
                                    ctypes.c_float, P, P, ctypes.c_int, ctypes.c_int, P]

@@ -134,6 +134,40 @@ int nconv_fwd_pooled(const nconv_layer* L, float* y, float* cout, float* y_pool,
     return rc ? fail(rc, "nconv_fwd_pooled", why) : 0;
 }
 
+int nconv_fwd_head(const nconv_layer* L1, const nconv_layer* L2, float* y, float* cout, float* y_pool,
+                   float* cout_pool, void* stream) {
+    const char* fn = "nconv_fwd_head";
+    if (const char* why = validate(L1, false)) return fail(-22, fn, why);
+    if (!L2) return fail(-22, fn, "null nconv2 descriptor");
+    if (!y || !cout || !y_pool || !cout_pool) return fail(-22, fn, "null output");
+    if (L1->load_mode != NCONV_LOAD_THRESH || L1->Cin != 1 || L1->Cout != 8 || L1->KH != 5 || L1->KW != 5 ||
+        L1->PH != 2 || L1->PW != 2 || L1->SH != 1 || L1->SW != 1 || L1->DH != 1 || L1->DW != 1 || L1->groups != 1)
+        return fail(-95, fn, "nconv1 must be 1 -> 8, 5x5, padding 2, stride 1, thresholded input");
+    if (L2->B != L1->B || L2->Cin != 8 || L2->Cout != 8 || L2->KH != 5 || L2->KW != 5 || L2->PH != 2 ||
+        L2->PW != 2 || L2->SH != 1 || L2->SW != 1 || L2->DH != 1 || L2->DW != 1 || L2->groups != 1)
+        return fail(-95, fn, "nconv2 must be 8 -> 8, 5x5, padding 2, stride 1");
+    if (L2->H != L1->Ho || L2->W != L1->Wo || L2->Ho != L2->H || L2->Wo != L2->W)
+        return fail(-22, fn, "nconv2 geometry inconsistent with nconv1's output");
+    if (L2->Ho < 2 || L2->Wo < 2) return fail(-22, fn, "output too small to pool");
+    if (!L2->weight || !L2->bias || !L2->wsum) return fail(-22, fn, "null nconv2 weight/bias/wsum");
+    if (L2->math != NCONV_MATH_BF16X3) return fail(-95, fn, "the fused head runs on the matrix cores only");
+    nconv_layer l2 = *L2;
+    l2.load_mode = NCONV_LOAD_PLAIN;
+    l2.a = L1->a;  // (the kernel reads the sparse depth through TailArgs)
+    nconv::TailArgs t{};
+    t.py = y_pool;
+    t.pc = cout_pool;
+    t.s_in = L1->a.x;
+    t.w1 = L1->weight;
+    t.b1 = L1->bias;
+    t.s1 = L1->wsum;
+    t.eps1 = L1->eps;
+    t.thresh1 = L1->thresh;
+    const char* why = nullptr;
+    int rc = nconv::launch_fwd_head(make_dev(&l2), t, y, cout, (hipStream_t)stream, &why);
+    return rc ? fail(rc, fn, why) : 0;
+}
+
 int nconv_fwd_tail(const nconv_layer* L6, const float* w7, const float* b7, const float* wsum7,
                    int cin7, int p7, float eps7, float* out, float* out_c, int out_h, int out_w,
                    void* stream) {

@@ -61,6 +61,10 @@ constexpr int kOutPitch = 36;  // floats per row of a wave's output-transpose re
 __device__ __forceinline__ void st_f32(__amdgpu_buffer_rsrc_t r, unsigned off, float v) {
     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, (int)off, 0, 0);
 }
+__device__ __forceinline__ void st_f2(__amdgpu_buffer_rsrc_t r, unsigned off, f2 v) {
+    typedef unsigned u2 __attribute__((ext_vector_type(2)));
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v), r, (int)off, 0, 0);
+}
 __device__ __forceinline__ void st_f4(__amdgpu_buffer_rsrc_t r, unsigned off, f4 v) {
     typedef unsigned u4 __attribute__((ext_vector_type(4)));
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, v), r, (int)off, 0, 0);
@@ -137,11 +141,13 @@ struct MfStage {
     }
 
     static constexpr int BYTES = 0;  // no LDS of its own
-    __device__ __forceinline__ void issue(const LayerDev& d, int b, int ih0, int iw0, unsigned char*, int tid) {
+    static constexpr bool SELF_SYNC = false;
+    __device__ __forceinline__ void issue(const LayerDev& d, const TailArgs&, int b, int ih0, int iw0, unsigned char*,
+                                          int tid) {
         load(d, b, ih0, iw0, tid);
     }
-    __device__ __forceinline__ void to_planes(const LayerDev&, int, int, unsigned char* lds, const unsigned char*,
-                                              int tid) const {
+    __device__ __forceinline__ void to_planes(const LayerDev&, const TailArgs&, int, int, unsigned char* lds,
+                                              unsigned char*, int tid) const {
         store(lds, tid);
     }
 
@@ -194,8 +200,9 @@ struct DmaStage {
     static constexpr int BYTES = NP * 1024;
     static_assert(4 * NVA >= C::IW + 3 && 4 * NVB >= (C::IW + 1) / 2 + 4, "staged columns cover the halo");
 
-    __device__ __forceinline__ void issue(const LayerDev& d, int b, int ih0, int iw0, unsigned char* stage,
-                                          int tid) const {
+    static constexpr bool SELF_SYNC = true;
+    __device__ __forceinline__ void issue(const LayerDev& d, const TailArgs&, int b, int ih0, int iw0,
+                                          unsigned char* stage, int tid) const {
         const nconv_layer& L = d.L;
         const int wave = tid >> 6, lane = tid & 63;
 #pragma unroll 1
@@ -219,8 +226,8 @@ struct DmaStage {
     }
 
     // Wait for this wave's pieces, then (all pieces landed) form the bf16 planes.
-    __device__ __forceinline__ void to_planes(const LayerDev& d, int ih0, int iw0, unsigned char* lds,
-                                              const unsigned char* stage, int tid) const {
+    __device__ __forceinline__ void to_planes(const LayerDev& d, const TailArgs&, int ih0, int iw0, unsigned char* lds,
+                                              unsigned char* stage, int tid) const {
         __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) expcnt(0) lgkmcnt(0)
         __syncthreads();
         const float* S = reinterpret_cast<const float*>(stage);
@@ -272,27 +279,131 @@ struct DmaStage {
     }
 };
 
+// Fused head (nconv_fwd_head): nconv2's input (x1, c1) = nconv1(S, S > thresh) is computed here,
+// per tile, from the (TH+8) x 40 sparse-depth halo, so it never exists in HBM. nconv1 runs on the
+// vector ALU in exact fp32 (packed {N, D} FMAs, the same tap order as fwd_tiled's nconv1, so the
+// values equal the unfused layer's), then feeds the split-bf16 planes like a loaded input.
+constexpr int kModeHead = 100;
+
+template <int TH>
+struct HeadStage {
+    using C = MfCfg<8, 5, TH>;
+    static constexpr int SH = C::IH + 4, SW = C::IW + 4;  // nconv1's own 5x5 halo around the tile
+    static constexpr int NS = SH * SW, NES = (NS + kMfThreads - 1) / kMfThreads;
+    static constexpr int BYTES = NS * 8;                  // {S * c0, c0} pairs
+    static constexpr bool SELF_SYNC = true;
+    float sv[NES];
+
+    __device__ __forceinline__ void issue(const LayerDev& d, const TailArgs& t, int b, int ih0, int iw0,
+                                          unsigned char*, int tid) {
+        const int H = d.L.H, W = d.L.W;
+        const __amdgpu_buffer_rsrc_t rs = plane_rsrc(t.s_in + (size_t)b * H * W, H * W * 4);
+#pragma unroll
+        for (int k = 0; k < NES; ++k) {
+            const int e = tid + kMfThreads * k;
+            const int r = e / SW, col = e - r * SW;
+            const int ih = ih0 - 2 + r, iw = iw0 - 2 + col;
+            const bool in = e < NS && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+            sv[k] = ld_f32(rs, in ? (unsigned)(ih * W + iw) * 4u : kOOB);
+        }
+    }
+
+    __device__ __forceinline__ void to_planes(const LayerDev& d, const TailArgs& t, int ih0, int iw0,
+                                              unsigned char* lds, unsigned char* stage, int tid) const {
+        f2* T = reinterpret_cast<f2*>(stage);
+#pragma unroll
+        for (int k = 0; k < NES; ++k) {
+            const int e = tid + kMfThreads * k;
+            const float c0 = sv[k] > t.thresh1 ? 1.0f : 0.0f;  // step1.py:53
+            if (NES * kMfThreads == NS || e < NS) T[e] = (f2){sv[k] * c0, c0};
+        }
+        __syncthreads();  // (also: every wave is done with the previous tile's planes)
+        // nconv1: wave w computes output channels 4 (w & 1) .. +3 (their 20 weights per kernel row
+        // are wave-uniform: scalar loads, one per 4 pixels) for quads of 4 adjacent positions,
+        // half of the 108 quads of the (IH x 36) tile per wave pair.
+        static_assert(C::IW == 36, "9 quads of 4 positions per staged row");
+        const int H = d.L.H, W = d.L.W;
+        const int wave = tid >> 6, lane = tid & 63, half = wave & 1;
+        constexpr int NQ = C::IH * 9, PERW = (NQ + 1) / 2;
+        const int tq = (wave >> 1) * PERW + lane;
+        if (lane < PERW && tq < NQ) {
+            const int r = tq / 9, c0 = 4 * (tq - 9 * (tq / 9));
+            const float* __restrict__ w1 = t.w1 + half * 4 * 25;
+            f2 acc[4][4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int o = 0; o < 4; ++o) acc[j][o] = (f2){0.f, 0.f};
+#pragma unroll 1
+            for (int kh = 0; kh < 5; ++kh) {
+                const f2* row = T + (r + kh) * SW + c0;
+                f2 v[8];
+#pragma unroll
+                for (int m = 0; m < 8; ++m) v[m] = row[m];
+#pragma unroll
+                for (int kw = 0; kw < 5; ++kw)
+#pragma unroll
+                    for (int o = 0; o < 4; ++o) {
+                        const float w = w1[o * 25 + kh * 5 + kw];
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) acc[j][o] = __builtin_elementwise_fma((f2){w, w}, v[j + kw], acc[j][o]);
+                    }
+            }
+            typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const bool in = (unsigned)(ih0 + r) < (unsigned)H && (unsigned)(iw0 + c0 + j) < (unsigned)W;
+                bf16x4 ph, pl, qh, ql;
+#pragma unroll
+                for (int o = 0; o < 4; ++o) {
+                    float xv, cv;
+                    nconv_epilogue(acc[j][o].x, acc[j][o].y, t.eps1, t.b1[half * 4 + o], t.s1[half * 4 + o], xv, cv);
+                    const float q = in ? cv : 0.f;  // nconv2's zero padding outside the image
+                    const float p = in ? xv * cv : 0.f;
+                    const __bf16 p1 = (__bf16)p, q1 = (__bf16)q;
+                    ph[o] = p1;
+                    pl[o] = (__bf16)(p - (float)p1);
+                    qh[o] = q1;
+                    ql[o] = (__bf16)(q - (float)q1);
+                }
+                unsigned char* base = lds + (r * C::IW + c0 + j) * 16 + half * 8;
+                *reinterpret_cast<bf16x4*>(base) = ph;
+                *reinterpret_cast<bf16x4*>(base + C::PSTRIDE) = pl;
+                *reinterpret_cast<bf16x4*>(base + 2 * C::PSTRIDE) = qh;
+                *reinterpret_cast<bf16x4*>(base + 3 * C::PSTRIDE) = ql;
+            }
+        }
+    }
+};
+
 // Persistent: gridDim.x (a multiple of 8) workgroups walk the tiles; the next tile's halo loads
 // are in flight while the current one's MFMAs and epilogue run.
+#ifndef NCONV_MF_TH5
+#define NCONV_MF_TH5 8  // output rows per tile of the 5x5 layers
+#endif
 #ifndef NCONV_MFMA_WAVES
 #define NCONV_MFMA_WAVES 3  // waves per SIMD: 168 VGPRs (3 workgroups per CU) without spilling
 #endif
 // POOL2 staging holds four values per element before pooling: 2 waves per SIMD (no spills)
 template <int MODE, bool DMA>
 constexpr int mf_waves() { return DMA || MODE == NCONV_LOAD_POOL2 ? 2 : NCONV_MFMA_WAVES; }
+template <int CIN, int K, int MODE, int TH, bool DMA>
+using StageOf = typename std::conditional<
+    MODE == kModeHead, HeadStage<TH>,
+    typename std::conditional<DMA, DmaStage<CIN, K, MODE, TH>, MfStage<CIN, K, MODE, TH>>::type>::type;
 template <int CIN, int K, int MODE, int EPI, int TH>
 constexpr int mf_lds_bytes(bool dma) {
     return MfCfg<CIN, K, TH>::LDS_IN + (EPI == kEpiTail ? 0 : 4 * 2 * 16 * kOutPitch * 4) +
-           (dma ? DmaStage<CIN, K, MODE, TH>::BYTES : 0);
+           (MODE == kModeHead ? HeadStage<TH>::BYTES : dma ? DmaStage<CIN, K, MODE, TH>::BYTES : 0);
 }
 template <int CIN, int K, int MODE, int EPI, int TH, bool VEC, bool DMA>
 __global__ __launch_bounds__(kMfThreads) __attribute__((amdgpu_waves_per_eu(mf_waves<MODE, DMA>(), mf_waves<MODE, DMA>()))) void fwd_mfma(LayerDev d, float* __restrict__ y, float* __restrict__ yc,
                                                        TailArgs t) {
     using C = MfCfg<CIN, K, TH>;
-    using Stage = typename std::conditional<DMA, DmaStage<CIN, K, MODE, TH>, MfStage<CIN, K, MODE, TH>>::type;
+    using Stage = StageOf<CIN, K, MODE, TH, DMA>;
     // input planes, (non-tail) four waves' output-transpose regions (y and cout), DMA staging
     __shared__ __attribute__((aligned(16))) unsigned char lds[mf_lds_bytes<CIN, K, MODE, EPI, TH>(DMA)];
-    unsigned char* const stage = lds + mf_lds_bytes<CIN, K, MODE, EPI, TH>(false);
+    unsigned char* const stage = lds + MfCfg<CIN, K, TH>::LDS_IN + (EPI == kEpiTail ? 0 : 4 * 2 * 16 * kOutPitch * 4);
     const nconv_layer& L = d.L;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const bool tail = EPI == kEpiTail;
@@ -305,7 +416,7 @@ __global__ __launch_bounds__(kMfThreads) __attribute__((amdgpu_waves_per_eu(mf_w
     int v = blockIdx.x;
     {  // loads are unconditional (a block without tiles loads the last one and never uses it)
         const TileCoord tc = xcd_tile(ntx, nty, L.B, v < ntiles ? v : ntiles - 1);
-        st.issue(d, tc.b, tc.ty * TH + off - L.PH, tc.tx * C::TW + off - L.PW, stage, tid);
+        st.issue(d, t, tc.b, tc.ty * TH + off - L.PH, tc.tx * C::TW + off - L.PW, stage, tid);
     }
 
     // ---- B fragments (weights, once per workgroup) and per-lane A offsets ----
@@ -341,12 +452,12 @@ __global__ __launch_bounds__(kMfThreads) __attribute__((amdgpu_waves_per_eu(mf_w
         const int b = tc.b;
         const int R0 = tc.ty * TH, C0 = tc.tx * C::TW;  // tile origin in the written grid
         const int oh0 = R0 + off, ow0 = C0 + off;         // ... in this layer's output grid
-        st.to_planes(d, oh0 - L.PH, ow0 - L.PW, lds, stage, tid);
+        st.to_planes(d, t, oh0 - L.PH, ow0 - L.PW, lds, stage, tid);
         __syncthreads();
         {  // next tile's loads fly during this tile's MFMAs (the last tile re-loads itself)
             const int vn = v + (int)gridDim.x < ntiles ? v + (int)gridDim.x : v;
             const TileCoord tn = xcd_tile(ntx, nty, L.B, vn);
-            st.issue(d, tn.b, tn.ty * TH + off - L.PH, tn.tx * C::TW + off - L.PW, stage, tid);
+            st.issue(d, t, tn.b, tn.ty * TH + off - L.PH, tn.tx * C::TW + off - L.PW, stage, tid);
         }
 
         // ---- MFMAs: wave w takes the row pairs rp = w, w+4, ..., both 16-column halves ct ----
@@ -442,11 +553,24 @@ __global__ __launch_bounds__(kMfThreads) __attribute__((amdgpu_waves_per_eu(mf_w
                     const unsigned pbytes = (unsigned)(8 * Hp * Wp) * 4u;
                     const __amdgpu_buffer_rsrc_t rpy = plane_rsrc(t.py + (size_t)b * 8 * Hp * Wp, pbytes);
                     const __amdgpu_buffer_rsrc_t rpc = plane_rsrc(t.pc + (size_t)b * 8 * Hp * Wp, pbytes);
+                    float pyv[2], pcv[2];
 #pragma unroll
                     for (int hh = 0; hh < 2; ++hh) {
-                        const unsigned po = pr < Hp && pc0 + hh < Wp ? (unsigned)((o8 * Hp + pr) * Wp + pc0 + hh) * 4u : kOOB;
-                        st_f32(rpy, po, pool4v(ry[0][2 * hh], ry[0][2 * hh + 1], ry[1][2 * hh], ry[1][2 * hh + 1]));
-                        st_f32(rpc, po, pool4v(rcv[0][2 * hh], rcv[0][2 * hh + 1], rcv[1][2 * hh], rcv[1][2 * hh + 1]));
+                        pyv[hh] = pool4v(ry[0][2 * hh], ry[0][2 * hh + 1], ry[1][2 * hh], ry[1][2 * hh + 1]);
+                        pcv[hh] = pool4v(rcv[0][2 * hh], rcv[0][2 * hh + 1], rcv[1][2 * hh], rcv[1][2 * hh + 1]);
+                    }
+                    const unsigned prow = (unsigned)((o8 * Hp + pr) * Wp) * 4u;
+                    if constexpr (VEC) {  // Wp even, pc0 even: one 8-byte store of both pooled columns
+                        const unsigned po = pr < Hp && pc0 < Wp ? prow + (unsigned)pc0 * 4u : kOOB;
+                        st_f2(rpy, po, (f2){pyv[0], pyv[1]});
+                        st_f2(rpc, po, (f2){pcv[0], pcv[1]});
+                    } else {
+#pragma unroll
+                        for (int hh = 0; hh < 2; ++hh) {
+                            const unsigned po = pr < Hp && pc0 + hh < Wp ? prow + (unsigned)(pc0 + hh) * 4u : kOOB;
+                            st_f32(rpy, po, pyv[hh]);
+                            st_f32(rpc, po, pcv[hh]);
+                        }
                     }
                 }
             } else {
@@ -498,7 +622,7 @@ __global__ __launch_bounds__(kMfThreads) __attribute__((amdgpu_waves_per_eu(mf_w
         }
         // every wave is done reading the planes before the next tile's are formed (DmaStage's own
         // barrier, after its wait, does this there; a __syncthreads here would drain the DMA)
-        if constexpr (!DMA) __syncthreads();
+        if constexpr (!Stage::SELF_SYNC) __syncthreads();
     }
 }
 
@@ -564,6 +688,16 @@ void go_mfma_any(const LayerDev& d, float* y, float* yc, const TailArgs& t, int 
 
 }  // namespace
 
+int launch_fwd_head(const LayerDev& d2, const TailArgs& t, float* y, float* yc, hipStream_t st, const char** why) {
+    go_mfma<8, 5, kModeHead, kEpiPool, NCONV_MF_TH5, false>(d2, y, yc, t, d2.L.Ho, d2.L.Wo, st);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        *why = hipGetErrorString(e);
+        return -5;
+    }
+    return 0;
+}
+
 // Returns true (and launches) when the layer has a matrix-core kernel: 8 output channels,
 // 8 input channels with a 5x5 kernel or 16 with a 3x3, stride 1, no dilation / groups.
 bool launch_fwd_mfma(const LayerDev& d, float* y, float* yc, const TailArgs& t, bool tail, hipStream_t st) {
@@ -575,9 +709,9 @@ bool launch_fwd_mfma(const LayerDev& d, float* y, float* yc, const TailArgs& t, 
     const int gh = tail ? t.out_h : L.Ho, gw = tail ? t.out_w : L.Wo;
     if (L.Cin == 8 && L.KH == 5 && L.load_mode == NCONV_LOAD_PLAIN && !tail) {
         if (pool)
-            go_mfma_any<8, 5, NCONV_LOAD_PLAIN, kEpiPool, 8>(d, y, yc, t, gh, gw, st);
+            go_mfma_any<8, 5, NCONV_LOAD_PLAIN, kEpiPool, NCONV_MF_TH5>(d, y, yc, t, gh, gw, st);
         else
-            go_mfma_any<8, 5, NCONV_LOAD_PLAIN, kEpiPlain, 8>(d, y, yc, t, gh, gw, st);
+            go_mfma_any<8, 5, NCONV_LOAD_PLAIN, kEpiPlain, NCONV_MF_TH5>(d, y, yc, t, gh, gw, st);
         return true;
     }
     if (L.Cin == 8 && L.KH == 5 && L.load_mode == NCONV_LOAD_POOL2 && !tail && !pool) {

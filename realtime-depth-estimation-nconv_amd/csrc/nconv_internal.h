@@ -15,6 +15,12 @@ struct TailArgs {
     float* out_c;
     float* py;  // optional 2x2 max-pooled copies of y / cout (non-tail launches), (B,Cout,Ho/2,Wo/2)
     float* pc;
+    // fused head (nconv_fwd_head): nconv1 evaluated while staging nconv2's input
+    const float* s_in;  // sparse depth (B, 1, H, W)
+    const float* w1;    // nconv1 weight (8, 1, 5, 5), bias, s[o]
+    const float* b1;
+    const float* s1;
+    float eps1, thresh1;
 };
 
 struct BwdArgs {
@@ -36,6 +42,7 @@ struct BwdArgs {
 // Forward. Return 0, or a negative errno with *why set.
 int launch_fwd(const LayerDev& d, float* y, float* yc, float* py, float* pc, hipStream_t st, const char** why);
 bool launch_fwd_mfma(const LayerDev& d, float* y, float* yc, const TailArgs& t, bool tail, hipStream_t st);
+int launch_fwd_head(const LayerDev& d2, const TailArgs& t, float* y, float* yc, hipStream_t st, const char** why);
 int launch_fwd_tail(const LayerDev& d, const TailArgs& t, float* out, hipStream_t st, const char** why);
 int launch_weight_prep(int n, float* const* w, const int* cout, const int* fan_in, const int* sp,
                        float* const* s, hipStream_t st, const char** why);

@@ -19,9 +19,9 @@ no weights, so the results are identical).
 import torch
 import torch.nn as nn
 
-from . import _lib
-from .nconv import (EnforcePos, NConv2d, _require_device, layer_forward_pooled, layer_forward_raw, nconv_layer,
-                    weight_prep)
+from . import _lib, nconv
+from .nconv import (EnforcePos, NConv2d, _require_device, layer_forward_head, layer_forward_pooled,
+                    layer_forward_raw, nconv_layer, weight_prep)
 
 LAYERS = ("nconv1", "nconv2", "nconv_down1", "nconv_down2", "nconv_down3", "nconv4", "nconv5",
           "nconv6", "nconv7")
@@ -120,11 +120,11 @@ class DNET(nn.Module):
         return xo[:, :, 1:1 + out_h, 1:1 + out_w]
 
     # -- inference ------------------------------------------------------------------------------
-    # Frames are independent, so the batch is split over `inference_streams` HIP streams, each
-    # running the whole layer chain on its share: the streams' kernels overlap, so the partial
-    # last round of one layer's workgroups and the drain/fill gap between dependent launches are
-    # filled with the other stream's work (the chain itself is strictly sequential).
-    inference_streams = 2
+    # Frames are independent, so the batch can be split over `inference_streams` HIP streams, each
+    # running the whole layer chain on its share, so that one stream's kernels fill the partial
+    # last round of the other's. The matrix-core layers run persistent grids sized to the chip,
+    # which leave no such gaps: one stream measures faster (B=8 352x1216: 0.507 vs 0.555 ms).
+    inference_streams = 1
 
     def _side_streams(self, device, n):
         key = (device.index, n)
@@ -156,8 +156,13 @@ class DNET(nn.Module):
         (l1, l2, d1, d2, d3, l4, l5, l6, l7) = layers
         (s1, s2, sd1, sd2, sd3, s4, s5, s6, s7) = wsum
         f, fp = layer_forward_raw, layer_forward_pooled
-        x1, c1 = f(l1.spec(_lib.THRESH, 0.01), S, None, None, None, l1.weight, l1.bias, s1)
-        x1, c1, p1, q1 = fp(l2.spec(), x1, c1, None, None, l2.weight, l2.bias, s2)
+        if self.fused_head and nconv.FORWARD_MATH == _lib.MATH_BF16X3 and self._head_shapes(l1, l2):
+            # nconv1 inside nconv2's staging: its 8-channel output never reaches HBM
+            x1, c1, p1, q1 = layer_forward_head(l1.spec(_lib.THRESH, 0.01), l2.spec(), S, l1.weight, l1.bias, s1,
+                                                l2.weight, l2.bias, s2)
+        else:
+            x1, c1 = f(l1.spec(_lib.THRESH, 0.01), S, None, None, None, l1.weight, l1.bias, s1)
+            x1, c1, p1, q1 = fp(l2.spec(), x1, c1, None, None, l2.weight, l2.bias, s2)
         x2, c2, p2, q2 = fp(d1.spec(), p1, q1, None, None, d1.weight, d1.bias, sd1)
         x3, c3, p3, q3 = fp(d2.spec(), p2, q2, None, None, d2.weight, d2.bias, sd2)
         x4, c4 = f(d3.spec(), p3, q3, None, None, d3.weight, d3.bias, sd3)
@@ -166,6 +171,18 @@ class DNET(nn.Module):
         x34, c34 = f(l4.spec(_lib.UPCAT_SKIP_FIRST), x3, c3, x4, c4, l4.weight, l4.bias, s4)
         x23, c23 = f(l5.spec(_lib.UPCAT_SKIP_FIRST), x2, c2, x34, c34, l5.weight, l5.bias, s5)
         self._fused_tail(l6, l7, s6, s7, x1, c1, x23, c23, out)
+
+    # Inference evaluates nconv1 inside nconv2's kernel (nconv_fwd_head) when the layers have
+    # DNET's geometry; set False to run them as two launches.
+    fused_head = True
+
+    @staticmethod
+    def _head_shapes(l1, l2):
+        return (l1.in_channels, l1.out_channels, tuple(l1.kernel_size), tuple(l1.padding), tuple(l1.stride)) == \
+            (1, 8, (5, 5), (2, 2), (1, 1)) and \
+            (l2.in_channels, l2.out_channels, tuple(l2.kernel_size), tuple(l2.padding), tuple(l2.stride)) == \
+            (8, 8, (5, 5), (2, 2), (1, 1)) and tuple(l1.dilation) == (1, 1) and tuple(l2.dilation) == (1, 1) \
+            and l1.groups == 1 and l2.groups == 1
 
     def _fused_tail(self, l6, l7, s6, s7, x1, c1, x23, c23, out):
         out_h, out_w = out.shape[2], out.shape[3]

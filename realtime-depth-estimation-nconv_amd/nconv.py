@@ -122,6 +122,22 @@ def layer_forward_pooled(spec: LayerSpec, xa, ca, xb, cb, weight, bias, wsum):
     return y, co, py, pc
 
 
+def layer_forward_head(spec1: LayerSpec, spec2: LayerSpec, S, w1, b1, s1, w2, b2, s2):
+    """nconv_fwd_head: nconv2(nconv1(S)) with nconv1 evaluated inside nconv2's staging (its output
+    never reaches HBM); returns nconv2's (y, cout, maxpool2x2(y), maxpool2x2(cout)). No autograd."""
+    L1 = spec1.descriptor(S, None, None, None, w1, b1, s1)
+    L2 = spec2.descriptor(S, S, None, None, w2, b2, s2)  # geometry only: the kernel reads S via L1
+    B, H, W = S.shape[0], L1.Ho, L1.Wo
+    y = torch.empty((B, 8, H, W), device=S.device, dtype=torch.float32)
+    co = torch.empty_like(y)
+    py = torch.empty((B, 8, H // 2, W // 2), device=S.device, dtype=torch.float32)
+    pc = torch.empty_like(py)
+    rc = _lib.lib().nconv_fwd_head(_lib.ctypes.byref(L1), _lib.ctypes.byref(L2), _lib.ptr(y), _lib.ptr(co),
+                                   _lib.ptr(py), _lib.ptr(pc), _lib.stream_handle(S.device))
+    _lib.check(rc, "nconv_fwd_head")
+    return y, co, py, pc
+
+
 class NConvLayerFn(torch.autograd.Function):
     """Autograd node of one fused NConv layer (glue + NConv2d.forward), kernels in libnconv."""
 

@@ -183,3 +183,31 @@ def test_fwd_pooled_outputs(nconv_amd, gpu, shape):
     assert torch.equal(y0, y1) and torch.equal(c0, c1)
     assert torch.equal(py, torch.nn.functional.max_pool2d(y1, 2, 2))
     assert torch.equal(pc, torch.nn.functional.max_pool2d(c1, 2, 2))
+
+
+@pytest.mark.parametrize("shape", [(2, 48, 128), (1, 37, 70), (1, 352, 1216)])
+def test_fwd_head_matches_unfused(nconv_amd, gpu, shape):
+    """nconv_fwd_head (nconv1 evaluated inside nconv2's staging) against nconv1 and nconv2 as two
+    launches: nconv1 is the same exact-fp32 arithmetic (its sums may round differently by an ulp),
+    so nconv2's outputs and pooled copies agree to 1e-5 relative; the pooled copies must be torch's
+    max_pool2d of the fused outputs exactly."""
+    B, H, W = shape
+    g = torch.Generator().manual_seed(H * W)
+    S = (torch.rand(B, 1, H, W, generator=g) * 79 + 1) * (torch.rand(B, 1, H, W, generator=g) < 0.05)
+    w1 = _gpu(rand_weight(g, 8, 1, 5, 5), gpu)
+    w2 = _gpu(rand_weight(g, 8, 8, 5, 5), gpu)
+    b1 = _gpu(torch.rand(8, generator=g) * 0.1, gpu)
+    b2 = _gpu(torch.rand(8, generator=g) * 0.1, gpu)
+    s1, s2 = _wsum(nconv_amd, w1), _wsum(nconv_amd, w2)
+    sp1 = nconv_amd.LayerSpec(1, 8, (5, 5), (1, 1), (2, 2), mode=THRESH)
+    sp2 = nconv_amd.LayerSpec(8, 8, (5, 5), (1, 1), (2, 2))
+    Sg = S.to(gpu)
+    N = nconv_amd.nconv
+    x1, c1 = N.layer_forward_raw(sp1, Sg, None, None, None, w1, b1, s1)
+    y0, c0, py0, pc0 = N.layer_forward_pooled(sp2, x1, c1, None, None, w2, b2, s2)
+    y1, c1f, py1, pc1 = N.layer_forward_head(sp1, sp2, Sg, w1, b1, s1, w2, b2, s2)
+    torch.cuda.synchronize()
+    for got, ref in ((y1, y0), (c1f, c0), (py1, py0), (pc1, pc0)):
+        torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-6)
+    assert torch.equal(py1, torch.nn.functional.max_pool2d(y1, 2, 2))
+    assert torch.equal(pc1, torch.nn.functional.max_pool2d(c1f, 2, 2))

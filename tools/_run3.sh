@@ -1,5 +1,6 @@
 set -e
-timeout -k 10 200 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_layers.py tests/test_gpu_dnet.py > gpurun_out/pytest_mfma.log 2>&1 || { tail -30 gpurun_out/pytest_mfma.log; exit 1; }
-tail -1 gpurun_out/pytest_mfma.log
-NCONV_MFMA_DMA=1 timeout -k 10 200 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_layers.py tests/test_gpu_dnet.py > gpurun_out/pytest_mfma_dma.log 2>&1 || { tail -30 gpurun_out/pytest_mfma_dma.log; exit 1; }
-tail -1 gpurun_out/pytest_mfma_dma.log
+B="python -u bench.py --no-guided --no-guided-train --no-cpu-baseline --no-train"
+for fh in 1 0; do for st in 1 2; do
+  timeout -k 10 120 $B --fused-head $fh --streams $st > gpurun_out/b.json 2> gpurun_out/b.err
+  python -c "import json; d=json.load(open('gpurun_out/b.json')); print('head', $fh, 'streams', $st, d['value'], d['ms_per_step'])"
+done; done

@@ -29,6 +29,13 @@ def main():
         x, c = r(B, 8, H, W) * 10, r(B, 8, H, W)
         spec = m.LayerSpec(8, 8, (5, 5), (1, 1), (2, 2))
         fn = lambda: N.layer_forward_pooled(spec, x, c, None, None, w8, b, s8)
+    elif which == "head":  # nconv1 inside nconv2 (nconv_fwd_head)
+        S = (r(B, 1, H, W) * 79 + 1) * (r(B, 1, H, W) < 0.05)
+        w1 = r(8, 1, 5, 5) + 0.05
+        s1 = w1.sum((1, 2, 3)).contiguous()
+        sp1 = m.LayerSpec(1, 8, (5, 5), (1, 1), (2, 2), mode=m._lib.THRESH)
+        spec = m.LayerSpec(8, 8, (5, 5), (1, 1), (2, 2))
+        fn = lambda: N.layer_forward_head(sp1, spec, S, w1, b, s1, w8, b, s8)
     elif which == "down1":
         x, c = r(B, 8, H // 2, W // 2) * 10, r(B, 8, H // 2, W // 2)
         spec = m.LayerSpec(8, 8, (5, 5), (1, 1), (2, 2))

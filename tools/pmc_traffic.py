@@ -47,41 +47,31 @@ def run():
     torch.cuda.synchronize()
 
 
-def _layer_of(name, grid, grids_by_name):
-    """Map a dispatch to a DNET layer: by template signature, and by grid size where one kernel
-    serves several layers (largest grid = highest resolution)."""
-    sig = name.split("(")[0]
-    order = sorted(grids_by_name[sig], reverse=True)  # the warm-up call's small grids sort last
-    pick = lambda names: names[order.index(grid)] if order.index(grid) < len(names) else None
-    # template arguments <CIN, COUT, K, MODE, TAIL, P>
-    if grid != order[0] and ("fwd_tiled<1, 8, 5, 1," in sig or ", true," in sig):
-        return None
-    if "fwd_tiled<1, 8, 5, 1, false," in sig:
-        return "nconv1"
-    if "fwd_tiled<8, 8, 5, 0, false," in sig:  # nconv2 and the down layers (pooled-copy inputs)
-        return pick(["nconv2", "nconv_down1", "nconv_down2", "nconv_down3"])
-    if "fwd_tiled<8, 8, 5, 2, false," in sig:  # down layers pooling on load (training path)
-        return pick(["nconv_down1", "nconv_down2", "nconv_down3"])
-    if "fwd_tiled<16, 8, 3, 3, false," in sig:
-        return pick(["nconv5", "nconv4"])
-    if "fwd_tiled<16, 8, 3, 4, true," in sig:
-        return "nconv6+7_tail"
-    return None
+ORDER = ["nconv1", "nconv2", "nconv_down1", "nconv_down2", "nconv_down3", "nconv4", "nconv5", "nconv6+7_tail"]
 
 
 def _read(dirpath, counter):
+    """Per layer mean of `counter` over the timed inference forwards. Dispatches are taken in
+    order: an inference forward is weight_prep followed by exactly the 8 layer launches of ORDER
+    (the warm-up training forward has 9 and is skipped)."""
     files = glob.glob(os.path.join(dirpath, "**", "*counter_collection.csv"), recursive=True)
     if not files:
         raise SystemExit(f"no counter_collection.csv under {dirpath}")
     rows = [r for f in files for r in csv.DictReader(open(f)) if r["Counter_Name"] == counter]
-    grids = defaultdict(set)
+    rows.sort(key=lambda r: int(r["Dispatch_Id"]))
+    groups, cur = [], None
     for r in rows:
-        grids[r["Kernel_Name"].split("(")[0]].add(int(r["Grid_Size"]))
+        if "weight_prep" in r["Kernel_Name"]:
+            cur = []
+            groups.append(cur)
+        elif cur is not None and ("nconv::" in r["Kernel_Name"]):
+            cur.append(r)
     per = defaultdict(list)
-    for r in rows:
-        lay = _layer_of(r["Kernel_Name"], int(r["Grid_Size"]), grids)
-        if lay:
-            per[lay].append(float(r["Counter_Value"]))
+    for g in groups:
+        if len(g) != len(ORDER):
+            continue
+        for name, r in zip(ORDER, g):
+            per[name].append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in per.items()}, {k: len(v) for k, v in per.items()}
 
 
