@@ -89,6 +89,14 @@ def layer_costs(B, H, W):
     return c
 
 
+def head_cost(B, H, W):
+    """nconv1+nconv2 fused launch (inference): reads the sparse depth, writes nconv2's y and cout
+    and their 2x2 max-pooled copies; flops of both layers."""
+    byt = (B * H * W * 1 + B * H * W * 16 + B * (H // 2) * (W // 2) * 16) * 4
+    fl = B * H * W * ((2 * 2 * 1 * 25 * 8 + 32) + (2 * 2 * 8 * 25 * 8 + 32))
+    return byt, fl
+
+
 def fused_tail_cost(B, H, W):
     """nconv6+nconv7 fused launch (inference): reads nconv6's inputs, writes the final output."""
     H2, W2 = H // 2, W // 2
@@ -119,9 +127,13 @@ def time_layers(m, net, S, reps=20):
         x34, c34 = fwd(l4.spec(lib.UPCAT_SKIP_FIRST), x3, c3, x4, c4, l4.weight, l4.bias, s4)
         x23, c23 = fwd(l5.spec(lib.UPCAT_SKIP_FIRST), x2, c2, x34, c34, l5.weight, l5.bias, s5)
     tail_out = torch.empty((S.shape[0], 1, oh, ow), device=S.device, dtype=torch.float32)
-    calls = {
+    head = d.fused_head and m.nconv.FORWARD_MATH == lib.MATH_BF16X3 and d._head_shapes(l1, l2)
+    first = {"nconv1+nconv2_head": lambda: m.nconv.layer_forward_head(
+        l1.spec(lib.THRESH, 0.01), l2.spec(), S, l1.weight, l1.bias, s1, l2.weight, l2.bias, s2)} if head else {
         "nconv1": lambda: fwd(l1.spec(lib.THRESH, 0.01), S, None, None, None, l1.weight, l1.bias, s1),
-        "nconv2": lambda: fpool(l2.spec(), x1, c1, None, None, l2.weight, l2.bias, s2),
+        "nconv2": lambda: fpool(l2.spec(), x1, c1, None, None, l2.weight, l2.bias, s2)}
+    calls = {
+        **first,
         "nconv_down1": lambda: fpool(d1.spec(), p1, q1, None, None, d1.weight, d1.bias, sd1),
         "nconv_down2": lambda: fpool(d2.spec(), p2, q2, None, None, d2.weight, d2.bias, sd2),
         "nconv_down3": lambda: fwd(d3.spec(), p3, q3, None, None, d3.weight, d3.bias, sd3),
@@ -146,7 +158,7 @@ def time_layers(m, net, S, reps=20):
 
 # Layers on the bf16x3 matrix-core kernel (fwd_mfma, include/nconv.h NCONV_MATH_BF16X3): output
 # rows per tile, k-steps (4 positions x 8 channels each) and the grid each launch writes.
-MFMA_LAYERS = {"nconv2": (8, 8, 1), "nconv_down1": (8, 8, 2), "nconv_down2": (8, 8, 4), "nconv_down3": (8, 8, 8),
+MFMA_LAYERS = {"nconv1+nconv2_head": (8, 8, 1), "nconv2": (8, 8, 1), "nconv_down1": (8, 8, 2), "nconv_down2": (8, 8, 4), "nconv_down3": (8, 8, 8),
                "nconv4": (8, 6, 4), "nconv5": (8, 6, 2), "nconv6+7_tail": (8, 6, 1)}
 
 
@@ -460,6 +472,7 @@ def main():
         lt = time_layers(m, net, S)
         costs = layer_costs(B, H, W)
         costs["nconv6+7_tail"] = fused_tail_cost(B, H, W)
+        costs["nconv1+nconv2_head"] = head_cost(B, H, W)
         dom = max(lt, key=lambda n: lt[n])  # kernels of the timed inference pass
         byt, fl = costs[dom]
         us = lt[dom]

@@ -325,6 +325,7 @@ struct HeadStage {
         const int H = d.L.H, W = d.L.W;
         const int wave = tid >> 6, lane = tid & 63, half = wave & 1;
         constexpr int NQ = C::IH * 9, PERW = (NQ + 1) / 2;
+        static_assert(PERW <= 64, "one quad per lane");
         const int tq = (wave >> 1) * PERW + lane;
         if (lane < PERW && tq < NQ) {
             const int r = tq / 9, c0 = 4 * (tq - 9 * (tq / 9));
@@ -689,7 +690,9 @@ void go_mfma_any(const LayerDev& d, float* y, float* yc, const TailArgs& t, int 
 }  // namespace
 
 int launch_fwd_head(const LayerDev& d2, const TailArgs& t, float* y, float* yc, hipStream_t st, const char** why) {
-    go_mfma<8, 5, kModeHead, kEpiPool, NCONV_MF_TH5, false>(d2, y, yc, t, d2.L.Ho, d2.L.Wo, st);
+    // (16-row tiles recompute less of nconv1's halo but fit two workgroups per CU instead of three:
+    // 228 vs 215 us at B=8 352x1216)
+    go_mfma<8, 5, kModeHead, kEpiPool, 8, false>(d2, y, yc, t, d2.L.Ho, d2.L.Wo, st);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         *why = hipGetErrorString(e);

@@ -1,6 +1,8 @@
 set -e
-B="python -u bench.py --no-guided --no-guided-train --no-cpu-baseline --no-train"
-for fh in 1 0; do for st in 1 2; do
-  timeout -k 10 120 $B --fused-head $fh --streams $st > gpurun_out/b.json 2> gpurun_out/b.err
-  python -c "import json; d=json.load(open('gpurun_out/b.json')); print('head', $fh, 'streams', $st, d['value'], d['ms_per_step'])"
-done; done
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+timeout -k 10 200 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_layers.py tests/test_gpu_dnet.py > gpurun_out/pytest_mfma.log 2>&1 || { tail -30 gpurun_out/pytest_mfma.log; exit 1; }
+tail -1 gpurun_out/pytest_mfma.log
+timeout -k 10 400 python -u bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_r1c -o run -- python bench.py --no-cpu-baseline > gpurun_out/bench_prof.json 2> gpurun_out/bench_prof.err
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python tools/pmc_traffic.py run > gpurun_out/pmcf.log 2>&1
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python tools/pmc_traffic.py run > gpurun_out/pmcw.log 2>&1

@@ -10,7 +10,9 @@ import csv
 import statistics
 import sys
 
-ORDER = ["nconv1", "nconv2", "nconv_down1", "nconv_down2", "nconv_down3", "nconv4", "nconv5", "nconv6+7_tail"]
+ORDER = ["nconv1+nconv2_head", "nconv_down1", "nconv_down2", "nconv_down3", "nconv4", "nconv5", "nconv6+7_tail"]
+# (without the fused head: "nconv1", "nconv2", ... as separate launches)
+ORDER_UNFUSED = ["nconv1", "nconv2"] + ORDER[1:]
 RUN = 21
 
 
@@ -31,11 +33,13 @@ def main(src, dst):
     for r in runs:
         if len(r) >= RUN:
             pieces += [r[k:k + RUN] for k in range(0, len(r) - RUN + 1, RUN)]
-    pieces = pieces[-len(ORDER):]
+    order = ORDER_UNFUSED if any("fwd_tiled<1, 8, 5, 1" in p[0]["Kernel_Name"] for p in pieces[-len(ORDER_UNFUSED):]) \
+        else ORDER
+    pieces = pieces[-len(order):]
     with open(dst, "w", newline="") as fh:
         w = csv.writer(fh)
         w.writerow(["Layer", "Kernel_Name", "Grid_Size", "Calls", "AverageNs", "MedianNs", "MinNs", "MaxNs"])
-        for name, p in zip(ORDER, pieces):
+        for name, p in zip(order, pieces):
             d = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in p[1:]]  # skip the warm-up
             w.writerow([name, p[0]["Kernel_Name"][:120], p[0]["Grid_Size_X"], len(d), round(sum(d) / len(d), 1),
                         statistics.median(d), min(d), max(d)])

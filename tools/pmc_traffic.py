@@ -47,13 +47,15 @@ def run():
     torch.cuda.synchronize()
 
 
-ORDER = ["nconv1", "nconv2", "nconv_down1", "nconv_down2", "nconv_down3", "nconv4", "nconv5", "nconv6+7_tail"]
+ORDER = ["nconv1+nconv2_head", "nconv_down1", "nconv_down2", "nconv_down3", "nconv4", "nconv5", "nconv6+7_tail"]
+# (without the fused head: "nconv1", "nconv2", ... as separate launches)
+ORDER_UNFUSED = ["nconv1", "nconv2"] + ORDER[1:]
 
 
 def _read(dirpath, counter):
     """Per layer mean of `counter` over the timed inference forwards. Dispatches are taken in
-    order: an inference forward is weight_prep followed by exactly the 8 layer launches of ORDER
-    (the warm-up training forward has 9 and is skipped)."""
+    order: an inference forward is weight_prep followed by the 7 layer launches of ORDER (8 without
+    the fused head; the warm-up training forward has 9 and is skipped)."""
     files = glob.glob(os.path.join(dirpath, "**", "*counter_collection.csv"), recursive=True)
     if not files:
         raise SystemExit(f"no counter_collection.csv under {dirpath}")
@@ -68,9 +70,10 @@ def _read(dirpath, counter):
             cur.append(r)
     per = defaultdict(list)
     for g in groups:
-        if len(g) != len(ORDER):
+        order = {len(ORDER): ORDER, len(ORDER_UNFUSED): ORDER_UNFUSED}.get(len(g))
+        if order is None:
             continue
-        for name, r in zip(ORDER, g):
+        for name, r in zip(order, g):
             per[name].append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in per.items()}, {k: len(v) for k, v in per.items()}
 
