@@ -43,6 +43,8 @@ def parse():
     p.add_argument("--train-steps", type=int, default=None, help="timed fwd+bwd steps (default: --steps)")
     p.add_argument("--no-train", action="store_true")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-fp32-forward", action="store_true",
+                   help="skip the exact-fp32 (vector ALU) forward measurement reported beside the headline")
     p.add_argument("--no-guided", action="store_true", help="skip the config-3 guided forward measurement")
     p.add_argument("--no-guided-train", action="store_true", help="skip the config-4 guided training step")
     p.add_argument("--guided-train-torch", action="store_true",
@@ -369,43 +371,64 @@ def main():
         if world > 1:
             dist.barrier()
 
+    def time_forward(steps):
+        """W warm-up passes (hipGraph capture when --graph), then `steps` timed passes between
+        barrier + synchronize; returns (this rank's seconds, max over ranks)."""
+        graph = None
+        with torch.no_grad():
+            for _ in range(max(a.warmup, 1)):
+                net(S)
+            if a.graph:
+                s = torch.cuda.Stream()
+                s.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(s):
+                    for _ in range(2):
+                        net(S)
+                torch.cuda.current_stream().wait_stream(s)
+                graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(graph):
+                    net(S)
+                for _ in range(a.warmup):
+                    graph.replay()
+        torch.cuda.synchronize()
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        with torch.no_grad():
+            for _ in range(steps):
+                if graph is not None:
+                    graph.replay()
+                else:
+                    net(S)
+        torch.cuda.synchronize()
+        barrier()
+        el = time.perf_counter() - t0
+        el_max = el
+        if world > 1:
+            t = torch.tensor([el], device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el_max = t.item()
+        return el, el_max
+
     # ---- forward (headline) ----
     log("config 2 forward")
-    graph = None
-    with torch.no_grad():
-        for _ in range(max(a.warmup, 1)):
-            out = net(S)
-        if a.graph:
-            s = torch.cuda.Stream()
-            s.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(s):
-                for _ in range(2):
-                    out = net(S)
-            torch.cuda.current_stream().wait_stream(s)
-            graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph):
-                out = net(S)
-            for _ in range(a.warmup):
-                graph.replay()
-    torch.cuda.synchronize()
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    with torch.no_grad():
-        for _ in range(a.steps):
-            if graph is not None:
-                graph.replay()
-            else:
-                out = net(S)
-    torch.cuda.synchronize()
-    barrier()
-    t_fwd = time.perf_counter() - t0
-    t_fwd_max = t_fwd
-    if world > 1:
-        t = torch.tensor([t_fwd], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        t_fwd_max = t.item()
+    t_fwd, t_fwd_max = time_forward(a.steps)
     fps = world * B * a.steps / t_fwd_max
+    graph = a.graph
+
+    # ---- the same forward with exact fp32 products on the vector ALU (NCONV_MATH_FP32) ----
+    fwd_fp32 = None
+    if not a.no_fp32_forward:
+        log("config 2 forward, exact-fp32 arithmetic")
+        math0 = m.nconv.FORWARD_MATH
+        m.nconv.FORWARD_MATH = m._lib.MATH_FP32
+        try:
+            _, t32 = time_forward(a.steps)
+        finally:
+            m.nconv.FORWARD_MATH = math0
+        fwd_fp32 = {"frames_per_sec": round(world * B * a.steps / t32, 2),
+                    "ms_per_step": round(t32 / a.steps * 1e3, 4),
+                    "arith": "exact fp32 products, packed-FP32 vector ALU (fwd_tiled)"}
 
     # ---- fwd + bwd + AdamW (config 4b) ----
     log("config 2 forward done:", round(fps, 1), "frames/s; config 4b training step")
@@ -507,8 +530,11 @@ def main():
             "config": {"workload": "config2: SETP1_NCONV/DNET forward, fused HIP NConv kernels",
                        "global_batch": B * world, "per_gpu_batch": B, "height": H, "width": W,
                        "crop": "generalized [1:H+1,1:W+1]", "parallelism": f"frame-sharded x{world}",
-                       "hipgraph": bool(graph is not None), "streams": a.streams,
+                       "hipgraph": bool(graph), "streams": a.streams,
                        "fused_head": bool(a.fused_head)},
+            "arith": "fp32 in/out and accumulation; 8-channel layers' products as split-bf16 (bf16x3) matrix-core "
+                     "terms (<= ~1.1e-5 relative per product, parity within the 1e-4 forward tolerance)",
+            "fwd_fp32_exact": fwd_fp32,
             "train_fwd_bwd_adamw": train,
             "guided_fwd": guided,
             "guided_train_fwd_bwd_adamw": guided_train,

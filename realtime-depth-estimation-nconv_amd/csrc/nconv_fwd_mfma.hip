@@ -107,33 +107,66 @@ struct MfStage {
                 gb[k] = in ? (unsigned)(sh * L.b.W + sw) * 4u : OOB;
             }
         }
+        // One buffer resource per source tensor of this image (all its channels; the host checks
+        // the size fits), the channel's plane offset in the scalar offset: 4 resources instead of
+        // 2 per input channel, which kept the 16-channel kernels spilling scalar registers.
+        int pa = L.a.H * L.a.W * 4;
+        int pb = UP ? L.b.H * L.b.W * 4 : 0;
+        // (opaque per call: keeps the per-channel offsets out of the tile loop's invariant SGPRs)
+        asm volatile("" : "+s"(pa), "+s"(pb));
+        const __amdgpu_buffer_rsrc_t rax = plane_rsrc(L.a.x + (size_t)b * L.a.C * (pa / 4), L.a.C * pa);
+        const __amdgpu_buffer_rsrc_t rac = plane_rsrc(L.a.c + (size_t)b * L.a.C * (pa / 4), L.a.C * pa);
+        const __amdgpu_buffer_rsrc_t rbx = UP ? plane_rsrc(L.b.x + (size_t)b * L.b.C * (pb / 4), L.b.C * pb) : rax;
+        const __amdgpu_buffer_rsrc_t rbc = UP ? plane_rsrc(L.b.c + (size_t)b * L.b.C * (pb / 4), L.b.C * pb) : rac;
 #pragma unroll
         for (int ci = 0; ci < CIN; ++ci) {
-            const ChanSrc s = chan_src<MODE>(d, b, ci);  // wave-uniform
-            const __amdgpu_buffer_rsrc_t rx = plane_rsrc(s.x, s.bytes), rc = plane_rsrc(s.c, s.bytes);
             if constexpr (MODE == NCONV_LOAD_POOL2) {
-                const unsigned row = (unsigned)s.W * 4u;
+                const unsigned row = (unsigned)L.a.W * 4u;
+                const int so = ci * pa;
 #pragma unroll
                 for (int k = 0; k < C::NE; ++k) {
                     const unsigned o2 = ga[k] == OOB ? OOB : ga[k] + row;
-                    const f2 x0 = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rx, ga[k], 0, 0));
-                    const f2 x1 = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rx, o2, 0, 0));
-                    const f2 c0 = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rc, ga[k], 0, 0));
-                    const f2 c1 = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rc, o2, 0, 0));
+                    const f2 x0 = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rax, ga[k], so, 0));
+                    const f2 x1 = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rax, o2, so, 0));
+                    const f2 c0 = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rac, ga[k], so, 0));
+                    const f2 c1 = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rac, o2, so, 0));
                     xv[k][ci] = pool4v(x0.x, x0.y, x1.x, x1.y);
                     cv[k][ci] = pool4v(c0.x, c0.y, c1.x, c1.y);
                 }
             } else {
-                const bool up = UP && s.kind == kUp;
+                // channel ci of the concatenation: source a or (nearest-upsampled) b, wave-uniform
+                bool from_a = true;
+                int cs = ci;
+                if constexpr (MODE == NCONV_LOAD_UPCAT_SKIP_FIRST) {
+                    from_a = ci < L.a.C;
+                    cs = from_a ? ci : ci - L.a.C;
+                } else if constexpr (MODE == NCONV_LOAD_UPCAT_UP_FIRST) {
+                    from_a = ci >= L.b.C;
+                    cs = from_a ? ci - L.b.C : ci;
+                }
 #pragma unroll
                 for (int k = 0; k < C::NE; ++k) {
-                    const unsigned o = UP ? (up ? gb[UP ? k : 0] : ga[k]) : ga[k];
 #ifdef NCONV_EXP_MF_NOLOAD
-                    xv[k][ci] = (float)(o & 255);
+                    xv[k][ci] = (float)(ga[k] & 255);
                     cv[k][ci] = 0.5f;
 #else
-                    xv[k][ci] = ld_f32(rx, o);
-                    cv[k][ci] = ld_f32(rc, o);
+#ifdef NCONV_MF_PERCHAN_RSRC
+                    {
+                        const ChanSrc cs_ = chan_src<MODE>(d, b, ci);
+                        const __amdgpu_buffer_rsrc_t rx = plane_rsrc(cs_.x, cs_.bytes), rc = plane_rsrc(cs_.c, cs_.bytes);
+                        const unsigned o = UP && cs_.kind == kUp ? gb[UP ? k : 0] : ga[k];
+                        xv[k][ci] = ld_f32(rx, o);
+                        cv[k][ci] = ld_f32(rc, o);
+                    }
+#else
+                    if (!UP || from_a) {
+                        xv[k][ci] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rax, ga[k], cs * pa, 0));
+                        cv[k][ci] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rac, ga[k], cs * pa, 0));
+                    } else {
+                        xv[k][ci] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rbx, gb[UP ? k : 0], cs * pb, 0));
+                        cv[k][ci] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rbc, gb[UP ? k : 0], cs * pb, 0));
+                    }
+#endif
 #endif
                 }
             }
@@ -290,9 +323,20 @@ struct HeadStage {
     using C = MfCfg<8, 5, TH>;
     static constexpr int SH = C::IH + 4, SW = C::IW + 4;  // nconv1's own 5x5 halo around the tile
     static constexpr int NS = SH * SW, NES = (NS + kMfThreads - 1) / kMfThreads;
-    static constexpr int BYTES = NS * 8;                  // {S * c0, c0} pairs
+    static constexpr int WOFF = NS * 8;                   // {S * c0, c0} pairs, then
+    static constexpr int BYTES = WOFF + 2 * 25 * 16;      // nconv1's weights [half][kw][kh][o4]
     static constexpr bool SELF_SYNC = true;
     float sv[NES];
+
+    // nconv1's weights into LDS once per workgroup (visible after to_planes' first barrier), in
+    // the order the column loop reads them: one broadcast float4 (4 output channels) per tap.
+    __device__ __forceinline__ void init(const TailArgs& t, unsigned char* stage, int tid) const {
+        if (tid < 200) {
+            const int half = tid / 100, rem = tid - 100 * half;
+            const int kw = rem / 20, kh = (rem / 4) % 5, o = rem % 4;
+            reinterpret_cast<float*>(stage + WOFF)[tid] = t.w1[(half * 4 + o) * 25 + kh * 5 + kw];
+        }
+    }
 
     __device__ __forceinline__ void issue(const LayerDev& d, const TailArgs& t, int b, int ih0, int iw0,
                                           unsigned char*, int tid) {
@@ -318,42 +362,48 @@ struct HeadStage {
             if (NES * kMfThreads == NS || e < NS) T[e] = (f2){sv[k] * c0, c0};
         }
         __syncthreads();  // (also: every wave is done with the previous tile's planes)
-        // nconv1: wave w computes output channels 4 (w & 1) .. +3 (their 20 weights per kernel row
-        // are wave-uniform: scalar loads, one per 4 pixels) for quads of 4 adjacent positions,
-        // half of the 108 quads of the (IH x 36) tile per wave pair.
-        static_assert(C::IW == 36, "9 quads of 4 positions per staged row");
+        // nconv1: wave w computes output channels 4 (w & 1) .. +3 for column quads — one staged
+        // column and 4 consecutive rows per lane, half of the (IH / 4) x 36 quads per wave pair.
+        // The weights come from LDS (broadcast reads; per-lane global weight loads were
+        // vector-memory reads the loop waited on each iteration together with the previous tile's
+        // outstanding stores, and scalar loads also stalled it); consecutive lanes read consecutive
+        // {x*c, c} pairs, so the window reads are free of LDS bank conflicts.
+        static_assert(C::IW == 36 && C::IH % 4 == 0, "36 staged columns, whole row quads");
         const int H = d.L.H, W = d.L.W;
-        const int wave = tid >> 6, lane = tid & 63, half = wave & 1;
-        constexpr int NQ = C::IH * 9, PERW = (NQ + 1) / 2;
+        const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, half = wave & 1;
+        constexpr int NQ = (C::IH / 4) * C::IW, PERW = (NQ + 1) / 2;
         static_assert(PERW <= 64, "one quad per lane");
         const int tq = (wave >> 1) * PERW + lane;
         if (lane < PERW && tq < NQ) {
-            const int r = tq / 9, c0 = 4 * (tq - 9 * (tq / 9));
-            const float* __restrict__ w1 = t.w1 + half * 4 * 25;
+            const int rq = tq / C::IW, c = tq - rq * C::IW, r0 = 4 * rq;
+            const f4* wl = reinterpret_cast<const f4*>(stage + WOFF) + half * 25;
             f2 acc[4][4];
 #pragma unroll
             for (int j = 0; j < 4; ++j)
 #pragma unroll
                 for (int o = 0; o < 4; ++o) acc[j][o] = (f2){0.f, 0.f};
 #pragma unroll 1
-            for (int kh = 0; kh < 5; ++kh) {
-                const f2* row = T + (r + kh) * SW + c0;
+            for (int kw = 0; kw < 5; ++kw) {
+                const f2* col = T + r0 * SW + c + kw;
                 f2 v[8];
 #pragma unroll
-                for (int m = 0; m < 8; ++m) v[m] = row[m];
+                for (int m = 0; m < 8; ++m) v[m] = col[m * SW];
 #pragma unroll
-                for (int kw = 0; kw < 5; ++kw)
+                for (int kh = 0; kh < 5; ++kh) {
+                    const f4 w4 = wl[kw * 5 + kh];
 #pragma unroll
                     for (int o = 0; o < 4; ++o) {
-                        const float w = w1[o * 25 + kh * 5 + kw];
+                        const float w = w4[o];
 #pragma unroll
-                        for (int j = 0; j < 4; ++j) acc[j][o] = __builtin_elementwise_fma((f2){w, w}, v[j + kw], acc[j][o]);
+                        for (int j = 0; j < 4; ++j) acc[j][o] = __builtin_elementwise_fma((f2){w, w}, v[j + kh], acc[j][o]);
                     }
+                }
             }
             typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const bool in = (unsigned)(ih0 + r) < (unsigned)H && (unsigned)(iw0 + c0 + j) < (unsigned)W;
+                const int r = r0 + j;
+                const bool in = (unsigned)(ih0 + r) < (unsigned)H && (unsigned)(iw0 + c) < (unsigned)W;
                 bf16x4 ph, pl, qh, ql;
 #pragma unroll
                 for (int o = 0; o < 4; ++o) {
@@ -367,7 +417,7 @@ struct HeadStage {
                     qh[o] = q1;
                     ql[o] = (__bf16)(q - (float)q1);
                 }
-                unsigned char* base = lds + (r * C::IW + c0 + j) * 16 + half * 8;
+                unsigned char* base = lds + (r * C::IW + c) * 16 + half * 8;
                 *reinterpret_cast<bf16x4*>(base) = ph;
                 *reinterpret_cast<bf16x4*>(base + C::PSTRIDE) = pl;
                 *reinterpret_cast<bf16x4*>(base + 2 * C::PSTRIDE) = qh;
@@ -386,8 +436,15 @@ struct HeadStage {
 #define NCONV_MFMA_WAVES 3  // waves per SIMD: 168 VGPRs (3 workgroups per CU) without spilling
 #endif
 // POOL2 staging holds four values per element before pooling: 2 waves per SIMD (no spills)
+#ifndef NCONV_MFMA_UP_WAVES
+#define NCONV_MFMA_UP_WAVES 2  // the 16-channel upsample-concat layers (nconv4/5/6): no spills
+#endif
 template <int MODE, bool DMA>
-constexpr int mf_waves() { return DMA || MODE == NCONV_LOAD_POOL2 ? 2 : NCONV_MFMA_WAVES; }
+constexpr int mf_waves() {
+    return DMA || MODE == NCONV_LOAD_POOL2 ? 2
+           : (MODE == NCONV_LOAD_UPCAT_SKIP_FIRST || MODE == NCONV_LOAD_UPCAT_UP_FIRST) ? NCONV_MFMA_UP_WAVES
+                                                                                         : NCONV_MFMA_WAVES;
+}
 template <int CIN, int K, int MODE, int TH, bool DMA>
 using StageOf = typename std::conditional<
     MODE == kModeHead, HeadStage<TH>,
@@ -406,7 +463,11 @@ __global__ __launch_bounds__(kMfThreads) __attribute__((amdgpu_waves_per_eu(mf_w
     __shared__ __attribute__((aligned(16))) unsigned char lds[mf_lds_bytes<CIN, K, MODE, EPI, TH>(DMA)];
     unsigned char* const stage = lds + MfCfg<CIN, K, TH>::LDS_IN + (EPI == kEpiTail ? 0 : 4 * 2 * 16 * kOutPitch * 4);
     const nconv_layer& L = d.L;
+#ifdef NCONV_MF_WAVE_VGPR
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#else
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+#endif
     const bool tail = EPI == kEpiTail;
     const int gh = tail ? t.out_h : L.Ho, gw = tail ? t.out_w : L.Wo;  // the written grid
     const int ntx = (gw + C::TW - 1) / C::TW, nty = (gh + TH - 1) / TH;
@@ -414,11 +475,28 @@ __global__ __launch_bounds__(kMfThreads) __attribute__((amdgpu_waves_per_eu(mf_w
     const int off = tail ? t.off : 0;
 
     Stage st;
+    if constexpr (MODE == kModeHead) st.init(t, stage, threadIdx.x);
     int v = blockIdx.x;
-    {  // loads are unconditional (a block without tiles loads the last one and never uses it)
-        const TileCoord tc = xcd_tile(ntx, nty, L.B, v < ntiles ? v : ntiles - 1);
-        st.issue(d, t, tc.b, tc.ty * TH + off - L.PH, tc.tx * C::TW + off - L.PW, stage, tid);
-    }
+    // The block's tiles: virtual ids v, v + gridDim.x, ... map (xcd_tile) to linear tiles t, t + G8,
+    // ... (G8 = gridDim.x / 8), so after one mapping the walk advances (tx, ty, b) by a fixed
+    // stride — no per-tile integer divisions by the runtime grid extents.
+    TileCoord tc = xcd_tile(ntx, nty, L.B, v < ntiles ? v : ntiles - 1);
+    const int g8 = (int)gridDim.x / 8, step_ty = g8 / ntx, step_tx = g8 - step_ty * ntx;
+    auto advance = [&](TileCoord c) {
+        c.tx += step_tx;
+        c.ty += step_ty;
+        if (c.tx >= ntx) {
+            c.tx -= ntx;
+            c.ty += 1;
+        }
+        while (c.ty >= nty) {
+            c.ty -= nty;
+            c.b += 1;
+        }
+        return c;
+    };
+    // loads are unconditional (a block without tiles loads the last one and never uses it)
+    st.issue(d, t, tc.b, tc.ty * TH + off - L.PH, tc.tx * C::TW + off - L.PW, stage, tid);
 
     // ---- B fragments (weights, once per workgroup) and per-lane A offsets ----
     const int u = lane & 15, h = lane >> 4;
@@ -449,16 +527,16 @@ __global__ __launch_bounds__(kMfThreads) __attribute__((amdgpu_waves_per_eu(mf_w
 
 #pragma unroll 1
     for (; v < ntiles; v += gridDim.x) {
-        const TileCoord tc = xcd_tile(ntx, nty, L.B, v);
+        TileCoord tc_next;
         const int b = tc.b;
         const int R0 = tc.ty * TH, C0 = tc.tx * C::TW;  // tile origin in the written grid
         const int oh0 = R0 + off, ow0 = C0 + off;         // ... in this layer's output grid
         st.to_planes(d, t, oh0 - L.PH, ow0 - L.PW, lds, stage, tid);
         __syncthreads();
         {  // next tile's loads fly during this tile's MFMAs (the last tile re-loads itself)
-            const int vn = v + (int)gridDim.x < ntiles ? v + (int)gridDim.x : v;
-            const TileCoord tn = xcd_tile(ntx, nty, L.B, vn);
+            const TileCoord tn = v + (int)gridDim.x < ntiles ? advance(tc) : tc;
             st.issue(d, t, tn.b, tn.ty * TH + off - L.PH, tn.tx * C::TW + off - L.PW, stage, tid);
+            tc_next = tn;
         }
 
         // ---- MFMAs: wave w takes the row pairs rp = w, w+4, ..., both 16-column halves ct ----
@@ -466,11 +544,11 @@ __global__ __launch_bounds__(kMfThreads) __attribute__((amdgpu_waves_per_eu(mf_w
 #pragma unroll 1
         for (int rpi = 0; rpi < C::NRP / 4; ++rpi) {
             const int rp = wave + 4 * rpi;
-            f4_ accN[2], accD[2];
-#pragma unroll
-            for (int ct = 0; ct < 2; ++ct) {
+            // the 16 x 16 {N, D} tiles of column half ct (16 ct .. +15) of row pair rp
+            auto mma = [&](int ct, f4_& n, f4_& dd) {
                 const unsigned char* tb = lds + (2 * rp * C::IW + 16 * ct) * 16;
-                f4_ n = {0.f, 0.f, 0.f, 0.f}, dd = {0.f, 0.f, 0.f, 0.f};
+                n = (f4_){0.f, 0.f, 0.f, 0.f};
+                dd = (f4_){0.f, 0.f, 0.f, 0.f};
 #ifdef NCONV_EXP_MF_NOMFMA
                 n[0] = tb[aoff[0]];
 #else
@@ -489,24 +567,25 @@ __global__ __launch_bounds__(kMfThreads) __attribute__((amdgpu_waves_per_eu(mf_w
                     dd = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dh, bh[q], dd, 0, 0, 0);
                 }
 #endif
-                accN[ct] = n;
-                accD[ct] = dd;
-            }
+            };
 
             // ---- epilogue: this lane holds (o, row oh, columns 16 ct + 4 h .. +3) per half ct ----
             // Every global store is an unconditional buffer store; lanes with nothing to write carry
             // an offset past the resource (dropped by the hardware). The number of stores per tile is
             // thus static, so the wait for the next tile's loads (issued before these stores) does not
             // also wait for the stores to complete.
-            float yv[2][4], cv[2][4];
-#pragma unroll
-            for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    yv[ct][r] = accN[ct][r] * __builtin_amdgcn_rcpf(accD[ct][r] + eps) + bo;
-                    cv[ct][r] = accD[ct][r] * rcp_s;
-                }
             if constexpr (EPI != kEpiTail) {
+                float yv[2][4], cv[2][4];
+#pragma unroll
+                for (int ct = 0; ct < 2; ++ct) {
+                    f4_ accN, accD;
+                    mma(ct, accN, accD);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        yv[ct][r] = accN[r] * __builtin_amdgcn_rcpf(accD[r] + eps) + bo;
+                        cv[ct][r] = accD[r] * rcp_s;
+                    }
+                }
                 // Transpose the row pair through this wave's LDS region ([o + 8 s][32 columns], pitch
                 // 36 floats: conflict-free f4 writes), so that each global store instruction writes
                 // eight whole 128-byte rows (lane: channel l>>3, columns 4 (l&7) .. +3) instead of
@@ -587,14 +666,18 @@ __global__ __launch_bounds__(kMfThreads) __attribute__((amdgpu_waves_per_eu(mf_w
                 const bool wr = o == 0 && orow < t.out_h;
                 const unsigned rowoff = (unsigned)(orow * t.out_w) * 4u;
 #pragma unroll
-                for (int ct = 0; ct < 2; ++ct) {
+                for (int ct = 0; ct < 2; ++ct) {  // one column half at a time: fewer live registers
+                    f4_ accN, accD;
+                    mma(ct, accN, accD);
                     const int ow = ow0 + 16 * ct + 4 * h, ocol = C0 + 16 * ct + 4 * h;
                     float n7[4], d7[4];
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
+                        const float yv = accN[r] * __builtin_amdgcn_rcpf(accD[r] + eps) + bo;
+                        const float cv = accD[r] * rcp_s;
                         const bool ok = (unsigned)oh < (unsigned)L.Ho && (unsigned)(ow + r) < (unsigned)L.Wo;
-                        n7[r] = ok ? w7 * (yv[ct][r] * cv[ct][r]) : 0.f;
-                        d7[r] = ok ? w7 * cv[ct][r] : 0.f;
+                        n7[r] = ok ? w7 * (yv * cv) : 0.f;
+                        d7[r] = ok ? w7 * cv : 0.f;
                     }
 #pragma unroll
                     for (int m = 1; m < 8; m <<= 1)
@@ -624,6 +707,7 @@ __global__ __launch_bounds__(kMfThreads) __attribute__((amdgpu_waves_per_eu(mf_w
         // every wave is done reading the planes before the next tile's are formed (DmaStage's own
         // barrier, after its wait, does this there; a __syncthreads here would drain the DMA)
         if constexpr (!Stage::SELF_SYNC) __syncthreads();
+        tc = tc_next;
     }
 }
 
@@ -707,6 +791,11 @@ bool launch_fwd_mfma(const LayerDev& d, float* y, float* yc, const TailArgs& t, 
     const nconv_layer& L = d.L;
     if (L.math != NCONV_MATH_BF16X3 || L.Cout != 8 || L.KH != L.KW || L.SH != 1 || L.SW != 1 || L.DH != 1 ||
         L.DW != 1 || L.groups != 1)
+        return false;
+    // MfStage addresses one image's channels of a source through one buffer resource
+    auto image_fits = [](const nconv_src& s) { return (long long)s.C * s.H * s.W * 4 < (1LL << 31); };
+    if (!image_fits(L.a) || ((L.load_mode == NCONV_LOAD_UPCAT_SKIP_FIRST || L.load_mode == NCONV_LOAD_UPCAT_UP_FIRST) &&
+                             !image_fits(L.b)))
         return false;
     const bool pool = !tail && t.py != nullptr;
     const int gh = tail ? t.out_h : L.Ho, gw = tail ? t.out_w : L.Wo;
