@@ -101,7 +101,7 @@ int nconv_fwd_pooled(const nconv_layer* L, float* y, float* cout, float* y_pool,
  * tile (step1.py:58; L2: 8 -> 8, 5x5, padding 2, stride 1; its sources are not read), so nconv1's
  * 8-channel output never reaches HBM. Writes nconv2's y, cout (B, 8, H, W) and their 2x2 max-pooled
  * copies (B, 8, H/2, W/2) like nconv_fwd_pooled. Matrix-core math only (L2->math ==
- * NCONV_MATH_BF16X3; nconv1 itself is exact fp32); -EOPNOTSUPP otherwise. */
+ * NCONV_MATH_BF16X3, which nconv1 then uses as well); -EOPNOTSUPP otherwise. */
 int nconv_fwd_head(const nconv_layer* L1, const nconv_layer* L2, float* y, float* cout, float* y_pool,
                    float* cout_pool, void* stream);
 

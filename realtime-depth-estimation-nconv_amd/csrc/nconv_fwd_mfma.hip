@@ -56,18 +56,24 @@ struct MfCfg {
 };
 
 constexpr unsigned kOOB = 0x80000000u;
-constexpr int kOutPitch = 36;  // floats per row of a wave's output-transpose region  // buffer offset past any resource: access dropped
+constexpr int kOutPitch = 36;  // floats per row of a wave's output-transpose region
+constexpr int kTrBytes = 4 * 16 * kOutPitch * 4;  // four waves' regions (y, then cout, through one)
 
+#ifdef NCONV_EXP_MF_NOSTORE
+#define NCONV_STORE_OFF(o) (((o) & 0u) | 0x80000000u)
+#else
+#define NCONV_STORE_OFF(o) (o)
+#endif
 __device__ __forceinline__ void st_f32(__amdgpu_buffer_rsrc_t r, unsigned off, float v) {
-    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, (int)off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, (int)NCONV_STORE_OFF(off), 0, 0);
 }
 __device__ __forceinline__ void st_f2(__amdgpu_buffer_rsrc_t r, unsigned off, f2 v) {
     typedef unsigned u2 __attribute__((ext_vector_type(2)));
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v), r, (int)off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v), r, (int)NCONV_STORE_OFF(off), 0, 0);
 }
 __device__ __forceinline__ void st_f4(__amdgpu_buffer_rsrc_t r, unsigned off, f4 v) {
     typedef unsigned u4 __attribute__((ext_vector_type(4)));
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, v), r, (int)off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, v), r, (int)NCONV_STORE_OFF(off), 0, 0);
 }
 
 __device__ __forceinline__ void split8(const float (&v)[8], bf16x8& hi, bf16x8& lo) {
@@ -382,6 +388,10 @@ struct HeadStage {
             for (int j = 0; j < 4; ++j)
 #pragma unroll
                 for (int o = 0; o < 4; ++o) acc[j][o] = (f2){0.f, 0.f};
+#ifdef NCONV_EXP_HEAD_NONC1
+            for (int j = 0; j < 4; ++j)
+                for (int o = 0; o < 4; ++o) acc[j][o] = T[(r0 + j) * SW + c + o];
+#else
 #pragma unroll 1
             for (int kw = 0; kw < 5; ++kw) {
                 const f2* col = T + r0 * SW + c + kw;
@@ -399,6 +409,7 @@ struct HeadStage {
                     }
                 }
             }
+#endif
             typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
@@ -427,6 +438,151 @@ struct HeadStage {
     }
 };
 
+// The fused head with nconv1 on the matrix cores as well (the default; -DNCONV_HEAD_NC1_VALU keeps
+// the exact-fp32 vector-ALU nconv1 above). GEMM per v_mfma_f32_16x16x32_bf16, per block of 16
+// columns x 4 rows of nconv1's (IH x IW) output region: D[(o, s')][u] = sum_k A[(o, s')][k] B[k][u]
+// with k = (kw: the lane group, kh': 8 consecutive rows of the window), so the lane holding output
+// column u reads 8 consecutive rows of one staged column: the thresholded depth is staged
+// column-major (bf16 planes S*c0 hi, S*c0 lo, c0 — c0 in {0, 1} is exact, so D takes 2 split
+// products and N 3), one 16-byte row window per (part, k-step) read as dwords (row offsets are
+// even, not multiples of 8). A (the weights, W1[o][kh' - s'][kw] for the window of output rows
+// 4g + 2m + s') is independent of the row pair m and lives in LDS. The lane's outputs are 4
+// channels of one position: the bf16x4 halves of nconv2's planes, written directly.
+template <int TH>
+struct HeadStageMf {
+    using C = MfCfg<8, 5, TH>;
+    static constexpr int SH = C::IH + 4, SW = C::IW + 4;  // nconv1's input halo
+    static constexpr int NS = SH * SW, NES = (NS + kMfThreads - 1) / kMfThreads;
+    static constexpr int NCB = (C::IW + 15) / 16, NG = C::IH / 4;  // column blocks, row groups
+    static constexpr int CW = 16 * NCB + 4;  // staged columns read (past SW: zeros)
+    static constexpr int RS = SH + 4;        // rows per staged column (+ zero rows), 2 B each
+    static constexpr int COLB = RS * 2;      // bytes per staged column: 40 (conflict-free b32 reads)
+    static constexpr int PART = CW * COLB;   // bytes per part
+    static constexpr int AOFF = 3 * PART;    // weights' A fragments [step][hi/lo][lane] bf16x8
+    static constexpr int BOFF = AOFF + 4 * 64 * 16;  // nconv1's bias[8], 1 / s[8]
+    static constexpr int BYTES = BOFF + 16 * 4;
+    static constexpr bool SELF_SYNC = true;
+    static_assert(C::IH % 4 == 0 && RS % 2 == 0 && (PART % 16) == 0, "layout");
+    float sv[NES];
+
+    __device__ __forceinline__ void init(const TailArgs& t, unsigned char* stage, int tid) const {
+        // zero the staged parts once: the padding rows / columns are read (against zero weights)
+        // and must hold finite values; the staging below rewrites only the SH x SW interior
+        for (int i = tid; i < AOFF / 16; i += kMfThreads) reinterpret_cast<f4*>(stage)[i] = (f4){0.f, 0.f, 0.f, 0.f};
+        // A fragment of lane l for k-step st (kw = 4 st + kg) and part (hi / lo)
+        const int f = tid >> 6, l = tid & 63, st = f >> 1, part = f & 1;
+        const int i = l & 15, o = i & 7, sp = i >> 3, kg = l >> 4, kw = 4 * st + kg;
+        float w[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int kh = e - sp;
+            w[e] = (kw < 5 && kh >= 0 && kh < 5) ? t.w1[(o * 5 + kh) * 5 + kw] : 0.f;
+        }
+        bf16x8 hi, lo;
+        split8(w, hi, lo);
+        *reinterpret_cast<bf16x8*>(stage + AOFF + (f * 64 + l) * 16) = part ? lo : hi;
+        if (tid < 16)
+            reinterpret_cast<float*>(stage + BOFF)[tid] = tid < 8 ? t.b1[tid] : __builtin_amdgcn_rcpf(t.s1[tid - 8]);
+    }
+
+    __device__ __forceinline__ void issue(const LayerDev& d, const TailArgs& t, int b, int ih0, int iw0,
+                                          unsigned char*, int tid) {
+        const int H = d.L.H, W = d.L.W;
+        const __amdgpu_buffer_rsrc_t rs = plane_rsrc(t.s_in + (size_t)b * H * W, H * W * 4);
+#pragma unroll
+        for (int k = 0; k < NES; ++k) {
+            const int e = tid + kMfThreads * k;
+            const int r = e / SW, col = e - r * SW;
+            const int ih = ih0 - 2 + r, iw = iw0 - 2 + col;
+            const bool in = e < NS && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+            sv[k] = ld_f32(rs, in ? (unsigned)(ih * W + iw) * 4u : kOOB);
+        }
+    }
+
+    // 8 consecutive bf16 of a staged column from a 4-byte-aligned address (two ds_read2_b32)
+    static __device__ __forceinline__ bf16x8 rd_window(const unsigned char* q) {
+        typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+        const unsigned* w = reinterpret_cast<const unsigned*>(q);
+        return __builtin_bit_cast(bf16x8, (u32x4){w[0], w[1], w[2], w[3]});
+    }
+
+    __device__ __forceinline__ void to_planes(const LayerDev& d, const TailArgs& t, int ih0, int iw0,
+                                              unsigned char* lds, unsigned char* stage, int tid) const {
+        // (every wave has finished the previous tile's nconv1 reads: the barrier before the MFMA
+        // phase separates them from these writes)
+#pragma unroll
+        for (int k = 0; k < NES; ++k) {
+            const int e = tid + kMfThreads * k;
+            if (NES * kMfThreads != NS && e >= NS) continue;
+            const int r = e / SW, col = e - r * SW;
+            const float c0 = sv[k] > t.thresh1 ? 1.0f : 0.0f;  // step1.py:53
+            const float p = sv[k] * c0;
+            const __bf16 ph = (__bf16)p;
+            unsigned char* q = stage + col * COLB + r * 2;
+            *reinterpret_cast<__bf16*>(q) = ph;
+            *reinterpret_cast<__bf16*>(q + PART) = (__bf16)(p - (float)ph);
+            *reinterpret_cast<__bf16*>(q + 2 * PART) = (__bf16)c0;
+        }
+        __syncthreads();
+        const int H = d.L.H, W = d.L.W;
+        const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+        const int u = lane & 15, kg = lane >> 4, half = kg & 1, sp = lane >> 5;
+        const bf16x8 a0h = *reinterpret_cast<const bf16x8*>(stage + AOFF + (0 * 64 + lane) * 16);
+        const bf16x8 a0l = *reinterpret_cast<const bf16x8*>(stage + AOFF + (1 * 64 + lane) * 16);
+        const bf16x8 a1h = *reinterpret_cast<const bf16x8*>(stage + AOFF + (2 * 64 + lane) * 16);
+        const bf16x8 a1l = *reinterpret_cast<const bf16x8*>(stage + AOFF + (3 * 64 + lane) * 16);
+        // (from LDS: a global load here would wait for the previous tile's stores as well)
+        const f4 bias = reinterpret_cast<const f4*>(stage + BOFF)[half];
+        const f4 rs1 = reinterpret_cast<const f4*>(stage + BOFF)[2 + half];
+        typedef float f4_ __attribute__((ext_vector_type(4)));
+#pragma unroll 1
+        for (int blk = wave; blk < NG * NCB; blk += 4) {
+            const int g = blk / NCB, cb = blk - g * NCB;
+#pragma unroll
+            for (int m = 0; m < 2; ++m) {
+                const int r0 = 4 * g + 2 * m;  // first window row (staged coordinates)
+                f4_ n = {0.f, 0.f, 0.f, 0.f}, dd = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int st = 0; st < 2; ++st) {
+                    const int kw = st == 0 ? kg : 4;  // k-step 1: only group 0 (kw 4) has weights
+                    const unsigned char* q = stage + (16 * cb + u + kw) * COLB + r0 * 2;
+                    const bf16x8 ph = rd_window(q), pl = rd_window(q + PART), cz = rd_window(q + 2 * PART);
+                    const bf16x8 ah = st ? a1h : a0h, al = st ? a1l : a0l;
+                    n = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, ph, n, 0, 0, 0);
+                    dd = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, cz, dd, 0, 0, 0);
+                    n = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, pl, n, 0, 0, 0);
+                    n = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, ph, n, 0, 0, 0);
+                    dd = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, cz, dd, 0, 0, 0);
+                }
+                // lane: channels 4 half .. +3 of nconv1 output (row r0 + sp, column 16 cb + u)
+                const int row = r0 + sp, col = 16 * cb + u;
+                const bool in = (unsigned)(ih0 + row) < (unsigned)H && (unsigned)(iw0 + col) < (unsigned)W;
+                typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+                bf16x4 xh, xl, qh, ql;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float xv = n[r] * __builtin_amdgcn_rcpf(dd[r] + t.eps1) + bias[r];
+                    const float cv = dd[r] * rs1[r];
+                    const float q = in ? cv : 0.f;  // nconv2's zero padding outside the image
+                    const float pv = in ? xv * cv : 0.f;
+                    const __bf16 p1 = (__bf16)pv, q1 = (__bf16)q;
+                    xh[r] = p1;
+                    xl[r] = (__bf16)(pv - (float)p1);
+                    qh[r] = q1;
+                    ql[r] = (__bf16)(q - (float)q1);
+                }
+                if (col < C::IW) {
+                    unsigned char* base = lds + (row * C::IW + col) * 16 + half * 8;
+                    *reinterpret_cast<bf16x4*>(base) = xh;
+                    *reinterpret_cast<bf16x4*>(base + C::PSTRIDE) = xl;
+                    *reinterpret_cast<bf16x4*>(base + 2 * C::PSTRIDE) = qh;
+                    *reinterpret_cast<bf16x4*>(base + 3 * C::PSTRIDE) = ql;
+                }
+            }
+        }
+    }
+};
+
 // Persistent: gridDim.x (a multiple of 8) workgroups walk the tiles; the next tile's halo loads
 // are in flight while the current one's MFMAs and epilogue run.
 #ifndef NCONV_MF_TH5
@@ -447,12 +603,17 @@ constexpr int mf_waves() {
 }
 template <int CIN, int K, int MODE, int TH, bool DMA>
 using StageOf = typename std::conditional<
-    MODE == kModeHead, HeadStage<TH>,
+    MODE == kModeHead,
+#ifdef NCONV_HEAD_NC1_VALU
+    HeadStage<TH>,
+#else
+    HeadStageMf<TH>,
+#endif
     typename std::conditional<DMA, DmaStage<CIN, K, MODE, TH>, MfStage<CIN, K, MODE, TH>>::type>::type;
 template <int CIN, int K, int MODE, int EPI, int TH>
 constexpr int mf_lds_bytes(bool dma) {
-    return MfCfg<CIN, K, TH>::LDS_IN + (EPI == kEpiTail ? 0 : 4 * 2 * 16 * kOutPitch * 4) +
-           (MODE == kModeHead ? HeadStage<TH>::BYTES : dma ? DmaStage<CIN, K, MODE, TH>::BYTES : 0);
+    return MfCfg<CIN, K, TH>::LDS_IN + (EPI == kEpiTail ? 0 : kTrBytes) +
+           (MODE == kModeHead ? StageOf<CIN, K, MODE, TH, false>::BYTES : dma ? DmaStage<CIN, K, MODE, TH>::BYTES : 0);
 }
 template <int CIN, int K, int MODE, int EPI, int TH, bool VEC, bool DMA>
 __global__ __launch_bounds__(kMfThreads) __attribute__((amdgpu_waves_per_eu(mf_waves<MODE, DMA>(), mf_waves<MODE, DMA>()))) void fwd_mfma(LayerDev d, float* __restrict__ y, float* __restrict__ yc,
@@ -461,7 +622,7 @@ __global__ __launch_bounds__(kMfThreads) __attribute__((amdgpu_waves_per_eu(mf_w
     using Stage = StageOf<CIN, K, MODE, TH, DMA>;
     // input planes, (non-tail) four waves' output-transpose regions (y and cout), DMA staging
     __shared__ __attribute__((aligned(16))) unsigned char lds[mf_lds_bytes<CIN, K, MODE, EPI, TH>(DMA)];
-    unsigned char* const stage = lds + MfCfg<CIN, K, TH>::LDS_IN + (EPI == kEpiTail ? 0 : 4 * 2 * 16 * kOutPitch * 4);
+    unsigned char* const stage = lds + MfCfg<CIN, K, TH>::LDS_IN + (EPI == kEpiTail ? 0 : kTrBytes);
     const nconv_layer& L = d.L;
 #ifdef NCONV_MF_WAVE_VGPR
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -475,7 +636,10 @@ __global__ __launch_bounds__(kMfThreads) __attribute__((amdgpu_waves_per_eu(mf_w
     const int off = tail ? t.off : 0;
 
     Stage st;
-    if constexpr (MODE == kModeHead) st.init(t, stage, threadIdx.x);
+    if constexpr (MODE == kModeHead) {
+        st.init(t, stage, threadIdx.x);
+        __syncthreads();  // (init's LDS writes before any thread's first staging writes)
+    }
     int v = blockIdx.x;
     // The block's tiles: virtual ids v, v + gridDim.x, ... map (xcd_tile) to linear tiles t, t + G8,
     // ... (G8 = gridDim.x / 8), so after one mapping the walk advances (tx, ty, b) by a fixed
@@ -569,6 +733,38 @@ __global__ __launch_bounds__(kMfThreads) __attribute__((amdgpu_waves_per_eu(mf_w
 #endif
             };
 
+            // both column halves, k-step outer: each k-step's 8 A-fragment reads are in flight
+            // together and feed 12 independent MFMAs (two accumulator pairs), which hides the LDS
+            // latency that one half's 6 dependent MFMAs per k-step leave exposed
+            auto mma2 = [&](f4_ (&n)[2], f4_ (&dd)[2]) {
+#pragma unroll
+                for (int ct = 0; ct < 2; ++ct) {
+                    n[ct] = (f4_){0.f, 0.f, 0.f, 0.f};
+                    dd[ct] = (f4_){0.f, 0.f, 0.f, 0.f};
+                }
+#pragma unroll
+                for (int q = 0; q < C::NT; ++q) {
+                    bf16x8 a[2][4];
+#pragma unroll
+                    for (int ct = 0; ct < 2; ++ct) {
+                        const unsigned char* p = lds + (2 * rp * C::IW + 16 * ct) * 16 + aoff[q];
+#pragma unroll
+                        for (int part = 0; part < 4; ++part)
+                            a[ct][part] = *reinterpret_cast<const bf16x8*>(p + part * C::PSTRIDE);
+                    }
+#pragma unroll
+                    for (int ct = 0; ct < 2; ++ct) {
+                        n[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ct][1], bh[q], n[ct], 0, 0, 0);
+                        dd[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ct][3], bh[q], dd[ct], 0, 0, 0);
+                        n[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ct][0], bl[q], n[ct], 0, 0, 0);
+                        dd[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ct][2], bl[q], dd[ct], 0, 0, 0);
+                        n[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ct][0], bh[q], n[ct], 0, 0, 0);
+                        dd[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ct][2], bh[q], dd[ct], 0, 0, 0);
+                    }
+                }
+            };
+            (void)mma2;
+
             // ---- epilogue: this lane holds (o, row oh, columns 16 ct + 4 h .. +3) per half ct ----
             // Every global store is an unconditional buffer store; lanes with nothing to write carry
             // an offset past the resource (dropped by the hardware). The number of stores per tile is
@@ -576,6 +772,7 @@ __global__ __launch_bounds__(kMfThreads) __attribute__((amdgpu_waves_per_eu(mf_w
             // also wait for the stores to complete.
             if constexpr (EPI != kEpiTail) {
                 float yv[2][4], cv[2][4];
+#ifdef NCONV_MF_CT_SEQ
 #pragma unroll
                 for (int ct = 0; ct < 2; ++ct) {
                     f4_ accN, accD;
@@ -586,26 +783,43 @@ __global__ __launch_bounds__(kMfThreads) __attribute__((amdgpu_waves_per_eu(mf_w
                         cv[ct][r] = accD[r] * rcp_s;
                     }
                 }
+#else
+                {
+                    f4_ accN[2], accD[2];
+                    mma2(accN, accD);
+#pragma unroll
+                    for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            yv[ct][r] = accN[ct][r] * __builtin_amdgcn_rcpf(accD[ct][r] + eps) + bo;
+                            cv[ct][r] = accD[ct][r] * rcp_s;
+                        }
+                }
+#endif
                 // Transpose the row pair through this wave's LDS region ([o + 8 s][32 columns], pitch
                 // 36 floats: conflict-free f4 writes), so that each global store instruction writes
                 // eight whole 128-byte rows (lane: channel l>>3, columns 4 (l&7) .. +3) instead of
                 // sixteen 64-byte pieces.
-                float* wy = reinterpret_cast<float*>(lds + C::LDS_IN) + wave * (2 * 16 * kOutPitch);
-                float* wc = wy + 16 * kOutPitch;
-#pragma unroll
-                for (int ct = 0; ct < 2; ++ct) {
-                    const int lo = (o + 8 * s) * kOutPitch + 16 * ct + 4 * h;
-                    *reinterpret_cast<f4*>(wy + lo) = (f4){yv[ct][0], yv[ct][1], yv[ct][2], yv[ct][3]};
-                    *reinterpret_cast<f4*>(wc + lo) = (f4){cv[ct][0], cv[ct][1], cv[ct][2], cv[ct][3]};
-                }
-                __builtin_amdgcn_wave_barrier();  // DS operations of one wave execute in order
+                // (y, then cout, through the same region: DS operations of one wave execute in
+                // order, so the cout writes cannot overtake the y reads)
+                float* wt = reinterpret_cast<float*>(lds + C::LDS_IN) + wave * (16 * kOutPitch);
                 const int o8 = lane >> 3, qc = 4 * (lane & 7);
                 f4 ry[2], rcv[2];
 #pragma unroll
-                for (int i = 0; i < 2; ++i) {
-                    ry[i] = *reinterpret_cast<const f4*>(wy + (o8 + 8 * i) * kOutPitch + qc);
-                    rcv[i] = *reinterpret_cast<const f4*>(wc + (o8 + 8 * i) * kOutPitch + qc);
-                }
+                for (int ct = 0; ct < 2; ++ct)
+                    *reinterpret_cast<f4*>(wt + (o + 8 * s) * kOutPitch + 16 * ct + 4 * h) =
+                        (f4){yv[ct][0], yv[ct][1], yv[ct][2], yv[ct][3]};
+                __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                for (int i = 0; i < 2; ++i) ry[i] = *reinterpret_cast<const f4*>(wt + (o8 + 8 * i) * kOutPitch + qc);
+                __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                for (int ct = 0; ct < 2; ++ct)
+                    *reinterpret_cast<f4*>(wt + (o + 8 * s) * kOutPitch + 16 * ct + 4 * h) =
+                        (f4){cv[ct][0], cv[ct][1], cv[ct][2], cv[ct][3]};
+                __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                for (int i = 0; i < 2; ++i) rcv[i] = *reinterpret_cast<const f4*>(wt + (o8 + 8 * i) * kOutPitch + qc);
                 __builtin_amdgcn_wave_barrier();
                 const int row0 = oh0 + 2 * rp, col = ow0 + qc;
                 const unsigned obytes = (unsigned)(8 * L.Ho * L.Wo) * 4u;
@@ -666,7 +880,7 @@ __global__ __launch_bounds__(kMfThreads) __attribute__((amdgpu_waves_per_eu(mf_w
                 const bool wr = o == 0 && orow < t.out_h;
                 const unsigned rowoff = (unsigned)(orow * t.out_w) * 4u;
 #pragma unroll
-                for (int ct = 0; ct < 2; ++ct) {  // one column half at a time: fewer live registers
+                for (int ct = 0; ct < 2; ++ct) {
                     f4_ accN, accD;
                     mma(ct, accN, accD);
                     const int ow = ow0 + 16 * ct + 4 * h, ocol = C0 + 16 * ct + 4 * h;

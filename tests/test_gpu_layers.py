@@ -187,10 +187,11 @@ def test_fwd_pooled_outputs(nconv_amd, gpu, shape):
 
 @pytest.mark.parametrize("shape", [(2, 48, 128), (1, 37, 70), (1, 352, 1216)])
 def test_fwd_head_matches_unfused(nconv_amd, gpu, shape):
-    """nconv_fwd_head (nconv1 evaluated inside nconv2's staging) against nconv1 and nconv2 as two
-    launches: nconv1 is the same exact-fp32 arithmetic (its sums may round differently by an ulp),
-    so nconv2's outputs and pooled copies agree to 1e-5 relative; the pooled copies must be torch's
-    max_pool2d of the fused outputs exactly."""
+    """nconv_fwd_head (nconv1 evaluated inside nconv2's staging, on the matrix cores in the same
+    split-bf16 arithmetic as nconv2) against nconv1 (exact fp32) and nconv2 as two launches: the
+    two differ by nconv1's split-product rounding (<= ~1.1e-5 relative per product), so nconv2's
+    outputs and pooled copies agree within the forward tolerance, 1e-4 relative; the pooled copies
+    must be torch's max_pool2d of the fused outputs exactly."""
     B, H, W = shape
     g = torch.Generator().manual_seed(H * W)
     S = (torch.rand(B, 1, H, W, generator=g) * 79 + 1) * (torch.rand(B, 1, H, W, generator=g) < 0.05)
@@ -208,6 +209,6 @@ def test_fwd_head_matches_unfused(nconv_amd, gpu, shape):
     y1, c1f, py1, pc1 = N.layer_forward_head(sp1, sp2, Sg, w1, b1, s1, w2, b2, s2)
     torch.cuda.synchronize()
     for got, ref in ((y1, y0), (c1f, c0), (py1, py0), (pc1, pc0)):
-        torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-5)
     assert torch.equal(py1, torch.nn.functional.max_pool2d(y1, 2, 2))
     assert torch.equal(pc1, torch.nn.functional.max_pool2d(c1f, 2, 2))
