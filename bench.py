@@ -161,18 +161,23 @@ def time_layers(m, net, S, reps=20):
 # Layers on the bf16x3 matrix-core kernel (fwd_mfma, include/nconv.h NCONV_MATH_BF16X3): output
 # rows per tile, k-steps (4 positions x 8 channels each) and the grid each launch writes.
 MFMA_LAYERS = {"nconv1+nconv2_head": (8, 8, 1), "nconv2": (8, 8, 1), "nconv_down1": (8, 8, 2), "nconv_down2": (8, 8, 4), "nconv_down3": (8, 8, 8),
-               "nconv4": (8, 6, 4), "nconv5": (8, 6, 2), "nconv6+7_tail": (8, 6, 1)}
+               "nconv4": (8, 6, 4), "nconv5": (8, 6, 2), "nconv6+7_tail": (16, 6, 1)}
+# the fused head's nconv1, also on the matrix cores: per tile 3 row groups x 3 column blocks x
+# 2 row pairs x 2 k-steps x 5 MFMAs (3 split products for N, 2 for D: c0 is exact)
+HEAD_NC1_MFMAS_PER_TILE = 3 * 3 * 2 * 2 * 5
 
 
 def mfma_issued_flops(layer, B, H, W):
-    """bf16 MFMA flops one fwd_mfma launch issues: per 8x32-pixel tile, 4 row pairs x 2 column
-    halves x NT k-steps x 6 v_mfma_f32_16x16x32_bf16 (3 split products x {N, D}) of 16384 flops."""
+    """bf16 MFMA flops one fwd_mfma launch issues: per TH x 32-pixel tile, TH/2 row pairs x 2 column
+    halves x NT k-steps x 6 v_mfma_f32_16x16x32_bf16 (3 split products x {N, D}) of 16384 flops,
+    plus the fused head's nconv1 MFMAs."""
     if layer not in MFMA_LAYERS:
         return None
     th, nt, div = MFMA_LAYERS[layer]
     h, w = H // div, W // div
     tiles = -(-h // th) * -(-w // 32) * B
-    return tiles * (th // 2) * 2 * nt * 6 * 16384
+    extra = HEAD_NC1_MFMAS_PER_TILE if layer == "nconv1+nconv2_head" else 0
+    return tiles * ((th // 2) * 2 * nt * 6 + extra) * 16384
 
 
 def pmc_traffic(kernel, B, H, W):

@@ -588,6 +588,12 @@ struct HeadStageMf {
 #ifndef NCONV_MF_TH5
 #define NCONV_MF_TH5 8  // output rows per tile of the 5x5 layers
 #endif
+#ifndef NCONV_MF_TH_TAIL
+// output rows per tile of the fused nconv6+7 tail: 16 (two row pairs per wave; its LDS, without
+// the epilogue transposes, still fits two workgroups per CU): 151 vs 162 us at B=8 352x1216.
+// (nconv4/5 keep 8: at 16 their LDS admits one workgroup per CU, 50 vs 44 us.)
+#define NCONV_MF_TH_TAIL 16
+#endif
 #ifndef NCONV_MFMA_WAVES
 #define NCONV_MFMA_WAVES 3  // waves per SIMD: 168 VGPRs (3 workgroups per CU) without spilling
 #endif
@@ -689,19 +695,16 @@ __global__ __launch_bounds__(kMfThreads) __attribute__((amdgpu_waves_per_eu(mf_w
     const float eps = L.eps, bo = L.bias[o];
     const float rcp_s = __builtin_amdgcn_rcpf(L.wsum[o]);
 
-#pragma unroll 1
-    for (; v < ntiles; v += gridDim.x) {
-        TileCoord tc_next;
+    // One tile: form its planes from the registers of `cur` (loaded one tile earlier), then
+    // reload `cur` with tile `tn`, whose loads fly during this tile's MFMAs and epilogue. (A
+    // second register stage, two tiles of cover, measured slower: 221 vs 166 us for the tail.)
+    auto body = [&](Stage& cur, const TileCoord tc, const TileCoord tn) {
         const int b = tc.b;
         const int R0 = tc.ty * TH, C0 = tc.tx * C::TW;  // tile origin in the written grid
         const int oh0 = R0 + off, ow0 = C0 + off;         // ... in this layer's output grid
-        st.to_planes(d, t, oh0 - L.PH, ow0 - L.PW, lds, stage, tid);
+        cur.to_planes(d, t, oh0 - L.PH, ow0 - L.PW, lds, stage, tid);
         __syncthreads();
-        {  // next tile's loads fly during this tile's MFMAs (the last tile re-loads itself)
-            const TileCoord tn = v + (int)gridDim.x < ntiles ? advance(tc) : tc;
-            st.issue(d, t, tn.b, tn.ty * TH + off - L.PH, tn.tx * C::TW + off - L.PW, stage, tid);
-            tc_next = tn;
-        }
+        cur.issue(d, t, tn.b, tn.ty * TH + off - L.PH, tn.tx * C::TW + off - L.PW, stage, tid);
 
         // ---- MFMAs: wave w takes the row pairs rp = w, w+4, ..., both 16-column halves ct ----
         typedef float f4_ __attribute__((ext_vector_type(4)));
@@ -921,7 +924,14 @@ __global__ __launch_bounds__(kMfThreads) __attribute__((amdgpu_waves_per_eu(mf_w
         // every wave is done reading the planes before the next tile's are formed (DmaStage's own
         // barrier, after its wait, does this there; a __syncthreads here would drain the DMA)
         if constexpr (!Stage::SELF_SYNC) __syncthreads();
-        tc = tc_next;
+    };
+
+    const int G = (int)gridDim.x;
+#pragma unroll 1
+    for (; v < ntiles; v += G) {
+        const TileCoord tn = v + G < ntiles ? advance(tc) : tc;  // (the last tile re-loads itself)
+        body(st, tc, tn);
+        tc = tn;
     }
 }
 
@@ -1031,7 +1041,7 @@ bool launch_fwd_mfma(const LayerDev& d, float* y, float* yc, const TailArgs& t, 
         }
         if (L.load_mode == NCONV_LOAD_UPCAT_UP_FIRST) {
             if (tail)
-                go_mfma_any<16, 3, NCONV_LOAD_UPCAT_UP_FIRST, kEpiTail, 8>(d, y, nullptr, t, gh, gw, st);
+                go_mfma_any<16, 3, NCONV_LOAD_UPCAT_UP_FIRST, kEpiTail, NCONV_MF_TH_TAIL>(d, y, nullptr, t, gh, gw, st);
             else
                 go_mfma_any<16, 3, NCONV_LOAD_UPCAT_UP_FIRST, kEpiPlain, 8>(d, y, yc, t, gh, gw, st);
             return true;
