@@ -1,0 +1,199 @@
+// loss.hip — the training loss of the reference (utils.py:95-151 calculate_loss) as three kernels.
+//
+//   rec  = masked_fill(r, t == 0, 0)                                    utils.py:139
+//   e    = rec - t,  diff = t - rec
+//   gx   = conv2d(diff, [[1,0,-1],[2,0,-2],[1,0,-1]], padding=1)         utils.py:95-106
+//   gy   = conv2d(diff, [[1,2,1],[0,0,0],[-1,-2,-1]], padding=1)         utils.py:109-122
+//   L    = 0.8 sqrt(mean e^2) + 0.2 (mean|gx| + mean|gy|)   (gradient loss), else mean e^2
+//
+// On one (H, W) plane (the reference evaluates it on element [0] of the batch). In PyTorch this is
+// ~45 elementwise / reduction launches forward and backward; here:
+//   loss_partials  one thread per pixel: e^2, |gx|, |gy| (3x3 window of diff, the same operation
+//                  order as train.gradient_x / _y, so signs match torch exactly), per-block sums
+//   loss_finalize  one block: fixed-order (double) sum of the block partials -> L and the two
+//                  backward coefficients, kept in the workspace for the backward
+//   loss_grad      one thread per pixel: dL/dr = go m [c_e e - c_g sum_q (sign gx(q) Kx(p - q) +
+//                  sign gy(q) Ky(p - q))] over the 3x3 neighbours q inside the plane (5x5 diff
+//                  window), with torch's sign(0) = 0 for |.|'.
+// Deterministic (no atomics). The planes may be row-strided views (the cropped DNET output).
+#include "nconv_internal.h"
+
+namespace nconv {
+
+constexpr int kLT = 256;
+
+struct LossPlane {
+    const float* r;
+    const float* t;
+    long long rs, ts;  // row strides (elements)
+    int H, W;
+};
+
+__device__ __forceinline__ float loss_diff(const LossPlane& p, int i, int j) {
+    // diff = t - masked_fill(r, t == 0, 0); zero outside the plane (conv padding)
+    if ((unsigned)i >= (unsigned)p.H || (unsigned)j >= (unsigned)p.W) return 0.f;
+    const float t = p.t[i * p.ts + j];
+    const float rec = t == 0.f ? 0.f : p.r[i * p.rs + j];
+    return t - rec;
+}
+
+// gradient_x at (i, j) from a diff window accessor, in train.gradient_x's order
+template <typename D>
+__device__ __forceinline__ float sobel_x(D d, int i, int j) {
+    const float a = d(i - 1, j - 1) - d(i - 1, j + 1);
+    const float b = d(i, j - 1) - d(i, j + 1);
+    const float c = d(i + 1, j - 1) - d(i + 1, j + 1);
+    return (a + 2.f * b) + c;
+}
+template <typename D>
+__device__ __forceinline__ float sobel_y(D d, int i, int j) {
+    const float a = d(i - 1, j - 1) - d(i + 1, j - 1);
+    const float b = d(i - 1, j) - d(i + 1, j);
+    const float c = d(i - 1, j + 1) - d(i + 1, j + 1);
+    return (a + 2.f * b) + c;
+}
+
+__device__ __forceinline__ float block_sum256(float v, float* red) {
+#pragma unroll
+    for (int s = 32; s > 0; s >>= 1) v += __shfl_xor(v, s);
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    __syncthreads();
+    if (lane == 0) red[w] = v;
+    __syncthreads();
+    return ((red[0] + red[1]) + red[2]) + red[3];
+}
+
+__global__ __launch_bounds__(kLT) void loss_partials(LossPlane p, int grad_loss, float* __restrict__ part) {
+    __shared__ float red[4];
+    const int n = p.H * p.W, e = blockIdx.x * kLT + threadIdx.x;
+    float sq = 0.f, ax = 0.f, ay = 0.f;
+    if (e < n) {
+        const int i = e / p.W, j = e - i * p.W;
+        const float dv = loss_diff(p, i, j);
+        sq = dv * dv;  // (rec - t)^2
+        if (grad_loss) {
+            auto d = [&](int a, int b) { return loss_diff(p, a, b); };
+            ax = fabsf(sobel_x(d, i, j));
+            ay = fabsf(sobel_y(d, i, j));
+        }
+    }
+    sq = block_sum256(sq, red);
+    ax = block_sum256(ax, red);
+    ay = block_sum256(ay, red);
+    if (threadIdx.x == 0) {
+        part[3 * blockIdx.x] = sq;
+        part[3 * blockIdx.x + 1] = ax;
+        part[3 * blockIdx.x + 2] = ay;
+    }
+}
+
+// coef[0] = L, coef[1] = dL/d(e^2 sum) factor c_e (dL/de = c_e e), coef[2] = c_g (0.2 / n)
+__global__ __launch_bounds__(kLT) void loss_finalize(const float* __restrict__ part, int nblk, int n, int grad_loss,
+                                                      float* __restrict__ loss, float* __restrict__ coef) {
+    __shared__ double red[3][kLT];
+    double s[3] = {0.0, 0.0, 0.0};
+    for (int b = threadIdx.x; b < nblk; b += kLT)
+        for (int k = 0; k < 3; ++k) s[k] += part[3 * b + k];
+    for (int k = 0; k < 3; ++k) red[k][threadIdx.x] = s[k];
+    __syncthreads();
+    for (int w = kLT / 2; w > 0; w >>= 1) {
+        if (threadIdx.x < w)
+            for (int k = 0; k < 3; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const float mse = (float)(red[0][0] / n);
+        float L, ce, cg;
+        if (grad_loss) {
+            const float rmse = sqrtf(mse);
+            L = rmse * 0.8f + ((float)(red[1][0] / n) + (float)(red[2][0] / n)) * 0.2f;
+            ce = 0.8f / (n * rmse);  // d(0.8 sqrt(sum e^2 / n)) / de
+            cg = 0.2f / n;
+        } else {
+            L = mse;
+            ce = 2.f / n;
+            cg = 0.f;
+        }
+        loss[0] = L;
+        coef[0] = L;
+        coef[1] = ce;
+        coef[2] = cg;
+    }
+}
+
+__device__ __forceinline__ float sgnf(float v) { return v > 0.f ? 1.f : (v < 0.f ? -1.f : 0.f); }
+
+__global__ __launch_bounds__(kLT) void loss_grad(LossPlane p, int grad_loss, const float* __restrict__ coef,
+                                                  const float* __restrict__ gout, float* __restrict__ g) {
+    const int n = p.H * p.W, e = blockIdx.x * kLT + threadIdx.x;
+    if (e >= n) return;
+    const int i = e / p.W, j = e - i * p.W;
+    const float t = p.t[i * p.ts + j];
+    if (t == 0.f) {  // masked_fill: no gradient reaches r here
+        g[e] = 0.f;
+        return;
+    }
+    const float go = gout ? gout[0] : 1.f;
+    float dw[5][5];  // diff(i - 2 .. i + 2, j - 2 .. j + 2)
+#pragma unroll
+    for (int a = 0; a < 5; ++a)
+#pragma unroll
+        for (int b = 0; b < 5; ++b) dw[a][b] = loss_diff(p, i + a - 2, j + b - 2);
+    // dL/drec = c_e e - c_g G,  e = rec - t = -diff(p)
+    float acc = coef[1] * (-dw[2][2]);
+    if (grad_loss) {
+        float G = 0.f;
+#pragma unroll
+        for (int qa = -1; qa <= 1; ++qa)
+#pragma unroll
+            for (int qb = -1; qb <= 1; ++qb) {
+                const int qi = i + qa, qj = j + qb;
+                if ((unsigned)qi >= (unsigned)p.H || (unsigned)qj >= (unsigned)p.W) continue;
+                // window accessor centred on q (local coordinates of dw)
+                auto d = [&](int a, int b) { return dw[a - i + 2][b - j + 2]; };
+                const float sx = sgnf(sobel_x(d, qi, qj)), sy = sgnf(sobel_y(d, qi, qj));
+                // Kx(dy, dx) = w(dy) (-dx), Ky(dy, dx) = w(dx) (-dy), (dy, dx) = p - q, w = 1, 2, 1
+                const int dy = -qa, dx = -qb;
+                const float wy = dy == 0 ? 2.f : 1.f, wx = dx == 0 ? 2.f : 1.f;
+                G += sx * wy * (float)(-dx) + sy * wx * (float)(-dy);
+            }
+        // d|gx|/drec = -(d|gx|/ddiff)
+        acc -= coef[2] * G;
+    }
+    g[e] = go * acc;
+}
+
+size_t loss_workspace_bytes(int H, int W) {
+    const size_t nblk = ((size_t)H * W + kLT - 1) / kLT;
+    return (3 * nblk + 4) * sizeof(float);
+}
+
+static int loss_err(const char** why) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        *why = hipGetErrorString(e);
+        return -5;
+    }
+    return 0;
+}
+
+int launch_loss_fwd(const float* r, long long rs, const float* t, long long ts, int H, int W, int grad_loss,
+                    float* loss, float* ws, hipStream_t st, const char** why) {
+    const LossPlane p{r, t, rs, ts, H, W};
+    const int n = H * W, nblk = (n + kLT - 1) / kLT;
+    float* coef = ws;
+    float* part = ws + 4;
+    hipLaunchKernelGGL(loss_partials, dim3(nblk), dim3(kLT), 0, st, p, grad_loss, part);
+    hipLaunchKernelGGL(loss_finalize, dim3(1), dim3(kLT), 0, st, part, nblk, n, grad_loss, loss, coef);
+    return loss_err(why);
+}
+
+int launch_loss_bwd(const float* r, long long rs, const float* t, long long ts, int H, int W, int grad_loss,
+                    const float* gout, const float* ws, float* g, hipStream_t st, const char** why) {
+    const LossPlane p{r, t, rs, ts, H, W};
+    const int n = H * W, nblk = (n + kLT - 1) / kLT;
+    hipLaunchKernelGGL(loss_grad, dim3(nblk), dim3(kLT), 0, st, p, grad_loss, ws, gout, g);
+    return loss_err(why);
+}
+
+}  // namespace nconv

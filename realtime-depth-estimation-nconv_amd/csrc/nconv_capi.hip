@@ -334,4 +334,45 @@ int nconv_conv3x3_c1(const float* x, int B, int Cin, int H, int W, const float* 
     return rc ? fail(rc, fn, why) : 0;
 }
 
+size_t nconv_depth_loss_workspace_bytes(int H, int W) {
+    if (H <= 0 || W <= 0 || (long long)H * W > (1LL << 30)) return 0;
+    return nconv::loss_workspace_bytes(H, W);
+}
+
+static const char* validate_loss(const float* r, long long rs, const float* t, long long ts, int H, int W,
+                                 size_t ws_bytes, const void* ws) {
+    if (!r || !t) return "null plane";
+    if (H <= 0 || W <= 0) return "non-positive H/W";
+    if ((long long)H * W > (1LL << 30)) return "plane too large";
+    if (rs < W || ts < W) return "row stride smaller than W";
+    if (!ws || ws_bytes < nconv::loss_workspace_bytes(H, W)) return "workspace too small";
+    return nullptr;
+}
+
+int nconv_depth_loss_fwd(const float* r, long long r_row_stride, const float* t, long long t_row_stride, int H,
+                         int W, int use_gradient_loss, float* loss, void* workspace, size_t workspace_bytes,
+                         void* stream) {
+    const char* fn = "nconv_depth_loss_fwd";
+    if (const char* why = validate_loss(r, r_row_stride, t, t_row_stride, H, W, workspace_bytes, workspace))
+        return fail(-22, fn, why);
+    if (!loss) return fail(-22, fn, "null loss");
+    const char* why = nullptr;
+    int rc = nconv::launch_loss_fwd(r, r_row_stride, t, t_row_stride, H, W, use_gradient_loss != 0, loss,
+                                    (float*)workspace, (hipStream_t)stream, &why);
+    return rc ? fail(rc, fn, why) : 0;
+}
+
+int nconv_depth_loss_bwd(const float* r, long long r_row_stride, const float* t, long long t_row_stride, int H,
+                         int W, int use_gradient_loss, const float* gloss, const void* workspace,
+                         size_t workspace_bytes, float* g, void* stream) {
+    const char* fn = "nconv_depth_loss_bwd";
+    if (const char* why = validate_loss(r, r_row_stride, t, t_row_stride, H, W, workspace_bytes, workspace))
+        return fail(-22, fn, why);
+    if (!g) return fail(-22, fn, "null g");
+    const char* why = nullptr;
+    int rc = nconv::launch_loss_bwd(r, r_row_stride, t, t_row_stride, H, W, use_gradient_loss != 0, gloss,
+                                    (const float*)workspace, g, (hipStream_t)stream, &why);
+    return rc ? fail(rc, fn, why) : 0;
+}
+
 }  // extern "C"

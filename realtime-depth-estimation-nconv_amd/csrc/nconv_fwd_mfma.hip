@@ -594,16 +594,23 @@ struct HeadStageMf {
 // (nconv4/5 keep 8: at 16 their LDS admits one workgroup per CU, 50 vs 44 us.)
 #define NCONV_MF_TH_TAIL 16
 #endif
+#ifndef NCONV_MF_TH_HEAD
+#define NCONV_MF_TH_HEAD 8  // output rows per tile of the fused nconv1+nconv2 head
+#endif
 #ifndef NCONV_MFMA_WAVES
 #define NCONV_MFMA_WAVES 3  // waves per SIMD: 168 VGPRs (3 workgroups per CU) without spilling
 #endif
 // POOL2 staging holds four values per element before pooling: 2 waves per SIMD (no spills)
+#ifndef NCONV_MFMA_HEAD_WAVES
+#define NCONV_MFMA_HEAD_WAVES 3  // fused head
+#endif
 #ifndef NCONV_MFMA_UP_WAVES
 #define NCONV_MFMA_UP_WAVES 2  // the 16-channel upsample-concat layers (nconv4/5/6): no spills
 #endif
 template <int MODE, bool DMA>
 constexpr int mf_waves() {
-    return DMA || MODE == NCONV_LOAD_POOL2 ? 2
+    return MODE == kModeHead ? NCONV_MFMA_HEAD_WAVES
+           : DMA || MODE == NCONV_LOAD_POOL2 ? 2
            : (MODE == NCONV_LOAD_UPCAT_SKIP_FIRST || MODE == NCONV_LOAD_UPCAT_UP_FIRST) ? NCONV_MFMA_UP_WAVES
                                                                                          : NCONV_MFMA_WAVES;
 }
@@ -1000,7 +1007,7 @@ void go_mfma_any(const LayerDev& d, float* y, float* yc, const TailArgs& t, int 
 int launch_fwd_head(const LayerDev& d2, const TailArgs& t, float* y, float* yc, hipStream_t st, const char** why) {
     // (16-row tiles recompute less of nconv1's halo but fit two workgroups per CU instead of three:
     // 228 vs 215 us at B=8 352x1216)
-    go_mfma<8, 5, kModeHead, kEpiPool, 8, false>(d2, y, yc, t, d2.L.Ho, d2.L.Wo, st);
+    go_mfma<8, 5, kModeHead, kEpiPool, NCONV_MF_TH_HEAD, false>(d2, y, yc, t, d2.L.Ho, d2.L.Wo, st);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         *why = hipGetErrorString(e);

@@ -1,7 +1,8 @@
 """Training-step glue of the reference (utils.py), on device: losses, optimizer factory, checkpoints.
 
-These are cheap elementwise/reduction ops around the NConv path; they run as PyTorch-ROCm ops.
-  calculate_loss                    utils.py:138-151   masked RMSE*0.8 + Sobel-gradient*0.2 (or MSE)
+Cheap elementwise/reduction glue around the NConv path (PyTorch-ROCm ops), except the loss itself.
+  calculate_loss                    utils.py:138-151   masked RMSE*0.8 + Sobel-gradient*0.2 (or MSE);
+                                    on device planes the fused libnconv kernels (DepthLossFn)
   gradient_loss / gradient_x / _y   utils.py:95-136
   calculate_loss_multi_resolution   utils.py:63-71     each scale bilinear-resized to 480x640, [0] only
   get_optimizer                     utils.py:53-61     AdamW / SGD / RMSprop
@@ -43,11 +44,60 @@ def gradient_loss(input_img, predicted_img):
     return torch.abs(gradient_x(diff)).mean() + torch.abs(gradient_y(diff)).mean()
 
 
-def calculate_loss(reconstructed_img, target_img, use_gradient_loss):
+def _calculate_loss_torch(reconstructed_img, target_img, use_gradient_loss):
     rec = reconstructed_img.masked_fill(target_img == 0, 0)
     if use_gradient_loss:
         return torch.sqrt(F.mse_loss(rec, target_img)) * 0.8 + gradient_loss(target_img, rec) * 0.2
     return F.mse_loss(rec, target_img)
+
+
+class DepthLossFn(torch.autograd.Function):
+    """calculate_loss (utils.py:138-151) on one (1, H, W) / (H, W) plane as libnconv kernels
+    (nconv_depth_loss_fwd / _bwd: 2 launches forward, 1 backward, instead of ~45 PyTorch ops)."""
+
+    @staticmethod
+    def forward(ctx, r, t, use_gradient_loss):
+        from . import _lib
+        H, W = r.shape[-2], r.shape[-1]
+        lib = _lib.lib()
+        nbytes = lib.nconv_depth_loss_workspace_bytes(H, W)
+        ws = torch.empty(max(nbytes, 4), dtype=torch.uint8, device=r.device)
+        loss = torch.empty((), dtype=torch.float32, device=r.device)
+        rc = lib.nconv_depth_loss_fwd(_lib.ptr(r), r.stride(-2), _lib.ptr(t), t.stride(-2), H, W,
+                                      int(bool(use_gradient_loss)), _lib.ptr(loss), _lib.ptr(ws), nbytes,
+                                      _lib.stream_handle(r.device))
+        _lib.check(rc, "nconv_depth_loss_fwd")
+        ctx.use_gradient_loss = bool(use_gradient_loss)
+        ctx.save_for_backward(r, t, ws)
+        return loss
+
+    @staticmethod
+    def backward(ctx, gloss):
+        from . import _lib
+        r, t, ws = ctx.saved_tensors
+        H, W = r.shape[-2], r.shape[-1]
+        g = torch.empty(r.shape, dtype=torch.float32, device=r.device)
+        gloss = gloss.contiguous()
+        rc = _lib.lib().nconv_depth_loss_bwd(_lib.ptr(r), r.stride(-2), _lib.ptr(t), t.stride(-2), H, W,
+                                             int(ctx.use_gradient_loss), _lib.ptr(gloss), _lib.ptr(ws),
+                                             ws.numel(), _lib.ptr(g), _lib.stream_handle(r.device))
+        _lib.check(rc, "nconv_depth_loss_bwd")
+        return g, None, None
+
+
+def _fused_loss_ok(r, t):
+    def plane(x):
+        return (x.is_cuda and x.dtype == torch.float32 and x.dim() in (2, 3) and (x.dim() == 2 or x.shape[0] == 1)
+                and x.stride(-1) == 1 and x.stride(-2) >= x.shape[-1])
+    return plane(r) and plane(t) and r.shape == t.shape and not t.requires_grad and r.device == t.device
+
+
+def calculate_loss(reconstructed_img, target_img, use_gradient_loss):
+    """utils.py:138-151. Device planes run the fused libnconv loss (DepthLossFn); anything else
+    (CPU tensors, several channels) the PyTorch ops of the reference."""
+    if _fused_loss_ok(reconstructed_img, target_img):
+        return DepthLossFn.apply(reconstructed_img, target_img, use_gradient_loss)
+    return _calculate_loss_torch(reconstructed_img, target_img, use_gradient_loss)
 
 
 def calculate_loss_multi_resolution(reconstructed_img, target_img, use_gradient_loss):

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """One NConv layer forward, repeated (developer tool for rocprofv3 / counter passes, GPU):
-python3 tools/fwd_layer_bench.py [nconv2|tail|down1|nconv5] [reps] -> us per launch."""
+python3 tools/fwd_layer_bench.py [nconv2|head|tail|down1|down2|down3|nconv4|nconv5] [reps] -> us per launch."""
 import os
 import sys
 
@@ -36,13 +36,15 @@ def main():
         sp1 = m.LayerSpec(1, 8, (5, 5), (1, 1), (2, 2), mode=m._lib.THRESH)
         spec = m.LayerSpec(8, 8, (5, 5), (1, 1), (2, 2))
         fn = lambda: N.layer_forward_head(sp1, spec, S, w1, b, s1, w8, b, s8)
-    elif which == "down1":
-        x, c = r(B, 8, H // 2, W // 2) * 10, r(B, 8, H // 2, W // 2)
+    elif which in ("down1", "down2", "down3"):
+        f = {"down1": 2, "down2": 4, "down3": 8}[which]
+        x, c = r(B, 8, H // f, W // f) * 10, r(B, 8, H // f, W // f)
         spec = m.LayerSpec(8, 8, (5, 5), (1, 1), (2, 2))
         fn = lambda: N.layer_forward_pooled(spec, x, c, None, None, w8, b, s8)
-    elif which == "nconv5":
-        xa, ca = r(B, 8, H // 2, W // 2) * 10, r(B, 8, H // 2, W // 2)
-        xb, cb = r(B, 8, H // 4, W // 4) * 10, r(B, 8, H // 4, W // 4)
+    elif which in ("nconv5", "nconv4"):
+        f = 2 if which == "nconv5" else 4
+        xa, ca = r(B, 8, H // f, W // f) * 10, r(B, 8, H // f, W // f)
+        xb, cb = r(B, 8, H // (2 * f), W // (2 * f)) * 10, r(B, 8, H // (2 * f), W // (2 * f))
         spec = m.LayerSpec(16, 8, (3, 3), (1, 1), (1, 1), mode=m._lib.UPCAT_SKIP_FIRST)
         fn = lambda: N.layer_forward_raw(spec, xa, ca, xb, cb, w16, b, s16)
     else:  # nconv6 + nconv7 tail
