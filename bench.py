@@ -320,7 +320,7 @@ def make_train_step(m, dev, B, H, W, world, rank, graph=True):
     graph=True replays the whole iteration from a hipGraph (m.train.GraphedTrainStep)."""
     torch.manual_seed(0)
     net = m.dp.DataParallelRCCL(m.SETP1_NCONV(crop="generalized").to(dev))
-    opt = m.train.get_optimizer(net, "adam", 1e-2, 1e-7, capturable=graph)
+    opt = m.train.get_optimizer(net, "adam", 1e-2, 1e-7, capturable=graph, fused=graph)
     g = torch.Generator().manual_seed(2000 + rank)
     S = sparse_depth(g, B, H, W, dev)
     gt = sparse_depth(g, B, H, W, dev)

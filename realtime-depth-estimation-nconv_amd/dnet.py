@@ -20,11 +20,83 @@ import torch
 import torch.nn as nn
 
 from . import _lib, nconv
-from .nconv import (EnforcePos, NConv2d, _require_device, layer_forward_head, layer_forward_pooled,
-                    layer_forward_raw, nconv_layer, weight_prep)
+from .nconv import (EnforcePos, NConv2d, _require_device, layer_backward, layer_forward_head,
+                    layer_forward_pooled, layer_forward_raw, nconv_layer, weight_prep)
 
 LAYERS = ("nconv1", "nconv2", "nconv_down1", "nconv_down2", "nconv_down3", "nconv4", "nconv5",
           "nconv6", "nconv7")
+
+
+class DNETFn(torch.autograd.Function):
+    """Autograd node of the whole 9-layer DNET graph (training path). The backward runs the layer
+    backwards in reverse order itself, so that the gradients of the three tensors two layers read
+    (nconv2's output: down1 and nconv6; down1's: down2 and nconv5; down2's: down3 and nconv4) are
+    summed inside the second consumer's dgrad kernel (NCONV_BWD_ACCUMULATE) instead of by separate
+    PyTorch adds over freshly allocated buffers. Inputs: specs, capture (dict or None), S, then
+    (weight, bias, s[o]) of each layer in LAYERS order; outputs: nconv7's (uncropped) y, cout."""
+
+    @staticmethod
+    def forward(ctx, specs, capture, S, *p):
+        W = [p[3 * i:3 * i + 3] for i in range(9)]
+        sp = specs
+        x1, c1 = layer_forward_raw(sp[0], S, None, None, None, *W[0])
+        x2, c2 = layer_forward_raw(sp[1], x1, c1, None, None, *W[1])
+        x3, c3 = layer_forward_raw(sp[2], x2, c2, None, None, *W[2])
+        x4, c4 = layer_forward_raw(sp[3], x3, c3, None, None, *W[3])
+        x5, c5 = layer_forward_raw(sp[4], x4, c4, None, None, *W[4])
+        x6, c6 = layer_forward_raw(sp[5], x4, c4, x5, c5, *W[5])
+        x7, c7 = layer_forward_raw(sp[6], x3, c3, x6, c6, *W[6])
+        x8, c8 = layer_forward_raw(sp[7], x2, c2, x7, c7, *W[7])
+        x9, c9 = layer_forward_raw(sp[8], x8, c8, None, None, *W[8])
+        if capture is not None:  # the three pooling stages' inputs (DNET.capture)
+            capture.update(down1=(x2.detach(), c2.detach()), down2=(x3.detach(), c3.detach()),
+                           down3=(x4.detach(), c4.detach()))
+        ctx.specs = specs
+        ctx.save_for_backward(S, *p, x1, c1, x2, c2, x3, c3, x4, c4, x5, c5, x6, c6, x7, c7, x8, c8, x9, c9)
+        ctx.mark_non_differentiable(c9)
+        return x9, c9
+
+    @staticmethod
+    def backward(ctx, g9, gc9):
+        sv = ctx.saved_tensors
+        S, p, acts = sv[0], sv[1:28], sv[28:]
+        W = [p[3 * i:3 * i + 3] for i in range(9)]
+        X = [None] + [(acts[2 * i], acts[2 * i + 1]) for i in range(9)]  # X[k] = output of layer k
+        need = ctx.needs_input_grad[1:]  # (capture, S, w1, b1, s1, ...)
+        gw = [torch.empty_like(W[i][0]) if need[2 + 3 * i] else None for i in range(9)]
+        gb = [torch.empty_like(W[i][1]) if need[3 + 3 * i] else None for i in range(9)]
+        e = torch.empty_like
+        # input gradients: G[k] = (gx, gc) of layer k's output
+        G = [None] * 10
+        sp = ctx.specs
+
+        def bwd(k, a, b, ga, gb_, acc=False):
+            xa, ca = X[a] if a else (S, None)
+            xb, cb = X[b] if b else (None, None)
+            gy, gco = G[k] if G[k] is not None else (g9, None)
+            layer_backward(sp[k - 1], (xa, ca, xb, cb, *W[k - 1]), X[k][0], X[k][1], gy, gco,
+                           (*(ga or (None, None)), *(gb_ or (None, None))), gw[k - 1], gb[k - 1], accumulate=acc)
+
+        G[8] = (e(X[8][0]), e(X[8][1]))
+        bwd(9, 8, 0, G[8], None)                        # nconv7
+        G[2], G[7] = (e(X[2][0]), e(X[2][1])), (e(X[7][0]), e(X[7][1]))
+        bwd(8, 2, 7, G[2], G[7])                        # nconv6: nconv2's output (overwrite) + up
+        G[3], G[6] = (e(X[3][0]), e(X[3][1])), (e(X[6][0]), e(X[6][1]))
+        bwd(7, 3, 6, G[3], G[6])                        # nconv5: down1's output + up
+        G[4], G[5] = (e(X[4][0]), e(X[4][1])), (e(X[5][0]), e(X[5][1]))
+        bwd(6, 4, 5, G[4], G[5])                        # nconv4: down2's output + up
+        bwd(5, 4, 0, G[4], None, acc=True)              # down3 adds into down2's output gradient
+        bwd(4, 3, 0, G[3], None, acc=True)              # down2 -> down1's
+        bwd(3, 2, 0, G[2], None, acc=True)              # down1 -> nconv2's
+        G[1] = (e(X[1][0]), e(X[1][1]))
+        bwd(2, 1, 0, G[1], None)                        # nconv2
+        gS = e(S) if need[1] else None
+        layer_backward(sp[0], (S, None, None, None, *W[0]), X[1][0], X[1][1], G[1][0], G[1][1],
+                       (gS, None, None, None), gw[0], gb[0])  # nconv1 (threshold: c0 has no gradient)
+        out = [None, None, gS]
+        for i in range(9):
+            out += [gw[i], gb[i], None]
+        return tuple(out)
 
 
 def crop_hw(H, W, crop):
@@ -60,6 +132,10 @@ class DNET(nn.Module):
         # Set to a dict to receive the (x, c) inputs of the three pooling stages on the next
         # forward (diagnostics / tests); None in normal use.
         self.capture = None
+
+    # Training path: one autograd node for the whole graph (DNETFn, gradients of shared tensors
+    # accumulated in-kernel); False: one node per layer (NConvLayerFn), for comparison.
+    whole_graph_autograd = True
 
     # -- hooks ----------------------------------------------------------------------------------
     def _prologue(self, layers, S):
@@ -104,6 +180,16 @@ class DNET(nn.Module):
             out = torch.empty((S.shape[0], 1, out_h, out_w), device=S.device, dtype=torch.float32)
             self._infer_split(S, layers, wsum, out)
             return out
+
+        if grad and self.whole_graph_autograd and S.shape[0] > 0:
+            specs = (l1.spec(_lib.THRESH, 0.01), l2.spec(), d1.spec(_lib.POOL2), d2.spec(_lib.POOL2),
+                     d3.spec(_lib.POOL2), l4.spec(_lib.UPCAT_SKIP_FIRST), l5.spec(_lib.UPCAT_SKIP_FIRST),
+                     l6.spec(_lib.UPCAT_UP_FIRST), l7.spec())
+            params = []
+            for m_, s_ in zip(layers, wsum):
+                params += [m_.weight, m_.bias, s_]
+            xo, _ = DNETFn.apply(specs, self.capture, S, *params)
+            return xo[:, :, 1:1 + out_h, 1:1 + out_w]
 
         x1, c1 = f(l1.spec(_lib.THRESH, 0.01), S, None, None, None, l1.weight, l1.bias, s1)
         x1, c1 = f(l2.spec(), x1, c1, None, None, l2.weight, l2.bias, s2)

@@ -153,25 +153,34 @@ class NConvLayerFn(torch.autograd.Function):
         spec = ctx.spec
         xa, ca, xb, cb, weight, bias, wsum, y, co = ctx.saved_tensors
         need = ctx.needs_input_grad  # (spec, xa, ca, xb, cb, weight, bias, wsum)
-        dev = y.device
-        if gy is None:
-            gy = torch.zeros_like(y)
-        gy = gy.contiguous()
-        gco = gco.contiguous() if gco is not None else None
         # the kernels overwrite every element of the input gradients (no zero-fill)
         z = lambda t, n: torch.empty_like(t) if (t is not None and n) else None
         gxa, gca, gxb, gcb = z(xa, need[1]), z(ca, need[2]), z(xb, need[3]), z(cb, need[4])
         gw = torch.empty_like(weight) if need[5] else None
         gb = torch.empty_like(bias) if need[6] else None
-        L = spec.descriptor(xa, ca, xb, cb, weight, bias, wsum)
-        lib = _lib.lib()
-        ws_bytes = lib.nconv_bwd_workspace_bytes(_lib.ctypes.byref(L))
-        ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
-        rc = lib.nconv_bwd(_lib.ctypes.byref(L), _lib.ptr(y), _lib.ptr(co), _lib.ptr(gy), _lib.ptr(gco),
-                           _lib.ptr(gxa), _lib.ptr(gca), _lib.ptr(gxb), _lib.ptr(gcb), _lib.ptr(gw),
-                           _lib.ptr(gb), _lib.ptr(ws), ws_bytes, 0, _lib.stream_handle(dev))
-        _lib.check(rc, "nconv_bwd")
+        layer_backward(spec, (xa, ca, xb, cb, weight, bias, wsum), y, co, gy, gco, (gxa, gca, gxb, gcb), gw, gb)
         return None, gxa, gca, gxb, gcb, gw, gb, None
+
+
+def layer_backward(spec: LayerSpec, inputs, y, co, gy, gco, gin, gw, gb, accumulate=False):
+    """nconv_bwd of one fused layer: gin = (gxa, gca, gxb, gcb) (None: skip) overwritten, or added
+    into with accumulate=True (NCONV_BWD_ACCUMULATE: a tensor consumed by two layers); gw, gb
+    overwritten (None: skip)."""
+    xa, ca, xb, cb, weight, bias, wsum = inputs
+    gxa, gca, gxb, gcb = gin
+    dev = y.device
+    if gy is None:
+        gy = torch.zeros_like(y)
+    gy = gy.contiguous()
+    gco = gco.contiguous() if gco is not None else None
+    L = spec.descriptor(xa, ca, xb, cb, weight, bias, wsum)
+    lib = _lib.lib()
+    ws_bytes = lib.nconv_bwd_workspace_bytes(_lib.ctypes.byref(L))
+    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+    rc = lib.nconv_bwd(_lib.ctypes.byref(L), _lib.ptr(y), _lib.ptr(co), _lib.ptr(gy), _lib.ptr(gco),
+                       _lib.ptr(gxa), _lib.ptr(gca), _lib.ptr(gxb), _lib.ptr(gcb), _lib.ptr(gw),
+                       _lib.ptr(gb), _lib.ptr(ws), ws_bytes, 1 if accumulate else 0, _lib.stream_handle(dev))
+    _lib.check(rc, "nconv_bwd")
 
 
 def nconv_layer(spec: LayerSpec, xa, ca, xb, cb, weight, bias, wsum):

@@ -60,6 +60,39 @@ def test_dnet_grad_path_matches_fused_tail(nconv_amd, gpu):
     torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-5)
 
 
+def _graph_has(fn, name, depth=6):
+    if fn is None or depth < 0:
+        return False
+    if name in type(fn).__name__:
+        return True
+    return any(_graph_has(f, name, depth - 1) for f, _ in fn.next_functions)
+
+
+@pytest.mark.parametrize("H,W", [(64, 96), (45, 67)])
+def test_whole_graph_autograd_matches_per_layer(nconv_amd, gpu, H, W):
+    """DNETFn (one autograd node, shared-tensor gradients accumulated in the dgrad kernels) against
+    one NConvLayerFn node per layer (PyTorch adds the two consumers' gradients): same kernels, so
+    outputs are bitwise equal and gradients agree to fp32 round-off of the accumulation (1e-6
+    relative per tensor); the input gradient of S too."""
+    g = torch.Generator().manual_seed(21)
+    S = sparse_depth(g, 2, H, W).to(gpu)
+    gt = (torch.rand(2, 1, H, W, generator=g) * 80).to(gpu)
+    res = []
+    for whole in (True, False):
+        net = make_net(nconv_amd, "generalized", gpu)
+        net.d_net.whole_graph_autograd = whole
+        x = S.clone().requires_grad_(True)
+        out = net(x)
+        assert _graph_has(out.grad_fn, "DNETFn") == whole
+        nconv_amd.train.calculate_loss(out[0], gt[0], True).backward()
+        res.append((out.detach(), x.grad, {k: v.grad for k, v in net.named_parameters() if v.grad is not None}))
+    (oa, ga, pa), (ob, gb, pb) = res
+    assert torch.equal(oa, ob)
+    assert set(pa) == set(pb) and len(pa) == 18
+    for a, b in [(ga, gb)] + [(pa[k], pb[k]) for k in pa]:
+        assert (a - b).abs().max().item() <= 1e-6 * b.abs().max().item() + 1e-30
+
+
 def test_enforcepos_drift(nconv_amd, gpu):
     """Training-mode forward applies softplus(beta=10) to every layer's weight, once per forward."""
     torch.manual_seed(0)

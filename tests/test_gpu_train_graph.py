@@ -9,11 +9,11 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _setup(nconv_amd, dev, capturable):
+def _setup(nconv_amd, dev, capturable, fused=False):
     torch.manual_seed(0)
     net = nconv_amd.SETP1_NCONV(crop="generalized").to(dev)
     net.train()
-    opt = nconv_amd.train.get_optimizer(net, "adam", 1e-2, 1e-7, capturable=capturable)
+    opt = nconv_amd.train.get_optimizer(net, "adam", 1e-2, 1e-7, capturable=capturable, fused=fused)
     return net, opt
 
 
@@ -23,14 +23,15 @@ def _loss(nconv_amd):
     return fn
 
 
-def test_graphed_train_step_matches_eager(nconv_amd, gpu):
+@pytest.mark.parametrize("fused", [False, True])
+def test_graphed_train_step_matches_eager(nconv_amd, gpu, fused):
     g = torch.Generator().manual_seed(5)
     S = ((torch.rand(2, 1, 64, 96, generator=g) * 79 + 1) * (torch.rand(2, 1, 64, 96, generator=g) < 0.1)).to(gpu)
     gt = ((torch.rand(2, 1, 64, 96, generator=g) * 79 + 1) * (torch.rand(2, 1, 64, 96, generator=g) < 0.3)).to(gpu)
     fn = _loss(nconv_amd)
 
-    net_e, opt_e = _setup(nconv_amd, gpu, capturable=True)
-    net_g, opt_g = _setup(nconv_amd, gpu, capturable=True)
+    net_e, opt_e = _setup(nconv_amd, gpu, capturable=True, fused=fused)
+    net_g, opt_g = _setup(nconv_amd, gpu, capturable=True, fused=fused)
     before = {k: v.clone() for k, v in net_g.state_dict().items()}
     step = nconv_amd.train.GraphedTrainStep(net_g, opt_g, fn, (S, gt))
     for k, v in net_g.state_dict().items():
