@@ -99,23 +99,31 @@ def weight_prep(weights, softplus_flags, wsums):
     _lib.check(rc, "nconv_weight_prep")
 
 
-def layer_forward_raw(spec: LayerSpec, xa, ca, xb, cb, weight, bias, wsum):
-    """Enqueue nconv_fwd; returns (y, cout). No autograd."""
+def _outputs(out, n, shapes, device):
+    if out is None:
+        return [torch.empty(sh, device=device, dtype=torch.float32) for sh in shapes]
+    if len(out) != n or any(tuple(t.shape) != tuple(sh) or not t.is_contiguous() or t.dtype != torch.float32
+                            for t, sh in zip(out, shapes)):
+        raise ValueError("out= tensors must be contiguous fp32 of the layer's output shapes")
+    return list(out)
+
+
+def layer_forward_raw(spec: LayerSpec, xa, ca, xb, cb, weight, bias, wsum, out=None):
+    """Enqueue nconv_fwd; returns (y, cout) (written into `out` if given). No autograd."""
     L = spec.descriptor(xa, ca, xb, cb, weight, bias, wsum)
-    y = torch.empty((L.B, L.Cout, L.Ho, L.Wo), device=xa.device, dtype=torch.float32)
-    co = torch.empty_like(y)
+    sh = (L.B, L.Cout, L.Ho, L.Wo)
+    y, co = _outputs(out, 2, (sh, sh), xa.device)
     rc = _lib.lib().nconv_fwd(_lib.ctypes.byref(L), _lib.ptr(y), _lib.ptr(co), _lib.stream_handle(xa.device))
     _lib.check(rc, "nconv_fwd")
     return y, co
 
 
-def layer_forward_pooled(spec: LayerSpec, xa, ca, xb, cb, weight, bias, wsum):
-    """nconv_fwd_pooled: (y, cout, maxpool2x2(y), maxpool2x2(cout)) in one launch. No autograd."""
+def layer_forward_pooled(spec: LayerSpec, xa, ca, xb, cb, weight, bias, wsum, out=None):
+    """nconv_fwd_pooled: (y, cout, maxpool2x2(y), maxpool2x2(cout)) in one launch (written into
+    `out` if given). No autograd."""
     L = spec.descriptor(xa, ca, xb, cb, weight, bias, wsum)
-    y = torch.empty((L.B, L.Cout, L.Ho, L.Wo), device=xa.device, dtype=torch.float32)
-    co = torch.empty_like(y)
-    py = torch.empty((L.B, L.Cout, L.Ho // 2, L.Wo // 2), device=xa.device, dtype=torch.float32)
-    pc = torch.empty_like(py)
+    sh, shp = (L.B, L.Cout, L.Ho, L.Wo), (L.B, L.Cout, L.Ho // 2, L.Wo // 2)
+    y, co, py, pc = _outputs(out, 4, (sh, sh, shp, shp), xa.device)
     rc = _lib.lib().nconv_fwd_pooled(_lib.ctypes.byref(L), _lib.ptr(y), _lib.ptr(co), _lib.ptr(py), _lib.ptr(pc),
                                      _lib.stream_handle(xa.device))
     _lib.check(rc, "nconv_fwd_pooled")

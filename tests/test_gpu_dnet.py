@@ -152,3 +152,24 @@ def test_dnet_train_gradients(nconv_amd, gpu, H, W):
                                    rtol=2e-6, atol=2e-7)
     print("\n".join(report))
     assert not any(r.endswith("FAIL") for r in report), "\n".join(report)
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_mid_streams_split_matches_one_stream(nconv_amd, gpu, n):
+    """Inference with down2/down3/nconv4 run on batch slices in several streams (DNET.mid_streams)
+    writes the same bits as the one-stream chain (same kernels per frame), eager and graphed."""
+    net = make_net(nconv_amd, "generalized", gpu)
+    g = torch.Generator().manual_seed(31)
+    S = sparse_depth(g, 5, 96, 160).to(gpu)
+    with torch.no_grad():
+        net.d_net.mid_streams = 1
+        a = net(S)
+        net.d_net.mid_streams = n
+        b = net(S)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            c = net(S)
+        graph.replay()
+        torch.cuda.synchronize()
+        net.d_net.mid_streams = 1
+    assert torch.equal(a, b) and torch.equal(a, c)
