@@ -1020,7 +1020,10 @@ static bool simple_geom(const nconv_layer& L) {
     return L.SH == 1 && L.SW == 1 && L.DH == 1 && L.DW == 1 && L.groups == 1 && L.KH == L.KW;
 }
 
-constexpr int kMaxWgBlocks = 1024;
+#ifndef NCONV_WG_MAX_BLOCKS
+#define NCONV_WG_MAX_BLOCKS 4096  // workspace bound; the launch uses at most one resident round
+#endif
+constexpr int kMaxWgBlocks = NCONV_WG_MAX_BLOCKS;
 
 enum Path { kTiled, kGeneric };
 
@@ -1108,12 +1111,24 @@ static void go_bwd_tiled(const LayerDev& d, const BwdArgs& a, float* part, float
     } else if (a.gw || a.gb) {
         using W = WgCfg<CIN, COUT, K>;
         const int ntw = (L.Wo + W::TW - 1) / W::TW, nth = (L.Ho + W::TH - 1) / W::TH;
-        const int nblk = (int)wg_blocks(L);
+        const int nblk_ws = (int)wg_blocks(L);
         size_t lds = (size_t)W::LDS_F2 * sizeof(f2);
         size_t red = (size_t)2 * COUT * kT * sizeof(float);
         const size_t red2 = (size_t)W::NSUB * COUT * CIN * K * K * sizeof(float);
         if (red2 > red) red = red2;
         if (red > lds) lds = red;
+        // blocks walk runs of tiles: launch at most the resident count (CUs x blocks per CU), so
+        // there is no second, partial round (nconv1's 13.4 k tiles: 768 resident at 3 waves/SIMD)
+        static int resident = 0;
+        if (resident == 0) {
+            int dev = 0, cus = 256, per_cu = 0;
+            if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, wgrad_tiled<CIN, COUT, K, MODE>, kT, lds) !=
+                    hipSuccess || per_cu <= 0)
+                per_cu = 1;
+            resident = cus * per_cu;
+        }
+        const int nblk = nblk_ws < resident ? nblk_ws : resident;
         hipLaunchKernelGGL((wgrad_tiled<CIN, COUT, K, MODE>), dim3(nblk), dim3(kT), lds, st, d, a, part, ntw, nth);
         const int nw = COUT * CIN * K * K;
         launch_wgrad_reduce(part, nblk, nw, COUT, CIN * K * K, L.wsum, a.gw, a.gb,
