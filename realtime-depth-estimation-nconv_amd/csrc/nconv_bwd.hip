@@ -1053,17 +1053,29 @@ static size_t wg_blocks(const nconv_layer& L) {
 }
 
 // wgrad_mfma grid: 64-wide q strips (q = ow + kw spans Wo + K - 1 columns) x row segments x images,
-// about kMfmaBlocks workgroups.
-constexpr int kMfmaBlocks = 2048;
+// at most `target` workgroups. The launch asks for two resident rounds of its instantiation (CUs x
+// blocks per CU x 2: a third, nearly empty round cost nconv2's weight gradient a third of its time
+// with a fixed 2048-block target); the workspace is sized for the largest possible occupancy.
+constexpr int kMfmaRounds = 2, kMfmaMaxPerCu = 4;
 struct WmGrid {
     int nstrip, nseg, seg_rows;
     size_t nblk;
 };
-static WmGrid wm_grid(const nconv_layer& L) {
+static int device_cus() {
+    static int cus = 0;
+    if (cus == 0) {
+        int dev = 0, n = 256;
+        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+        cus = n > 0 ? n : 256;
+    }
+    return cus;
+}
+static WmGrid wm_grid(const nconv_layer& L, int target = 0) {
+    if (target <= 0) target = kMfmaRounds * kMfmaMaxPerCu * device_cus();  // workspace bound
     WmGrid g;
     g.nstrip = (L.Wo + L.KW - 1 + 63) / 64;
     const int per_img = g.nstrip * L.B;
-    int nseg = (kMfmaBlocks + per_img - 1) / per_img;
+    int nseg = target / per_img;  // floor: never more blocks than the target (nseg >= 1 below)
     nseg = nseg < 1 ? 1 : (nseg > L.Ho ? L.Ho : nseg);
     g.seg_rows = (L.Ho + nseg - 1) / nseg;
     if (g.seg_rows < 1) g.seg_rows = 1;
@@ -1101,7 +1113,15 @@ static void go_bwd_tiled(const LayerDev& d, const BwdArgs& a, float* part, float
     }
     if constexpr (K > 1 && CIN > 1) {
         if (a.gw || a.gb) {
-            const WmGrid g = wm_grid(L);
+            static int resident = 0;
+            if (resident == 0) {
+                int per_cu = 0;
+                if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, wgrad_mfma<CIN, COUT, K, MODE>, kT, 0) !=
+                        hipSuccess || per_cu <= 0)
+                    per_cu = 1;
+                resident = device_cus() * (per_cu < kMfmaMaxPerCu ? per_cu : kMfmaMaxPerCu);
+            }
+            const WmGrid g = wm_grid(L, kMfmaRounds * resident);
             hipLaunchKernelGGL((wgrad_mfma<CIN, COUT, K, MODE>), dim3(g.nblk), dim3(kT), 0, st, d, a, part,
                                g.nstrip, g.nseg, g.seg_rows);
             const int nw = COUT * CIN * K * K;
