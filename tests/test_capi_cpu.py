@@ -137,3 +137,33 @@ def test_dense_fwd_geometry_validation(nconv_amd):
     d.Cout = 0
     assert lib.nconv_dense_conv_fwd(ctypes.byref(d), None) == -22
     assert "Cout" in lib.nconv_last_error().decode()
+
+
+def test_depth_loss_validation_is_host_only(nconv_amd):
+    """nconv_depth_loss_*: workspace query and argument checks (null planes, strides below W,
+    short workspace, non-positive sizes) fail on the host with -22 before any launch; the loss on
+    CPU tensors runs the reference's PyTorch ops, not the library."""
+    import torch
+    L = nconv_amd._lib
+    lib = L.lib()
+    ws_bytes = lib.nconv_depth_loss_workspace_bytes(352, 1216)
+    assert ws_bytes >= (3 * ((352 * 1216 + 255) // 256) + 4) * 4
+    assert lib.nconv_depth_loss_workspace_bytes(0, 5) == 0
+    p = ctypes.c_void_p(0x1000)
+    cases = [
+        ((None, 8, p, 8, 4, 8, 1, p, p, ws_bytes, None), "null plane"),
+        ((p, 7, p, 8, 4, 8, 1, p, p, ws_bytes, None), "row stride"),
+        ((p, 8, p, 8, 0, 8, 1, p, p, ws_bytes, None), "non-positive"),
+        ((p, 8, p, 8, 4, 8, 1, p, p, 4, None), "workspace too small"),
+        ((p, 8, p, 8, 4, 8, 1, None, p, ws_bytes, None), "null loss"),
+    ]
+    for args, msg in cases:
+        assert lib.nconv_depth_loss_fwd(*args) == -22
+        assert msg in lib.nconv_last_error().decode()
+    assert lib.nconv_depth_loss_bwd(p, 8, p, 8, 4, 8, 1, None, p, ws_bytes, None, None) == -22
+    assert "null g" in lib.nconv_last_error().decode()
+    r = torch.rand(1, 6, 9) * 10
+    t = (torch.rand(1, 6, 9) * 10) * (torch.rand(1, 6, 9) < 0.5)
+    assert not nconv_amd.train._fused_loss_ok(r, t)
+    got = nconv_amd.train.calculate_loss(r, t, True)
+    assert torch.equal(got, nconv_amd.train._calculate_loss_torch(r, t, True))
