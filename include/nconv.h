@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define NCONV_ABI_VERSION 10
+#define NCONV_ABI_VERSION 11
 
 /* How a layer's input (data x, confidence c) is produced from its source tensors. These are the
  * DNET glue ops fused into the layer's load stage (models/step1.py:53,61-90). */
@@ -65,7 +65,7 @@ typedef struct nconv_layer {
     const float* weight; /* (Cout, Cin/groups, KH, KW), positive in practice                   */
     const float* bias;   /* (Cout)                                                              */
     const float* wsum;   /* (Cout): s[o] = sum of weight[o] (step1.py:141-144), see nconv_weight_prep */
-    int math;            /* enum nconv_math (forward only; 0 = default)                         */
+    int math;            /* enum nconv_math (forward only; 0 = default; other values: -EINVAL)  */
 } nconv_layer;
 
 /* ABI version, for the Python loader's sanity check. */
@@ -255,21 +255,22 @@ size_t nconv_relu_bias_bwd_workspace_bytes(int B, int C, int H, int W);
 int nconv_relu_bias_bwd(int B, int C, int H, int W, const float* g, const float* out, float* g_masked,
                         float* gbias, void* workspace, size_t workspace_bytes, void* stream);
 
-/* Training loss of the reference on one (H, W) plane (utils.py:95-151 calculate_loss, evaluated
- * by train_step1.py:61 on element [0] of the batch): rec = r masked to 0 where t == 0;
- * use_gradient_loss != 0: L = 0.8 sqrt(mean (rec - t)^2) + 0.2 (mean |Sobel_x(t - rec)| +
- * mean |Sobel_y(t - rec)|), else L = mean (rec - t)^2. r and t are fp32 planes with row strides
- * r_row_stride / t_row_stride (elements; r may be a cropped view). nconv_depth_loss_fwd writes L
- * to loss[0] (device) and keeps the backward's coefficients in the workspace, which
- * nconv_depth_loss_bwd reads: g (contiguous H x W, OVERWRITTEN) = gloss[0] * dL/dr (gloss NULL: 1).
- * Deterministic (fixed-order reductions). */
-size_t nconv_depth_loss_workspace_bytes(int H, int W);
-int nconv_depth_loss_fwd(const float* r, long long r_row_stride, const float* t, long long t_row_stride, int H,
-                         int W, int use_gradient_loss, float* loss, void* workspace, size_t workspace_bytes,
-                         void* stream);
-int nconv_depth_loss_bwd(const float* r, long long r_row_stride, const float* t, long long t_row_stride, int H,
-                         int W, int use_gradient_loss, const float* gloss, const void* workspace,
-                         size_t workspace_bytes, float* g, void* stream);
+/* Training loss of the reference (utils.py:95-151 calculate_loss) on B (H, W) planes: the training
+ * loop calls it on the whole (B, 1, H, W) batch (train_step1.py:63), the validation loop on element
+ * [0] (utils.py:36; B = 1). rec = r masked to 0 where t == 0; use_gradient_loss != 0:
+ * L = 0.8 sqrt(mean (rec - t)^2) + 0.2 (mean |Sobel_x(t - rec)| + mean |Sobel_y(t - rec)|), else
+ * L = mean (rec - t)^2; means over B*H*W, each image's Sobel response zero-padded on its own
+ * (F.conv2d, padding 1). r and t are fp32 with image / row strides in elements (r may be a cropped
+ * view). nconv_depth_loss_fwd writes L to loss[0] (device) and keeps the backward's coefficients in
+ * the workspace, which nconv_depth_loss_bwd reads: g (contiguous B x H x W, OVERWRITTEN) =
+ * gloss[0] * dL/dr (gloss NULL: 1). Deterministic (fixed-order reductions). */
+size_t nconv_depth_loss_workspace_bytes(int B, int H, int W);
+int nconv_depth_loss_fwd(const float* r, long long r_image_stride, long long r_row_stride, const float* t,
+                         long long t_image_stride, long long t_row_stride, int B, int H, int W, int use_gradient_loss,
+                         float* loss, void* workspace, size_t workspace_bytes, void* stream);
+int nconv_depth_loss_bwd(const float* r, long long r_image_stride, long long r_row_stride, const float* t,
+                         long long t_image_stride, long long t_row_stride, int B, int H, int W, int use_gradient_loss,
+                         const float* gloss, const void* workspace, size_t workspace_bytes, float* g, void* stream);
 
 #ifdef __cplusplus
 }

@@ -13,7 +13,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # NCONV_LIB: an alternative build of the same library (kernel-tuning experiments)
 LIB_PATH = os.environ.get("NCONV_LIB") or os.path.join(_HERE, "libnconv.so")
-ABI_VERSION = 10
+ABI_VERSION = 11
 BWD_ACCUMULATE = 1
 
 # enum nconv_load_mode
@@ -141,11 +141,11 @@ def _declare(lib):
     lib.nconv_relu_bias_bwd.argtypes = [I, I, I, I, P, P, P, P, P, ctypes.c_size_t, P]
     L = ctypes.c_longlong
     lib.nconv_depth_loss_workspace_bytes.restype = ctypes.c_size_t
-    lib.nconv_depth_loss_workspace_bytes.argtypes = [I, I]
+    lib.nconv_depth_loss_workspace_bytes.argtypes = [I, I, I]
     lib.nconv_depth_loss_fwd.restype = I
-    lib.nconv_depth_loss_fwd.argtypes = [P, L, P, L, I, I, I, P, P, ctypes.c_size_t, P]
+    lib.nconv_depth_loss_fwd.argtypes = [P, L, L, P, L, L, I, I, I, I, P, P, ctypes.c_size_t, P]
     lib.nconv_depth_loss_bwd.restype = I
-    lib.nconv_depth_loss_bwd.argtypes = [P, L, P, L, I, I, I, P, P, ctypes.c_size_t, P, P]
+    lib.nconv_depth_loss_bwd.argtypes = [P, L, L, P, L, L, I, I, I, I, P, P, ctypes.c_size_t, P, P]
 
 
 def lib():

@@ -6,8 +6,10 @@
 //   gy   = conv2d(diff, [[1,2,1],[0,0,0],[-1,-2,-1]], padding=1)         utils.py:109-122
 //   L    = 0.8 sqrt(mean e^2) + 0.2 (mean|gx| + mean|gy|)   (gradient loss), else mean e^2
 //
-// On one (H, W) plane (the reference evaluates it on element [0] of the batch). In PyTorch this is
-// ~45 elementwise / reduction launches forward and backward; here:
+// On B planes of (H, W): the training loop calls it on the whole (B, 1, H, W) batch
+// (train_step1.py:63; the means run over B*H*W, the Sobel convolutions pad each image on its own),
+// the validation loop on element [0] (utils.py:36, B = 1). In PyTorch this is ~45 elementwise /
+// reduction launches forward and backward; here:
 //   loss_partials  one thread per pixel: e^2, |gx|, |gy| (3x3 window of diff, the same operation
 //                  order as train.gradient_x / _y, so signs match torch exactly), per-block sums
 //   loss_finalize  one block: fixed-order (double) sum of the block partials -> L and the two
@@ -25,8 +27,16 @@ constexpr int kLT = 256;
 struct LossPlane {
     const float* r;
     const float* t;
-    long long rs, ts;  // row strides (elements)
-    int H, W;
+    long long rs, ts;    // row strides (elements)
+    long long rbs, tbs;  // image strides (elements)
+    int B, H, W;
+    // image b's planes
+    __device__ __forceinline__ LossPlane image(int b) const {
+        LossPlane q = *this;
+        q.r += b * rbs;
+        q.t += b * tbs;
+        return q;
+    }
 };
 
 __device__ __forceinline__ float loss_diff(const LossPlane& p, int i, int j) {
@@ -63,8 +73,10 @@ __device__ __forceinline__ float block_sum256(float v, float* red) {
     return ((red[0] + red[1]) + red[2]) + red[3];
 }
 
-__global__ __launch_bounds__(kLT) void loss_partials(LossPlane p, int grad_loss, float* __restrict__ part) {
+// grid: (blocks per plane, B); the partial sums are indexed plane-major (a fixed order)
+__global__ __launch_bounds__(kLT) void loss_partials(LossPlane pb, int grad_loss, float* __restrict__ part) {
     __shared__ float red[4];
+    const LossPlane p = pb.image(blockIdx.y);
     const int n = p.H * p.W, e = blockIdx.x * kLT + threadIdx.x;
     float sq = 0.f, ax = 0.f, ay = 0.f;
     if (e < n) {
@@ -81,9 +93,10 @@ __global__ __launch_bounds__(kLT) void loss_partials(LossPlane p, int grad_loss,
     ax = block_sum256(ax, red);
     ay = block_sum256(ay, red);
     if (threadIdx.x == 0) {
-        part[3 * blockIdx.x] = sq;
-        part[3 * blockIdx.x + 1] = ax;
-        part[3 * blockIdx.x + 2] = ay;
+        const int blk = blockIdx.y * gridDim.x + blockIdx.x;
+        part[3 * blk] = sq;
+        part[3 * blk + 1] = ax;
+        part[3 * blk + 2] = ay;
     }
 }
 
@@ -123,10 +136,12 @@ __global__ __launch_bounds__(kLT) void loss_finalize(const float* __restrict__ p
 
 __device__ __forceinline__ float sgnf(float v) { return v > 0.f ? 1.f : (v < 0.f ? -1.f : 0.f); }
 
-__global__ __launch_bounds__(kLT) void loss_grad(LossPlane p, int grad_loss, const float* __restrict__ coef,
+__global__ __launch_bounds__(kLT) void loss_grad(LossPlane pb, int grad_loss, const float* __restrict__ coef,
                                                   const float* __restrict__ gout, float* __restrict__ g) {
+    const LossPlane p = pb.image(blockIdx.y);
     const int n = p.H * p.W, e = blockIdx.x * kLT + threadIdx.x;
     if (e >= n) return;
+    g += (size_t)blockIdx.y * n;  // contiguous (B, H, W) gradient
     const int i = e / p.W, j = e - i * p.W;
     const float t = p.t[i * p.ts + j];
     if (t == 0.f) {  // masked_fill: no gradient reaches r here
@@ -163,8 +178,8 @@ __global__ __launch_bounds__(kLT) void loss_grad(LossPlane p, int grad_loss, con
     g[e] = go * acc;
 }
 
-size_t loss_workspace_bytes(int H, int W) {
-    const size_t nblk = ((size_t)H * W + kLT - 1) / kLT;
+size_t loss_workspace_bytes(int B, int H, int W) {
+    const size_t nblk = (size_t)B * (((size_t)H * W + kLT - 1) / kLT);
     return (3 * nblk + 4) * sizeof(float);
 }
 
@@ -177,22 +192,22 @@ static int loss_err(const char** why) {
     return 0;
 }
 
-int launch_loss_fwd(const float* r, long long rs, const float* t, long long ts, int H, int W, int grad_loss,
-                    float* loss, float* ws, hipStream_t st, const char** why) {
-    const LossPlane p{r, t, rs, ts, H, W};
-    const int n = H * W, nblk = (n + kLT - 1) / kLT;
+int launch_loss_fwd(const LossArgs& a, int grad_loss, float* loss, float* ws, hipStream_t st, const char** why) {
+    const LossPlane p{a.r, a.t, a.rs, a.ts, a.rbs, a.tbs, a.B, a.H, a.W};
+    const int nblk = (a.H * a.W + kLT - 1) / kLT;
     float* coef = ws;
     float* part = ws + 4;
-    hipLaunchKernelGGL(loss_partials, dim3(nblk), dim3(kLT), 0, st, p, grad_loss, part);
-    hipLaunchKernelGGL(loss_finalize, dim3(1), dim3(kLT), 0, st, part, nblk, n, grad_loss, loss, coef);
+    hipLaunchKernelGGL(loss_partials, dim3(nblk, a.B), dim3(kLT), 0, st, p, grad_loss, part);
+    hipLaunchKernelGGL(loss_finalize, dim3(1), dim3(kLT), 0, st, part, nblk * a.B, a.B * a.H * a.W, grad_loss, loss,
+                       coef);
     return loss_err(why);
 }
 
-int launch_loss_bwd(const float* r, long long rs, const float* t, long long ts, int H, int W, int grad_loss,
-                    const float* gout, const float* ws, float* g, hipStream_t st, const char** why) {
-    const LossPlane p{r, t, rs, ts, H, W};
-    const int n = H * W, nblk = (n + kLT - 1) / kLT;
-    hipLaunchKernelGGL(loss_grad, dim3(nblk), dim3(kLT), 0, st, p, grad_loss, ws, gout, g);
+int launch_loss_bwd(const LossArgs& a, int grad_loss, const float* gout, const float* ws, float* g, hipStream_t st,
+                    const char** why) {
+    const LossPlane p{a.r, a.t, a.rs, a.ts, a.rbs, a.tbs, a.B, a.H, a.W};
+    const int nblk = (a.H * a.W + kLT - 1) / kLT;
+    hipLaunchKernelGGL(loss_grad, dim3(nblk, a.B), dim3(kLT), 0, st, p, grad_loss, ws, gout, g);
     return loss_err(why);
 }
 

@@ -26,6 +26,7 @@ const char* validate(const nconv_layer* L, bool need_c) {
     if (ho != L->Ho || wo != L->Wo) return "Ho/Wo inconsistent with H/W/kernel/stride/padding/dilation";
     if (!L->weight || !L->bias || !L->wsum) return "null weight/bias/wsum";
     if (!L->a.x) return "null source a.x";
+    if (L->math != NCONV_MATH_BF16X3 && L->math != NCONV_MATH_FP32) return "unknown math (enum nconv_math)";
     switch (L->load_mode) {
         case NCONV_LOAD_PLAIN:
             if (!L->a.c && need_c) return "null source a.c";
@@ -334,44 +335,43 @@ int nconv_conv3x3_c1(const float* x, int B, int Cin, int H, int W, const float* 
     return rc ? fail(rc, fn, why) : 0;
 }
 
-size_t nconv_depth_loss_workspace_bytes(int H, int W) {
-    if (H <= 0 || W <= 0 || (long long)H * W > (1LL << 30)) return 0;
-    return nconv::loss_workspace_bytes(H, W);
+size_t nconv_depth_loss_workspace_bytes(int B, int H, int W) {
+    if (B <= 0 || H <= 0 || W <= 0 || (long long)B * H * W > (1LL << 30)) return 0;
+    return nconv::loss_workspace_bytes(B, H, W);
 }
 
-static const char* validate_loss(const float* r, long long rs, const float* t, long long ts, int H, int W,
-                                 size_t ws_bytes, const void* ws) {
-    if (!r || !t) return "null plane";
-    if (H <= 0 || W <= 0) return "non-positive H/W";
-    if ((long long)H * W > (1LL << 30)) return "plane too large";
-    if (rs < W || ts < W) return "row stride smaller than W";
-    if (!ws || ws_bytes < nconv::loss_workspace_bytes(H, W)) return "workspace too small";
+static const char* validate_loss(const nconv::LossArgs& a, size_t ws_bytes, const void* ws) {
+    if (!a.r || !a.t) return "null plane";
+    if (a.B <= 0 || a.H <= 0 || a.W <= 0) return "non-positive B/H/W";
+    if ((long long)a.B * a.H * a.W > (1LL << 30)) return "batch too large";
+    if (a.rs < a.W || a.ts < a.W) return "row stride smaller than W";
+    if (a.B > 1 && (a.rbs < a.H * a.rs || a.tbs < a.H * a.ts)) return "image stride smaller than H * row stride";
+    if (!ws || ws_bytes < nconv::loss_workspace_bytes(a.B, a.H, a.W)) return "workspace too small";
     return nullptr;
 }
 
-int nconv_depth_loss_fwd(const float* r, long long r_row_stride, const float* t, long long t_row_stride, int H,
-                         int W, int use_gradient_loss, float* loss, void* workspace, size_t workspace_bytes,
-                         void* stream) {
+int nconv_depth_loss_fwd(const float* r, long long r_image_stride, long long r_row_stride, const float* t,
+                         long long t_image_stride, long long t_row_stride, int B, int H, int W, int use_gradient_loss,
+                         float* loss, void* workspace, size_t workspace_bytes, void* stream) {
     const char* fn = "nconv_depth_loss_fwd";
-    if (const char* why = validate_loss(r, r_row_stride, t, t_row_stride, H, W, workspace_bytes, workspace))
-        return fail(-22, fn, why);
+    const nconv::LossArgs a{r, t, r_image_stride, r_row_stride, t_image_stride, t_row_stride, B, H, W};
+    if (const char* why = validate_loss(a, workspace_bytes, workspace)) return fail(-22, fn, why);
     if (!loss) return fail(-22, fn, "null loss");
     const char* why = nullptr;
-    int rc = nconv::launch_loss_fwd(r, r_row_stride, t, t_row_stride, H, W, use_gradient_loss != 0, loss,
-                                    (float*)workspace, (hipStream_t)stream, &why);
+    int rc = nconv::launch_loss_fwd(a, use_gradient_loss != 0, loss, (float*)workspace, (hipStream_t)stream, &why);
     return rc ? fail(rc, fn, why) : 0;
 }
 
-int nconv_depth_loss_bwd(const float* r, long long r_row_stride, const float* t, long long t_row_stride, int H,
-                         int W, int use_gradient_loss, const float* gloss, const void* workspace,
-                         size_t workspace_bytes, float* g, void* stream) {
+int nconv_depth_loss_bwd(const float* r, long long r_image_stride, long long r_row_stride, const float* t,
+                         long long t_image_stride, long long t_row_stride, int B, int H, int W, int use_gradient_loss,
+                         const float* gloss, const void* workspace, size_t workspace_bytes, float* g, void* stream) {
     const char* fn = "nconv_depth_loss_bwd";
-    if (const char* why = validate_loss(r, r_row_stride, t, t_row_stride, H, W, workspace_bytes, workspace))
-        return fail(-22, fn, why);
+    const nconv::LossArgs a{r, t, r_image_stride, r_row_stride, t_image_stride, t_row_stride, B, H, W};
+    if (const char* why = validate_loss(a, workspace_bytes, workspace)) return fail(-22, fn, why);
     if (!g) return fail(-22, fn, "null g");
     const char* why = nullptr;
-    int rc = nconv::launch_loss_bwd(r, r_row_stride, t, t_row_stride, H, W, use_gradient_loss != 0, gloss,
-                                    (const float*)workspace, g, (hipStream_t)stream, &why);
+    int rc = nconv::launch_loss_bwd(a, use_gradient_loss != 0, gloss, (const float*)workspace, g, (hipStream_t)stream,
+                                    &why);
     return rc ? fail(rc, fn, why) : 0;
 }
 

@@ -71,11 +71,17 @@ int launch_relu_bias_bwd(int B, int C, int H, int W, const float* g, const float
 int launch_bn_train_bwd(const nconv_bn_train& p, const float* gy, float* gx, float* ggamma, float* gbeta, float* ws,
                         hipStream_t st, const char** why);
 
-// Training loss (utils.py calculate_loss) on one plane.
-size_t loss_workspace_bytes(int H, int W);
-int launch_loss_fwd(const float* r, long long rs, const float* t, long long ts, int H, int W, int grad_loss,
-                    float* loss, float* ws, hipStream_t st, const char** why);
-int launch_loss_bwd(const float* r, long long rs, const float* t, long long ts, int H, int W, int grad_loss,
-                    const float* gout, const float* ws, float* g, hipStream_t st, const char** why);
+// Training loss (utils.py calculate_loss) on B planes.
+struct LossArgs {
+    const float* r;
+    const float* t;
+    long long rbs, rs;  // image / row strides of r (elements)
+    long long tbs, ts;  // ... of t
+    int B, H, W;
+};
+size_t loss_workspace_bytes(int B, int H, int W);
+int launch_loss_fwd(const LossArgs& a, int grad_loss, float* loss, float* ws, hipStream_t st, const char** why);
+int launch_loss_bwd(const LossArgs& a, int grad_loss, const float* gout, const float* ws, float* g, hipStream_t st,
+                    const char** why);
 
 }  // namespace nconv

@@ -2,7 +2,7 @@
 
 Cheap elementwise/reduction glue around the NConv path (PyTorch-ROCm ops), except the loss itself.
   calculate_loss                    utils.py:138-151   masked RMSE*0.8 + Sobel-gradient*0.2 (or MSE);
-                                    on device planes the fused libnconv kernels (DepthLossFn)
+                                    on device planes / batches the fused libnconv kernels (DepthLossFn)
   gradient_loss / gradient_x / _y   utils.py:95-136
   calculate_loss_multi_resolution   utils.py:63-71     each scale bilinear-resized to 480x640, [0] only
   get_optimizer                     utils.py:53-61     AdamW / SGD / RMSprop
@@ -51,19 +51,40 @@ def _calculate_loss_torch(reconstructed_img, target_img, use_gradient_loss):
     return F.mse_loss(rec, target_img)
 
 
+def _planes(x):
+    """(B, H, W) view geometry of a loss operand: (H, W), (1, H, W) or (B, 1, H, W) -> (B, image
+    stride, row stride); None if it is not such a set of unit-stride rows."""
+    if x.dim() == 2:
+        B, bs = 1, 0
+    elif x.dim() == 3 and x.shape[0] == 1:
+        B, bs = 1, 0
+    elif x.dim() == 4 and x.shape[1] == 1:
+        B, bs = x.shape[0], x.stride(0)
+    else:
+        return None
+    H, W = x.shape[-2], x.shape[-1]
+    if x.stride(-1) != 1 or x.stride(-2) < W or (B > 1 and bs < H * x.stride(-2)):
+        return None
+    return B, bs, x.stride(-2)
+
+
 class DepthLossFn(torch.autograd.Function):
-    """calculate_loss (utils.py:138-151) on one (1, H, W) / (H, W) plane as libnconv kernels
-    (nconv_depth_loss_fwd / _bwd: 2 launches forward, 1 backward, instead of ~45 PyTorch ops)."""
+    """calculate_loss (utils.py:138-151) on a (H, W) / (1, H, W) plane or a (B, 1, H, W) batch as
+    libnconv kernels (nconv_depth_loss_fwd / _bwd: 2 launches forward, 1 backward, instead of ~45
+    PyTorch ops). The batch form is the training loop's call (train_step1.py:63): means over all
+    B*H*W elements, each image's Sobel response padded on its own, like F.conv2d on the batch."""
 
     @staticmethod
     def forward(ctx, r, t, use_gradient_loss):
         from . import _lib
         H, W = r.shape[-2], r.shape[-1]
+        B, rbs, rs = _planes(r)
+        _, tbs, ts = _planes(t)
         lib = _lib.lib()
-        nbytes = lib.nconv_depth_loss_workspace_bytes(H, W)
+        nbytes = lib.nconv_depth_loss_workspace_bytes(B, H, W)
         ws = torch.empty(max(nbytes, 4), dtype=torch.uint8, device=r.device)
         loss = torch.empty((), dtype=torch.float32, device=r.device)
-        rc = lib.nconv_depth_loss_fwd(_lib.ptr(r), r.stride(-2), _lib.ptr(t), t.stride(-2), H, W,
+        rc = lib.nconv_depth_loss_fwd(_lib.ptr(r), rbs, rs, _lib.ptr(t), tbs, ts, B, H, W,
                                       int(bool(use_gradient_loss)), _lib.ptr(loss), _lib.ptr(ws), nbytes,
                                       _lib.stream_handle(r.device))
         _lib.check(rc, "nconv_depth_loss_fwd")
@@ -76,9 +97,11 @@ class DepthLossFn(torch.autograd.Function):
         from . import _lib
         r, t, ws = ctx.saved_tensors
         H, W = r.shape[-2], r.shape[-1]
+        B, rbs, rs = _planes(r)
+        _, tbs, ts = _planes(t)
         g = torch.empty(r.shape, dtype=torch.float32, device=r.device)
         gloss = gloss.contiguous()
-        rc = _lib.lib().nconv_depth_loss_bwd(_lib.ptr(r), r.stride(-2), _lib.ptr(t), t.stride(-2), H, W,
+        rc = _lib.lib().nconv_depth_loss_bwd(_lib.ptr(r), rbs, rs, _lib.ptr(t), tbs, ts, B, H, W,
                                              int(ctx.use_gradient_loss), _lib.ptr(gloss), _lib.ptr(ws),
                                              ws.numel(), _lib.ptr(g), _lib.stream_handle(r.device))
         _lib.check(rc, "nconv_depth_loss_bwd")
@@ -86,15 +109,14 @@ class DepthLossFn(torch.autograd.Function):
 
 
 def _fused_loss_ok(r, t):
-    def plane(x):
-        return (x.is_cuda and x.dtype == torch.float32 and x.dim() in (2, 3) and (x.dim() == 2 or x.shape[0] == 1)
-                and x.stride(-1) == 1 and x.stride(-2) >= x.shape[-1])
-    return plane(r) and plane(t) and r.shape == t.shape and not t.requires_grad and r.device == t.device
+    def ok(x):
+        return x.is_cuda and x.dtype == torch.float32 and _planes(x) is not None
+    return ok(r) and ok(t) and r.shape == t.shape and not t.requires_grad and r.device == t.device
 
 
 def calculate_loss(reconstructed_img, target_img, use_gradient_loss):
-    """utils.py:138-151. Device planes run the fused libnconv loss (DepthLossFn); anything else
-    (CPU tensors, several channels) the PyTorch ops of the reference."""
+    """utils.py:138-151. Device planes / (B, 1, H, W) batches run the fused libnconv loss
+    (DepthLossFn); anything else (CPU tensors, several channels) the PyTorch ops of the reference."""
     if _fused_loss_ok(reconstructed_img, target_img):
         return DepthLossFn.apply(reconstructed_img, target_img, use_gradient_loss)
     return _calculate_loss_torch(reconstructed_img, target_img, use_gradient_loss)

@@ -140,30 +140,61 @@ def test_dense_fwd_geometry_validation(nconv_amd):
 
 
 def test_depth_loss_validation_is_host_only(nconv_amd):
-    """nconv_depth_loss_*: workspace query and argument checks (null planes, strides below W,
-    short workspace, non-positive sizes) fail on the host with -22 before any launch; the loss on
-    CPU tensors runs the reference's PyTorch ops, not the library."""
+    """nconv_depth_loss_*: workspace query and argument checks (null planes, strides below W or
+    overlapping images, short workspace, non-positive sizes) fail on the host with -22 before any
+    launch; the loss on CPU tensors runs the reference's PyTorch ops, not the library."""
     import torch
     L = nconv_amd._lib
     lib = L.lib()
-    ws_bytes = lib.nconv_depth_loss_workspace_bytes(352, 1216)
+    ws_bytes = lib.nconv_depth_loss_workspace_bytes(1, 352, 1216)
     assert ws_bytes >= (3 * ((352 * 1216 + 255) // 256) + 4) * 4
-    assert lib.nconv_depth_loss_workspace_bytes(0, 5) == 0
+    assert lib.nconv_depth_loss_workspace_bytes(8, 352, 1216) >= (3 * 8 * ((352 * 1216 + 255) // 256) + 4) * 4
+    assert lib.nconv_depth_loss_workspace_bytes(1, 0, 5) == 0
+    assert lib.nconv_depth_loss_workspace_bytes(0, 5, 5) == 0
     p = ctypes.c_void_p(0x1000)
+    ws2 = lib.nconv_depth_loss_workspace_bytes(2, 4, 8)
+    # (r, r_image_stride, r_row_stride, t, t_image_stride, t_row_stride, B, H, W, grad, loss, ws, ws_bytes, stream)
     cases = [
-        ((None, 8, p, 8, 4, 8, 1, p, p, ws_bytes, None), "null plane"),
-        ((p, 7, p, 8, 4, 8, 1, p, p, ws_bytes, None), "row stride"),
-        ((p, 8, p, 8, 0, 8, 1, p, p, ws_bytes, None), "non-positive"),
-        ((p, 8, p, 8, 4, 8, 1, p, p, 4, None), "workspace too small"),
-        ((p, 8, p, 8, 4, 8, 1, None, p, ws_bytes, None), "null loss"),
+        ((None, 32, 8, p, 32, 8, 1, 4, 8, 1, p, p, ws_bytes, None), "null plane"),
+        ((p, 32, 7, p, 32, 8, 1, 4, 8, 1, p, p, ws_bytes, None), "row stride"),
+        ((p, 32, 8, p, 32, 8, 1, 0, 8, 1, p, p, ws_bytes, None), "non-positive"),
+        ((p, 32, 8, p, 32, 8, 0, 4, 8, 1, p, p, ws_bytes, None), "non-positive"),
+        ((p, 31, 8, p, 32, 8, 2, 4, 8, 1, p, p, ws2, None), "image stride"),
+        ((p, 32, 8, p, 32, 8, 1, 4, 8, 1, p, p, 4, None), "workspace too small"),
+        ((p, 32, 8, p, 32, 8, 2, 4, 8, 1, p, p, ws2 - 4, None), "workspace too small"),
+        ((p, 32, 8, p, 32, 8, 1, 4, 8, 1, None, p, ws_bytes, None), "null loss"),
     ]
     for args, msg in cases:
-        assert lib.nconv_depth_loss_fwd(*args) == -22
+        assert lib.nconv_depth_loss_fwd(*args) == -22, msg
         assert msg in lib.nconv_last_error().decode()
-    assert lib.nconv_depth_loss_bwd(p, 8, p, 8, 4, 8, 1, None, p, ws_bytes, None, None) == -22
+    assert lib.nconv_depth_loss_bwd(p, 32, 8, p, 32, 8, 1, 4, 8, 1, None, p, ws_bytes, None, None) == -22
     assert "null g" in lib.nconv_last_error().decode()
     r = torch.rand(1, 6, 9) * 10
     t = (torch.rand(1, 6, 9) * 10) * (torch.rand(1, 6, 9) < 0.5)
     assert not nconv_amd.train._fused_loss_ok(r, t)
     got = nconv_amd.train.calculate_loss(r, t, True)
     assert torch.equal(got, nconv_amd.train._calculate_loss_torch(r, t, True))
+
+
+def test_loss_plane_geometry(nconv_amd):
+    """The batch geometry the fused loss accepts: (H, W), (1, H, W), (B, 1, H, W) incl. cropped views
+    (row / image strides); several channels or a non-unit column stride are not loss planes."""
+    import torch
+    P = nconv_amd.train._planes
+    assert P(torch.empty(5, 7)) == (1, 0, 7)
+    assert P(torch.empty(1, 5, 7)) == (1, 0, 7)
+    assert P(torch.empty(3, 1, 5, 7)) == (3, 35, 7)
+    v = torch.empty(3, 1, 9, 11)[:, :, 1:6, 1:8]
+    assert P(v) == (3, 99, 11)
+    assert P(torch.empty(3, 2, 5, 7)) is None
+    assert P(torch.empty(2, 5, 7)) is None
+    assert P(torch.empty(7, 5).t()) is None
+
+
+def test_fwd_rejects_unknown_math(nconv_amd):
+    """nconv_layer.math outside enum nconv_math (e.g. a host struct without the field) is refused."""
+    lib = nconv_amd._lib.lib()
+    for m in (2, -1, 0x7fff):
+        L = _layer(nconv_amd, math=m)
+        assert lib.nconv_fwd(ctypes.byref(L), ctypes.c_void_p(0x2000), ctypes.c_void_p(0x3000), None) == -22
+        assert "unknown math" in lib.nconv_last_error().decode()
