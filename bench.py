@@ -3,10 +3,19 @@
 
 Headline (BASELINE.json metric, config 2): frames/sec of the unguided NConv U-Net (DNET /
 SETP1_NCONV, models/step1.py:15-94) forward on B=8 synthetic KITTI-shaped 352x1216 sparse depth
-per GPU, fp32, inputs resident in HBM. Also reported (same JSON line): fwd+bwd+AdamW training-step
-frames/sec (config 4b: EnforcePos drift + calculate_loss + backward + AdamW, train_step1.py:59-65),
-per-layer kernel times, the roofline of the dominant kernel, and the CPU baseline (the oracle's
-restatement of the reference, timed on this host's cores).
+per GPU, inputs resident in HBM, computed in EXACT fp32 (every product an fp32 product, as the
+reference's F.conv2d; include/nconv.h NCONV_MATH_FP32). Also on the same JSON line:
+  fwd_bf16x3         the same forward with split-bf16 matrix-core products (NCONV_MATH_BF16X3,
+                     <= ~1.1e-5 relative per product: narrower than fp32, reported separately)
+  config5            B=16 1024x2048 forward (BASELINE configs[4]), both arithmetics, own roofline
+  train_fwd_bwd_adamw  config 4b: EnforcePos drift + calculate_loss on the whole batch
+                     (train_step1.py:63) + backward + AdamW, hipGraph-replayed, with its roofline
+  guided_fwd / guided_train_fwd_bwd_adamw  configs 3 / 4 with their fp32-MFMA fraction
+  layer_us / roofline  per-kernel device time of the headline forward and the roofline of its
+                     dominant kernel (HIP events on the launch stream; profiles/ has the rocprofv3
+                     summary of the same command)
+  cpu_baseline       the oracle (the reference's op sequence) on this host's cores: the config-2
+                     workload (B=8, generalized crop) and config 1 (3-layer forward, B=1)
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 8] [--height 352] [--width 1216]
     torchrun --nproc-per-node N bench.py --gpus N ...      # one process per GPU, RCCL
@@ -26,9 +35,14 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md, chip-level parameters (spec)
-MFMA_BF16_PEAK_TFLOPS = 2500.0  # dense bf16 matrix peak (no sparsity), MI355X_MICROARCH.md
-FP32_PEAK_TFLOPS = 157.3   # same table: FP32 vector / matrix peak
+HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md, chip-level parameters (spec)
+MFMA_BF16_PEAK_TFLOPS = 2500.0  # dense bf16 matrix peak (no sparsity)
+FP32_PEAK_TFLOPS = 157.3        # FP32 vector = FP32 matrix peak (same table)
+PASS_BYTES_PER_FRAME = 238.44e6  # fused per-layer forward, 352x1216
+PASS_FLOPS_PER_FRAME = 6.620e9
+BWD_BYTES_PER_FRAME = 373.9e6    # SURVEY.md 8(d) backward estimate, 352x1216
+BWD_FLOPS_PER_FRAME = 12.79e9
+GUIDED_DENSE_FLOPS_PER_FRAME = 133.6e9  # RGB encoder 7.94 + fusion decoder 125.69 GFLOP
 LAYERS = ("nconv1", "nconv2", "nconv_down1", "nconv_down2", "nconv_down3", "nconv4", "nconv5", "nconv6", "nconv7")
 
 
@@ -43,20 +57,22 @@ def parse():
     p.add_argument("--train-steps", type=int, default=None, help="timed fwd+bwd steps (default: --steps)")
     p.add_argument("--no-train", action="store_true")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--no-fp32-forward", action="store_true",
-                   help="skip the exact-fp32 (vector ALU) forward measurement reported beside the headline")
+    p.add_argument("--no-bf16x3", action="store_true", help="skip the split-bf16 forward reported beside the headline")
+    p.add_argument("--no-config5", action="store_true", help="skip the B=16 1024x2048 forward (config 5)")
     p.add_argument("--no-guided", action="store_true", help="skip the config-3 guided forward measurement")
     p.add_argument("--no-guided-train", action="store_true", help="skip the config-4 guided training step")
-    p.add_argument("--guided-train-torch", action="store_true",
-                   help="also time the config-4 step on the PyTorch-ROCm modules (MIOpen), for comparison")
-    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU time of each CPU-baseline sample")
     p.add_argument("--graph", type=int, default=1, help="capture the forward in a hipGraph (1) or run eager (0)")
-    p.add_argument("--streams", type=int, default=1, help="HIP streams the inference batch is split over")
     p.add_argument("--fused-head", type=int, default=1, help="nconv1 inside nconv2's kernel (nconv_fwd_head)")
     p.add_argument("--train-graph", type=int, default=-1,
                    help="replay the training step from a hipGraph (1) or eager (0); default: 1 on one GPU, 0 with "
                         "several (the RCCL all-reduce stays outside graph capture)")
     return p.parse_args()
+
+
+def log(*msg):
+    """Progress on stderr (a long silent run looks hung to the GPU harness)."""
+    print("[bench]", *msg, file=sys.stderr, flush=True)
 
 
 def sparse_depth(g, B, H, W, device):
@@ -65,76 +81,67 @@ def sparse_depth(g, B, H, W, device):
     return d.to(device)
 
 
-# ---- algorithmic per-layer cost --------------------------------------------------
-def layer_costs(B, H, W):
-    """Per fused layer: (bytes, flops) per launch, SURVEY.md 8(d)'s algorithmic count. Bytes: each
-    layer reads its producers' x and c once at their native resolution (glue fused) and writes y
-    and c once; nconv1 reads S only. (The inference path's pooled copies change the down layers'
-    actual reads; the algorithmic count is kept as the common yardstick.)
-    Flops: 2 convs x 2 flop/FMA x Cin x k^2 x Cout per output pixel, + 4*Cout (div, bias, conf)."""
-    f = 4
-    H2, W2, H4, W4, H8, W8 = H // 2, W // 2, H // 4, W // 4, H // 8, W // 8
+# ---- algorithmic cost per kernel -------------------------------------------------
+def kernel_costs(B, H, W):
+    """(bytes, flops) per launch of each kernel of the inference forward. Bytes: the kernel's
+    sources read once at their native resolution and its outputs written once (including the
+    2x2 max-pooled copies the pooled launches write for the next down layer); fp32, 4 B.
+    Flops: 2 convolutions x 2 flop/FMA x Cin k^2 Cout per output pixel, + 4 Cout (div, bias, conf).
+    Per unit (one output pixel of the layer): nconv1 68 B / 832 flop; nconv2 (pooled) 144 B /
+    6432; head (nconv1+2, pooled) 84 B / 7264; down1/down2 (pooled) 144 B / 6432; down3 128 B /
+    6432; nconv4/5 64 B + 64 B per skip / low-res source pixel / 4640; tail 64 B per nconv2 pixel
+    + 64 B per nconv5 pixel + 4 B output / 4640 (nconv6) + 36 (nconv7)."""
+    f4 = 4
+    H2, W2, H4, W4, H8, W8, H16, W16 = H // 2, W // 2, H // 4, W // 4, H // 8, W // 8, H // 16, W // 16
     px = lambda h, w: B * h * w
-    c = {}
-    c["nconv1"] = (px(H, W) * (1 * f + 16 * f), px(H, W) * (2 * 2 * 1 * 25 * 8 + 32))
-    c["nconv2"] = (px(H, W) * (16 * f + 16 * f), px(H, W) * (2 * 2 * 8 * 25 * 8 + 32))
-    c["nconv_down1"] = (px(H, W) * 16 * f + px(H2, W2) * 16 * f, px(H2, W2) * (6400 + 32))
-    c["nconv_down2"] = (px(H2, W2) * 16 * f + px(H4, W4) * 16 * f, px(H4, W4) * (6400 + 32))
-    c["nconv_down3"] = (px(H4, W4) * 16 * f + px(H8, W8) * 16 * f, px(H8, W8) * (6400 + 32))
-    c["nconv4"] = (px(H4, W4) * 16 * f + px(H8, W8) * 16 * f + px(H4, W4) * 16 * f,
-                   px(H4, W4) * (2 * 2 * 16 * 9 * 8 + 32))
-    c["nconv5"] = (px(H2, W2) * 16 * f + px(H4, W4) * 16 * f + px(H2, W2) * 16 * f,
-                   px(H2, W2) * (2 * 2 * 16 * 9 * 8 + 32))
-    c["nconv6"] = (px(H, W) * 16 * f + px(H2, W2) * 16 * f + px(H - 2, W - 2) * 16 * f,
-                   px(H - 2, W - 2) * (2 * 2 * 16 * 9 * 8 + 32))
-    c["nconv7"] = (px(H - 2, W - 2) * 16 * f + px(H + 2, W + 2) * 1 * f, px(H + 2, W + 2) * (2 * 2 * 8 + 4))
+    F5, F3 = 2 * 2 * 8 * 25 * 8 + 32, 2 * 2 * 16 * 9 * 8 + 32
+    c = {
+        "nconv1": (px(H, W) * (1 + 16) * f4, px(H, W) * (2 * 2 * 1 * 25 * 8 + 32)),
+        "nconv2": (px(H, W) * (16 + 16 + 4) * f4, px(H, W) * F5),
+        "nconv1+nconv2_head": (px(H, W) * (1 + 16 + 4) * f4, px(H, W) * (F5 + 2 * 2 * 25 * 8 + 32)),
+        "nconv_down1": (px(H2, W2) * (16 + 16 + 4) * f4, px(H2, W2) * F5),
+        "nconv_down2": (px(H4, W4) * (16 + 16 + 4) * f4, px(H4, W4) * F5),
+        "nconv_down3": (px(H8, W8) * (16 + 16) * f4, px(H8, W8) * F5),
+        "nconv4": ((px(H4, W4) * 32 + px(H8, W8) * 16) * f4, px(H4, W4) * F3),
+        "nconv5": ((px(H2, W2) * 32 + px(H4, W4) * 16) * f4, px(H2, W2) * F3),
+        "nconv6+7_tail": ((px(H, W) * (16 + 1) + px(H2, W2) * 16) * f4,
+                          px(H - 2, W - 2) * F3 + px(H + 2, W + 2) * (2 * 2 * 8 + 4)),
+    }
+    del H16, W16
     return c
 
 
-def head_cost(B, H, W):
-    """nconv1+nconv2 fused launch (inference): reads the sparse depth, writes nconv2's y and cout
-    and their 2x2 max-pooled copies; flops of both layers."""
-    byt = (B * H * W * 1 + B * H * W * 16 + B * (H // 2) * (W // 2) * 16) * 4
-    fl = B * H * W * ((2 * 2 * 1 * 25 * 8 + 32) + (2 * 2 * 8 * 25 * 8 + 32))
-    return byt, fl
-
-
-def fused_tail_cost(B, H, W):
-    """nconv6+nconv7 fused launch (inference): reads nconv6's inputs, writes the final output."""
-    H2, W2 = H // 2, W // 2
-    byt = (B * H * W * 16 + B * H2 * W2 * 16 + B * H * W * 1) * 4
-    fl = B * (H - 2) * (W - 2) * (2 * 2 * 16 * 9 * 8 + 32) + B * H * W * (2 * 2 * 8 + 4)
-    return byt, fl
-
-
-def time_layers(m, net, S, reps=20):
-    """Average device time per launch of each kernel of the inference forward (HIP events on the
-    launch stream): nconv1, nconv2 (+pooled copy), down1..3 (reading the pooled copies), nconv4/5,
-    and the fused nconv6+7 tail."""
+def inference_calls(m, net, S):
+    """The inference forward's launches, one callable each (same kernels and order as
+    DNET._infer), for per-kernel timing."""
     lib = m._lib
     d = net.d_net
     layers = [getattr(d, n) for n in LAYERS]
     wsum = d._prologue(layers, S)
     l1, l2, d1, d2, d3, l4, l5, l6, l7 = layers
     s1, s2, sd1, sd2, sd3, s4, s5, s6, s7 = wsum
-    fwd, fpool = m.nconv.layer_forward_raw, m.nconv.layer_forward_pooled
+    fwd, fpool, fhead = m.nconv.layer_forward_raw, m.nconv.layer_forward_pooled, m.nconv.layer_forward_head
     H, W = S.shape[2], S.shape[3]
     oh, ow = m.crop_hw(H, W, d.crop)
+    head = d._use_head(l1, l2)
     with torch.no_grad():
-        x1, c1 = fwd(l1.spec(lib.THRESH, 0.01), S, None, None, None, l1.weight, l1.bias, s1)
-        x1b, c1b, p1, q1 = fpool(l2.spec(), x1, c1, None, None, l2.weight, l2.bias, s2)
+        if head:
+            x1b, c1b, p1, q1 = fhead(l1.spec(lib.THRESH, 0.01), l2.spec(), S, l1.weight, l1.bias, s1, l2.weight,
+                                     l2.bias, s2)
+        else:
+            x1, c1 = fwd(l1.spec(lib.THRESH, 0.01), S, None, None, None, l1.weight, l1.bias, s1)
+            x1b, c1b, p1, q1 = fpool(l2.spec(), x1, c1, None, None, l2.weight, l2.bias, s2)
         x2, c2, p2, q2 = fpool(d1.spec(), p1, q1, None, None, d1.weight, d1.bias, sd1)
         x3, c3, p3, q3 = fpool(d2.spec(), p2, q2, None, None, d2.weight, d2.bias, sd2)
         x4, c4 = fwd(d3.spec(), p3, q3, None, None, d3.weight, d3.bias, sd3)
         x34, c34 = fwd(l4.spec(lib.UPCAT_SKIP_FIRST), x3, c3, x4, c4, l4.weight, l4.bias, s4)
         x23, c23 = fwd(l5.spec(lib.UPCAT_SKIP_FIRST), x2, c2, x34, c34, l5.weight, l5.bias, s5)
     tail_out = torch.empty((S.shape[0], 1, oh, ow), device=S.device, dtype=torch.float32)
-    head = d.fused_head and m.nconv.FORWARD_MATH == lib.MATH_BF16X3 and d._head_shapes(l1, l2)
-    first = {"nconv1+nconv2_head": lambda: m.nconv.layer_forward_head(
-        l1.spec(lib.THRESH, 0.01), l2.spec(), S, l1.weight, l1.bias, s1, l2.weight, l2.bias, s2)} if head else {
+    first = {"nconv1+nconv2_head": lambda: fhead(l1.spec(lib.THRESH, 0.01), l2.spec(), S, l1.weight, l1.bias, s1,
+                                                 l2.weight, l2.bias, s2)} if head else {
         "nconv1": lambda: fwd(l1.spec(lib.THRESH, 0.01), S, None, None, None, l1.weight, l1.bias, s1),
         "nconv2": lambda: fpool(l2.spec(), x1, c1, None, None, l2.weight, l2.bias, s2)}
-    calls = {
+    return {
         **first,
         "nconv_down1": lambda: fpool(d1.spec(), p1, q1, None, None, d1.weight, d1.bias, sd1),
         "nconv_down2": lambda: fpool(d2.spec(), p2, q2, None, None, d2.weight, d2.bias, sd2),
@@ -143,36 +150,74 @@ def time_layers(m, net, S, reps=20):
         "nconv5": lambda: fwd(l5.spec(lib.UPCAT_SKIP_FIRST), x2, c2, x34, c34, l5.weight, l5.bias, s5),
         "nconv6+7_tail": lambda: d._fused_tail(l6, l7, s6, s7, x1b, c1b, x23, c23, tail_out),
     }
+
+
+def time_layers(m, net, S, reps=20):
+    """Average device time (us) per launch of each kernel of the inference forward: one HIP-event
+    pair per launch, recorded on the stream the kernel is launched on."""
+    calls = inference_calls(m, net, S)
     out = {}
     stream = torch.cuda.current_stream()
     with torch.no_grad():
         for name, fn in calls.items():
             fn()
             ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
-            for e0, e1 in ev:  # one event pair per launch: device time of the kernel alone
+            for e0, e1 in ev:
                 e0.record(stream)
                 fn()
                 e1.record(stream)
             ev[-1][1].synchronize()
-            out[name] = sum(e0.elapsed_time(e1) for e0, e1 in ev) / reps * 1e3  # us
+            out[name] = sum(e0.elapsed_time(e1) for e0, e1 in ev) / reps * 1e3
     return out
 
 
-# Layers on the bf16x3 matrix-core kernel (fwd_mfma, include/nconv.h NCONV_MATH_BF16X3): output
-# rows per tile, k-steps (4 positions x 8 channels each) and the grid each launch writes.
-MFMA_LAYERS = {"nconv1+nconv2_head": (8, 8, 1), "nconv2": (8, 8, 1), "nconv_down1": (8, 8, 2), "nconv_down2": (8, 8, 4), "nconv_down3": (8, 8, 8),
-               "nconv4": (8, 6, 4), "nconv5": (8, 6, 2), "nconv6+7_tail": (16, 6, 1)}
-# the fused head's nconv1, also on the matrix cores: per tile 3 row groups x 3 column blocks x
-# 2 row pairs x 2 k-steps x 5 MFMAs (3 split products for N, 2 for D: c0 is exact)
+def pmc_traffic(kernel, math, B, H, W):
+    """HBM bytes per launch of `kernel` from the committed PMC summary (profiles/pmc_traffic.json,
+    written by tools/pmc_traffic.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes,
+    FETCH_SIZE doubled per MI355X_MICROARCH.md's gfx950 correction), or None if this kernel was not
+    measured at this configuration."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        d = json.load(open(path))
+        if tuple(d.get("config", ())) != (B, H, W):
+            return None
+        e = d.get("kernels", {}).get(math, {}).get(kernel)
+        return e["hbm_bytes_per_launch"] if e else None
+    except (ValueError, KeyError, TypeError, AttributeError):
+        return None
+
+
+def roofline(layer_us, costs, math, B, H, W, issued_mfma=None):
+    """The roofline object of the dominant (longest) kernel of the forward."""
+    dom = max(layer_us, key=lambda n: layer_us[n])
+    byt, fl = costs[dom]
+    us = layer_us[dom]
+    gbs = byt / (us * 1e-6) / 1e9
+    r = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+         "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(dom, math, B, H, W),
+         "kernel": dom, "kernel_us": round(us, 2), "algorithmic_bytes_per_launch": byt, "flops_per_launch": fl,
+         "useful_fp32_tflops": round(fl / (us * 1e-6) / 1e12, 2), "fp32_peak_tflops": FP32_PEAK_TFLOPS,
+         "fp32_frac": round(fl / (us * 1e-6) / 1e12 / FP32_PEAK_TFLOPS, 4)}
+    if issued_mfma:
+        r["mfma_issued_bf16_tflops"] = round(issued_mfma(dom) / (us * 1e-6) / 1e12, 2)
+        r["mfma_bf16_dense_peak_tflops"] = MFMA_BF16_PEAK_TFLOPS
+    return r
+
+
+# Layers on the bf16x3 matrix-core kernel (fwd_mfma): output rows per tile, k-steps and resolution
+MFMA_LAYERS = {"nconv1+nconv2_head": (8, 8, 1), "nconv2": (8, 8, 1), "nconv_down1": (8, 8, 2),
+               "nconv_down2": (8, 8, 4), "nconv_down3": (8, 8, 8), "nconv4": (8, 6, 4), "nconv5": (8, 6, 2),
+               "nconv6+7_tail": (16, 6, 1)}
 HEAD_NC1_MFMAS_PER_TILE = 3 * 3 * 2 * 2 * 5
 
 
 def mfma_issued_flops(layer, B, H, W):
-    """bf16 MFMA flops one fwd_mfma launch issues: per TH x 32-pixel tile, TH/2 row pairs x 2 column
-    halves x NT k-steps x 6 v_mfma_f32_16x16x32_bf16 (3 split products x {N, D}) of 16384 flops,
-    plus the fused head's nconv1 MFMAs."""
+    """bf16 MFMA flops one fwd_mfma launch issues (6 v_mfma_f32_16x16x32_bf16 per k-step and row
+    pair / column half, plus the fused head's nconv1 MFMAs)."""
     if layer not in MFMA_LAYERS:
-        return None
+        return 0
     th, nt, div = MFMA_LAYERS[layer]
     h, w = H // div, W // div
     tiles = -(-h // th) * -(-w // 32) * B
@@ -180,56 +225,85 @@ def mfma_issued_flops(layer, B, H, W):
     return tiles * ((th // 2) * 2 * nt * 6 + extra) * 16384
 
 
-def pmc_traffic(kernel, B, H, W):
-    """HBM bytes per launch of `kernel` from the committed PMC summary (profiles/pmc_traffic.json,
-    written by tools/pmc_traffic.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes,
-    FETCH_SIZE doubled per MI355X_MICROARCH.md's gfx950 correction), or None if not measured for
-    this configuration."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if not os.path.exists(path):
-        return None
+# ---- CPU baseline ----------------------------------------------------------------------------------
+def host_cores():
+    """(threads this process may use, the machine's physical cores)."""
     try:
-        d = json.load(open(path))
-        e = d.get("kernels", {}).get(kernel)
-        if e and tuple(d.get("config", ())) == (B, H, W):
-            return e["hbm_bytes_per_launch"]
-    except (ValueError, KeyError, TypeError):
-        return None
-    return None
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count() or 1
+    phys = None
+    try:
+        seen = set()
+        cur = {}
+        for line in open("/proc/cpuinfo"):
+            if ":" in line:
+                k, v = (s.strip() for s in line.split(":", 1))
+                cur[k] = v
+            elif cur:
+                seen.add((cur.get("physical id"), cur.get("core id")))
+                cur = {}
+        if cur:
+            seen.add((cur.get("physical id"), cur.get("core id")))
+        phys = len(seen) or None
+    except OSError:
+        pass
+    return usable, phys
 
 
 def cpu_baseline(B, H, W, seconds):
     """The oracle (oracle/nconv_ref.py: the reference's DNET forward restated with the same torch
-    CPU ops; bitwise equal to the reference on the same torch build) timed on this host."""
+    CPU ops; bitwise equal to the reference on the same torch build) timed on this host on every
+    core this process may use: the config-2 workload (B frames, generalized crop, the GPU's crop),
+    and config 1 (nconv1 -> nconv2 -> nconv7, B=1, step1.py:38-39,49)."""
     from oracle import nconv_ref as R
     import nconv_pkg
     m = nconv_pkg.load()
-    threads = min(16, os.cpu_count() or 1)
+    usable, phys = host_cores()
+    threads = usable
     torch.set_num_threads(threads)
     torch.manual_seed(0)
     net = m.SETP1_NCONV()
     params = R.dnet_params_from_state_dict({k: R.softplus_pos(v) if k.endswith(".weight") and "bnorm" not in k
                                             else v for k, v in net.state_dict().items()})
     g = torch.Generator().manual_seed(0)
-    S = sparse_depth(g, 1, H, W, "cpu")
-    with torch.no_grad():
-        R.dnet_forward(S, params)  # warm-up
+    S = sparse_depth(g, B, H, W, "cpu")
+
+    def timed(fn, max_n):
+        fn()  # warm-up
         n, t0 = 0, time.perf_counter()
         while True:
-            R.dnet_forward(S, params)
+            fn()
             n += 1
             el = time.perf_counter() - t0
-            if el >= seconds or n >= 200:
-                break
-    return {"value": n / el, "unit": "frames/sec", "cores": threads, "kind": "port",
-            "sample": f"{n} single-frame {H}x{W} DNET forwards (oracle/nconv_ref.dnet_forward, fp32, "
-                      f"torch CPU, {threads} threads) in {el:.1f} s"}
+            if el >= seconds or n >= max_n:
+                return n, el
+
+    with torch.no_grad():
+        n, el = timed(lambda: R.dnet_forward(S, params, "generalized"), 200)
+        S1 = S[:1]
+        nc = {k: params[k] for k in ("nconv1", "nconv2", "nconv7")}
+
+        def three_layer():
+            c0 = (S1 > 0.01).float()
+            x, c = R.nconv2d(S1, c0, *nc["nconv1"], (1, 1), (2, 2))
+            x, c = R.nconv2d(x, c, *nc["nconv2"], (1, 1), (2, 2))
+            return R.nconv2d(x, c, *nc["nconv7"], (1, 1), (2, 2))
+        n1, el1 = timed(three_layer, 2000)
+    return {"value": round(n * B / el, 3), "unit": "frames/sec", "cores": threads, "kind": "port",
+            "physical_cores_on_host": phys,
+            "sample": f"{n} B={B} {H}x{W} DNET forwards (config-2 workload, generalized crop; "
+                      f"oracle/nconv_ref.dnet_forward, fp32, torch CPU, {threads} threads = every core this "
+                      f"process may use) in {el:.1f} s",
+            "config1_3layer_frames_per_sec": round(n1 / el1, 2),
+            "config1_sample": f"{n1} single-frame {H}x{W} nconv1->nconv2->nconv7 forwards in {el1:.1f} s"}
 
 
+# ---- guided configs ---------------------------------------------------------------------------------
 def guided_forward(m, dev, B, H, W, steps, warmup, rank):
-    """Config 3: SETP2 (RGB-guided, models/step2.py:80-126) forward on B/2 + B/2 frames (rgb0/depth0,
-    rgb1/depth1) per GPU, eval, hipGraph-captured; step 1 runs on the libnconv kernels, the RGB
-    encoder and fusion decoder convolutions on PyTorch-ROCm. Returns frames/sec of this rank."""
+    """Config 3: SETP2 (RGB-guided, models/step2.py:80-126) forward on B/2 + B/2 frames per GPU,
+    eval, hipGraph-captured; step 1 and every dense convolution on libnconv kernels. Returns the
+    timed seconds of this rank."""
     torch.manual_seed(1)
     net = m.SETP2_BP_EXPORT(step1_crop="generalized").to(dev).eval()
     g = torch.Generator().manual_seed(3000 + rank)
@@ -260,16 +334,13 @@ def guided_forward(m, dev, B, H, W, steps, warmup, rank):
     return el
 
 
-def make_guided_train_step(m, dev, B, H, W, rank, kernels=True):
-    """Config 4 per GPU: one SETP2_BP_TRAIN iteration as train_step2.py:60-66 — train mode (frozen
-    step 1, still EnforcePos-drifted; BatchNorm batch statistics), forward on B/2 + B/2 frames,
-    calculate_loss_multi_resolution over the four scales of pair 0 (utils.py:63-71; MSE:
-    use_gradient_loss = False, train_step2.py:21), backward, RCCL all-reduce of the present
-    gradients when several ranks run, AdamW lr 1e-4 / wd 1e-7 (train_step2.py:17-18).
-    kernels=False runs the same step on the PyTorch-ROCm modules (MIOpen) for comparison."""
+def make_guided_train_step(m, dev, B, H, W, rank):
+    """Config 4 per GPU: one SETP2_BP_TRAIN iteration as train_step2.py:60-66 (train mode, frozen
+    step 1 still EnforcePos-drifted, batch-statistics BatchNorm), forward on B/2 + B/2 frames,
+    calculate_loss_multi_resolution (MSE, train_step2.py:21), backward, RCCL all-reduce with
+    several ranks, AdamW lr 1e-4 / wd 1e-7."""
     torch.manual_seed(1)
     model = m.SETP2_BP_TRAIN(None, step1_crop="generalized").to(dev)
-    model.dense_kernels = kernels
     net = m.dp.DataParallelRCCL(model)
     opt = m.train.get_optimizer(net, "adam", 1e-4, 1e-7)
     g = torch.Generator().manual_seed(4000 + rank)
@@ -278,7 +349,7 @@ def make_guided_train_step(m, dev, B, H, W, rank, kernels=True):
     rgb1 = (torch.rand(h, 3, H, W, generator=g) * 255).to(dev)
     d0 = sparse_depth(g, h, H, W, dev)
     d1 = sparse_depth(g, h, H, W, dev)
-    gt = sparse_depth(g, h, 480, 640, dev)  # the loss resizes every scale to 480x640 (utils.py:67)
+    gt = sparse_depth(g, h, 480, 640, dev)
     net.train()
 
     def step():
@@ -291,33 +362,11 @@ def make_guided_train_step(m, dev, B, H, W, rank, kernels=True):
     return step
 
 
-def timed_steps(step, steps, warmup, world, dev, barrier):
-    for i in range(max(warmup, 1)):
-        t0 = time.perf_counter()
-        step()
-        torch.cuda.synchronize()
-        log(f"  warm-up step {i}: {time.perf_counter() - t0:.3f} s")
-    torch.cuda.synchronize()
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        step()
-    torch.cuda.synchronize()
-    barrier()
-    tt = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([tt], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        tt = t.item()
-    return tt
-
-
-def make_train_step(m, dev, B, H, W, world, rank, graph=True):
-    """One step-1 training iteration as train_step1.py:59-65: train-mode forward (EnforcePos
-    drift), calculate_loss on element [0] with the gradient loss, backward, (RCCL gradient
-    all-reduce when world > 1), AdamW lr 1e-2 / wd 1e-7 (train_step1.py:16-17, utils.py:55).
-    graph=True replays the whole iteration from a hipGraph (m.train.GraphedTrainStep)."""
+def make_train_step(m, dev, B, H, W, rank, graph=True):
+    """One step-1 training iteration as train_step1.py:59-65: train-mode forward (EnforcePos drift),
+    calculate_loss(estimated_depth, gt) on the whole batch with the gradient loss (train_step1.py:63),
+    backward, (RCCL gradient all-reduce when several ranks run), AdamW lr 1e-2 / wd 1e-7
+    (train_step1.py:16-17, utils.py:55). graph=True replays the iteration from a hipGraph."""
     torch.manual_seed(0)
     net = m.dp.DataParallelRCCL(m.SETP1_NCONV(crop="generalized").to(dev))
     opt = m.train.get_optimizer(net, "adam", 1e-2, 1e-7, capturable=graph, fused=graph)
@@ -327,8 +376,7 @@ def make_train_step(m, dev, B, H, W, world, rank, graph=True):
     net.train()
 
     def loss_fn(model, S, gt):
-        est = model(S)
-        return m.train.calculate_loss(est[0, :, :, :], gt[0, :, :, :], True)
+        return m.train.calculate_loss(model(S), gt, True)
 
     if graph:
         gstep = m.train.GraphedTrainStep(net, opt, loss_fn, (S, gt))
@@ -343,11 +391,6 @@ def make_train_step(m, dev, B, H, W, world, rank, graph=True):
     return step
 
 
-def log(*msg):
-    """Progress on stderr (a long silent run looks hung to the GPU harness)."""
-    print("[bench]", *msg, file=sys.stderr, flush=True)
-
-
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -360,6 +403,7 @@ def main():
 
     import nconv_pkg
     m = nconv_pkg.load()
+    lib = m._lib
     B, H, W = a.batch, a.height, a.width
     torch.manual_seed(0)
     net = m.SETP1_NCONV(crop="generalized").to(dev)
@@ -367,7 +411,6 @@ def main():
     with torch.no_grad():
         net(torch.zeros(1, 1, 32, 32, device=dev))  # one EnforcePos: positive (trained-like) weights
     net.eval()
-    net.d_net.inference_streams = a.streams
     net.d_net.fused_head = bool(a.fused_head)
     g = torch.Generator().manual_seed(1000 + rank)
     S = sparse_depth(g, B, H, W, dev)
@@ -376,23 +419,31 @@ def main():
         if world > 1:
             dist.barrier()
 
-    def time_forward(steps):
-        """W warm-up passes (hipGraph capture when --graph), then `steps` timed passes between
-        barrier + synchronize; returns (this rank's seconds, max over ranks)."""
+    def max_over_ranks(el):
+        if world > 1:
+            t = torch.tensor([el], device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            return t.item()
+        return el
+
+    def time_forward(Sx, steps, math):
+        """Warm-up passes (hipGraph capture when --graph), then `steps` timed passes between barrier
+        + synchronize; returns the max over ranks of the timed seconds."""
+        m.nconv.FORWARD_MATH = math
         graph = None
         with torch.no_grad():
             for _ in range(max(a.warmup, 1)):
-                net(S)
+                net(Sx)
             if a.graph:
                 s = torch.cuda.Stream()
                 s.wait_stream(torch.cuda.current_stream())
                 with torch.cuda.stream(s):
                     for _ in range(2):
-                        net(S)
+                        net(Sx)
                 torch.cuda.current_stream().wait_stream(s)
                 graph = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(graph):
-                    net(S)
+                    net(Sx)
                 for _ in range(a.warmup):
                     graph.replay()
         torch.cuda.synchronize()
@@ -404,43 +455,53 @@ def main():
                 if graph is not None:
                     graph.replay()
                 else:
-                    net(S)
+                    net(Sx)
         torch.cuda.synchronize()
         barrier()
         el = time.perf_counter() - t0
-        el_max = el
-        if world > 1:
-            t = torch.tensor([el], device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            el_max = t.item()
-        return el, el_max
+        del graph
+        return max_over_ranks(el)
 
-    # ---- forward (headline) ----
-    log("config 2 forward")
-    t_fwd, t_fwd_max = time_forward(a.steps)
-    fps = world * B * a.steps / t_fwd_max
-    graph = a.graph
+    FP32, BF = lib.MATH_FP32, lib.MATH_BF16X3
 
-    # ---- the same forward with exact fp32 products on the vector ALU (NCONV_MATH_FP32) ----
-    fwd_fp32 = None
-    if not a.no_fp32_forward:
-        log("config 2 forward, exact-fp32 arithmetic")
-        math0 = m.nconv.FORWARD_MATH
-        m.nconv.FORWARD_MATH = m._lib.MATH_FP32
-        try:
-            _, t32 = time_forward(a.steps)
-        finally:
-            m.nconv.FORWARD_MATH = math0
-        fwd_fp32 = {"frames_per_sec": round(world * B * a.steps / t32, 2),
-                    "ms_per_step": round(t32 / a.steps * 1e3, 4),
-                    "arith": "exact fp32 products, packed-FP32 vector ALU (fwd_tiled)"}
+    # ---- headline: config 2 forward, exact fp32 ----
+    log("config 2 forward, exact fp32")
+    t_fwd = time_forward(S, a.steps, FP32)
+    fps = world * B * a.steps / t_fwd
 
-    # ---- fwd + bwd + AdamW (config 4b) ----
-    log("config 2 forward done:", round(fps, 1), "frames/s; config 4b training step")
+    fwd_bf = None
+    if not a.no_bf16x3:
+        log("config 2 forward, bf16x3 products")
+        t_bf = time_forward(S, a.steps, BF)
+        fwd_bf = {"frames_per_sec": round(world * B * a.steps / t_bf, 2), "ms_per_step": round(t_bf / a.steps * 1e3, 4),
+                  "dtype": "fp32 io and accumulation, bf16x3 products",
+                  "arith": "8-channel layers' products as split-bf16 matrix-core terms (<= ~1.1e-5 relative per "
+                           "product, inside the 1e-4 forward tolerance; narrower than fp32)",
+                  "whole_pass_hbm_frac": round(PASS_BYTES_PER_FRAME * B * a.steps / t_bf / 1e9 / HBM_PEAK_GBS, 4) if (H, W) == (352, 1216) else None}
+
+    # ---- config 5: B=16 1024x2048 ----
+    c5 = None
+    S5 = None
+    if not a.no_config5:
+        B5, H5, W5 = 16, 1024, 2048
+        log("config 5 forward (B=16 1024x2048)")
+        S5 = sparse_depth(torch.Generator().manual_seed(5000 + rank), B5, H5, W5, dev)
+        k5 = max(3, a.steps // 4)
+        t5 = time_forward(S5, k5, FP32)
+        c5 = {"workload": "config5: DNET forward, B=16 1024x2048 per GPU, generalized crop, exact fp32",
+              "frames_per_sec": round(world * B5 * k5 / t5, 2), "ms_per_step": round(t5 / k5 * 1e3, 3),
+              "steps": k5, "per_gpu_batch": B5}
+        if not a.no_bf16x3:
+            t5b = time_forward(S5, k5, BF)
+            c5["bf16x3_frames_per_sec"] = round(world * B5 * k5 / t5b, 2)
+    m.nconv.FORWARD_MATH = FP32
+
+    # ---- config 4b: fwd + bwd + AdamW ----
     train = None
     if not a.no_train:
+        log("config 4b training step")
         tg = (world == 1) if a.train_graph < 0 else bool(a.train_graph)
-        step = make_train_step(m, dev, B, H, W, world, rank, graph=tg)
+        step = make_train_step(m, dev, B, H, W, rank, graph=tg)
         ks = a.train_steps or a.steps
         for _ in range(max(a.warmup, 1)):
             step()
@@ -452,99 +513,104 @@ def main():
             step()
         torch.cuda.synchronize()
         barrier()
-        tt = time.perf_counter() - t0
-        if world > 1:
-            t = torch.tensor([tt], device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            tt = t.item()
-        train = {"frames_per_sec": round(world * B * ks / tt, 2), "ms_per_step": round(tt / ks * 1e3, 4), "steps": ks,
-                 "hipgraph": tg}
-
-    # ---- config 3: guided forward ----
-    log("config 3 guided forward")
-    guided = None
-    if not a.no_guided:
-        gsteps = max(5, a.steps // 5)
-        el = guided_forward(m, dev, B, H, W, gsteps, min(a.warmup, 3), rank)
-        barrier()
-        if world > 1:
-            t = torch.tensor([el], device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            el = t.item()
-        guided = {"frames_per_sec": round(world * B * gsteps / el, 2), "ms_per_step": round(el / gsteps * 1e3, 3),
-                  "steps": gsteps, "frames_per_step": B * world,
-                  "workload": "config3: SETP2_BP_EXPORT forward, B/2+B/2 frames per GPU, hipGraph"}
-
-    # ---- config 4: guided training step (per GPU B/2 + B/2 frames) ----
-    log("config 4 guided training step")
-    guided_train = None
-    if not a.no_guided_train:
-        gts = max(3, a.steps // 10)
-        tt = timed_steps(make_guided_train_step(m, dev, B, H, W, rank), gts, min(a.warmup, 2), world, dev, barrier)
-        guided_train = {"frames_per_sec": round(world * B * gts / tt, 2), "ms_per_step": round(tt / gts * 1e3, 3),
-                        "steps": gts, "frames_per_step": B * world,
-                        "workload": "config4: SETP2_BP_TRAIN fwd+bwd+AdamW, B/2+B/2 frames per GPU, dense convs "
-                                    "on libnconv MFMA kernels, eager"}
-        log("config 4 done:", guided_train["frames_per_sec"], "frames/s")
-        if a.guided_train_torch:
-            log("config 4 on the PyTorch-ROCm modules")
-            tt = timed_steps(make_guided_train_step(m, dev, B, H, W, rank, kernels=False), gts, min(a.warmup, 2),
-                             world, dev, barrier)
-            guided_train["torch_modules_frames_per_sec"] = round(world * B * gts / tt, 2)
+        tt = max_over_ranks(time.perf_counter() - t0)
+        ms = tt / ks * 1e3
+        fl = (PASS_FLOPS_PER_FRAME + BWD_FLOPS_PER_FRAME) * B * (H * W) / (352 * 1216)
+        by = (PASS_BYTES_PER_FRAME + BWD_BYTES_PER_FRAME) * B * (H * W) / (352 * 1216)
+        train = {"frames_per_sec": round(world * B * ks / tt, 2), "ms_per_step": round(ms, 4), "steps": ks,
+                 "hipgraph": tg, "loss": "calculate_loss(est, gt) on the whole batch (train_step1.py:63)",
+                 "forward_math": "exact fp32 (training forward), exact fp32 backward",
+                 "roofline": {"bound": "fp32", "flops_per_step": fl, "bytes_per_step": by,
+                              "achieved_tflops": round(fl / (ms * 1e-3) / 1e12, 2), "peak_tflops": FP32_PEAK_TFLOPS,
+                              "frac": round(fl / (ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS, 4),
+                              "hbm_frac": round(by / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                              "basis": "SURVEY.md 8(d): forward 6.62 GFLOP / 238.4 MB + backward 12.79 GFLOP / "
+                                       "373.9 MB per 352x1216 frame"}}
+        del step
         torch.cuda.empty_cache()
 
-    # ---- per-kernel times, roofline (rank 0) ----
-    result = None
+    # ---- config 3: guided forward ----
+    guided = None
+    if not a.no_guided:
+        log("config 3 guided forward")
+        gsteps = max(5, a.steps // 5)
+        el = max_over_ranks(guided_forward(m, dev, B, H, W, gsteps, min(a.warmup, 3), rank))
+        fl = (GUIDED_DENSE_FLOPS_PER_FRAME + PASS_FLOPS_PER_FRAME) * B * (H * W) / (352 * 1216)
+        guided = {"frames_per_sec": round(world * B * gsteps / el, 2), "ms_per_step": round(el / gsteps * 1e3, 3),
+                  "steps": gsteps, "frames_per_step": B * world,
+                  "workload": "config3: SETP2_BP_EXPORT forward, B/2+B/2 frames per GPU, hipGraph",
+                  "fp32_tflops": round(fl / (el / gsteps) / 1e12, 2),
+                  "fp32_mfma_frac": round(fl / (el / gsteps) / 1e12 / FP32_PEAK_TFLOPS, 4)}
+        torch.cuda.empty_cache()
+
+    # ---- config 4: guided training step ----
+    guided_train = None
+    if not a.no_guided_train:
+        log("config 4 guided training step")
+        gts = max(3, a.steps // 10)
+        st = make_guided_train_step(m, dev, B, H, W, rank)
+        for _ in range(max(min(a.warmup, 2), 1)):
+            st()
+        torch.cuda.synchronize()
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(gts):
+            st()
+        torch.cuda.synchronize()
+        barrier()
+        tt = max_over_ranks(time.perf_counter() - t0)
+        # forward + input gradient + weight gradient of every dense conv; frozen step 1 forward only
+        fl = (3 * GUIDED_DENSE_FLOPS_PER_FRAME + PASS_FLOPS_PER_FRAME) * B * (H * W) / (352 * 1216)
+        guided_train = {"frames_per_sec": round(world * B * gts / tt, 2), "ms_per_step": round(tt / gts * 1e3, 3),
+                        "steps": gts, "frames_per_step": B * world,
+                        "workload": "config4: SETP2_BP_TRAIN fwd+bwd+AdamW, B/2+B/2 frames per GPU, eager",
+                        "fp32_tflops": round(fl / (tt / gts) / 1e12, 2),
+                        "fp32_mfma_frac": round(fl / (tt / gts) / 1e12 / FP32_PEAK_TFLOPS, 4)}
+        del st
+        torch.cuda.empty_cache()
+
+    # ---- per-kernel times, rooflines, CPU baseline (rank 0) ----
     if rank == 0:
-        log("per-layer kernel times")
+        log("per-kernel times")
+        m.nconv.FORWARD_MATH = FP32
         lt = time_layers(m, net, S)
-        costs = layer_costs(B, H, W)
-        costs["nconv6+7_tail"] = fused_tail_cost(B, H, W)
-        costs["nconv1+nconv2_head"] = head_cost(B, H, W)
-        dom = max(lt, key=lambda n: lt[n])  # kernels of the timed inference pass
-        byt, fl = costs[dom]
-        us = lt[dom]
-        traffic = pmc_traffic(dom, B, H, W)
-        gbs = byt / (us * 1e-6) / 1e9
-        tfl = fl / (us * 1e-6) / 1e12
-        tail_b, tail_f = fused_tail_cost(B, H, W)
-        pass_bytes = 238.44e6 * B if (H, W) == (352, 1216) else None
-        on_mfma = m.nconv.FORWARD_MATH == m._lib.MATH_BF16X3 and dom in MFMA_LAYERS
-        issued = mfma_issued_flops(dom, B, H, W) if on_mfma else None
-        roof = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": f"{dom} ({'fwd_mfma, bf16x3 matrix cores' if on_mfma else 'fwd_tiled, packed FP32'})",
-                "kernel_us": round(us, 2),
-                "algorithmic_bytes_per_launch": byt, "flops_per_launch": fl,
-                "useful_tflops": round(tfl, 2),
-                "mfma_issued_tflops": round(issued / (us * 1e-6) / 1e12, 2) if issued else None,
-                "mfma_bf16_dense_peak_tflops": MFMA_BF16_PEAK_TFLOPS if issued else None,
-                "mfma_frac": round(issued / (us * 1e-6) / 1e12 / MFMA_BF16_PEAK_TFLOPS, 4) if issued else None,
-                "fp32_vector_peak_tflops": FP32_PEAK_TFLOPS,
-                "whole_pass_hbm_frac": round(pass_bytes * a.steps / t_fwd / 1e9 / HBM_PEAK_GBS, 4) if pass_bytes else None}
+        costs = kernel_costs(B, H, W)
+        roof = roofline(lt, costs, "fp32", B, H, W)
+        roof["whole_pass_hbm_frac"] = round(PASS_BYTES_PER_FRAME * B * a.steps / t_fwd / 1e9 / HBM_PEAK_GBS, 4) if (H, W) == (352, 1216) else None
+        if fwd_bf is not None:
+            m.nconv.FORWARD_MATH = BF
+            lt_bf = time_layers(m, net, S)
+            fwd_bf["layer_us"] = {k: round(v, 2) for k, v in lt_bf.items()}
+            fwd_bf["roofline"] = roofline(lt_bf, costs, "bf16x3", B, H, W,
+                                          issued_mfma=lambda k: mfma_issued_flops(k, B, H, W))
+            m.nconv.FORWARD_MATH = FP32
+        if c5 is not None:
+            lt5 = time_layers(m, net, S5, reps=5)
+            c5["layer_us"] = {k: round(v, 2) for k, v in lt5.items()}
+            c5["roofline"] = roofline(lt5, kernel_costs(16, 1024, 2048), "fp32", 16, 1024, 2048)
+            c5["whole_pass_hbm_frac"] = round(1169.4e6 * 16 / (c5["ms_per_step"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
         cpu = None
         if not a.no_cpu_baseline and world == 1:
             log("CPU baseline")
-            cpu = cpu_baseline(1, H, W, a.cpu_seconds)
+            cpu = cpu_baseline(B, H, W, a.cpu_seconds)
         result = {
             "metric": "frames/sec (352x1216 sparse depth, DNET NConv U-Net forward, B=8 per GPU)",
             "value": round(fps, 2), "unit": "frames/sec", "n_gpus": world, "steps": a.steps,
-            "warmup": a.warmup, "ms_per_step": round(t_fwd_max / a.steps * 1e3, 4),
+            "warmup": a.warmup, "ms_per_step": round(t_fwd / a.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
             "data": "synthetic (seeded 5%-dense U(1,80) depth, seeded init + one EnforcePos)",
-            "config": {"workload": "config2: SETP1_NCONV/DNET forward, fused HIP NConv kernels",
+            "config": {"workload": "config2: SETP1_NCONV/DNET forward, fused HIP NConv kernels, exact fp32",
                        "global_batch": B * world, "per_gpu_batch": B, "height": H, "width": W,
                        "crop": "generalized [1:H+1,1:W+1]", "parallelism": f"frame-sharded x{world}",
-                       "hipgraph": bool(graph), "streams": a.streams,
-                       "fused_head": bool(a.fused_head)},
-            "arith": "fp32 in/out and accumulation; 8-channel layers' products as split-bf16 (bf16x3) matrix-core "
-                     "terms (<= ~1.1e-5 relative per product, parity within the 1e-4 forward tolerance)",
-            "fwd_fp32_exact": fwd_fp32,
+                       "hipgraph": bool(a.graph), "fused_head": bool(a.fused_head)},
+            "arith": "exact fp32: every product an fp32 product, fp32 accumulation (NCONV_MATH_FP32)",
+            "layer_us": {k: round(v, 2) for k, v in lt.items()},
+            "roofline": roof,
+            "fwd_bf16x3": fwd_bf,
+            "config5": c5,
             "train_fwd_bwd_adamw": train,
             "guided_fwd": guided,
             "guided_train_fwd_bwd_adamw": guided_train,
-            "layer_us": {k: round(v, 2) for k, v in lt.items()},
-            "roofline": roof,
             "cpu_baseline": cpu,
         }
         if cpu:

@@ -244,7 +244,7 @@ class DNET(nn.Module):
         (l1, l2, d1, d2, d3, l4, l5, l6, l7) = layers
         (s1, s2, sd1, sd2, sd3, s4, s5, s6, s7) = wsum
         f, fp = layer_forward_raw, layer_forward_pooled
-        if self.fused_head and nconv.FORWARD_MATH == _lib.MATH_BF16X3 and self._head_shapes(l1, l2):
+        if self._use_head(l1, l2):
             # nconv1 inside nconv2's staging: its 8-channel output never reaches HBM
             x1, c1, p1, q1 = layer_forward_head(l1.spec(_lib.THRESH, 0.01), l2.spec(), S, l1.weight, l1.bias, s1,
                                                 l2.weight, l2.bias, s2)
@@ -307,6 +307,9 @@ class DNET(nn.Module):
     # Inference evaluates nconv1 inside nconv2's kernel (nconv_fwd_head) when the layers have
     # DNET's geometry; set False to run them as two launches.
     fused_head = True
+
+    def _use_head(self, l1, l2):
+        return self.fused_head and nconv.FORWARD_MATH == _lib.MATH_BF16X3 and self._head_shapes(l1, l2)
 
     @staticmethod
     def _head_shapes(l1, l2):

@@ -19,11 +19,12 @@ from torch.nn.modules.utils import _pair
 from . import _lib
 
 
-# Arithmetic of the forward sums N = W*(x*c), D = W*c (include/nconv.h enum nconv_math): "bf16x3"
-# (default: split-bf16 products on the matrix cores, <= ~1.1e-5 relative per product) or "fp32"
-# (exact fp32 products on the vector ALU). NCONV_FWD_MATH selects it; tests switch this global.
+# Arithmetic of the forward sums N = W*(x*c), D = W*c (include/nconv.h enum nconv_math): "fp32"
+# (default: exact fp32 products, as the reference's F.conv2d) or "bf16x3" (opt-in: split-bf16
+# products on the matrix cores, <= ~1.1e-5 relative per product, faster; a NaN input may spread
+# one row further than in the reference). NCONV_FWD_MATH selects it; tests switch this global.
 _MATH_NAMES = {"bf16x3": _lib.MATH_BF16X3, "fp32": _lib.MATH_FP32}
-FORWARD_MATH = _MATH_NAMES[os.environ.get("NCONV_FWD_MATH", "bf16x3")]
+FORWARD_MATH = _MATH_NAMES[os.environ.get("NCONV_FWD_MATH", "fp32")]
 
 
 def _require_device(t: torch.Tensor, what: str):

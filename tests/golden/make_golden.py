@@ -17,6 +17,11 @@ Fixtures written (small .npz, float32 unless noted):
   f4_masks.npz    c0 threshold masks and max_pool2d argmax with ties / NaN (uint8 / int64)
   f5_guided.npz   SETP2_BP_TRAIN 4-scale + EXPORT outputs, 1+1 frames at 480x640 (step-1 call shim)
   f6_init.npz     torch.manual_seed(0) initial parameters of SETP1_NCONV, SETP2 param sums
+  f7_loss.npz     calculate_loss on a (B, 1, H, W) batch (the training loop's call,
+                  train_step1.py:63) and on element [0], both loss modes, + autograd gradients
+  f8_train_batch.npz  two DNET training steps with the full-batch loss of train_step1.py:63
+
+    python tests/golden/make_golden.py [/root/reference] [f7 f8 ...]   # a subset
 """
 import os
 import sys
@@ -27,7 +32,8 @@ import numpy as np
 import torch
 
 OUT = os.path.dirname(os.path.abspath(__file__))
-REF = sys.argv[1] if len(sys.argv) > 1 else "/root/reference"
+REF = sys.argv[1] if len(sys.argv) > 1 and not sys.argv[1].startswith("f") else "/root/reference"
+ONLY = [a for a in sys.argv[1:] if a.startswith("f")]
 
 
 def import_reference():
@@ -114,8 +120,10 @@ def _ref_calculate_loss():
     return ref_utils
 
 
-def train_fixtures(step1):
-    """F3: two training steps, train_step1.py:59-65 semantics (AdamW lr 1e-2, wd 1e-7)."""
+def train_fixtures(step1, full_batch=False):
+    """F3: two training steps, train_step1.py:59-65 semantics (AdamW lr 1e-2, wd 1e-7), the loss on
+    element [0] (the validation loop's call, utils.py:36). F8 (full_batch): the same with the loss on
+    the whole batch, as the training loop calls it (train_step1.py:63)."""
     ref_utils = _ref_calculate_loss()
     torch.manual_seed(0)
     net = step1.SETP1_NCONV()
@@ -129,7 +137,10 @@ def train_fixtures(step1):
         net.train()
         opt.zero_grad()
         est = net(S)
-        loss = ref_utils.calculate_loss(est[0, :, :, :], gt[0, :, :, :], True)
+        if full_batch:
+            loss = ref_utils.calculate_loss(est, gt, True)
+        else:
+            loss = ref_utils.calculate_loss(est[0, :, :, :], gt[0, :, :, :], True)
         loss.requires_grad_().backward()
         out[f"step{step}_S"], out[f"step{step}_gt"] = np32(S), np32(gt)
         out[f"step{step}_loss"] = np.array(loss.item(), np.float64)
@@ -140,7 +151,32 @@ def train_fixtures(step1):
         opt.step()
         for k, p in net.named_parameters():
             out[f"step{step}_after_{k}"] = np32(p)
-    np.savez_compressed(os.path.join(OUT, "f3_train.npz"), **out)
+    np.savez_compressed(os.path.join(OUT, "f8_train_batch.npz" if full_batch else "f3_train.npz"), **out)
+
+
+def loss_fixtures():
+    """F7: utils.calculate_loss on a (B, 1, H, W) batch and on element [0], both loss modes, with
+    autograd gradients w.r.t. the estimate; includes exact zeros of the Sobel response (flat
+    regions) and masked targets."""
+    ref_utils = _ref_calculate_loss()
+    g = torch.Generator().manual_seed(17)
+    B, H, W = 3, 33, 47
+    est = torch.rand(B, 1, H, W, generator=g) * 80
+    gt = (torch.rand(B, 1, H, W, generator=g) * 79 + 1) * (torch.rand(B, 1, H, W, generator=g) < 0.4)
+    est[1, 0, 0:6, :] = 5.0
+    gt[1, 0, 0:6, :] = 5.0
+    out = {"est": np32(est), "gt": np32(gt)}
+    for tag, sl in (("batch", slice(None)), ("first", 0)):
+        for use_grad in (True, False):
+            e = est.clone().requires_grad_(True)
+            r = e if tag == "batch" else e[sl, :, :, :]
+            t = gt if tag == "batch" else gt[sl, :, :, :]
+            loss = ref_utils.calculate_loss(r, t, use_grad)
+            loss.backward()
+            k = f"{tag}_{int(use_grad)}"
+            out[k + "_loss"] = np.array(loss.item(), np.float64)
+            out[k + "_grad"] = np32(e.grad)
+    np.savez_compressed(os.path.join(OUT, "f7_loss.npz"), **out)
 
 
 def mask_fixtures():
@@ -222,12 +258,13 @@ def init_fixtures(step1, step2):
 def main():
     torch.set_num_threads(1)  # reproducible oneDNN reduction order for the fixtures
     step1, step2 = import_reference()
-    layer_fixtures(step1)
-    dnet_fixtures(step1)
-    train_fixtures(step1)
-    mask_fixtures()
-    guided_fixtures(step1, step2)
-    init_fixtures(step1, step2)
+    jobs = {"f1": lambda: layer_fixtures(step1), "f2": lambda: dnet_fixtures(step1),
+            "f3": lambda: train_fixtures(step1), "f4": mask_fixtures,
+            "f5": lambda: guided_fixtures(step1, step2), "f6": lambda: init_fixtures(step1, step2),
+            "f7": loss_fixtures, "f8": lambda: train_fixtures(step1, full_batch=True)}
+    for k, job in jobs.items():
+        if not ONLY or k in ONLY:
+            job()
     for f in sorted(os.listdir(OUT)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(OUT, f)))

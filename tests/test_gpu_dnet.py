@@ -173,3 +173,53 @@ def test_mid_streams_split_matches_one_stream(nconv_amd, gpu, n):
         torch.cuda.synchronize()
         net.d_net.mid_streams = 1
     assert torch.equal(a, b) and torch.equal(a, c)
+
+
+# ---- full-size configurations (BASELINE.json configs[1] and configs[4]) ----------------------------
+_ORACLE_CACHE = {}
+
+
+def _oracle_out(net, S, crop):
+    key = (tuple(S.shape), crop, float(S.sum()))
+    if key not in _ORACLE_CACHE:
+        _ORACLE_CACHE.clear()
+        _ORACLE_CACHE[key] = R.dnet_forward(S.double(), oracle_params(net), crop)
+    return _ORACLE_CACHE[key]
+
+
+@pytest.fixture(params=["fp32", "bf16x3"])
+def fwd_math(request, nconv_amd, monkeypatch):
+    monkeypatch.setattr(nconv_amd.nconv, "FORWARD_MATH", {"bf16x3": 0, "fp32": 1}[request.param])
+    return request.param
+
+
+@pytest.mark.parametrize("B,H,W,crop", [(8, 352, 1216, "generalized"), (1, 1024, 2048, "generalized"),
+                                        (1, 1024, 2048, "literal")])
+def test_dnet_full_size_vs_oracle(nconv_amd, gpu, fwd_math, B, H, W, crop):
+    """Config 2 (B=8 352x1216: per-image buffer resources, the persistent grids' tile walk across
+    images) and the config-5 plane (1024x2048; the literal crop returns 480x640 there) against the
+    fp64 oracle, both arithmetics."""
+    net = make_net(nconv_amd, crop, gpu)
+    g = torch.Generator().manual_seed(B * 7 + H)
+    S = sparse_depth(g, B, H, W)
+    with torch.no_grad():
+        out = net(S.to(gpu)).double().cpu()
+    ref = _oracle_out(net, S, crop)
+    assert out.shape == ref.shape == (B, 1) + ((H, W) if crop == "generalized" else (min(480, H + 1), min(640, W + 1)))
+    err = (out - ref).abs()
+    bound = 1e-4 * ref.abs() + 1e-4
+    assert (err <= bound).all(), f"max err {err.max():.3e} ratio {(err / bound).max():.3f}"
+
+
+def test_config5_batch16_matches_per_frame(nconv_amd, gpu, fwd_math):
+    """Config 5 shape (B=16, 1024x2048, generalized crop): the batched forward is finite and
+    bitwise equal to sixteen B=1 forwards (frames are independent; checks the per-image offset /
+    resource arithmetic at a 2 M-pixel plane and 16 images)."""
+    net = make_net(nconv_amd, "generalized", gpu)
+    g = torch.Generator().manual_seed(55)
+    S = sparse_depth(g, 16, 1024, 2048).to(gpu)
+    with torch.no_grad():
+        out = net(S)
+        assert out.shape == (16, 1, 1024, 2048) and torch.isfinite(out).all()
+        for i in range(16):
+            assert torch.equal(net(S[i:i + 1]), out[i:i + 1]), f"frame {i}"

@@ -186,12 +186,13 @@ def test_fwd_pooled_outputs(nconv_amd, gpu, shape):
 
 
 @pytest.mark.parametrize("shape", [(2, 48, 128), (1, 37, 70), (1, 352, 1216)])
-def test_fwd_head_matches_unfused(nconv_amd, gpu, shape):
+def test_fwd_head_matches_unfused(nconv_amd, gpu, shape, monkeypatch):
     """nconv_fwd_head (nconv1 evaluated inside nconv2's staging, on the matrix cores in the same
     split-bf16 arithmetic as nconv2) against nconv1 (exact fp32) and nconv2 as two launches: the
     two differ by nconv1's split-product rounding (<= ~1.1e-5 relative per product), so nconv2's
     outputs and pooled copies agree within the forward tolerance, 1e-4 relative; the pooled copies
     must be torch's max_pool2d of the fused outputs exactly."""
+    monkeypatch.setattr(nconv_amd.nconv, "FORWARD_MATH", nconv_amd._lib.MATH_BF16X3)
     B, H, W = shape
     g = torch.Generator().manual_seed(H * W)
     S = (torch.rand(B, 1, H, W, generator=g) * 79 + 1) * (torch.rand(B, 1, H, W, generator=g) < 0.05)
