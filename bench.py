@@ -43,6 +43,14 @@ PASS_FLOPS_PER_FRAME = 6.620e9
 BWD_BYTES_PER_FRAME = 373.9e6    # SURVEY.md 8(d) backward estimate, 352x1216
 BWD_FLOPS_PER_FRAME = 12.79e9
 GUIDED_DENSE_FLOPS_PER_FRAME = 133.6e9  # RGB encoder 7.94 + fusion decoder 125.69 GFLOP
+MATH_DTYPE = {"fp32": "fp32", "bf16x9": "fp32", "bf16x3": "fp32 io and accumulation, bf16x3 products"}
+MATH_ARITH = {
+    "fp32": "exact fp32: every product an fp32 fmaf product on the vector ALU, fp32 accumulation (NCONV_MATH_FP32)",
+    "bf16x9": "exact products: both operands split into three bf16 parts (an exact decomposition), all nine "
+              "partial products (each exact in fp32) accumulated in fp32 on the matrix cores; nconv7 and "
+              "non-DNET shapes on the vector ALU (NCONV_MATH_BF16X9)",
+    "bf16x3": "8-channel layers' products as two-part split-bf16 matrix-core terms (<= ~1.1e-5 relative per "
+              "product, inside the 1e-4 forward tolerance; narrower than fp32) (NCONV_MATH_BF16X3)"}
 LAYERS = ("nconv1", "nconv2", "nconv_down1", "nconv_down2", "nconv_down3", "nconv4", "nconv5", "nconv6", "nconv7")
 
 
@@ -57,7 +65,10 @@ def parse():
     p.add_argument("--train-steps", type=int, default=None, help="timed fwd+bwd steps (default: --steps)")
     p.add_argument("--no-train", action="store_true")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--no-bf16x3", action="store_true", help="skip the split-bf16 forward reported beside the headline")
+    p.add_argument("--math", default="fp32", choices=("fp32", "bf16x9", "bf16x3"),
+                   help="forward arithmetic of the headline (include/nconv.h enum nconv_math)")
+    p.add_argument("--alt-math", default="bf16x9,bf16x3", type=lambda v: [x for x in v.split(",") if x],
+                   help="other arithmetics measured beside the headline (comma list; '' for none)")
     p.add_argument("--no-config5", action="store_true", help="skip the B=16 1024x2048 forward (config 5)")
     p.add_argument("--no-guided", action="store_true", help="skip the config-3 guided forward measurement")
     p.add_argument("--no-guided-train", action="store_true", help="skip the config-4 guided training step")
@@ -154,21 +165,24 @@ def inference_calls(m, net, S):
 
 def time_layers(m, net, S, reps=20):
     """Average device time (us) per launch of each kernel of the inference forward: one HIP-event
-    pair per launch, recorded on the stream the kernel is launched on."""
+    pair per launch, recorded on the stream the kernel is launched on. The launches run in the
+    forward's own order, pass after pass (not one kernel repeated back to back), so each kernel
+    meets the clock and cache state it has inside the real forward."""
     calls = inference_calls(m, net, S)
-    out = {}
     stream = torch.cuda.current_stream()
+    ev = {name: [] for name in calls}
     with torch.no_grad():
-        for name, fn in calls.items():
+        for fn in calls.values():
             fn()
-            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
-            for e0, e1 in ev:
+        for _ in range(reps):
+            for name, fn in calls.items():
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(stream)
                 fn()
                 e1.record(stream)
-            ev[-1][1].synchronize()
-            out[name] = sum(e0.elapsed_time(e1) for e0, e1 in ev) / reps * 1e3
-    return out
+                ev[name].append((e0, e1))
+    torch.cuda.synchronize()
+    return {name: sum(e0.elapsed_time(e1) for e0, e1 in pairs) / len(pairs) * 1e3 for name, pairs in ev.items()}
 
 
 def pmc_traffic(kernel, math, B, H, W):
@@ -206,23 +220,27 @@ def roofline(layer_us, costs, math, B, H, W, issued_mfma=None):
     return r
 
 
-# Layers on the bf16x3 matrix-core kernel (fwd_mfma): output rows per tile, k-steps and resolution
+# Layers on the matrix-core kernel (fwd_mfma): output rows per tile, k-steps and resolution
 MFMA_LAYERS = {"nconv1+nconv2_head": (8, 8, 1), "nconv2": (8, 8, 1), "nconv_down1": (8, 8, 2),
                "nconv_down2": (8, 8, 4), "nconv_down3": (8, 8, 8), "nconv4": (8, 6, 4), "nconv5": (8, 6, 2),
                "nconv6+7_tail": (16, 6, 1)}
-HEAD_NC1_MFMAS_PER_TILE = 3 * 3 * 2 * 2 * 5
+# v_mfma_f32_16x16x32_bf16 per {N, D} k-step and per head nconv1 k-step (N terms + D terms)
+MFMA_TERMS = {"bf16x3": (6, 5), "bf16x9": (18, 12)}
 
 
-def mfma_issued_flops(layer, B, H, W):
-    """bf16 MFMA flops one fwd_mfma launch issues (6 v_mfma_f32_16x16x32_bf16 per k-step and row
-    pair / column half, plus the fused head's nconv1 MFMAs)."""
-    if layer not in MFMA_LAYERS:
+def mfma_issued_flops(layer, B, H, W, math):
+    """bf16 MFMA flops one fwd_mfma launch issues (the split terms per k-step and row pair /
+    column half, plus the fused head's nconv1 MFMAs: 3 x 3 blocks x 2 row pairs x 2 k-steps)."""
+    if layer not in MFMA_LAYERS or math not in MFMA_TERMS:
         return 0
     th, nt, div = MFMA_LAYERS[layer]
+    if math == "bf16x9" and layer == "nconv6+7_tail":
+        th = 8
+    per_k, head_k = MFMA_TERMS[math]
     h, w = H // div, W // div
     tiles = -(-h // th) * -(-w // 32) * B
-    extra = HEAD_NC1_MFMAS_PER_TILE if layer == "nconv1+nconv2_head" else 0
-    return tiles * ((th // 2) * 2 * nt * 6 + extra) * 16384
+    extra = 3 * 3 * 2 * 2 * head_k if layer == "nconv1+nconv2_head" else 0
+    return tiles * ((th // 2) * 2 * nt * per_k + extra) * 16384
 
 
 # ---- CPU baseline ----------------------------------------------------------------------------------
@@ -462,22 +480,25 @@ def main():
         del graph
         return max_over_ranks(el)
 
-    FP32, BF = lib.MATH_FP32, lib.MATH_BF16X3
+    MATHS = {"fp32": lib.MATH_FP32, "bf16x9": lib.MATH_BF16X9, "bf16x3": lib.MATH_BF16X3}
+    HEAD = MATHS[a.math]
+    pass_frac = lambda t, k: round(PASS_BYTES_PER_FRAME * B * k / t / 1e9 / HBM_PEAK_GBS, 4) \
+        if (H, W) == (352, 1216) else None
 
-    # ---- headline: config 2 forward, exact fp32 ----
-    log("config 2 forward, exact fp32")
-    t_fwd = time_forward(S, a.steps, FP32)
+    # ---- headline: config 2 forward ----
+    log(f"config 2 forward, {a.math}")
+    t_fwd = time_forward(S, a.steps, HEAD)
     fps = world * B * a.steps / t_fwd
 
-    fwd_bf = None
-    if not a.no_bf16x3:
-        log("config 2 forward, bf16x3 products")
-        t_bf = time_forward(S, a.steps, BF)
-        fwd_bf = {"frames_per_sec": round(world * B * a.steps / t_bf, 2), "ms_per_step": round(t_bf / a.steps * 1e3, 4),
-                  "dtype": "fp32 io and accumulation, bf16x3 products",
-                  "arith": "8-channel layers' products as split-bf16 matrix-core terms (<= ~1.1e-5 relative per "
-                           "product, inside the 1e-4 forward tolerance; narrower than fp32)",
-                  "whole_pass_hbm_frac": round(PASS_BYTES_PER_FRAME * B * a.steps / t_bf / 1e9 / HBM_PEAK_GBS, 4) if (H, W) == (352, 1216) else None}
+    # ---- the same forward in the other arithmetics ----
+    alt = {}
+    for name in a.alt_math:
+        if name == a.math:
+            continue
+        log(f"config 2 forward, {name}")
+        t = time_forward(S, a.steps, MATHS[name])
+        alt[name] = {"frames_per_sec": round(world * B * a.steps / t, 2), "ms_per_step": round(t / a.steps * 1e3, 4),
+                     "dtype": MATH_DTYPE[name], "arith": MATH_ARITH[name], "whole_pass_hbm_frac": pass_frac(t, a.steps)}
 
     # ---- config 5: B=16 1024x2048 ----
     c5 = None
@@ -487,14 +508,15 @@ def main():
         log("config 5 forward (B=16 1024x2048)")
         S5 = sparse_depth(torch.Generator().manual_seed(5000 + rank), B5, H5, W5, dev)
         k5 = max(3, a.steps // 4)
-        t5 = time_forward(S5, k5, FP32)
-        c5 = {"workload": "config5: DNET forward, B=16 1024x2048 per GPU, generalized crop, exact fp32",
+        t5 = time_forward(S5, k5, HEAD)
+        c5 = {"workload": f"config5: DNET forward, B=16 1024x2048 per GPU, generalized crop, {a.math}",
               "frames_per_sec": round(world * B5 * k5 / t5, 2), "ms_per_step": round(t5 / k5 * 1e3, 3),
               "steps": k5, "per_gpu_batch": B5}
-        if not a.no_bf16x3:
-            t5b = time_forward(S5, k5, BF)
-            c5["bf16x3_frames_per_sec"] = round(world * B5 * k5 / t5b, 2)
-    m.nconv.FORWARD_MATH = FP32
+        for name in a.alt_math:
+            if name != a.math:
+                t5b = time_forward(S5, k5, MATHS[name])
+                c5[f"{name}_frames_per_sec"] = round(world * B5 * k5 / t5b, 2)
+    m.nconv.FORWARD_MATH = lib.MATH_FP32
 
     # ---- config 4b: fwd + bwd + AdamW ----
     train = None
@@ -572,23 +594,26 @@ def main():
     # ---- per-kernel times, rooflines, CPU baseline (rank 0) ----
     if rank == 0:
         log("per-kernel times")
-        m.nconv.FORWARD_MATH = FP32
-        lt = time_layers(m, net, S)
         costs = kernel_costs(B, H, W)
-        roof = roofline(lt, costs, "fp32", B, H, W)
-        roof["whole_pass_hbm_frac"] = round(PASS_BYTES_PER_FRAME * B * a.steps / t_fwd / 1e9 / HBM_PEAK_GBS, 4) if (H, W) == (352, 1216) else None
-        if fwd_bf is not None:
-            m.nconv.FORWARD_MATH = BF
-            lt_bf = time_layers(m, net, S)
-            fwd_bf["layer_us"] = {k: round(v, 2) for k, v in lt_bf.items()}
-            fwd_bf["roofline"] = roofline(lt_bf, costs, "bf16x3", B, H, W,
-                                          issued_mfma=lambda k: mfma_issued_flops(k, B, H, W))
-            m.nconv.FORWARD_MATH = FP32
+        m.nconv.FORWARD_MATH = HEAD
+        lt = time_layers(m, net, S)
+        issued = (lambda k: mfma_issued_flops(k, B, H, W, a.math)) if a.math in MFMA_TERMS else None
+        roof = roofline(lt, costs, a.math, B, H, W, issued_mfma=issued)
+        roof["whole_pass_hbm_frac"] = pass_frac(t_fwd, a.steps)
+        for name, rec in alt.items():
+            m.nconv.FORWARD_MATH = MATHS[name]
+            lt_a = time_layers(m, net, S)
+            rec["layer_us"] = {k: round(v, 2) for k, v in lt_a.items()}
+            rec["roofline"] = roofline(lt_a, costs, name, B, H, W,
+                                       issued_mfma=(lambda k, n=name: mfma_issued_flops(k, B, H, W, n))
+                                       if name in MFMA_TERMS else None)
         if c5 is not None:
+            m.nconv.FORWARD_MATH = HEAD
             lt5 = time_layers(m, net, S5, reps=5)
             c5["layer_us"] = {k: round(v, 2) for k, v in lt5.items()}
-            c5["roofline"] = roofline(lt5, kernel_costs(16, 1024, 2048), "fp32", 16, 1024, 2048)
+            c5["roofline"] = roofline(lt5, kernel_costs(16, 1024, 2048), a.math, 16, 1024, 2048)
             c5["whole_pass_hbm_frac"] = round(1169.4e6 * 16 / (c5["ms_per_step"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+        m.nconv.FORWARD_MATH = lib.MATH_FP32
         cpu = None
         if not a.no_cpu_baseline and world == 1:
             log("CPU baseline")
@@ -597,16 +622,16 @@ def main():
             "metric": "frames/sec (352x1216 sparse depth, DNET NConv U-Net forward, B=8 per GPU)",
             "value": round(fps, 2), "unit": "frames/sec", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(t_fwd / a.steps * 1e3, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": MATH_DTYPE[a.math],
             "data": "synthetic (seeded 5%-dense U(1,80) depth, seeded init + one EnforcePos)",
-            "config": {"workload": "config2: SETP1_NCONV/DNET forward, fused HIP NConv kernels, exact fp32",
+            "config": {"workload": f"config2: SETP1_NCONV/DNET forward, fused HIP NConv kernels, {a.math}",
                        "global_batch": B * world, "per_gpu_batch": B, "height": H, "width": W,
                        "crop": "generalized [1:H+1,1:W+1]", "parallelism": f"frame-sharded x{world}",
                        "hipgraph": bool(a.graph), "fused_head": bool(a.fused_head)},
-            "arith": "exact fp32: every product an fp32 product, fp32 accumulation (NCONV_MATH_FP32)",
+            "arith": MATH_ARITH[a.math],
             "layer_us": {k: round(v, 2) for k, v in lt.items()},
             "roofline": roof,
-            "fwd_bf16x3": fwd_bf,
+            "fwd_other_arith": alt,
             "config5": c5,
             "train_fwd_bwd_adamw": train,
             "guided_fwd": guided,

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define NCONV_ABI_VERSION 11
+#define NCONV_ABI_VERSION 12
 
 /* How a layer's input (data x, confidence c) is produced from its source tensors. These are the
  * DNET glue ops fused into the layer's load stage (models/step1.py:53,61-90). */
@@ -41,7 +41,11 @@ enum nconv_math {
     NCONV_MATH_BF16X3 = 0, /* default: bf16 matrix cores on split operands, v = hi + lo, products
                               hi*hi + lo*hi + hi*lo in fp32 (<= ~1.1e-5 relative per product), for
                               the 8-output-channel 5x5 (8 in) / 3x3 (16 in) layers; others FP32 */
-    NCONV_MATH_FP32 = 1    /* exact fp32 products on the vector ALU (packed FP32 FMA) */
+    NCONV_MATH_FP32 = 1,   /* exact fp32 products on the vector ALU (packed FP32 FMA) */
+    NCONV_MATH_BF16X9 = 2  /* exact products on the bf16 matrix cores: v = v0 + v1 + v2 and
+                              w = w0 + w1 + w2 (three bf16 parts, an exact decomposition), all nine
+                              partial products (each exact in fp32) accumulated in fp32, for the same
+                              layers as BF16X3; others FP32 */
 };
 
 /* One source tensor pair (data, confidence), physical shape (B, C, H, W). */
@@ -101,7 +105,7 @@ int nconv_fwd_pooled(const nconv_layer* L, float* y, float* cout, float* y_pool,
  * tile (step1.py:58; L2: 8 -> 8, 5x5, padding 2, stride 1; its sources are not read), so nconv1's
  * 8-channel output never reaches HBM. Writes nconv2's y, cout (B, 8, H, W) and their 2x2 max-pooled
  * copies (B, 8, H/2, W/2) like nconv_fwd_pooled. Matrix-core math only (L2->math ==
- * NCONV_MATH_BF16X3, which nconv1 then uses as well); -EOPNOTSUPP otherwise. */
+ * NCONV_MATH_BF16X3 or NCONV_MATH_BF16X9, which nconv1 then uses as well); -EOPNOTSUPP otherwise. */
 int nconv_fwd_head(const nconv_layer* L1, const nconv_layer* L2, float* y, float* cout, float* y_pool,
                    float* cout_pool, void* stream);
 

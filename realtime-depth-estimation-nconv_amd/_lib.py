@@ -13,13 +13,13 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # NCONV_LIB: an alternative build of the same library (kernel-tuning experiments)
 LIB_PATH = os.environ.get("NCONV_LIB") or os.path.join(_HERE, "libnconv.so")
-ABI_VERSION = 11
+ABI_VERSION = 12
 BWD_ACCUMULATE = 1
 
 # enum nconv_load_mode
 PLAIN, THRESH, POOL2, UPCAT_SKIP_FIRST, UPCAT_UP_FIRST = 0, 1, 2, 3, 4
 # enum nconv_math
-MATH_BF16X3, MATH_FP32 = 0, 1
+MATH_BF16X3, MATH_FP32, MATH_BF16X9 = 0, 1, 2
 # enum nconv_dense_kind
 DENSE_3X3, DENSE_1X1, DENSE_TRANSPOSED_4X4, DENSE_CONV4X4_S2 = 0, 1, 2, 3
 

@@ -26,7 +26,7 @@ const char* validate(const nconv_layer* L, bool need_c) {
     if (ho != L->Ho || wo != L->Wo) return "Ho/Wo inconsistent with H/W/kernel/stride/padding/dilation";
     if (!L->weight || !L->bias || !L->wsum) return "null weight/bias/wsum";
     if (!L->a.x) return "null source a.x";
-    if (L->math != NCONV_MATH_BF16X3 && L->math != NCONV_MATH_FP32) return "unknown math (enum nconv_math)";
+    if (L->math != NCONV_MATH_BF16X3 && L->math != NCONV_MATH_FP32 && L->math != NCONV_MATH_BF16X9) return "unknown math (enum nconv_math)";
     switch (L->load_mode) {
         case NCONV_LOAD_PLAIN:
             if (!L->a.c && need_c) return "null source a.c";
@@ -151,7 +151,8 @@ int nconv_fwd_head(const nconv_layer* L1, const nconv_layer* L2, float* y, float
         return fail(-22, fn, "nconv2 geometry inconsistent with nconv1's output");
     if (L2->Ho < 2 || L2->Wo < 2) return fail(-22, fn, "output too small to pool");
     if (!L2->weight || !L2->bias || !L2->wsum) return fail(-22, fn, "null nconv2 weight/bias/wsum");
-    if (L2->math != NCONV_MATH_BF16X3) return fail(-95, fn, "the fused head runs on the matrix cores only");
+    if (L2->math != NCONV_MATH_BF16X3 && L2->math != NCONV_MATH_BF16X9)
+        return fail(-95, fn, "the fused head runs on the matrix cores only");
     nconv_layer l2 = *L2;
     l2.load_mode = NCONV_LOAD_PLAIN;
     l2.a = L1->a;  // (the kernel reads the sparse depth through TailArgs)

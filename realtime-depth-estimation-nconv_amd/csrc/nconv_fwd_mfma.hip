@@ -27,6 +27,14 @@
 // y = N/(D+eps)+b, cout = D/s, 16-B stores, optionally the fused 2x2 max-pooled copies (rows s=0/1
 // of a pixel pair sit in lanes l, l^8) or nconv7 (1x1 over the 8 channels = lanes l^1, l^2, l^4)
 // with the crop, as the VALU kernels of nconv_fwd.hip do.
+//
+// Exact products (NCONV_MATH_BF16X9): with three parts per operand, v = v0 + v1 + v2 (v0 = bf16(v),
+// v1 = bf16(v - v0), v2 = v - v0 - v1, which has at most 8 significant bits and is exact in bf16),
+// the decomposition is exact, every partial product vi*wj of two 8-bit significands is exact in
+// fp32, and all nine enter the fp32 accumulator: sum_ij vi*wj = v*w exactly, so the only rounding
+// is the fp32 accumulation, as in any fp32 convolution. The kernels are the same with NP = 3 parts
+// (three planes per operand, three B fragments per k-step) and nine MFMAs per {N, D} k-step,
+// smallest terms first.
 #include <cstdlib>
 #include "nconv_internal.h"
 
@@ -40,7 +48,7 @@ constexpr int kMfThreads = 256;
 
 enum MfEpi { kEpiPlain = 0, kEpiPool = 1, kEpiTail = 2 };
 
-template <int CIN, int K, int TH>
+template <int CIN, int K, int TH, int NP = 2>
 struct MfCfg {
     static constexpr int G = CIN / 8;  // 8-channel groups (one bf16x8 per position and part)
     static constexpr int TW = 32;      // two 16-column MFMA tiles
@@ -48,48 +56,75 @@ struct MfCfg {
     static constexpr int NPOS = IH * IW;
     static constexpr int NE = (NPOS + kMfThreads - 1) / kMfThreads;  // positions per thread
     static constexpr int PSTRIDE = NPOS * 16;                        // bytes of one plane
-    static constexpr int LDS_IN = 4 * G * PSTRIDE;                   // [g][part][pos] bf16x8
+    static constexpr int NPL = 2 * NP;                               // planes: x*c parts, c parts
+    static constexpr int LDS_IN = NPL * G * PSTRIDE;                 // [g][plane][pos] bf16x8
     static constexpr int NKP = (K + 1) * K * G;                      // k positions (kh', kw, g)
     static constexpr int NT = (NKP + 3) / 4;                         // k-steps (4 positions each)
     static constexpr int NRP = TH / 2;                               // row pairs, NRP / 4 per wave
     static_assert(CIN % 8 == 0 && NRP % 4 == 0, "tile shape");
 };
 
+// Split products: which (data part i, weight part j) terms a math mode forms. Two parts (bf16x3):
+// i + j <= 1 (the lo*lo term dropped). Three parts (bf16x9): all nine (exact products).
+template <int NP>
+__device__ __forceinline__ constexpr bool use_term(int i, int j) {
+    return NP == 2 ? i + j <= 1 : true;
+}
+
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+// v = sum of NP bf16 parts, each the bf16 rounding of what the previous parts left (VT: a bf16
+// vector of N lanes)
+template <int NP, typename VT, int N>
+__device__ __forceinline__ void split_parts(const float (&v)[N], VT (&out)[NP]) {
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        float r = v[j];
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+            const __bf16 h = (__bf16)r;
+            out[p][j] = h;
+            if (p + 1 < NP) r -= (float)h;
+        }
+    }
+}
+
 constexpr unsigned kOOB = 0x80000000u;
 constexpr int kOutPitch = 36;  // floats per row of a wave's output-transpose region
 constexpr int kTrBytes = 4 * 16 * kOutPitch * 4;  // four waves' regions (y, then cout, through one)
 
-#ifdef NCONV_EXP_MF_NOSTORE
-#define NCONV_STORE_OFF(o) (((o) & 0u) | 0x80000000u)
-#else
-#define NCONV_STORE_OFF(o) (o)
-#endif
 __device__ __forceinline__ void st_f32(__amdgpu_buffer_rsrc_t r, unsigned off, float v) {
-    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, (int)NCONV_STORE_OFF(off), 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, (int)off, 0, 0);
 }
 __device__ __forceinline__ void st_f2(__amdgpu_buffer_rsrc_t r, unsigned off, f2 v) {
     typedef unsigned u2 __attribute__((ext_vector_type(2)));
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v), r, (int)NCONV_STORE_OFF(off), 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v), r, (int)off, 0, 0);
 }
 __device__ __forceinline__ void st_f4(__amdgpu_buffer_rsrc_t r, unsigned off, f4 v) {
     typedef unsigned u4 __attribute__((ext_vector_type(4)));
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, v), r, (int)NCONV_STORE_OFF(off), 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, v), r, (int)off, 0, 0);
 }
 
-__device__ __forceinline__ void split8(const float (&v)[8], bf16x8& hi, bf16x8& lo) {
+// One position's 8 channels of {x*c, c} into the planes of a tile (base = plane 0 of the
+// position's channel group): x*c parts in planes 0 .. NP-1, c parts in NP .. 2NP-1.
+template <typename C>
+__device__ __forceinline__ void store_planes(unsigned char* base, const float (&p)[8], const float (&q)[8]) {
+    constexpr int NP = C::NPL / 2;
+    bf16x8 sp[NP], sq[NP];
+    split_parts<NP>(p, sp);
+    split_parts<NP>(q, sq);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        const __bf16 h = (__bf16)v[j];
-        hi[j] = h;
-        lo[j] = (__bf16)(v[j] - (float)h);
+    for (int i = 0; i < NP; ++i) {
+        *reinterpret_cast<bf16x8*>(base + i * C::PSTRIDE) = sp[i];
+        *reinterpret_cast<bf16x8*>(base + (NP + i) * C::PSTRIDE) = sq[i];
     }
 }
 
 // Staging of one tile's halo: per thread NE positions x CIN channels of {x, c}, loaded into
-// registers (load: glue evaluated, no wait) and later split into the four bf16x8 planes (store).
-template <int CIN, int K, int MODE, int TH>
+// registers (load: glue evaluated, no wait) and later split into the 2 NP bf16x8 planes (store).
+template <int CIN, int K, int MODE, int TH, int NP>
 struct MfStage {
-    using C = MfCfg<CIN, K, TH>;
+    using C = MfCfg<CIN, K, TH, NP>;
     static constexpr bool UP = MODE == NCONV_LOAD_UPCAT_SKIP_FIRST || MODE == NCONV_LOAD_UPCAT_UP_FIRST;
     static constexpr unsigned OOB = 0x80000000u;
     float xv[C::NE][CIN], cv[C::NE][CIN];
@@ -152,19 +187,6 @@ struct MfStage {
                 }
 #pragma unroll
                 for (int k = 0; k < C::NE; ++k) {
-#ifdef NCONV_EXP_MF_NOLOAD
-                    xv[k][ci] = (float)(ga[k] & 255);
-                    cv[k][ci] = 0.5f;
-#else
-#ifdef NCONV_MF_PERCHAN_RSRC
-                    {
-                        const ChanSrc cs_ = chan_src<MODE>(d, b, ci);
-                        const __amdgpu_buffer_rsrc_t rx = plane_rsrc(cs_.x, cs_.bytes), rc = plane_rsrc(cs_.c, cs_.bytes);
-                        const unsigned o = UP && cs_.kind == kUp ? gb[UP ? k : 0] : ga[k];
-                        xv[k][ci] = ld_f32(rx, o);
-                        cv[k][ci] = ld_f32(rc, o);
-                    }
-#else
                     if (!UP || from_a) {
                         xv[k][ci] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rax, ga[k], cs * pa, 0));
                         cv[k][ci] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rac, ga[k], cs * pa, 0));
@@ -172,8 +194,6 @@ struct MfStage {
                         xv[k][ci] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rbx, gb[UP ? k : 0], cs * pb, 0));
                         cv[k][ci] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rbc, gb[UP ? k : 0], cs * pb, 0));
                     }
-#endif
-#endif
                 }
             }
         }
@@ -203,14 +223,7 @@ struct MfStage {
                     q[j] = cv[k][8 * g + j];
                     p[j] = xv[k][8 * g + j] * q[j];
                 }
-                bf16x8 h, l;
-                unsigned char* base = lds + g * 4 * C::PSTRIDE + e * 16;
-                split8(p, h, l);
-                *reinterpret_cast<bf16x8*>(base) = h;
-                *reinterpret_cast<bf16x8*>(base + C::PSTRIDE) = l;
-                split8(q, h, l);
-                *reinterpret_cast<bf16x8*>(base + 2 * C::PSTRIDE) = h;
-                *reinterpret_cast<bf16x8*>(base + 3 * C::PSTRIDE) = l;
+                store_planes<C>(lds + g * C::NPL * C::PSTRIDE + e * 16, p, q);
             }
         }
     }
@@ -226,17 +239,17 @@ __device__ __forceinline__ int floor_div4(int v) { return v >> 2; }  // arithmet
 // and for the upsample-concat modes source b at its own half resolution (IH/2+1 rows x 6 vectors),
 // the exact 2x nearest upsampling being applied when the planes are formed. Sections (a.x, a.c,
 // b.x, b.c) are padded to whole 1-KiB pieces; LDS is lane-linear within a piece.
-template <int CIN, int K, int MODE, int TH>
+template <int CIN, int K, int MODE, int TH, int NP>
 struct DmaStage {
-    using C = MfCfg<CIN, K, TH>;
+    using C = MfCfg<CIN, K, TH, NP>;
     static constexpr bool UP = MODE == NCONV_LOAD_UPCAT_SKIP_FIRST || MODE == NCONV_LOAD_UPCAT_UP_FIRST;
     static constexpr int CA = UP ? CIN / 2 : CIN, CB = UP ? CIN / 2 : 0;
     static constexpr int NVA = 10, SRA = C::IH;            // source a: vectors per row, rows
     static constexpr int NVB = 6, SRB = C::IH / 2 + 1;     // source b (half resolution)
     static constexpr int PA = (CA * SRA * NVA + 63) / 64;  // 1-KiB pieces per tensor of source a
     static constexpr int PB = UP ? (CB * SRB * NVB + 63) / 64 : 0;
-    static constexpr int NP = 2 * PA + 2 * PB;
-    static constexpr int BYTES = NP * 1024;
+    static constexpr int NPC = 2 * PA + 2 * PB;  // pieces
+    static constexpr int BYTES = NPC * 1024;
     static_assert(4 * NVA >= C::IW + 3 && 4 * NVB >= (C::IW + 1) / 2 + 4, "staged columns cover the halo");
 
     static constexpr bool SELF_SYNC = true;
@@ -245,7 +258,7 @@ struct DmaStage {
         const nconv_layer& L = d.L;
         const int wave = tid >> 6, lane = tid & 63;
 #pragma unroll 1
-        for (int j = wave; j < NP; j += 4) {  // wave-uniform piece index
+        for (int j = wave; j < NPC; j += 4) {  // wave-uniform piece index
             const int sec = j < 2 * PA ? j / PA : 2 + (j - 2 * PA) / PB;
             const int jj = sec < 2 ? j - sec * PA : j - 2 * PA - (sec - 2) * PB;
             const bool a = sec < 2;
@@ -305,14 +318,7 @@ struct DmaStage {
                     q[j] = cv;
                     p[j] = xv * cv;
                 }
-                bf16x8 hh, ll;
-                unsigned char* base = lds + g * 4 * C::PSTRIDE + e * 16;
-                split8(p, hh, ll);
-                *reinterpret_cast<bf16x8*>(base) = hh;
-                *reinterpret_cast<bf16x8*>(base + C::PSTRIDE) = ll;
-                split8(q, hh, ll);
-                *reinterpret_cast<bf16x8*>(base + 2 * C::PSTRIDE) = hh;
-                *reinterpret_cast<bf16x8*>(base + 3 * C::PSTRIDE) = ll;
+                store_planes<C>(lds + g * C::NPL * C::PSTRIDE + e * 16, p, q);
             }
         }
     }
@@ -324,9 +330,23 @@ struct DmaStage {
 // values equal the unfused layer's), then feeds the split-bf16 planes like a loaded input.
 constexpr int kModeHead = 100;
 
-template <int TH>
+// One position's 4 channels (a bf16x4 half of the position's 16-byte slot) into the planes.
+template <typename C>
+__device__ __forceinline__ void store_half_planes(unsigned char* base, const float (&p)[4], const float (&q)[4]) {
+    constexpr int NP = C::NPL / 2;
+    bf16x4 sp[NP], sq[NP];
+    split_parts<NP>(p, sp);
+    split_parts<NP>(q, sq);
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+        *reinterpret_cast<bf16x4*>(base + i * C::PSTRIDE) = sp[i];
+        *reinterpret_cast<bf16x4*>(base + (NP + i) * C::PSTRIDE) = sq[i];
+    }
+}
+
+template <int TH, int NP>
 struct HeadStage {
-    using C = MfCfg<8, 5, TH>;
+    using C = MfCfg<8, 5, TH, NP>;
     static constexpr int SH = C::IH + 4, SW = C::IW + 4;  // nconv1's own 5x5 halo around the tile
     static constexpr int NS = SH * SW, NES = (NS + kMfThreads - 1) / kMfThreads;
     static constexpr int WOFF = NS * 8;                   // {S * c0, c0} pairs, then
@@ -388,10 +408,7 @@ struct HeadStage {
             for (int j = 0; j < 4; ++j)
 #pragma unroll
                 for (int o = 0; o < 4; ++o) acc[j][o] = (f2){0.f, 0.f};
-#ifdef NCONV_EXP_HEAD_NONC1
-            for (int j = 0; j < 4; ++j)
-                for (int o = 0; o < 4; ++o) acc[j][o] = T[(r0 + j) * SW + c + o];
-#else
+
 #pragma unroll 1
             for (int kw = 0; kw < 5; ++kw) {
                 const f2* col = T + r0 * SW + c + kw;
@@ -409,30 +426,19 @@ struct HeadStage {
                     }
                 }
             }
-#endif
-            typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const int r = r0 + j;
                 const bool in = (unsigned)(ih0 + r) < (unsigned)H && (unsigned)(iw0 + c) < (unsigned)W;
-                bf16x4 ph, pl, qh, ql;
+                float p[4], q[4];
 #pragma unroll
                 for (int o = 0; o < 4; ++o) {
                     float xv, cv;
                     nconv_epilogue(acc[j][o].x, acc[j][o].y, t.eps1, t.b1[half * 4 + o], t.s1[half * 4 + o], xv, cv);
-                    const float q = in ? cv : 0.f;  // nconv2's zero padding outside the image
-                    const float p = in ? xv * cv : 0.f;
-                    const __bf16 p1 = (__bf16)p, q1 = (__bf16)q;
-                    ph[o] = p1;
-                    pl[o] = (__bf16)(p - (float)p1);
-                    qh[o] = q1;
-                    ql[o] = (__bf16)(q - (float)q1);
+                    q[o] = in ? cv : 0.f;  // nconv2's zero padding outside the image
+                    p[o] = in ? xv * cv : 0.f;
                 }
-                unsigned char* base = lds + (r * C::IW + c) * 16 + half * 8;
-                *reinterpret_cast<bf16x4*>(base) = ph;
-                *reinterpret_cast<bf16x4*>(base + C::PSTRIDE) = pl;
-                *reinterpret_cast<bf16x4*>(base + 2 * C::PSTRIDE) = qh;
-                *reinterpret_cast<bf16x4*>(base + 3 * C::PSTRIDE) = ql;
+                store_half_planes<C>(lds + (r * C::IW + c) * 16 + half * 8, p, q);
             }
         }
     }
@@ -443,14 +449,15 @@ struct HeadStage {
 // columns x 4 rows of nconv1's (IH x IW) output region: D[(o, s')][u] = sum_k A[(o, s')][k] B[k][u]
 // with k = (kw: the lane group, kh': 8 consecutive rows of the window), so the lane holding output
 // column u reads 8 consecutive rows of one staged column: the thresholded depth is staged
-// column-major (bf16 planes S*c0 hi, S*c0 lo, c0 — c0 in {0, 1} is exact, so D takes 2 split
-// products and N 3), one 16-byte row window per (part, k-step) read as dwords (row offsets are
-// even, not multiples of 8). A (the weights, W1[o][kh' - s'][kw] for the window of output rows
-// 4g + 2m + s') is independent of the row pair m and lives in LDS. The lane's outputs are 4
-// channels of one position: the bf16x4 halves of nconv2's planes, written directly.
-template <int TH>
+// column-major (NP bf16 parts of S*c0, then c0 — c0 in {0, 1} is exact, so D takes NP split
+// products, one per weight part, and N the split terms of the math mode), one 16-byte row window
+// per (part, k-step) read as dwords (row offsets are even, not multiples of 8). A (the weights'
+// NP parts, W1[o][kh' - s'][kw] for the window of output rows 4g + 2m + s') is independent of the
+// row pair m and lives in LDS. The lane's outputs are 4 channels of one position: the bf16x4
+// halves of nconv2's planes, written directly.
+template <int TH, int NP>
 struct HeadStageMf {
-    using C = MfCfg<8, 5, TH>;
+    using C = MfCfg<8, 5, TH, NP>;
     static constexpr int SH = C::IH + 4, SW = C::IW + 4;  // nconv1's input halo
     static constexpr int NS = SH * SW, NES = (NS + kMfThreads - 1) / kMfThreads;
     static constexpr int NCB = (C::IW + 15) / 16, NG = C::IH / 4;  // column blocks, row groups
@@ -458,8 +465,8 @@ struct HeadStageMf {
     static constexpr int RS = SH + 4;        // rows per staged column (+ zero rows), 2 B each
     static constexpr int COLB = RS * 2;      // bytes per staged column: 40 (conflict-free b32 reads)
     static constexpr int PART = CW * COLB;   // bytes per part
-    static constexpr int AOFF = 3 * PART;    // weights' A fragments [step][hi/lo][lane] bf16x8
-    static constexpr int BOFF = AOFF + 4 * 64 * 16;  // nconv1's bias[8], 1 / s[8]
+    static constexpr int AOFF = (NP + 1) * PART;          // weights' A fragments [step][part][lane] bf16x8
+    static constexpr int BOFF = AOFF + 2 * NP * 64 * 16;  // nconv1's bias[8], 1 / s[8]
     static constexpr int BYTES = BOFF + 16 * 4;
     static constexpr bool SELF_SYNC = true;
     static_assert(C::IH % 4 == 0 && RS % 2 == 0 && (PART % 16) == 0, "layout");
@@ -469,18 +476,21 @@ struct HeadStageMf {
         // zero the staged parts once: the padding rows / columns are read (against zero weights)
         // and must hold finite values; the staging below rewrites only the SH x SW interior
         for (int i = tid; i < AOFF / 16; i += kMfThreads) reinterpret_cast<f4*>(stage)[i] = (f4){0.f, 0.f, 0.f, 0.f};
-        // A fragment of lane l for k-step st (kw = 4 st + kg) and part (hi / lo)
-        const int f = tid >> 6, l = tid & 63, st = f >> 1, part = f & 1;
-        const int i = l & 15, o = i & 7, sp = i >> 3, kg = l >> 4, kw = 4 * st + kg;
-        float w[8];
+        // A fragment of lane l for k-step st (kw = 4 st + kg) and weight part
+        const int l = tid & 63;
+        for (int f = tid >> 6; f < 2 * NP; f += 4) {
+            const int st = f / NP, part = f - st * NP;
+            const int i = l & 15, o = i & 7, sp = i >> 3, kg = l >> 4, kw = 4 * st + kg;
+            float w[8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            const int kh = e - sp;
-            w[e] = (kw < 5 && kh >= 0 && kh < 5) ? t.w1[(o * 5 + kh) * 5 + kw] : 0.f;
+            for (int e = 0; e < 8; ++e) {
+                const int kh = e - sp;
+                w[e] = (kw < 5 && kh >= 0 && kh < 5) ? t.w1[(o * 5 + kh) * 5 + kw] : 0.f;
+            }
+            bf16x8 wp[NP];
+            split_parts<NP>(w, wp);
+            *reinterpret_cast<bf16x8*>(stage + AOFF + (f * 64 + l) * 16) = wp[part];
         }
-        bf16x8 hi, lo;
-        split8(w, hi, lo);
-        *reinterpret_cast<bf16x8*>(stage + AOFF + (f * 64 + l) * 16) = part ? lo : hi;
         if (tid < 16)
             reinterpret_cast<float*>(stage + BOFF)[tid] = tid < 8 ? t.b1[tid] : __builtin_amdgcn_rcpf(t.s1[tid - 8]);
     }
@@ -516,21 +526,26 @@ struct HeadStageMf {
             if (NES * kMfThreads != NS && e >= NS) continue;
             const int r = e / SW, col = e - r * SW;
             const float c0 = sv[k] > t.thresh1 ? 1.0f : 0.0f;  // step1.py:53
-            const float p = sv[k] * c0;
-            const __bf16 ph = (__bf16)p;
+            float p = sv[k] * c0;
             unsigned char* q = stage + col * COLB + r * 2;
-            *reinterpret_cast<__bf16*>(q) = ph;
-            *reinterpret_cast<__bf16*>(q + PART) = (__bf16)(p - (float)ph);
-            *reinterpret_cast<__bf16*>(q + 2 * PART) = (__bf16)c0;
+#pragma unroll
+            for (int i = 0; i < NP; ++i) {
+                const __bf16 h = (__bf16)p;
+                *reinterpret_cast<__bf16*>(q + i * PART) = h;
+                if (i + 1 < NP) p -= (float)h;
+            }
+            *reinterpret_cast<__bf16*>(q + NP * PART) = (__bf16)c0;
         }
         __syncthreads();
         const int H = d.L.H, W = d.L.W;
         const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
         const int u = lane & 15, kg = lane >> 4, half = kg & 1, sp = lane >> 5;
-        const bf16x8 a0h = *reinterpret_cast<const bf16x8*>(stage + AOFF + (0 * 64 + lane) * 16);
-        const bf16x8 a0l = *reinterpret_cast<const bf16x8*>(stage + AOFF + (1 * 64 + lane) * 16);
-        const bf16x8 a1h = *reinterpret_cast<const bf16x8*>(stage + AOFF + (2 * 64 + lane) * 16);
-        const bf16x8 a1l = *reinterpret_cast<const bf16x8*>(stage + AOFF + (3 * 64 + lane) * 16);
+        bf16x8 a[2][NP];
+#pragma unroll
+        for (int st = 0; st < 2; ++st)
+#pragma unroll
+            for (int j = 0; j < NP; ++j)
+                a[st][j] = *reinterpret_cast<const bf16x8*>(stage + AOFF + ((st * NP + j) * 64 + lane) * 16);
         // (from LDS: a global load here would wait for the previous tile's stores as well)
         const f4 bias = reinterpret_cast<const f4*>(stage + BOFF)[half];
         const f4 rs1 = reinterpret_cast<const f4*>(stage + BOFF)[2 + half];
@@ -546,38 +561,35 @@ struct HeadStageMf {
                 for (int st = 0; st < 2; ++st) {
                     const int kw = st == 0 ? kg : 4;  // k-step 1: only group 0 (kw 4) has weights
                     const unsigned char* q = stage + (16 * cb + u + kw) * COLB + r0 * 2;
-                    const bf16x8 ph = rd_window(q), pl = rd_window(q + PART), cz = rd_window(q + 2 * PART);
-                    const bf16x8 ah = st ? a1h : a0h, al = st ? a1l : a0l;
-                    n = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, ph, n, 0, 0, 0);
-                    dd = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, cz, dd, 0, 0, 0);
-                    n = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, pl, n, 0, 0, 0);
-                    n = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, ph, n, 0, 0, 0);
-                    dd = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, cz, dd, 0, 0, 0);
+                    bf16x8 pw[NP];
+#pragma unroll
+                    for (int i = 0; i < NP; ++i) pw[i] = rd_window(q + i * PART);
+                    const bf16x8 cz = rd_window(q + NP * PART);
+                    // smallest terms first: N over the (data part i, weight part j) terms of the
+                    // mode, D over the weight parts (c0 is exact)
+#pragma unroll
+                    for (int s = 2 * (NP - 1); s >= 0; --s) {
+#pragma unroll
+                        for (int i = NP - 1; i >= 0; --i) {
+                            const int j = s - i;
+                            if (j < 0 || j >= NP || !use_term<NP>(i, j)) continue;
+                            n = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[st][j], pw[i], n, 0, 0, 0);
+                        }
+                        if (s < NP) dd = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[st][s], cz, dd, 0, 0, 0);
+                    }
                 }
                 // lane: channels 4 half .. +3 of nconv1 output (row r0 + sp, column 16 cb + u)
                 const int row = r0 + sp, col = 16 * cb + u;
                 const bool in = (unsigned)(ih0 + row) < (unsigned)H && (unsigned)(iw0 + col) < (unsigned)W;
-                typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-                bf16x4 xh, xl, qh, ql;
+                float pv[4], qv[4];
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const float xv = n[r] * __builtin_amdgcn_rcpf(dd[r] + t.eps1) + bias[r];
                     const float cv = dd[r] * rs1[r];
-                    const float q = in ? cv : 0.f;  // nconv2's zero padding outside the image
-                    const float pv = in ? xv * cv : 0.f;
-                    const __bf16 p1 = (__bf16)pv, q1 = (__bf16)q;
-                    xh[r] = p1;
-                    xl[r] = (__bf16)(pv - (float)p1);
-                    qh[r] = q1;
-                    ql[r] = (__bf16)(q - (float)q1);
+                    qv[r] = in ? cv : 0.f;  // nconv2's zero padding outside the image
+                    pv[r] = in ? xv * cv : 0.f;
                 }
-                if (col < C::IW) {
-                    unsigned char* base = lds + (row * C::IW + col) * 16 + half * 8;
-                    *reinterpret_cast<bf16x4*>(base) = xh;
-                    *reinterpret_cast<bf16x4*>(base + C::PSTRIDE) = xl;
-                    *reinterpret_cast<bf16x4*>(base + 2 * C::PSTRIDE) = qh;
-                    *reinterpret_cast<bf16x4*>(base + 3 * C::PSTRIDE) = ql;
-                }
+                if (col < C::IW) store_half_planes<C>(lds + (row * C::IW + col) * 16 + half * 8, pv, qv);
             }
         }
     }
@@ -607,41 +619,43 @@ struct HeadStageMf {
 #ifndef NCONV_MFMA_UP_WAVES
 #define NCONV_MFMA_UP_WAVES 2  // the 16-channel upsample-concat layers (nconv4/5/6): no spills
 #endif
-template <int MODE, bool DMA>
+// three-part (exact-product) kernels: three B fragments per k-step and 1.5x the staged planes
+#ifndef NCONV_MFMA_X9_WAVES
+#define NCONV_MFMA_X9_WAVES 2
+#endif
+template <int MODE, bool DMA, int NP>
 constexpr int mf_waves() {
-    return MODE == kModeHead ? NCONV_MFMA_HEAD_WAVES
+    return NP == 3 ? NCONV_MFMA_X9_WAVES
+           : MODE == kModeHead ? NCONV_MFMA_HEAD_WAVES
            : DMA || MODE == NCONV_LOAD_POOL2 ? 2
            : (MODE == NCONV_LOAD_UPCAT_SKIP_FIRST || MODE == NCONV_LOAD_UPCAT_UP_FIRST) ? NCONV_MFMA_UP_WAVES
                                                                                          : NCONV_MFMA_WAVES;
 }
-template <int CIN, int K, int MODE, int TH, bool DMA>
+template <int CIN, int K, int MODE, int TH, bool DMA, int NP>
 using StageOf = typename std::conditional<
     MODE == kModeHead,
 #ifdef NCONV_HEAD_NC1_VALU
-    HeadStage<TH>,
+    HeadStage<TH, NP>,
 #else
-    HeadStageMf<TH>,
+    HeadStageMf<TH, NP>,
 #endif
-    typename std::conditional<DMA, DmaStage<CIN, K, MODE, TH>, MfStage<CIN, K, MODE, TH>>::type>::type;
-template <int CIN, int K, int MODE, int EPI, int TH>
+    typename std::conditional<DMA, DmaStage<CIN, K, MODE, TH, NP>, MfStage<CIN, K, MODE, TH, NP>>::type>::type;
+template <int CIN, int K, int MODE, int EPI, int TH, int NP>
 constexpr int mf_lds_bytes(bool dma) {
-    return MfCfg<CIN, K, TH>::LDS_IN + (EPI == kEpiTail ? 0 : kTrBytes) +
-           (MODE == kModeHead ? StageOf<CIN, K, MODE, TH, false>::BYTES : dma ? DmaStage<CIN, K, MODE, TH>::BYTES : 0);
+    return MfCfg<CIN, K, TH, NP>::LDS_IN + (EPI == kEpiTail ? 0 : kTrBytes) +
+           (MODE == kModeHead ? StageOf<CIN, K, MODE, TH, false, NP>::BYTES
+                              : dma ? DmaStage<CIN, K, MODE, TH, NP>::BYTES : 0);
 }
-template <int CIN, int K, int MODE, int EPI, int TH, bool VEC, bool DMA>
-__global__ __launch_bounds__(kMfThreads) __attribute__((amdgpu_waves_per_eu(mf_waves<MODE, DMA>(), mf_waves<MODE, DMA>()))) void fwd_mfma(LayerDev d, float* __restrict__ y, float* __restrict__ yc,
+template <int CIN, int K, int MODE, int EPI, int TH, bool VEC, bool DMA, int NP>
+__global__ __launch_bounds__(kMfThreads) __attribute__((amdgpu_waves_per_eu(mf_waves<MODE, DMA, NP>(), mf_waves<MODE, DMA, NP>()))) void fwd_mfma(LayerDev d, float* __restrict__ y, float* __restrict__ yc,
                                                        TailArgs t) {
-    using C = MfCfg<CIN, K, TH>;
-    using Stage = StageOf<CIN, K, MODE, TH, DMA>;
+    using C = MfCfg<CIN, K, TH, NP>;
+    using Stage = StageOf<CIN, K, MODE, TH, DMA, NP>;
     // input planes, (non-tail) four waves' output-transpose regions (y and cout), DMA staging
-    __shared__ __attribute__((aligned(16))) unsigned char lds[mf_lds_bytes<CIN, K, MODE, EPI, TH>(DMA)];
-    unsigned char* const stage = lds + MfCfg<CIN, K, TH>::LDS_IN + (EPI == kEpiTail ? 0 : kTrBytes);
+    __shared__ __attribute__((aligned(16))) unsigned char lds[mf_lds_bytes<CIN, K, MODE, EPI, TH, NP>(DMA)];
+    unsigned char* const stage = lds + C::LDS_IN + (EPI == kEpiTail ? 0 : kTrBytes);
     const nconv_layer& L = d.L;
-#ifdef NCONV_MF_WAVE_VGPR
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-#else
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-#endif
     const bool tail = EPI == kEpiTail;
     const int gh = tail ? t.out_h : L.Ho, gw = tail ? t.out_w : L.Wo;  // the written grid
     const int ntx = (gw + C::TW - 1) / C::TW, nty = (gh + TH - 1) / TH;
@@ -675,10 +689,10 @@ __global__ __launch_bounds__(kMfThreads) __attribute__((amdgpu_waves_per_eu(mf_w
     // loads are unconditional (a block without tiles loads the last one and never uses it)
     st.issue(d, t, tc.b, tc.ty * TH + off - L.PH, tc.tx * C::TW + off - L.PW, stage, tid);
 
-    // ---- B fragments (weights, once per workgroup) and per-lane A offsets ----
+    // ---- B fragments (weights' NP parts, once per workgroup) and per-lane A offsets ----
     const int u = lane & 15, h = lane >> 4;
     const int o = lane & 7, s = (lane >> 3) & 1;  // this lane's B / C column (o, s)
-    bf16x8 bh[C::NT], bl[C::NT];
+    bf16x8 bw[C::NT][NP];
     int aoff[C::NT];
 #pragma unroll
     for (int q = 0; q < C::NT; ++q) {
@@ -689,14 +703,14 @@ __global__ __launch_bounds__(kMfThreads) __attribute__((amdgpu_waves_per_eu(mf_w
         int a = (1 * C::IW) * 16;  // padding positions read (kh'=1, kw=0): inside both rows' windows
         if (pos < C::NKP) {
             const int g = pos % C::G, qq = pos / C::G, kw = qq % K, khp = qq / K, kh = khp - s;
-            a = g * 4 * C::PSTRIDE + (khp * C::IW + kw) * 16;
+            a = g * C::NPL * C::PSTRIDE + (khp * C::IW + kw) * 16;
             if (kh >= 0 && kh < K) {
                 const float* wp = L.weight + ((size_t)(o * CIN + g * 8) * K + kh) * K + kw;
 #pragma unroll
                 for (int j = 0; j < 8; ++j) w[j] = wp[j * K * K];
             }
         }
-        split8(w, bh[q], bl[q]);
+        split_parts<NP>(w, bw[q]);
         aoff[q] = a + u * 16;
     }
     const float eps = L.eps, bo = L.bias[o];
@@ -719,33 +733,43 @@ __global__ __launch_bounds__(kMfThreads) __attribute__((amdgpu_waves_per_eu(mf_w
         for (int rpi = 0; rpi < C::NRP / 4; ++rpi) {
             const int rp = wave + 4 * rpi;
             // the 16 x 16 {N, D} tiles of column half ct (16 ct .. +15) of row pair rp
+            // one k-step of one column half: the split terms of N (x*c parts) and D (c parts)
+            // against the weights' parts, smallest terms first
+            auto terms = [&](const bf16x8 (&an)[NP], const bf16x8 (&ad)[NP], const bf16x8 (&b)[NP], f4_& n,
+                             f4_& dd) {
+#pragma unroll
+                for (int sum = 2 * (NP - 1); sum >= 0; --sum)
+#pragma unroll
+                    for (int i = NP - 1; i >= 0; --i) {
+                        const int j = sum - i;
+                        if (j < 0 || j >= NP || !use_term<NP>(i, j)) continue;
+                        n = __builtin_amdgcn_mfma_f32_16x16x32_bf16(an[i], b[j], n, 0, 0, 0);
+                        dd = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ad[i], b[j], dd, 0, 0, 0);
+                    }
+            };
+            auto ld_parts = [&](const unsigned char* p, bf16x8 (&an)[NP], bf16x8 (&ad)[NP]) {
+#pragma unroll
+                for (int i = 0; i < NP; ++i) {
+                    an[i] = *reinterpret_cast<const bf16x8*>(p + i * C::PSTRIDE);
+                    ad[i] = *reinterpret_cast<const bf16x8*>(p + (NP + i) * C::PSTRIDE);
+                }
+            };
+            // the 16 x 16 {N, D} tiles of column half ct (16 ct .. +15) of row pair rp
             auto mma = [&](int ct, f4_& n, f4_& dd) {
                 const unsigned char* tb = lds + (2 * rp * C::IW + 16 * ct) * 16;
                 n = (f4_){0.f, 0.f, 0.f, 0.f};
                 dd = (f4_){0.f, 0.f, 0.f, 0.f};
-#ifdef NCONV_EXP_MF_NOMFMA
-                n[0] = tb[aoff[0]];
-#else
 #pragma unroll
                 for (int q = 0; q < C::NT; ++q) {
-                    const unsigned char* p = tb + aoff[q];
-                    const bf16x8 nh = *reinterpret_cast<const bf16x8*>(p);
-                    const bf16x8 nl = *reinterpret_cast<const bf16x8*>(p + C::PSTRIDE);
-                    const bf16x8 dh = *reinterpret_cast<const bf16x8*>(p + 2 * C::PSTRIDE);
-                    const bf16x8 dl = *reinterpret_cast<const bf16x8*>(p + 3 * C::PSTRIDE);
-                    n = __builtin_amdgcn_mfma_f32_16x16x32_bf16(nl, bh[q], n, 0, 0, 0);
-                    dd = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dl, bh[q], dd, 0, 0, 0);
-                    n = __builtin_amdgcn_mfma_f32_16x16x32_bf16(nh, bl[q], n, 0, 0, 0);
-                    dd = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dh, bl[q], dd, 0, 0, 0);
-                    n = __builtin_amdgcn_mfma_f32_16x16x32_bf16(nh, bh[q], n, 0, 0, 0);
-                    dd = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dh, bh[q], dd, 0, 0, 0);
+                    bf16x8 an[NP], ad[NP];
+                    ld_parts(tb + aoff[q], an, ad);
+                    terms(an, ad, bw[q], n, dd);
                 }
-#endif
             };
 
-            // both column halves, k-step outer: each k-step's 8 A-fragment reads are in flight
-            // together and feed 12 independent MFMAs (two accumulator pairs), which hides the LDS
-            // latency that one half's 6 dependent MFMAs per k-step leave exposed
+            // both column halves, k-step outer: each k-step's A-fragment reads are in flight
+            // together and feed two accumulator pairs, which hides the LDS latency that one half's
+            // dependent MFMAs per k-step leave exposed
             auto mma2 = [&](f4_ (&n)[2], f4_ (&dd)[2]) {
 #pragma unroll
                 for (int ct = 0; ct < 2; ++ct) {
@@ -754,26 +778,13 @@ __global__ __launch_bounds__(kMfThreads) __attribute__((amdgpu_waves_per_eu(mf_w
                 }
 #pragma unroll
                 for (int q = 0; q < C::NT; ++q) {
-                    bf16x8 a[2][4];
+                    bf16x8 an[2][NP], ad[2][NP];
 #pragma unroll
-                    for (int ct = 0; ct < 2; ++ct) {
-                        const unsigned char* p = lds + (2 * rp * C::IW + 16 * ct) * 16 + aoff[q];
+                    for (int ct = 0; ct < 2; ++ct) ld_parts(lds + (2 * rp * C::IW + 16 * ct) * 16 + aoff[q], an[ct], ad[ct]);
 #pragma unroll
-                        for (int part = 0; part < 4; ++part)
-                            a[ct][part] = *reinterpret_cast<const bf16x8*>(p + part * C::PSTRIDE);
-                    }
-#pragma unroll
-                    for (int ct = 0; ct < 2; ++ct) {
-                        n[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ct][1], bh[q], n[ct], 0, 0, 0);
-                        dd[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ct][3], bh[q], dd[ct], 0, 0, 0);
-                        n[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ct][0], bl[q], n[ct], 0, 0, 0);
-                        dd[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ct][2], bl[q], dd[ct], 0, 0, 0);
-                        n[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ct][0], bh[q], n[ct], 0, 0, 0);
-                        dd[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ct][2], bh[q], dd[ct], 0, 0, 0);
-                    }
+                    for (int ct = 0; ct < 2; ++ct) terms(an[ct], ad[ct], bw[q], n[ct], dd[ct]);
                 }
             };
-            (void)mma2;
 
             // ---- epilogue: this lane holds (o, row oh, columns 16 ct + 4 h .. +3) per half ct ----
             // Every global store is an unconditional buffer store; lanes with nothing to write carry
@@ -782,18 +793,6 @@ __global__ __launch_bounds__(kMfThreads) __attribute__((amdgpu_waves_per_eu(mf_w
             // also wait for the stores to complete.
             if constexpr (EPI != kEpiTail) {
                 float yv[2][4], cv[2][4];
-#ifdef NCONV_MF_CT_SEQ
-#pragma unroll
-                for (int ct = 0; ct < 2; ++ct) {
-                    f4_ accN, accD;
-                    mma(ct, accN, accD);
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        yv[ct][r] = accN[r] * __builtin_amdgcn_rcpf(accD[r] + eps) + bo;
-                        cv[ct][r] = accD[r] * rcp_s;
-                    }
-                }
-#else
                 {
                     f4_ accN[2], accD[2];
                     mma2(accN, accD);
@@ -805,7 +804,6 @@ __global__ __launch_bounds__(kMfThreads) __attribute__((amdgpu_waves_per_eu(mf_w
                             cv[ct][r] = accD[ct][r] * rcp_s;
                         }
                 }
-#endif
                 // Transpose the row pair through this wave's LDS region ([o + 8 s][32 columns], pitch
                 // 36 floats: conflict-free f4 writes), so that each global store instruction writes
                 // eight whole 128-byte rows (lane: channel l>>3, columns 4 (l&7) .. +3) instead of
@@ -956,16 +954,16 @@ int mfma_grid_blocks(int waves, int lds_bytes) {
     return (cus * (per_cu > 0 ? per_cu : 1) + 7) / 8 * 8;
 }
 
-template <int CIN, int K, int MODE, int EPI, int TH, bool DMA>
+template <int CIN, int K, int MODE, int EPI, int TH, bool DMA, int NP>
 void go_mfma(const LayerDev& d, float* y, float* yc, const TailArgs& t, int gh, int gw, hipStream_t st) {
-    using C = MfCfg<CIN, K, TH>;
+    using C = MfCfg<CIN, K, TH, NP>;
     const int ntiles = ((gw + C::TW - 1) / C::TW) * ((gh + TH - 1) / TH) * d.L.B;
-    int grid = mfma_grid_blocks(mf_waves<MODE, DMA>(), mf_lds_bytes<CIN, K, MODE, EPI, TH>(DMA));
+    int grid = mfma_grid_blocks(mf_waves<MODE, DMA, NP>(), mf_lds_bytes<CIN, K, MODE, EPI, TH, NP>(DMA));
     if (ntiles < grid) grid = (ntiles + 7) / 8 * 8;
     if (gw % 4 == 0)
-        hipLaunchKernelGGL((fwd_mfma<CIN, K, MODE, EPI, TH, true, DMA>), grid, dim3(kMfThreads), 0, st, d, y, yc, t);
+        hipLaunchKernelGGL((fwd_mfma<CIN, K, MODE, EPI, TH, true, DMA, NP>), grid, dim3(kMfThreads), 0, st, d, y, yc, t);
     else
-        hipLaunchKernelGGL((fwd_mfma<CIN, K, MODE, EPI, TH, false, DMA>), grid, dim3(kMfThreads), 0, st, d, y, yc, t);
+        hipLaunchKernelGGL((fwd_mfma<CIN, K, MODE, EPI, TH, false, DMA, NP>), grid, dim3(kMfThreads), 0, st, d, y, yc, t);
 }
 
 // LDS-DMA staging: rows of every source a multiple of 4 floats (16-B vectors never straddle a row
@@ -992,14 +990,23 @@ bool dma_ok(const nconv_layer& L, int cin) {
            L.W == 2 * L.b.W;
 }
 
+template <int CIN, int K, int MODE, int EPI, int TH, int NP>
+void go_mfma_np(const LayerDev& d, float* y, float* yc, const TailArgs& t, int gh, int gw, hipStream_t st) {
+    if constexpr (MODE == NCONV_LOAD_POOL2 || NP != 2)
+        go_mfma<CIN, K, MODE, EPI, TH, false, NP>(d, y, yc, t, gh, gw, st);
+    else if (dma_ok(d.L, CIN))
+        go_mfma<CIN, K, MODE, EPI, TH, true, NP>(d, y, yc, t, gh, gw, st);
+    else
+        go_mfma<CIN, K, MODE, EPI, TH, false, NP>(d, y, yc, t, gh, gw, st);
+}
+
+// NP = 2 split parts (bf16x3) or 3 (bf16x9, exact products) by the layer's math
 template <int CIN, int K, int MODE, int EPI, int TH>
 void go_mfma_any(const LayerDev& d, float* y, float* yc, const TailArgs& t, int gh, int gw, hipStream_t st) {
-    if constexpr (MODE == NCONV_LOAD_POOL2)
-        go_mfma<CIN, K, MODE, EPI, TH, false>(d, y, yc, t, gh, gw, st);
-    else if (dma_ok(d.L, CIN))
-        go_mfma<CIN, K, MODE, EPI, TH, true>(d, y, yc, t, gh, gw, st);
+    if (d.L.math == NCONV_MATH_BF16X9)
+        go_mfma_np<CIN, K, MODE, EPI, TH, 3>(d, y, yc, t, gh, gw, st);
     else
-        go_mfma<CIN, K, MODE, EPI, TH, false>(d, y, yc, t, gh, gw, st);
+        go_mfma_np<CIN, K, MODE, EPI, TH, 2>(d, y, yc, t, gh, gw, st);
 }
 
 }  // namespace
@@ -1007,7 +1014,10 @@ void go_mfma_any(const LayerDev& d, float* y, float* yc, const TailArgs& t, int 
 int launch_fwd_head(const LayerDev& d2, const TailArgs& t, float* y, float* yc, hipStream_t st, const char** why) {
     // (16-row tiles recompute less of nconv1's halo but fit two workgroups per CU instead of three:
     // 228 vs 215 us at B=8 352x1216)
-    go_mfma<8, 5, kModeHead, kEpiPool, NCONV_MF_TH_HEAD, false>(d2, y, yc, t, d2.L.Ho, d2.L.Wo, st);
+    if (d2.L.math == NCONV_MATH_BF16X9)
+        go_mfma<8, 5, kModeHead, kEpiPool, NCONV_MF_TH_HEAD, false, 3>(d2, y, yc, t, d2.L.Ho, d2.L.Wo, st);
+    else
+        go_mfma<8, 5, kModeHead, kEpiPool, NCONV_MF_TH_HEAD, false, 2>(d2, y, yc, t, d2.L.Ho, d2.L.Wo, st);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         *why = hipGetErrorString(e);
@@ -1020,7 +1030,7 @@ int launch_fwd_head(const LayerDev& d2, const TailArgs& t, float* y, float* yc, 
 // 8 input channels with a 5x5 kernel or 16 with a 3x3, stride 1, no dilation / groups.
 bool launch_fwd_mfma(const LayerDev& d, float* y, float* yc, const TailArgs& t, bool tail, hipStream_t st) {
     const nconv_layer& L = d.L;
-    if (L.math != NCONV_MATH_BF16X3 || L.Cout != 8 || L.KH != L.KW || L.SH != 1 || L.SW != 1 || L.DH != 1 ||
+    if ((L.math != NCONV_MATH_BF16X3 && L.math != NCONV_MATH_BF16X9) || L.Cout != 8 || L.KH != L.KW || L.SH != 1 || L.SW != 1 || L.DH != 1 ||
         L.DW != 1 || L.groups != 1)
         return false;
     // MfStage addresses one image's channels of a source through one buffer resource
@@ -1047,8 +1057,10 @@ bool launch_fwd_mfma(const LayerDev& d, float* y, float* yc, const TailArgs& t, 
             return true;
         }
         if (L.load_mode == NCONV_LOAD_UPCAT_UP_FIRST) {
-            if (tail)
-                go_mfma_any<16, 3, NCONV_LOAD_UPCAT_UP_FIRST, kEpiTail, NCONV_MF_TH_TAIL>(d, y, nullptr, t, gh, gw, st);
+            if (tail && L.math == NCONV_MATH_BF16X9)  // (16-row tiles of three-part planes: one workgroup per CU)
+                go_mfma_np<16, 3, NCONV_LOAD_UPCAT_UP_FIRST, kEpiTail, 8, 3>(d, y, nullptr, t, gh, gw, st);
+            else if (tail)
+                go_mfma_np<16, 3, NCONV_LOAD_UPCAT_UP_FIRST, kEpiTail, NCONV_MF_TH_TAIL, 2>(d, y, nullptr, t, gh, gw, st);
             else
                 go_mfma_any<16, 3, NCONV_LOAD_UPCAT_UP_FIRST, kEpiPlain, 8>(d, y, yc, t, gh, gw, st);
             return true;

@@ -309,7 +309,8 @@ class DNET(nn.Module):
     fused_head = True
 
     def _use_head(self, l1, l2):
-        return self.fused_head and nconv.FORWARD_MATH == _lib.MATH_BF16X3 and self._head_shapes(l1, l2)
+        return self.fused_head and nconv.FORWARD_MATH in (_lib.MATH_BF16X3, _lib.MATH_BF16X9) and \
+            self._head_shapes(l1, l2)
 
     @staticmethod
     def _head_shapes(l1, l2):

@@ -20,10 +20,12 @@ from . import _lib
 
 
 # Arithmetic of the forward sums N = W*(x*c), D = W*c (include/nconv.h enum nconv_math): "fp32"
-# (default: exact fp32 products, as the reference's F.conv2d) or "bf16x3" (opt-in: split-bf16
-# products on the matrix cores, <= ~1.1e-5 relative per product, faster; a NaN input may spread
-# one row further than in the reference). NCONV_FWD_MATH selects it; tests switch this global.
-_MATH_NAMES = {"bf16x3": _lib.MATH_BF16X3, "fp32": _lib.MATH_FP32}
+# (default: exact fp32 products on the vector ALU, as the reference's F.conv2d), "bf16x9" (exact
+# products on the matrix cores: both operands split into three bf16 parts, an exact
+# decomposition, all nine partial products accumulated in fp32) or "bf16x3" (split-bf16 products,
+# <= ~1.1e-5 relative per product). With either matrix-core math a NaN input may spread one row
+# further than in the reference. NCONV_FWD_MATH selects it; tests switch this global.
+_MATH_NAMES = {"bf16x3": _lib.MATH_BF16X3, "fp32": _lib.MATH_FP32, "bf16x9": _lib.MATH_BF16X9}
 FORWARD_MATH = _MATH_NAMES[os.environ.get("NCONV_FWD_MATH", "fp32")]
 
 

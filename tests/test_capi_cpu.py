@@ -194,7 +194,7 @@ def test_loss_plane_geometry(nconv_amd):
 def test_fwd_rejects_unknown_math(nconv_amd):
     """nconv_layer.math outside enum nconv_math (e.g. a host struct without the field) is refused."""
     lib = nconv_amd._lib.lib()
-    for m in (2, -1, 0x7fff):
+    for m in (3, -1, 0x7fff):
         L = _layer(nconv_amd, math=m)
         assert lib.nconv_fwd(ctypes.byref(L), ctypes.c_void_p(0x2000), ctypes.c_void_p(0x3000), None) == -22
         assert "unknown math" in lib.nconv_last_error().decode()

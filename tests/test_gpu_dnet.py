@@ -187,9 +187,9 @@ def _oracle_out(net, S, crop):
     return _ORACLE_CACHE[key]
 
 
-@pytest.fixture(params=["fp32", "bf16x3"])
+@pytest.fixture(params=["fp32", "bf16x9", "bf16x3"])
 def fwd_math(request, nconv_amd, monkeypatch):
-    monkeypatch.setattr(nconv_amd.nconv, "FORWARD_MATH", {"bf16x3": 0, "fp32": 1}[request.param])
+    monkeypatch.setattr(nconv_amd.nconv, "FORWARD_MATH", {"bf16x3": 0, "fp32": 1, "bf16x9": 2}[request.param])
     return request.param
 
 

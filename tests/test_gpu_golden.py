@@ -37,9 +37,9 @@ def T(a, dev=None):
     return t.to(dev) if dev is not None else t
 
 
-@pytest.fixture(params=["fp32", "bf16x3"])
+@pytest.fixture(params=["fp32", "bf16x9", "bf16x3"])
 def fwd_math(request, nconv_amd, monkeypatch):
-    monkeypatch.setattr(nconv_amd.nconv, "FORWARD_MATH", {"bf16x3": 0, "fp32": 1}[request.param])
+    monkeypatch.setattr(nconv_amd.nconv, "FORWARD_MATH", {"bf16x3": 0, "fp32": 1, "bf16x9": 2}[request.param])
     return request.param
 
 
@@ -231,7 +231,7 @@ def test_f4_threshold_mask_bit_exact(nconv_amd, gpu, fwd_math):
     y1, co1 = N.layer_forward_raw(sp1, S, None, None, None, w1, b1, s1)
     for o in range(8):
         assert torch.equal(co1[:, o:o + 1].cpu(), c0), f"nconv1 cout channel {o}"
-    if fwd_math == "bf16x3":
+    if fwd_math != "fp32":  # the fused head (matrix-core maths)
         sp2, w2, b2, s2 = _center_layer(nconv_amd, gpu, 8, 8, 5, nconv_amd._lib.PLAIN)
         _, co2, _, _ = N.layer_forward_head(sp1, sp2, S, w1, b1, s1, w2, b2, s2)
         for o in range(8):
@@ -244,7 +244,7 @@ def test_f4_threshold_mask_bit_exact(nconv_amd, gpu, fwd_math):
 
 
 def _nan_sets_agree(got, ref, fwd_math):
-    """Exact fp32: NaN exactly where the reference has it. bf16x3 (opt-in): its matrix-core GEMM
+    """Exact fp32: NaN exactly where the reference has it. bf16x3 / bf16x9: the matrix-core GEMM
     folds two output rows into one operand, so an input NaN also meets the zero weights of the
     partner row's out-of-window tap (0 * NaN = NaN): the NaN set may grow by rows next to the
     reference's (include/nconv.h, NCONV_MATH_BF16X3), never shrink."""

@@ -48,10 +48,10 @@ def _wsum(nconv_amd, w):
     return s
 
 
-@pytest.fixture(params=["bf16x3", "fp32"])
+@pytest.fixture(params=["bf16x3", "bf16x9", "fp32"])
 def fwd_math(request, nconv_amd, monkeypatch):
-    """Both forward arithmetics (include/nconv.h enum nconv_math)."""
-    monkeypatch.setattr(nconv_amd.nconv, "FORWARD_MATH", {"bf16x3": 0, "fp32": 1}[request.param])
+    """Every forward arithmetic (include/nconv.h enum nconv_math)."""
+    monkeypatch.setattr(nconv_amd.nconv, "FORWARD_MATH", {"bf16x3": 0, "fp32": 1, "bf16x9": 2}[request.param])
     return request.param
 
 
