@@ -203,13 +203,8 @@ __device__ __forceinline__ ChanSrc chan_src(const LayerDev& d, int b, int ci) {
 // (x, c) of the layer input at (ih, iw), in range, from a resolved channel source.
 __device__ __forceinline__ void load_chan(const LayerDev& d, const ChanSrc& s, int ih, int iw, float& x,
                                           float& c) {
-#ifdef NCONV_EXP_L2HIT
-#define NCONV_EXP_MASK(i) ((i) & 1023)
-#else
-#define NCONV_EXP_MASK(i) (i)
-#endif
     if (s.kind == kDirect) {
-        const int i = NCONV_EXP_MASK(ih * s.W + iw);
+        const int i = ih * s.W + iw;
         x = s.x[i];
         c = s.c[i];
     } else if (s.kind == kThresh) {
@@ -229,17 +224,15 @@ __device__ __forceinline__ void load_chan(const LayerDev& d, const ChanSrc& s, i
     } else {
         const int sh = nearest_src(ih, d.L.b.H, d.L.H, d.up_scale_h);
         const int sw = nearest_src(iw, d.L.b.W, d.L.W, d.up_scale_w);
-        const int i = NCONV_EXP_MASK(sh * s.W + sw);
+        const int i = sh * s.W + sw;
         x = s.x[i];
         c = s.c[i];
     }
 }
 
-// One channel plane of {x*c, c} over an IHT x IWT halo tile (origin ih0, iw0), split into a load
-// phase (global -> registers) and a store phase (registers -> LDS, row pitch IWP). Between the two
-// a kernel can compute on the previous plane, so the loads' latency hides behind packed FMAs
-// (register-staged software pipeline). 256 threads, IWT >= 64: lanes map to columns, waves to
-// rows; every address is clamped into the source plane so all of a thread's loads are issued
+// One channel plane of {x*c, c} over an IHT x IWT halo tile (origin ih0, iw0) (the weight
+// gradient's staging, wgrad_tiled), in a load phase (global -> registers) and a store phase
+// (registers -> LDS, row pitch IWP). 256 threads, IWT >= 64: lanes map to columns, waves to rows; every address is clamped into the source plane so all of a thread's loads are issued
 // before the first is consumed, and out-of-range elements are zeroed at store time. The plane
 // must hold round_up(IHT, 4) rows: the last row group is written unconditionally.
 template <int IHT, int IWT, int IWP>
@@ -299,49 +292,6 @@ struct PlaneRegs {
     }
 };
 
-// The same for tiles narrower than a wave (IWT < 64): elements are dealt to the 256 threads in
-// row-major order (e = tid + 256 k), so consecutive lanes still read consecutive columns.
-template <int IHT, int IWT, int IWP>
-struct PlaneRegsLin {
-    static constexpr int NT = IHT * IWT;
-    static constexpr int NE = (NT + 255) / 256;
-    float x[NE], c[NE];
-
-    __device__ __forceinline__ void load(const LayerDev& d, const ChanSrc& s, int ih0, int iw0, int tid) {
-        const int H = d.L.H, W = d.L.W;
-#pragma unroll
-        for (int k = 0; k < NE; ++k) {
-            int e = tid + 256 * k;
-            e = e < NT ? e : NT - 1;
-            const int r = e / IWT, col = e - r * IWT;
-            const int ih = ih0 + r, iw = iw0 + col;
-            const int ihc = ih < 0 ? 0 : (ih >= H ? H - 1 : ih);
-            const int iwc = iw < 0 ? 0 : (iw >= W ? W - 1 : iw);
-#ifdef NCONV_EXP_NO_LOADS
-            x[k] = (float)(ihc + iwc); c[k] = 1.f;
-#else
-            load_chan(d, s, ihc, iwc, x[k], c[k]);
-#endif
-        }
-    }
-
-    __device__ __forceinline__ void store(const LayerDev& d, f2* t, int ih0, int iw0, int tid) const {
-        const int H = d.L.H, W = d.L.W;
-#pragma unroll
-        for (int k = 0; k < NE; ++k) {
-            const int e = tid + 256 * k;
-            const int r = e / IWT, col = e - r * IWT;
-            const bool ok = (unsigned)(ih0 + r) < (unsigned)H && (unsigned)(iw0 + col) < (unsigned)W;
-            const float xv = ok ? x[k] : 0.f, cv = ok ? c[k] : 0.f;
-            if (NE * 256 == NT || e < NT) t[r * IWP + col] = (f2){xv * cv, cv};
-        }
-    }
-};
-
-template <int IHT, int IWT, int IWP>
-using PlaneStage = typename std::conditional<(IWT >= 64), PlaneRegs<IHT, IWT, IWP>,
-                                             PlaneRegsLin<IHT, IWT, IWP>>::type;
-
 // Load and store back to back (no pipelining): one staged plane.
 template <int IHT, int IWT, int IWP>
 __device__ __forceinline__ void stage_plane(const LayerDev& d, const ChanSrc& s, f2* t, int ih0, int iw0,
@@ -358,7 +308,7 @@ __device__ __forceinline__ void stage_plane(const LayerDev& d, const ChanSrc& s,
 // computed once per workgroup. Per plane a load is then one buffer_load with the plane's base in
 // an SGPR resource and the precomputed offset, no address arithmetic; out-of-image elements carry
 // an offset past the resource's size, for which the hardware returns 0 (the zero padding).
-// Elements are dealt to the 256 threads in row-major order, so consecutive lanes read consecutive
+// Elements are dealt to the NTH threads in row-major order, so consecutive lanes read consecutive
 // columns; slots past the tile go to a dump slot after the plane (PLANE_STRIDE).
 // ------------------------------------------------------------------------------------------------
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(const float* p, int bytes) {
@@ -369,10 +319,10 @@ __device__ __forceinline__ float ld_f32(__amdgpu_buffer_rsrc_t r, unsigned off) 
     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
 }
 
-template <int IHT, int IWT, int IWP, int MODE>
+template <int IHT, int IWT, int IWP, int MODE, int NTH = 256>
 struct TileStager {
     static constexpr int NT = IHT * IWT;
-    static constexpr int NE = (NT + 255) / 256;  // elements per thread
+    static constexpr int NE = (NT + NTH - 1) / NTH;  // elements per thread
     static constexpr int PLANE = IHT * IWP;      // f2 slots of the plane ...
     static constexpr int PLANE_STRIDE = PLANE + 2;  // ... + the dump slot, 16-B aligned
     static constexpr bool UP = MODE == NCONV_LOAD_UPCAT_SKIP_FIRST || MODE == NCONV_LOAD_UPCAT_UP_FIRST;
@@ -385,7 +335,7 @@ struct TileStager {
         const nconv_layer& L = d.L;
 #pragma unroll
         for (int k = 0; k < NE; ++k) {
-            const int e = tid + 256 * k;
+            const int e = tid + NTH * k;
             const int r = e / IWT, col = e - r * IWT;
             const int ih = ih0 + r, iw = iw0 + col;
             const bool in = e < NT && (unsigned)ih < (unsigned)L.H && (unsigned)iw < (unsigned)L.W;
@@ -427,13 +377,8 @@ struct TileStager {
 #pragma unroll
             for (int k = 0; k < NE; ++k) {
                 const unsigned o = UP ? (up ? gb[UP ? k : 0] : ga[k]) : ga[k];
-#ifdef NCONV_EXP_NO_LOADS
-                x[k] = (float)(o & 255);
-                c[k] = 1.f;
-#else
                 x[k] = ld_f32(rx, o);
                 c[k] = ld_f32(rc, o);
-#endif
             }
         }
     }

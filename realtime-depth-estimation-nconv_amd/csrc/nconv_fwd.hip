@@ -7,44 +7,51 @@
 // op_sel_hi:[0,1,1]): the weight stream is wave-uniform and rides the scalar cache, the packed
 // {x*c, c} operand is staged once per input element in LDS.
 //
-// Tiling: a 256-thread workgroup owns a 16 x 64 output tile of one image and all Cout channels;
-// each thread owns 4 horizontally adjacent pixels (a sliding window of 4+K-1 staged inputs per
-// kernel row feeds K*4*Cout packed FMAs). Input channels are staged one plane of
-// (16+K-1) x (64+K-1) {x*c, c} pairs at a time into two LDS buffers (register-staged software
-// pipeline), with the layer's glue (threshold / 2x2 max-pool / nearest upsample + concat,
-// step1.py:53-90) evaluated while staging, so glued tensors never hit HBM.
+// Tiling: a 256-thread workgroup owns a TH x 32 output tile of one image; each thread owns 2
+// horizontally adjacent pixels (a sliding window of 2+K-1 staged inputs per kernel row feeds
+// 2*K*Cout/CS packed FMAs) of Cout/CS output channels, the workgroup's CS channel slices being
+// whole waves (TH = 16 / CS rows). Input channels are staged one plane of (TH+K-1) x (32+K-1)
+// {x*c, c} pairs at a time into two LDS buffers (register-staged software pipeline), with the
+// layer's glue (threshold / 2x2 max-pool / nearest upsample + concat, step1.py:53-90) evaluated
+// while staging, so glued tensors never hit HBM. CS = 1 for the full- and half-resolution layers;
+// the small layers split the channels so their few pixels still fill the chip (go_tiled).
+#include <cstdlib>
 #include "nconv_internal.h"
 
 namespace nconv {
 
 constexpr int kThreads = 256;
 
-template <int CIN, int K, int P_>
+template <int CIN, int K, int P_, int NTH, int CS>
 struct FwdCfg {
-    // P pixels per thread, 16 threads per tile row, 16 rows
-    static constexpr int P = P_, TW = 16 * P, TH = 16;
+    // P pixels per thread, 16 threads per tile row; the NTH threads form CS groups (one per slice
+    // of COUT / CS output channels) of NTH / CS threads each, so NTH / (16 CS) rows per tile
+    static constexpr int P = P_, TW = 16 * P, TG = NTH / CS, TH = TG / 16;
     static constexpr int IHT = TH + K - 1, IWT = TW + K - 1;
     static constexpr int IWP = (IWT + 1) & ~1;  // even pitch keeps the f4 reads 16-B aligned
-    static constexpr int PLANE = ((IHT + 3) / 4 * 4) * IWP;  // stage_plane writes whole 4-row groups
-    static constexpr int NV = P + K - 1;  // sliding-window width per kernel row
+    static constexpr int NV = P + K - 1;         // sliding-window width per kernel row
+    static_assert(IWT < 64, "narrow tiles: the buffer-load stager");
 };
 
-#ifdef NCONV_EXP_WAVES
-#define NCONV_FWD_ATTR __attribute__((amdgpu_waves_per_eu(NCONV_EXP_WAVES, NCONV_EXP_WAVES)))
-#else
-#define NCONV_FWD_ATTR
-#endif
-template <int CIN, int COUT, int K, int MODE, bool TAIL, int P>
-__global__ __launch_bounds__(kThreads) NCONV_FWD_ATTR void fwd_tiled(LayerDev d, float* __restrict__ y,
-                                                      float* __restrict__ yc, TailArgs t) {
-    using C = FwdCfg<CIN, K, P>;
-    using TS = TileStager<C::IHT, C::IWT, C::IWP, MODE>;
-    constexpr bool kBufStage = C::IWT < 64;  // buffer-load stager (narrow tiles)
-    constexpr int kStride = kBufStage ? TS::PLANE_STRIDE : C::PLANE;  // f2 per plane buffer
-    __shared__ __attribute__((aligned(16))) f2 tile[2 * kStride];
+template <int CIN, int COUT, int K, int MODE, bool TAIL, int P, int NTH, int CS>
+__global__ __launch_bounds__(NTH) void fwd_tiled(LayerDev d, float* __restrict__ y, float* __restrict__ yc,
+                                                 TailArgs t) {
+    using C = FwdCfg<CIN, K, P, NTH, CS>;
+    using TS = TileStager<C::IHT, C::IWT, C::IWP, MODE, NTH>;
+    constexpr int kStride = TS::PLANE_STRIDE;  // f2 per plane buffer
+    constexpr int CO = COUT / CS;              // output channels per thread
+    static_assert(COUT % CS == 0 && C::TG % 64 == 0 && (!TAIL || CS == 1), "channel slices are whole waves");
+    // CS > 1 (small layers): the input channels staged PG at a time (one load latency and one
+    // barrier per group instead of per channel); at most 8 planes of LDS, so up to 8 workgroups
+    // stay resident per CU and the small grids run in one round
+    constexpr bool ALLP = CS > 1;
+    constexpr int PG = CIN < 8 ? CIN : 8;
+    static_assert(!ALLP || CIN % PG == 0, "whole plane groups");
+    __shared__ __attribute__((aligned(16))) f2 tile[(ALLP ? PG : 2) * kStride];
     const nconv_layer& L = d.L;
-    const float* __restrict__ wgt = L.weight;
     const int tid = threadIdx.x;
+    const int og = __builtin_amdgcn_readfirstlane(tid / C::TG), lt = tid % C::TG;  // slice, thread in it
+    const float* __restrict__ wgt = L.weight + (size_t)og * CO * CIN * K * K;
     const int gh = TAIL ? t.out_h : L.Ho, gw = TAIL ? t.out_w : L.Wo;  // the written grid
     const TileCoord tc = xcd_tile((gw + C::TW - 1) / C::TW, (gh + C::TH - 1) / C::TH, L.B);
     const int b = tc.b;
@@ -52,11 +59,11 @@ __global__ __launch_bounds__(kThreads) NCONV_FWD_ATTR void fwd_tiled(LayerDev d,
     const int off = TAIL ? t.off : 0;
     const int oh0 = R0 + off, ow0 = C0 + off;  // tile origin in this layer's output grid
     const int ih0 = oh0 - L.PH, iw0 = ow0 - L.PW;
-    const int ty = tid >> 4, tx = (tid & 15) * C::P;
+    const int ty = lt >> 4, tx = (lt & 15) * C::P;
 
-    f2 acc[COUT][C::P];
+    f2 acc[CO][C::P];
 #pragma unroll
-    for (int o = 0; o < COUT; ++o)
+    for (int o = 0; o < CO; ++o)
 #pragma unroll
         for (int j = 0; j < C::P; ++j) acc[o][j] = (f2){0.f, 0.f};
 
@@ -83,31 +90,45 @@ __global__ __launch_bounds__(kThreads) NCONV_FWD_ATTR void fwd_tiled(LayerDev d,
 #pragma unroll
                 for (int m = 0; m < C::NV; ++m) v[m] = row[m];
             }
-#ifndef NCONV_FMA_REPEAT
-#define NCONV_FMA_REPEAT 1
-#endif
 #pragma unroll
-            for (int rep = 0; rep < NCONV_FMA_REPEAT; ++rep)
+            for (int kw = 0; kw < K; ++kw)
 #pragma unroll
-                for (int kw = 0; kw < K; ++kw)
+                for (int o = 0; o < CO; ++o) {
+                    const float w = wr[o * CIN * K * K + kw];
+                    const f2 w2 = (f2){w, w};
 #pragma unroll
-                    for (int o = 0; o < COUT; ++o) {
-                        const float w = wr[o * CIN * K * K + kw];
-                        const f2 w2 = (f2){w, w};
-#pragma unroll
-                        for (int j = 0; j < C::P; ++j)
-                            acc[o][j] = __builtin_elementwise_fma(w2, v[j + kw], acc[o][j]);
-                    }
+                    for (int j = 0; j < C::P; ++j) acc[o][j] = __builtin_elementwise_fma(w2, v[j + kw], acc[o][j]);
+                }
         }
     };
 
-    // Software pipeline over input channels with two LDS plane buffers and one barrier per
-    // channel (a buffer is rewritten two steps after it was read, with a barrier in between).
-    if constexpr (kBufStage) {
-        // Loads run two planes ahead: plane ci+2's buffer loads are issued right after plane ci
-        // is stored, so each has two planes of FMAs to land.
-        TS ts;
-        ts.init(d, ih0, iw0, tid);
+    TS ts;
+    ts.init(d, ih0, iw0, tid);
+    if constexpr (ALLP) {
+        // small tiles: a group's loads in flight together, then one store phase and one barrier
+        // (the per-plane pipeline below serialises one load latency per plane, which the few FMAs
+        // of a small tile's plane cannot cover); the next group's loads fly during this one's FMAs
+        float xs[PG][TS::NE], cs_[PG][TS::NE];
+#pragma unroll
+        for (int i = 0; i < PG; ++i) ts.load(chan_src<MODE>(d, b, i), xs[i], cs_[i]);
+#pragma unroll
+        for (int g0 = 0; g0 < CIN; g0 += PG) {
+            if (g0) __syncthreads();  // every wave is done with the previous group's planes
+#pragma unroll
+            for (int i = 0; i < PG; ++i) ts.store(tile + i * kStride, xs[i], cs_[i], L.thresh);
+            __syncthreads();
+            if (g0 + PG < CIN) {
+#pragma unroll
+                for (int i = 0; i < PG; ++i) ts.load(chan_src<MODE>(d, b, g0 + PG + i), xs[i], cs_[i]);
+            }
+#pragma unroll 1
+            for (int i = 0; i < PG; ++i) fma_plane(g0 + i, i);
+        }
+    } else {
+        // Software pipeline over input channels with two LDS plane buffers and one barrier per
+        // channel (a buffer is rewritten two steps after it was read, with a barrier in between).
+        // Loads run two planes ahead: plane ci+2's buffer loads are issued right after plane ci is
+        // stored, so each has two planes of FMAs to land.
         float xa[TS::NE], ca[TS::NE], xb[TS::NE], cb[TS::NE];
         ts.load(chan_src<MODE>(d, b, 0), xa, ca);
         if (CIN > 1) ts.load(chan_src<MODE>(d, b, 1), xb, cb);
@@ -127,17 +148,6 @@ __global__ __launch_bounds__(kThreads) NCONV_FWD_ATTR void fwd_tiled(LayerDev d,
                 fma_plane(ci + 1, 1);
             }
         }
-    } else {
-        // wide tiles: loads one plane ahead through the column-mapped register stage
-        PlaneStage<C::IHT, C::IWT, C::IWP> pr;
-        pr.load(d, chan_src<MODE>(d, b, 0), ih0, iw0, tid);
-#pragma unroll 1
-        for (int ci = 0; ci < CIN; ++ci) {
-            pr.store(d, tile + (ci & 1) * kStride, ih0, iw0, tid);
-            __syncthreads();
-            if (ci + 1 < CIN) pr.load(d, chan_src<MODE>(d, b, ci + 1), ih0, iw0, tid);
-            fma_plane(ci, ci & 1);
-        }
     }
 
     // ---- epilogue ----
@@ -146,17 +156,18 @@ __global__ __launch_bounds__(kThreads) NCONV_FWD_ATTR void fwd_tiled(LayerDev d,
         constexpr int VW = C::P % 4 == 0 ? 4 : C::P % 2 == 0 ? 2 : 1;  // vector store width
         const bool vec = (L.Wo % VW) == 0 && (ow0 + tx + C::P - 1) < L.Wo;
         // optional fused 2x2 max-pool of the outputs (the next down layer's input, step1.py:62-75):
-        // rows oh and oh^1 sit in lanes l and l^16 of one wave (ty = tid >> 4, tile origin even)
+        // rows oh and oh^1 sit in lanes l and l^16 of one wave (ty = lt >> 4, tile origin even)
         const bool pool = t.py != nullptr;
         const int Hp = L.Ho >> 1, Wp = L.Wo >> 1;
         const int pr = oh >> 1, pc0 = (ow0 + tx) >> 1;
         const bool pool_row = pool && ((ty & 1) == 0) && pr < Hp;
 #pragma unroll
-        for (int o = 0; o < COUT; ++o) {
+        for (int oo = 0; oo < CO; ++oo) {
+            const int o = og * CO + oo;
             const float s = L.wsum[o], bo = L.bias[o];
             float yv[C::P], cv[C::P];
 #pragma unroll
-            for (int j = 0; j < C::P; ++j) nconv_epilogue(acc[o][j].x, acc[o][j].y, L.eps, bo, s, yv[j], cv[j]);
+            for (int j = 0; j < C::P; ++j) nconv_epilogue(acc[oo][j].x, acc[oo][j].y, L.eps, bo, s, yv[j], cv[j]);
             if (pool) {  // every lane joins the shuffles
                 float yb[C::P], cb[C::P];
 #pragma unroll
@@ -167,7 +178,7 @@ __global__ __launch_bounds__(kThreads) NCONV_FWD_ATTR void fwd_tiled(LayerDev d,
                 if constexpr (C::P == 1) {  // the window's right column sits in lane l^1
                     const float ya = __shfl_xor(yv[0], 1), ca = __shfl_xor(cv[0], 1);
                     const float yd = __shfl_xor(yb[0], 1), cd = __shfl_xor(cb[0], 1);
-                    if (pool_row && (tid & 1) == 0 && pc0 < Wp) {
+                    if (pool_row && (lt & 1) == 0 && pc0 < Wp) {
                         const size_t pi = plane_idx(b, o, COUT, Hp, Wp, pr, pc0);
                         t.py[pi] = pool4v(yv[0], ya, yb[0], yd);
                         t.pc[pi] = pool4v(cv[0], ca, cb[0], cd);
@@ -182,9 +193,6 @@ __global__ __launch_bounds__(kThreads) NCONV_FWD_ATTR void fwd_tiled(LayerDev d,
                         }
                 }
             }
-#ifdef NCONV_EXP_NO_STORES
-            if (yv[0] != 1234.5f) continue;
-#endif
             if (oh >= L.Ho) continue;
             const size_t base = plane_idx(b, o, COUT, L.Ho, L.Wo, oh, ow0 + tx);
             if (vec) {
@@ -342,20 +350,43 @@ static bool simple_geometry(const nconv_layer& L) {
     return L.SH == 1 && L.SW == 1 && L.DH == 1 && L.DW == 1 && L.groups == 1 && L.KH == L.KW;
 }
 
-template <int CIN, int COUT, int K, int MODE, bool TAIL, int P>
-static void go_tiled_p(const LayerDev& d, float* y, float* yc, const TailArgs& t, int gh, int gw,
-                       hipStream_t st) {
-    using C = FwdCfg<CIN, K, P>;
+template <int CIN, int COUT, int K, int MODE, bool TAIL, int CS>
+static void go_tiled_cs(const LayerDev& d, float* y, float* yc, const TailArgs& t, int gh, int gw, hipStream_t st) {
+    using C = FwdCfg<CIN, K, 2, 256, CS>;
     dim3 grid(((gw + C::TW - 1) / C::TW) * ((gh + C::TH - 1) / C::TH) * d.L.B);  // see xcd_tile
-    hipLaunchKernelGGL((fwd_tiled<CIN, COUT, K, MODE, TAIL, P>), grid, dim3(kThreads), 0, st, d, y, yc, t);
+    hipLaunchKernelGGL((fwd_tiled<CIN, COUT, K, MODE, TAIL, 2, 256, CS>), grid, dim3(256), 0, st, d, y, yc, t);
 }
 
-// 2 pixels per thread: 32 x 16 tiles (measured against P = 1 and P = 4: 4 pixels needs 105-125
-// VGPRs, 4 waves/SIMD; 1 pixel doubles the LDS reads per FMA)
+// 2 pixels per thread, 32-column tiles, 256 threads (measured against 1 and 4 pixels: 4 needs
+// 105-125 VGPRs, 4 waves/SIMD; 1 doubles the LDS reads per FMA). A thread computes all 8 output
+// channels of its pixels while the layer has at least four 16-row tiles per CU (the full and half
+// resolution layers); the small quarter / eighth-resolution layers would leave most SIMDs with no
+// wave at all, so their waves split the output channels (2 or 4 slices, on 8- or 4-row tiles;
+// a slice is whole waves, so its weights stay wave-uniform) and the layer spreads over the whole
+// chip. NCONV_TILED_CS forces a slice count.
+static int tiled_cs(long tiles16, int cout, int mode) {
+    static const int forced = [] {
+        const char* e = getenv("NCONV_TILED_CS");
+        return e ? atoi(e) : 0;
+    }();
+    // (the max-pooling loads of the down layers gain from the shorter pipeline already at half
+    // resolution: down1 66 vs 72 us at B=8 352x1216; nconv5 does not, 56 vs 53 us)
+    const long big = mode == NCONV_LOAD_POOL2 ? 2048 : 1024;
+    int cs = forced ? forced : tiles16 >= big ? 1 : tiles16 >= 512 ? 2 : 4;
+    if (cs > 4) cs = 4;
+    while (cs > 1 && cout % cs) cs >>= 1;
+    return cs;
+}
+
 template <int CIN, int COUT, int K, int MODE, bool TAIL>
-static void go_tiled(const LayerDev& d, float* y, float* yc, const TailArgs& t, int gh, int gw,
-                     hipStream_t st) {
-    go_tiled_p<CIN, COUT, K, MODE, TAIL, 2>(d, y, yc, t, gh, gw, st);
+static void go_tiled(const LayerDev& d, float* y, float* yc, const TailArgs& t, int gh, int gw, hipStream_t st) {
+    const long tiles16 = (long)((gw + 31) / 32) * ((gh + 15) / 16) * d.L.B;
+    const int cs = (TAIL || MODE == NCONV_LOAD_THRESH) ? 1 : tiled_cs(tiles16, COUT, MODE);
+    if constexpr (!TAIL && COUT % 8 == 0) {
+        if (cs == 4) return go_tiled_cs<CIN, COUT, K, MODE, TAIL, 4>(d, y, yc, t, gh, gw, st);
+        if (cs == 2) return go_tiled_cs<CIN, COUT, K, MODE, TAIL, 2>(d, y, yc, t, gh, gw, st);
+    }
+    go_tiled_cs<CIN, COUT, K, MODE, TAIL, 1>(d, y, yc, t, gh, gw, st);
 }
 
 int launch_fwd(const LayerDev& d, float* y, float* yc, float* py, float* pc, hipStream_t st, const char** why) {
