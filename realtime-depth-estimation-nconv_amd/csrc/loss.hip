@@ -9,20 +9,24 @@
 // On B planes of (H, W): the training loop calls it on the whole (B, 1, H, W) batch
 // (train_step1.py:63; the means run over B*H*W, the Sobel convolutions pad each image on its own),
 // the validation loop on element [0] (utils.py:36, B = 1). In PyTorch this is ~45 elementwise /
-// reduction launches forward and backward; here:
-//   loss_partials  one thread per pixel: e^2, |gx|, |gy| (3x3 window of diff, the same operation
-//                  order as train.gradient_x / _y, so signs match torch exactly), per-block sums
-//   loss_finalize  one block: fixed-order (double) sum of the block partials -> L and the two
+// reduction launches forward and backward; here, on 16 x 64 pixel tiles whose diff window
+// (diff = t - masked r, 2-pixel halo, zero outside the image) is staged once in LDS:
+//   loss_partials  per tile: e^2, |gx|, |gy| (the same operation order as train.gradient_x / _y,
+//                  so signs match torch exactly), one per-tile partial of each
+//   loss_finalize  one block: fixed-order (double) sum of the tile partials -> L and the two
 //                  backward coefficients, kept in the workspace for the backward
-//   loss_grad      one thread per pixel: dL/dr = go m [c_e e - c_g sum_q (sign gx(q) Kx(p - q) +
-//                  sign gy(q) Ky(p - q))] over the 3x3 neighbours q inside the plane (5x5 diff
-//                  window), with torch's sign(0) = 0 for |.|'.
+//   loss_grad      per tile: the signs of gx, gy over the tile + 1-pixel halo into LDS, then
+//                  dL/dr = go m [c_e e - c_g sum_q (sign gx(q) Kx(p - q) + sign gy(q) Ky(p - q))]
+//                  over the 3x3 neighbours q inside the plane, with torch's sign(0) = 0 for |.|'.
 // Deterministic (no atomics). The planes may be row-strided views (the cropped DNET output).
 #include "nconv_internal.h"
 
 namespace nconv {
 
 constexpr int kLT = 256;
+constexpr int kTH = 16, kTW = 64;                // pixel tile of one workgroup (4 pixels per thread)
+constexpr int kDH = kTH + 4, kDW = kTW + 4;      // staged diff window (2-pixel halo)
+constexpr int kSH = kTH + 2, kSW = kTW + 2;      // sign window (1-pixel halo)
 
 struct LossPlane {
     const float* r;
@@ -63,6 +67,29 @@ __device__ __forceinline__ float sobel_y(D d, int i, int j) {
     return (a + 2.f * b) + c;
 }
 
+// Tiles of the grid: (tiles per image row band) x (row bands) x B, blockIdx.x linear.
+struct LossTile {
+    int b, i0, j0;
+};
+__device__ __forceinline__ LossTile loss_tile(const LossPlane& p) {
+    const int ntw = (p.W + kTW - 1) / kTW, nth = (p.H + kTH - 1) / kTH;
+    const int t = blockIdx.x;
+    LossTile lt;
+    lt.b = t / (ntw * nth);
+    const int r = t - lt.b * ntw * nth;
+    lt.i0 = (r / ntw) * kTH;
+    lt.j0 = (r % ntw) * kTW;
+    return lt;
+}
+
+// The tile's diff window (rows i0-2 .. i0+kTH+1, columns j0-2 .. j0+kTW+1) into LDS.
+__device__ __forceinline__ void stage_diff(const LossPlane& p, int i0, int j0, float* dw) {
+    for (int e = threadIdx.x; e < kDH * kDW; e += kLT) {
+        const int a = e / kDW, c = e - a * kDW;
+        dw[e] = loss_diff(p, i0 - 2 + a, j0 - 2 + c);
+    }
+}
+
 __device__ __forceinline__ float block_sum256(float v, float* red) {
 #pragma unroll
     for (int s = 32; s > 0; s >>= 1) v += __shfl_xor(v, s);
@@ -73,30 +100,36 @@ __device__ __forceinline__ float block_sum256(float v, float* red) {
     return ((red[0] + red[1]) + red[2]) + red[3];
 }
 
-// grid: (blocks per plane, B); the partial sums are indexed plane-major (a fixed order)
+// one workgroup per tile; the partial sums are indexed by tile (a fixed order)
 __global__ __launch_bounds__(kLT) void loss_partials(LossPlane pb, int grad_loss, float* __restrict__ part) {
+    __shared__ float dw[kDH * kDW];
     __shared__ float red[4];
-    const LossPlane p = pb.image(blockIdx.y);
-    const int n = p.H * p.W, e = blockIdx.x * kLT + threadIdx.x;
+    const LossTile lt = loss_tile(pb);
+    const LossPlane p = pb.image(lt.b);
+    stage_diff(p, lt.i0, lt.j0, dw);
+    __syncthreads();
+    // window accessor in plane coordinates
+    auto d = [&](int a, int b) { return dw[(a - lt.i0 + 2) * kDW + (b - lt.j0 + 2)]; };
     float sq = 0.f, ax = 0.f, ay = 0.f;
-    if (e < n) {
-        const int i = e / p.W, j = e - i * p.W;
-        const float dv = loss_diff(p, i, j);
-        sq = dv * dv;  // (rec - t)^2
-        if (grad_loss) {
-            auto d = [&](int a, int b) { return loss_diff(p, a, b); };
-            ax = fabsf(sobel_x(d, i, j));
-            ay = fabsf(sobel_y(d, i, j));
+#pragma unroll
+    for (int k = 0; k < kTH * kTW / kLT; ++k) {
+        const int e = threadIdx.x + kLT * k, i = lt.i0 + e / kTW, j = lt.j0 + e % kTW;
+        if (i < p.H && j < p.W) {
+            const float dv = d(i, j);
+            sq += dv * dv;  // (rec - t)^2
+            if (grad_loss) {
+                ax += fabsf(sobel_x(d, i, j));
+                ay += fabsf(sobel_y(d, i, j));
+            }
         }
     }
     sq = block_sum256(sq, red);
     ax = block_sum256(ax, red);
     ay = block_sum256(ay, red);
     if (threadIdx.x == 0) {
-        const int blk = blockIdx.y * gridDim.x + blockIdx.x;
-        part[3 * blk] = sq;
-        part[3 * blk + 1] = ax;
-        part[3 * blk + 2] = ay;
+        part[3 * blockIdx.x] = sq;
+        part[3 * blockIdx.x + 1] = ax;
+        part[3 * blockIdx.x + 2] = ay;
     }
 }
 
@@ -138,50 +171,60 @@ __device__ __forceinline__ float sgnf(float v) { return v > 0.f ? 1.f : (v < 0.f
 
 __global__ __launch_bounds__(kLT) void loss_grad(LossPlane pb, int grad_loss, const float* __restrict__ coef,
                                                   const float* __restrict__ gout, float* __restrict__ g) {
-    const LossPlane p = pb.image(blockIdx.y);
-    const int n = p.H * p.W, e = blockIdx.x * kLT + threadIdx.x;
-    if (e >= n) return;
-    g += (size_t)blockIdx.y * n;  // contiguous (B, H, W) gradient
-    const int i = e / p.W, j = e - i * p.W;
-    const float t = p.t[i * p.ts + j];
-    if (t == 0.f) {  // masked_fill: no gradient reaches r here
-        g[e] = 0.f;
-        return;
+    __shared__ float dw[kDH * kDW];
+    __shared__ float sgx[kSH * kSW], sgy[kSH * kSW];
+    const LossTile lt = loss_tile(pb);
+    const LossPlane p = pb.image(lt.b);
+    const int n = p.H * p.W;
+    g += (size_t)lt.b * n;  // contiguous (B, H, W) gradient
+    stage_diff(p, lt.i0, lt.j0, dw);
+    __syncthreads();
+    auto d = [&](int a, int b) { return dw[(a - lt.i0 + 2) * kDW + (b - lt.j0 + 2)]; };
+    if (grad_loss) {
+        // signs of gx, gy at the tile's pixels and their 1-pixel halo; 0 outside the plane (such
+        // neighbours contribute nothing)
+        for (int e = threadIdx.x; e < kSH * kSW; e += kLT) {
+            const int a = e / kSW, c = e - a * kSW, qi = lt.i0 - 1 + a, qj = lt.j0 - 1 + c;
+            const bool in = (unsigned)qi < (unsigned)p.H && (unsigned)qj < (unsigned)p.W;
+            sgx[e] = in ? sgnf(sobel_x(d, qi, qj)) : 0.f;
+            sgy[e] = in ? sgnf(sobel_y(d, qi, qj)) : 0.f;
+        }
+        __syncthreads();
     }
     const float go = gout ? gout[0] : 1.f;
-    float dw[5][5];  // diff(i - 2 .. i + 2, j - 2 .. j + 2)
+    const float ce = coef[1], cg = coef[2];
 #pragma unroll
-    for (int a = 0; a < 5; ++a)
+    for (int k = 0; k < kTH * kTW / kLT; ++k) {
+        const int e = threadIdx.x + kLT * k, li = e / kTW, lj = e % kTW, i = lt.i0 + li, j = lt.j0 + lj;
+        if (i >= p.H || j >= p.W) continue;
+        if (p.t[i * p.ts + j] == 0.f) {  // masked_fill: no gradient reaches r here
+            g[i * p.W + j] = 0.f;
+            continue;
+        }
+        // dL/drec = c_e e - c_g G,  e = rec - t = -diff(p)
+        float acc = ce * (-d(i, j));
+        if (grad_loss) {
+            float G = 0.f;
 #pragma unroll
-        for (int b = 0; b < 5; ++b) dw[a][b] = loss_diff(p, i + a - 2, j + b - 2);
-    // dL/drec = c_e e - c_g G,  e = rec - t = -diff(p)
-    float acc = coef[1] * (-dw[2][2]);
-    if (grad_loss) {
-        float G = 0.f;
+            for (int qa = -1; qa <= 1; ++qa)
 #pragma unroll
-        for (int qa = -1; qa <= 1; ++qa)
-#pragma unroll
-            for (int qb = -1; qb <= 1; ++qb) {
-                const int qi = i + qa, qj = j + qb;
-                if ((unsigned)qi >= (unsigned)p.H || (unsigned)qj >= (unsigned)p.W) continue;
-                // window accessor centred on q (local coordinates of dw)
-                auto d = [&](int a, int b) { return dw[a - i + 2][b - j + 2]; };
-                const float sx = sgnf(sobel_x(d, qi, qj)), sy = sgnf(sobel_y(d, qi, qj));
-                // Kx(dy, dx) = w(dy) (-dx), Ky(dy, dx) = w(dx) (-dy), (dy, dx) = p - q, w = 1, 2, 1
-                const int dy = -qa, dx = -qb;
-                const float wy = dy == 0 ? 2.f : 1.f, wx = dx == 0 ? 2.f : 1.f;
-                G += sx * wy * (float)(-dx) + sy * wx * (float)(-dy);
-            }
-        // d|gx|/drec = -(d|gx|/ddiff)
-        acc -= coef[2] * G;
+                for (int qb = -1; qb <= 1; ++qb) {
+                    const int si = (li + 1 + qa) * kSW + (lj + 1 + qb);
+                    // Kx(dy, dx) = w(dy) (-dx), Ky(dy, dx) = w(dx) (-dy), (dy, dx) = p - q, w = 1, 2, 1
+                    const int dy = -qa, dx = -qb;
+                    const float wy = dy == 0 ? 2.f : 1.f, wx = dx == 0 ? 2.f : 1.f;
+                    G += sgx[si] * wy * (float)(-dx) + sgy[si] * wx * (float)(-dy);
+                }
+            // d|gx|/drec = -(d|gx|/ddiff)
+            acc -= cg * G;
+        }
+        g[i * p.W + j] = go * acc;
     }
-    g[e] = go * acc;
 }
 
-size_t loss_workspace_bytes(int B, int H, int W) {
-    const size_t nblk = (size_t)B * (((size_t)H * W + kLT - 1) / kLT);
-    return (3 * nblk + 4) * sizeof(float);
-}
+static int loss_tiles(int B, int H, int W) { return B * ((H + kTH - 1) / kTH) * ((W + kTW - 1) / kTW); }
+
+size_t loss_workspace_bytes(int B, int H, int W) { return (3 * (size_t)loss_tiles(B, H, W) + 4) * sizeof(float); }
 
 static int loss_err(const char** why) {
     hipError_t e = hipGetLastError();
@@ -194,20 +237,18 @@ static int loss_err(const char** why) {
 
 int launch_loss_fwd(const LossArgs& a, int grad_loss, float* loss, float* ws, hipStream_t st, const char** why) {
     const LossPlane p{a.r, a.t, a.rs, a.ts, a.rbs, a.tbs, a.B, a.H, a.W};
-    const int nblk = (a.H * a.W + kLT - 1) / kLT;
+    const int nblk = loss_tiles(a.B, a.H, a.W);
     float* coef = ws;
     float* part = ws + 4;
-    hipLaunchKernelGGL(loss_partials, dim3(nblk, a.B), dim3(kLT), 0, st, p, grad_loss, part);
-    hipLaunchKernelGGL(loss_finalize, dim3(1), dim3(kLT), 0, st, part, nblk * a.B, a.B * a.H * a.W, grad_loss, loss,
-                       coef);
+    hipLaunchKernelGGL(loss_partials, dim3(nblk), dim3(kLT), 0, st, p, grad_loss, part);
+    hipLaunchKernelGGL(loss_finalize, dim3(1), dim3(kLT), 0, st, part, nblk, a.B * a.H * a.W, grad_loss, loss, coef);
     return loss_err(why);
 }
 
 int launch_loss_bwd(const LossArgs& a, int grad_loss, const float* gout, const float* ws, float* g, hipStream_t st,
                     const char** why) {
     const LossPlane p{a.r, a.t, a.rs, a.ts, a.rbs, a.tbs, a.B, a.H, a.W};
-    const int nblk = (a.H * a.W + kLT - 1) / kLT;
-    hipLaunchKernelGGL(loss_grad, dim3(nblk, a.B), dim3(kLT), 0, st, p, grad_loss, ws, gout, g);
+    hipLaunchKernelGGL(loss_grad, dim3(loss_tiles(a.B, a.H, a.W)), dim3(kLT), 0, st, p, grad_loss, ws, gout, g);
     return loss_err(why);
 }
 
