@@ -245,11 +245,29 @@ def mfma_issued_flops(layer, B, H, W, math):
 
 # ---- CPU baseline ----------------------------------------------------------------------------------
 def host_cores():
-    """(threads this process may use, the machine's physical cores)."""
+    """(threads the CPU baseline uses, the machine's physical cores, how the first was found).
+    The thread count is what this process can actually run at once: its CPU affinity, capped by
+    the cgroup CPU quota when one is set (a GPU box's job may see every CPU of the machine but be
+    given a 16-CPU share; oversubscribing torch's thread pool on it is ~30x slower)."""
     try:
         usable = len(os.sched_getaffinity(0))
     except AttributeError:
         usable = os.cpu_count() or 1
+    how = "affinity"
+    for path in ("/sys/fs/cgroup/cpu.max", "/sys/fs/cgroup/cpu/cpu.cfs_quota_us"):
+        try:
+            txt = open(path).read().split()
+            if path.endswith("cpu.max"):
+                quota, period = txt[0], float(txt[1])
+            else:
+                quota, period = txt[0], float(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if quota != "max" and float(quota) > 0:
+                q = max(1, int(float(quota) / period))
+                if q < usable:
+                    usable, how = q, f"cgroup quota ({path})"
+            break
+        except (OSError, ValueError, IndexError):
+            continue
     phys = None
     try:
         seen = set()
@@ -266,7 +284,7 @@ def host_cores():
         phys = len(seen) or None
     except OSError:
         pass
-    return usable, phys
+    return usable, phys, how
 
 
 def cpu_baseline(B, H, W, seconds):
@@ -277,7 +295,7 @@ def cpu_baseline(B, H, W, seconds):
     from oracle import nconv_ref as R
     import nconv_pkg
     m = nconv_pkg.load()
-    usable, phys = host_cores()
+    usable, phys, how = host_cores()
     threads = usable
     torch.set_num_threads(threads)
     torch.manual_seed(0)
@@ -309,10 +327,10 @@ def cpu_baseline(B, H, W, seconds):
             return R.nconv2d(x, c, *nc["nconv7"], (1, 1), (2, 2))
         n1, el1 = timed(three_layer, 2000)
     return {"value": round(n * B / el, 3), "unit": "frames/sec", "cores": threads, "kind": "port",
-            "physical_cores_on_host": phys,
+            "physical_cores_on_host": phys, "threads_from": how,
             "sample": f"{n} B={B} {H}x{W} DNET forwards (config-2 workload, generalized crop; "
-                      f"oracle/nconv_ref.dnet_forward, fp32, torch CPU, {threads} threads = every core this "
-                      f"process may use) in {el:.1f} s",
+                      f"oracle/nconv_ref.dnet_forward, fp32, torch CPU, {threads} threads = every CPU this "
+                      f"process may run on at once) in {el:.1f} s",
             "config1_3layer_frames_per_sec": round(n1 / el1, 2),
             "config1_sample": f"{n1} single-frame {H}x{W} nconv1->nconv2->nconv7 forwards in {el1:.1f} s"}
 

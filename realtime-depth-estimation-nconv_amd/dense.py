@@ -8,7 +8,8 @@ Host side of nconv_dense_conv_fwd / nconv_dense_pack / nconv_conv3x3_c1 / nconv_
     ConvTranspose2d 4x4 s2 (+ bias, + fused ReLU, two-source input = the reference's torch.cat)
     and for the 3x3 -> 1 depth heads. Backward: the input gradient is the forward kernel on
     re-arranged weights (_dgrad_plan), the weight gradient nconv_dense_conv_wgrad, the bias
-    gradient a reduction; BatchNorm (batch statistics) stays a PyTorch-ROCm op between them.
+    gradient a reduction; training-mode BatchNorm (batch statistics + ReLU, forward and backward)
+    on libnconv's nconv_bn_train_* / nconv_relu_bias_bwd kernels (bn_relu).
 """
 import ctypes
 

@@ -8,10 +8,16 @@ the gradient all-reduce after backward:
     parameters that never receive a gradient (the unused bnorm.* of NConv2d, rgb_encoder4 of
     SETP2_BP_TRAIN, frozen step-1 weights) are skipped without DDP's unused-parameter search;
   * all_reduce(SUM) then / world_size, i.e. the gradient of the mean of the per-rank losses;
-  * BatchNorm statistics stay per replica (as DataParallel's replicas do); parameters and
-    buffers are broadcast from rank 0 once at wrap time.
+  * parameters and buffers are broadcast from rank 0 once at wrap time.
 EnforcePos mutates weights deterministically on every rank, so replicas stay identical without
 further communication.
+
+BatchNorm running statistics (SETP2's encoder / decoder, train mode): each rank updates its own
+from its own frames, as each nn.DataParallel replica does; DataParallel then keeps only device 0's
+replica as THE module, so its stats are device 0's. Policy here, the same: rank 0's buffers are the
+model's. sync_buffers() (every rank calls it, e.g. before evaluation or a checkpoint) broadcasts
+them; checkpoints are written by rank 0 (is_primary()), so a checkpoint and an evaluation see the
+buffers DataParallel would have.
 
 state_dict() keys carry the `module.` prefix, like nn.DataParallel's, so checkpoints written by
 save_checkpoint stay loadable by the reference's loaders (models/step2.py:32-35).
@@ -42,11 +48,32 @@ class DataParallelRCCL(nn.Module):
     def forward(self, *args, **kwargs):
         return self.module(*args, **kwargs)
 
+    def is_primary(self):
+        """True on the rank whose buffers (BatchNorm running statistics) are the model's."""
+        if not (dist.is_available() and dist.is_initialized()):
+            return True
+        return dist.get_rank() == self._src_rank()
+
+    @torch.no_grad()
+    def sync_buffers(self):
+        """Broadcast rank 0's buffers (BatchNorm running statistics) to every rank (collective:
+        every rank calls it)."""
+        if self.world_size() <= 1:
+            return
+        for t in self.module.buffers():
+            dist.broadcast(t.data, src=self._src_rank(), group=self.process_group)
+
+    def grad_bucket(self):
+        """(name, gradient) of every parameter that has a gradient, in registration order: what one
+        allreduce_grads call reduces. Parameters without one (the unused bnorm.* of NConv2d, the
+        unused rgb_encoder4 and the frozen step 1 of SETP2_BP_TRAIN) are not in it."""
+        return [(n, p.grad) for n, p in self.module.named_parameters() if p.grad is not None]
+
     @torch.no_grad()
     def allreduce_grads(self):
         """Average present gradients across ranks in one bucketed all-reduce."""
         ws = self.world_size()
-        grads = [p.grad for p in self.module.parameters() if p.grad is not None]
+        grads = [g for _, g in self.grad_bucket()]
         if ws <= 1 or not grads:
             return
         flat = torch.cat([g.reshape(-1) for g in grads])

@@ -13,9 +13,12 @@ epilogue, and each torch.cat replaced by two-source loads / channel-offset store
 
 Training (or any forward that records autograd) on the device: every convolution is a
 dense.DenseConvFn / dense.HeadFn — forward, input gradient and weight gradient on the same MFMA
-kernels, ReLU after a bias-only convolution fused, torch.cat replaced by two-source loads —
-while BatchNorm (batch statistics, running-stat updates) and the bilinear depth downsampling stay
-PyTorch-ROCm ops. `model.dense_kernels = False` selects the plain PyTorch modules instead.
+kernels, ReLU after a bias-only convolution fused, torch.cat replaced by two-source loads — and
+training-mode BatchNorm (batch statistics, running-stat updates) + ReLU on libnconv's BN kernels
+(dense.bn_relu); only the bilinear depth downsampling (F.interpolate) stays a PyTorch-ROCm op.
+`model.dense_kernels = False` runs the dense layers as the plain torch modules — the fp32
+PyTorch reference the GPU tests compare the kernels against (tests/test_gpu_dense.py), not a
+product path (step 1 still runs on libnconv and refuses CPU tensors).
 """
 from collections import OrderedDict
 
