@@ -21,7 +21,7 @@ import os
 import torch
 import torch.nn as nn
 
-from . import _lib, nconv
+from . import _lib, export, nconv
 from .nconv import (EnforcePos, NConv2d, _require_device, layer_backward, layer_forward_head,
                     layer_forward_pooled, layer_forward_raw, nconv_layer, weight_prep)
 
@@ -165,6 +165,8 @@ class DNET(nn.Module):
 
     # -- forward ----------------------------------------------------------------------------------
     def forward(self, S):
+        if export.is_exporting():  # the export graph: the reference's own ops (export.py)
+            return export.dnet(self, S)
         _require_device(S, "DNET.forward")
         if S.dim() != 4 or S.shape[1] != 1:
             raise ValueError(f"DNET expects (B, 1, H, W) sparse depth, got {tuple(S.shape)}")

@@ -1,0 +1,49 @@
+"""Export graph of the NConv path: what torch.onnx.export / torch.jit.trace record.
+
+The reference exports SETP2_BP_EXPORT to ONNX (export_to_onnx.py:58-74, opset 17, dynamic batch).
+A graph of libnconv launches cannot be exported (the kernels are opaque to the tracer and to an
+ONNX runtime), so while a graph is being recorded (`is_exporting()`) NConv2d and DNET emit the
+reference's own operator sequence instead (models/step1.py:51-149: conv2d for the confidence mass
+and the numerator, the eps-guarded divide, bias, the weight-sum normaliser, the threshold,
+max_pool2d, nearest interpolation, cat and the crop) — standard ops every ONNX runtime executes.
+This is the export graph only: outside tracing the modules run libnconv and refuse CPU tensors.
+The guided model's dense layers are plain nn.Conv2d / ConvTranspose2d / BatchNorm2d modules and
+trace as such (guided._guided_forward's module path).
+"""
+import torch
+import torch.nn.functional as F
+
+
+def is_exporting():
+    """True while torch.jit.trace or torch.onnx.export records a graph."""
+    return torch.jit.is_tracing() or torch.onnx.is_in_onnx_export()
+
+
+def nconv2d(m, data, conf):
+    """NConv2d.forward as recorded ops (step1.py:116-149)."""
+    denom = F.conv2d(conf, m.weight, None, m.stride, m.padding, m.dilation, m.groups)
+    nomin = F.conv2d(data * conf, m.weight, None, m.stride, m.padding, m.dilation, m.groups)
+    nconv = nomin / (denom + m.eps)
+    nconv = nconv + m.bias.view(1, -1, 1, 1)
+    s = torch.sum(m.weight.reshape(m.weight.shape[0], -1), dim=-1, keepdim=True)  # (Cout, 1)
+    cout = denom / s.view(1, -1, 1, 1)
+    return nconv, cout
+
+
+def dnet(d, S):
+    """DNET.forward as recorded ops (step1.py:51-94), each NConv2d through nconv2d(), with the
+    module's crop (literal [1:481, 1:641] or generalized [1:H+1, 1:W+1])."""
+    c0 = (S > 0.01).float()
+    x1, c1 = nconv2d(d.nconv1, S, c0)
+    x1, c1 = nconv2d(d.nconv2, x1, c1)
+    x2, c2 = nconv2d(d.nconv_down1, F.max_pool2d(x1, 2, 2), F.max_pool2d(c1, 2, 2))
+    x3, c3 = nconv2d(d.nconv_down2, F.max_pool2d(x2, 2, 2), F.max_pool2d(c2, 2, 2))
+    x4, c4 = nconv2d(d.nconv_down3, F.max_pool2d(x3, 2, 2), F.max_pool2d(c3, 2, 2))
+    up = lambda t, ref: F.interpolate(t, ref.shape[2:], mode="nearest")
+    x34, c34 = nconv2d(d.nconv4, torch.cat((x3, up(x4, c3)), 1), torch.cat((c3, up(c4, c3)), 1))
+    x23, c23 = nconv2d(d.nconv5, torch.cat((x2, up(x34, c2)), 1), torch.cat((c2, up(c34, c2)), 1))
+    xo, co = nconv2d(d.nconv6, torch.cat((up(x23, S), x1), 1), torch.cat((up(c23, S), c1), 1))
+    xo, co = nconv2d(d.nconv7, xo, co)
+    if d.crop == "literal":
+        return xo[:, :, 1:481, 1:641]
+    return xo[:, :, 1:S.shape[2] + 1, 1:S.shape[3] + 1]

@@ -16,7 +16,7 @@ import torch.nn.functional as F
 from torch.nn.modules.conv import _ConvNd
 from torch.nn.modules.utils import _pair
 
-from . import _lib
+from . import _lib, export
 
 
 # Arithmetic of the forward sums N = W*(x*c), D = W*c (include/nconv.h enum nconv_math): "fp32"
@@ -296,6 +296,8 @@ class NConv2d(_ConvNd):
         return wsum
 
     def forward(self, data, conf):
+        if export.is_exporting():  # the export graph: the reference's own ops (export.py)
+            return export.nconv2d(self, data, conf)
         _require_device(data, "NConv2d.forward")
         _require_device(conf, "NConv2d.forward")
         if data.shape != conf.shape:
