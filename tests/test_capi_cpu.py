@@ -147,8 +147,9 @@ def test_depth_loss_validation_is_host_only(nconv_amd):
     L = nconv_amd._lib
     lib = L.lib()
     ws_bytes = lib.nconv_depth_loss_workspace_bytes(1, 352, 1216)
-    assert ws_bytes >= (3 * ((352 * 1216 + 255) // 256) + 4) * 4
-    assert lib.nconv_depth_loss_workspace_bytes(8, 352, 1216) >= (3 * 8 * ((352 * 1216 + 255) // 256) + 4) * 4
+    tiles = lambda B, H, W: B * -(-H // 16) * -(-W // 64)  # one partial triple per 16 x 64 tile
+    assert ws_bytes >= (3 * tiles(1, 352, 1216) + 4) * 4
+    assert lib.nconv_depth_loss_workspace_bytes(8, 352, 1216) >= (3 * tiles(8, 352, 1216) + 4) * 4
     assert lib.nconv_depth_loss_workspace_bytes(1, 0, 5) == 0
     assert lib.nconv_depth_loss_workspace_bytes(0, 5, 5) == 0
     p = ctypes.c_void_p(0x1000)
