@@ -7,7 +7,7 @@ kernels behind the C ABI of include/nconv.h (libnconv.so, built in-tree).
 The directory name is not a Python identifier; import it through the repo-root helper
 `nconv_pkg.load()`, which registers it as the module `nconv_amd`.
 """
-from . import _lib, dense, dp, export, guided, train
+from . import _lib, data, dense, dp, export, guided, train
 from .nconv import EnforcePos, LayerSpec, NConv2d, NConvLayerFn, nconv_layer, weight_prep
 from .dnet import DNET, SETP1_NCONV, crop_hw
 from .guided import SETP2_BP_EXPORT, SETP2_BP_TRAIN, RGBEncoder
