@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define NCONV_ABI_VERSION 12
+#define NCONV_ABI_VERSION 13
 
 /* How a layer's input (data x, confidence c) is produced from its source tensors. These are the
  * DNET glue ops fused into the layer's load stage (models/step1.py:53,61-90). */
@@ -69,7 +69,10 @@ typedef struct nconv_layer {
     const float* weight; /* (Cout, Cin/groups, KH, KW), positive in practice                   */
     const float* bias;   /* (Cout)                                                              */
     const float* wsum;   /* (Cout): s[o] = sum of weight[o] (step1.py:141-144), see nconv_weight_prep */
-    int math;            /* enum nconv_math (forward only; 0 = default; other values: -EINVAL)  */
+    int math;            /* enum nconv_math of the forward sums (0 = default; other values: -EINVAL) */
+    int bwd_math;        /* enum nconv_math of the weight gradient's products (nconv_bwd, 3x3 / 5x5
+                            layers with Cin > 1): NCONV_MATH_FP32 = fp32 matrix cores (exact
+                            products), BF16X3 / BF16X9 = split-bf16 matrix cores; -EINVAL otherwise */
 } nconv_layer;
 
 /* ABI version, for the Python loader's sanity check. */

@@ -13,7 +13,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # NCONV_LIB: an alternative build of the same library (kernel-tuning experiments)
 LIB_PATH = os.environ.get("NCONV_LIB") or os.path.join(_HERE, "libnconv.so")
-ABI_VERSION = 12
+ABI_VERSION = 13
 BWD_ACCUMULATE = 1
 
 # enum nconv_load_mode
@@ -63,7 +63,7 @@ class NconvLayer(ctypes.Structure):
                 ("groups", ctypes.c_int), ("eps", ctypes.c_float), ("load_mode", ctypes.c_int),
                 ("thresh", ctypes.c_float), ("a", NconvSrc), ("b", NconvSrc),
                 ("weight", ctypes.c_void_p), ("bias", ctypes.c_void_p), ("wsum", ctypes.c_void_p),
-                ("math", ctypes.c_int)]
+                ("math", ctypes.c_int), ("bwd_math", ctypes.c_int)]
 
 
 class NconvDenseConv(ctypes.Structure):

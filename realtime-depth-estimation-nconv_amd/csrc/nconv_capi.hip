@@ -26,6 +26,8 @@ const char* validate(const nconv_layer* L, bool need_c) {
     if (ho != L->Ho || wo != L->Wo) return "Ho/Wo inconsistent with H/W/kernel/stride/padding/dilation";
     if (!L->weight || !L->bias || !L->wsum) return "null weight/bias/wsum";
     if (!L->a.x) return "null source a.x";
+    if (L->bwd_math != NCONV_MATH_BF16X3 && L->bwd_math != NCONV_MATH_FP32 && L->bwd_math != NCONV_MATH_BF16X9)
+        return "unknown bwd_math (enum nconv_math)";
     if (L->math != NCONV_MATH_BF16X3 && L->math != NCONV_MATH_FP32 && L->math != NCONV_MATH_BF16X9) return "unknown math (enum nconv_math)";
     switch (L->load_mode) {
         case NCONV_LOAD_PLAIN:

@@ -391,3 +391,40 @@ struct TileStager {
         }
     }
 };
+
+// (x, c) of layer-input pixel (ih, iw) of a resolved channel, zero outside the image (buffer
+// loads: out-of-range offsets read 0). THRESH leaves c to the caller.
+template <int MODE>
+__device__ __forceinline__ void load_px(const LayerDev& d, const ChanSrc& s, int ih, int iw, float& x, float& c) {
+    const nconv_layer& L = d.L;
+    const bool in = (unsigned)ih < (unsigned)L.H && (unsigned)iw < (unsigned)L.W;
+    constexpr unsigned OOB = 0x80000000u;
+    const __amdgpu_buffer_rsrc_t rx = plane_rsrc(s.x, s.bytes);
+    if constexpr (MODE == NCONV_LOAD_THRESH) {
+        x = ld_f32(rx, in ? (unsigned)(ih * s.W + iw) * 4u : OOB);
+        c = 0.f;
+    } else if constexpr (MODE == NCONV_LOAD_POOL2) {
+        const __amdgpu_buffer_rsrc_t rc = plane_rsrc(s.c, s.bytes);
+        const unsigned o1 = in ? (unsigned)((2 * ih) * s.W + 2 * iw) * 4u : OOB;
+        const unsigned o2 = in ? o1 + (unsigned)s.W * 4u : OOB;
+        const f2 x0 = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rx, o1, 0, 0));
+        const f2 x1 = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rx, o2, 0, 0));
+        const f2 c0 = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rc, o1, 0, 0));
+        const f2 c1 = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rc, o2, 0, 0));
+        x = pool4v(x0.x, x0.y, x1.x, x1.y);
+        c = pool4v(c0.x, c0.y, c1.x, c1.y);
+    } else {
+        const __amdgpu_buffer_rsrc_t rc = plane_rsrc(s.c, s.bytes);
+        unsigned off;
+        if (s.kind == kUp) {
+            const int sh = nearest_src(in ? ih : 0, L.b.H, L.H, d.up_scale_h);
+            const int sw = nearest_src(in ? iw : 0, L.b.W, L.W, d.up_scale_w);
+            off = in ? (unsigned)(sh * s.W + sw) * 4u : OOB;
+        } else {
+            off = in ? (unsigned)(ih * s.W + iw) * 4u : OOB;
+        }
+        x = ld_f32(rx, off);
+        c = ld_f32(rc, off);
+    }
+}
+

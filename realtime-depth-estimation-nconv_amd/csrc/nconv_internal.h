@@ -49,6 +49,10 @@ int launch_weight_prep(int n, float* const* w, const int* cout, const int* fan_i
 
 // Backward.
 size_t bwd_workspace_bytes(const LayerDev& d);
+// weight gradient on the bf16 matrix cores (nconv_wgrad_bf.hip): np = 2 (bf16x3) or 3 (bf16x9) split
+// parts; at most max_blocks partial rows into part; returns the number written
+template <int CIN, int COUT, int K, int MODE>
+int go_wgrad_bf(const LayerDev& d, const BwdArgs& a, float* part, int max_blocks, int np, hipStream_t st);
 int launch_bwd(const LayerDev& d, const BwdArgs& a, hipStream_t st, const char** why);
 
 // Dense convolutions (RGB-guided model).

@@ -20,6 +20,7 @@ int main(void) {
     F(nconv_layer, groups); F(nconv_layer, eps); F(nconv_layer, load_mode); F(nconv_layer, thresh);
     F(nconv_layer, a); F(nconv_layer, b); F(nconv_layer, weight); F(nconv_layer, bias); F(nconv_layer, wsum);
     F(nconv_layer, math);
+    F(nconv_layer, bwd_math);
     S(nconv_dense_conv);
     F(nconv_dense_conv, B); F(nconv_dense_conv, x0); F(nconv_dense_conv, C0); F(nconv_dense_conv, x1);
     F(nconv_dense_conv, C1); F(nconv_dense_conv, H); F(nconv_dense_conv, W); F(nconv_dense_conv, Cout);
@@ -41,7 +42,7 @@ int main(void) {
     nconv_layer L = {0};
     L.B = 1; L.Cin = 8; L.H = 16; L.W = 16; L.Cout = 8; L.Ho = 16; L.Wo = 16;
     L.KH = L.KW = 5; L.SH = L.SW = L.DH = L.DW = L.groups = 1; L.PH = L.PW = 2; L.eps = 1e-7f;
-    L.load_mode = NCONV_LOAD_PLAIN; L.thresh = 0.01f; L.math = NCONV_MATH_FP32;
+    L.load_mode = NCONV_LOAD_PLAIN; L.thresh = 0.01f; L.math = NCONV_MATH_FP32; L.bwd_math = NCONV_MATH_FP32;
     const float* fake = (const float*)0x1000; /* never dereferenced: validation fails first */
     L.a.x = fake; L.a.c = fake; L.a.C = 8; L.a.H = 16; L.a.W = 16;
     L.weight = L.bias = L.wsum = fake;

@@ -75,8 +75,15 @@ def test_layer_forward(nconv_amd, gpu, case, fwd_math):
         print(f"{name} [{fwd_math}]: max rel err {(err / (ref.abs() + 1e-30)).max():.2e}")
 
 
+@pytest.fixture(params=["bf16x3", "bf16x9", "fp32"])
+def bwd_math(request, nconv_amd, monkeypatch):
+    """Every weight-gradient arithmetic (include/nconv.h nconv_layer.bwd_math)."""
+    monkeypatch.setattr(nconv_amd.nconv, "BACKWARD_MATH", {"bf16x3": 0, "fp32": 1, "bf16x9": 2}[request.param])
+    return request.param
+
+
 @pytest.mark.parametrize("case", LAYER_CASES, ids=[c[0] for c in LAYER_CASES])
-def test_layer_backward(nconv_amd, gpu, case):
+def test_layer_backward(nconv_amd, gpu, case, bwd_math):
     xa, ca, xb, cb, w, b = _build(case, 4321)
     name, mode, cin, cout, k, pad, stride, dil, groups, *_ = case
     leaves = [t.clone().requires_grad_(True) if t is not None else None for t in (xa, ca, xb, cb, w, b)]
@@ -97,7 +104,9 @@ def test_layer_backward(nconv_amd, gpu, case):
         ref = ref_leaf.grad
         got = got_leaf.grad.double().cpu()
         rel = ((got - ref).abs().max() / ref.abs().max().clamp_min(1e-30)).item()
-        assert rel <= 1e-3, f"{name} {lab}: normwise rel err {rel:.3e}"
+        assert rel <= 1e-3, f"{name} {lab} [{bwd_math}]: normwise rel err {rel:.3e}"
+        if lab == "g_w":
+            print(f"{name} g_w [{bwd_math}]: normwise rel err {rel:.2e}")
 
 
 @pytest.mark.parametrize("case", [c for c in LAYER_CASES if c[0] in ("nconv2_plain", "down_pool_odd",
