@@ -14,6 +14,7 @@
 // wgrad accumulates per-workgroup partial sums in registers over several tiles and a second
 // kernel reduces them in a fixed order (bitwise deterministic, no float atomics).
 #include "nconv_internal.h"
+#include "nconv_route.h"
 
 namespace nconv {
 
@@ -24,85 +25,6 @@ constexpr int pick_chunk(int n, int plane_f2, int budget) {
     for (int cc = 1; cc <= n; ++cc)
         if (n % cc == 0 && cc * plane_f2 * 8 <= budget) best = cc;
     return best;
-}
-
-// ---- gradient routing from a layer-input pixel to the producer tensors --------------------------
-// a.accumulate != 0: += into the outputs; == 0: overwrite (every element of every requested output
-// is written exactly once, so the caller need not zero-fill; see pool_zero_leftovers).
-__device__ __forceinline__ void put(float* p, size_t i, float v, bool acc) {
-    if (acc) p[i] += v;
-    else p[i] = v;
-}
-
-template <int MODE>
-__device__ __forceinline__ void route_grad(const LayerDev& d, const BwdArgs& a, int b, int ci, int ih,
-                                           int iw, float gxc, float gc_direct, float* tmp_x,
-                                           float* tmp_c) {
-    const nconv_layer& L = d.L;
-    const bool acc = a.accumulate != 0;
-    if constexpr (MODE == NCONV_LOAD_PLAIN) {
-        const size_t i = plane_idx(b, ci, L.a.C, L.a.H, L.a.W, ih, iw);
-        const float x = L.a.x[i], c = L.a.c[i];
-        if (a.gxa) put(a.gxa, i, gxc * c, acc);
-        if (a.gca) put(a.gca, i, gc_direct + gxc * x, acc);
-    } else if constexpr (MODE == NCONV_LOAD_THRESH) {
-        const size_t i = plane_idx(b, ci, L.a.C, L.a.H, L.a.W, ih, iw);
-        const float x = L.a.x[i];
-        const float c = (x > L.thresh) ? 1.0f : 0.0f;
-        if (a.gxa) put(a.gxa, i, gxc * c, acc);  // c = (S > thr) carries no gradient
-    } else if constexpr (MODE == NCONV_LOAD_POOL2) {
-        const size_t i0 = plane_idx(b, ci, L.a.C, L.a.H, L.a.W, 2 * ih, 2 * iw);
-        const size_t W2 = (size_t)L.a.W;
-        const size_t off[4] = {0, 1, W2, W2 + 1};
-        int ax, ac;
-        const float x = pool4(L.a.x[i0], L.a.x[i0 + 1], L.a.x[i0 + W2], L.a.x[i0 + W2 + 1], ax);
-        const float c = pool4(L.a.c[i0], L.a.c[i0 + 1], L.a.c[i0 + W2], L.a.c[i0 + W2 + 1], ac);
-        const float gx = gxc * c, gc = gc_direct + gxc * x;
-        if (acc) {
-            if (a.gxa) a.gxa[i0 + off[ax]] += gx;
-            if (a.gca) a.gca[i0 + off[ac]] += gc;
-        } else {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                if (a.gxa) a.gxa[i0 + off[k]] = (k == ax) ? gx : 0.f;
-                if (a.gca) a.gca[i0 + off[k]] = (k == ac) ? gc : 0.f;
-            }
-        }
-    } else {
-        const bool skip_first = (MODE == NCONV_LOAD_UPCAT_SKIP_FIRST);
-        const int first_c = skip_first ? L.a.C : L.b.C;
-        const bool from_a = skip_first ? (ci < first_c) : (ci >= first_c);
-        float x, c;
-        load_xc<MODE>(d, b, ci, ih, iw, x, c);
-        const float gx = gxc * c, gc = gc_direct + gxc * x;
-        if (from_a) {
-            const int ca = skip_first ? ci : ci - first_c;
-            const size_t i = plane_idx(b, ca, L.a.C, L.a.H, L.a.W, ih, iw);
-            if (a.gxa) put(a.gxa, i, gx, acc);
-            if (a.gca) put(a.gca, i, gc, acc);
-        } else {
-            const int cb = skip_first ? ci - first_c : ci;
-            const size_t i = plane_idx(b, cb, L.b.C, L.H, L.W, ih, iw);
-            tmp_x[i] = gx;
-            tmp_c[i] = gc;
-        }
-    }
-}
-
-// Overwrite mode, POOL2: source rows/cols that no 2x2 window covers (odd source H or W) get 0.
-__device__ __forceinline__ void pool_zero_leftovers(const LayerDev& d, const BwdArgs& a, int b, int ci, int ih,
-                                                    int iw) {
-    const nconv_layer& L = d.L;
-    const bool oddh = (L.a.H & 1) && ih == L.H - 1, oddw = (L.a.W & 1) && iw == L.W - 1;
-    if (!(oddh || oddw)) return;
-    const size_t base = plane_idx(b, ci, L.a.C, L.a.H, L.a.W, 0, 0);
-    auto z = [&](int h, int w) {
-        if (a.gxa) a.gxa[base + (size_t)h * L.a.W + w] = 0.f;
-        if (a.gca) a.gca[base + (size_t)h * L.a.W + w] = 0.f;
-    };
-    if (oddh) { z(L.a.H - 1, 2 * iw); z(L.a.H - 1, 2 * iw + 1); }
-    if (oddw) { z(2 * ih, L.a.W - 1); z(2 * ih + 1, L.a.W - 1); }
-    if (oddh && oddw) z(L.a.H - 1, L.a.W - 1);
 }
 
 // Staging of output-side planes {gN, gD} over an OHT x OWT halo tile (origin oh0, ow0) for the
@@ -1072,13 +994,20 @@ static void go_bwd_tiled(const LayerDev& d, const BwdArgs& a, float* part, float
     const nconv_layer& L = d.L;
     using D = DgCfg<CIN, K>;
     if (a.gxa || a.gca || a.gxb || a.gcb) {
-        dim3 g(((L.W + D::TW - 1) / D::TW) * ((L.H + D::TH - 1) / D::TH) * L.B);  // see xcd_tile
-        hipLaunchKernelGGL((dgrad_tiled<CIN, COUT, K, MODE>), g, dim3(kT), 0, st, d, a, tx, tc);
+        if (K > 1 && CIN > 1 && L.bwd_math != NCONV_MATH_FP32) {  // split-bf16 matrix cores
+            if constexpr (K > 1 && CIN > 1)
+                go_dgrad_bf<CIN, COUT, K, MODE>(d, a, tx, tc, L.bwd_math == NCONV_MATH_BF16X9 ? 3 : 2, st);
+        } else {
+            dim3 g(((L.W + D::TW - 1) / D::TW) * ((L.H + D::TH - 1) / D::TH) * L.B);  // see xcd_tile
+            hipLaunchKernelGGL((dgrad_tiled<CIN, COUT, K, MODE>), g, dim3(kT), 0, st, d, a, tx, tc);
+        }
     }
     if constexpr (K > 1 && CIN > 1) {
-        if ((a.gw || a.gb) && L.bwd_math != NCONV_MATH_FP32) {  // split-bf16 matrix cores
-            const int nblk = go_wgrad_bf<CIN, COUT, K, MODE>(d, a, part, (int)wm_grid(L).nblk,
-                                                             L.bwd_math == NCONV_MATH_BF16X9 ? 3 : 2, st);
+        int nblk = -1;  // split-bf16 matrix cores (-1: the grid would not fit the workspace)
+        if ((a.gw || a.gb) && L.bwd_math != NCONV_MATH_FP32)
+            nblk = go_wgrad_bf<CIN, COUT, K, MODE>(d, a, part, (int)wm_grid(L).nblk,
+                                                   L.bwd_math == NCONV_MATH_BF16X9 ? 3 : 2, st);
+        if (nblk >= 0) {
             const int nw = COUT * CIN * K * K;
             launch_wgrad_reduce(part, nblk, nw, COUT, CIN * K * K, L.wsum, a.gw, a.gb,
                                 part + (size_t)nblk * (nw + 2 * COUT), st);

@@ -318,6 +318,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(const float* p, int
 __device__ __forceinline__ float ld_f32(__amdgpu_buffer_rsrc_t r, unsigned off) {
     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
 }
+// with a wave-uniform byte offset in soffset (a plane of a multi-plane resource); the range check
+// covers voffset + soffset, so an out-of-range voffset (>= 2^31) still reads 0
+__device__ __forceinline__ float ld_f32s(__amdgpu_buffer_rsrc_t r, unsigned off, int soff) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, soff, 0));
+}
 
 template <int IHT, int IWT, int IWP, int MODE, int NTH = 256>
 struct TileStager {

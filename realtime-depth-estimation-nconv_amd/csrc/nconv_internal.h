@@ -53,6 +53,9 @@ size_t bwd_workspace_bytes(const LayerDev& d);
 // parts; at most max_blocks partial rows into part; returns the number written
 template <int CIN, int COUT, int K, int MODE>
 int go_wgrad_bf(const LayerDev& d, const BwdArgs& a, float* part, int max_blocks, int np, hipStream_t st);
+// input gradient on the bf16 matrix cores (nconv_dgrad_bf.hip), np as go_wgrad_bf
+template <int CIN, int COUT, int K, int MODE>
+void go_dgrad_bf(const LayerDev& d, const BwdArgs& a, float* tmp_x, float* tmp_c, int np, hipStream_t st);
 int launch_bwd(const LayerDev& d, const BwdArgs& a, hipStream_t st, const char** why);
 
 // Dense convolutions (RGB-guided model).

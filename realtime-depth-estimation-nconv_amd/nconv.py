@@ -27,11 +27,13 @@ from . import _lib, export
 # further than in the reference. NCONV_FWD_MATH selects it; tests switch this global.
 _MATH_NAMES = {"bf16x3": _lib.MATH_BF16X3, "fp32": _lib.MATH_FP32, "bf16x9": _lib.MATH_BF16X9}
 FORWARD_MATH = _MATH_NAMES[os.environ.get("NCONV_FWD_MATH", "fp32")]
-# Arithmetic of the weight gradient's products (include/nconv.h nconv_layer.bwd_math): "bf16x3"
-# (default: split-bf16 matrix cores, ~1e-5 relative per product, well inside the backward's 1e-3
-# normwise tolerance), "bf16x9" (exact products) or "fp32" (fp32 matrix cores).
+# Arithmetic of the backward's products, weight and input gradient of the 3x3 / 5x5 layers with
+# several input channels (include/nconv.h nconv_layer.bwd_math): "fp32" (default: exact fp32
+# products — fp32 matrix cores for the weight gradient, packed fp32 on the vector ALU for the input
+# gradient), "bf16x3" (split-bf16 matrix cores, ~1e-5 relative per product, inside the backward's
+# 1e-3 normwise tolerance) or "bf16x9" (exact products on the bf16 matrix cores).
 # NCONV_BWD_MATH selects it; tests switch this global.
-BACKWARD_MATH = _MATH_NAMES[os.environ.get("NCONV_BWD_MATH", "bf16x3")]
+BACKWARD_MATH = _MATH_NAMES[os.environ.get("NCONV_BWD_MATH", "fp32")]
 
 
 def _require_device(t: torch.Tensor, what: str):

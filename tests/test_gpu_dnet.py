@@ -111,8 +111,14 @@ def test_enforcepos_drift(nconv_amd, gpu):
         assert torch.equal(v.detach(), w_eval[k]), "eval mode must not touch the weights"
 
 
+@pytest.fixture(params=["fp32", "bf16x3"])
+def bwd_math(request, nconv_amd, monkeypatch):
+    monkeypatch.setattr(nconv_amd.nconv, "BACKWARD_MATH", {"bf16x3": 0, "fp32": 1, "bf16x9": 2}[request.param])
+    return request.param
+
+
 @pytest.mark.parametrize("H,W", [(64, 96), (45, 67)])
-def test_dnet_train_gradients(nconv_amd, gpu, H, W):
+def test_dnet_train_gradients(nconv_amd, gpu, H, W, bwd_math):
     """Step-1 training gradients (EnforcePos + calculate_loss on [0] + backward) vs the fp64 oracle.
 
     Near an isolated depth sample every window holds the same single sample, so neighbouring

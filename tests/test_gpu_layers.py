@@ -77,7 +77,7 @@ def test_layer_forward(nconv_amd, gpu, case, fwd_math):
 
 @pytest.fixture(params=["bf16x3", "bf16x9", "fp32"])
 def bwd_math(request, nconv_amd, monkeypatch):
-    """Every weight-gradient arithmetic (include/nconv.h nconv_layer.bwd_math)."""
+    """Every backward arithmetic (include/nconv.h nconv_layer.bwd_math: weight and input gradient)."""
     monkeypatch.setattr(nconv_amd.nconv, "BACKWARD_MATH", {"bf16x3": 0, "fp32": 1, "bf16x9": 2}[request.param])
     return request.param
 
@@ -112,7 +112,7 @@ def test_layer_backward(nconv_amd, gpu, case, bwd_math):
 @pytest.mark.parametrize("case", [c for c in LAYER_CASES if c[0] in ("nconv2_plain", "down_pool_odd",
                                                                       "nconv5_upcat_inexact", "generic_stride2")],
                          ids=lambda c: c[0])
-def test_bwd_accumulate_flag(nconv_amd, gpu, case):
+def test_bwd_accumulate_flag(nconv_amd, gpu, case, bwd_math):
     """NCONV_BWD_ACCUMULATE adds into pre-filled input-gradient buffers; without it every element
     is overwritten (garbage-filled buffers must come out identical to zero-filled ones)."""
     import ctypes

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """One NConv layer backward at B=8 352x1216, repeated (developer tool for rocprofv3 / counter passes,
 GPU): python3 tools/bwd_layer_bench.py [nconv2|down1|nconv6|nconv5] [reps] -> us per backward.
-NCONV_BWD_MATH selects the weight-gradient arithmetic."""
+NCONV_BWD_MATH selects the backward arithmetic."""
 import os
 import sys
 
@@ -52,7 +52,7 @@ def main():
         step()
     e1.record()
     e1.synchronize()
-    print(f"{which} bwd [{os.environ.get('NCONV_BWD_MATH', 'bf16x3')}]: {e0.elapsed_time(e1) / reps * 1e3:.1f} us", flush=True)
+    print(f"{which} bwd [{os.environ.get('NCONV_BWD_MATH', 'fp32')}]: {e0.elapsed_time(e1) / reps * 1e3:.1f} us", flush=True)
 
 
 if __name__ == "__main__":
