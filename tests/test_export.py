@@ -10,7 +10,7 @@ CPU (no GPU needed):
     image; torch needs it only for an optional post-pass that attaches onnxscript functions (none
     here), so the test stubs that one pass and checks the serialized graph's operator types.
     Running the .onnx file in an ONNX runtime is parity-unpinned here (no runtime installed).
-GPU: tracing on device tensors (the reference exports on cuda) gives the HIP forward's outputs.
+GPU: tracing on device tensors (the reference exports on cuda) reproduces f2, as the HIP forward does.
 """
 import io
 import os
@@ -84,11 +84,24 @@ def test_onnx_export_graph(nconv_amd, monkeypatch):
 
 @pytest.mark.gpu
 def test_traced_on_device_matches_hip_forward(nconv_amd, gpu):
+    """The traced graph on device (the reference exports on cuda) against the reference's own f2
+    output and the HIP forward. PyTorch lets its GPU convolutions use reduced-precision (TF32-class)
+    products by default (torch.backends.cudnn.allow_tf32 = True), which through nine NConv layers
+    moves DNET outputs by up to a few percent — so the reference's op sequence is run here with
+    fp32 convolutions, as the fp32 claim needs; tolerance as the DNET parity tests."""
     net, f = _f2_net(nconv_amd)
     net = net.to(gpu)
     S = torch.from_numpy(np.array(f["S_64x96"])).to(gpu)
-    with torch.no_grad():
-        hip = net(S)
-        traced = torch.jit.trace(net, (S,), check_trace=False)
-        out = traced(S)
-    torch.testing.assert_close(out, hip, rtol=1e-4, atol=1e-5)
+    ref = torch.from_numpy(np.array(f["out_64x96"])).double()
+    tf32 = (torch.backends.cudnn.allow_tf32, torch.backends.cuda.matmul.allow_tf32)
+    try:
+        torch.backends.cudnn.allow_tf32 = torch.backends.cuda.matmul.allow_tf32 = False
+        with torch.no_grad():
+            hip = net(S)
+            traced = torch.jit.trace(net, (S,), check_trace=False)
+            out = traced(S)
+    finally:
+        torch.backends.cudnn.allow_tf32, torch.backends.cuda.matmul.allow_tf32 = tf32
+    for got in (out, hip):
+        err = (got.double().cpu() - ref).abs()
+        assert (err <= 1e-4 * ref.abs() + 1e-4).all(), err.max().item()
