@@ -947,15 +947,7 @@ struct WmGrid {
     int nstrip, nseg, seg_rows;
     size_t nblk;
 };
-static int device_cus() {
-    static int cus = 0;
-    if (cus == 0) {
-        int dev = 0, n = 256;
-        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-        cus = n > 0 ? n : 256;
-    }
-    return cus;
-}
+static int device_cus() { return dev_cus(); }
 static WmGrid wm_grid(const nconv_layer& L, int target = 0) {
     if (target <= 0) target = kMfmaRounds * kMfmaMaxPerCu * device_cus();  // workspace bound
     WmGrid g;
@@ -1012,14 +1004,8 @@ static void go_bwd_tiled(const LayerDev& d, const BwdArgs& a, float* part, float
             launch_wgrad_reduce(part, nblk, nw, COUT, CIN * K * K, L.wsum, a.gw, a.gb,
                                 part + (size_t)nblk * (nw + 2 * COUT), st);
         } else if (a.gw || a.gb) {
-            static int resident = 0;
-            if (resident == 0) {
-                int per_cu = 0;
-                if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, wgrad_mfma<CIN, COUT, K, MODE>, kT, 0) !=
-                        hipSuccess || per_cu <= 0)
-                    per_cu = 1;
-                resident = device_cus() * (per_cu < kMfmaMaxPerCu ? per_cu : kMfmaMaxPerCu);
-            }
+            const int per_cu = dev_occupancy((const void*)wgrad_mfma<CIN, COUT, K, MODE>, kT, 0);
+            const int resident = device_cus() * (per_cu < kMfmaMaxPerCu ? per_cu : kMfmaMaxPerCu);
             const WmGrid g = wm_grid(L, kMfmaRounds * resident);
             hipLaunchKernelGGL((wgrad_mfma<CIN, COUT, K, MODE>), dim3(g.nblk), dim3(kT), 0, st, d, a, part,
                                g.nstrip, g.nseg, g.seg_rows);
@@ -1038,15 +1024,7 @@ static void go_bwd_tiled(const LayerDev& d, const BwdArgs& a, float* part, float
         if (red > lds) lds = red;
         // blocks walk runs of tiles: launch at most the resident count (CUs x blocks per CU), so
         // there is no second, partial round (nconv1's 13.4 k tiles: 768 resident at 3 waves/SIMD)
-        static int resident = 0;
-        if (resident == 0) {
-            int dev = 0, cus = 256, per_cu = 0;
-            if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, wgrad_tiled<CIN, COUT, K, MODE>, kT, lds) !=
-                    hipSuccess || per_cu <= 0)
-                per_cu = 1;
-            resident = cus * per_cu;
-        }
+        const int resident = device_cus() * dev_occupancy((const void*)wgrad_tiled<CIN, COUT, K, MODE>, kT, lds);
         const int nblk = nblk_ws < resident ? nblk_ws : resident;
         hipLaunchKernelGGL((wgrad_tiled<CIN, COUT, K, MODE>), dim3(nblk), dim3(kT), lds, st, d, a, part, ntw, nth);
         const int nw = COUT * CIN * K * K;

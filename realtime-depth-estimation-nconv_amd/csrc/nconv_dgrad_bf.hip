@@ -281,16 +281,8 @@ template <int CIN, int COUT, int K, int MODE, int NP>
 static void go_dgrad_bf_np(const LayerDev& d, const BwdArgs& a, float* tmp_x, float* tmp_c, hipStream_t st) {
     using C = DbCfg<CIN, COUT, K, NP>;
     const nconv_layer& L = d.L;
-    static int per_cu = 0;
-    if (per_cu == 0) {
-        int n = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, dgrad_bf<CIN, COUT, K, MODE, NP>, kDbT, 0) != hipSuccess ||
-            n <= 0)
-            n = 1;
-        per_cu = n;
-    }
-    int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const int per_cu = dev_occupancy((const void*)dgrad_bf<CIN, COUT, K, MODE, NP>, kDbT, 0);
+    const int cus = dev_cus();
     const int target = per_cu * cus;
     const int nstrip = (L.W + C::SW - 1) / C::SW;
     const int per_img = nstrip * L.B;

@@ -943,12 +943,7 @@ __global__ __launch_bounds__(kMfThreads) __attribute__((amdgpu_waves_per_eu(mf_w
 // Persistent grid: resident workgroups per CU (by waves per SIMD and LDS) x CUs, a multiple of 8
 // (one XCD per blockIdx % 8).
 int mfma_grid_blocks(int waves, int lds_bytes) {
-    static int cus = 0;
-    if (cus == 0) {
-        int dev = 0, n = 256;
-        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-        cus = n;
-    }
+    const int cus = dev_cus();
     int per_cu = waves < (160 * 1024) / lds_bytes ? waves : (160 * 1024) / lds_bytes;
     if (const char* e = getenv("NCONV_MFMA_WG_PER_CU")) per_cu = atoi(e);
     return (cus * (per_cu > 0 ? per_cu : 1) + 7) / 8 * 8;

@@ -47,6 +47,11 @@ int launch_fwd_tail(const LayerDev& d, const TailArgs& t, float* out, hipStream_
 int launch_weight_prep(int n, float* const* w, const int* cout, const int* fan_in, const int* sp,
                        float* const* s, hipStream_t st, const char** why);
 
+// Grid sizing (nconv_occ.hip): CUs of the current device, resident workgroups per CU of a kernel
+// on it (>= 1); cached per device ordinal, thread-safe.
+int dev_cus();
+int dev_occupancy(const void* kernel, int threads, size_t dyn_lds);
+
 // Backward.
 size_t bwd_workspace_bytes(const LayerDev& d);
 // weight gradient on the bf16 matrix cores (nconv_wgrad_bf.hip): np = 2 (bf16x3) or 3 (bf16x9) split

@@ -338,16 +338,8 @@ template <int CIN, int COUT, int K, int MODE, int NP>
 static int go_wgrad_bf_np(const LayerDev& d, const BwdArgs& a, float* part, int max_blocks, hipStream_t st) {
     using C = WbCfg<CIN, COUT, K, NP>;
     const nconv_layer& L = d.L;
-    static int per_cu = 0;
-    if (per_cu == 0) {
-        int n = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, wgrad_bf<CIN, COUT, K, MODE, NP>, kWbT, 0) != hipSuccess ||
-            n <= 0)
-            n = 1;
-        per_cu = n;
-    }
-    int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const int per_cu = dev_occupancy((const void*)wgrad_bf<CIN, COUT, K, MODE, NP>, kWbT, 0);
+    const int cus = dev_cus();
     int target = per_cu * cus;
     if (target > max_blocks) target = max_blocks;
     const int nstrip = (L.Wo + C::OW - 1) / C::OW;
