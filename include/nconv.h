@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define NCONV_ABI_VERSION 13
+#define NCONV_ABI_VERSION 14
 
 /* How a layer's input (data x, confidence c) is produced from its source tensors. These are the
  * DNET glue ops fused into the layer's load stage (models/step1.py:53,61-90). */
@@ -36,16 +36,29 @@ enum nconv_load_mode {
     NCONV_LOAD_UPCAT_UP_FIRST = 4    /* x = cat(up(b.x), a.x), c likewise                   (step1.py:88-90)    */
 };
 
-/* Arithmetic of the NConv forward sums N = W*(x*c), D = W*c (nconv_layer.math). */
+/* Arithmetic of the NConv sums (nconv_layer.math: forward N = W*(x*c), D = W*c; nconv_layer.bwd_math:
+ * the backward's products). The zero value is the reference's arithmetic (F.conv2d in fp32,
+ * models/step1.py:119-122), so a zero-initialised descriptor computes exact fp32. */
 enum nconv_math {
-    NCONV_MATH_BF16X3 = 0, /* default: bf16 matrix cores on split operands, v = hi + lo, products
+    NCONV_MATH_FP32 = 0,   /* default: exact fp32 products (forward: packed FP32 FMA on the vector ALU;
+                              backward: fp32 matrix cores for the weight gradient, packed FP32 for the
+                              input gradient) */
+    NCONV_MATH_BF16X3 = 1, /* bf16 matrix cores on split operands, v = hi + lo, products
                               hi*hi + lo*hi + hi*lo in fp32 (<= ~1.1e-5 relative per product), for
                               the 8-output-channel 5x5 (8 in) / 3x3 (16 in) layers; others FP32 */
-    NCONV_MATH_FP32 = 1,   /* exact fp32 products on the vector ALU (packed FP32 FMA) */
     NCONV_MATH_BF16X9 = 2  /* exact products on the bf16 matrix cores: v = v0 + v1 + v2 and
                               w = w0 + w1 + w2 (three bf16 parts, an exact decomposition), all nine
                               partial products (each exact in fp32) accumulated in fp32, for the same
                               layers as BF16X3; others FP32 */
+};
+
+/* Kernel family a launch runs (nconv_plan). */
+enum nconv_kernel {
+    NCONV_KERNEL_GENERIC = 0,     /* direct one-thread-per-element kernels (any NConv2d geometry)       */
+    NCONV_KERNEL_TILED_FP32 = 1,  /* LDS-tiled, exact fp32 products on the vector ALU (packed FP32)     */
+    NCONV_KERNEL_MFMA_FP32 = 2,   /* fp32 matrix cores, exact fp32 products                            */
+    NCONV_KERNEL_MFMA_BF16X3 = 3, /* bf16 matrix cores, two-part split operands (NCONV_MATH_BF16X3)    */
+    NCONV_KERNEL_MFMA_BF16X9 = 4  /* bf16 matrix cores, three-part split, exact products (BF16X9)      */
 };
 
 /* One source tensor pair (data, confidence), physical shape (B, C, H, W). */
@@ -69,10 +82,11 @@ typedef struct nconv_layer {
     const float* weight; /* (Cout, Cin/groups, KH, KW), positive in practice                   */
     const float* bias;   /* (Cout)                                                              */
     const float* wsum;   /* (Cout): s[o] = sum of weight[o] (step1.py:141-144), see nconv_weight_prep */
-    int math;            /* enum nconv_math of the forward sums (0 = default; other values: -EINVAL) */
-    int bwd_math;        /* enum nconv_math of the weight gradient's products (nconv_bwd, 3x3 / 5x5
-                            layers with Cin > 1): NCONV_MATH_FP32 = fp32 matrix cores (exact
-                            products), BF16X3 / BF16X9 = split-bf16 matrix cores; -EINVAL otherwise */
+    int math;            /* enum nconv_math of the forward sums (0 = NCONV_MATH_FP32; unknown: -EINVAL) */
+    int bwd_math;        /* enum nconv_math of the backward's products (nconv_bwd, weight and input
+                            gradient of the 3x3 / 5x5 layers with Cin > 1): 0 = NCONV_MATH_FP32
+                            (exact products), BF16X3 / BF16X9 = split-bf16 matrix cores; unknown:
+                            -EINVAL */
 } nconv_layer;
 
 /* ABI version, for the Python loader's sanity check. */
@@ -121,6 +135,11 @@ int nconv_fwd_head(const nconv_layer* L1, const nconv_layer* L2, float* y, float
 int nconv_fwd_tail(const nconv_layer* L6, const float* w7, const float* b7, const float* wsum7,
                    int cin7, int p7, float eps7, float* out, float* out_c, int out_h, int out_w,
                    void* stream);
+
+/* Which kernels nconv_fwd (without fused pooling) and nconv_bwd run for L (enum nconv_kernel):
+ * the arithmetic a descriptor selects, made observable to hosts and tests. Host-only (no device
+ * work); any output pointer may be NULL. Returns 0 or -EINVAL for an invalid descriptor. */
+int nconv_plan(const nconv_layer* L, int* fwd_kernel, int* dgrad_kernel, int* wgrad_kernel);
 
 /* Workspace needed by nconv_bwd (bytes). */
 size_t nconv_bwd_workspace_bytes(const nconv_layer* L);

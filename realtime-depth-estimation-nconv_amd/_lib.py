@@ -13,13 +13,16 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # NCONV_LIB: an alternative build of the same library (kernel-tuning experiments)
 LIB_PATH = os.environ.get("NCONV_LIB") or os.path.join(_HERE, "libnconv.so")
-ABI_VERSION = 13
+ABI_VERSION = 14
 BWD_ACCUMULATE = 1
 
 # enum nconv_load_mode
 PLAIN, THRESH, POOL2, UPCAT_SKIP_FIRST, UPCAT_UP_FIRST = 0, 1, 2, 3, 4
 # enum nconv_math
-MATH_BF16X3, MATH_FP32, MATH_BF16X9 = 0, 1, 2
+MATH_FP32, MATH_BF16X3, MATH_BF16X9 = 0, 1, 2
+# enum nconv_kernel (nconv_plan)
+KERNEL_GENERIC, KERNEL_TILED_FP32, KERNEL_MFMA_FP32, KERNEL_MFMA_BF16X3, KERNEL_MFMA_BF16X9 = 0, 1, 2, 3, 4
+KERNEL_NAMES = ("generic", "tiled_fp32", "mfma_fp32", "mfma_bf16x3", "mfma_bf16x9")
 # enum nconv_dense_kind
 DENSE_3X3, DENSE_1X1, DENSE_TRANSPOSED_4X4, DENSE_CONV4X4_S2 = 0, 1, 2, 3
 
@@ -31,6 +34,7 @@ EXPORTED = (
     "nconv_fwd_pooled",
     "nconv_fwd_tail",
     "nconv_fwd_head",
+    "nconv_plan",
     "nconv_bwd_workspace_bytes",
     "nconv_bwd",
     "nconv_dense_packed_floats",
@@ -111,6 +115,8 @@ def _declare(lib):
     lib.nconv_fwd_tail.restype = ctypes.c_int
     lib.nconv_fwd_tail.argtypes = [ctypes.POINTER(NconvLayer), P, P, P, ctypes.c_int, ctypes.c_int,
                                    ctypes.c_float, P, P, ctypes.c_int, ctypes.c_int, P]
+    lib.nconv_plan.restype = ctypes.c_int
+    lib.nconv_plan.argtypes = [ctypes.POINTER(NconvLayer), P, P, P]
     lib.nconv_bwd_workspace_bytes.restype = ctypes.c_size_t
     lib.nconv_bwd_workspace_bytes.argtypes = [ctypes.POINTER(NconvLayer)]
     lib.nconv_bwd.restype = ctypes.c_int

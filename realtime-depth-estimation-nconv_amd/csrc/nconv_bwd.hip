@@ -980,9 +980,24 @@ size_t bwd_workspace_bytes(const LayerDev& d) {
     return bytes;
 }
 
+void plan_bwd(const nconv_layer& L, int* dgrad, int* wgrad) {
+    if (pick_path(L) == kGeneric) {
+        *dgrad = *wgrad = NCONV_KERNEL_GENERIC;
+        return;
+    }
+    const int bf = L.bwd_math == NCONV_MATH_BF16X9 ? NCONV_KERNEL_MFMA_BF16X9 : NCONV_KERNEL_MFMA_BF16X3;
+    const bool multi = L.KH > 1 && L.Cin > 1;  // 3x3 / 5x5 layers with several input channels
+    const bool fp32 = L.bwd_math == NCONV_MATH_FP32;
+    *dgrad = multi && !fp32 ? bf : NCONV_KERNEL_TILED_FP32;
+    *wgrad = multi ? (fp32 ? NCONV_KERNEL_MFMA_FP32 : bf) : NCONV_KERNEL_TILED_FP32;
+}
+
+// Returns 0, or -EIO when the bf16 weight-gradient grid would not fit the workspace (it cannot:
+// its strips are wider than wgrad_mfma's, for which the workspace is sized; checked anyway, so
+// a bf16 request never silently runs another kernel).
 template <int CIN, int COUT, int K, int MODE>
-static void go_bwd_tiled(const LayerDev& d, const BwdArgs& a, float* part, float* tx, float* tc,
-                         hipStream_t st) {
+static int go_bwd_tiled(const LayerDev& d, const BwdArgs& a, float* part, float* tx, float* tc,
+                        hipStream_t st) {
     const nconv_layer& L = d.L;
     using D = DgCfg<CIN, K>;
     if (a.gxa || a.gca || a.gxb || a.gcb) {
@@ -995,11 +1010,10 @@ static void go_bwd_tiled(const LayerDev& d, const BwdArgs& a, float* part, float
         }
     }
     if constexpr (K > 1 && CIN > 1) {
-        int nblk = -1;  // split-bf16 matrix cores (-1: the grid would not fit the workspace)
-        if ((a.gw || a.gb) && L.bwd_math != NCONV_MATH_FP32)
-            nblk = go_wgrad_bf<CIN, COUT, K, MODE>(d, a, part, (int)wm_grid(L).nblk,
-                                                   L.bwd_math == NCONV_MATH_BF16X9 ? 3 : 2, st);
-        if (nblk >= 0) {
+        if ((a.gw || a.gb) && L.bwd_math != NCONV_MATH_FP32) {  // split-bf16 matrix cores
+            const int nblk = go_wgrad_bf<CIN, COUT, K, MODE>(d, a, part, (int)wm_grid(L).nblk,
+                                                             L.bwd_math == NCONV_MATH_BF16X9 ? 3 : 2, st);
+            if (nblk < 0) return -5;
             const int nw = COUT * CIN * K * K;
             launch_wgrad_reduce(part, nblk, nw, COUT, CIN * K * K, L.wsum, a.gw, a.gb,
                                 part + (size_t)nblk * (nw + 2 * COUT), st);
@@ -1031,6 +1045,7 @@ static void go_bwd_tiled(const LayerDev& d, const BwdArgs& a, float* part, float
         launch_wgrad_reduce(part, nblk, nw, COUT, CIN * K * K, L.wsum, a.gw, a.gb,
                             part + (size_t)nblk * (nw + 2 * COUT), st);
     }
+    return 0;
 }
 
 template <int MODE>
@@ -1071,12 +1086,17 @@ int launch_bwd(const LayerDev& d, const BwdArgs& a, hipStream_t st, const char**
 
     if (path == kTiled) {
         const int m = L.load_mode;
-        if (L.Cin == 1 && m == NCONV_LOAD_THRESH) go_bwd_tiled<1, 8, 5, NCONV_LOAD_THRESH>(d, a, part, tx, tc, st);
-        else if (L.Cin == 8 && L.Cout == 8 && m == NCONV_LOAD_PLAIN) go_bwd_tiled<8, 8, 5, NCONV_LOAD_PLAIN>(d, a, part, tx, tc, st);
-        else if (L.Cin == 8 && L.Cout == 8 && m == NCONV_LOAD_POOL2) go_bwd_tiled<8, 8, 5, NCONV_LOAD_POOL2>(d, a, part, tx, tc, st);
-        else if (m == NCONV_LOAD_UPCAT_SKIP_FIRST) go_bwd_tiled<16, 8, 3, NCONV_LOAD_UPCAT_SKIP_FIRST>(d, a, part, tx, tc, st);
-        else if (m == NCONV_LOAD_UPCAT_UP_FIRST) go_bwd_tiled<16, 8, 3, NCONV_LOAD_UPCAT_UP_FIRST>(d, a, part, tx, tc, st);
-        else go_bwd_tiled<8, 1, 1, NCONV_LOAD_PLAIN>(d, a, part, tx, tc, st);
+        int rc;
+        if (L.Cin == 1 && m == NCONV_LOAD_THRESH) rc = go_bwd_tiled<1, 8, 5, NCONV_LOAD_THRESH>(d, a, part, tx, tc, st);
+        else if (L.Cin == 8 && L.Cout == 8 && m == NCONV_LOAD_PLAIN) rc = go_bwd_tiled<8, 8, 5, NCONV_LOAD_PLAIN>(d, a, part, tx, tc, st);
+        else if (L.Cin == 8 && L.Cout == 8 && m == NCONV_LOAD_POOL2) rc = go_bwd_tiled<8, 8, 5, NCONV_LOAD_POOL2>(d, a, part, tx, tc, st);
+        else if (m == NCONV_LOAD_UPCAT_SKIP_FIRST) rc = go_bwd_tiled<16, 8, 3, NCONV_LOAD_UPCAT_SKIP_FIRST>(d, a, part, tx, tc, st);
+        else if (m == NCONV_LOAD_UPCAT_UP_FIRST) rc = go_bwd_tiled<16, 8, 3, NCONV_LOAD_UPCAT_UP_FIRST>(d, a, part, tx, tc, st);
+        else rc = go_bwd_tiled<8, 1, 1, NCONV_LOAD_PLAIN>(d, a, part, tx, tc, st);
+        if (rc) {
+            *why = "bf16 weight-gradient grid exceeds the workspace";
+            return rc;
+        }
     } else {
         switch (L.load_mode) {
             case NCONV_LOAD_PLAIN: go_bwd_generic<NCONV_LOAD_PLAIN>(d, a, part, tx, tc, st); break;

@@ -26,9 +26,10 @@ const char* validate(const nconv_layer* L, bool need_c) {
     if (ho != L->Ho || wo != L->Wo) return "Ho/Wo inconsistent with H/W/kernel/stride/padding/dilation";
     if (!L->weight || !L->bias || !L->wsum) return "null weight/bias/wsum";
     if (!L->a.x) return "null source a.x";
-    if (L->bwd_math != NCONV_MATH_BF16X3 && L->bwd_math != NCONV_MATH_FP32 && L->bwd_math != NCONV_MATH_BF16X9)
+    if (L->bwd_math != NCONV_MATH_FP32 && L->bwd_math != NCONV_MATH_BF16X3 && L->bwd_math != NCONV_MATH_BF16X9)
         return "unknown bwd_math (enum nconv_math)";
-    if (L->math != NCONV_MATH_BF16X3 && L->math != NCONV_MATH_FP32 && L->math != NCONV_MATH_BF16X9) return "unknown math (enum nconv_math)";
+    if (L->math != NCONV_MATH_FP32 && L->math != NCONV_MATH_BF16X3 && L->math != NCONV_MATH_BF16X9)
+        return "unknown math (enum nconv_math)";
     switch (L->load_mode) {
         case NCONV_LOAD_PLAIN:
             if (!L->a.c && need_c) return "null source a.c";
@@ -185,6 +186,16 @@ int nconv_fwd_tail(const nconv_layer* L6, const float* w7, const float* b7, cons
     const char* why = nullptr;
     int rc = nconv::launch_fwd_tail(make_dev(L6), t, out, (hipStream_t)stream, &why);
     return rc ? fail(rc, "nconv_fwd_tail", why) : 0;
+}
+
+int nconv_plan(const nconv_layer* L, int* fwd_kernel, int* dgrad_kernel, int* wgrad_kernel) {
+    if (const char* why = validate(L, false)) return fail(-22, "nconv_plan", why);
+    int dg, wg;
+    nconv::plan_bwd(*L, &dg, &wg);
+    if (fwd_kernel) *fwd_kernel = nconv::plan_fwd(*L);
+    if (dgrad_kernel) *dgrad_kernel = dg;
+    if (wgrad_kernel) *wgrad_kernel = wg;
+    return 0;
 }
 
 size_t nconv_bwd_workspace_bytes(const nconv_layer* L) {

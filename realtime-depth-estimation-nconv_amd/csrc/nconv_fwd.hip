@@ -363,17 +363,12 @@ static void go_tiled_cs(const LayerDev& d, float* y, float* yc, const TailArgs& 
 // resolution layers); the small quarter / eighth-resolution layers would leave most SIMDs with no
 // wave at all, so their waves split the output channels (2 or 4 slices, on 8- or 4-row tiles;
 // a slice is whole waves, so its weights stay wave-uniform) and the layer spreads over the whole
-// chip. NCONV_TILED_CS forces a slice count.
+// chip.
 static int tiled_cs(long tiles16, int cout, int mode) {
-    static const int forced = [] {
-        const char* e = getenv("NCONV_TILED_CS");
-        return e ? atoi(e) : 0;
-    }();
     // (the max-pooling loads of the down layers gain from the shorter pipeline already at half
     // resolution: down1 66 vs 72 us at B=8 352x1216; nconv5 does not, 56 vs 53 us)
     const long big = mode == NCONV_LOAD_POOL2 ? 2048 : 1024;
-    int cs = forced ? forced : tiles16 >= big ? 1 : tiles16 >= 512 ? 2 : 4;
-    if (cs > 4) cs = 4;
+    int cs = tiles16 >= big ? 1 : tiles16 >= 512 ? 2 : 4;
     while (cs > 1 && cout % cs) cs >>= 1;
     return cs;
 }
@@ -387,6 +382,22 @@ static void go_tiled(const LayerDev& d, float* y, float* yc, const TailArgs& t, 
         if (cs == 2) return go_tiled_cs<CIN, COUT, K, MODE, TAIL, 2>(d, y, yc, t, gh, gw, st);
     }
     go_tiled_cs<CIN, COUT, K, MODE, TAIL, 1>(d, y, yc, t, gh, gw, st);
+}
+
+static bool fwd_tiled_shape(const nconv_layer& L) {
+    const int m = L.load_mode;
+    return simple_geometry(L) &&
+           ((L.Cin == 1 && L.Cout == 8 && L.KH == 5 && m == NCONV_LOAD_THRESH) ||
+            (L.Cin == 8 && L.Cout == 8 && L.KH == 5 && (m == NCONV_LOAD_PLAIN || m == NCONV_LOAD_POOL2)) ||
+            (L.Cin == 16 && L.Cout == 8 && L.KH == 3 &&
+             (m == NCONV_LOAD_UPCAT_SKIP_FIRST || m == NCONV_LOAD_UPCAT_UP_FIRST)) ||
+            (L.Cin == 8 && L.Cout == 1 && L.KH == 1 && m == NCONV_LOAD_PLAIN));
+}
+
+int plan_fwd(const nconv_layer& L) {
+    if (fwd_mfma_supported(L, false, false))
+        return L.math == NCONV_MATH_BF16X9 ? NCONV_KERNEL_MFMA_BF16X9 : NCONV_KERNEL_MFMA_BF16X3;
+    return fwd_tiled_shape(L) ? NCONV_KERNEL_TILED_FP32 : NCONV_KERNEL_GENERIC;
 }
 
 int launch_fwd(const LayerDev& d, float* y, float* yc, float* py, float* pc, hipStream_t st, const char** why) {

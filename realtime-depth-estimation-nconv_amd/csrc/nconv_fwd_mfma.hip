@@ -945,7 +945,6 @@ __global__ __launch_bounds__(kMfThreads) __attribute__((amdgpu_waves_per_eu(mf_w
 int mfma_grid_blocks(int waves, int lds_bytes) {
     const int cus = dev_cus();
     int per_cu = waves < (160 * 1024) / lds_bytes ? waves : (160 * 1024) / lds_bytes;
-    if (const char* e = getenv("NCONV_MFMA_WG_PER_CU")) per_cu = atoi(e);
     return (cus * (per_cu > 0 ? per_cu : 1) + 7) / 8 * 8;
 }
 
@@ -1021,19 +1020,29 @@ int launch_fwd_head(const LayerDev& d2, const TailArgs& t, float* y, float* yc, 
     return 0;
 }
 
-// Returns true (and launches) when the layer has a matrix-core kernel: 8 output channels,
-// 8 input channels with a 5x5 kernel or 16 with a 3x3, stride 1, no dilation / groups.
-bool launch_fwd_mfma(const LayerDev& d, float* y, float* yc, const TailArgs& t, bool tail, hipStream_t st) {
-    const nconv_layer& L = d.L;
-    if ((L.math != NCONV_MATH_BF16X3 && L.math != NCONV_MATH_BF16X9) || L.Cout != 8 || L.KH != L.KW || L.SH != 1 || L.SW != 1 || L.DH != 1 ||
-        L.DW != 1 || L.groups != 1)
+// True when the layer has a matrix-core kernel: matrix-core math, 8 output channels, 8 input
+// channels with a 5x5 kernel or 16 with a 3x3, stride 1, no dilation / groups (the dispatch of
+// launch_fwd_mfma below; nconv_plan reports it).
+bool fwd_mfma_supported(const nconv_layer& L, bool tail, bool pool) {
+    if ((L.math != NCONV_MATH_BF16X3 && L.math != NCONV_MATH_BF16X9) || L.Cout != 8 || L.KH != L.KW || L.SH != 1 ||
+        L.SW != 1 || L.DH != 1 || L.DW != 1 || L.groups != 1)
         return false;
     // MfStage addresses one image's channels of a source through one buffer resource
     auto image_fits = [](const nconv_src& s) { return (long long)s.C * s.H * s.W * 4 < (1LL << 31); };
-    if (!image_fits(L.a) || ((L.load_mode == NCONV_LOAD_UPCAT_SKIP_FIRST || L.load_mode == NCONV_LOAD_UPCAT_UP_FIRST) &&
-                             !image_fits(L.b)))
-        return false;
+    const bool up = L.load_mode == NCONV_LOAD_UPCAT_SKIP_FIRST || L.load_mode == NCONV_LOAD_UPCAT_UP_FIRST;
+    if (!image_fits(L.a) || (up && !image_fits(L.b))) return false;
+    if (L.Cin == 8 && L.KH == 5 && L.load_mode == NCONV_LOAD_PLAIN) return !tail;
+    if (L.Cin == 8 && L.KH == 5 && L.load_mode == NCONV_LOAD_POOL2) return !tail && !pool;
+    if (L.Cin == 16 && L.KH == 3 && !pool)
+        return (L.load_mode == NCONV_LOAD_UPCAT_SKIP_FIRST && !tail) || L.load_mode == NCONV_LOAD_UPCAT_UP_FIRST;
+    return false;
+}
+
+// Returns true (and launches) when fwd_mfma_supported.
+bool launch_fwd_mfma(const LayerDev& d, float* y, float* yc, const TailArgs& t, bool tail, hipStream_t st) {
+    const nconv_layer& L = d.L;
     const bool pool = !tail && t.py != nullptr;
+    if (!fwd_mfma_supported(L, tail, pool)) return false;
     const int gh = tail ? t.out_h : L.Ho, gw = tail ? t.out_w : L.Wo;
     if (L.Cin == 8 && L.KH == 5 && L.load_mode == NCONV_LOAD_PLAIN && !tail) {
         if (pool)
@@ -1061,7 +1070,7 @@ bool launch_fwd_mfma(const LayerDev& d, float* y, float* yc, const TailArgs& t, 
             return true;
         }
     }
-    return false;
+    return false;  // (unreachable: fwd_mfma_supported)
 }
 
 }  // namespace nconv

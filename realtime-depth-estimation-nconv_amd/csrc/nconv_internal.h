@@ -41,7 +41,11 @@ struct BwdArgs {
 
 // Forward. Return 0, or a negative errno with *why set.
 int launch_fwd(const LayerDev& d, float* y, float* yc, float* py, float* pc, hipStream_t st, const char** why);
+bool fwd_mfma_supported(const nconv_layer& L, bool tail, bool pool);
 bool launch_fwd_mfma(const LayerDev& d, float* y, float* yc, const TailArgs& t, bool tail, hipStream_t st);
+// enum nconv_kernel of the forward / input-gradient / weight-gradient launches (nconv_plan)
+int plan_fwd(const nconv_layer& L);
+void plan_bwd(const nconv_layer& L, int* dgrad, int* wgrad);
 int launch_fwd_head(const LayerDev& d2, const TailArgs& t, float* y, float* yc, hipStream_t st, const char** why);
 int launch_fwd_tail(const LayerDev& d, const TailArgs& t, float* out, hipStream_t st, const char** why);
 int launch_weight_prep(int n, float* const* w, const int* cout, const int* fan_in, const int* sp,

@@ -202,6 +202,17 @@ def layer_backward(spec: LayerSpec, inputs, y, co, gy, gco, gin, gw, gb, accumul
     _lib.check(rc, "nconv_bwd")
 
 
+def kernel_plan(spec: LayerSpec, xa, ca, xb, cb, weight, bias, wsum):
+    """nconv_plan: the kernel families (forward, input gradient, weight gradient) that nconv_fwd /
+    nconv_bwd run for this layer under the current FORWARD_MATH / BACKWARD_MATH, by name
+    (_lib.KERNEL_NAMES). Host-only: no device work."""
+    L = spec.descriptor(xa, ca, xb, cb, weight, bias, wsum)
+    out = [_lib.ctypes.c_int(-1) for _ in range(3)]
+    rc = _lib.lib().nconv_plan(_lib.ctypes.byref(L), *[_lib.ctypes.byref(v) for v in out])
+    _lib.check(rc, "nconv_plan")
+    return tuple(_lib.KERNEL_NAMES[v.value] for v in out)
+
+
 def nconv_layer(spec: LayerSpec, xa, ca, xb, cb, weight, bias, wsum):
     """Differentiable fused layer. Inputs must be contiguous fp32 device tensors."""
     return NConvLayerFn.apply(spec, xa, ca, xb, cb, weight, bias, wsum)

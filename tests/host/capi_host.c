@@ -60,6 +60,12 @@ int main(void) {
     rc = nconv_fwd(&bad, out, out, NULL);
     printf("\"rc_bad_mode\": [%d, \"%s\"],\n", rc, nconv_last_error());
     printf("\"bwd_ws_ok\": [%zu, 0],\n", nconv_bwd_workspace_bytes(&L));
+    /* a descriptor whose math fields are left at zero computes exact fp32 (the reference's) */
+    nconv_layer z = L;
+    z.math = 0; z.bwd_math = 0;
+    int kf = -1, kd = -1, kw = -1;
+    rc = nconv_plan(&z, &kf, &kd, &kw);
+    printf("\"plan_zero\": [%d, %d, %d, %d, %d],\n", rc, z.math == NCONV_MATH_FP32, kf, kd, kw);
     printf("\"abi\": [%d, %d]\n}\n", nconv_abi_version(), NCONV_ABI_VERSION);
     return 0;
 }

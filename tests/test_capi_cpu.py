@@ -199,3 +199,40 @@ def test_fwd_rejects_unknown_math(nconv_amd):
         L = _layer(nconv_amd, math=m)
         assert lib.nconv_fwd(ctypes.byref(L), ctypes.c_void_p(0x2000), ctypes.c_void_p(0x3000), None) == -22
         assert "unknown math" in lib.nconv_last_error().decode()
+
+
+def _plan(nconv_amd, L):
+    lib = nconv_amd._lib.lib()
+    f, d, w = ctypes.c_int(-1), ctypes.c_int(-1), ctypes.c_int(-1)
+    rc = lib.nconv_plan(ctypes.byref(L), ctypes.byref(f), ctypes.byref(d), ctypes.byref(w))
+    assert rc == 0, lib.nconv_last_error().decode()
+    return tuple(nconv_amd._lib.KERNEL_NAMES[v.value] for v in (f, d, w))
+
+
+def test_zero_math_is_exact_fp32(nconv_amd):
+    """A descriptor whose math / bwd_math are left zero (ctypes zero-initialises, as `= {0}` in C)
+    runs the reference's arithmetic: exact fp32 products forward and backward (include/nconv.h
+    enum nconv_math; the reference's F.conv2d in fp32, models/step1.py:119-122)."""
+    L = _layer(nconv_amd)
+    assert (L.math, L.bwd_math) == (0, 0) == (nconv_amd._lib.MATH_FP32,) * 2
+    assert _plan(nconv_amd, L) == ("tiled_fp32", "tiled_fp32", "mfma_fp32")
+
+
+@pytest.mark.parametrize("math,expect", [
+    ("fp32", ("tiled_fp32", "tiled_fp32", "mfma_fp32")),
+    ("bf16x3", ("mfma_bf16x3", "mfma_bf16x3", "mfma_bf16x3")),
+    ("bf16x9", ("mfma_bf16x9", "mfma_bf16x9", "mfma_bf16x9")),
+])
+def test_plan_follows_requested_math(nconv_amd, math, expect):
+    """nconv_plan names the kernels a math selects, so a bf16 request can never silently run
+    another arithmetic (tests/test_gpu_layers.py asserts the plan next to each parity check)."""
+    m = nconv_amd.nconv._MATH_NAMES[math]
+    assert _plan(nconv_amd, _layer(nconv_amd, math=m, bwd_math=m)) == expect
+    # nconv1 (1 input channel) and the 1x1 nconv7 stay on the exact VALU / tiled kernels
+    L1 = _layer(nconv_amd, Cin=1, load_mode=nconv_amd._lib.THRESH, math=m, bwd_math=m)
+    L1.a.C = 1
+    assert _plan(nconv_amd, L1) == ("tiled_fp32",) * 3
+    L7 = _layer(nconv_amd, Cout=1, KH=1, KW=1, PH=0, PW=0, math=m, bwd_math=m)
+    assert _plan(nconv_amd, L7) == ("tiled_fp32",) * 3
+    # other geometries: the generic kernels whatever the math
+    assert _plan(nconv_amd, _layer(nconv_amd, SH=2, SW=2, Ho=8, Wo=8, math=m, bwd_math=m)) == ("generic",) * 3

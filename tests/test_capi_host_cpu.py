@@ -58,6 +58,8 @@ def test_host_validation_and_abi(host_report):
         rc, err = host_report[key]
         assert rc == -22 and msg in err, (key, rc, err)
     assert host_report["bwd_ws_ok"][0] > 0
+    # zero-initialised math: NCONV_MATH_FP32, VALU forward / input gradient, fp32-MFMA weight gradient
+    assert host_report["plan_zero"] == [0, 1, 1, 1, 2]
 
 
 def test_integration_doc_binding_matches_ctypes(nconv_amd):

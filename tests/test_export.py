@@ -84,24 +84,22 @@ def test_onnx_export_graph(nconv_amd, monkeypatch):
 
 @pytest.mark.gpu
 def test_traced_on_device_matches_hip_forward(nconv_amd, gpu):
-    """The traced graph on device (the reference exports on cuda) against the reference's own f2
-    output and the HIP forward. PyTorch lets its GPU convolutions use reduced-precision (TF32-class)
-    products by default (torch.backends.cudnn.allow_tf32 = True), which through nine NConv layers
-    moves DNET outputs by up to a few percent — so the reference's op sequence is run here with
-    fp32 convolutions, as the fp32 claim needs; tolerance as the DNET parity tests."""
+    """The traced graph on device (the reference exports on cuda, export_to_onnx.py:36-38) against
+    the reference's own f2 output and the HIP forward. MIOpen's default fp32 solver for these
+    shapes is Winograd (ConvBinWinogradRxSf2x3g1, tools/export_probe.py), whose error is relative
+    to a tile's largest term: windows with no depth sample get D, N ~ 1e-5 instead of 0, and the
+    divide by D + 1e-7 moves DNET outputs by up to 2.4 %. export.exact_convolutions() runs the
+    graph on torch's native fp32 convolution instead; tolerance as the DNET parity tests."""
     net, f = _f2_net(nconv_amd)
     net = net.to(gpu)
     S = torch.from_numpy(np.array(f["S_64x96"])).to(gpu)
     ref = torch.from_numpy(np.array(f["out_64x96"])).double()
-    tf32 = (torch.backends.cudnn.allow_tf32, torch.backends.cuda.matmul.allow_tf32)
-    try:
-        torch.backends.cudnn.allow_tf32 = torch.backends.cuda.matmul.allow_tf32 = False
-        with torch.no_grad():
-            hip = net(S)
+    with torch.no_grad():
+        hip = net(S)
+        with nconv_amd.export.exact_convolutions():
             traced = torch.jit.trace(net, (S,), check_trace=False)
             out = traced(S)
-    finally:
-        torch.backends.cudnn.allow_tf32, torch.backends.cuda.matmul.allow_tf32 = tf32
+    assert torch.backends.cudnn.enabled  # restored
     for got in (out, hip):
         err = (got.double().cpu() - ref).abs()
         assert (err <= 1e-4 * ref.abs() + 1e-4).all(), err.max().item()

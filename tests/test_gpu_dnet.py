@@ -113,7 +113,7 @@ def test_enforcepos_drift(nconv_amd, gpu):
 
 @pytest.fixture(params=["fp32", "bf16x3"])
 def bwd_math(request, nconv_amd, monkeypatch):
-    monkeypatch.setattr(nconv_amd.nconv, "BACKWARD_MATH", {"bf16x3": 0, "fp32": 1, "bf16x9": 2}[request.param])
+    monkeypatch.setattr(nconv_amd.nconv, "BACKWARD_MATH", nconv_amd.nconv._MATH_NAMES[request.param])
     return request.param
 
 
@@ -195,7 +195,7 @@ def _oracle_out(net, S, crop):
 
 @pytest.fixture(params=["fp32", "bf16x9", "bf16x3"])
 def fwd_math(request, nconv_amd, monkeypatch):
-    monkeypatch.setattr(nconv_amd.nconv, "FORWARD_MATH", {"bf16x3": 0, "fp32": 1, "bf16x9": 2}[request.param])
+    monkeypatch.setattr(nconv_amd.nconv, "FORWARD_MATH", nconv_amd.nconv._MATH_NAMES[request.param])
     return request.param
 
 

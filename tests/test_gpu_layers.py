@@ -51,7 +51,7 @@ def _wsum(nconv_amd, w):
 @pytest.fixture(params=["bf16x3", "bf16x9", "fp32"])
 def fwd_math(request, nconv_amd, monkeypatch):
     """Every forward arithmetic (include/nconv.h enum nconv_math)."""
-    monkeypatch.setattr(nconv_amd.nconv, "FORWARD_MATH", {"bf16x3": 0, "fp32": 1, "bf16x9": 2}[request.param])
+    monkeypatch.setattr(nconv_amd.nconv, "FORWARD_MATH", nconv_amd.nconv._MATH_NAMES[request.param])
     return request.param
 
 
@@ -78,7 +78,7 @@ def test_layer_forward(nconv_amd, gpu, case, fwd_math):
 @pytest.fixture(params=["bf16x3", "bf16x9", "fp32"])
 def bwd_math(request, nconv_amd, monkeypatch):
     """Every backward arithmetic (include/nconv.h nconv_layer.bwd_math: weight and input gradient)."""
-    monkeypatch.setattr(nconv_amd.nconv, "BACKWARD_MATH", {"bf16x3": 0, "fp32": 1, "bf16x9": 2}[request.param])
+    monkeypatch.setattr(nconv_amd.nconv, "BACKWARD_MATH", nconv_amd.nconv._MATH_NAMES[request.param])
     return request.param
 
 
@@ -94,7 +94,14 @@ def test_layer_backward(nconv_amd, gpu, case, bwd_math):
     (ry * gy + rc * gc).sum().backward()
 
     gl = [_gpu(t, gpu, grad=True) for t in (xa, ca, xb, cb, w, b)]
-    y, c = nconv_amd.nconv_layer(_spec(nconv_amd, case), *gl[:4], gl[4], gl[5], _wsum(nconv_amd, gl[4]))
+    wsum = _wsum(nconv_amd, gl[4])
+    # the kernels that ran (nconv_plan): a bf16 request on a multi-channel 3x3 / 5x5 layer must run
+    # the bf16 matrix-core kernels, never a silent fallback to another arithmetic
+    _, dg_k, wg_k = nconv_amd.nconv.kernel_plan(_spec(nconv_amd, case), *gl[:4], gl[4], gl[5], wsum)
+    if wg_k != "generic" and cin > 1 and k > 1:
+        want = ("tiled_fp32", "mfma_fp32") if bwd_math == "fp32" else ("mfma_" + bwd_math,) * 2
+        assert (dg_k, wg_k) == want, (name, bwd_math, dg_k, wg_k)
+    y, c = nconv_amd.nconv_layer(_spec(nconv_amd, case), *gl[:4], gl[4], gl[5], wsum)
     (y * gy.to(gpu, torch.float32) + c * gc.to(gpu, torch.float32)).sum().backward()
     torch.cuda.synchronize()
     labels = ("g_xa", "g_ca", "g_xb", "g_cb", "g_w", "g_b")
