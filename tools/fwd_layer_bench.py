@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """One NConv layer forward, repeated (developer tool for rocprofv3 / counter passes, GPU):
-python3 tools/fwd_layer_bench.py [nconv2|head|tail|down1|down2|down3|nconv4|nconv5] [reps] -> us per launch."""
+python3 tools/fwd_layer_bench.py [nconv1|nconv2|head|tail|down1|down2|down3|nconv4|nconv5] [reps] -> us per launch."""
 import os
 import sys
 
@@ -29,6 +29,12 @@ def main():
         x, c = r(B, 8, H, W) * 10, r(B, 8, H, W)
         spec = m.LayerSpec(8, 8, (5, 5), (1, 1), (2, 2))
         fn = lambda: N.layer_forward_pooled(spec, x, c, None, None, w8, b, s8)
+    elif which == "nconv1":  # exact-fp32 nconv1 on the thresholded sparse depth
+        S = (r(B, 1, H, W) * 79 + 1) * (r(B, 1, H, W) < 0.05)
+        w1 = r(8, 1, 5, 5) + 0.05
+        s1 = w1.sum((1, 2, 3)).contiguous()
+        spec = m.LayerSpec(1, 8, (5, 5), (1, 1), (2, 2), mode=m._lib.THRESH)
+        fn = lambda: N.layer_forward_raw(spec, S, None, None, None, w1, b, s1)
     elif which == "head":  # nconv1 inside nconv2 (nconv_fwd_head)
         S = (r(B, 1, H, W) * 79 + 1) * (r(B, 1, H, W) < 0.05)
         w1 = r(8, 1, 5, 5) + 0.05
