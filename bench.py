@@ -135,6 +135,8 @@ def inference_calls(m, net, S):
     H, W = S.shape[2], S.shape[3]
     oh, ow = m.crop_hw(H, W, d.crop)
     head = d._use_head(l1, l2)
+    wph = d._phase_weights(S.device)
+    w4, w5, w6 = (None, None, None) if wph is None else tuple(wph)
     with torch.no_grad():
         if head:
             x1b, c1b, p1, q1 = fhead(l1.spec(lib.THRESH, 0.01), l2.spec(), S, l1.weight, l1.bias, s1, l2.weight,
@@ -145,8 +147,8 @@ def inference_calls(m, net, S):
         x2, c2, p2, q2 = fpool(d1.spec(), p1, q1, None, None, d1.weight, d1.bias, sd1)
         x3, c3, p3, q3 = fpool(d2.spec(), p2, q2, None, None, d2.weight, d2.bias, sd2)
         x4, c4 = fwd(d3.spec(), p3, q3, None, None, d3.weight, d3.bias, sd3)
-        x34, c34 = fwd(l4.spec(lib.UPCAT_SKIP_FIRST), x3, c3, x4, c4, l4.weight, l4.bias, s4)
-        x23, c23 = fwd(l5.spec(lib.UPCAT_SKIP_FIRST), x2, c2, x34, c34, l5.weight, l5.bias, s5)
+        x34, c34 = fwd(l4.spec(lib.UPCAT_SKIP_FIRST), x3, c3, x4, c4, l4.weight, l4.bias, s4, wphase=w4)
+        x23, c23 = fwd(l5.spec(lib.UPCAT_SKIP_FIRST), x2, c2, x34, c34, l5.weight, l5.bias, s5, wphase=w5)
     tail_out = torch.empty((S.shape[0], 1, oh, ow), device=S.device, dtype=torch.float32)
     first = {"nconv1+nconv2_head": lambda: fhead(l1.spec(lib.THRESH, 0.01), l2.spec(), S, l1.weight, l1.bias, s1,
                                                  l2.weight, l2.bias, s2)} if head else {
@@ -157,9 +159,9 @@ def inference_calls(m, net, S):
         "nconv_down1": lambda: fpool(d1.spec(), p1, q1, None, None, d1.weight, d1.bias, sd1),
         "nconv_down2": lambda: fpool(d2.spec(), p2, q2, None, None, d2.weight, d2.bias, sd2),
         "nconv_down3": lambda: fwd(d3.spec(), p3, q3, None, None, d3.weight, d3.bias, sd3),
-        "nconv4": lambda: fwd(l4.spec(lib.UPCAT_SKIP_FIRST), x3, c3, x4, c4, l4.weight, l4.bias, s4),
-        "nconv5": lambda: fwd(l5.spec(lib.UPCAT_SKIP_FIRST), x2, c2, x34, c34, l5.weight, l5.bias, s5),
-        "nconv6+7_tail": lambda: d._fused_tail(l6, l7, s6, s7, x1b, c1b, x23, c23, tail_out),
+        "nconv4": lambda: fwd(l4.spec(lib.UPCAT_SKIP_FIRST), x3, c3, x4, c4, l4.weight, l4.bias, s4, wphase=w4),
+        "nconv5": lambda: fwd(l5.spec(lib.UPCAT_SKIP_FIRST), x2, c2, x34, c34, l5.weight, l5.bias, s5, wphase=w5),
+        "nconv6+7_tail": lambda: d._fused_tail(l6, l7, s6, s7, x1b, c1b, x23, c23, tail_out, w6),
     }
 
 

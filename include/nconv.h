@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define NCONV_ABI_VERSION 14
+#define NCONV_ABI_VERSION 15
 
 /* How a layer's input (data x, confidence c) is produced from its source tensors. These are the
  * DNET glue ops fused into the layer's load stage (models/step1.py:53,61-90). */
@@ -58,7 +58,10 @@ enum nconv_kernel {
     NCONV_KERNEL_TILED_FP32 = 1,  /* LDS-tiled, exact fp32 products on the vector ALU (packed FP32)     */
     NCONV_KERNEL_MFMA_FP32 = 2,   /* fp32 matrix cores, exact fp32 products                            */
     NCONV_KERNEL_MFMA_BF16X3 = 3, /* bf16 matrix cores, two-part split operands (NCONV_MATH_BF16X3)    */
-    NCONV_KERNEL_MFMA_BF16X9 = 4  /* bf16 matrix cores, three-part split, exact products (BF16X9)      */
+    NCONV_KERNEL_MFMA_BF16X9 = 4, /* bf16 matrix cores, three-part split, exact products (BF16X9)      */
+    NCONV_KERNEL_TILED_FP32_PHASE = 5 /* as TILED_FP32, the nearest-2x-upsampled half of the input
+                                     channels convolved at native resolution with phase weights
+                                     (nconv_layer.wphase, nconv_phase_weights)                     */
 };
 
 /* One source tensor pair (data, confidence), physical shape (B, C, H, W). */
@@ -87,6 +90,13 @@ typedef struct nconv_layer {
                             gradient of the 3x3 / 5x5 layers with Cin > 1): 0 = NCONV_MATH_FP32
                             (exact products), BF16X3 / BF16X9 = split-bf16 matrix cores; unknown:
                             -EINVAL */
+    const float* wphase; /* optional (NULL = unused): phase weights of an UPCAT layer's upsampled
+                            channels, written by nconv_phase_weights. With exact-fp32 math, 16 -> 8
+                            channels (8 + 8), 3x3, stride 1 and an exact nearest 2x upsampling
+                            (H = 2 b.H, W = 2 b.W) the forward then convolves source b at its own
+                            resolution: 4 fp32 taps of summed weights instead of 9 per pixel (the
+                            regrouping (w1 + w2) * v of w1 * v + w2 * v, fp32 throughout); ignored
+                            otherwise */
 } nconv_layer;
 
 /* ABI version, for the Python loader's sanity check. */
@@ -102,6 +112,18 @@ const char* nconv_last_error(void);
  * weights[i] has counts[i] = Cout_i * fan_in_i floats; wsums[i] receives Cout_i floats. */
 int nconv_weight_prep(int n, float* const* weights, const int* couts, const int* fan_ins,
                       const int* apply_softplus, float* const* wsums, void* stream);
+
+/* Phase weights (nconv_layer.wphase) of n UPCAT layers with 8 output channels, 3x3 kernels and 8
+ * nearest-2x-upsampled input channels, one launch; call after nconv_weight_prep (they are sums of
+ * the current weights: 1, 2 or 4 fp32 weights each, in a fixed order). weights[i] is the layer's
+ * (8, cins[i], 3, 3) weight, its upsampled channels are [up_first[i], up_first[i] + 8) (8 for
+ * cat(skip, up(low)), 0 for cat(up(low), skip)); wphases[i] receives 1024 floats
+ * (= nconv_phase_weights_floats of the layer). The nearest-2x upsampling maps a 3x3 window onto a
+ * 2x2 block of source-b pixels; which taps share a pixel depends only on the parity of the window's
+ * first row / column (models/step1.py:78-90 glue + :119-122). */
+size_t nconv_phase_weights_floats(const nconv_layer* L); /* 0 if L has no phase form */
+int nconv_phase_weights(int n, const float* const* weights, const int* cins, const int* up_first,
+                        float* const* wphases, void* stream);
 
 /* Forward of one NConv2d with fused input glue.
  * Replaces models/step1.py:119-147 (2x F.conv2d, mul, div, bias add, confidence normalisation)

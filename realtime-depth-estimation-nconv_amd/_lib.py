@@ -13,7 +13,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # NCONV_LIB: an alternative build of the same library (kernel-tuning experiments)
 LIB_PATH = os.environ.get("NCONV_LIB") or os.path.join(_HERE, "libnconv.so")
-ABI_VERSION = 14
+ABI_VERSION = 15
 BWD_ACCUMULATE = 1
 
 # enum nconv_load_mode
@@ -22,7 +22,8 @@ PLAIN, THRESH, POOL2, UPCAT_SKIP_FIRST, UPCAT_UP_FIRST = 0, 1, 2, 3, 4
 MATH_FP32, MATH_BF16X3, MATH_BF16X9 = 0, 1, 2
 # enum nconv_kernel (nconv_plan)
 KERNEL_GENERIC, KERNEL_TILED_FP32, KERNEL_MFMA_FP32, KERNEL_MFMA_BF16X3, KERNEL_MFMA_BF16X9 = 0, 1, 2, 3, 4
-KERNEL_NAMES = ("generic", "tiled_fp32", "mfma_fp32", "mfma_bf16x3", "mfma_bf16x9")
+KERNEL_TILED_FP32_PHASE = 5
+KERNEL_NAMES = ("generic", "tiled_fp32", "mfma_fp32", "mfma_bf16x3", "mfma_bf16x9", "tiled_fp32_phase")
 # enum nconv_dense_kind
 DENSE_3X3, DENSE_1X1, DENSE_TRANSPOSED_4X4, DENSE_CONV4X4_S2 = 0, 1, 2, 3
 
@@ -35,6 +36,8 @@ EXPORTED = (
     "nconv_fwd_tail",
     "nconv_fwd_head",
     "nconv_plan",
+    "nconv_phase_weights_floats",
+    "nconv_phase_weights",
     "nconv_bwd_workspace_bytes",
     "nconv_bwd",
     "nconv_dense_packed_floats",
@@ -67,7 +70,7 @@ class NconvLayer(ctypes.Structure):
                 ("groups", ctypes.c_int), ("eps", ctypes.c_float), ("load_mode", ctypes.c_int),
                 ("thresh", ctypes.c_float), ("a", NconvSrc), ("b", NconvSrc),
                 ("weight", ctypes.c_void_p), ("bias", ctypes.c_void_p), ("wsum", ctypes.c_void_p),
-                ("math", ctypes.c_int), ("bwd_math", ctypes.c_int)]
+                ("math", ctypes.c_int), ("bwd_math", ctypes.c_int), ("wphase", ctypes.c_void_p)]
 
 
 class NconvDenseConv(ctypes.Structure):
@@ -117,6 +120,10 @@ def _declare(lib):
                                    ctypes.c_float, P, P, ctypes.c_int, ctypes.c_int, P]
     lib.nconv_plan.restype = ctypes.c_int
     lib.nconv_plan.argtypes = [ctypes.POINTER(NconvLayer), P, P, P]
+    lib.nconv_phase_weights_floats.restype = ctypes.c_size_t
+    lib.nconv_phase_weights_floats.argtypes = [ctypes.POINTER(NconvLayer)]
+    lib.nconv_phase_weights.restype = ctypes.c_int
+    lib.nconv_phase_weights.argtypes = [ctypes.c_int, P, P, P, P, P]
     lib.nconv_bwd_workspace_bytes.restype = ctypes.c_size_t
     lib.nconv_bwd_workspace_bytes.argtypes = [ctypes.POINTER(NconvLayer)]
     lib.nconv_bwd.restype = ctypes.c_int

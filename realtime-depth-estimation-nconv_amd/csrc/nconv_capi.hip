@@ -198,6 +198,24 @@ int nconv_plan(const nconv_layer* L, int* fwd_kernel, int* dgrad_kernel, int* wg
     return 0;
 }
 
+size_t nconv_phase_weights_floats(const nconv_layer* L) {
+    if (validate(L, false)) return 0;
+    return nconv::phase_weight_floats(*L);
+}
+
+int nconv_phase_weights(int n, const float* const* weights, const int* cins, const int* up_first,
+                        float* const* wphases, void* stream) {
+    const char* fn = "nconv_phase_weights";
+    if (n < 0 || (n > 0 && (!weights || !cins || !up_first || !wphases))) return fail(-22, fn, "null argument");
+    for (int i = 0; i < n; ++i) {
+        if (!weights[i] || !wphases[i]) return fail(-22, fn, "null weight / output");
+        if (up_first[i] < 0 || up_first[i] + 8 > cins[i]) return fail(-22, fn, "upsampled channels outside [0, Cin)");
+    }
+    const char* why = nullptr;
+    int rc = nconv::launch_phase_weights(n, weights, cins, up_first, wphases, (hipStream_t)stream, &why);
+    return rc ? fail(rc, fn, why) : 0;
+}
+
 size_t nconv_bwd_workspace_bytes(const nconv_layer* L) {
     if (validate(L, true)) return 0;
     return nconv::bwd_workspace_bytes(make_dev(L));

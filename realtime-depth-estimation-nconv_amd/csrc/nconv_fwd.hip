@@ -397,6 +397,7 @@ static bool fwd_tiled_shape(const nconv_layer& L) {
 int plan_fwd(const nconv_layer& L) {
     if (fwd_mfma_supported(L, false, false))
         return L.math == NCONV_MATH_BF16X9 ? NCONV_KERNEL_MFMA_BF16X9 : NCONV_KERNEL_MFMA_BF16X3;
+    if (fwd_phase_supported(L, false)) return NCONV_KERNEL_TILED_FP32_PHASE;
     return fwd_tiled_shape(L) ? NCONV_KERNEL_TILED_FP32 : NCONV_KERNEL_GENERIC;
 }
 
@@ -406,6 +407,7 @@ int launch_fwd(const LayerDev& d, float* y, float* yc, float* py, float* pc, hip
     t.py = py;
     t.pc = pc;
     if (launch_fwd_mfma(d, y, yc, t, false, st)) return last_launch(why);
+    if (launch_fwd_phase(d, y, yc, t, false, st)) return last_launch(why);
     if (simple_geometry(L)) {
 #define NCONV_TRY(CIN, COUT, K, MODE)                                                       \
     if (L.Cin == CIN && L.Cout == COUT && L.KH == K && L.load_mode == MODE) {               \
@@ -460,6 +462,7 @@ int launch_fwd_tail(const LayerDev& d, const TailArgs& t, float* out, hipStream_
     }
     if (t.out_h <= 0 || t.out_w <= 0) return 0;
     if (launch_fwd_mfma(d, out, nullptr, t, true, st)) return last_launch(why);
+    if (launch_fwd_phase(d, out, nullptr, t, true, st)) return last_launch(why);
     go_tiled<16, 8, 3, NCONV_LOAD_UPCAT_UP_FIRST, true>(d, out, nullptr, t, t.out_h, t.out_w, st);
     return last_launch(why);
 }

@@ -43,6 +43,12 @@ struct BwdArgs {
 int launch_fwd(const LayerDev& d, float* y, float* yc, float* py, float* pc, hipStream_t st, const char** why);
 bool fwd_mfma_supported(const nconv_layer& L, bool tail, bool pool);
 bool launch_fwd_mfma(const LayerDev& d, float* y, float* yc, const TailArgs& t, bool tail, hipStream_t st);
+// exact-fp32 UPCAT layers with the upsampled half at native resolution (nconv_fwd_phase.hip)
+bool fwd_phase_supported(const nconv_layer& L, bool tail);
+bool launch_fwd_phase(const LayerDev& d, float* y, float* yc, const TailArgs& t, bool tail, hipStream_t st);
+size_t phase_weight_floats(const nconv_layer& L);
+int launch_phase_weights(int n, const float* const* w, const int* cin, const int* up_first, float* const* out,
+                         hipStream_t st, const char** why);
 // enum nconv_kernel of the forward / input-gradient / weight-gradient launches (nconv_plan)
 int plan_fwd(const nconv_layer& L);
 void plan_bwd(const nconv_layer& L, int* dgrad, int* wgrad);

@@ -23,7 +23,7 @@ import torch.nn as nn
 
 from . import _lib, export, nconv
 from .nconv import (EnforcePos, NConv2d, _require_device, layer_backward, layer_forward_head,
-                    layer_forward_pooled, layer_forward_raw, nconv_layer, weight_prep)
+                    layer_forward_pooled, layer_forward_raw, nconv_layer, phase_weights, weight_prep)
 
 LAYERS = ("nconv1", "nconv2", "nconv_down1", "nconv_down2", "nconv_down3", "nconv4", "nconv5",
           "nconv6", "nconv7")
@@ -182,7 +182,7 @@ class DNET(nn.Module):
 
         if not grad and min(H, W) >= 16:
             out = torch.empty((S.shape[0], 1, out_h, out_w), device=S.device, dtype=torch.float32)
-            self._infer_split(S, layers, wsum, out)
+            self._infer_split(S, layers, wsum, out, self._phase_weights(S.device))
             return out
 
         if grad and self.whole_graph_autograd and S.shape[0] > 0:
@@ -210,6 +210,23 @@ class DNET(nn.Module):
         return xo[:, :, 1:1 + out_h, 1:1 + out_w]
 
     # -- inference ------------------------------------------------------------------------------
+    # Exact-fp32 inference convolves the nearest-2x-upsampled half of nconv4/5/6's inputs at its
+    # own resolution with phase weights (include/nconv.h nconv_layer.wphase; the kernel uses them
+    # where the upsampling is exactly 2x); False: the 3x3 taps over the upsampled planes.
+    phase_upcat = True
+
+    def _phase_weights(self, device):
+        """Phase weights of nconv4, nconv5 (cat(skip, up): up channels 8..15) and nconv6
+        (cat(up, skip): 0..7) from the current weights, one launch; None when not in use."""
+        if not self.phase_upcat or nconv.FORWARD_MATH != _lib.MATH_FP32:
+            return None
+        ls = (self.nconv4, self.nconv5, self.nconv6)
+        if any(m.weight.shape[0] != 8 or m.weight.shape[1] != 16 or tuple(m.weight.shape[2:]) != (3, 3)
+               for m in ls):
+            return None
+        buf = torch.empty((3, 1024), device=device, dtype=torch.float32)
+        phase_weights([m.weight for m in ls], [8, 8, 0], list(buf))
+        return buf
     # Frames are independent, so the batch can be split over `inference_streams` HIP streams, each
     # running the whole layer chain on its share, so that one stream's kernels fill the partial
     # last round of the other's. The matrix-core layers run persistent grids sized to the chip,
@@ -223,11 +240,11 @@ class DNET(nn.Module):
             cache[key] = [torch.cuda.Stream(device=device) for _ in range(n)]
         return cache[key]
 
-    def _infer_split(self, S, layers, wsum, out):
+    def _infer_split(self, S, layers, wsum, out, wph=None):
         B = S.shape[0]
         n = max(1, min(int(self.inference_streams), B))
         if n == 1:
-            self._infer(S, layers, wsum, out)
+            self._infer(S, layers, wsum, out, wph)
             return
         cur = torch.cuda.current_stream(S.device)
         side = self._side_streams(S.device, n - 1)
@@ -236,15 +253,17 @@ class DNET(nn.Module):
             st.wait_stream(cur)
         for k, st in enumerate([cur] + side):
             with torch.cuda.stream(st):
-                self._infer(S[bounds[k]:bounds[k + 1]], layers, wsum, out[bounds[k]:bounds[k + 1]])
+                self._infer(S[bounds[k]:bounds[k + 1]], layers, wsum, out[bounds[k]:bounds[k + 1]], wph)
         for st in side:
             cur.wait_stream(st)
 
-    def _infer(self, S, layers, wsum, out):
+    def _infer(self, S, layers, wsum, out, wph=None):
         """The inference chain on the current stream: each producer also writes the pooled input
-        of the next down layer, and nconv6+nconv7+crop run as one launch writing `out`."""
+        of the next down layer, and nconv6+nconv7+crop run as one launch writing `out`. wph: the
+        phase weights of nconv4/5/6 (_phase_weights) or None."""
         (l1, l2, d1, d2, d3, l4, l5, l6, l7) = layers
         (s1, s2, sd1, sd2, sd3, s4, s5, s6, s7) = wsum
+        w4, w5, w6 = (None, None, None) if wph is None else tuple(wph)
         f, fp = layer_forward_raw, layer_forward_pooled
         if self._use_head(l1, l2):
             # nconv1 inside nconv2's staging: its 8-channel output never reaches HBM
@@ -258,13 +277,13 @@ class DNET(nn.Module):
         if n == 1:
             x3, c3, p3, q3 = fp(d2.spec(), p2, q2, None, None, d2.weight, d2.bias, sd2)
             x4, c4 = f(d3.spec(), p3, q3, None, None, d3.weight, d3.bias, sd3)
-            x34, c34 = f(l4.spec(_lib.UPCAT_SKIP_FIRST), x3, c3, x4, c4, l4.weight, l4.bias, s4)
+            x34, c34 = f(l4.spec(_lib.UPCAT_SKIP_FIRST), x3, c3, x4, c4, l4.weight, l4.bias, s4, wphase=w4)
         else:
-            x3, c3, p3, q3, x4, c4, x34, c34 = self._mid_split(n, layers, wsum, p2, q2)
+            x3, c3, p3, q3, x4, c4, x34, c34 = self._mid_split(n, layers, wsum, p2, q2, w4)
         if self.capture is not None:
             self.capture.update(down1=(x1, c1), down2=(x2, c2), down3=(x3, c3))
-        x23, c23 = f(l5.spec(_lib.UPCAT_SKIP_FIRST), x2, c2, x34, c34, l5.weight, l5.bias, s5)
-        self._fused_tail(l6, l7, s6, s7, x1, c1, x23, c23, out)
+        x23, c23 = f(l5.spec(_lib.UPCAT_SKIP_FIRST), x2, c2, x34, c34, l5.weight, l5.bias, s5, wphase=w5)
+        self._fused_tail(l6, l7, s6, s7, x1, c1, x23, c23, out, w6)
 
     # The quarter- and eighth-resolution layers (down2, down3, nconv4) have too few tiles to fill
     # the chip evenly (e.g. 836 tiles of down2 on 768 resident workgroups: a second, nearly empty
@@ -274,7 +293,7 @@ class DNET(nn.Module):
     # with 4: each slice's persistent grid is sized to the whole chip), so the default is 1.
     mid_streams = int(os.environ.get("NCONV_MID_STREAMS", "1"))
 
-    def _mid_split(self, n, layers, wsum, p2, q2):
+    def _mid_split(self, n, layers, wsum, p2, q2, w4=None):
         (l1, l2, d1, d2, d3, l4, l5, l6, l7) = layers
         (s1, s2, sd1, sd2, sd3, s4, s5, s6, s7) = wsum
         B, C, H4, W4 = p2.shape
@@ -301,7 +320,7 @@ class DNET(nn.Module):
                 layer_forward_raw(d3.spec(), p3[sl], q3[sl], None, None, d3.weight, d3.bias, sd3,
                                   out=(x4[sl], c4[sl]))
                 layer_forward_raw(sp4, x3[sl], c3[sl], x4[sl], c4[sl], l4.weight, l4.bias, s4,
-                                  out=(x34[sl], c34[sl]))
+                                  out=(x34[sl], c34[sl]), wphase=w4)
         for st in side:
             cur.wait_stream(st)
         return x3, c3, p3, q3, x4, c4, x34, c34
@@ -322,11 +341,11 @@ class DNET(nn.Module):
             (8, 8, (5, 5), (2, 2), (1, 1)) and tuple(l1.dilation) == (1, 1) and tuple(l2.dilation) == (1, 1) \
             and l1.groups == 1 and l2.groups == 1
 
-    def _fused_tail(self, l6, l7, s6, s7, x1, c1, x23, c23, out):
+    def _fused_tail(self, l6, l7, s6, s7, x1, c1, x23, c23, out, w6=None):
         out_h, out_w = out.shape[2], out.shape[3]
         if out_h == 0 or out_w == 0 or out.shape[0] == 0:
             return out
-        L = l6.spec(_lib.UPCAT_UP_FIRST).descriptor(x1, c1, x23, c23, l6.weight, l6.bias, s6)
+        L = l6.spec(_lib.UPCAT_UP_FIRST).descriptor(x1, c1, x23, c23, l6.weight, l6.bias, s6, w6)
         if tuple(l7.kernel_size) != (1, 1) or l7.padding[0] != l7.padding[1] or tuple(l7.stride) != (1, 1):
             raise RuntimeError("fused tail needs nconv7 = 1x1, stride 1, square padding")
         rc = _lib.lib().nconv_fwd_tail(

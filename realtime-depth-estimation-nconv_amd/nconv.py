@@ -71,7 +71,7 @@ class LayerSpec:
         wo = (W + 2 * self.padding[1] - self.dilation[1] * (kw - 1) - 1) // self.stride[1] + 1
         return ho, wo
 
-    def descriptor(self, xa, ca, xb, cb, weight, bias, wsum):
+    def descriptor(self, xa, ca, xb, cb, weight, bias, wsum, wphase=None):
         H, W = self.in_hw(xa.shape)
         Ho, Wo = self.out_hw(H, W)
         L = _lib.NconvLayer()
@@ -90,6 +90,7 @@ class LayerSpec:
         L.weight, L.bias, L.wsum = weight.data_ptr(), bias.data_ptr(), wsum.data_ptr()
         L.math = FORWARD_MATH
         L.bwd_math = BACKWARD_MATH
+        L.wphase = wphase.data_ptr() if wphase is not None else None
         return L
 
 
@@ -119,9 +120,24 @@ def _outputs(out, n, shapes, device):
     return list(out)
 
 
-def layer_forward_raw(spec: LayerSpec, xa, ca, xb, cb, weight, bias, wsum, out=None):
-    """Enqueue nconv_fwd; returns (y, cout) (written into `out` if given). No autograd."""
-    L = spec.descriptor(xa, ca, xb, cb, weight, bias, wsum)
+def phase_weights(weights, up_first, outs):
+    """nconv_phase_weights: one launch filling outs[i] (1024 floats) with the phase weights of the
+    UPCAT layer whose (8, Cin, 3, 3) weight is weights[i] and whose upsampled channels start at
+    up_first[i], from the current weights (after weight_prep)."""
+    n = len(weights)
+    if n == 0:
+        return
+    P, I = _lib.ctypes.c_void_p * n, _lib.ctypes.c_int * n
+    rc = _lib.lib().nconv_phase_weights(n, P(*[w.data_ptr() for w in weights]), I(*[w.shape[1] for w in weights]),
+                                        I(*up_first), P(*[o.data_ptr() for o in outs]),
+                                        _lib.stream_handle(outs[0].device))
+    _lib.check(rc, "nconv_phase_weights")
+
+
+def layer_forward_raw(spec: LayerSpec, xa, ca, xb, cb, weight, bias, wsum, out=None, wphase=None):
+    """Enqueue nconv_fwd; returns (y, cout) (written into `out` if given). No autograd. `wphase`:
+    the layer's phase weights (UPCAT layers, phase_weights), or None."""
+    L = spec.descriptor(xa, ca, xb, cb, weight, bias, wsum, wphase)
     sh = (L.B, L.Cout, L.Ho, L.Wo)
     y, co = _outputs(out, 2, (sh, sh), xa.device)
     rc = _lib.lib().nconv_fwd(_lib.ctypes.byref(L), _lib.ptr(y), _lib.ptr(co), _lib.stream_handle(xa.device))

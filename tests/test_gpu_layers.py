@@ -229,3 +229,50 @@ def test_fwd_head_matches_unfused(nconv_amd, gpu, shape, monkeypatch):
         torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-5)
     assert torch.equal(py1, torch.nn.functional.max_pool2d(y1, 2, 2))
     assert torch.equal(pc1, torch.nn.functional.max_pool2d(c1f, 2, 2))
+
+
+# Exact-2x UPCAT layers on the phase path (nconv_layer.wphase, nconv_fwd_phase.hip): both channel
+# orders, paddings 0 / 1 / 2 (both phase parities), ragged widths, tiles cut by the image edge.
+# (name, mode, pad, a-shape, b-shape)
+PHASE_CASES = [
+    ("skip_p1", 3, 1, (8, 24, 70), (8, 12, 35)),
+    ("skip_p1_w4", 3, 1, (8, 26, 72), (8, 13, 36)),
+    ("skip_p0", 3, 0, (8, 20, 64), (8, 10, 32)),
+    ("skip_p2", 3, 2, (8, 18, 46), (8, 9, 23)),
+    ("up_p0", 4, 0, (8, 34, 72), (8, 17, 36)),
+    ("up_p1", 4, 1, (8, 36, 66), (8, 18, 33)),
+]
+
+
+@pytest.mark.parametrize("case", PHASE_CASES, ids=[c[0] for c in PHASE_CASES])
+def test_upcat_phase_forward(nconv_amd, gpu, case):
+    """The phase path (upsampled half at native resolution with summed fp32 weights) against the
+    oracle's reference glue (cat + F.interpolate nearest) + NConv2d.forward, same tolerance as the
+    dense kernels; nconv_plan must name the phase kernel and the dense path must agree."""
+    name, mode, pad, a_shape, b_shape = case
+    g = torch.Generator().manual_seed(11)
+    xa, ca = rand_pair(g, 3, *a_shape, dtype=torch.float64)
+    xb, cb = rand_pair(g, 3, *b_shape, dtype=torch.float64)
+    w = rand_weight(g, 8, 16, 3, 3, torch.float64)
+    b = torch.rand(8, generator=g, dtype=torch.float64) * 0.1
+    ry, rc = oracle_layer(mode, xa, ca, xb, cb, w, b, (1, 1), (pad, pad))
+    spec = nconv_amd.LayerSpec(16, 8, (3, 3), (1, 1), (pad, pad), mode=mode)
+    t = [_gpu(v, gpu) for v in (xa, ca, xb, cb, w, b)]
+    wsum = _wsum(nconv_amd, t[4])
+    wph = torch.empty(1024, device=gpu)
+    nconv_amd.nconv.phase_weights([t[4]], [8 if mode == 3 else 0], [wph])
+    assert nconv_amd.nconv.kernel_plan(spec, *t[:4], t[4], t[5], wsum)[0] == "tiled_fp32"
+    L = spec.descriptor(*t[:4], t[4], t[5], wsum, wph)
+    import ctypes
+    k = ctypes.c_int(-1)
+    assert nconv_amd._lib.lib().nconv_plan(ctypes.byref(L), ctypes.byref(k), None, None) == 0
+    assert nconv_amd._lib.KERNEL_NAMES[k.value] == "tiled_fp32_phase"
+    y, c = nconv_amd.nconv.layer_forward_raw(spec, *t[:4], t[4], t[5], wsum, wphase=wph)
+    yd, cd = nconv_amd.nconv.layer_forward_raw(spec, *t[:4], t[4], t[5], wsum)
+    torch.cuda.synchronize()
+    for got, ref in ((y, ry), (c, rc), (yd, ry), (cd, rc)):
+        got = got.double().cpu()
+        err = (got - ref).abs()
+        bound = 1e-4 * ref.abs() + 1e-5
+        assert (err <= bound).all(), f"{name}: max err {err.max():.3e}, worst ratio {(err / bound).max():.3f}"
+    print(f"{name}: phase vs dense max rel {((y - yd).abs() / (yd.abs() + 1e-30)).max().item():.2e}")

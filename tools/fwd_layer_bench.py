@@ -52,7 +52,11 @@ def main():
         xa, ca = r(B, 8, H // f, W // f) * 10, r(B, 8, H // f, W // f)
         xb, cb = r(B, 8, H // (2 * f), W // (2 * f)) * 10, r(B, 8, H // (2 * f), W // (2 * f))
         spec = m.LayerSpec(16, 8, (3, 3), (1, 1), (1, 1), mode=m._lib.UPCAT_SKIP_FIRST)
-        fn = lambda: N.layer_forward_raw(spec, xa, ca, xb, cb, w16, b, s16)
+        wph = None
+        if os.environ.get("NCONV_PHASE", "1") == "1":
+            wph = torch.empty(1024, device=dev)
+            N.phase_weights([w16], [8], [wph])
+        fn = lambda: N.layer_forward_raw(spec, xa, ca, xb, cb, w16, b, s16, wphase=wph)
     else:  # nconv6 + nconv7 tail
         net = m.DNET(32, crop="generalized").to(dev).eval()
         xa, ca = r(B, 8, H, W) * 10, r(B, 8, H, W)
@@ -60,7 +64,9 @@ def main():
         out = torch.empty(B, 1, H, W, device=dev)
         s6 = net.nconv6.weight.sum((1, 2, 3)).contiguous()
         s7 = net.nconv7.weight.sum((1, 2, 3)).contiguous()
-        fn = lambda: net._fused_tail(net.nconv6, net.nconv7, s6, s7, xa, ca, xb, cb, out)
+        net.phase_upcat = os.environ.get("NCONV_PHASE", "1") == "1"
+        wph = net._phase_weights(dev)
+        fn = lambda: net._fused_tail(net.nconv6, net.nconv7, s6, s7, xa, ca, xb, cb, out, None if wph is None else wph[2])
     fn()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
