@@ -75,6 +75,10 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU time of each CPU-baseline sample")
     p.add_argument("--graph", type=int, default=1, help="capture the forward in a hipGraph (1) or run eager (0)")
     p.add_argument("--fused-head", type=int, default=1, help="nconv1 inside nconv2's kernel (nconv_fwd_head)")
+    p.add_argument("--inference-streams", type=int, default=None,
+                   help="DNET.inference_streams: batch slices on that many streams (default: the module's)")
+    p.add_argument("--mid-streams", type=int, default=None,
+                   help="DNET.mid_streams: the quarter/eighth-resolution layers on that many batch slices")
     p.add_argument("--train-graph", type=int, default=-1,
                    help="replay the training step from a hipGraph (1) or eager (0); default: 1 on one GPU, 0 with "
                         "several (the RCCL all-reduce stays outside graph capture)")
@@ -450,6 +454,10 @@ def main():
         net(torch.zeros(1, 1, 32, 32, device=dev))  # one EnforcePos: positive (trained-like) weights
     net.eval()
     net.d_net.fused_head = bool(a.fused_head)
+    if a.inference_streams is not None:
+        net.d_net.inference_streams = a.inference_streams
+    if a.mid_streams is not None:
+        net.d_net.mid_streams = a.mid_streams
     g = torch.Generator().manual_seed(1000 + rank)
     S = sparse_depth(g, B, H, W, dev)
 

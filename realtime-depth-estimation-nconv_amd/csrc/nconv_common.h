@@ -324,6 +324,18 @@ __device__ __forceinline__ float ld_f32s(__amdgpu_buffer_rsrc_t r, unsigned off,
     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, soff, 0));
 }
 
+__device__ __forceinline__ void st_f32(__amdgpu_buffer_rsrc_t r, unsigned off, float v) {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, (int)off, 0, 0);
+}
+__device__ __forceinline__ void st_f2(__amdgpu_buffer_rsrc_t r, unsigned off, f2 v) {
+    typedef unsigned u2 __attribute__((ext_vector_type(2)));
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v), r, (int)off, 0, 0);
+}
+__device__ __forceinline__ void st_f4(__amdgpu_buffer_rsrc_t r, unsigned off, f4 v) {
+    typedef unsigned u4 __attribute__((ext_vector_type(4)));
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, v), r, (int)off, 0, 0);
+}
+
 template <int IHT, int IWT, int IWP, int MODE, int NTH = 256>
 struct TileStager {
     static constexpr int NT = IHT * IWT;

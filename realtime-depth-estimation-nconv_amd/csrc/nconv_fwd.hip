@@ -153,14 +153,31 @@ __global__ __launch_bounds__(NTH) void fwd_tiled(LayerDev d, float* __restrict__
     // ---- epilogue ----
     const int oh = oh0 + ty;
     if constexpr (!TAIL) {
-        constexpr int VW = C::P % 4 == 0 ? 4 : C::P % 2 == 0 ? 2 : 1;  // vector store width
-        const bool vec = (L.Wo % VW) == 0 && (ow0 + tx + C::P - 1) < L.Wo;
+        // Buffer stores through one resource per output plane (base and size in SGPRs, built by
+        // scalar ops per channel): the per-lane byte offset is computed once, and pixels outside
+        // the output carry an offset past the plane, which the store drops -- no 64-bit address
+        // arithmetic and no bounds branches per channel.
+        constexpr unsigned OOB = 0x80000000u;
+        const int ow = ow0 + tx;
+        const size_t plane = (size_t)L.Ho * L.Wo;
+        const int pbytes = (int)(plane * 4);
+        unsigned so[C::P];
+#pragma unroll
+        for (int j = 0; j < C::P; ++j)
+            so[j] = (oh < L.Ho && ow + j < L.Wo) ? (unsigned)(oh * L.Wo + ow + j) * 4u : OOB;
+        const bool vec = (L.Wo % 2) == 0 && (ow + C::P - 1) < L.Wo && oh < L.Ho;  // pairs: 8-byte stores
         // optional fused 2x2 max-pool of the outputs (the next down layer's input, step1.py:62-75):
         // rows oh and oh^1 sit in lanes l and l^16 of one wave (ty = lt >> 4, tile origin even)
         const bool pool = t.py != nullptr;
         const int Hp = L.Ho >> 1, Wp = L.Wo >> 1;
-        const int pr = oh >> 1, pc0 = (ow0 + tx) >> 1;
+        const size_t pplane = (size_t)Hp * Wp;
+        const int ppbytes = (int)(pplane * 4);
+        const int pr = oh >> 1, pc0 = ow >> 1;
         const bool pool_row = pool && ((ty & 1) == 0) && pr < Hp;
+        unsigned po[C::P > 1 ? C::P / 2 : 1];
+#pragma unroll
+        for (int h = 0; h < (C::P > 1 ? C::P / 2 : 1); ++h)
+            po[h] = (pool_row && pc0 + h < Wp && (C::P > 1 || (lt & 1) == 0)) ? (unsigned)(pr * Wp + pc0 + h) * 4u : OOB;
 #pragma unroll
         for (int oo = 0; oo < CO; ++oo) {
             const int o = og * CO + oo;
@@ -175,47 +192,36 @@ __global__ __launch_bounds__(NTH) void fwd_tiled(LayerDev d, float* __restrict__
                     yb[j] = __shfl_xor(yv[j], 16);
                     cb[j] = __shfl_xor(cv[j], 16);
                 }
+                const size_t pofs = ((size_t)b * COUT + o) * pplane;
+                const __amdgpu_buffer_rsrc_t rpy = plane_rsrc(t.py + pofs, ppbytes);
+                const __amdgpu_buffer_rsrc_t rpc = plane_rsrc(t.pc + pofs, ppbytes);
                 if constexpr (C::P == 1) {  // the window's right column sits in lane l^1
                     const float ya = __shfl_xor(yv[0], 1), ca = __shfl_xor(cv[0], 1);
                     const float yd = __shfl_xor(yb[0], 1), cd = __shfl_xor(cb[0], 1);
-                    if (pool_row && (lt & 1) == 0 && pc0 < Wp) {
-                        const size_t pi = plane_idx(b, o, COUT, Hp, Wp, pr, pc0);
-                        t.py[pi] = pool4v(yv[0], ya, yb[0], yd);
-                        t.pc[pi] = pool4v(cv[0], ca, cb[0], cd);
-                    }
-                } else if (pool_row) {
-                    const size_t pbase = plane_idx(b, o, COUT, Hp, Wp, pr, pc0);
+                    st_f32(rpy, po[0], pool4v(yv[0], ya, yb[0], yd));
+                    st_f32(rpc, po[0], pool4v(cv[0], ca, cb[0], cd));
+                } else {
 #pragma unroll
-                    for (int h = 0; h < C::P / 2; ++h)
-                        if (pc0 + h < Wp) {
-                            t.py[pbase + h] = pool4v(yv[2 * h], yv[2 * h + 1], yb[2 * h], yb[2 * h + 1]);
-                            t.pc[pbase + h] = pool4v(cv[2 * h], cv[2 * h + 1], cb[2 * h], cb[2 * h + 1]);
-                        }
+                    for (int h = 0; h < C::P / 2; ++h) {
+                        st_f32(rpy, po[h], pool4v(yv[2 * h], yv[2 * h + 1], yb[2 * h], yb[2 * h + 1]));
+                        st_f32(rpc, po[h], pool4v(cv[2 * h], cv[2 * h + 1], cb[2 * h], cb[2 * h + 1]));
+                    }
                 }
             }
-            if (oh >= L.Ho) continue;
-            const size_t base = plane_idx(b, o, COUT, L.Ho, L.Wo, oh, ow0 + tx);
-            if (vec) {
+            const size_t ofs = ((size_t)b * COUT + o) * plane;
+            const __amdgpu_buffer_rsrc_t ry = plane_rsrc(y + ofs, pbytes), rc = plane_rsrc(yc + ofs, pbytes);
+            if (C::P % 2 == 0 && vec) {
 #pragma unroll
-                for (int q = 0; q < C::P; q += VW) {
-                    if constexpr (VW == 4) {
-                        *reinterpret_cast<f4*>(y + base + q) = (f4){yv[q], yv[q + 1], yv[q + 2], yv[q + 3]};
-                        *reinterpret_cast<f4*>(yc + base + q) = (f4){cv[q], cv[q + 1], cv[q + 2], cv[q + 3]};
-                    } else if constexpr (VW == 2) {
-                        *reinterpret_cast<f2*>(y + base + q) = (f2){yv[q], yv[q + 1]};
-                        *reinterpret_cast<f2*>(yc + base + q) = (f2){cv[q], cv[q + 1]};
-                    } else {
-                        y[base + q] = yv[q];
-                        yc[base + q] = cv[q];
-                    }
+                for (int q = 0; q < C::P; q += 2) {
+                    st_f2(ry, so[q], (f2){yv[q], yv[q + 1]});
+                    st_f2(rc, so[q], (f2){cv[q], cv[q + 1]});
                 }
             } else {
 #pragma unroll
-                for (int j = 0; j < C::P; ++j)
-                    if (ow0 + tx + j < L.Wo) {
-                        y[base + j] = yv[j];
-                        yc[base + j] = cv[j];
-                    }
+                for (int j = 0; j < C::P; ++j) {
+                    st_f32(ry, so[j], yv[j]);
+                    st_f32(rc, so[j], cv[j]);
+                }
             }
         }
     } else {

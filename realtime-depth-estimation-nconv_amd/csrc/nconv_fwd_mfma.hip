@@ -93,17 +93,6 @@ constexpr unsigned kOOB = 0x80000000u;
 constexpr int kOutPitch = 36;  // floats per row of a wave's output-transpose region
 constexpr int kTrBytes = 4 * 16 * kOutPitch * 4;  // four waves' regions (y, then cout, through one)
 
-__device__ __forceinline__ void st_f32(__amdgpu_buffer_rsrc_t r, unsigned off, float v) {
-    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, (int)off, 0, 0);
-}
-__device__ __forceinline__ void st_f2(__amdgpu_buffer_rsrc_t r, unsigned off, f2 v) {
-    typedef unsigned u2 __attribute__((ext_vector_type(2)));
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v), r, (int)off, 0, 0);
-}
-__device__ __forceinline__ void st_f4(__amdgpu_buffer_rsrc_t r, unsigned off, f4 v) {
-    typedef unsigned u4 __attribute__((ext_vector_type(4)));
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, v), r, (int)off, 0, 0);
-}
 
 // One position's 8 channels of {x*c, c} into the planes of a tile (base = plane 0 of the
 // position's channel group): x*c parts in planes 0 .. NP-1, c parts in NP .. 2NP-1.

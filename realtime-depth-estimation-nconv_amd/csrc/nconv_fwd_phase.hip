@@ -191,27 +191,32 @@ __global__ __launch_bounds__(kPT) void fwd_phase(LayerDev d, float* __restrict__
     // ---- epilogue ----
     const int oh = oh0 + ty;
     if constexpr (!TAIL) {
-        if (oh >= L.Ho) return;
+        // per-plane buffer stores (as fwd_tiled): offsets past the plane are dropped
+        constexpr unsigned OOB = 0x80000000u;
+        const int ow = ow0 + tx;
         const size_t plane = (size_t)L.Ho * L.Wo;
-        const size_t base = plane_idx(b, 0, kPCO, L.Ho, L.Wo, oh, ow0 + tx);
-        const bool vec = (L.Wo % 2) == 0 && (ow0 + tx + 1) < L.Wo;
+        const int pbytes = (int)(plane * 4);
+        unsigned so[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) so[j] = (oh < L.Ho && ow + j < L.Wo) ? (unsigned)(oh * L.Wo + ow + j) * 4u : OOB;
+        const bool vec = (L.Wo % 2) == 0 && ow + 1 < L.Wo && oh < L.Ho;
 #pragma unroll
         for (int o = 0; o < kPCO; ++o) {
             float yv[2], cv[2];
             const float s = L.wsum[o], bo = L.bias[o];
 #pragma unroll
             for (int j = 0; j < 2; ++j) nconv_epilogue(acc[o][j].x, acc[o][j].y, L.eps, bo, s, yv[j], cv[j]);
-            const size_t i = base + o * plane;
+            const size_t ofs = ((size_t)b * kPCO + o) * plane;
+            const __amdgpu_buffer_rsrc_t ry = plane_rsrc(y + ofs, pbytes), rc = plane_rsrc(yc + ofs, pbytes);
             if (vec) {
-                *reinterpret_cast<f2*>(y + i) = (f2){yv[0], yv[1]};
-                *reinterpret_cast<f2*>(yc + i) = (f2){cv[0], cv[1]};
+                st_f2(ry, so[0], (f2){yv[0], yv[1]});
+                st_f2(rc, so[0], (f2){cv[0], cv[1]});
             } else {
 #pragma unroll
-                for (int j = 0; j < 2; ++j)
-                    if (ow0 + tx + j < L.Wo) {
-                        y[i + j] = yv[j];
-                        yc[i + j] = cv[j];
-                    }
+                for (int j = 0; j < 2; ++j) {
+                    st_f32(ry, so[j], yv[j]);
+                    st_f32(rc, so[j], cv[j]);
+                }
             }
         }
     } else {

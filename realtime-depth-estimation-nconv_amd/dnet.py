@@ -229,9 +229,17 @@ class DNET(nn.Module):
         return buf
     # Frames are independent, so the batch can be split over `inference_streams` HIP streams, each
     # running the whole layer chain on its share, so that one stream's kernels fill the partial
-    # last round of the other's. The matrix-core layers run persistent grids sized to the chip,
-    # which leave no such gaps: one stream measures faster (B=8 352x1216: 0.507 vs 0.555 ms).
-    inference_streams = 1
+    # last round of the other's (and its small quarter / eighth-resolution layers overlap the other
+    # share's large ones). None = automatic: 2 for the exact-fp32 kernels (B=8 352x1216: 0.616 vs
+    # 0.628 ms), 1 for the matrix-core maths, whose persistent grids are sized to the chip and
+    # leave no such gaps (0.507 vs 0.555 ms). A frame's result does not depend on the split.
+    inference_streams = None
+
+    def _n_streams(self, B):
+        n = self.inference_streams
+        if n is None:
+            n = 2 if nconv.FORWARD_MATH == _lib.MATH_FP32 else 1
+        return max(1, min(int(n), B))
 
     def _side_streams(self, device, n):
         key = (device.index, n)
@@ -242,7 +250,7 @@ class DNET(nn.Module):
 
     def _infer_split(self, S, layers, wsum, out, wph=None):
         B = S.shape[0]
-        n = max(1, min(int(self.inference_streams), B))
+        n = self._n_streams(B)
         if n == 1:
             self._infer(S, layers, wsum, out, wph)
             return
@@ -253,14 +261,15 @@ class DNET(nn.Module):
             st.wait_stream(cur)
         for k, st in enumerate([cur] + side):
             with torch.cuda.stream(st):
-                self._infer(S[bounds[k]:bounds[k + 1]], layers, wsum, out[bounds[k]:bounds[k + 1]], wph)
+                self._infer(S[bounds[k]:bounds[k + 1]], layers, wsum, out[bounds[k]:bounds[k + 1]], wph, mid=False)
         for st in side:
             cur.wait_stream(st)
 
-    def _infer(self, S, layers, wsum, out, wph=None):
+    def _infer(self, S, layers, wsum, out, wph=None, mid=True):
         """The inference chain on the current stream: each producer also writes the pooled input
         of the next down layer, and nconv6+nconv7+crop run as one launch writing `out`. wph: the
-        phase weights of nconv4/5/6 (_phase_weights) or None."""
+        phase weights of nconv4/5/6 (_phase_weights) or None. mid=False (inside an inference
+        split): no nested mid_streams split."""
         (l1, l2, d1, d2, d3, l4, l5, l6, l7) = layers
         (s1, s2, sd1, sd2, sd3, s4, s5, s6, s7) = wsum
         w4, w5, w6 = (None, None, None) if wph is None else tuple(wph)
@@ -273,7 +282,7 @@ class DNET(nn.Module):
             x1, c1 = f(l1.spec(_lib.THRESH, 0.01), S, None, None, None, l1.weight, l1.bias, s1)
             x1, c1, p1, q1 = fp(l2.spec(), x1, c1, None, None, l2.weight, l2.bias, s2)
         x2, c2, p2, q2 = fp(d1.spec(), p1, q1, None, None, d1.weight, d1.bias, sd1)
-        n = max(1, min(int(self.mid_streams), S.shape[0]))
+        n = max(1, min(int(self.mid_streams), S.shape[0])) if mid else 1
         if n == 1:
             x3, c3, p3, q3 = fp(d2.spec(), p2, q2, None, None, d2.weight, d2.bias, sd2)
             x4, c4 = f(d3.spec(), p3, q3, None, None, d3.weight, d3.bias, sd3)
