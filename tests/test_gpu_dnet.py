@@ -165,6 +165,7 @@ def test_mid_streams_split_matches_one_stream(nconv_amd, gpu, n):
     """Inference with down2/down3/nconv4 run on batch slices in several streams (DNET.mid_streams)
     writes the same bits as the one-stream chain (same kernels per frame), eager and graphed."""
     net = make_net(nconv_amd, "generalized", gpu)
+    net.d_net.inference_streams = 1  # (mid_streams applies to an unsplit chain)
     g = torch.Generator().manual_seed(31)
     S = sparse_depth(g, 5, 96, 160).to(gpu)
     with torch.no_grad():
@@ -178,6 +179,28 @@ def test_mid_streams_split_matches_one_stream(nconv_amd, gpu, n):
         graph.replay()
         torch.cuda.synchronize()
         net.d_net.mid_streams = 1
+    assert torch.equal(a, b) and torch.equal(a, c)
+
+
+@pytest.mark.parametrize("n", [2, 3, 8])
+def test_inference_streams_split_matches_one_stream(nconv_amd, gpu, n):
+    """The whole inference chain on batch slices in n streams (DNET.inference_streams; the
+    exact-fp32 default is 2) writes the same bits as one stream, eager and graphed (n = 8 > B:
+    one frame per stream)."""
+    net = make_net(nconv_amd, "generalized", gpu)
+    g = torch.Generator().manual_seed(37)
+    S = sparse_depth(g, 5, 96, 160).to(gpu)
+    with torch.no_grad():
+        net.d_net.inference_streams = 1
+        a = net(S)
+        net.d_net.inference_streams = n
+        b = net(S)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            c = net(S)
+        graph.replay()
+        torch.cuda.synchronize()
+        net.d_net.inference_streams = None
     assert torch.equal(a, b) and torch.equal(a, c)
 
 
