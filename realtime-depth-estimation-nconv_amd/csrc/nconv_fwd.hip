@@ -369,12 +369,17 @@ static void go_tiled_cs(const LayerDev& d, float* y, float* yc, const TailArgs& 
 // resolution layers); the small quarter / eighth-resolution layers would leave most SIMDs with no
 // wave at all, so their waves split the output channels (2 or 4 slices, on 8- or 4-row tiles;
 // a slice is whole waves, so its weights stay wave-uniform) and the layer spreads over the whole
-// chip.
+// chip. (Thresholds measured: a CS=1 limit of 1024 tiles against 2048 / 4096 / 8192 / never at
+// B=8 352x1216, one and two inference streams: profiles/r3_ab_fwd_cs.log.)
+#ifndef NCONV_CS1_TILES
+#define NCONV_CS1_TILES 1024
+#endif
+#ifndef NCONV_CS2_TILES
+#define NCONV_CS2_TILES 512
+#endif
 static int tiled_cs(long tiles16, int cout, int mode) {
-    // (the max-pooling loads of the down layers gain from the shorter pipeline already at half
-    // resolution: down1 66 vs 72 us at B=8 352x1216; nconv5 does not, 56 vs 53 us)
-    const long big = mode == NCONV_LOAD_POOL2 ? 2048 : 1024;
-    int cs = tiles16 >= big ? 1 : tiles16 >= 512 ? 2 : 4;
+    (void)mode;
+    int cs = tiles16 >= NCONV_CS1_TILES ? 1 : tiles16 >= NCONV_CS2_TILES ? 2 : 4;
     while (cs > 1 && cout % cs) cs >>= 1;
     return cs;
 }

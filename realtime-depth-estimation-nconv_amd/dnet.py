@@ -39,22 +39,27 @@ class DNETFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, specs, capture, S, *p):
+        """p: (weight, bias, s[o]) of each layer, then the phase weights of nconv4/5/6 (a (3, 1024)
+        tensor, DNET._phase_weights) or None."""
         W = [p[3 * i:3 * i + 3] for i in range(9)]
+        wph = p[27] if len(p) > 27 and p[27] is not None else None
+        w4, w5, w6 = (None, None, None) if wph is None else tuple(wph)
         sp = specs
         x1, c1 = layer_forward_raw(sp[0], S, None, None, None, *W[0])
         x2, c2 = layer_forward_raw(sp[1], x1, c1, None, None, *W[1])
         x3, c3 = layer_forward_raw(sp[2], x2, c2, None, None, *W[2])
         x4, c4 = layer_forward_raw(sp[3], x3, c3, None, None, *W[3])
         x5, c5 = layer_forward_raw(sp[4], x4, c4, None, None, *W[4])
-        x6, c6 = layer_forward_raw(sp[5], x4, c4, x5, c5, *W[5])
-        x7, c7 = layer_forward_raw(sp[6], x3, c3, x6, c6, *W[6])
-        x8, c8 = layer_forward_raw(sp[7], x2, c2, x7, c7, *W[7])
+        x6, c6 = layer_forward_raw(sp[5], x4, c4, x5, c5, *W[5], wphase=w4)
+        x7, c7 = layer_forward_raw(sp[6], x3, c3, x6, c6, *W[6], wphase=w5)
+        x8, c8 = layer_forward_raw(sp[7], x2, c2, x7, c7, *W[7], wphase=w6)
         x9, c9 = layer_forward_raw(sp[8], x8, c8, None, None, *W[8])
         if capture is not None:  # the three pooling stages' inputs (DNET.capture)
             capture.update(down1=(x2.detach(), c2.detach()), down2=(x3.detach(), c3.detach()),
                            down3=(x4.detach(), c4.detach()))
         ctx.specs = specs
-        ctx.save_for_backward(S, *p, x1, c1, x2, c2, x3, c3, x4, c4, x5, c5, x6, c6, x7, c7, x8, c8, x9, c9)
+        ctx.n_extra = len(p) - 27
+        ctx.save_for_backward(S, *p[:27], x1, c1, x2, c2, x3, c3, x4, c4, x5, c5, x6, c6, x7, c7, x8, c8, x9, c9)
         ctx.mark_non_differentiable(c9)
         return x9, c9
 
@@ -98,7 +103,7 @@ class DNETFn(torch.autograd.Function):
         out = [None, None, gS]
         for i in range(9):
             out += [gw[i], gb[i], None]
-        return tuple(out)
+        return tuple(out + [None] * ctx.n_extra)
 
 
 def crop_hw(H, W, crop):
@@ -178,7 +183,7 @@ class DNET(nn.Module):
         grad = torch.is_grad_enabled() and (S.requires_grad or any(p.requires_grad for p in self.parameters()))
         H, W = S.shape[2], S.shape[3]
         out_h, out_w = crop_hw(H, W, self.crop)
-        f = nconv_layer if grad else (lambda spec, *a: layer_forward_raw(spec, *a))
+        f = nconv_layer if grad else (lambda spec, *a, wphase=None: layer_forward_raw(spec, *a, wphase=wphase))
 
         if not grad and min(H, W) >= 16:
             out = torch.empty((S.shape[0], 1, out_h, out_w), device=S.device, dtype=torch.float32)
@@ -192,8 +197,11 @@ class DNET(nn.Module):
             params = []
             for m_, s_ in zip(layers, wsum):
                 params += [m_.weight, m_.bias, s_]
-            xo, _ = DNETFn.apply(specs, self.capture, S, *params)
+            xo, _ = DNETFn.apply(specs, self.capture, S, *params, self._phase_weights(S.device))
             return xo[:, :, 1:1 + out_h, 1:1 + out_w]
+
+        wph = self._phase_weights(S.device)
+        w4, w5, w6 = (None, None, None) if wph is None else tuple(wph)
 
         x1, c1 = f(l1.spec(_lib.THRESH, 0.01), S, None, None, None, l1.weight, l1.bias, s1)
         x1, c1 = f(l2.spec(), x1, c1, None, None, l2.weight, l2.bias, s2)
@@ -203,9 +211,9 @@ class DNET(nn.Module):
         if self.capture is not None:
             self.capture.update(down1=(x1.detach(), c1.detach()), down2=(x2.detach(), c2.detach()),
                                 down3=(x3.detach(), c3.detach()))
-        x34, c34 = f(l4.spec(_lib.UPCAT_SKIP_FIRST), x3, c3, x4, c4, l4.weight, l4.bias, s4)
-        x23, c23 = f(l5.spec(_lib.UPCAT_SKIP_FIRST), x2, c2, x34, c34, l5.weight, l5.bias, s5)
-        xo, co = f(l6.spec(_lib.UPCAT_UP_FIRST), x1, c1, x23, c23, l6.weight, l6.bias, s6)
+        x34, c34 = f(l4.spec(_lib.UPCAT_SKIP_FIRST), x3, c3, x4, c4, l4.weight, l4.bias, s4, wphase=w4)
+        x23, c23 = f(l5.spec(_lib.UPCAT_SKIP_FIRST), x2, c2, x34, c34, l5.weight, l5.bias, s5, wphase=w5)
+        xo, co = f(l6.spec(_lib.UPCAT_UP_FIRST), x1, c1, x23, c23, l6.weight, l6.bias, s6, wphase=w6)
         xo, co = f(l7.spec(), xo, co, None, None, l7.weight, l7.bias, s7)
         return xo[:, :, 1:1 + out_h, 1:1 + out_w]
 

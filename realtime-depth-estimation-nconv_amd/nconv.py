@@ -177,8 +177,8 @@ class NConvLayerFn(torch.autograd.Function):
     """Autograd node of one fused NConv layer (glue + NConv2d.forward), kernels in libnconv."""
 
     @staticmethod
-    def forward(ctx, spec, xa, ca, xb, cb, weight, bias, wsum):
-        y, co = layer_forward_raw(spec, xa, ca, xb, cb, weight, bias, wsum)
+    def forward(ctx, spec, xa, ca, xb, cb, weight, bias, wsum, wphase=None):
+        y, co = layer_forward_raw(spec, xa, ca, xb, cb, weight, bias, wsum, wphase=wphase)
         ctx.spec = spec
         ctx.save_for_backward(xa, ca, xb, cb, weight, bias, wsum, y, co)
         return y, co
@@ -194,7 +194,7 @@ class NConvLayerFn(torch.autograd.Function):
         gw = torch.empty_like(weight) if need[5] else None
         gb = torch.empty_like(bias) if need[6] else None
         layer_backward(spec, (xa, ca, xb, cb, weight, bias, wsum), y, co, gy, gco, (gxa, gca, gxb, gcb), gw, gb)
-        return None, gxa, gca, gxb, gcb, gw, gb, None
+        return None, gxa, gca, gxb, gcb, gw, gb, None, None
 
 
 def layer_backward(spec: LayerSpec, inputs, y, co, gy, gco, gin, gw, gb, accumulate=False):
@@ -229,9 +229,10 @@ def kernel_plan(spec: LayerSpec, xa, ca, xb, cb, weight, bias, wsum):
     return tuple(_lib.KERNEL_NAMES[v.value] for v in out)
 
 
-def nconv_layer(spec: LayerSpec, xa, ca, xb, cb, weight, bias, wsum):
-    """Differentiable fused layer. Inputs must be contiguous fp32 device tensors."""
-    return NConvLayerFn.apply(spec, xa, ca, xb, cb, weight, bias, wsum)
+def nconv_layer(spec: LayerSpec, xa, ca, xb, cb, weight, bias, wsum, wphase=None):
+    """Differentiable fused layer. Inputs must be contiguous fp32 device tensors. `wphase`: the
+    layer's phase weights (UPCAT layers, phase_weights; no gradient flows through them), or None."""
+    return NConvLayerFn.apply(spec, xa, ca, xb, cb, weight, bias, wsum, wphase)
 
 
 # ------------------------------------------------------------------------------------------------

@@ -14,7 +14,7 @@ if [ -n "$2" ]; then
   tail -1 gpurun_out/ab_fwd_pytest.log | tee -a $out
 fi
 for v in $1; do
-  for l in nconv1 nconv2 down1 down2 down3 nconv4 nconv5 tail; do
+  for l in ${LAYERS:-nconv1 nconv2 down1 down2 down3 nconv4 nconv5 tail}; do
     NCONV_LIB=_exp/$v/libnconv.so timeout -k 10 120 python -u tools/fwd_layer_bench.py $l 30 2>/dev/null | sed "s/^/$v /" >> $out || stop $v-$l $?
   done
   NCONV_LIB=_exp/$v/libnconv.so timeout -k 10 300 python -u bench.py --no-train --alt-math '' --no-config5 --no-guided \

@@ -9,10 +9,14 @@ on gfx950 FETCH_SIZE reports half of a wide coalesced read, so it is doubled):
            python3 tools/pmc_traffic.py run
        rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- \\
            python3 tools/pmc_traffic.py run
-  2. anywhere: python3 tools/pmc_traffic.py parse gpurun_out/pmc_fetch gpurun_out/pmc_write
-     -> profiles/pmc_traffic.json  {config: [B,H,W], kernels: {name: {hbm_bytes_per_launch, ...}}}
+  2. anywhere: python3 tools/pmc_traffic.py parse gpurun_out/pmc_fetch gpurun_out/pmc_write [MATH] [REV]
+     -> profiles/pmc_traffic.json  {config: [B,H,W], kernels: {MATH: {name: {hbm_bytes_per_launch, ...}}}}
 
-FETCH_SIZE / WRITE_SIZE are in KiB. hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.
+FETCH_SIZE / WRITE_SIZE are in KiB. The guide's factor 2 on FETCH_SIZE is calibrated for 16-byte
+per-lane reads; the NConv kernels stage with 4-byte buffer loads, so the run also times a
+calibration launch of known bytes in the same access pattern (a 1x1 8 -> 1 NConv layer over B=8
+352x1216 fresh planes: reads 64 B and writes 8 B per pixel, no reuse) and the parse scales every
+kernel's counters by that launch's measured/algorithmic ratios (reported beside the raw counts).
 """
 import csv
 import glob
@@ -44,7 +48,18 @@ def run():
     with torch.no_grad():
         for _ in range(REPS):
             net(S)
+        # calibration: known bytes, the forward kernels' staging loads (4 B per lane) and stores
+        spec = m.LayerSpec(8, 1, (1, 1))
+        w = torch.rand(1, 8, 1, 1, device=dev) + 0.1
+        bias = torch.zeros(1, device=dev)
+        wsum = w.sum((1, 2, 3)).contiguous()
+        for _ in range(REPS):
+            x, c = torch.rand(B, 8, H, W, device=dev), torch.rand(B, 8, H, W, device=dev)
+            m.nconv.layer_forward_raw(spec, x, c, None, None, w, bias, wsum)
     torch.cuda.synchronize()
+
+
+CALIB_READ, CALIB_WRITE = B * H * W * 16 * 4, B * H * W * 2 * 4  # bytes per calibration launch
 
 
 ORDER = ["nconv1+nconv2_head", "nconv_down1", "nconv_down2", "nconv_down3", "nconv4", "nconv5", "nconv6+7_tail"]
@@ -61,12 +76,16 @@ def _read(dirpath, counter):
         raise SystemExit(f"no counter_collection.csv under {dirpath}")
     rows = [r for f in files for r in csv.DictReader(open(f)) if r["Counter_Name"] == counter]
     rows.sort(key=lambda r: int(r["Dispatch_Id"]))
-    groups, cur = [], None
+    groups, cur, calib = [], None, []
     for r in rows:
-        if "weight_prep" in r["Kernel_Name"]:
+        name = r["Kernel_Name"]
+        if "fwd_tiled<8, 1, 1," in name and int(r["Grid_Size"]) >= 1 << 20:
+            calib.append(float(r["Counter_Value"]))
+            cur = None
+        elif "weight_prep" in name:
             cur = []
             groups.append(cur)
-        elif cur is not None and ("nconv::" in r["Kernel_Name"]):
+        elif cur is not None and "nconv::" in name and "phase_weights" not in name:
             cur.append(r)
     per = defaultdict(list)
     for g in groups:
@@ -75,20 +94,32 @@ def _read(dirpath, counter):
             continue
         for name, r in zip(order, g):
             per[name].append(float(r["Counter_Value"]))
+    if calib:
+        per["_calibration"] = calib
     return {k: sum(v) / len(v) for k, v in per.items()}, {k: len(v) for k, v in per.items()}
 
 
-def parse(fetch_dir, write_dir):
+def parse(fetch_dir, write_dir, math="fp32", revision="unknown"):
     fetch, nf = _read(fetch_dir, "FETCH_SIZE")
     write, nw = _read(write_dir, "WRITE_SIZE")
+    fr = fw = None
+    if "_calibration" in fetch and "_calibration" in write:
+        fr = CALIB_READ / (fetch.pop("_calibration") * 1024)
+        fw = CALIB_WRITE / (write.pop("_calibration") * 1024)
     out = {"config": [B, H, W],
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over "
-                     "tools/pmc_traffic.py run; hbm_bytes = (2*FETCH_SIZE + WRITE_SIZE)*1024 "
-                     "(FETCH_SIZE doubled: gfx950 reports half of a wide coalesced read)",
-           "kernels": {}}
+                     "tools/pmc_traffic.py run (inference forwards, then a calibration launch of known "
+                     "bytes in the kernels' own access pattern: 4-byte staging loads, 8-byte stores); "
+                     "hbm_bytes = FETCH_SIZE*1024*read_scale + WRITE_SIZE*1024*write_scale with the "
+                     "scales measured on the calibration launch (without one: 2 and 1, the guide's "
+                     "16-byte-read correction)",
+           "calibration": {"read_scale": fr and round(fr, 4), "write_scale": fw and round(fw, 4),
+                           "read_bytes": CALIB_READ, "write_bytes": CALIB_WRITE},
+           "revision": revision, "math": math, "kernels": {math: {}}}
+    rs, ws = (fr, fw) if fr else (2.0, 1.0)
     for k in sorted(set(fetch) & set(write)):
-        out["kernels"][k] = {"fetch_kib": round(fetch[k], 1), "write_kib": round(write[k], 1),
-                             "hbm_bytes_per_launch": int((2 * fetch[k] + write[k]) * 1024),
+        out["kernels"][math][k] = {"fetch_kib": round(fetch[k], 1), "write_kib": round(write[k], 1),
+                             "hbm_bytes_per_launch": int((rs * fetch[k] + ws * write[k]) * 1024),
                              "dispatches": [nf[k], nw[k]]}
     dst = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     with open(dst, "w") as fh:
@@ -100,4 +131,4 @@ if __name__ == "__main__":
     if sys.argv[1] == "run":
         run()
     else:
-        parse(sys.argv[2], sys.argv[3])
+        parse(sys.argv[2], sys.argv[3], *sys.argv[4:6])
