@@ -141,10 +141,14 @@ def inference_calls(m, net, S):
     head = d._use_head(l1, l2)
     wph = d._phase_weights(S.device)
     w4, w5, w6 = (None, None, None) if wph is None else tuple(wph)
+    w21 = None
+    if head and m.nconv.FORWARD_MATH == lib.MATH_FP32:
+        w21 = m.nconv.head_weights(l1.spec(lib.THRESH, 0.01), l2.spec(), S, l1.weight, l1.bias, s1, l2.weight,
+                                   l2.bias, s2)
     with torch.no_grad():
         if head:
             x1b, c1b, p1, q1 = fhead(l1.spec(lib.THRESH, 0.01), l2.spec(), S, l1.weight, l1.bias, s1, l2.weight,
-                                     l2.bias, s2)
+                                     l2.bias, s2, w21)
         else:
             x1, c1 = fwd(l1.spec(lib.THRESH, 0.01), S, None, None, None, l1.weight, l1.bias, s1)
             x1b, c1b, p1, q1 = fpool(l2.spec(), x1, c1, None, None, l2.weight, l2.bias, s2)
@@ -155,7 +159,7 @@ def inference_calls(m, net, S):
         x23, c23 = fwd(l5.spec(lib.UPCAT_SKIP_FIRST), x2, c2, x34, c34, l5.weight, l5.bias, s5, wphase=w5)
     tail_out = torch.empty((S.shape[0], 1, oh, ow), device=S.device, dtype=torch.float32)
     first = {"nconv1+nconv2_head": lambda: fhead(l1.spec(lib.THRESH, 0.01), l2.spec(), S, l1.weight, l1.bias, s1,
-                                                 l2.weight, l2.bias, s2)} if head else {
+                                                 l2.weight, l2.bias, s2, w21)} if head else {
         "nconv1": lambda: fwd(l1.spec(lib.THRESH, 0.01), S, None, None, None, l1.weight, l1.bias, s1),
         "nconv2": lambda: fpool(l2.spec(), x1, c1, None, None, l2.weight, l2.bias, s2)}
     return {

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define NCONV_ABI_VERSION 15
+#define NCONV_ABI_VERSION 16
 
 /* How a layer's input (data x, confidence c) is produced from its source tensors. These are the
  * DNET glue ops fused into the layer's load stage (models/step1.py:53,61-90). */
@@ -61,7 +61,7 @@ enum nconv_kernel {
     NCONV_KERNEL_MFMA_BF16X9 = 4, /* bf16 matrix cores, three-part split, exact products (BF16X9)      */
     NCONV_KERNEL_TILED_FP32_PHASE = 5 /* as TILED_FP32, the nearest-2x-upsampled half of the input
                                      channels convolved at native resolution with phase weights
-                                     (nconv_layer.wphase, nconv_phase_weights)                     */
+                                     (nconv_layer.waux, nconv_phase_weights)                     */
 };
 
 /* One source tensor pair (data, confidence), physical shape (B, C, H, W). */
@@ -90,13 +90,15 @@ typedef struct nconv_layer {
                             gradient of the 3x3 / 5x5 layers with Cin > 1): 0 = NCONV_MATH_FP32
                             (exact products), BF16X3 / BF16X9 = split-bf16 matrix cores; unknown:
                             -EINVAL */
-    const float* wphase; /* optional (NULL = unused): phase weights of an UPCAT layer's upsampled
-                            channels, written by nconv_phase_weights. With exact-fp32 math, 16 -> 8
-                            channels (8 + 8), 3x3, stride 1 and an exact nearest 2x upsampling
-                            (H = 2 b.H, W = 2 b.W) the forward then convolves source b at its own
-                            resolution: 4 fp32 taps of summed weights instead of 9 per pixel (the
-                            regrouping (w1 + w2) * v of w1 * v + w2 * v, fp32 throughout); ignored
-                            otherwise */
+    const float* waux;   /* optional precomputed auxiliary weights (NULL = unused):
+                            - UPCAT layer: its phase weights (nconv_phase_weights). With exact-fp32
+                              math, 16 -> 8 channels (8 + 8), 3x3, stride 1 and an exact nearest 2x
+                              upsampling (H = 2 b.H, W = 2 b.W) the forward then convolves source b
+                              at its own resolution: 4 fp32 taps of summed weights instead of 9 per
+                              pixel (the regrouping (w1 + w2) * v of w1 * v + w2 * v); ignored
+                              otherwise;
+                            - nconv2 of nconv_fwd_head with exact-fp32 math: the composed
+                              confidence weights (nconv_head_weights), required there */
 } nconv_layer;
 
 /* ABI version, for the Python loader's sanity check. */
@@ -113,7 +115,7 @@ const char* nconv_last_error(void);
 int nconv_weight_prep(int n, float* const* weights, const int* couts, const int* fan_ins,
                       const int* apply_softplus, float* const* wsums, void* stream);
 
-/* Phase weights (nconv_layer.wphase) of n UPCAT layers with 8 output channels, 3x3 kernels and 8
+/* Phase weights (nconv_layer.waux) of n UPCAT layers with 8 output channels, 3x3 kernels and 8
  * nearest-2x-upsampled input channels, one launch; call after nconv_weight_prep (they are sums of
  * the current weights: 1, 2 or 4 fp32 weights each, in a fixed order). weights[i] is the layer's
  * (8, cins[i], 3, 3) weight, its upsampled channels are [up_first[i], up_first[i] + 8) (8 for
@@ -143,10 +145,21 @@ int nconv_fwd_pooled(const nconv_layer* L, float* y, float* cout, float* y_pool,
  * L1: Cin 1, Cout 8, 5x5, padding 2, NCONV_LOAD_THRESH) is evaluated while staging nconv2's input
  * tile (step1.py:58; L2: 8 -> 8, 5x5, padding 2, stride 1; its sources are not read), so nconv1's
  * 8-channel output never reaches HBM. Writes nconv2's y, cout (B, 8, H, W) and their 2x2 max-pooled
- * copies (B, 8, H/2, W/2) like nconv_fwd_pooled. Matrix-core math only (L2->math ==
- * NCONV_MATH_BF16X3 or NCONV_MATH_BF16X9, which nconv1 then uses as well); -EOPNOTSUPP otherwise. */
+ * copies (B, 8, H/2, W/2) like nconv_fwd_pooled. L2->math selects the arithmetic:
+ *  - NCONV_MATH_FP32: exact fp32 (nconv_fwd_head.hip). nconv1 visits only the nonzero taps of each
+ *    window (bitwise its dense sums); nconv2's confidence mass D2 is the 9x9 convolution of the
+ *    binary mask c0 with the composed weights sum_i W2[o,i] (x) W1[i] / s1[i] that L2->waux must
+ *    hold (nconv_head_weights), except in tiles whose window nconv2's zero padding truncates;
+ *  - NCONV_MATH_BF16X3 / BF16X9: the matrix-core head (nconv1 uses the same split). */
 int nconv_fwd_head(const nconv_layer* L1, const nconv_layer* L2, float* y, float* cout, float* y_pool,
                    float* cout_pool, void* stream);
+
+/* Composed confidence weights of the exact fused head (L2->waux of nconv_fwd_head): w21 receives
+ * 648 floats, w21[(qh * 8 + o) * 9 + qw] = sum_i (1 / s1[i]) sum W2[o][i][kh][kw] W1[i][kh'][kw'] over
+ * kh + kh' = qh, kw + kw' = qw (fp64, rounded once), s1 = L1->wsum. nconv1's cout = D1 / s1
+ * (models/step1.py:141-147), so nconv2's D2 = sum_i W2[o,i] * c1[i] = W21[o] * c0 wherever nconv2's
+ * window is not truncated by its zero padding. Call after nconv_weight_prep. */
+int nconv_head_weights(const nconv_layer* L1, const nconv_layer* L2, float* w21, void* stream);
 
 /* Inference-only fused tail: the last 3x3 NConv (nconv6, step1.py:88-90) with its 1x1 successor
  * (nconv7, step1.py:92) evaluated in the epilogue, written straight into the cropped output

@@ -13,7 +13,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # NCONV_LIB: an alternative build of the same library (kernel-tuning experiments)
 LIB_PATH = os.environ.get("NCONV_LIB") or os.path.join(_HERE, "libnconv.so")
-ABI_VERSION = 15
+ABI_VERSION = 16
 BWD_ACCUMULATE = 1
 
 # enum nconv_load_mode
@@ -35,6 +35,7 @@ EXPORTED = (
     "nconv_fwd_pooled",
     "nconv_fwd_tail",
     "nconv_fwd_head",
+    "nconv_head_weights",
     "nconv_plan",
     "nconv_phase_weights_floats",
     "nconv_phase_weights",
@@ -70,7 +71,7 @@ class NconvLayer(ctypes.Structure):
                 ("groups", ctypes.c_int), ("eps", ctypes.c_float), ("load_mode", ctypes.c_int),
                 ("thresh", ctypes.c_float), ("a", NconvSrc), ("b", NconvSrc),
                 ("weight", ctypes.c_void_p), ("bias", ctypes.c_void_p), ("wsum", ctypes.c_void_p),
-                ("math", ctypes.c_int), ("bwd_math", ctypes.c_int), ("wphase", ctypes.c_void_p)]
+                ("math", ctypes.c_int), ("bwd_math", ctypes.c_int), ("waux", ctypes.c_void_p)]
 
 
 class NconvDenseConv(ctypes.Structure):
@@ -115,6 +116,8 @@ def _declare(lib):
     lib.nconv_fwd_pooled.argtypes = [ctypes.POINTER(NconvLayer), P, P, P, P, P]
     lib.nconv_fwd_head.restype = ctypes.c_int
     lib.nconv_fwd_head.argtypes = [ctypes.POINTER(NconvLayer), ctypes.POINTER(NconvLayer), P, P, P, P, P]
+    lib.nconv_head_weights.restype = ctypes.c_int
+    lib.nconv_head_weights.argtypes = [ctypes.POINTER(NconvLayer), ctypes.POINTER(NconvLayer), P, P]
     lib.nconv_fwd_tail.restype = ctypes.c_int
     lib.nconv_fwd_tail.argtypes = [ctypes.POINTER(NconvLayer), P, P, P, ctypes.c_int, ctypes.c_int,
                                    ctypes.c_float, P, P, ctypes.c_int, ctypes.c_int, P]

@@ -154,8 +154,8 @@ int nconv_fwd_head(const nconv_layer* L1, const nconv_layer* L2, float* y, float
         return fail(-22, fn, "nconv2 geometry inconsistent with nconv1's output");
     if (L2->Ho < 2 || L2->Wo < 2) return fail(-22, fn, "output too small to pool");
     if (!L2->weight || !L2->bias || !L2->wsum) return fail(-22, fn, "null nconv2 weight/bias/wsum");
-    if (L2->math != NCONV_MATH_BF16X3 && L2->math != NCONV_MATH_BF16X9)
-        return fail(-95, fn, "the fused head runs on the matrix cores only");
+    const bool exact = L2->math == NCONV_MATH_FP32;
+    if (exact && !L2->waux) return fail(-22, fn, "exact-fp32 head needs nconv2's waux = nconv_head_weights output");
     nconv_layer l2 = *L2;
     l2.load_mode = NCONV_LOAD_PLAIN;
     l2.a = L1->a;  // (the kernel reads the sparse depth through TailArgs)
@@ -169,7 +169,20 @@ int nconv_fwd_head(const nconv_layer* L1, const nconv_layer* L2, float* y, float
     t.eps1 = L1->eps;
     t.thresh1 = L1->thresh;
     const char* why = nullptr;
-    int rc = nconv::launch_fwd_head(make_dev(&l2), t, y, cout, (hipStream_t)stream, &why);
+    int rc = exact ? nconv::launch_fwd_head_exact(make_dev(&l2), t, y, cout, (hipStream_t)stream, &why)
+                   : nconv::launch_fwd_head(make_dev(&l2), t, y, cout, (hipStream_t)stream, &why);
+    return rc ? fail(rc, fn, why) : 0;
+}
+
+int nconv_head_weights(const nconv_layer* L1, const nconv_layer* L2, float* w21, void* stream) {
+    const char* fn = "nconv_head_weights";
+    if (!L1 || !L2 || !w21) return fail(-22, fn, "null argument");
+    if (!L1->weight || !L1->wsum || !L2->weight) return fail(-22, fn, "null weight / wsum");
+    if (L1->Cin != 1 || L1->Cout != 8 || L1->KH != 5 || L1->KW != 5 || L2->Cin != 8 || L2->Cout != 8 ||
+        L2->KH != 5 || L2->KW != 5 || L1->groups != 1 || L2->groups != 1)
+        return fail(-95, fn, "nconv1 must be 1 -> 8 and nconv2 8 -> 8, both 5x5");
+    const char* why = nullptr;
+    int rc = nconv::launch_head_weights(L1->weight, L1->wsum, L2->weight, w21, (hipStream_t)stream, &why);
     return rc ? fail(rc, fn, why) : 0;
 }
 

@@ -130,7 +130,7 @@ __global__ __launch_bounds__(kPT) void fwd_phase(LayerDev d, float* __restrict__
     // jx + PAR .. jx + PAR + 1 (pixel 1); column phases beta0 = PAR, beta1 = 1 - PAR
     const f2* lowbase = &low[((ty + PAR) >> 1) * kPLP + jx];
     // phase weights: [i][alpha][dh][o][beta][dw] (nconv_phase_weights), 32 floats per (i, alpha, dh)
-    const cfloat* wph = (const cfloat*)L.wphase;
+    const cfloat* wph = (const cfloat*)L.waux;
     auto fma_up = [&](int cb, int bufi) {
         const f2* row = lowbase + bufi * kPLStride;
         const cfloat* wr = wph + ((size_t)cb * 2 + alpha) * 2 * 32;
@@ -289,7 +289,7 @@ __global__ __launch_bounds__(256) void phase_weights(PhaseArgs a) {
 bool fwd_phase_supported(const nconv_layer& L, bool tail) {
     (void)tail;
     const bool up = L.load_mode == NCONV_LOAD_UPCAT_SKIP_FIRST || L.load_mode == NCONV_LOAD_UPCAT_UP_FIRST;
-    if (!up || !L.wphase || L.math != NCONV_MATH_FP32) return false;
+    if (!up || !L.waux || L.math != NCONV_MATH_FP32) return false;
     if (L.Cin != 16 || L.Cout != 8 || L.a.C != 8 || L.b.C != 8 || L.KH != 3 || L.KW != 3) return false;
     if (L.SH != 1 || L.SW != 1 || L.DH != 1 || L.DW != 1 || L.groups != 1 || L.PH != L.PW) return false;
     return L.H == 2 * L.b.H && L.W == 2 * L.b.W;

@@ -53,6 +53,11 @@ int launch_phase_weights(int n, const float* const* w, const int* cin, const int
 int plan_fwd(const nconv_layer& L);
 void plan_bwd(const nconv_layer& L, int* dgrad, int* wgrad);
 int launch_fwd_head(const LayerDev& d2, const TailArgs& t, float* y, float* yc, hipStream_t st, const char** why);
+// exact-fp32 fused head (nconv_fwd_head.hip); d2.L.waux = the composed confidence weights
+int launch_fwd_head_exact(const LayerDev& d2, const TailArgs& t, float* y, float* yc, hipStream_t st,
+                          const char** why);
+int launch_head_weights(const float* w1, const float* s1, const float* w2, float* out, hipStream_t st,
+                        const char** why);
 int launch_fwd_tail(const LayerDev& d, const TailArgs& t, float* out, hipStream_t st, const char** why);
 int launch_weight_prep(int n, float* const* w, const int* cout, const int* fan_in, const int* sp,
                        float* const* s, hipStream_t st, const char** why);

@@ -22,7 +22,7 @@ import torch
 import torch.nn as nn
 
 from . import _lib, export, nconv
-from .nconv import (EnforcePos, NConv2d, _require_device, layer_backward, layer_forward_head,
+from .nconv import (EnforcePos, NConv2d, _require_device, head_weights, layer_backward, layer_forward_head,
                     layer_forward_pooled, layer_forward_raw, nconv_layer, phase_weights, weight_prep)
 
 LAYERS = ("nconv1", "nconv2", "nconv_down1", "nconv_down2", "nconv_down3", "nconv4", "nconv5",
@@ -284,8 +284,11 @@ class DNET(nn.Module):
         f, fp = layer_forward_raw, layer_forward_pooled
         if self._use_head(l1, l2):
             # nconv1 inside nconv2's staging: its 8-channel output never reaches HBM
-            x1, c1, p1, q1 = layer_forward_head(l1.spec(_lib.THRESH, 0.01), l2.spec(), S, l1.weight, l1.bias, s1,
-                                                l2.weight, l2.bias, s2)
+            sp1, sp2 = l1.spec(_lib.THRESH, 0.01), l2.spec()
+            w21 = None
+            if nconv.FORWARD_MATH == _lib.MATH_FP32:  # the exact head's composed confidence weights
+                w21 = head_weights(sp1, sp2, S, l1.weight, l1.bias, s1, l2.weight, l2.bias, s2)
+            x1, c1, p1, q1 = layer_forward_head(sp1, sp2, S, l1.weight, l1.bias, s1, l2.weight, l2.bias, s2, w21)
         else:
             x1, c1 = f(l1.spec(_lib.THRESH, 0.01), S, None, None, None, l1.weight, l1.bias, s1)
             x1, c1, p1, q1 = fp(l2.spec(), x1, c1, None, None, l2.weight, l2.bias, s2)
@@ -343,12 +346,13 @@ class DNET(nn.Module):
         return x3, c3, p3, q3, x4, c4, x34, c34
 
     # Inference evaluates nconv1 inside nconv2's kernel (nconv_fwd_head) when the layers have
-    # DNET's geometry; set False to run them as two launches.
+    # DNET's geometry -- in exact fp32 with nconv1 on the nonzero taps only and nconv2's confidence
+    # mass from composed weights (include/nconv.h nconv_fwd_head); set False to run them as two
+    # launches.
     fused_head = True
 
     def _use_head(self, l1, l2):
-        return self.fused_head and nconv.FORWARD_MATH in (_lib.MATH_BF16X3, _lib.MATH_BF16X9) and \
-            self._head_shapes(l1, l2)
+        return self.fused_head and self._head_shapes(l1, l2)
 
     @staticmethod
     def _head_shapes(l1, l2):

@@ -71,7 +71,7 @@ class LayerSpec:
         wo = (W + 2 * self.padding[1] - self.dilation[1] * (kw - 1) - 1) // self.stride[1] + 1
         return ho, wo
 
-    def descriptor(self, xa, ca, xb, cb, weight, bias, wsum, wphase=None):
+    def descriptor(self, xa, ca, xb, cb, weight, bias, wsum, waux=None):
         H, W = self.in_hw(xa.shape)
         Ho, Wo = self.out_hw(H, W)
         L = _lib.NconvLayer()
@@ -90,7 +90,7 @@ class LayerSpec:
         L.weight, L.bias, L.wsum = weight.data_ptr(), bias.data_ptr(), wsum.data_ptr()
         L.math = FORWARD_MATH
         L.bwd_math = BACKWARD_MATH
-        L.wphase = wphase.data_ptr() if wphase is not None else None
+        L.waux = waux.data_ptr() if waux is not None else None
         return L
 
 
@@ -157,11 +157,25 @@ def layer_forward_pooled(spec: LayerSpec, xa, ca, xb, cb, weight, bias, wsum, ou
     return y, co, py, pc
 
 
-def layer_forward_head(spec1: LayerSpec, spec2: LayerSpec, S, w1, b1, s1, w2, b2, s2):
-    """nconv_fwd_head: nconv2(nconv1(S)) with nconv1 evaluated inside nconv2's staging (its output
-    never reaches HBM); returns nconv2's (y, cout, maxpool2x2(y), maxpool2x2(cout)). No autograd."""
+def head_weights(spec1: LayerSpec, spec2: LayerSpec, S, w1, b1, s1, w2, b2, s2, out=None):
+    """nconv_head_weights: the exact fused head's composed confidence weights (648 floats,
+    sum_i W2[o,i] (x) W1[i] / s1[i]) from the current weights and nconv1's s[o]; one launch."""
     L1 = spec1.descriptor(S, None, None, None, w1, b1, s1)
-    L2 = spec2.descriptor(S, S, None, None, w2, b2, s2)  # geometry only: the kernel reads S via L1
+    L2 = spec2.descriptor(S, S, None, None, w2, b2, s2)
+    if out is None:
+        out = torch.empty(648, device=S.device, dtype=torch.float32)
+    rc = _lib.lib().nconv_head_weights(_lib.ctypes.byref(L1), _lib.ctypes.byref(L2), _lib.ptr(out),
+                                       _lib.stream_handle(S.device))
+    _lib.check(rc, "nconv_head_weights")
+    return out
+
+
+def layer_forward_head(spec1: LayerSpec, spec2: LayerSpec, S, w1, b1, s1, w2, b2, s2, w21=None):
+    """nconv_fwd_head: nconv2(nconv1(S)) with nconv1 evaluated inside nconv2's staging (its output
+    never reaches HBM); returns nconv2's (y, cout, maxpool2x2(y), maxpool2x2(cout)). No autograd.
+    With FORWARD_MATH == exact fp32 the composed weights `w21` (head_weights) are required."""
+    L1 = spec1.descriptor(S, None, None, None, w1, b1, s1)
+    L2 = spec2.descriptor(S, S, None, None, w2, b2, s2, w21)  # geometry only: the kernel reads S via L1
     B, H, W = S.shape[0], L1.Ho, L1.Wo
     y = torch.empty((B, 8, H, W), device=S.device, dtype=torch.float32)
     co = torch.empty_like(y)

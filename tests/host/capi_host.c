@@ -21,7 +21,7 @@ int main(void) {
     F(nconv_layer, a); F(nconv_layer, b); F(nconv_layer, weight); F(nconv_layer, bias); F(nconv_layer, wsum);
     F(nconv_layer, math);
     F(nconv_layer, bwd_math);
-    F(nconv_layer, wphase);
+    F(nconv_layer, waux);
     S(nconv_dense_conv);
     F(nconv_dense_conv, B); F(nconv_dense_conv, x0); F(nconv_dense_conv, C0); F(nconv_dense_conv, x1);
     F(nconv_dense_conv, C1); F(nconv_dense_conv, H); F(nconv_dense_conv, W); F(nconv_dense_conv, Cout);

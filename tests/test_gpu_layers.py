@@ -201,6 +201,41 @@ def test_fwd_pooled_outputs(nconv_amd, gpu, shape):
     assert torch.equal(pc, torch.nn.functional.max_pool2d(c1, 2, 2))
 
 
+@pytest.mark.parametrize("shape", [(2, 48, 128), (1, 37, 70), (3, 64, 96), (1, 352, 1216), (1, 20, 30)])
+def test_fwd_head_exact_matches_unfused(nconv_amd, gpu, shape):
+    """The exact-fp32 fused head (nconv1 on nonzero taps inside nconv2's tile, nconv2's N from
+    two-pixel packed FMAs, its D from the composed 9x9 weights on c0 away from the image edge)
+    against nconv1 and nconv2 as two exact launches: the edge tiles (here the top 16 rows) and every
+    NaN position agree bit for bit, the rest within D2's regrouping rounding (fp32, non-negative
+    terms); the pooled copies are torch's max_pool2d of the fused outputs exactly. The depth
+    carries NaN (not > thresh: c0 = 0, S * c0 = NaN) and negative values like the f4 fixture."""
+    B, H, W = shape
+    g = torch.Generator().manual_seed(H * W + 1)
+    S = (torch.rand(B, 1, H, W, generator=g) * 79 + 1) * (torch.rand(B, 1, H, W, generator=g) < 0.05)
+    S[torch.rand(B, 1, H, W, generator=g) < 0.002] = float("nan")
+    S[torch.rand(B, 1, H, W, generator=g) < 0.002] = -3.0
+    w1 = _gpu(rand_weight(g, 8, 1, 5, 5), gpu)
+    w2 = _gpu(rand_weight(g, 8, 8, 5, 5), gpu)
+    b1 = _gpu(torch.rand(8, generator=g) * 0.1, gpu)
+    b2 = _gpu(torch.rand(8, generator=g) * 0.1, gpu)
+    s1, s2 = _wsum(nconv_amd, w1), _wsum(nconv_amd, w2)
+    sp1 = nconv_amd.LayerSpec(1, 8, (5, 5), (1, 1), (2, 2), mode=THRESH)
+    sp2 = nconv_amd.LayerSpec(8, 8, (5, 5), (1, 1), (2, 2))
+    Sg = S.to(gpu)
+    N = nconv_amd.nconv
+    x1, c1 = N.layer_forward_raw(sp1, Sg, None, None, None, w1, b1, s1)
+    y0, c0, py0, pc0 = N.layer_forward_pooled(sp2, x1, c1, None, None, w2, b2, s2)
+    w21 = N.head_weights(sp1, sp2, Sg, w1, b1, s1, w2, b2, s2)
+    y1, c1f, py1, pc1 = N.layer_forward_head(sp1, sp2, Sg, w1, b1, s1, w2, b2, s2, w21)
+    torch.cuda.synchronize()
+    for got, ref in ((y1, y0), (c1f, c0)):
+        assert torch.equal(torch.isnan(got), torch.isnan(ref))
+        assert torch.equal(got[:, :, :16].nan_to_num(7.0), ref[:, :, :16].nan_to_num(7.0))  # edge tiles
+        torch.testing.assert_close(got.nan_to_num(7.0), ref.nan_to_num(7.0), rtol=1e-5, atol=1e-6)
+    assert torch.equal(py1.nan_to_num(7.0), torch.nn.functional.max_pool2d(y1, 2, 2).nan_to_num(7.0))
+    assert torch.equal(pc1, torch.nn.functional.max_pool2d(c1f, 2, 2))
+
+
 @pytest.mark.parametrize("shape", [(2, 48, 128), (1, 37, 70), (1, 352, 1216)])
 def test_fwd_head_matches_unfused(nconv_amd, gpu, shape, monkeypatch):
     """nconv_fwd_head (nconv1 evaluated inside nconv2's staging, on the matrix cores in the same

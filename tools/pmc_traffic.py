@@ -85,7 +85,7 @@ def _read(dirpath, counter):
         elif "weight_prep" in name:
             cur = []
             groups.append(cur)
-        elif cur is not None and "nconv::" in name and "phase_weights" not in name:
+        elif cur is not None and "nconv::" in name and "phase_weights" not in name and "head_weights" not in name:
             cur.append(r)
     per = defaultdict(list)
     for g in groups:
