@@ -154,9 +154,10 @@ int nconv_fwd_pooled(const nconv_layer* L, float* y, float* cout, float* y_pool,
 int nconv_fwd_head(const nconv_layer* L1, const nconv_layer* L2, float* y, float* cout, float* y_pool,
                    float* cout_pool, void* stream);
 
-/* Composed confidence weights of the exact fused head (L2->waux of nconv_fwd_head): w21 receives
- * 648 floats, w21[(qh * 8 + o) * 9 + qw] = sum_i (1 / s1[i]) sum W2[o][i][kh][kw] W1[i][kh'][kw'] over
- * kh + kh' = qh, kw + kw' = qw (fp64, rounded once), s1 = L1->wsum. nconv1's cout = D1 / s1
+/* Auxiliary weights of the exact fused head (L2->waux of nconv_fwd_head): w21 receives 2248 floats,
+ * the composed confidence weights w21[(qh * 8 + o) * 9 + qw] = sum_i (1 / s1[i]) sum
+ * W2[o][i][kh][kw] W1[i][kh'][kw'] over kh + kh' = qh, kw + kw' = qw (fp64, rounded once; s1 =
+ * L1->wsum), then nconv2's weights transposed to [i][kh][kw][o] (1600 floats). nconv1's cout = D1 / s1
  * (models/step1.py:141-147), so nconv2's D2 = sum_i W2[o,i] * c1[i] = W21[o] * c0 wherever nconv2's
  * window is not truncated by its zero padding. Call after nconv_weight_prep. */
 int nconv_head_weights(const nconv_layer* L1, const nconv_layer* L2, float* w21, void* stream);

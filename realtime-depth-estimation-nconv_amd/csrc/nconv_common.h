@@ -46,6 +46,19 @@ __device__ __forceinline__ float pool4v(float v0, float v1, float v2, float v3) 
     return pool4(v0, v1, v2, v3, a);
 }
 
+// Cross-lane reads without the LDS crossbar (ds_bpermute): xor 1 by a DPP quad permutation,
+// xor 16 by v_permlane16_swap (gfx950; swapping a copy of v with itself gives rows {1,0,3,2} in
+// one of the two results depending on the row's parity), xor 17 as both.
+__device__ __forceinline__ float shfl_xor1(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float shfl_xor16(float v) {
+    const int iv = __builtin_bit_cast(int, v);
+    const auto r = __builtin_amdgcn_permlane16_swap(iv, iv, false, false);
+    return __builtin_bit_cast(float, ((threadIdx.x >> 4) & 1) ? r[0] : r[1]);
+}
+__device__ __forceinline__ float shfl_xor17(float v) { return shfl_xor1(shfl_xor16(v)); }
+
 __device__ __forceinline__ size_t plane_idx(int b, int c, int C, int H, int W, int h, int w) {
     return (((size_t)b * C + c) * H + h) * (size_t)W + w;
 }

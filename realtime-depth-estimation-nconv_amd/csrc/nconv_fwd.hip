@@ -189,15 +189,15 @@ __global__ __launch_bounds__(NTH) void fwd_tiled(LayerDev d, float* __restrict__
                 float yb[C::P], cb[C::P];
 #pragma unroll
                 for (int j = 0; j < C::P; ++j) {
-                    yb[j] = __shfl_xor(yv[j], 16);
-                    cb[j] = __shfl_xor(cv[j], 16);
+                    yb[j] = shfl_xor16(yv[j]);
+                    cb[j] = shfl_xor16(cv[j]);
                 }
                 const size_t pofs = ((size_t)b * COUT + o) * pplane;
                 const __amdgpu_buffer_rsrc_t rpy = plane_rsrc(t.py + pofs, ppbytes);
                 const __amdgpu_buffer_rsrc_t rpc = plane_rsrc(t.pc + pofs, ppbytes);
                 if constexpr (C::P == 1) {  // the window's right column sits in lane l^1
-                    const float ya = __shfl_xor(yv[0], 1), ca = __shfl_xor(cv[0], 1);
-                    const float yd = __shfl_xor(yb[0], 1), cd = __shfl_xor(cb[0], 1);
+                    const float ya = shfl_xor1(yv[0]), ca = shfl_xor1(cv[0]);
+                    const float yd = shfl_xor1(yb[0]), cd = shfl_xor1(cb[0]);
                     st_f32(rpy, po[0], pool4v(yv[0], ya, yb[0], yd));
                     st_f32(rpc, po[0], pool4v(cv[0], ca, cb[0], cd));
                 } else {

@@ -33,6 +33,7 @@ constexpr int kHH = kHTH + 4, kHW = kHTW + 4;     // nconv1 outputs nconv2 reads
 constexpr int kHP = kHW - 16;                     // halo pair slots per row: (c, c + 16), c < 20
 constexpr int kCP = kSW - 16;                     // mask pair slots per row: c < 24
 constexpr int kHPlane = kHH * kHP;                // f2 per halo pair plane
+constexpr int kW21 = 9 * 8 * 9;                   // composed weights, then W2 as [ci][kh][kw][o]
 
 typedef const float __attribute__((address_space(4))) cfloat;
 
@@ -41,7 +42,7 @@ __global__ __launch_bounds__(kHT) void fwd_head_exact(LayerDev d2, TailArgs t, f
     const nconv_layer& L = d2.L;  // nconv2 (8 -> 8, 5x5, padding 2); nconv1 through t
     __shared__ __attribute__((aligned(16))) f2 sxc[kSH * kSW];      // {S * c0, c0}
     __shared__ __attribute__((aligned(16))) f2 c0p[kSH * kCP];      // {c0(c), c0(c + 16)}
-    __shared__ __attribute__((aligned(16))) f2 hp[8 * kHPlane];     // {x1c1(c), x1c1(c + 16)} / c1
+    __shared__ __attribute__((aligned(16))) f2 hp[8 * kHPlane + 1]; // {x1c1(c), x1c1(c + 16)} / c1; + dump
     __shared__ __attribute__((aligned(16))) float w1t[25 * 8];      // nconv1 weights [tap][o]
     __shared__ unsigned long long rowmask[kSH];
     const int tid = threadIdx.x;
@@ -82,6 +83,7 @@ __global__ __launch_bounds__(kHT) void fwd_head_exact(LayerDev d2, TailArgs t, f
     // ---- nconv1 on the 20 x 36 halo (origin R0 - 2, C0 - 2), nonzero taps only ----
     constexpr int NH = (kHH * kHW + kHT - 1) / kHT;  // 3 halo pixels per thread (the last partly)
     float c1keep[NH][8];                              // c1 of the thread's halo pixels (edge tiles)
+    int hofs[NH][2];                                  // their pair-plane float offsets
 #pragma unroll
     for (int k = 0; k < NH; ++k) {
         const int e = tid + kHT * k;
@@ -93,7 +95,11 @@ __global__ __launch_bounds__(kHT) void fwd_head_exact(LayerDev d2, TailArgs t, f
 #pragma unroll
         for (int o = 0; o < 8; ++o) acc[o] = (f2){0.f, 0.f};
         unsigned m = 0;
+#ifdef NCONV_HEAD_PROBE_NO_N1  // timing probe only (wrong results): no nconv1 taps
+        if (false) {
+#else
         if (in) {
+#endif
 #pragma unroll
             for (int kh = 0; kh < 5; ++kh) m |= (unsigned)((rowmask[r + kh] >> c) & 31ull) << (5 * kh);
         }
@@ -107,17 +113,22 @@ __global__ __launch_bounds__(kHT) void fwd_head_exact(LayerDev d2, TailArgs t, f
 #pragma unroll
             for (int o = 0; o < 8; ++o) acc[o] = __builtin_elementwise_fma((f2){wv[o], wv[o]}, v, acc[o]);
         }
+        // float offsets of this pixel in a pair plane (as .x of pair c, .y of pair c - 16), or the
+        // dump slot: every lane stores, no branches
+        const int dump = 8 * kHPlane * 2;
+        hofs[k][0] = (valid && c < kHP) ? (r * kHP + c) * 2 : dump;
+        hofs[k][1] = (valid && c >= 16) ? (r * kHP + c - 16) * 2 + 1 : dump;
 #pragma unroll
         for (int o = 0; o < 8; ++o) {
-            float y1 = 0.f, cc1 = 0.f;
-            if (in) nconv_epilogue(acc[o].x, acc[o].y, t.eps1, t.b1[o], t.s1[o], y1, cc1);
+            float y1, cc1;
+            nconv_epilogue(acc[o].x, acc[o].y, t.eps1, t.b1[o], t.s1[o], y1, cc1);
+            y1 = in ? y1 : 0.f;  // nconv2's zero padding outside the image
+            cc1 = in ? cc1 : 0.f;
             c1keep[k][o] = cc1;
-            if (valid) {
-                float* pl = reinterpret_cast<float*>(hp + o * kHPlane);
-                const float xc1 = y1 * cc1;  // nconv2's staged x * c
-                if (c < kHP) pl[(r * kHP + c) * 2] = xc1;
-                if (c >= 16) pl[(r * kHP + c - 16) * 2 + 1] = xc1;
-            }
+            float* pl = reinterpret_cast<float*>(hp + o * kHPlane);
+            const float xc1 = y1 * cc1;  // nconv2's staged x * c
+            pl[hofs[k][0] - (hofs[k][0] == dump ? o * kHPlane * 2 : 0)] = xc1;
+            pl[hofs[k][1] - (hofs[k][1] == dump ? o * kHPlane * 2 : 0)] = xc1;
         }
     }
     __syncthreads();
@@ -127,15 +138,17 @@ __global__ __launch_bounds__(kHT) void fwd_head_exact(LayerDev d2, TailArgs t, f
     f2 accN[8], accD[8];
 #pragma unroll
     for (int o = 0; o < 8; ++o) accN[o] = accD[o] = (f2){0.f, 0.f};
-    const float* __restrict__ w2 = L.weight;
+    // nconv2's weights transposed to [ci][kh][kw][o] (nconv_head_weights, after W21): one kernel
+    // row's 40 weights are contiguous -- three scalar loads instead of sixteen
+    const cfloat* w2t = (const cfloat*)L.waux + kW21;
     // N2 (or, for edge tiles, D2 from c1) over the 8 halo pair planes: {N(p), N(p+16)} += w * pair
     auto sum_planes = [&](f2 (&acc)[8]) {
 #pragma unroll 1
         for (int ci = 0; ci < 8; ++ci) {
             const f2* row = hp + ci * kHPlane + ty * kHP + j;
-            const float* wr = w2 + ci * 25;
+            const cfloat* wr = w2t + ci * 200;
 #pragma unroll 1
-            for (int kh = 0; kh < 5; ++kh, row += kHP, wr += 5) {
+            for (int kh = 0; kh < 5; ++kh, row += kHP, wr += 40) {
                 f2 v[5];
 #pragma unroll
                 for (int kw = 0; kw < 5; ++kw) v[kw] = row[kw];
@@ -143,17 +156,25 @@ __global__ __launch_bounds__(kHT) void fwd_head_exact(LayerDev d2, TailArgs t, f
                 for (int kw = 0; kw < 5; ++kw)
 #pragma unroll
                     for (int o = 0; o < 8; ++o) {
-                        const float wv = wr[o * 200 + kw];
+                        const float wv = wr[kw * 8 + o];
                         acc[o] = __builtin_elementwise_fma((f2){wv, wv}, v[kw], acc[o]);
                     }
             }
         }
     };
+#ifndef NCONV_HEAD_PROBE_NO_N2  // timing probe only (wrong results): no nconv2 data sums
     sum_planes(accN);
+#endif
     const bool interior = R0 >= 2 && R0 + kHTH + 2 <= H && C0 >= 2 && C0 + kHTW + 2 <= W;
+#ifdef NCONV_HEAD_PROBE_NO_D2  // timing probe only (wrong results): no confidence sums
+    if (true) {
+    } else if (interior) {
+#else
     if (interior) {
+#endif
         // D2 = W21 * c0 over the 9 x 9 window (mask tile origin R0 - 4 = output row - 4)
         const cfloat* w21 = (const cfloat*)L.waux;  // [qh][o][qw]
+        // (each row in two steps of <= 5 taps: 40 weights in SGPRs at a time, as nconv2's rows)
 #pragma unroll 1
         for (int qh = 0; qh < 9; ++qh) {
             const f2* row = c0p + (ty + qh) * kCP + j;
@@ -162,7 +183,15 @@ __global__ __launch_bounds__(kHT) void fwd_head_exact(LayerDev d2, TailArgs t, f
 #pragma unroll
             for (int qw = 0; qw < 9; ++qw) v[qw] = row[qw];
 #pragma unroll
-            for (int qw = 0; qw < 9; ++qw)
+            for (int qw = 0; qw < 5; ++qw)
+#pragma unroll
+                for (int o = 0; o < 8; ++o) {
+                    const float wv = wr[o * 9 + qw];
+                    accD[o] = __builtin_elementwise_fma((f2){wv, wv}, v[qw], accD[o]);
+                }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int qw = 5; qw < 9; ++qw)
 #pragma unroll
                 for (int o = 0; o < 8; ++o) {
                     const float wv = wr[o * 9 + qw];
@@ -172,19 +201,15 @@ __global__ __launch_bounds__(kHT) void fwd_head_exact(LayerDev d2, TailArgs t, f
     } else {
         // edge tile: nconv2's zero padding truncates the window -- sum W2 * c1 as the unfused path
         __syncthreads();  // every wave is done reading the x1c1 planes
+        const int dump = 8 * kHPlane * 2;
 #pragma unroll
-        for (int k = 0; k < NH; ++k) {
-            const int e = tid + kHT * k;
-            const int r = e / kHW, c = e - (e / kHW) * kHW;
-            if (e < kHH * kHW) {
+        for (int k = 0; k < NH; ++k)
 #pragma unroll
-                for (int o = 0; o < 8; ++o) {
-                    float* pl = reinterpret_cast<float*>(hp + o * kHPlane);
-                    if (c < kHP) pl[(r * kHP + c) * 2] = c1keep[k][o];
-                    if (c >= 16) pl[(r * kHP + c - 16) * 2 + 1] = c1keep[k][o];
-                }
+            for (int o = 0; o < 8; ++o) {
+                float* pl = reinterpret_cast<float*>(hp + o * kHPlane);
+                pl[hofs[k][0] - (hofs[k][0] == dump ? o * kHPlane * 2 : 0)] = c1keep[k][o];
+                pl[hofs[k][1] - (hofs[k][1] == dump ? o * kHPlane * 2 : 0)] = c1keep[k][o];
             }
-        }
         __syncthreads();
         sum_planes(accD);
     }
@@ -222,9 +247,12 @@ __global__ __launch_bounds__(kHT) void fwd_head_exact(LayerDev d2, TailArgs t, f
         for (int h = 0; h < 2; ++h) {
             st_f32(ry, so[h], yv[h]);
             st_f32(rc, so[h], cv[h]);
+#ifdef NCONV_HEAD_PROBE_NO_POOL  // timing probe only (wrong results): no pooled copies
+            continue;
+#endif
             // window (r, c) (r, c+1) (r+1, c) (r+1, c+1): lanes l, l^1, l^16, l^17 (torch order)
-            const float ya = __shfl_xor(yv[h], 1), yb = __shfl_xor(yv[h], 16), yd = __shfl_xor(yv[h], 17);
-            const float ca = __shfl_xor(cv[h], 1), cb = __shfl_xor(cv[h], 16), cd = __shfl_xor(cv[h], 17);
+            const float yb = shfl_xor16(yv[h]), cb = shfl_xor16(cv[h]);
+            const float ya = shfl_xor1(yv[h]), yd = shfl_xor1(yb), ca = shfl_xor1(cv[h]), cd = shfl_xor1(cb);
             st_f32(rpy, po[h], pool4v(yv[h], ya, yb, yd));
             st_f32(rpc, po[h], pool4v(cv[h], ca, cb, cd));
         }
@@ -252,6 +280,10 @@ __global__ __launch_bounds__(256) void head_weights(const float* __restrict__ w1
             acc += si / (double)s1[i];
         }
         out[e] = (float)acc;
+    }
+    for (int e = threadIdx.x; e < 1600; e += blockDim.x) {  // W2t[ci][kh][kw][o] = W2[o][ci][kh][kw]
+        const int o = e & 7, kk = (e >> 3) % 25, ci = e / 200;
+        out[kW21 + e] = w2[(o * 8 + ci) * 25 + kk];
     }
 }
 

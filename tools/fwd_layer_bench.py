@@ -41,7 +41,8 @@ def main():
         s1 = w1.sum((1, 2, 3)).contiguous()
         sp1 = m.LayerSpec(1, 8, (5, 5), (1, 1), (2, 2), mode=m._lib.THRESH)
         spec = m.LayerSpec(8, 8, (5, 5), (1, 1), (2, 2))
-        fn = lambda: N.layer_forward_head(sp1, spec, S, w1, b, s1, w8, b, s8)
+        w21 = N.head_weights(sp1, spec, S, w1, b, s1, w8, b, s8) if N.FORWARD_MATH == m._lib.MATH_FP32 else None
+        fn = lambda: N.layer_forward_head(sp1, spec, S, w1, b, s1, w8, b, s8, w21)
     elif which in ("down1", "down2", "down3"):
         f = {"down1": 2, "down2": 4, "down3": 8}[which]
         x, c = r(B, 8, H // f, W // f) * 10, r(B, 8, H // f, W // f)
