@@ -214,16 +214,30 @@ def pmc_traffic(kernel, math, B, H, W):
 
 
 def roofline(layer_us, costs, math, B, H, W, issued_mfma=None):
-    """The roofline object of the dominant (longest) kernel of the forward."""
+    """The roofline object of the dominant (longest) kernel of the forward. Its bound is the roof
+    its arithmetic intensity (algorithmic flop per algorithmic byte) meets first:
+    above the fp32 ridge (157.3 TF/s / 8 TB/s = 19.7 flop/B) the compute roof -- "mfma", the dense
+    fp32 matrix peak of MI355X_MICROARCH.md, which the packed-FP32 vector ALU shares (the two peaks
+    are equal and do not add, tools/microbench/fp32_rates.hip) -- with achieved = the reference's
+    algorithmic fp32 flops per launch / the launch time; below it HBM. Both fractions are reported."""
     dom = max(layer_us, key=lambda n: layer_us[n])
     byt, fl = costs[dom]
     us = layer_us[dom]
     gbs = byt / (us * 1e-6) / 1e9
-    r = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-         "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(dom, math, B, H, W),
+    tfs = fl / (us * 1e-6) / 1e12
+    compute = fl / byt > FP32_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBS * 1e9)
+    r = {"bound": "mfma" if compute else "hbm",
+         "achieved": round(tfs, 2) if compute else round(gbs, 1),
+         "peak": FP32_PEAK_TFLOPS if compute else HBM_PEAK_GBS,
+         "unit": "TFLOP/s" if compute else "GB/s",
+         "frac": round(tfs / FP32_PEAK_TFLOPS, 4) if compute else round(gbs / HBM_PEAK_GBS, 4),
+         "traffic": pmc_traffic(dom, math, B, H, W),
          "kernel": dom, "kernel_us": round(us, 2), "algorithmic_bytes_per_launch": byt, "flops_per_launch": fl,
-         "useful_fp32_tflops": round(fl / (us * 1e-6) / 1e12, 2), "fp32_peak_tflops": FP32_PEAK_TFLOPS,
-         "fp32_frac": round(fl / (us * 1e-6) / 1e12 / FP32_PEAK_TFLOPS, 4)}
+         "arithmetic_intensity_flop_per_byte": round(fl / byt, 2),
+         "compute_roof": "fp32: packed FMA on the vector ALU (exact products); peak = the dense fp32 MFMA peak, "
+                         "which equals the vector peak" if math == "fp32" else f"{math} products on the bf16 matrix cores",
+         "hbm_achieved_gbs": round(gbs, 1), "hbm_frac": round(gbs / HBM_PEAK_GBS, 4),
+         "fp32_tflops": round(tfs, 2), "fp32_frac": round(tfs / FP32_PEAK_TFLOPS, 4)}
     if issued_mfma:
         r["mfma_issued_bf16_tflops"] = round(issued_mfma(dom) / (us * 1e-6) / 1e12, 2)
         r["mfma_bf16_dense_peak_tflops"] = MFMA_BF16_PEAK_TFLOPS
