@@ -261,30 +261,33 @@ __global__ __launch_bounds__(kHT) void fwd_head_exact(LayerDev d2, TailArgs t, f
 
 // W21[qh][o][qw] = sum_i (1 / s1[i]) sum_{kh + kh' = qh, kw + kw' = qw} W2[o][i][kh][kw] W1[i][kh'][kw']
 // in fp64, rounded once (s1 = nconv1's weight sums, as the forward's cout = D1 / s1 uses them).
-__global__ __launch_bounds__(256) void head_weights(const float* __restrict__ w1, const float* __restrict__ s1,
-                                                    const float* __restrict__ w2, float* __restrict__ out) {
-    for (int e = threadIdx.x; e < 9 * 8 * 9; e += blockDim.x) {
-        const int qh = e / 72, o = (e / 9) % 8, qw = e % 9;
-        double acc = 0.0;
-        for (int i = 0; i < 8; ++i) {
-            double si = 0.0;
-            for (int kh = 0; kh < 5; ++kh) {
-                const int kh1 = qh - kh;
-                if (kh1 < 0 || kh1 > 4) continue;
-                for (int kw = 0; kw < 5; ++kw) {
-                    const int kw1 = qw - kw;
-                    if (kw1 < 0 || kw1 > 4) continue;
-                    si += (double)w2[((o * 8 + i) * 5 + kh) * 5 + kw] * (double)w1[(i * 5 + kh1) * 5 + kw1];
-                }
-            }
-            acc += si / (double)s1[i];
+// One 64-lane block per (qh, qw): lane (o, i) forms channel i's term, the 8 terms of an output
+// are summed over lanes in a fixed butterfly order; block 81 writes W2 transposed to [i][kh][kw][o].
+__global__ __launch_bounds__(64) void head_weights(const float* __restrict__ w1, const float* __restrict__ s1,
+                                                   const float* __restrict__ w2, float* __restrict__ out) {
+    const int blk = blockIdx.x, lane = threadIdx.x;
+    if (blk == 81) {
+        for (int e = lane; e < 1600; e += 64) {  // W2t[ci][kh][kw][o] = W2[o][ci][kh][kw]
+            const int o = e & 7, kk = (e >> 3) % 25, ci = e / 200;
+            out[kW21 + e] = w2[(o * 8 + ci) * 25 + kk];
         }
-        out[e] = (float)acc;
+        return;
     }
-    for (int e = threadIdx.x; e < 1600; e += blockDim.x) {  // W2t[ci][kh][kw][o] = W2[o][ci][kh][kw]
-        const int o = e & 7, kk = (e >> 3) % 25, ci = e / 200;
-        out[kW21 + e] = w2[(o * 8 + ci) * 25 + kk];
+    const int qh = blk / 9, qw = blk % 9, o = lane >> 3, i = lane & 7;
+    double si = 0.0;
+    for (int kh = 0; kh < 5; ++kh) {
+        const int kh1 = qh - kh;
+        if (kh1 < 0 || kh1 > 4) continue;
+        for (int kw = 0; kw < 5; ++kw) {
+            const int kw1 = qw - kw;
+            if (kw1 < 0 || kw1 > 4) continue;
+            si += (double)w2[((o * 8 + i) * 5 + kh) * 5 + kw] * (double)w1[(i * 5 + kh1) * 5 + kw1];
+        }
     }
+    si /= (double)s1[i];
+#pragma unroll
+    for (int m = 1; m < 8; m <<= 1) si += __shfl_xor(si, m);
+    if (i == 0) out[(qh * 8 + o) * 9 + qw] = (float)si;
 }
 
 }  // namespace
@@ -304,7 +307,7 @@ int launch_fwd_head_exact(const LayerDev& d2, const TailArgs& t, float* y, float
 
 int launch_head_weights(const float* w1, const float* s1, const float* w2, float* out, hipStream_t st,
                         const char** why) {
-    hipLaunchKernelGGL(head_weights, dim3(1), dim3(256), 0, st, w1, s1, w2, out);
+    hipLaunchKernelGGL(head_weights, dim3(82), dim3(64), 0, st, w1, s1, w2, out);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         *why = hipGetErrorString(e);
