@@ -29,12 +29,11 @@
 
 namespace nconv {
 
+#ifndef NCONV_DENSE_TH32
+#define NCONV_DENSE_TH32 1  // row multiplier of the 32-output-channel tiles (2: 8-12 % slower)
+#endif
 constexpr int kDT = 256;
 constexpr int kCK = 8;  // input channels per staged chunk
-
-constexpr int round_mod64(int n, int target) {  // smallest m >= n with m % 64 == target
-    return n + (((target - n) % 64) + 64) % 64;
-}
 
 __host__ __device__ constexpr int dense_taps(int kind) {
     return kind == NCONV_DENSE_3X3 ? 9 : kind == NCONV_DENSE_1X1 ? 1 : kind == NCONV_DENSE_TRANSPOSED_4X4 ? 4 : 16;
@@ -54,15 +53,16 @@ struct DcCfg {
     static constexpr int KS = KIND == NCONV_DENSE_1X1 ? 1 : (KIND == NCONV_DENSE_CONV4X4_S2 ? 4 : 3);
     static constexpr int PAD = KIND == NCONV_DENSE_1X1 ? 0 : 1;
     // rows per wave: 4 (2 strided) with 32 output channels, 2 (1) with 64: 4 MFMAs per 4-5 LDS reads
-    static constexpr int TH = (SP == 1 ? 8 : 4) * (COUT == 32 ? 2 : 1), RW = TH / 4, TW = 32;
+    static constexpr int TH = (SP == 1 ? 8 : 4) * (COUT == 32 ? NCONV_DENSE_TH32 : 1), RW = TH / 4, TW = 32;
     static constexpr int PR = (TH - 1) * SP + KS, PC = (TW - 1) * SP + KS;
     static constexpr int ROW = PC;
-    // B reads: 32 lanes on the columns of one patch row, lane half kk on the channel plane:
-    // kk * PLANE must shift to the other 32 banks (stride 1) or the odd banks (stride 2)
-    static constexpr int PLANE = SP == 1 ? round_mod64(PR * ROW, 32) : ((PR * ROW) | 1);
+    // B reads (ds_read_b32): 32 lanes on the columns of one patch row form one bank group, lane
+    // half kk (the other group) the next channel plane, so the planes need no padding and the
+    // patch image is the linear element order: element e of the chunk lands at lds[e].
+    static constexpr int PLANE = PR * ROW;
     static constexpr int MT = COUT / 32;
     static constexpr int COP = COUT == 32 ? 32 : 96;      // A reads: kk * COP == 32 (mod 64)
-    static constexpr int W_OFF = kCK * PLANE;
+    static constexpr int W_OFF = (kCK * PLANE + 3) & ~3;  // 16-byte aligned weight rows
     static constexpr int WS_OFF = W_OFF + TAPS * kCK * COP;  // shortcut weights [ci][COP]
     static constexpr int LDS = WS_OFF + kCK * COP;
     static constexpr int NP = (kCK * PR * PC + kDT - 1) / kDT;        // patch elements per thread
@@ -96,20 +96,43 @@ __global__ __launch_bounds__(kDT) void dense_conv_mfma(nconv_dense_conv p, int n
     const int HW = p.H * p.W;
 
     // ---- staging: patch (8 channels x PR x PC, zero outside the image / past Cin) + weights ----
+    // Each thread's patch elements keep one byte offset each within a channel plane of the source
+    // (out-of-image elements: past the buffer's end, read as 0), computed once; a chunk's loads are
+    // buffer loads of that offset from a per-chunk resource (the chunk's first channel) -- no
+    // address arithmetic per chunk. Channels past Cin read past the resource's end (0) as well.
+    constexpr unsigned OOB = 0x80000000u;
+    unsigned poff[C::NP];
+#pragma unroll
+    for (int k = 0; k < C::NP; ++k) {
+        const int e = tid + kDT * k;
+        const int ci = e / (C::PR * C::PC), rem = e - ci * (C::PR * C::PC);
+        const int r = rem / C::PC, c = rem - r * C::PC;
+        const int iy = iy0 + r, ix = ix0 + c;
+        const bool in = e < kCK * C::PR * C::PC && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
+        poff[k] = in ? (unsigned)(ci * HW + iy * p.W + ix) * 4u : OOB;
+    }
+    const int bytes0 = p.C0 * HW * 4, bytes1 = p.C1 * HW * 4;
     float pv[C::NP];
     f4 wv[C::NW4], sv[C::NS4];
     auto load_chunk = [&](int ch) {
+        const int g0 = ch * kCK;  // first channel of the chunk
+        if (g0 + kCK <= p.C0 || g0 >= p.C0) {  // one source (uniform)
+            const bool a = g0 < p.C0;
+            const __amdgpu_buffer_rsrc_t rs =
+                a ? plane_rsrc(p.x0 + ((size_t)b * p.C0 + g0) * HW, bytes0 - g0 * HW * 4)
+                  : plane_rsrc(p.x1 + ((size_t)b * p.C1 + (g0 - p.C0)) * HW, bytes1 - (g0 - p.C0) * HW * 4);
 #pragma unroll
-        for (int k = 0; k < C::NP; ++k) {
-            const int e = tid + kDT * k;
-            const int ci = e / (C::PR * C::PC), rem = e - ci * (C::PR * C::PC);
-            const int r = rem / C::PC, c = rem - r * C::PC;
-            const int gc = ch * kCK + ci, iy = iy0 + r, ix = ix0 + c;
-            const bool in = e < kCK * C::PR * C::PC && gc < Cin && (unsigned)iy < (unsigned)p.H &&
-                            (unsigned)ix < (unsigned)p.W;
-            const float* src = gc < p.C0 ? p.x0 + ((size_t)b * p.C0 + gc) * HW
-                                         : p.x1 + ((size_t)b * p.C1 + (gc - p.C0)) * HW;
-            pv[k] = in ? src[iy * p.W + ix] : 0.f;
+            for (int k = 0; k < C::NP; ++k) pv[k] = ld_f32(rs, poff[k]);
+        } else {  // the chunk straddles the two sources: both loads, the wrong one out of range
+            const __amdgpu_buffer_rsrc_t r0 = plane_rsrc(p.x0 + ((size_t)b * p.C0 + g0) * HW, bytes0 - g0 * HW * 4);
+            const __amdgpu_buffer_rsrc_t r1 = plane_rsrc(p.x1 + (size_t)b * p.C1 * HW, bytes1);
+            const unsigned shift = (unsigned)(p.C0 - g0) * HW * 4u;  // x1's channel 0 in chunk offsets
+#pragma unroll
+            for (int k = 0; k < C::NP; ++k) {
+                const bool in1 = poff[k] != OOB && poff[k] >= shift;
+                const float v0 = ld_f32(r0, poff[k]), v1 = ld_f32(r1, in1 ? poff[k] - shift : OOB);
+                pv[k] = in1 ? v1 : v0;
+            }
         }
         const f4* wg = reinterpret_cast<const f4*>(
             p.wpack + (((size_t)cls * ncot + cot) * nchunk + ch) * C::TAPS * kCK * COUT);
@@ -131,11 +154,7 @@ __global__ __launch_bounds__(kDT) void dense_conv_mfma(nconv_dense_conv p, int n
 #pragma unroll
         for (int k = 0; k < C::NP; ++k) {
             const int e = tid + kDT * k;
-            if (e < kCK * C::PR * C::PC) {
-                const int ci = e / (C::PR * C::PC), rem = e - ci * (C::PR * C::PC);
-                const int r = rem / C::PC, c = rem - r * C::PC;
-                lds[ci * C::PLANE + r * C::ROW + c] = pv[k];
-            }
+            if (e < kCK * C::PR * C::PC) lds[e] = pv[k];
         }
 #pragma unroll
         for (int k = 0; k < C::NW4; ++k) {
@@ -217,25 +236,33 @@ __global__ __launch_bounds__(kDT) void dense_conv_mfma(nconv_dense_conv p, int n
     }
 
     // ---- epilogue: bias, ReLU, shortcut; C[row = co][col = pixel]: col = lane & 31,
-    //      row = (q & 3) + 8 (q >> 2) + 4 (lane >> 5) for register q ----
+    //      row = (q & 3) + 8 (q >> 2) + 4 (lane >> 5) for register q. Stores through one
+    //      resource over the image's output channel range: the lane's byte offset (its pixel and
+    //      lane-half channel) once, each register's channel offset a uniform soffset; pixels and
+    //      channels outside the output are dropped by the range check ----
     const int Hc = C::TR ? p.H : p.Ho, Wc = C::TR ? p.W : p.Wo;  // (class) grid
     const int ox = ox0 + li;
+    const int HWo = p.Ho * p.Wo;
+    const int co0 = cot * COUT;  // first output channel of this tile
+    const int nco = p.Cout - co0 < COUT ? p.Cout - co0 : COUT;
+    const __amdgpu_buffer_rsrc_t ro =
+        plane_rsrc(p.out + ((size_t)b * p.out_C + p.out_c0 + co0) * HWo, nco * HWo * 4);
 #pragma unroll
     for (int r = 0; r < C::RW; ++r) {
         const int oy = oy0 + w * C::RW + r;
-        if (oy >= Hc || ox >= Wc) continue;
         const int oyo = C::TR ? 2 * oy + pa : oy, oxo = C::TR ? 2 * ox + pb : ox;
-        if (C::TR && (oyo >= p.Ho || oxo >= p.Wo)) continue;  // cropped transposed output
+        const bool in = oy < Hc && ox < Wc && oyo < p.Ho && oxo < p.Wo;  // (cropped transposed output)
+        const unsigned lo = in ? (unsigned)(4 * kk * HWo + oyo * p.Wo + oxo) * 4u : OOB;
 #pragma unroll
         for (int m = 0; m < C::MT; ++m)
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
-                const int co = cot * COUT + 32 * m + (q & 3) + 8 * (q >> 2) + 4 * kk;
-                if (co >= p.Cout) continue;
-                float v = acc[m][r][q] + (p.bias ? p.bias[co] : 0.f);
+                const int cr = 32 * m + (q & 3) + 8 * (q >> 2);  // channel in the tile, lane half 0
+                const int co = co0 + cr + 4 * kk;
+                float v = acc[m][r][q] + ((p.bias && co < p.Cout) ? p.bias[co] : 0.f);
                 if (p.relu) v = fmaxf(v, 0.f);
                 if constexpr (SC) v += acs[m][r][q];
-                p.out[(((size_t)b * p.out_C + p.out_c0 + co) * p.Ho + oyo) * p.Wo + oxo] = v;
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), ro, (int)lo, cr * HWo * 4, 0);
             }
     }
 }

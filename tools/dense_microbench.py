@@ -33,7 +33,11 @@ def main():
               ("fuse2 conv 128->64", 0, 1, 128, 64, 176, 608), ("fuse2 conv 64->64", 0, 1, 64, 64, 176, 608),
               ("enc1 3x3 s2 32->64", 0, 2, 32, 64, 352, 1216), ("fuse3 upf TR 33->32", 2, 2, 33, 32, 176, 608),
               ("fuse2 upf TR 65->64", 2, 2, 65, 64, 88, 304), ("dgrad TR: C4 32->33", 3, 2, 32, 33, 352, 1216)]
+    only = sys.argv[1].split(",") if len(sys.argv) > 1 else None  # name substrings
+    fwd_only = os.environ.get("DENSE_FWD_ONLY") == "1"
     for name, kind, s, cin, cout, H, W in shapes:
+        if only and not any(o in name for o in only):
+            continue
         x = torch.randn(B, cin, H, W, device=dev)
         k = 3 if kind == 0 else (4 if kind == 3 else 1)
         w = torch.randn(cin, cout, 4, 4, device=dev) if kind == 2 else torch.randn(cout, cin, k, k, device=dev)
@@ -44,7 +48,7 @@ def main():
         fl = 2 * cin * cout * taps * pix
         us = timeit(lambda: D.conv(x, kind, s, wp, None, False, cout, out=out))
         print(f"fwd   {name:24s} {us:9.1f} us {fl / us / 1e6:7.1f} TF/s", flush=True)
-        if kind in (0, 2):
+        if kind in (0, 2) and not fwd_only:
             g = torch.randn_like(out)
             us = timeit(lambda: D.wgrad(x, None, g, kind, s, w.shape))
             print(f"wgrad {name:24s} {us:9.1f} us {fl / us / 1e6:7.1f} TF/s", flush=True)
