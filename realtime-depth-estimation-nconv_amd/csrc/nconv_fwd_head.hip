@@ -40,15 +40,21 @@ typedef const float __attribute__((address_space(4))) cfloat;
 __global__ __launch_bounds__(kHT) void fwd_head_exact(LayerDev d2, TailArgs t, float* __restrict__ y,
                                                       float* __restrict__ yc) {
     const nconv_layer& L = d2.L;  // nconv2 (8 -> 8, 5x5, padding 2); nconv1 through t
-    __shared__ __attribute__((aligned(16))) f2 sxc[kSH * kSW];      // {S * c0, c0}
-    __shared__ __attribute__((aligned(16))) f2 c0p[kSH * kCP];      // {c0(c), c0(c + 16)}
-    __shared__ __attribute__((aligned(16))) f2 hp[8 * kHPlane + 1]; // {x1c1(c), x1c1(c + 16)} / c1; + dump
-    __shared__ __attribute__((aligned(16))) float w1t[25 * 8];      // nconv1 weights [tap][o]
+    // LDS (30.5 KB: five workgroups per CU): the depth tile's S * c0 (c0 = (S * c0 > thresh): S
+    // itself where S > thresh, NaN * 0 = NaN and +-0 otherwise), nconv1's weights, the nonzero
+    // masks, and one region holding first the mask pairs of the interior D2, then nconv1's
+    // x * c (or, in edge tiles, c) as 8 planes of column pairs
+    __shared__ __attribute__((aligned(16))) float sx[kSH * kSW];
+    __shared__ __attribute__((aligned(16))) f2 hp[8 * kHPlane + 1];  // + dump slot
+    __shared__ __attribute__((aligned(16))) float w1t[25 * 8];       // nconv1 weights [tap][o]
     __shared__ unsigned long long rowmask[kSH];
+    f2* const c0p = hp;  // {c0(c), c0(c + 16)}, kSH x kCP, until the interior D2 is done
+    static_assert(kSH * kCP <= 8 * kHPlane, "mask pairs fit the plane region");
     const int tid = threadIdx.x;
     const int H = L.Ho, W = L.Wo;
     const TileCoord tc = xcd_tile((W + kHTW - 1) / kHTW, (H + kHTH - 1) / kHTH, L.B);
     const int b = tc.b, R0 = tc.ty * kHTH, C0 = tc.tx * kHTW;
+    const bool interior = R0 >= 2 && R0 + kHTH + 2 <= H && C0 >= 2 && C0 + kHTW + 2 <= W;
 
     // ---- stage the depth tile (origin R0 - 4, C0 - 4), its nonzero masks and nconv1's weights ----
     if (tid < kSH) rowmask[tid] = 0ull;
@@ -71,64 +77,11 @@ __global__ __launch_bounds__(kHT) void fwd_head_exact(LayerDev d2, TailArgs t, f
             if (e < kSH * kSW) {
                 const float c0 = sv[k] > t.thresh1 ? 1.0f : 0.0f;  // step1.py:53
                 const float xc = sv[k] * c0;
-                sxc[e] = (f2){xc, c0};
+                sx[e] = xc;
                 if (c < kCP) reinterpret_cast<float*>(c0p)[(r * kCP + c) * 2] = c0;
                 if (c >= 16) reinterpret_cast<float*>(c0p)[(r * kCP + c - 16) * 2 + 1] = c0;
                 if (!(xc == 0.f && c0 == 0.f)) atomicOr(&rowmask[r], 1ull << c);  // NaN counts as nonzero
             }
-        }
-    }
-    __syncthreads();
-
-    // ---- nconv1 on the 20 x 36 halo (origin R0 - 2, C0 - 2), nonzero taps only ----
-    constexpr int NH = (kHH * kHW + kHT - 1) / kHT;  // 3 halo pixels per thread (the last partly)
-    float c1keep[NH][8];                              // c1 of the thread's halo pixels (edge tiles)
-    int hofs[NH][2];                                  // their pair-plane float offsets
-#pragma unroll
-    for (int k = 0; k < NH; ++k) {
-        const int e = tid + kHT * k;
-        const int r = e / kHW, c = e - (e / kHW) * kHW;
-        const int gr = R0 - 2 + r, gc = C0 - 2 + c;
-        const bool valid = e < kHH * kHW;
-        const bool in = valid && (unsigned)gr < (unsigned)H && (unsigned)gc < (unsigned)W;
-        f2 acc[8];
-#pragma unroll
-        for (int o = 0; o < 8; ++o) acc[o] = (f2){0.f, 0.f};
-        unsigned m = 0;
-#ifdef NCONV_HEAD_PROBE_NO_N1  // timing probe only (wrong results): no nconv1 taps
-        if (false) {
-#else
-        if (in) {
-#endif
-#pragma unroll
-            for (int kh = 0; kh < 5; ++kh) m |= (unsigned)((rowmask[r + kh] >> c) & 31ull) << (5 * kh);
-        }
-        while (m) {
-            const int tp = __builtin_ctz(m);
-            m &= m - 1;
-            const int kh = (tp * 13) >> 6, kw = tp - 5 * kh;  // tp / 5 for tp < 25
-            const f2 v = sxc[(r + kh) * kSW + c + kw];
-            const f4 wa = reinterpret_cast<const f4*>(w1t)[tp * 2], wb = reinterpret_cast<const f4*>(w1t)[tp * 2 + 1];
-            const float wv[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
-#pragma unroll
-            for (int o = 0; o < 8; ++o) acc[o] = __builtin_elementwise_fma((f2){wv[o], wv[o]}, v, acc[o]);
-        }
-        // float offsets of this pixel in a pair plane (as .x of pair c, .y of pair c - 16), or the
-        // dump slot: every lane stores, no branches
-        const int dump = 8 * kHPlane * 2;
-        hofs[k][0] = (valid && c < kHP) ? (r * kHP + c) * 2 : dump;
-        hofs[k][1] = (valid && c >= 16) ? (r * kHP + c - 16) * 2 + 1 : dump;
-#pragma unroll
-        for (int o = 0; o < 8; ++o) {
-            float y1, cc1;
-            nconv_epilogue(acc[o].x, acc[o].y, t.eps1, t.b1[o], t.s1[o], y1, cc1);
-            y1 = in ? y1 : 0.f;  // nconv2's zero padding outside the image
-            cc1 = in ? cc1 : 0.f;
-            c1keep[k][o] = cc1;
-            float* pl = reinterpret_cast<float*>(hp + o * kHPlane);
-            const float xc1 = y1 * cc1;  // nconv2's staged x * c
-            pl[hofs[k][0] - (hofs[k][0] == dump ? o * kHPlane * 2 : 0)] = xc1;
-            pl[hofs[k][1] - (hofs[k][1] == dump ? o * kHPlane * 2 : 0)] = xc1;
         }
     }
     __syncthreads();
@@ -138,6 +91,96 @@ __global__ __launch_bounds__(kHT) void fwd_head_exact(LayerDev d2, TailArgs t, f
     f2 accN[8], accD[8];
 #pragma unroll
     for (int o = 0; o < 8; ++o) accN[o] = accD[o] = (f2){0.f, 0.f};
+
+#ifdef NCONV_HEAD_PROBE_NO_D2  // timing probe only (wrong results): no interior confidence sums
+    if (false) {
+#else
+    if (interior) {
+#endif
+        // D2 = W21 * c0 over the 9 x 9 window (mask tile origin R0 - 4 = output row - 4); rows in
+        // two steps of <= 5 taps: 40 weights in SGPRs at a time, as nconv2's rows
+        const cfloat* w21 = (const cfloat*)L.waux;  // [qh][o][qw]
+#pragma unroll 1
+        for (int qh = 0; qh < 9; ++qh) {
+            const f2* row = c0p + (ty + qh) * kCP + j;
+            const cfloat* wr = w21 + qh * 72;
+            f2 v[9];
+#pragma unroll
+            for (int qw = 0; qw < 9; ++qw) v[qw] = row[qw];
+#pragma unroll
+            for (int qw = 0; qw < 5; ++qw)
+#pragma unroll
+                for (int o = 0; o < 8; ++o) {
+                    const float wv = wr[o * 9 + qw];
+                    accD[o] = __builtin_elementwise_fma((f2){wv, wv}, v[qw], accD[o]);
+                }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int qw = 5; qw < 9; ++qw)
+#pragma unroll
+                for (int o = 0; o < 8; ++o) {
+                    const float wv = wr[o * 9 + qw];
+                    accD[o] = __builtin_elementwise_fma((f2){wv, wv}, v[qw], accD[o]);
+                }
+        }
+    }
+    __syncthreads();  // the mask pairs are dead: the region becomes nconv1's planes
+
+    // ---- nconv1 on the 20 x 36 halo (origin R0 - 2, C0 - 2), nonzero taps only; writes x * c
+    //      (want_c false) or c (want_c true, edge tiles' second pass) into the pair planes ----
+    constexpr int NH = (kHH * kHW + kHT - 1) / kHT;  // 3 halo pixels per thread (the last partly)
+    auto nconv1_planes = [&](bool want_c) {
+#pragma unroll 1
+        for (int k = 0; k < NH; ++k) {
+            const int e = tid + kHT * k;
+            const int r = e / kHW, c = e - (e / kHW) * kHW;
+            const int gr = R0 - 2 + r, gc = C0 - 2 + c;
+            const bool valid = e < kHH * kHW;
+            const bool in = valid && (unsigned)gr < (unsigned)H && (unsigned)gc < (unsigned)W;
+            f2 acc[8];
+#pragma unroll
+            for (int o = 0; o < 8; ++o) acc[o] = (f2){0.f, 0.f};
+            unsigned m = 0;
+#ifdef NCONV_HEAD_PROBE_NO_N1  // timing probe only (wrong results): no nconv1 taps
+            if (false) {
+#else
+            if (in) {
+#endif
+#pragma unroll
+                for (int kh = 0; kh < 5; ++kh) m |= (unsigned)((rowmask[r + kh] >> c) & 31ull) << (5 * kh);
+            }
+            while (m) {
+                const int tp = __builtin_ctz(m);
+                m &= m - 1;
+                const int kh = (tp * 13) >> 6, kw = tp - 5 * kh;  // tp / 5 for tp < 25
+                const float xc = sx[(r + kh) * kSW + c + kw];
+                const f2 v = (f2){xc, xc > t.thresh1 ? 1.0f : 0.0f};  // {S * c0, c0}
+                const f4 wa = reinterpret_cast<const f4*>(w1t)[tp * 2], wb = reinterpret_cast<const f4*>(w1t)[tp * 2 + 1];
+                const float wv[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
+#pragma unroll
+                for (int o = 0; o < 8; ++o) acc[o] = __builtin_elementwise_fma((f2){wv[o], wv[o]}, v, acc[o]);
+            }
+            // float offsets of this pixel in a pair plane (.x of pair c, .y of pair c - 16), or
+            // the dump slot: every lane stores, no branches
+            const int dump = 8 * kHPlane * 2;
+            const int h0 = (valid && c < kHP) ? (r * kHP + c) * 2 : dump;
+            const int h1 = (valid && c >= 16) ? (r * kHP + c - 16) * 2 + 1 : dump;
+#pragma unroll
+            for (int o = 0; o < 8; ++o) {
+                float y1, cc1;
+                nconv_epilogue(acc[o].x, acc[o].y, t.eps1, t.b1[o], t.s1[o], y1, cc1);
+                y1 = in ? y1 : 0.f;  // nconv2's zero padding outside the image
+                cc1 = in ? cc1 : 0.f;
+                const float v = want_c ? cc1 : y1 * cc1;  // nconv2's staged x * c, or c
+                float* pl = reinterpret_cast<float*>(hp + o * kHPlane);
+                pl[h0 - (h0 == dump ? o * kHPlane * 2 : 0)] = v;
+                pl[h1 - (h1 == dump ? o * kHPlane * 2 : 0)] = v;
+            }
+        }
+    };
+    nconv1_planes(false);
+    __syncthreads();
+
     // nconv2's weights transposed to [ci][kh][kw][o] (nconv_head_weights, after W21): one kernel
     // row's 40 weights are contiguous -- three scalar loads instead of sixteen
     const cfloat* w2t = (const cfloat*)L.waux + kW21;
@@ -165,51 +208,11 @@ __global__ __launch_bounds__(kHT) void fwd_head_exact(LayerDev d2, TailArgs t, f
 #ifndef NCONV_HEAD_PROBE_NO_N2  // timing probe only (wrong results): no nconv2 data sums
     sum_planes(accN);
 #endif
-    const bool interior = R0 >= 2 && R0 + kHTH + 2 <= H && C0 >= 2 && C0 + kHTW + 2 <= W;
-#ifdef NCONV_HEAD_PROBE_NO_D2  // timing probe only (wrong results): no confidence sums
-    if (true) {
-    } else if (interior) {
-#else
-    if (interior) {
-#endif
-        // D2 = W21 * c0 over the 9 x 9 window (mask tile origin R0 - 4 = output row - 4)
-        const cfloat* w21 = (const cfloat*)L.waux;  // [qh][o][qw]
-        // (each row in two steps of <= 5 taps: 40 weights in SGPRs at a time, as nconv2's rows)
-#pragma unroll 1
-        for (int qh = 0; qh < 9; ++qh) {
-            const f2* row = c0p + (ty + qh) * kCP + j;
-            const cfloat* wr = w21 + qh * 72;
-            f2 v[9];
-#pragma unroll
-            for (int qw = 0; qw < 9; ++qw) v[qw] = row[qw];
-#pragma unroll
-            for (int qw = 0; qw < 5; ++qw)
-#pragma unroll
-                for (int o = 0; o < 8; ++o) {
-                    const float wv = wr[o * 9 + qw];
-                    accD[o] = __builtin_elementwise_fma((f2){wv, wv}, v[qw], accD[o]);
-                }
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int qw = 5; qw < 9; ++qw)
-#pragma unroll
-                for (int o = 0; o < 8; ++o) {
-                    const float wv = wr[o * 9 + qw];
-                    accD[o] = __builtin_elementwise_fma((f2){wv, wv}, v[qw], accD[o]);
-                }
-        }
-    } else {
-        // edge tile: nconv2's zero padding truncates the window -- sum W2 * c1 as the unfused path
-        __syncthreads();  // every wave is done reading the x1c1 planes
-        const int dump = 8 * kHPlane * 2;
-#pragma unroll
-        for (int k = 0; k < NH; ++k)
-#pragma unroll
-            for (int o = 0; o < 8; ++o) {
-                float* pl = reinterpret_cast<float*>(hp + o * kHPlane);
-                pl[hofs[k][0] - (hofs[k][0] == dump ? o * kHPlane * 2 : 0)] = c1keep[k][o];
-                pl[hofs[k][1] - (hofs[k][1] == dump ? o * kHPlane * 2 : 0)] = c1keep[k][o];
-            }
+    if (!interior) {
+        // edge tile: nconv2's zero padding truncates the window -- D2 = W2 * c1 as the unfused
+        // path, with c1 from a second nonzero-tap pass of nconv1 into the planes
+        __syncthreads();  // every wave is done reading the x * c planes
+        nconv1_planes(true);
         __syncthreads();
         sum_planes(accD);
     }
