@@ -60,8 +60,10 @@ enum nconv_kernel {
     NCONV_KERNEL_MFMA_BF16X3 = 3, /* bf16 matrix cores, two-part split operands (NCONV_MATH_BF16X3)    */
     NCONV_KERNEL_MFMA_BF16X9 = 4, /* bf16 matrix cores, three-part split, exact products (BF16X9)      */
     NCONV_KERNEL_TILED_FP32_PHASE = 5 /* as TILED_FP32, the nearest-2x-upsampled half of the input
-                                     channels convolved at native resolution with phase weights
-                                     (nconv_layer.waux, nconv_phase_weights)                     */
+                                     channels at native resolution: forward with phase weights
+                                     (nconv_layer.waux, nconv_phase_weights); input gradient as
+                                     4x4 box-summed weights per low pixel (exact-2x UpCat layers
+                                     with bwd_math FP32, no waux needed)                         */
 };
 
 /* One source tensor pair (data, confidence), physical shape (B, C, H, W). */

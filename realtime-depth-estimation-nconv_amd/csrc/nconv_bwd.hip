@@ -250,6 +250,171 @@ __global__ __launch_bounds__(kT) void dgrad_tiled(LayerDev d, BwdArgs a, float* 
     }
 }
 
+// ---- dgrad, phase form for an exactly 2x nearest-upsampled half (16 = 8 + 8 -> 8, 3x3, stride 1) ----
+// The upsampled channels' input gradient is only needed summed over each 2x2 block (the
+// nearest-upsample backward), and a block's sum is a 4x4 correlation of {gN, gD} with box-summed
+// weights. Low pixel (lr, lc) of the tile covers full-resolution rows 2lr + e (e = 0, 1); staged
+// output row 2lr + t receives input row 2lr + e through tap kh = e + 2 - t, so t = 0..3 collects the
+// taps S(0) = {2}, S(1) = {1, 2}, S(2) = {0, 1}, S(3) = {0} (columns alike):
+//     SG[i][lr][lc] = sum_o sum_{t,u} Wb[o][i][t][u] * g[o][2lr + t][2lc + u],  Wb = sum_{S(t) x S(u)} W
+// 16 taps per low pixel instead of 4 x 9 per block, and the result goes straight to the producer's
+// gradient (gx = SG_xc * c, gc = SG_c + SG_xc * x at the low pixel): no staged full-resolution plane,
+// no gather kernel. The 8 skip channels run as in dgrad_tiled. Thread roles: 2 skip pixels x 8
+// channels (dgrad_tiled's map) plus one low pixel x 4 upsampled channels, the channel half
+// wave-uniform (waves 0-1 / 2-3) so the box weights stay scalar.
+__global__ __launch_bounds__(kT) void box_weights(const float* __restrict__ w, int first_up, float* __restrict__ wb) {
+    const int e = blockIdx.x * kT + threadIdx.x;  // [o][i][t][u], 8 x 8 x 4 x 4
+    if (e >= 1024) return;
+    const int u = e & 3, t = (e >> 2) & 3, i = (e >> 4) & 7, o = e >> 7;
+    const float* wk = w + ((size_t)o * 16 + first_up + i) * 9;
+    const int h0 = t == 0 ? 2 : (t == 1 ? 1 : 0), nh = (t == 1 || t == 2) ? 2 : 1;
+    const int w0 = u == 0 ? 2 : (u == 1 ? 1 : 0), nw = (u == 1 || u == 2) ? 2 : 1;
+    float sum = 0.f;
+    for (int r = 0; r < nh; ++r)
+        for (int c = 0; c < nw; ++c) sum += wk[(h0 + r) * 3 + w0 + c];
+    wb[e] = sum;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kT) void dgrad_phase(LayerDev d, BwdArgs a, const float* __restrict__ wbox) {
+    using C = DgCfg<16, 3>;
+    using GS = GTileStager<C::OHT, C::OWT, C::OWP>;
+    constexpr int P = C::P, K = 3, CS = 8;
+    constexpr int SK0 = (MODE == NCONV_LOAD_UPCAT_SKIP_FIRST) ? 0 : 8;  // first skip channel of W
+    static_assert(C::TH % 2 == 0 && C::TW % 2 == 0 && C::OHT >= C::TH + 2 && C::OWT >= C::TW + 2, "low tile");
+    __shared__ __attribute__((aligned(16))) f2 tile[2 * GS::PLANE_STRIDE];
+    const nconv_layer& L = d.L;
+    const float* __restrict__ wgt = L.weight;
+    const TileCoord tcd = xcd_tile((L.W + C::TW - 1) / C::TW, (L.H + C::TH - 1) / C::TH, L.B);
+    const int tid = threadIdx.x, b = tcd.b;
+    const int ih0 = tcd.ty * C::TH, iw0 = tcd.tx * C::TW;
+    const int oh0 = ih0 + L.PH - (K - 1), ow0 = iw0 + L.PW - (K - 1);
+    const int ty = tid / C::TPR, tx = (tid % C::TPR) * P;
+    const int half = __builtin_amdgcn_readfirstlane(tid >> 7);  // upsampled channels 4 half .. +3
+    const int lq = tid & 127, lr = lq / (C::TW / 2), lc = lq % (C::TW / 2);
+    static_assert((C::TH / 2) * (C::TW / 2) == 128, "one low pixel per thread and channel half");
+
+    f2 acc[CS][P], au[4];
+#pragma unroll
+    for (int i = 0; i < CS; ++i)
+#pragma unroll
+        for (int j = 0; j < P; ++j) acc[i][j] = (f2){0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) au[c] = (f2){0.f, 0.f};
+
+    auto fma_plane = [&](int o, int bufi) {
+        const f2* pl = &tile[bufi * GS::PLANE_STRIDE];
+        const f2* row = pl + (ty + K - 1) * C::OWP + tx;
+        const float* wr = wgt + ((size_t)o * 16 + SK0) * K * K;
+#pragma unroll 1
+        for (int kh = 0; kh < K; ++kh, row -= C::OWP, wr += K) {
+            f2 v[C::NV];
+#pragma unroll
+            for (int m = 0; m < C::NV / 2; ++m) {
+                const f4 qv = reinterpret_cast<const f4*>(row)[m];
+                v[2 * m] = qv.xy;
+                v[2 * m + 1] = qv.zw;
+            }
+#pragma unroll
+            for (int kw = 0; kw < K; ++kw)
+#pragma unroll
+                for (int i = 0; i < CS; ++i) {
+                    const float w = wr[i * K * K + kw];
+                    const f2 w2 = (f2){w, w};
+#pragma unroll
+                    for (int j = 0; j < P; ++j)
+                        acc[i][j] = __builtin_elementwise_fma(w2, v[j + K - 1 - kw], acc[i][j]);
+                }
+        }
+        const f2* q = pl + (2 * lr) * C::OWP + 2 * lc;
+        const float* wb = wbox + ((size_t)o * 8 + 4 * half) * 16;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const f4 q0 = reinterpret_cast<const f4*>(q + t * C::OWP)[0];
+            const f4 q1 = reinterpret_cast<const f4*>(q + t * C::OWP)[1];
+            const f2 g[4] = {q0.xy, q0.zw, q1.xy, q1.zw};
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const float w = wb[c * 16 + t * 4 + u];
+                    au[c] = __builtin_elementwise_fma((f2){w, w}, g[u], au[c]);
+                }
+        }
+    };
+
+    GS gs;
+    gs.init(L, oh0, ow0, tid);
+    float va[4][GS::NE], vb[4][GS::NE];
+    gs.load(L, a, b, 0, va);
+    gs.load(L, a, b, 1, vb);
+#pragma unroll 1
+    for (int o = 0; o < 8; o += 2) {
+        gs.store(L, o, va, tile);
+        __syncthreads();
+        gs.load(L, a, b, o + 2 < 8 ? o + 2 : 7, va);
+        fma_plane(o, 0);
+        gs.store(L, o + 1, vb, tile + GS::PLANE_STRIDE);
+        __syncthreads();
+        gs.load(L, a, b, o + 3 < 8 ? o + 3 : 7, vb);
+        fma_plane(o + 1, 1);
+    }
+
+    const bool accm = a.accumulate != 0;
+    // ---- upsampled half: the low pixel's gradient, straight into the producer's planes ----
+    {
+        const int lh = (ih0 >> 1) + lr, lw = (iw0 >> 1) + lc;
+        if (lh < L.b.H && lw < L.b.W) {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const size_t off = plane_idx(b, 4 * half + c, L.b.C, L.b.H, L.b.W, lh, lw);
+                const float x = L.b.x[off], cf = L.b.c[off];
+                if (a.gxb) put(a.gxb, off, au[c].x * cf, accm);
+                if (a.gcb) put(a.gcb, off, au[c].y + au[c].x * x, accm);
+            }
+        }
+    }
+    // ---- skip half: gx = G_xc*c, gc = G_c + G_xc*x at full resolution ----
+    const int ih = ih0 + ty, iwb = iw0 + tx;
+    if (ih >= L.H) return;
+    const bool full = (L.W % P) == 0 && iwb + P <= L.W;
+#pragma unroll
+    for (int i = 0; i < CS; ++i) {
+        const size_t off = plane_idx(b, i, L.a.C, L.a.H, L.a.W, ih, iwb);
+        if (full) {
+            const f2 xv = *reinterpret_cast<const f2*>(L.a.x + off);
+            const f2 cv = *reinterpret_cast<const f2*>(L.a.c + off);
+            const f2 gxv = {acc[i][0].x * cv.x, acc[i][1].x * cv.y};
+            const f2 gcv = {acc[i][0].y + acc[i][0].x * xv.x, acc[i][1].y + acc[i][1].x * xv.y};
+            if (a.gxa) {
+                f2* p = reinterpret_cast<f2*>(a.gxa + off);
+                *p = accm ? *p + gxv : gxv;
+            }
+            if (a.gca) {
+                f2* p = reinterpret_cast<f2*>(a.gca + off);
+                *p = accm ? *p + gcv : gcv;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < P; ++j)
+                if (iwb + j < L.W) {
+                    const float x = L.a.x[off + j], cf = L.a.c[off + j];
+                    if (a.gxa) put(a.gxa, off + j, acc[i][j].x * cf, accm);
+                    if (a.gca) put(a.gca, off + j, acc[i][j].y + acc[i][j].x * x, accm);
+                }
+        }
+    }
+}
+
+// the phase input gradient applies: exact fp32 backward of a DNET-shaped exactly-2x UpCat layer
+static bool dgrad_phase_ok(const nconv_layer& L) {
+    const bool up = L.load_mode == NCONV_LOAD_UPCAT_SKIP_FIRST || L.load_mode == NCONV_LOAD_UPCAT_UP_FIRST;
+    if (!up || L.bwd_math != NCONV_MATH_FP32) return false;
+    if (L.Cin != 16 || L.Cout != 8 || L.a.C != 8 || L.b.C != 8 || L.KH != 3 || L.KW != 3) return false;
+    if (L.SH != 1 || L.SW != 1 || L.DH != 1 || L.DW != 1 || L.groups != 1) return false;
+    return L.a.H == L.H && L.a.W == L.W && L.H == 2 * L.b.H && L.W == 2 * L.b.W;
+}
+
 // ---- dgrad: generic (any stride / dilation / groups) ------------------------------------------------
 template <int MODE>
 __global__ __launch_bounds__(kT) void dgrad_generic(LayerDev d, BwdArgs a, float* tmp_x, float* tmp_c) {
@@ -778,11 +943,19 @@ __global__ __launch_bounds__(kT) NCONV_WM_ATTR void wgrad_mfma(LayerDev d, BwdAr
             }
         }
     };
+    // the wave's output channels' bias and normaliser, read once (not per row: a load right before
+    // its use would put a global-memory round trip into every row)
+    float bias_o[C::OPW], wsum_o[C::OPW];
+#pragma unroll
+    for (int kk = 0; kk < C::OPW; ++kk) {
+        bias_o[kk] = L.bias[w + 4 * kk];
+        wsum_o[kk] = L.wsum[w + 4 * kk];
+    }
     auto store_g = [&](int buf) {
 #pragma unroll
         for (int kk = 0; kk < C::OPW; ++kk) {
             const int o = w + 4 * kk;
-            const float bo = L.bias[o], so = L.wsum[o];
+            const float bo = bias_o[kk], so = wsum_o[kk];
 #pragma unroll
             for (int p = 0; p < 2; ++p) {
                 const int col = p * 64 + lane;
@@ -975,8 +1148,11 @@ size_t bwd_workspace_bytes(const LayerDev& d) {
                                        : (size_t)generic_chunks(L);
     size_t bytes = (nblk + kReduceSplit) * stride * sizeof(float);  // partial rows + slice sums
     bytes = (bytes + 255) & ~(size_t)255;
-    if (L.load_mode == NCONV_LOAD_UPCAT_SKIP_FIRST || L.load_mode == NCONV_LOAD_UPCAT_UP_FIRST)
-        bytes += 2 * (size_t)L.B * L.b.C * L.H * L.W * sizeof(float);
+    if (L.load_mode == NCONV_LOAD_UPCAT_SKIP_FIRST || L.load_mode == NCONV_LOAD_UPCAT_UP_FIRST) {
+        // staged upsampled-channel planes for upsample_bwd_gather, or dgrad_phase's box weights
+        const size_t planes = 2 * (size_t)L.B * L.b.C * L.H * L.W;
+        bytes += (planes > 1024 ? planes : 1024) * sizeof(float);
+    }
     return bytes;
 }
 
@@ -988,7 +1164,7 @@ void plan_bwd(const nconv_layer& L, int* dgrad, int* wgrad) {
     const int bf = L.bwd_math == NCONV_MATH_BF16X9 ? NCONV_KERNEL_MFMA_BF16X9 : NCONV_KERNEL_MFMA_BF16X3;
     const bool multi = L.KH > 1 && L.Cin > 1;  // 3x3 / 5x5 layers with several input channels
     const bool fp32 = L.bwd_math == NCONV_MATH_FP32;
-    *dgrad = multi && !fp32 ? bf : NCONV_KERNEL_TILED_FP32;
+    *dgrad = multi && !fp32 ? bf : (dgrad_phase_ok(L) ? NCONV_KERNEL_TILED_FP32_PHASE : NCONV_KERNEL_TILED_FP32);
     *wgrad = multi ? (fp32 ? NCONV_KERNEL_MFMA_FP32 : bf) : NCONV_KERNEL_TILED_FP32;
 }
 
@@ -1006,7 +1182,18 @@ static int go_bwd_tiled(const LayerDev& d, const BwdArgs& a, float* part, float*
                 go_dgrad_bf<CIN, COUT, K, MODE>(d, a, tx, tc, L.bwd_math == NCONV_MATH_BF16X9 ? 3 : 2, st);
         } else {
             dim3 g(((L.W + D::TW - 1) / D::TW) * ((L.H + D::TH - 1) / D::TH) * L.B);  // see xcd_tile
-            hipLaunchKernelGGL((dgrad_tiled<CIN, COUT, K, MODE>), g, dim3(kT), 0, st, d, a, tx, tc);
+            constexpr bool up = MODE == NCONV_LOAD_UPCAT_SKIP_FIRST || MODE == NCONV_LOAD_UPCAT_UP_FIRST;
+            if constexpr (up && CIN == 16 && COUT == 8 && K == 3) {
+                if (dgrad_phase_ok(L)) {  // box weights into the (then unused) staging planes
+                    hipLaunchKernelGGL(box_weights, dim3(1024 / kT), dim3(kT), 0, st, L.weight,
+                                       MODE == NCONV_LOAD_UPCAT_SKIP_FIRST ? 8 : 0, tx);
+                    hipLaunchKernelGGL((dgrad_phase<MODE>), g, dim3(kT), 0, st, d, a, tx);
+                } else {
+                    hipLaunchKernelGGL((dgrad_tiled<CIN, COUT, K, MODE>), g, dim3(kT), 0, st, d, a, tx, tc);
+                }
+            } else {
+                hipLaunchKernelGGL((dgrad_tiled<CIN, COUT, K, MODE>), g, dim3(kT), 0, st, d, a, tx, tc);
+            }
         }
     }
     if constexpr (K > 1 && CIN > 1) {
@@ -1107,7 +1294,7 @@ int launch_bwd(const LayerDev& d, const BwdArgs& a, hipStream_t st, const char**
             default: *why = "unknown load mode"; return -22;
         }
     }
-    if (up && (a.gxb || a.gcb)) {
+    if (up && (a.gxb || a.gcb) && !(path == kTiled && dgrad_phase_ok(L))) {  // (dgrad_phase writes them itself)
         const size_t n = (size_t)L.B * L.b.C * L.b.H * L.b.W;
         size_t blocks = (n + kT - 1) / kT;
         if (blocks > (1u << 20)) blocks = 1u << 20;

@@ -952,13 +952,11 @@ void go_mfma(const LayerDev& d, float* y, float* yc, const TailArgs& t, int gh, 
 // LDS-DMA staging: rows of every source a multiple of 4 floats (16-B vectors never straddle a row
 // end), exact 2x upsampling of source b with 8 + 8 channels, per-image sources below 2 GiB.
 // Measured slower than register staging at two workgroups per CU (nconv2 198 vs 179 us, the tail
-// 272 vs 169 us at B=8 352x1216): opt-in with NCONV_MFMA_DMA=1 while it is being tuned.
+// 272 vs 169 us at B=8 352x1216): compiled in only with -DNCONV_MFMA_DMA=1 (build-time experiment).
+#ifndef NCONV_MFMA_DMA
+#define NCONV_MFMA_DMA 0
+#endif
 bool dma_ok(const nconv_layer& L, int cin) {
-    static const bool on = [] {
-        const char* e = getenv("NCONV_MFMA_DMA");
-        return e && atoi(e) != 0;
-    }();
-    if (!on) return false;
     if (L.load_mode != NCONV_LOAD_PLAIN && L.load_mode != NCONV_LOAD_UPCAT_SKIP_FIRST &&
         L.load_mode != NCONV_LOAD_UPCAT_UP_FIRST)
         return false;
@@ -975,7 +973,7 @@ bool dma_ok(const nconv_layer& L, int cin) {
 
 template <int CIN, int K, int MODE, int EPI, int TH, int NP>
 void go_mfma_np(const LayerDev& d, float* y, float* yc, const TailArgs& t, int gh, int gw, hipStream_t st) {
-    if constexpr (MODE == NCONV_LOAD_POOL2 || NP != 2)
+    if constexpr (MODE == NCONV_LOAD_POOL2 || NP != 2 || !NCONV_MFMA_DMA)
         go_mfma<CIN, K, MODE, EPI, TH, false, NP>(d, y, yc, t, gh, gw, st);
     else if (dma_ok(d.L, CIN))
         go_mfma<CIN, K, MODE, EPI, TH, true, NP>(d, y, yc, t, gh, gw, st);

@@ -184,19 +184,26 @@ __global__ __launch_bounds__(kWbT) void wgrad_bf(LayerDev d, BwdArgs a, float* p
         }
     };
     const bool g_st = lane + C::HALO < C::GP;  // the lane's G dword lies inside its row
-    auto store_g = [&](int buf) {
+    float bias_o[C::OPW], wsum_o[C::OPW];        // read once, not per row
+#pragma unroll
+    for (int k = 0; k < C::OPW; ++k) {
+        bias_o[k] = L.bias[w * C::OPW + k];
+        wsum_o[k] = L.wsum[w * C::OPW + k];
+    }
+    auto store_g = [&](int buf, bool count) {  // count: a new row (its bias / wsum sums taken)
 #pragma unroll
         for (int k = 0; k < C::OPW; ++k) {
             const int o = w * C::OPW + k;
-            const float bo = L.bias[o], so = L.wsum[o];
+            const float bo = bias_o[k], so = wsum_o[k];
             float gN[2], gD[2];
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
                 nconv_grad_nd(gq[k][j][0], gq[k][j][3], gq[k][j][2], gq[k][j][1], L.eps, bo, so, gN[j], gD[j]);
                 gN[j] = g_in[j] ? gN[j] : 0.f;
                 gD[j] = g_in[j] ? gD[j] : 0.f;
-                gb_acc[k] += gq[k][j][0];  // (0 outside the strip's own columns)
-                gs_acc[k] = fmaf(gq[k][j][3], gq[k][j][1], gs_acc[k]);
+                // (0 outside the strip's own columns)
+                gb_acc[k] = count ? gb_acc[k] + gq[k][j][0] : gb_acc[k];
+                gs_acc[k] = count ? fmaf(gq[k][j][3], gq[k][j][1], gs_acc[k]) : gs_acc[k];
             }
             unsigned pn[NP], pd[NP];
             split2<NP>(gN[0], gN[1], pn);
@@ -231,7 +238,7 @@ __global__ __launch_bounds__(kWbT) void wgrad_bf(LayerDev d, BwdArgs a, float* p
             store_in(mod_slots(r0 - L.PH + kh));
         }
         load_g(r0);
-        store_g(0);
+        store_g(0, true);
         load_in(r0 + 1 - L.PH + K - 1);
         load_g(r0 + 1 < r1 ? r0 + 1 : r0);
         __syncthreads();
@@ -260,10 +267,12 @@ __global__ __launch_bounds__(kWbT) void wgrad_bf(LayerDev d, BwdArgs a, float* p
                 fb[u][p] = __builtin_bit_cast(bf16x8, (u4v){q[0], q[1], q[2], q[3]});
             }
         }
-        if (oh + 1 < r1) {  // (block-uniform) the next row's input row and g row, then its loads
+        {   // the next row's input row and g row, then its loads. Unconditional (after the last row
+            // they fill a ring slot and a g buffer no MFMA of this row reads): a branch here would make
+            // the compiler copy the in-flight load registers, i.e. wait for them, before the MFMAs
             store_in(s0 + K >= C::SLOTS ? s0 + K - C::SLOTS : s0 + K);
-            store_g(buf ^ 1);
-            const int nx = oh + 2 < r1 ? oh + 2 : oh + 1;
+            store_g(buf ^ 1, oh + 1 < r1);
+            const int nx = oh + 2 < r1 ? oh + 2 : r1 - 1;
             load_in(nx - L.PH + K - 1);
             load_g(nx);
         }

@@ -99,7 +99,10 @@ def test_layer_backward(nconv_amd, gpu, case, bwd_math):
     # the bf16 matrix-core kernels, never a silent fallback to another arithmetic
     _, dg_k, wg_k = nconv_amd.nconv.kernel_plan(_spec(nconv_amd, case), *gl[:4], gl[4], gl[5], wsum)
     if wg_k != "generic" and cin > 1 and k > 1:
-        want = ("tiled_fp32", "mfma_fp32") if bwd_math == "fp32" else ("mfma_" + bwd_math,) * 2
+        a_shape, b_shape = case[9], case[10]
+        exact_up = b_shape is not None and a_shape[1:] == (2 * b_shape[1], 2 * b_shape[2])
+        dg_fp32 = "tiled_fp32_phase" if exact_up else "tiled_fp32"  # dgrad_phase: exact-2x UpCat
+        want = (dg_fp32, "mfma_fp32") if bwd_math == "fp32" else ("mfma_" + bwd_math,) * 2
         assert (dg_k, wg_k) == want, (name, bwd_math, dg_k, wg_k)
     y, c = nconv_amd.nconv_layer(_spec(nconv_amd, case), *gl[:4], gl[4], gl[5], wsum)
     (y * gy.to(gpu, torch.float32) + c * gc.to(gpu, torch.float32)).sum().backward()
@@ -117,7 +120,8 @@ def test_layer_backward(nconv_amd, gpu, case, bwd_math):
 
 
 @pytest.mark.parametrize("case", [c for c in LAYER_CASES if c[0] in ("nconv2_plain", "down_pool_odd",
-                                                                      "nconv5_upcat_inexact", "generic_stride2")],
+                                                                      "nconv5_upcat_inexact", "nconv5_upcat_w4",
+                                                                      "nconv6_upfirst_w4", "generic_stride2")],
                          ids=lambda c: c[0])
 def test_bwd_accumulate_flag(nconv_amd, gpu, case, bwd_math):
     """NCONV_BWD_ACCUMULATE adds into pre-filled input-gradient buffers; without it every element
@@ -311,3 +315,34 @@ def test_upcat_phase_forward(nconv_amd, gpu, case):
         bound = 1e-4 * ref.abs() + 1e-5
         assert (err <= bound).all(), f"{name}: max err {err.max():.3e}, worst ratio {(err / bound).max():.3f}"
     print(f"{name}: phase vs dense max rel {((y - yd).abs() / (yd.abs() + 1e-30)).max().item():.2e}")
+
+
+@pytest.mark.parametrize("case", PHASE_CASES, ids=[c[0] for c in PHASE_CASES])
+def test_upcat_phase_backward(nconv_amd, gpu, case):
+    """Exact-fp32 backward of exactly-2x UpCat layers: the input gradient of the upsampled half runs
+    at native resolution with box-summed weights (dgrad_phase, no staged plane or gather kernel).
+    Every gradient against the oracle's autograd of cat + F.interpolate + NConv2d (normwise 1e-3,
+    SURVEY 8(c)), with nconv_plan naming the phase kernel; padding 0 / 1 / 2 and both channel orders
+    put the low pixels' 4x4 windows at every alignment against the image edge."""
+    name, mode, pad, a_shape, b_shape = case
+    g = torch.Generator().manual_seed(23)
+    xa, ca = rand_pair(g, 2, *a_shape, dtype=torch.float64)
+    xb, cb = rand_pair(g, 2, *b_shape, dtype=torch.float64)
+    w = rand_weight(g, 8, 16, 3, 3, torch.float64)
+    b = torch.rand(8, generator=g, dtype=torch.float64) * 0.1
+    leaves = [t.clone().requires_grad_(True) for t in (xa, ca, xb, cb, w, b)]
+    ry, rc = oracle_layer(mode, *leaves, (1, 1), (pad, pad))
+    gy = torch.randn(ry.shape, generator=g, dtype=torch.float64)
+    gc = torch.randn(rc.shape, generator=g, dtype=torch.float64)
+    (ry * gy + rc * gc).sum().backward()
+    spec = nconv_amd.LayerSpec(16, 8, (3, 3), (1, 1), (pad, pad), mode=mode)
+    gl = [_gpu(t, gpu, grad=True) for t in (xa, ca, xb, cb, w, b)]
+    wsum = _wsum(nconv_amd, gl[4])
+    assert nconv_amd.nconv.kernel_plan(spec, *gl[:4], gl[4], gl[5], wsum)[1:] == ("tiled_fp32_phase", "mfma_fp32")
+    y, c = nconv_amd.nconv_layer(spec, *gl[:4], gl[4], gl[5], wsum)
+    (y * gy.to(gpu, torch.float32) + c * gc.to(gpu, torch.float32)).sum().backward()
+    torch.cuda.synchronize()
+    for lab, ref_leaf, got_leaf in zip(("g_xa", "g_ca", "g_xb", "g_cb", "g_w", "g_b"), leaves, gl):
+        ref, got = ref_leaf.grad, got_leaf.grad.double().cpu()
+        rel = ((got - ref).abs().max() / ref.abs().max().clamp_min(1e-30)).item()
+        assert rel <= 1e-3, f"{name} {lab}: normwise rel err {rel:.3e}"
