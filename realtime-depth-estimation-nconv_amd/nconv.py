@@ -120,13 +120,19 @@ def _outputs(out, n, shapes, device):
     return list(out)
 
 
+PHASE_WEIGHT_FLOATS = 1024  # one UpCat layer's phase-weight buffer (nconv_phase_weights_floats)
+
+
 def phase_weights(weights, up_first, outs):
-    """nconv_phase_weights: one launch filling outs[i] (1024 floats) with the phase weights of the
+    """nconv_phase_weights: one launch filling outs[i] (PHASE_WEIGHT_FLOATS floats) with the phase weights of the
     UPCAT layer whose (8, Cin, 3, 3) weight is weights[i] and whose upsampled channels start at
     up_first[i], from the current weights (after weight_prep)."""
     n = len(weights)
     if n == 0:
         return
+    for o in outs:
+        if o.numel() < PHASE_WEIGHT_FLOATS or not o.is_contiguous() or o.dtype != torch.float32:
+            raise ValueError(f"phase-weight buffers need {PHASE_WEIGHT_FLOATS} contiguous fp32 elements")
     P, I = _lib.ctypes.c_void_p * n, _lib.ctypes.c_int * n
     rc = _lib.lib().nconv_phase_weights(n, P(*[w.data_ptr() for w in weights]), I(*[w.shape[1] for w in weights]),
                                         I(*up_first), P(*[o.data_ptr() for o in outs]),

@@ -13,3 +13,6 @@ for i in 1 2; do
      --steps 30 --warmup 5 ${BENCH_ARGS} > gpurun_out/r3fc_bench.log 2>&1 || stop bench $?
   python3 -c "import json; d=json.loads(open('gpurun_out/r3fc_bench.log').read().strip().splitlines()[-1]); print(d['value'], d['ms_per_step'], json.dumps(d['layer_us']))"
 done
+for l in tail nconv5; do
+  timeout -k 10 120 python -u tools/fwd_layer_bench.py $l 50 || stop layer_$l $?
+done
