@@ -535,6 +535,13 @@ def main():
     log(f"config 2 forward, {a.math}")
     t_fwd = time_forward(S, a.steps, HEAD)
     fps = world * B * a.steps / t_fwd
+    # per-kernel times of each forward right after its timed run (rank 0), so the roofline's kernel
+    # time is taken in the same conditions as the headline, not after the heavier legs below
+    lt_of = {}
+    if rank == 0:
+        log("per-kernel times")
+        m.nconv.FORWARD_MATH = HEAD
+        lt_of[a.math] = time_layers(m, net, S)
 
     # ---- the same forward in the other arithmetics ----
     alt = {}
@@ -543,6 +550,9 @@ def main():
             continue
         log(f"config 2 forward, {name}")
         t = time_forward(S, a.steps, MATHS[name])
+        if rank == 0:
+            m.nconv.FORWARD_MATH = MATHS[name]
+            lt_of[name] = time_layers(m, net, S)
         alt[name] = {"frames_per_sec": round(world * B * a.steps / t, 2), "ms_per_step": round(t / a.steps * 1e3, 4),
                      "dtype": MATH_DTYPE[name], "arith": MATH_ARITH[name], "whole_pass_hbm_frac": pass_frac(t, a.steps)}
 
@@ -555,6 +565,9 @@ def main():
         S5 = sparse_depth(torch.Generator().manual_seed(5000 + rank), B5, H5, W5, dev)
         k5 = max(3, a.steps // 4)
         t5 = time_forward(S5, k5, HEAD)
+        if rank == 0:
+            m.nconv.FORWARD_MATH = HEAD
+            lt_of["config5"] = time_layers(m, net, S5, reps=5)
         c5 = {"workload": f"config5: DNET forward, B=16 1024x2048 per GPU, generalized crop, {a.math}",
               "frames_per_sec": round(world * B5 * k5 / t5, 2), "ms_per_step": round(t5 / k5 * 1e3, 3),
               "steps": k5, "per_gpu_batch": B5}
@@ -639,23 +652,19 @@ def main():
 
     # ---- per-kernel times, rooflines, CPU baseline (rank 0) ----
     if rank == 0:
-        log("per-kernel times")
         costs = kernel_costs(B, H, W)
-        m.nconv.FORWARD_MATH = HEAD
-        lt = time_layers(m, net, S)
+        lt = lt_of[a.math]
         issued = (lambda k: mfma_issued_flops(k, B, H, W, a.math)) if a.math in MFMA_TERMS else None
         roof = roofline(lt, costs, a.math, B, H, W, issued_mfma=issued)
         roof["whole_pass_hbm_frac"] = pass_frac(t_fwd, a.steps)
         for name, rec in alt.items():
-            m.nconv.FORWARD_MATH = MATHS[name]
-            lt_a = time_layers(m, net, S)
+            lt_a = lt_of[name]
             rec["layer_us"] = {k: round(v, 2) for k, v in lt_a.items()}
             rec["roofline"] = roofline(lt_a, costs, name, B, H, W,
                                        issued_mfma=(lambda k, n=name: mfma_issued_flops(k, B, H, W, n))
                                        if name in MFMA_TERMS else None)
         if c5 is not None:
-            m.nconv.FORWARD_MATH = HEAD
-            lt5 = time_layers(m, net, S5, reps=5)
+            lt5 = lt_of["config5"]
             c5["layer_us"] = {k: round(v, 2) for k, v in lt5.items()}
             c5["roofline"] = roofline(lt5, kernel_costs(16, 1024, 2048), a.math, 16, 1024, 2048)
             c5["whole_pass_hbm_frac"] = round(1169.4e6 * 16 / (c5["ms_per_step"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
