@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define NCONV_ABI_VERSION 16
+#define NCONV_ABI_VERSION 17
 
 /* How a layer's input (data x, confidence c) is produced from its source tensors. These are the
  * DNET glue ops fused into the layer's load stage (models/step1.py:53,61-90). */
@@ -197,10 +197,24 @@ size_t nconv_bwd_workspace_bytes(const nconv_layer* L);
  *   g(xc) = W^T * gN, gx = g(xc)*c, gc = W^T * gD + g(xc)*x.
  * D and N/(D+eps) are recovered from the saved outputs as cout*s and y-b. */
 #define NCONV_BWD_ACCUMULATE 1u
+/* (flags & NCONV_BWD_DEFER_REDUCE): the weight gradient is left in the workspace as per-workgroup
+ * partial rows and nconv_bwd returns their number (>= 0; 0 when gw and gbias are both NULL) instead
+ * of 0; gw / gbias are written by a later nconv_wgrad_reduce over that workspace (which must stay
+ * untouched until then). A training backward defers every layer and reduces them all in two
+ * launches instead of two per layer. Same sums, same fixed order: the result is bitwise that of
+ * the undeferred call. */
+#define NCONV_BWD_DEFER_REDUCE 2u
 
 int nconv_bwd(const nconv_layer* L, const float* y, const float* cout, const float* gy,
               const float* gcout, float* gxa, float* gca, float* gxb, float* gcb, float* gw,
               float* gbias, void* workspace, size_t workspace_bytes, unsigned flags, void* stream);
+
+/* Weight / bias gradients of n (1..16) layers whose nconv_bwd ran with NCONV_BWD_DEFER_REDUCE:
+ * layers[k] the descriptor of that call (its weight normaliser wsum is read), workspaces[k] and
+ * nparts[k] its workspace and return value, gw[k] / gbias[k] the outputs (either may be NULL;
+ * layers with nparts[k] == 0 are skipped). Two launches on `stream`. Returns 0 or -EINVAL. */
+int nconv_wgrad_reduce(int n, const nconv_layer* layers, void* const* workspaces, const int* nparts,
+                       float* const* gw, float* const* gbias, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Dense convolutions of the RGB-guided model on the matrix cores (fp32 MFMA, exact f32 products).

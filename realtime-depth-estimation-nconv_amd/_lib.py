@@ -13,8 +13,9 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # NCONV_LIB: an alternative build of the same library (kernel-tuning experiments)
 LIB_PATH = os.environ.get("NCONV_LIB") or os.path.join(_HERE, "libnconv.so")
-ABI_VERSION = 16
+ABI_VERSION = 17
 BWD_ACCUMULATE = 1
+BWD_DEFER_REDUCE = 2
 
 # enum nconv_load_mode
 PLAIN, THRESH, POOL2, UPCAT_SKIP_FIRST, UPCAT_UP_FIRST = 0, 1, 2, 3, 4
@@ -41,6 +42,7 @@ EXPORTED = (
     "nconv_phase_weights",
     "nconv_bwd_workspace_bytes",
     "nconv_bwd",
+    "nconv_wgrad_reduce",
     "nconv_dense_packed_floats",
     "nconv_dense_pack",
     "nconv_dense_conv_fwd",
@@ -132,6 +134,8 @@ def _declare(lib):
     lib.nconv_bwd.restype = ctypes.c_int
     lib.nconv_bwd.argtypes = [ctypes.POINTER(NconvLayer), P, P, P, P, P, P, P, P, P, P, P,
                               ctypes.c_size_t, ctypes.c_uint, P]
+    lib.nconv_wgrad_reduce.restype = ctypes.c_int
+    lib.nconv_wgrad_reduce.argtypes = [ctypes.c_int, ctypes.POINTER(NconvLayer), P, P, P, P, P]
     I = ctypes.c_int
     lib.nconv_dense_packed_floats.restype = ctypes.c_size_t
     lib.nconv_dense_packed_floats.argtypes = [I, I, I]

@@ -184,6 +184,45 @@ __global__ __launch_bounds__(kT) void dgrad_tiled(LayerDev d, BwdArgs a, float* 
 #pragma unroll
     for (int i = 0; i < CIN; ++i) {
         if constexpr (MODE == NCONV_LOAD_POOL2) {
+            if (P == 2 && full && (L.a.W & 3) == 0) {
+                // the two pooled pixels' 2x2 windows are 4 columns x 2 rows of the producer: 16-byte
+                // loads of x / c for the argmax, 16-byte stores (or read-modify-writes) of gx / gc with
+                // 0 at the other three slots (what the reference's max_pool2d backward adds there)
+                const size_t W2 = (size_t)L.a.W;
+                const size_t i0 = plane_idx(b, i, L.a.C, L.a.H, L.a.W, 2 * ih, 2 * iwb);
+                const f4 x0 = *reinterpret_cast<const f4*>(L.a.x + i0);
+                const f4 x1 = *reinterpret_cast<const f4*>(L.a.x + i0 + W2);
+                const f4 c0 = *reinterpret_cast<const f4*>(L.a.c + i0);
+                const f4 c1 = *reinterpret_cast<const f4*>(L.a.c + i0 + W2);
+                f4 gx[2], gc[2];
+#pragma unroll
+                for (int j = 0; j < P; ++j) {
+                    int ax, ac;
+                    const float xm = pool4(x0[2 * j], x0[2 * j + 1], x1[2 * j], x1[2 * j + 1], ax);
+                    const float cm = pool4(c0[2 * j], c0[2 * j + 1], c1[2 * j], c1[2 * j + 1], ac);
+                    const float vx = acc[i][j].x * cm, vc = acc[i][j].y + acc[i][j].x * xm;
+#pragma unroll
+                    for (int s = 0; s < 4; ++s) {
+                        gx[s >> 1][2 * j + (s & 1)] = (s == ax) ? vx : 0.f;
+                        gc[s >> 1][2 * j + (s & 1)] = (s == ac) ? vc : 0.f;
+                    }
+                }
+#pragma unroll
+                for (int r = 0; r < 2; ++r) {
+                    if (a.gxa) {
+                        f4* p = reinterpret_cast<f4*>(a.gxa + i0 + r * W2);
+                        *p = accm ? *p + gx[r] : gx[r];
+                    }
+                    if (a.gca) {
+                        f4* p = reinterpret_cast<f4*>(a.gca + i0 + r * W2);
+                        *p = accm ? *p + gc[r] : gc[r];
+                    }
+                }
+                if (!accm)
+#pragma unroll
+                    for (int j = 0; j < P; ++j) pool_zero_leftovers(d, a, b, i, ih, iwb + j);
+                continue;
+            }
 #pragma unroll
             for (int j = 0; j < P; ++j)
                 if (iwb + j < L.W) {
@@ -751,23 +790,44 @@ __global__ __launch_bounds__(kT) void wgrad_generic(LayerDev d, BwdArgs a, float
 // Stage 2 (wgrad_finish) adds the kReduceSplit slice sums in order — deterministic, no atomics.
 constexpr int kReduceSplit = 16;
 
-__global__ __launch_bounds__(kT) void wgrad_reduce_sum(const float* part, int nblk, int stride, float* sub) {
+// Both stages take a table of up to kMaxRedJobs layers (nconv_wgrad_reduce: every layer of a
+// backward pass in two launches instead of two per layer); a block finds its layer by a
+// wave-uniform scan of the table's first-block offsets.
+struct RedTable {
+    RedJob j[kMaxRedJobs];
+    int x0[kMaxRedJobs + 1];  // first stage-1 block (64 entries of a row) of each job
+    int f0[kMaxRedJobs + 1];  // first stage-2 block of each job
+    int n;
+};
+
+__device__ __forceinline__ int red_job(const int* first, int n, int blk) {
+    int k = 0;
+    while (k + 1 < n && blk >= first[k + 1]) ++k;
+    return k;
+}
+
+__global__ __launch_bounds__(kT) void wgrad_reduce_sum(const RedTable T) {
     __shared__ float red[kT];
+    const int k = red_job(T.x0, T.n, blockIdx.x);
+    const RedJob& J = T.j[k];
+    const int stride = J.nw + 2 * J.cout, nblk = J.nblk;
+    const float* part = J.part;
+    float* sub = const_cast<float*>(J.part) + (size_t)nblk * stride;
     const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
-    const int e = blockIdx.x * 64 + lane;
+    const int e = (blockIdx.x - T.x0[k]) * 64 + lane;
     const int per = (nblk + kReduceSplit - 1) / kReduceSplit;
     const int k0 = blockIdx.y * per, k1 = min(nblk, k0 + per);
     float s = 0.f;
     if (e < stride) {
-        int k = k0 + grp;
-        for (; k + 28 < k1; k += 32) {
+        int r = k0 + grp;
+        for (; r + 28 < k1; r += 32) {
             float v[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) v[u] = part[(size_t)(k + 4 * u) * stride + e];
+            for (int u = 0; u < 8; ++u) v[u] = part[(size_t)(r + 4 * u) * stride + e];
 #pragma unroll
             for (int u = 0; u < 8; ++u) s += v[u];
         }
-        for (; k < k1; k += 4) s += part[(size_t)k * stride + e];
+        for (; r < k1; r += 4) s += part[(size_t)r * stride + e];
     }
     red[threadIdx.x] = s;
     __syncthreads();
@@ -784,27 +844,51 @@ __device__ __forceinline__ float slice_total(const float* sub, int stride, int e
     return t;
 }
 
-__global__ __launch_bounds__(kT) void wgrad_finish(const float* sub, int nw, int cout, int fan, const float* wsum,
-                                                   float* gw, float* gb) {
-    const int stride = nw + 2 * cout;
-    for (int w = blockIdx.x * kT + threadIdx.x; w < nw + cout; w += gridDim.x * kT) {
-        if (w < nw) {
-            const int o = w / fan;
-            if (gw) gw[w] = slice_total(sub, stride, w) + (-slice_total(sub, stride, nw + cout + o) / wsum[o]);
-        } else if (gb) {
-            gb[w - nw] = slice_total(sub, stride, w);
-        }
+__global__ __launch_bounds__(kT) void wgrad_finish(const RedTable T) {
+    const int k = red_job(T.f0, T.n, blockIdx.x);
+    const RedJob& J = T.j[k];
+    const int nw = J.nw, cout = J.cout, stride = nw + 2 * cout;
+    const float* sub = J.part + (size_t)J.nblk * stride;
+    const int w = (blockIdx.x - T.f0[k]) * kT + threadIdx.x;
+    if (w < nw) {
+        const int o = w / J.fan;
+        if (J.gw) J.gw[w] = slice_total(sub, stride, w) + (-slice_total(sub, stride, nw + cout + o) / J.wsum[o]);
+    } else if (w < nw + cout && J.gb) {
+        J.gb[w - nw] = slice_total(sub, stride, w);
     }
 }
 
-// part: nblk partial rows followed by kReduceSplit rows of slice sums (see bwd_workspace_bytes)
-static void launch_wgrad_reduce(const float* part, int nblk, int nw, int cout, int fan, const float* wsum,
-                                float* gw, float* gb, float* sub, hipStream_t st) {
-    const int stride = nw + 2 * cout;
-    hipLaunchKernelGGL(wgrad_reduce_sum, dim3((stride + 63) / 64, kReduceSplit), dim3(kT), 0, st, part, nblk,
-                       stride, sub);
-    hipLaunchKernelGGL(wgrad_finish, dim3((nw + cout + kT - 1) / kT), dim3(kT), 0, st, sub, nw, cout, fan, wsum,
-                       gw, gb);
+int launch_wgrad_reduce_multi(int n, const RedJob* jobs, hipStream_t st, const char** why) {
+    if (n < 1 || n > kMaxRedJobs) {
+        *why = "between 1 and 16 layers per reduction";
+        return -22;
+    }
+    RedTable T;
+    T.n = n;
+    T.x0[0] = T.f0[0] = 0;
+    for (int k = 0; k < n; ++k) {
+        T.j[k] = jobs[k];
+        const int stride = jobs[k].nw + 2 * jobs[k].cout;
+        T.x0[k + 1] = T.x0[k] + (stride + 63) / 64;
+        T.f0[k + 1] = T.f0[k] + (jobs[k].nw + jobs[k].cout + kT - 1) / kT;
+    }
+    for (int k = n + 1; k <= kMaxRedJobs; ++k) T.x0[k] = T.f0[k] = 0;
+    hipLaunchKernelGGL(wgrad_reduce_sum, dim3(T.x0[n], kReduceSplit), dim3(kT), 0, st, T);
+    hipLaunchKernelGGL(wgrad_finish, dim3(T.f0[n]), dim3(kT), 0, st, T);
+    return 0;
+}
+
+// part: nblk partial rows followed by kReduceSplit rows of slice sums (see bwd_workspace_bytes);
+// with a.defer the rows stay for a later nconv_wgrad_reduce over every layer of the pass
+static void launch_wgrad_reduce(const BwdArgs& a, const float* part, int nblk, int nw, int cout, int fan,
+                                const float* wsum, hipStream_t st) {
+    if (a.defer) {
+        *a.nparts = nblk;
+        return;
+    }
+    const RedJob J{part, wsum, a.gw, a.gb, nblk, nw, cout, fan};
+    const char* why = nullptr;
+    launch_wgrad_reduce_multi(1, &J, st, &why);
 }
 
 // ---- wgrad on the matrix cores (fp32 MFMA 16x16x4, exact f32 products) -----------------------------
@@ -1202,8 +1286,7 @@ static int go_bwd_tiled(const LayerDev& d, const BwdArgs& a, float* part, float*
                                                              L.bwd_math == NCONV_MATH_BF16X9 ? 3 : 2, st);
             if (nblk < 0) return -5;
             const int nw = COUT * CIN * K * K;
-            launch_wgrad_reduce(part, nblk, nw, COUT, CIN * K * K, L.wsum, a.gw, a.gb,
-                                part + (size_t)nblk * (nw + 2 * COUT), st);
+            launch_wgrad_reduce(a, part, nblk, nw, COUT, CIN * K * K, L.wsum, st);
         } else if (a.gw || a.gb) {
             const int per_cu = dev_occupancy((const void*)wgrad_mfma<CIN, COUT, K, MODE>, kT, 0);
             const int resident = device_cus() * (per_cu < kMfmaMaxPerCu ? per_cu : kMfmaMaxPerCu);
@@ -1211,8 +1294,7 @@ static int go_bwd_tiled(const LayerDev& d, const BwdArgs& a, float* part, float*
             hipLaunchKernelGGL((wgrad_mfma<CIN, COUT, K, MODE>), dim3(g.nblk), dim3(kT), 0, st, d, a, part,
                                g.nstrip, g.nseg, g.seg_rows);
             const int nw = COUT * CIN * K * K;
-            launch_wgrad_reduce(part, (int)g.nblk, nw, COUT, CIN * K * K, L.wsum, a.gw, a.gb,
-                                part + g.nblk * (nw + 2 * COUT), st);
+            launch_wgrad_reduce(a, part, (int)g.nblk, nw, COUT, CIN * K * K, L.wsum, st);
         }
     } else if (a.gw || a.gb) {
         using W = WgCfg<CIN, COUT, K>;
@@ -1229,8 +1311,7 @@ static int go_bwd_tiled(const LayerDev& d, const BwdArgs& a, float* part, float*
         const int nblk = nblk_ws < resident ? nblk_ws : resident;
         hipLaunchKernelGGL((wgrad_tiled<CIN, COUT, K, MODE>), dim3(nblk), dim3(kT), lds, st, d, a, part, ntw, nth);
         const int nw = COUT * CIN * K * K;
-        launch_wgrad_reduce(part, nblk, nw, COUT, CIN * K * K, L.wsum, a.gw, a.gb,
-                            part + (size_t)nblk * (nw + 2 * COUT), st);
+        launch_wgrad_reduce(a, part, nblk, nw, COUT, CIN * K * K, L.wsum, st);
     }
     return 0;
 }
@@ -1250,8 +1331,7 @@ static void go_bwd_generic(const LayerDev& d, const BwdArgs& a, float* part, flo
         const int nw = L.Cout * fan;
         const int nchunk = generic_chunks(L);
         hipLaunchKernelGGL(wgrad_generic<MODE>, dim3(nchunk, nw + 2 * L.Cout), dim3(kT), 0, st, d, a, part, nchunk);
-        launch_wgrad_reduce(part, nchunk, nw, L.Cout, fan, L.wsum, a.gw, a.gb,
-                            part + (size_t)nchunk * (nw + 2 * L.Cout), st);
+        launch_wgrad_reduce(a, part, nchunk, nw, L.Cout, fan, L.wsum, st);
     }
 }
 

@@ -245,11 +245,40 @@ int nconv_bwd(const nconv_layer* L, const float* y, const float* cout, const flo
     const int fan = (L->Cin / L->groups) * L->KH * L->KW;
     if ((long)L->Cout * fan + 2L * L->Cout > 65535)
         return fail(-22, "nconv_bwd", "weight-gradient path supports at most 65535 weights per layer");
+    int nparts = 0;
+    const int defer = (flags & NCONV_BWD_DEFER_REDUCE) ? 1 : 0;
     nconv::BwdArgs a{y, cout, gy, gcout, gxa, gca, gxb, gcb, gw, gbias, (float*)workspace, workspace_bytes,
-                     (flags & NCONV_BWD_ACCUMULATE) ? 1 : 0};
+                     (flags & NCONV_BWD_ACCUMULATE) ? 1 : 0, defer, &nparts};
     const char* why = nullptr;
     int rc = nconv::launch_bwd(d, a, (hipStream_t)stream, &why);
-    return rc ? fail(rc, "nconv_bwd", why) : 0;
+    if (rc) return fail(rc, "nconv_bwd", why);
+    return defer ? nparts : 0;
+}
+
+int nconv_wgrad_reduce(int n, const nconv_layer* layers, void* const* workspaces, const int* nparts,
+                       float* const* gw, float* const* gbias, void* stream) {
+    const char* fn = "nconv_wgrad_reduce";
+    if (n < 1 || n > nconv::kMaxRedJobs) return fail(-22, fn, "n must be 1..16");
+    if (!layers || !workspaces || !nparts || !gw || !gbias) return fail(-22, fn, "null array");
+    nconv::RedJob jobs[nconv::kMaxRedJobs];
+    int m = 0;
+    for (int k = 0; k < n; ++k) {
+        if (nparts[k] < 0) return fail(-22, fn, "negative partial-row count");
+        if (nparts[k] == 0 || (!gw[k] && !gbias[k])) continue;
+        const nconv_layer* L = &layers[k];
+        if (!workspaces[k] || !L->wsum) return fail(-22, fn, "null workspace / wsum");
+        if (L->Cout <= 0 || L->Cin <= 0 || L->groups <= 0 || L->KH <= 0 || L->KW <= 0)
+            return fail(-22, fn, "invalid layer geometry");
+        const int fan = (L->Cin / L->groups) * L->KH * L->KW;
+        jobs[m++] = nconv::RedJob{(const float*)workspaces[k], L->wsum, gw[k], gbias[k], nparts[k],
+                                  L->Cout * fan, L->Cout, fan};
+    }
+    if (m == 0) return 0;
+    const char* why = nullptr;
+    const int rc = nconv::launch_wgrad_reduce_multi(m, jobs, (hipStream_t)stream, &why);
+    if (rc) return fail(rc, fn, why);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : fail(-5, fn, hipGetErrorString(e));
 }
 
 size_t nconv_dense_packed_floats(int kind, int Cin, int Cout) {

@@ -37,7 +37,20 @@ struct BwdArgs {
     float* ws;  // workspace
     size_t ws_bytes;
     int accumulate;  // 1: += into gxa/gca/gxb/gcb; 0: overwrite every element
+    int defer;       // 1: leave the weight gradient as partial rows (reduced by launch_wgrad_reduce_multi)
+    int* nparts;     // out (defer): the number of partial rows written
 };
+
+// One layer's deferred weight-gradient reduction (nconv_wgrad_reduce): its workspace's partial rows.
+struct RedJob {
+    const float* part;  // nblk partial rows of nw + 2 cout floats, then the kReduceSplit slice rows
+    const float* wsum;
+    float* gw;
+    float* gb;
+    int nblk, nw, cout, fan;
+};
+constexpr int kMaxRedJobs = 16;
+int launch_wgrad_reduce_multi(int n, const RedJob* jobs, hipStream_t st, const char** why);
 
 // Forward. Return 0, or a negative errno with *why set.
 int launch_fwd(const LayerDev& d, float* y, float* yc, float* py, float* pc, hipStream_t st, const char** why);

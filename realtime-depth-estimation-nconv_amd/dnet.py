@@ -22,8 +22,8 @@ import torch
 import torch.nn as nn
 
 from . import _lib, export, nconv
-from .nconv import (EnforcePos, NConv2d, _require_device, head_weights, layer_backward, layer_forward_head,
-                    layer_forward_pooled, layer_forward_raw, nconv_layer, phase_weights, weight_prep)
+from .nconv import (EnforcePos, NConv2d, WgradReduce, _require_device, head_weights, layer_backward,
+                    layer_forward_head, layer_forward_pooled, layer_forward_raw, nconv_layer, phase_weights, weight_prep)
 
 LAYERS = ("nconv1", "nconv2", "nconv_down1", "nconv_down2", "nconv_down3", "nconv4", "nconv5",
           "nconv6", "nconv7")
@@ -76,13 +76,15 @@ class DNETFn(torch.autograd.Function):
         # input gradients: G[k] = (gx, gc) of layer k's output
         G = [None] * 10
         sp = ctx.specs
+        red = WgradReduce()  # every layer's weight-gradient reduction in two launches at the end
 
         def bwd(k, a, b, ga, gb_, acc=False):
             xa, ca = X[a] if a else (S, None)
             xb, cb = X[b] if b else (None, None)
             gy, gco = G[k] if G[k] is not None else (g9, None)
             layer_backward(sp[k - 1], (xa, ca, xb, cb, *W[k - 1]), X[k][0], X[k][1], gy, gco,
-                           (*(ga or (None, None)), *(gb_ or (None, None))), gw[k - 1], gb[k - 1], accumulate=acc)
+                           (*(ga or (None, None)), *(gb_ or (None, None))), gw[k - 1], gb[k - 1], accumulate=acc,
+                           defer=red)
 
         G[8] = (e(X[8][0]), e(X[8][1]))
         bwd(9, 8, 0, G[8], None)                        # nconv7
@@ -99,7 +101,8 @@ class DNETFn(torch.autograd.Function):
         bwd(2, 1, 0, G[1], None)                        # nconv2
         gS = e(S) if need[1] else None
         layer_backward(sp[0], (S, None, None, None, *W[0]), X[1][0], X[1][1], G[1][0], G[1][1],
-                       (gS, None, None, None), gw[0], gb[0])  # nconv1 (threshold: c0 has no gradient)
+                       (gS, None, None, None), gw[0], gb[0], defer=red)  # nconv1 (threshold: c0 has no gradient)
+        red.run(S.device)
         out = [None, None, gS]
         for i in range(9):
             out += [gw[i], gb[i], None]

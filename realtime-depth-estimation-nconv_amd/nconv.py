@@ -218,10 +218,11 @@ class NConvLayerFn(torch.autograd.Function):
         return None, gxa, gca, gxb, gcb, gw, gb, None, None
 
 
-def layer_backward(spec: LayerSpec, inputs, y, co, gy, gco, gin, gw, gb, accumulate=False):
+def layer_backward(spec: LayerSpec, inputs, y, co, gy, gco, gin, gw, gb, accumulate=False, defer=None):
     """nconv_bwd of one fused layer: gin = (gxa, gca, gxb, gcb) (None: skip) overwritten, or added
     into with accumulate=True (NCONV_BWD_ACCUMULATE: a tensor consumed by two layers); gw, gb
-    overwritten (None: skip)."""
+    overwritten (None: skip). defer: a WgradReduce collecting the layer's weight-gradient partial
+    rows (NCONV_BWD_DEFER_REDUCE): gw / gb are then written by its run()."""
     xa, ca, xb, cb, weight, bias, wsum = inputs
     gxa, gca, gxb, gcb = gin
     dev = y.device
@@ -233,10 +234,40 @@ def layer_backward(spec: LayerSpec, inputs, y, co, gy, gco, gin, gw, gb, accumul
     lib = _lib.lib()
     ws_bytes = lib.nconv_bwd_workspace_bytes(_lib.ctypes.byref(L))
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+    flags = (_lib.BWD_ACCUMULATE if accumulate else 0) | (_lib.BWD_DEFER_REDUCE if defer is not None else 0)
     rc = lib.nconv_bwd(_lib.ctypes.byref(L), _lib.ptr(y), _lib.ptr(co), _lib.ptr(gy), _lib.ptr(gco),
                        _lib.ptr(gxa), _lib.ptr(gca), _lib.ptr(gxb), _lib.ptr(gcb), _lib.ptr(gw),
-                       _lib.ptr(gb), _lib.ptr(ws), ws_bytes, 1 if accumulate else 0, _lib.stream_handle(dev))
+                       _lib.ptr(gb), _lib.ptr(ws), ws_bytes, flags, _lib.stream_handle(dev))
+    if defer is not None and rc >= 0:
+        defer.add(L, ws, rc, gw, gb)
+        return
     _lib.check(rc, "nconv_bwd")
+
+
+class WgradReduce:
+    """The deferred weight-gradient reductions of one backward pass (nconv_wgrad_reduce): every
+    layer's partial rows reduced in two launches instead of two per layer. Keeps the layers'
+    workspaces alive until run()."""
+
+    def __init__(self):
+        self.jobs = []
+
+    def add(self, L, ws, nparts, gw, gb):
+        self.jobs.append((L, ws, nparts, gw, gb))
+
+    def run(self, device):
+        for k in range(0, len(self.jobs), 16):
+            jobs = self.jobs[k:k + 16]
+            n = len(jobs)
+            layers = (_lib.NconvLayer * n)(*[j[0] for j in jobs])
+            VP = _lib.ctypes.c_void_p * n
+            wss = VP(*[j[1].data_ptr() for j in jobs])
+            nparts = (_lib.ctypes.c_int * n)(*[j[2] for j in jobs])
+            gws = VP(*[(j[3].data_ptr() if j[3] is not None else None) for j in jobs])
+            gbs = VP(*[(j[4].data_ptr() if j[4] is not None else None) for j in jobs])
+            rc = _lib.lib().nconv_wgrad_reduce(n, layers, wss, nparts, gws, gbs, _lib.stream_handle(device))
+            _lib.check(rc, "nconv_wgrad_reduce")
+        self.jobs = []
 
 
 def kernel_plan(spec: LayerSpec, xa, ca, xb, cb, weight, bias, wsum):

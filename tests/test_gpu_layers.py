@@ -158,6 +158,29 @@ def test_bwd_accumulate_flag(nconv_amd, gpu, case, bwd_math):
         torch.testing.assert_close(a2, a0 + 1.5, rtol=1e-6, atol=1e-6)
     assert torch.equal(gw0, gw1) and torch.equal(gw0, gw2) and torch.equal(gb0, gb2)
 
+    # NCONV_BWD_DEFER_REDUCE + nconv_wgrad_reduce (here batched with a second, independent
+    # workspace of the same layer): bitwise the undeferred weight / bias gradients
+    ws2 = torch.empty(ws_bytes, dtype=torch.uint8, device=gpu)
+    outs = [torch.empty_like(v) if v is not None else None for v in t[:4]]
+    gws = [torch.full_like(t[4], float("nan")) for _ in range(2)]
+    gbs = [torch.full_like(t[5], float("nan")) for _ in range(2)]
+    nparts = []
+    for wsk in (ws, ws2):
+        rc = lib.lib().nconv_bwd(ctypes.byref(L), lib.ptr(y), lib.ptr(co), lib.ptr(gy), lib.ptr(gc),
+                                 *[lib.ptr(o) for o in outs], lib.ptr(gws[0]), lib.ptr(gbs[0]), lib.ptr(wsk),
+                                 ws_bytes, lib.BWD_DEFER_REDUCE, lib.stream_handle(gpu))
+        assert rc > 0, f"deferred nconv_bwd returned {rc}"
+        nparts.append(rc)
+    layers = (lib.NconvLayer * 2)(L, L)
+    VP = ctypes.c_void_p * 2
+    rc = lib.lib().nconv_wgrad_reduce(2, layers, VP(ws.data_ptr(), ws2.data_ptr()), (ctypes.c_int * 2)(*nparts),
+                                      VP(*[g.data_ptr() for g in gws]), VP(*[g.data_ptr() for g in gbs]),
+                                      lib.stream_handle(gpu))
+    lib.check(rc, "nconv_wgrad_reduce")
+    torch.cuda.synchronize()
+    for k in range(2):
+        assert torch.equal(gws[k], gw0) and torch.equal(gbs[k], gb0), "deferred reduction differs"
+
 
 def test_nconv2d_module_train_step(nconv_amd, gpu):
     """Standalone NConv2d (the reference's layer API): EnforcePos pre-hook + forward + backward."""

@@ -94,6 +94,28 @@ __global__ __launch_bounds__(256) void k(float* out, float a, int iters) {
             p = (p + 256) & 4095;
         }
         for (int i = 0; i < 8; ++i) s += acc[i][0] + acc[i][3];
+    } else if constexpr (KIND == 7) {  // wave-specialised: even waves f32 MFMA, odd waves v_pk_fma
+        // (NV bit 0: run the MFMA waves, bit 1: run the VALU waves) -- do the two pipes add?
+        const int wv = threadIdx.x >> 6;
+        if ((wv & 1) == 0 && (NV & 1)) {
+            f4 acc[4];
+            for (int i = 0; i < 4; ++i) acc[i] = (f4){x, x, x, x};
+            const float b = a * 0.5f;
+            for (int it = 0; it < iters; ++it)
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[i], 0, 0, 0);
+            for (int i = 0; i < 4; ++i) s += acc[i][0] + acc[i][3];
+        } else if ((wv & 1) == 1 && (NV & 2)) {
+            f2 acc[16];
+            for (int i = 0; i < 16; ++i) acc[i] = (f2){x + i, x - i};
+            const f2 w = {a, a};
+            for (int it = 0; it < iters * 8; ++it)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) acc[i] = __builtin_elementwise_fma(w, acc[i], w);
+            for (int i = 0; i < 16; ++i) s += acc[i].x + acc[i].y;
+        }
     }
     out[blockIdx.x * 256 + threadIdx.x] = s;
 }
@@ -151,6 +173,11 @@ int main() {
         run<6, 1>("4x4x1_16b, 1 ds_read_b32 per mfma", d, blocks, it / 4, 8 * 8 * 8.0);
         run<6, 2>("4x4x1_16b, 1 ds_read_b32 per 2", d, blocks, it / 4, 8 * 8 * 8.0);
         run<6, 4>("4x4x1_16b, 1 ds_read_b32 per 4", d, blocks, it / 4, 8 * 8 * 8.0);
+        // per thread-iteration averaged over the block: half the threads 32 MFMAs (32 flop/lane
+        // each), half 8*16 v_pk_fma (4 flop/lane each)
+        run<7, 1>("split waves: MFMA half only", d, blocks, it / 4, 0.5 * 32 * 32.0);
+        run<7, 2>("split waves: VALU half only", d, blocks, it / 4, 0.5 * 128 * 4.0);
+        run<7, 3>("split waves: both halves", d, blocks, it / 4, 0.5 * 32 * 32.0 + 0.5 * 128 * 4.0);
     }
     {
         const int K = 200;
