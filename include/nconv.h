@@ -139,9 +139,12 @@ int nconv_fwd(const nconv_layer* L, float* y, float* cout, void* stream);
  * first maximum wins, NaN propagates) into y_pool, cout_pool (B, Cout, Ho/2, Wo/2): the input of
  * the next down layer (models/step1.py:62-75), which then loads it with NCONV_LOAD_PLAIN instead
  * of re-reading and pooling the full-resolution tensors. Built for the tiled DNET layer shapes
- * (returns -EOPNOTSUPP otherwise). */
+ * (returns -EOPNOTSUPP otherwise). argmax (may be NULL; exact-fp32 tiled layers only): one byte
+ * per pooled element, the window slot (2*row + column) of y's first maximum in bits 0-1 and of
+ * cout's in bits 2-3 -- what nconv_bwd_ex routes the pooled tensors' gradient by (the indices of
+ * max_pool2d_with_indices, step1.py:62-75 under autograd). */
 int nconv_fwd_pooled(const nconv_layer* L, float* y, float* cout, float* y_pool, float* cout_pool,
-                     void* stream);
+                     unsigned char* argmax, void* stream);
 
 /* Inference-only fused head: nconv1 on the thresholded sparse depth (models/step1.py:53-57;
  * L1: Cin 1, Cout 8, 5x5, padding 2, NCONV_LOAD_THRESH) is evaluated while staging nconv2's input
@@ -208,6 +211,33 @@ size_t nconv_bwd_workspace_bytes(const nconv_layer* L);
 int nconv_bwd(const nconv_layer* L, const float* y, const float* cout, const float* gy,
               const float* gcout, float* gxa, float* gca, float* gxb, float* gcb, float* gw,
               float* gbias, void* workspace, size_t workspace_bytes, unsigned flags, void* stream);
+
+/* nconv_bwd with its tensors in one struct, plus the gradient arriving through a 2x2 max-pool of
+ * this layer's outputs (training: the next down layer read the y_pool / cout_pool that
+ * nconv_fwd_pooled materialised, so its input gradient is pooled-sized): gy_pool, gcout_pool
+ * (B, Cout, Ho/2, Wo/2) are added to gy / gcout at each window's first maximum, as pool_argmax
+ * (that nconv_fwd_pooled call's codes) records -- the max_pool2d backward of step1.py:62-75 summed
+ * with the other consumer's gradient, without a full-resolution read-modify-write. All three or
+ * none; with them, built for the exact-fp32 8->8 5x5 stride-1 layers with NCONV_LOAD_PLAIN
+ * (-EOPNOTSUPP otherwise). Returns as nconv_bwd. */
+typedef struct nconv_bwd_io {
+    const float* y;
+    const float* cout;
+    const float* gy;
+    const float* gcout;             /* may be NULL (= 0) */
+    float* gxa;
+    float* gca;
+    float* gxb;
+    float* gcb;
+    float* gw;
+    float* gbias;
+    const float* gy_pool;           /* optional pooled-output gradient (see above) */
+    const float* gcout_pool;
+    const unsigned char* pool_argmax;
+} nconv_bwd_io;
+
+int nconv_bwd_ex(const nconv_layer* L, const nconv_bwd_io* io, void* workspace, size_t workspace_bytes,
+                 unsigned flags, void* stream);
 
 /* Weight / bias gradients of n (1..16) layers whose nconv_bwd ran with NCONV_BWD_DEFER_REDUCE:
  * layers[k] the descriptor of that call (its weight normaliser wsum is read), workspaces[k] and

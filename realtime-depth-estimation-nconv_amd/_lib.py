@@ -42,6 +42,7 @@ EXPORTED = (
     "nconv_phase_weights",
     "nconv_bwd_workspace_bytes",
     "nconv_bwd",
+    "nconv_bwd_ex",
     "nconv_wgrad_reduce",
     "nconv_dense_packed_floats",
     "nconv_dense_pack",
@@ -74,6 +75,11 @@ class NconvLayer(ctypes.Structure):
                 ("thresh", ctypes.c_float), ("a", NconvSrc), ("b", NconvSrc),
                 ("weight", ctypes.c_void_p), ("bias", ctypes.c_void_p), ("wsum", ctypes.c_void_p),
                 ("math", ctypes.c_int), ("bwd_math", ctypes.c_int), ("waux", ctypes.c_void_p)]
+
+
+class NconvBwdIo(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in ("y", "cout", "gy", "gcout", "gxa", "gca", "gxb", "gcb", "gw",
+                                               "gbias", "gy_pool", "gcout_pool", "pool_argmax")]
 
 
 class NconvDenseConv(ctypes.Structure):
@@ -115,7 +121,7 @@ def _declare(lib):
     lib.nconv_fwd.restype = ctypes.c_int
     lib.nconv_fwd.argtypes = [ctypes.POINTER(NconvLayer), P, P, P]
     lib.nconv_fwd_pooled.restype = ctypes.c_int
-    lib.nconv_fwd_pooled.argtypes = [ctypes.POINTER(NconvLayer), P, P, P, P, P]
+    lib.nconv_fwd_pooled.argtypes = [ctypes.POINTER(NconvLayer), P, P, P, P, P, P]
     lib.nconv_fwd_head.restype = ctypes.c_int
     lib.nconv_fwd_head.argtypes = [ctypes.POINTER(NconvLayer), ctypes.POINTER(NconvLayer), P, P, P, P, P]
     lib.nconv_head_weights.restype = ctypes.c_int
@@ -134,6 +140,9 @@ def _declare(lib):
     lib.nconv_bwd.restype = ctypes.c_int
     lib.nconv_bwd.argtypes = [ctypes.POINTER(NconvLayer), P, P, P, P, P, P, P, P, P, P, P,
                               ctypes.c_size_t, ctypes.c_uint, P]
+    lib.nconv_bwd_ex.restype = ctypes.c_int
+    lib.nconv_bwd_ex.argtypes = [ctypes.POINTER(NconvLayer), ctypes.POINTER(NconvBwdIo), P, ctypes.c_size_t,
+                                 ctypes.c_uint, P]
     lib.nconv_wgrad_reduce.restype = ctypes.c_int
     lib.nconv_wgrad_reduce.argtypes = [ctypes.c_int, ctypes.POINTER(NconvLayer), P, P, P, P, P]
     I = ctypes.c_int

@@ -32,15 +32,18 @@ constexpr int pick_chunk(int n, int plane_f2, int budget) {
 // padding) is computed once per workgroup; per output channel the four saved planes (gy, gcout,
 // y, cout) are read with buffer loads and {gN, gD} are formed at store time. Elements are dealt
 // to the 256 threads row-major; slots past the tile go to a dump slot after the plane.
-template <int OHT, int OWT, int OWP>
+template <int OHT, int OWT, int OWP, bool GP = false>
 struct GTileStager {
     static constexpr int NT = OHT * OWT;
     static constexpr int NE = (NT + 255) / 256;
     static constexpr int PLANE = OHT * OWP;
     static constexpr int PLANE_STRIDE = PLANE + 2;
+    static constexpr int NV = GP ? 7 : 4;  // gy, gcout, y, cout (+ pooled gy, gcout, argmax code)
     static constexpr unsigned OOB = 0x80000000u;
     unsigned lofs[NE];
     unsigned go[NE];
+    unsigned gpo[GP ? NE : 1];  // pooled element offsets, window slots (GP)
+    unsigned gsub[GP ? NE : 1];
 
     __device__ __forceinline__ void init(const nconv_layer& L, int oh0, int ow0, int tid) {
 #pragma unroll
@@ -51,12 +54,16 @@ struct GTileStager {
             const bool in = e < NT && (unsigned)oh < (unsigned)L.Ho && (unsigned)ow < (unsigned)L.Wo;
             lofs[k] = e < NT ? r * OWP + col : PLANE;
             go[k] = in ? (unsigned)(oh * L.Wo + ow) * 4u : OOB;
+            if constexpr (GP) {
+                gpo[k] = in ? pool_elem_off(oh, ow, L.Ho >> 1, L.Wo >> 1, OOB) : OOB;
+                gsub[k] = (unsigned)(((oh & 1) << 1) | (ow & 1));
+            }
         }
     }
 
-    // raw (gy, gcout, y, cout) of output channel o of image b, no wait
+    // raw (gy, gcout, y, cout [, pooled gy, pooled gcout, code]) of output channel o of image b, no wait
     __device__ __forceinline__ void load(const nconv_layer& L, const BwdArgs& a, int b, int o,
-                                         float (&v)[4][NE]) const {
+                                         float (&v)[NV][NE]) const {
         const int plane = L.Ho * L.Wo;
         const size_t base = ((size_t)b * L.Cout + o) * plane;
         const __amdgpu_buffer_rsrc_t rgy = plane_rsrc(a.gy + base, plane * 4);
@@ -76,14 +83,29 @@ struct GTileStager {
 #pragma unroll
             for (int k = 0; k < NE; ++k) v[1][k] = 0.f;
         }
+        if constexpr (GP) {
+            const int pplane = (L.Ho >> 1) * (L.Wo >> 1);
+            const size_t pbase = ((size_t)b * L.Cout + o) * pplane;
+            const __amdgpu_buffer_rsrc_t rpy = plane_rsrc(a.gpy + pbase, pplane * 4);
+            const __amdgpu_buffer_rsrc_t rpc = plane_rsrc(a.gpc + pbase, pplane * 4);
+            const __amdgpu_buffer_rsrc_t rpa = plane_rsrc((const float*)(a.parg + pbase), pplane);
+#pragma unroll
+            for (int k = 0; k < NE; ++k) {
+                v[4][k] = ld_f32(rpy, gpo[k]);
+                v[5][k] = ld_f32(rpc, gpo[k]);
+                v[6][k] = __builtin_bit_cast(float, ld_u8(rpa, gpo[k] >> 2));
+            }
+        }
     }
 
-    __device__ __forceinline__ void store(const nconv_layer& L, int o, const float (&v)[4][NE], f2* t) const {
+    __device__ __forceinline__ void store(const nconv_layer& L, int o, const float (&v)[NV][NE], f2* t) const {
         const float bo = L.bias[o], so = L.wsum[o];
 #pragma unroll
         for (int k = 0; k < NE; ++k) {
+            float gy = v[0][k], gco = v[1][k];
+            if constexpr (GP) pool_route(gy, gco, v[4][k], v[5][k], __builtin_bit_cast(unsigned, v[6][k]), gsub[k]);
             float gN, gD;  // zero padding: gy = gcout = y = cout = 0 gives gN = gD = 0
-            nconv_grad_nd(v[0][k], v[1][k], v[2][k], v[3][k], L.eps, bo, so, gN, gD);
+            nconv_grad_nd(gy, gco, v[2][k], v[3][k], L.eps, bo, so, gN, gD);
             t[lofs[k]] = (f2){gN, gD};
         }
     }
@@ -109,10 +131,10 @@ struct VecOf<2> { typedef f2 T; };
 // One (output channel o, kernel row kh) step per iteration of the inner loop, not unrolled: its
 // Cin*K weights ride SGPRs. The {gN, gD} planes of the output channels are staged one at a time
 // into two LDS buffers, the loads two channels ahead (as the forward's input planes).
-template <int CIN, int COUT, int K, int MODE>
+template <int CIN, int COUT, int K, int MODE, bool GP = false>
 __global__ __launch_bounds__(kT) void dgrad_tiled(LayerDev d, BwdArgs a, float* tmp_x, float* tmp_c) {
     using C = DgCfg<CIN, K>;
-    using GS = GTileStager<C::OHT, C::OWT, C::OWP>;
+    using GS = GTileStager<C::OHT, C::OWT, C::OWP, GP>;
     constexpr int P = C::P;
     __shared__ __attribute__((aligned(16))) f2 tile[2 * GS::PLANE_STRIDE];
     const nconv_layer& L = d.L;
@@ -157,7 +179,7 @@ __global__ __launch_bounds__(kT) void dgrad_tiled(LayerDev d, BwdArgs a, float* 
 
     GS gs;
     gs.init(L, oh0, ow0, tid);
-    float va[4][GS::NE], vb[4][GS::NE];
+    float va[GS::NV][GS::NE], vb[GS::NV][GS::NE];
     gs.load(L, a, b, 0, va);
     if (COUT > 1) gs.load(L, a, b, 1, vb);
 #pragma unroll 1
@@ -940,7 +962,7 @@ struct WmCfg {
 #define NCONV_WM_WAVES 3
 #endif
 #define NCONV_WM_ATTR __attribute__((amdgpu_waves_per_eu(NCONV_WM_WAVES, 8)))
-template <int CIN, int COUT, int K, int MODE>
+template <int CIN, int COUT, int K, int MODE, bool GP = false>
 __global__ __launch_bounds__(kT) NCONV_WM_ATTR void wgrad_mfma(LayerDev d, BwdArgs a, float* part, int nstrip, int nseg,
                                                  int seg_rows) {
     using C = WmCfg<CIN, COUT, K>;
@@ -980,7 +1002,8 @@ __global__ __launch_bounds__(kT) NCONV_WM_ATTR void wgrad_mfma(LayerDev d, BwdAr
 
     // ---- staging: one input row (CIN x 64 columns) and one g row (COUT x (64+K-1) columns) ----
     float px[C::CPW], pc[C::CPW];
-    float gq[C::OPW][2][4];
+    constexpr int NG = GP ? 7 : 4;  // gy, gco, y, cout (+ pooled gy, gcout, argmax code)
+    float gq[C::OPW][2][NG];
     float gb_acc[C::OPW], gs_acc[C::OPW];
 #pragma unroll
     for (int kk = 0; kk < C::OPW; ++kk) gb_acc[kk] = gs_acc[kk] = 0.f;
@@ -1006,6 +1029,7 @@ __global__ __launch_bounds__(kT) NCONV_WM_ATTR void wgrad_mfma(LayerDev d, BwdAr
         }
     };
     const int plane = L.Ho * L.Wo;
+    const int Hp = L.Ho >> 1, Wp = L.Wo >> 1, pplane = Hp * Wp;
     auto load_g = [&](int oh) {
 #pragma unroll
         for (int kk = 0; kk < C::OPW; ++kk) {
@@ -1024,6 +1048,14 @@ __global__ __launch_bounds__(kT) NCONV_WM_ATTR void wgrad_mfma(LayerDev d, BwdAr
                 gq[kk][p][1] = ld_f32(rco, off);
                 gq[kk][p][2] = ld_f32(ry, off);
                 gq[kk][p][3] = a.gco ? ld_f32(plane_rsrc(a.gco + base, plane * 4), off) : 0.f;
+                if constexpr (GP) {
+                    const size_t pbase = ((size_t)b * COUT + o) * pplane;
+                    const unsigned po = in ? pool_elem_off(oh, ow, Hp, Wp, OOB) : OOB;
+                    gq[kk][p][4] = ld_f32(plane_rsrc(a.gpy + pbase, pplane * 4), po);
+                    gq[kk][p][5] = ld_f32(plane_rsrc(a.gpc + pbase, pplane * 4), po);
+                    gq[kk][p][6] = __builtin_bit_cast(
+                        float, ld_u8(plane_rsrc((const float*)(a.parg + pbase), pplane), po >> 2));
+                }
             }
         }
     };
@@ -1035,7 +1067,7 @@ __global__ __launch_bounds__(kT) NCONV_WM_ATTR void wgrad_mfma(LayerDev d, BwdAr
         bias_o[kk] = L.bias[w + 4 * kk];
         wsum_o[kk] = L.wsum[w + 4 * kk];
     }
-    auto store_g = [&](int buf) {
+    auto store_g = [&](int buf, int oh_cur) {
 #pragma unroll
         for (int kk = 0; kk < C::OPW; ++kk) {
             const int o = w + 4 * kk;
@@ -1044,14 +1076,20 @@ __global__ __launch_bounds__(kT) NCONV_WM_ATTR void wgrad_mfma(LayerDev d, BwdAr
             for (int p = 0; p < 2; ++p) {
                 const int col = p * 64 + lane;
                 if (p == 1 && lane >= K - 1) continue;
+                float gy = gq[kk][p][0], gco = gq[kk][p][3];
+                if constexpr (GP) {
+                    const int ow = ow0 - (K - 1) + col;
+                    pool_route(gy, gco, gq[kk][p][4], gq[kk][p][5], __builtin_bit_cast(unsigned, gq[kk][p][6]),
+                               (unsigned)(((oh_cur & 1) << 1) | (ow & 1)));
+                }
                 float gN, gD;
-                nconv_grad_nd(gq[kk][p][0], gq[kk][p][3], gq[kk][p][2], gq[kk][p][1], L.eps, bo, so, gN, gD);
+                nconv_grad_nd(gy, gco, gq[kk][p][2], gq[kk][p][1], L.eps, bo, so, gN, gD);
                 float* g = lds + C::G_OFF + buf * C::GBUF + o * C::GP + col;
                 g[0] = gN;
                 g[C::GPART] = gD;
                 if (col >= K - 1) {  // this strip's own columns: the bias / wsum gradient sums
-                    gb_acc[kk] += gq[kk][p][0];
-                    gs_acc[kk] = fmaf(gq[kk][p][3], gq[kk][p][1], gs_acc[kk]);
+                    gb_acc[kk] += gy;
+                    gs_acc[kk] = fmaf(gco, gq[kk][p][1], gs_acc[kk]);
                 }
             }
         }
@@ -1075,7 +1113,7 @@ __global__ __launch_bounds__(kT) NCONV_WM_ATTR void wgrad_mfma(LayerDev d, BwdAr
     for (int oh = r0; oh < r1; ++oh) {
         const int buf = (oh - r0) & 1;
         store_in(oh - L.PH + K - 1);
-        store_g(buf);
+        store_g(buf, oh);
         __syncthreads();
         {   // next row's loads in flight during this row's MFMAs (re-reads the last row at the end)
             const int nx = oh + 1 < r1 ? oh + 1 : oh;
@@ -1255,7 +1293,7 @@ void plan_bwd(const nconv_layer& L, int* dgrad, int* wgrad) {
 // Returns 0, or -EIO when the bf16 weight-gradient grid would not fit the workspace (it cannot:
 // its strips are wider than wgrad_mfma's, for which the workspace is sized; checked anyway, so
 // a bf16 request never silently runs another kernel).
-template <int CIN, int COUT, int K, int MODE>
+template <int CIN, int COUT, int K, int MODE, bool GP = false>
 static int go_bwd_tiled(const LayerDev& d, const BwdArgs& a, float* part, float* tx, float* tc,
                         hipStream_t st) {
     const nconv_layer& L = d.L;
@@ -1276,7 +1314,7 @@ static int go_bwd_tiled(const LayerDev& d, const BwdArgs& a, float* part, float*
                     hipLaunchKernelGGL((dgrad_tiled<CIN, COUT, K, MODE>), g, dim3(kT), 0, st, d, a, tx, tc);
                 }
             } else {
-                hipLaunchKernelGGL((dgrad_tiled<CIN, COUT, K, MODE>), g, dim3(kT), 0, st, d, a, tx, tc);
+                hipLaunchKernelGGL((dgrad_tiled<CIN, COUT, K, MODE, GP>), g, dim3(kT), 0, st, d, a, tx, tc);
             }
         }
     }
@@ -1288,10 +1326,10 @@ static int go_bwd_tiled(const LayerDev& d, const BwdArgs& a, float* part, float*
             const int nw = COUT * CIN * K * K;
             launch_wgrad_reduce(a, part, nblk, nw, COUT, CIN * K * K, L.wsum, st);
         } else if (a.gw || a.gb) {
-            const int per_cu = dev_occupancy((const void*)wgrad_mfma<CIN, COUT, K, MODE>, kT, 0);
+            const int per_cu = dev_occupancy((const void*)wgrad_mfma<CIN, COUT, K, MODE, GP>, kT, 0);
             const int resident = device_cus() * (per_cu < kMfmaMaxPerCu ? per_cu : kMfmaMaxPerCu);
             const WmGrid g = wm_grid(L, kMfmaRounds * resident);
-            hipLaunchKernelGGL((wgrad_mfma<CIN, COUT, K, MODE>), dim3(g.nblk), dim3(kT), 0, st, d, a, part,
+            hipLaunchKernelGGL((wgrad_mfma<CIN, COUT, K, MODE, GP>), dim3(g.nblk), dim3(kT), 0, st, d, a, part,
                                g.nstrip, g.nseg, g.seg_rows);
             const int nw = COUT * CIN * K * K;
             launch_wgrad_reduce(a, part, (int)g.nblk, nw, COUT, CIN * K * K, L.wsum, st);
@@ -1351,6 +1389,16 @@ int launch_bwd(const LayerDev& d, const BwdArgs& a, hipStream_t st, const char**
     float* tc = tx + (size_t)L.B * L.b.C * L.H * L.W;
     const bool up = L.load_mode == NCONV_LOAD_UPCAT_SKIP_FIRST || L.load_mode == NCONV_LOAD_UPCAT_UP_FIRST;
 
+    if (a.gpy || a.gpc || a.parg) {  // pooled-gradient routing: built for the 8->8 5x5 exact-fp32 layers
+        if (!(a.gpy && a.gpc && a.parg) || path != kTiled || L.Cin != 8 || L.Cout != 8 || L.KH != 5 ||
+            L.load_mode != NCONV_LOAD_PLAIN || L.bwd_math != NCONV_MATH_FP32 || L.Ho < 2 || L.Wo < 2) {
+            *why = "pooled-output gradient needs gy_pool, gcout_pool and the argmax codes, on an exact-fp32 "
+                   "8->8 5x5 stride-1 layer with plain loads";
+            return -95;
+        }
+        go_bwd_tiled<8, 8, 5, NCONV_LOAD_PLAIN, true>(d, a, part, tx, tc, st);
+        return last_err(why);
+    }
     if (path == kTiled) {
         const int m = L.load_mode;
         int rc;

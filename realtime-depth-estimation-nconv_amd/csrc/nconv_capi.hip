@@ -124,17 +124,17 @@ int nconv_fwd(const nconv_layer* L, float* y, float* cout, void* stream) {
     if (const char* why = validate(L, true)) return fail(-22, "nconv_fwd", why);
     if (!y || !cout) return fail(-22, "nconv_fwd", "null output");
     const char* why = nullptr;
-    int rc = nconv::launch_fwd(make_dev(L), y, cout, nullptr, nullptr, (hipStream_t)stream, &why);
+    int rc = nconv::launch_fwd(make_dev(L), y, cout, nullptr, nullptr, nullptr, (hipStream_t)stream, &why);
     return rc ? fail(rc, "nconv_fwd", why) : 0;
 }
 
 int nconv_fwd_pooled(const nconv_layer* L, float* y, float* cout, float* y_pool, float* cout_pool,
-                     void* stream) {
+                     unsigned char* argmax, void* stream) {
     if (const char* why = validate(L, true)) return fail(-22, "nconv_fwd_pooled", why);
     if (!y || !cout || !y_pool || !cout_pool) return fail(-22, "nconv_fwd_pooled", "null output");
     if (L->Ho < 2 || L->Wo < 2) return fail(-22, "nconv_fwd_pooled", "output too small to pool");
     const char* why = nullptr;
-    int rc = nconv::launch_fwd(make_dev(L), y, cout, y_pool, cout_pool, (hipStream_t)stream, &why);
+    int rc = nconv::launch_fwd(make_dev(L), y, cout, y_pool, cout_pool, argmax, (hipStream_t)stream, &why);
     return rc ? fail(rc, "nconv_fwd_pooled", why) : 0;
 }
 
@@ -234,11 +234,11 @@ size_t nconv_bwd_workspace_bytes(const nconv_layer* L) {
     return nconv::bwd_workspace_bytes(make_dev(L));
 }
 
-int nconv_bwd(const nconv_layer* L, const float* y, const float* cout, const float* gy,
-              const float* gcout, float* gxa, float* gca, float* gxb, float* gcb, float* gw,
-              float* gbias, void* workspace, size_t workspace_bytes, unsigned flags, void* stream) {
+int nconv_bwd_ex(const nconv_layer* L, const nconv_bwd_io* io, void* workspace, size_t workspace_bytes,
+                 unsigned flags, void* stream) {
     if (const char* why = validate(L, true)) return fail(-22, "nconv_bwd", why);
-    if (!y || !cout || !gy) return fail(-22, "nconv_bwd", "null y/cout/gy");
+    if (!io) return fail(-22, "nconv_bwd", "null io");
+    if (!io->y || !io->cout || !io->gy) return fail(-22, "nconv_bwd", "null y/cout/gy");
     const LayerDev d = make_dev(L);
     const size_t need = nconv::bwd_workspace_bytes(d);
     if (need && (!workspace || workspace_bytes < need)) return fail(-22, "nconv_bwd", "workspace too small");
@@ -247,12 +247,20 @@ int nconv_bwd(const nconv_layer* L, const float* y, const float* cout, const flo
         return fail(-22, "nconv_bwd", "weight-gradient path supports at most 65535 weights per layer");
     int nparts = 0;
     const int defer = (flags & NCONV_BWD_DEFER_REDUCE) ? 1 : 0;
-    nconv::BwdArgs a{y, cout, gy, gcout, gxa, gca, gxb, gcb, gw, gbias, (float*)workspace, workspace_bytes,
-                     (flags & NCONV_BWD_ACCUMULATE) ? 1 : 0, defer, &nparts};
+    nconv::BwdArgs a{io->y, io->cout, io->gy, io->gcout, io->gxa, io->gca, io->gxb, io->gcb, io->gw, io->gbias,
+                     (float*)workspace, workspace_bytes, (flags & NCONV_BWD_ACCUMULATE) ? 1 : 0, defer, &nparts,
+                     io->gy_pool, io->gcout_pool, io->pool_argmax};
     const char* why = nullptr;
     int rc = nconv::launch_bwd(d, a, (hipStream_t)stream, &why);
     if (rc) return fail(rc, "nconv_bwd", why);
     return defer ? nparts : 0;
+}
+
+int nconv_bwd(const nconv_layer* L, const float* y, const float* cout, const float* gy,
+              const float* gcout, float* gxa, float* gca, float* gxb, float* gcb, float* gw,
+              float* gbias, void* workspace, size_t workspace_bytes, unsigned flags, void* stream) {
+    const nconv_bwd_io io{y, cout, gy, gcout, gxa, gca, gxb, gcb, gw, gbias, nullptr, nullptr, nullptr};
+    return nconv_bwd_ex(L, &io, workspace, workspace_bytes, flags, stream);
 }
 
 int nconv_wgrad_reduce(int n, const nconv_layer* layers, void* const* workspaces, const int* nparts,

@@ -337,6 +337,24 @@ __device__ __forceinline__ float ld_f32s(__amdgpu_buffer_rsrc_t r, unsigned off,
     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, soff, 0));
 }
 
+__device__ __forceinline__ unsigned ld_u8(__amdgpu_buffer_rsrc_t r, unsigned off) {
+    return __builtin_amdgcn_raw_buffer_load_b8(r, off, 0, 0);
+}
+
+// Pooled-gradient routing (training backward of a layer whose outputs feed a 2x2 max-pool that
+// nconv_fwd_pooled materialised with its argmax codes): the output element at window slot `sub`
+// (2*row + column) receives the pooled element's gradient when it is that window's first maximum
+// (y's slot in code bits 0-1, cout's in bits 2-3), +0 otherwise -- max_pool2d's backward added to
+// the other consumer's gradient. Byte offset of the pooled element, or OOB past the pooled plane
+// (odd last rows / columns, which no window covers: the load then returns 0).
+__device__ __forceinline__ unsigned pool_elem_off(int oh, int ow, int Hp, int Wp, unsigned oob) {
+    return ((oh >> 1) < Hp && (ow >> 1) < Wp) ? (unsigned)((oh >> 1) * Wp + (ow >> 1)) * 4u : oob;
+}
+__device__ __forceinline__ void pool_route(float& gy, float& gco, float gpy, float gpc, unsigned code, unsigned sub) {
+    gy += ((code & 3u) == sub) ? gpy : 0.f;
+    gco += (((code >> 2) & 3u) == sub) ? gpc : 0.f;
+}
+
 __device__ __forceinline__ void st_f32(__amdgpu_buffer_rsrc_t r, unsigned off, float v) {
     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, (int)off, 0, 0);
 }

@@ -195,16 +195,23 @@ __global__ __launch_bounds__(NTH) void fwd_tiled(LayerDev d, float* __restrict__
                 const size_t pofs = ((size_t)b * COUT + o) * pplane;
                 const __amdgpu_buffer_rsrc_t rpy = plane_rsrc(t.py + pofs, ppbytes);
                 const __amdgpu_buffer_rsrc_t rpc = plane_rsrc(t.pc + pofs, ppbytes);
+                // with t.parg: each window's first-maximum slots (y in bits 0-1, cout in bits 2-3,
+                // slot = 2*row + column), what the training backward routes the pooled gradient by
+                unsigned char* parg = t.parg ? t.parg + pofs : nullptr;
                 if constexpr (C::P == 1) {  // the window's right column sits in lane l^1
                     const float ya = shfl_xor1(yv[0]), ca = shfl_xor1(cv[0]);
                     const float yd = shfl_xor1(yb[0]), cd = shfl_xor1(cb[0]);
-                    st_f32(rpy, po[0], pool4v(yv[0], ya, yb[0], yd));
-                    st_f32(rpc, po[0], pool4v(cv[0], ca, cb[0], cd));
+                    int ay, ac;
+                    st_f32(rpy, po[0], pool4(yv[0], ya, yb[0], yd, ay));
+                    st_f32(rpc, po[0], pool4(cv[0], ca, cb[0], cd, ac));
+                    if (parg && po[0] != OOB) parg[po[0] >> 2] = (unsigned char)(ay | (ac << 2));
                 } else {
 #pragma unroll
                     for (int h = 0; h < C::P / 2; ++h) {
-                        st_f32(rpy, po[h], pool4v(yv[2 * h], yv[2 * h + 1], yb[2 * h], yb[2 * h + 1]));
-                        st_f32(rpc, po[h], pool4v(cv[2 * h], cv[2 * h + 1], cb[2 * h], cb[2 * h + 1]));
+                        int ay, ac;
+                        st_f32(rpy, po[h], pool4(yv[2 * h], yv[2 * h + 1], yb[2 * h], yb[2 * h + 1], ay));
+                        st_f32(rpc, po[h], pool4(cv[2 * h], cv[2 * h + 1], cb[2 * h], cb[2 * h + 1], ac));
+                        if (parg && po[h] != OOB) parg[po[h] >> 2] = (unsigned char)(ay | (ac << 2));
                     }
                 }
             }
@@ -412,13 +419,20 @@ int plan_fwd(const nconv_layer& L) {
     return fwd_tiled_shape(L) ? NCONV_KERNEL_TILED_FP32 : NCONV_KERNEL_GENERIC;
 }
 
-int launch_fwd(const LayerDev& d, float* y, float* yc, float* py, float* pc, hipStream_t st, const char** why) {
+int launch_fwd(const LayerDev& d, float* y, float* yc, float* py, float* pc, unsigned char* parg, hipStream_t st,
+               const char** why) {
     const nconv_layer& L = d.L;
     TailArgs t{};
     t.py = py;
     t.pc = pc;
-    if (launch_fwd_mfma(d, y, yc, t, false, st)) return last_launch(why);
-    if (launch_fwd_phase(d, y, yc, t, false, st)) return last_launch(why);
+    t.parg = parg;
+    if (!parg) {  // the argmax codes are written by the tiled fp32 kernels only
+        if (launch_fwd_mfma(d, y, yc, t, false, st)) return last_launch(why);
+        if (launch_fwd_phase(d, y, yc, t, false, st)) return last_launch(why);
+    } else if (!fwd_tiled_shape(L) || L.math != NCONV_MATH_FP32) {
+        *why = "pooling argmax codes need an exact-fp32 tiled layer (8->8 5x5, 1->8 5x5 threshold, 16->8 3x3)";
+        return -95;
+    }
     if (simple_geometry(L)) {
 #define NCONV_TRY(CIN, COUT, K, MODE)                                                       \
     if (L.Cin == CIN && L.Cout == COUT && L.KH == K && L.load_mode == MODE) {               \

@@ -15,6 +15,7 @@ struct TailArgs {
     float* out_c;
     float* py;  // optional 2x2 max-pooled copies of y / cout (non-tail launches), (B,Cout,Ho/2,Wo/2)
     float* pc;
+    unsigned char* parg;  // optional (with py): per pooled element the two first-maximum slots
     // fused head (nconv_fwd_head): nconv1 evaluated while staging nconv2's input
     const float* s_in;  // sparse depth (B, 1, H, W)
     const float* w1;    // nconv1 weight (8, 1, 5, 5), bias, s[o]
@@ -39,6 +40,11 @@ struct BwdArgs {
     int accumulate;  // 1: += into gxa/gca/gxb/gcb; 0: overwrite every element
     int defer;       // 1: leave the weight gradient as partial rows (reduced by launch_wgrad_reduce_multi)
     int* nparts;     // out (defer): the number of partial rows written
+    // optional: gradient of the 2x2 max-pooled outputs (B, Cout, Ho/2, Wo/2) and the pooling argmax
+    // codes (nconv_fwd_pooled), routed into gy / gcout while {gN, gD} are formed (pool_route)
+    const float* gpy;
+    const float* gpc;
+    const unsigned char* parg;
 };
 
 // One layer's deferred weight-gradient reduction (nconv_wgrad_reduce): its workspace's partial rows.
@@ -53,7 +59,8 @@ constexpr int kMaxRedJobs = 16;
 int launch_wgrad_reduce_multi(int n, const RedJob* jobs, hipStream_t st, const char** why);
 
 // Forward. Return 0, or a negative errno with *why set.
-int launch_fwd(const LayerDev& d, float* y, float* yc, float* py, float* pc, hipStream_t st, const char** why);
+int launch_fwd(const LayerDev& d, float* y, float* yc, float* py, float* pc, unsigned char* parg, hipStream_t st,
+               const char** why);
 bool fwd_mfma_supported(const nconv_layer& L, bool tail, bool pool);
 bool launch_fwd_mfma(const LayerDev& d, float* y, float* yc, const TailArgs& t, bool tail, hipStream_t st);
 // exact-fp32 UPCAT layers with the upsampled half at native resolution (nconv_fwd_phase.hip)

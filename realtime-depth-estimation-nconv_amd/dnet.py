@@ -16,6 +16,7 @@ output directly. EnforcePos pre-hooks of all nine layers are applied in one laun
 mode, before any layer runs (the reference applies each right before its layer; the layers share
 no weights, so the results are identical).
 """
+import dataclasses
 import os
 
 import torch
@@ -31,11 +32,19 @@ LAYERS = ("nconv1", "nconv2", "nconv_down1", "nconv_down2", "nconv_down3", "ncon
 
 class DNETFn(torch.autograd.Function):
     """Autograd node of the whole 9-layer DNET graph (training path). The backward runs the layer
-    backwards in reverse order itself, so that the gradients of the three tensors two layers read
-    (nconv2's output: down1 and nconv6; down1's: down2 and nconv5; down2's: down3 and nconv4) are
-    summed inside the second consumer's dgrad kernel (NCONV_BWD_ACCUMULATE) instead of by separate
-    PyTorch adds over freshly allocated buffers. Inputs: specs, capture (dict or None), S, then
-    (weight, bias, s[o]) of each layer in LAYERS order; outputs: nconv7's (uncropped) y, cout."""
+    backwards in reverse order itself. Inputs: specs, capture (dict or None), S, then (weight, bias,
+    s[o]) of each layer in LAYERS order, then the phase weights; outputs: nconv7's (uncropped) y,
+    cout.
+
+    Three tensors are read by two layers each (nconv2's output: down1 through the 2x2 max-pool and
+    nconv6; down1's: down2 and nconv5; down2's: down3 and nconv4). With exact-fp32 forward and
+    backward (the default) the pool is materialised: nconv2 / down1 / down2 write their pooled
+    outputs and the pooling argmax codes in the same launch (nconv_fwd_pooled), the down layers read
+    the pooled copies with plain loads, their input gradients stay pooled-sized, and each producer's
+    backward adds them to the other consumer's full-resolution gradient at the argmax while forming
+    {gN, gD} (nconv_bwd_ex) -- no full-resolution read-modify-write and no argmax recomputation.
+    With a bf16 backward the down layers pool while loading and their input gradients are added
+    into the full-resolution gradient (NCONV_BWD_ACCUMULATE)."""
 
     @staticmethod
     def forward(ctx, specs, capture, S, *p):
@@ -45,11 +54,21 @@ class DNETFn(torch.autograd.Function):
         wph = p[27] if len(p) > 27 and p[27] is not None else None
         w4, w5, w6 = (None, None, None) if wph is None else tuple(wph)
         sp = specs
+        pooled = _materialise_pool(S)
         x1, c1 = layer_forward_raw(sp[0], S, None, None, None, *W[0])
-        x2, c2 = layer_forward_raw(sp[1], x1, c1, None, None, *W[1])
-        x3, c3 = layer_forward_raw(sp[2], x2, c2, None, None, *W[2])
-        x4, c4 = layer_forward_raw(sp[3], x3, c3, None, None, *W[3])
-        x5, c5 = layer_forward_raw(sp[4], x4, c4, None, None, *W[4])
+        if pooled:
+            spp = [dataclasses.replace(sp[k], mode=_lib.PLAIN) for k in (2, 3, 4)]
+            x2, c2, p2x, p2c, a2 = layer_forward_pooled(sp[1], x1, c1, None, None, *W[1], argmax=True)
+            x3, c3, p3x, p3c, a3 = layer_forward_pooled(spp[0], p2x, p2c, None, None, *W[2], argmax=True)
+            x4, c4, p4x, p4c, a4 = layer_forward_pooled(spp[1], p3x, p3c, None, None, *W[3], argmax=True)
+            x5, c5 = layer_forward_raw(spp[2], p4x, p4c, None, None, *W[4])
+            pools = (p2x, p2c, a2, p3x, p3c, a3, p4x, p4c, a4)
+        else:
+            x2, c2 = layer_forward_raw(sp[1], x1, c1, None, None, *W[1])
+            x3, c3 = layer_forward_raw(sp[2], x2, c2, None, None, *W[2])
+            x4, c4 = layer_forward_raw(sp[3], x3, c3, None, None, *W[3])
+            x5, c5 = layer_forward_raw(sp[4], x4, c4, None, None, *W[4])
+            pools = ()
         x6, c6 = layer_forward_raw(sp[5], x4, c4, x5, c5, *W[5], wphase=w4)
         x7, c7 = layer_forward_raw(sp[6], x3, c3, x6, c6, *W[6], wphase=w5)
         x8, c8 = layer_forward_raw(sp[7], x2, c2, x7, c7, *W[7], wphase=w6)
@@ -58,15 +77,17 @@ class DNETFn(torch.autograd.Function):
             capture.update(down1=(x2.detach(), c2.detach()), down2=(x3.detach(), c3.detach()),
                            down3=(x4.detach(), c4.detach()))
         ctx.specs = specs
+        ctx.pooled = pooled
         ctx.n_extra = len(p) - 27
-        ctx.save_for_backward(S, *p[:27], x1, c1, x2, c2, x3, c3, x4, c4, x5, c5, x6, c6, x7, c7, x8, c8, x9, c9)
+        ctx.save_for_backward(S, *p[:27], x1, c1, x2, c2, x3, c3, x4, c4, x5, c5, x6, c6, x7, c7, x8, c8, x9, c9,
+                              *pools)
         ctx.mark_non_differentiable(c9)
         return x9, c9
 
     @staticmethod
     def backward(ctx, g9, gc9):
         sv = ctx.saved_tensors
-        S, p, acts = sv[0], sv[1:28], sv[28:]
+        S, p, acts, pools = sv[0], sv[1:28], sv[28:46], sv[46:]
         W = [p[3 * i:3 * i + 3] for i in range(9)]
         X = [None] + [(acts[2 * i], acts[2 * i + 1]) for i in range(9)]  # X[k] = output of layer k
         need = ctx.needs_input_grad[1:]  # (capture, S, w1, b1, s1, ...)
@@ -78,13 +99,13 @@ class DNETFn(torch.autograd.Function):
         sp = ctx.specs
         red = WgradReduce()  # every layer's weight-gradient reduction in two launches at the end
 
-        def bwd(k, a, b, ga, gb_, acc=False):
-            xa, ca = X[a] if a else (S, None)
+        def bwd(k, a, b, ga, gb_, acc=False, src_a=None, spec=None, pool_grad=None):
+            xa, ca = src_a if src_a is not None else (X[a] if a else (S, None))
             xb, cb = X[b] if b else (None, None)
             gy, gco = G[k] if G[k] is not None else (g9, None)
-            layer_backward(sp[k - 1], (xa, ca, xb, cb, *W[k - 1]), X[k][0], X[k][1], gy, gco,
+            layer_backward(spec or sp[k - 1], (xa, ca, xb, cb, *W[k - 1]), X[k][0], X[k][1], gy, gco,
                            (*(ga or (None, None)), *(gb_ or (None, None))), gw[k - 1], gb[k - 1], accumulate=acc,
-                           defer=red)
+                           defer=red, pool_grad=pool_grad)
 
         G[8] = (e(X[8][0]), e(X[8][1]))
         bwd(9, 8, 0, G[8], None)                        # nconv7
@@ -94,11 +115,23 @@ class DNETFn(torch.autograd.Function):
         bwd(7, 3, 6, G[3], G[6])                        # nconv5: down1's output + up
         G[4], G[5] = (e(X[4][0]), e(X[4][1])), (e(X[5][0]), e(X[5][1]))
         bwd(6, 4, 5, G[4], G[5])                        # nconv4: down2's output + up
-        bwd(5, 4, 0, G[4], None, acc=True)              # down3 adds into down2's output gradient
-        bwd(4, 3, 0, G[3], None, acc=True)              # down2 -> down1's
-        bwd(3, 2, 0, G[2], None, acc=True)              # down1 -> nconv2's
-        G[1] = (e(X[1][0]), e(X[1][1]))
-        bwd(2, 1, 0, G[1], None)                        # nconv2
+        if ctx.pooled:
+            p2x, p2c, a2, p3x, p3c, a3, p4x, p4c, a4 = pools
+            plain = [dataclasses.replace(sp[k], mode=_lib.PLAIN) for k in (2, 3, 4)]
+            gp4 = (e(p4x), e(p4c))
+            bwd(5, 0, 0, gp4, None, src_a=(p4x, p4c), spec=plain[2])     # down3 -> pooled gradient
+            gp3 = (e(p3x), e(p3c))
+            bwd(4, 0, 0, gp3, None, src_a=(p3x, p3c), spec=plain[1], pool_grad=(*gp4, a4))  # down2
+            gp2 = (e(p2x), e(p2c))
+            bwd(3, 0, 0, gp2, None, src_a=(p2x, p2c), spec=plain[0], pool_grad=(*gp3, a3))  # down1
+            G[1] = (e(X[1][0]), e(X[1][1]))
+            bwd(2, 1, 0, G[1], None, pool_grad=(*gp2, a2))                 # nconv2
+        else:
+            bwd(5, 4, 0, G[4], None, acc=True)              # down3 adds into down2's output gradient
+            bwd(4, 3, 0, G[3], None, acc=True)              # down2 -> down1's
+            bwd(3, 2, 0, G[2], None, acc=True)              # down1 -> nconv2's
+            G[1] = (e(X[1][0]), e(X[1][1]))
+            bwd(2, 1, 0, G[1], None)                        # nconv2
         gS = e(S) if need[1] else None
         layer_backward(sp[0], (S, None, None, None, *W[0]), X[1][0], X[1][1], G[1][0], G[1][1],
                        (gS, None, None, None), gw[0], gb[0], defer=red)  # nconv1 (threshold: c0 has no gradient)
@@ -107,6 +140,13 @@ class DNETFn(torch.autograd.Function):
         for i in range(9):
             out += [gw[i], gb[i], None]
         return tuple(out + [None] * ctx.n_extra)
+
+
+def _materialise_pool(S):
+    """The training graph's pooled form (DNETFn): both arithmetics exact fp32 and every pooled
+    level at least 2x2 (nconv_fwd_pooled / the pooled-gradient backward are built for that)."""
+    return (nconv.FORWARD_MATH == _lib.MATH_FP32 and nconv.BACKWARD_MATH == _lib.MATH_FP32 and
+            min(S.shape[2], S.shape[3]) >= 16)
 
 
 def crop_hw(H, W, crop):

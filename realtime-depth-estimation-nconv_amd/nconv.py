@@ -151,16 +151,19 @@ def layer_forward_raw(spec: LayerSpec, xa, ca, xb, cb, weight, bias, wsum, out=N
     return y, co
 
 
-def layer_forward_pooled(spec: LayerSpec, xa, ca, xb, cb, weight, bias, wsum, out=None):
+def layer_forward_pooled(spec: LayerSpec, xa, ca, xb, cb, weight, bias, wsum, out=None, argmax=False):
     """nconv_fwd_pooled: (y, cout, maxpool2x2(y), maxpool2x2(cout)) in one launch (written into
-    `out` if given). No autograd."""
+    `out` if given). With argmax=True also the pooling windows' first-maximum codes (uint8, one per
+    pooled element; the training backward routes the pooled tensors' gradient by them) as a fifth
+    result. No autograd."""
     L = spec.descriptor(xa, ca, xb, cb, weight, bias, wsum)
     sh, shp = (L.B, L.Cout, L.Ho, L.Wo), (L.B, L.Cout, L.Ho // 2, L.Wo // 2)
     y, co, py, pc = _outputs(out, 4, (sh, sh, shp, shp), xa.device)
+    arg = torch.empty(shp, dtype=torch.uint8, device=xa.device) if argmax else None
     rc = _lib.lib().nconv_fwd_pooled(_lib.ctypes.byref(L), _lib.ptr(y), _lib.ptr(co), _lib.ptr(py), _lib.ptr(pc),
-                                     _lib.stream_handle(xa.device))
+                                     _lib.ptr(arg), _lib.stream_handle(xa.device))
     _lib.check(rc, "nconv_fwd_pooled")
-    return y, co, py, pc
+    return (y, co, py, pc, arg) if argmax else (y, co, py, pc)
 
 
 def head_weights(spec1: LayerSpec, spec2: LayerSpec, S, w1, b1, s1, w2, b2, s2, out=None):
@@ -218,11 +221,14 @@ class NConvLayerFn(torch.autograd.Function):
         return None, gxa, gca, gxb, gcb, gw, gb, None, None
 
 
-def layer_backward(spec: LayerSpec, inputs, y, co, gy, gco, gin, gw, gb, accumulate=False, defer=None):
+def layer_backward(spec: LayerSpec, inputs, y, co, gy, gco, gin, gw, gb, accumulate=False, defer=None,
+                   pool_grad=None):
     """nconv_bwd of one fused layer: gin = (gxa, gca, gxb, gcb) (None: skip) overwritten, or added
     into with accumulate=True (NCONV_BWD_ACCUMULATE: a tensor consumed by two layers); gw, gb
     overwritten (None: skip). defer: a WgradReduce collecting the layer's weight-gradient partial
-    rows (NCONV_BWD_DEFER_REDUCE): gw / gb are then written by its run()."""
+    rows (NCONV_BWD_DEFER_REDUCE): gw / gb are then written by its run(). pool_grad: (gy_pool,
+    gcout_pool, argmax) -- the gradient of this layer's 2x2-pooled outputs (the next down layer read
+    layer_forward_pooled's copies), routed into gy / gco by the argmax codes (nconv_bwd_ex)."""
     xa, ca, xb, cb, weight, bias, wsum = inputs
     gxa, gca, gxb, gcb = gin
     dev = y.device
@@ -235,9 +241,14 @@ def layer_backward(spec: LayerSpec, inputs, y, co, gy, gco, gin, gw, gb, accumul
     ws_bytes = lib.nconv_bwd_workspace_bytes(_lib.ctypes.byref(L))
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
     flags = (_lib.BWD_ACCUMULATE if accumulate else 0) | (_lib.BWD_DEFER_REDUCE if defer is not None else 0)
-    rc = lib.nconv_bwd(_lib.ctypes.byref(L), _lib.ptr(y), _lib.ptr(co), _lib.ptr(gy), _lib.ptr(gco),
-                       _lib.ptr(gxa), _lib.ptr(gca), _lib.ptr(gxb), _lib.ptr(gcb), _lib.ptr(gw),
-                       _lib.ptr(gb), _lib.ptr(ws), ws_bytes, flags, _lib.stream_handle(dev))
+    io = _lib.NconvBwdIo()
+    gpy, gpc, parg = pool_grad if pool_grad is not None else (None, None, None)
+    for name, t in (("y", y), ("cout", co), ("gy", gy), ("gcout", gco), ("gxa", gxa), ("gca", gca), ("gxb", gxb),
+                    ("gcb", gcb), ("gw", gw), ("gbias", gb), ("gy_pool", gpy), ("gcout_pool", gpc),
+                    ("pool_argmax", parg)):
+        setattr(io, name, t.data_ptr() if t is not None else None)
+    rc = lib.nconv_bwd_ex(_lib.ctypes.byref(L), _lib.ctypes.byref(io), _lib.ptr(ws), ws_bytes, flags,
+                          _lib.stream_handle(dev))
     if defer is not None and rc >= 0:
         defer.add(L, ws, rc, gw, gb)
         return

@@ -33,6 +33,10 @@ int main(void) {
     F(nconv_dense_wgrad, C0); F(nconv_dense_wgrad, x1); F(nconv_dense_wgrad, C1); F(nconv_dense_wgrad, H);
     F(nconv_dense_wgrad, W); F(nconv_dense_wgrad, gy); F(nconv_dense_wgrad, Cout); F(nconv_dense_wgrad, Ho);
     F(nconv_dense_wgrad, Wo); F(nconv_dense_wgrad, gw);
+    S(nconv_bwd_io);
+    F(nconv_bwd_io, y); F(nconv_bwd_io, cout); F(nconv_bwd_io, gy); F(nconv_bwd_io, gcout); F(nconv_bwd_io, gxa);
+    F(nconv_bwd_io, gca); F(nconv_bwd_io, gxb); F(nconv_bwd_io, gcb); F(nconv_bwd_io, gw); F(nconv_bwd_io, gbias);
+    F(nconv_bwd_io, gy_pool); F(nconv_bwd_io, gcout_pool); F(nconv_bwd_io, pool_argmax);
     S(nconv_bn_train);
     F(nconv_bn_train, B); F(nconv_bn_train, C); F(nconv_bn_train, H); F(nconv_bn_train, W); F(nconv_bn_train, x);
     F(nconv_bn_train, gamma); F(nconv_bn_train, beta); F(nconv_bn_train, running_mean);

@@ -44,6 +44,7 @@ def _ctypes_layout(struct):
 @pytest.mark.parametrize("c_name,py_name", [("nconv_src", "NconvSrc"), ("nconv_layer", "NconvLayer"),
                                             ("nconv_dense_conv", "NconvDenseConv"),
                                             ("nconv_dense_wgrad", "NconvDenseWgrad"),
+                                            ("nconv_bwd_io", "NconvBwdIo"),
                                             ("nconv_bn_train", "NconvBnTrain")])
 def test_struct_layout_matches_ctypes(nconv_amd, host_report, c_name, py_name):
     py = _ctypes_layout(getattr(nconv_amd._lib, py_name))

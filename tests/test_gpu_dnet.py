@@ -5,6 +5,8 @@ and the fwd+bwd gradients of a step-1 training loss.
 Tolerances: forward elementwise |gpu-ref| <= 1e-4*|ref| + 1e-4 (fp32 kernels vs fp64 oracle; the
 absolute term covers outputs near 0); gradients normwise max|gpu-ref|/max|ref| <= 1e-3.
 """
+import sys
+
 import pytest
 import torch
 
@@ -91,6 +93,32 @@ def test_whole_graph_autograd_matches_per_layer(nconv_amd, gpu, H, W):
     assert set(pa) == set(pb) and len(pa) == 18
     for a, b in [(ga, gb)] + [(pa[k], pb[k]) for k in pa]:
         assert (a - b).abs().max().item() <= 1e-6 * b.abs().max().item() + 1e-30
+
+
+@pytest.mark.parametrize("H,W", [(64, 96), (45, 67)])
+def test_materialised_pool_matches_pool_on_load(nconv_amd, gpu, H, W, monkeypatch):
+    """DNETFn's exact-fp32 training graph with the 2x2 max-pools materialised (nconv_fwd_pooled
+    argmax codes; pooled-sized down-layer input gradients routed into the producer's {gN, gD} by
+    nconv_bwd_ex) against pooling on load with full-resolution accumulation: the same sums in the
+    same order, so outputs and every gradient are bitwise equal (odd sizes: rows / columns no
+    window covers get no pooled gradient in both)."""
+    g = torch.Generator().manual_seed(22)
+    S = sparse_depth(g, 2, H, W).to(gpu)
+    gt = (torch.rand(2, 1, H, W, generator=g) * 80).to(gpu)
+    dnet = sys.modules[nconv_amd.DNET.__module__]
+    res = []
+    for pooled in (True, False):
+        monkeypatch.setattr(dnet, "_materialise_pool", lambda S_, v=pooled: v)
+        net = make_net(nconv_amd, "generalized", gpu)
+        x = S.clone().requires_grad_(True)
+        out = net(x)
+        nconv_amd.train.calculate_loss(out[0], gt[0], True).backward()
+        res.append((out.detach(), x.grad, {k: v.grad for k, v in net.named_parameters() if v.grad is not None}))
+    (oa, ga, pa), (ob, gb, pb) = res
+    assert torch.equal(oa, ob) and torch.equal(ga, gb)
+    assert set(pa) == set(pb) and len(pa) == 18
+    for k in pa:
+        assert torch.equal(pa[k], pb[k]), k
 
 
 def test_enforcepos_drift(nconv_amd, gpu):
