@@ -234,10 +234,26 @@ typedef struct nconv_bwd_io {
     const float* gy_pool;           /* optional pooled-output gradient (see above) */
     const float* gcout_pool;
     const unsigned char* pool_argmax;
+    /* optional: the weight gradient of the layer that produced L's input, fused into L's input
+     * gradient (DNET training: nconv2's backward computes nconv1's gW / gb in-tile, so nconv1's
+     * input gradient never reaches HBM and nconv1 needs no nconv_bwd). head = nconv1's descriptor
+     * (1 -> 8, 5x5, padding 2, stride 1, NCONV_LOAD_THRESH on the sparse depth; its output is L's
+     * source a); L must be an exact-fp32 8 -> 8 5x5 layer with NCONV_LOAD_PLAIN. head_workspace:
+     * nconv_bwd_head_workspace_bytes(L) bytes. Without NCONV_BWD_DEFER_REDUCE head_gw / head_gbias
+     * are written in this call; with it head_nparts receives the partial-row count for
+     * nconv_wgrad_reduce (layer head, workspace head_workspace). gxa / gca (nconv1's output
+     * gradient) are then optional. */
+    const nconv_layer* head;
+    void* head_workspace;
+    size_t head_workspace_bytes;
+    float* head_gw;
+    float* head_gbias;
+    int head_nparts;                /* out */
 } nconv_bwd_io;
 
-int nconv_bwd_ex(const nconv_layer* L, const nconv_bwd_io* io, void* workspace, size_t workspace_bytes,
+int nconv_bwd_ex(const nconv_layer* L, nconv_bwd_io* io, void* workspace, size_t workspace_bytes,
                  unsigned flags, void* stream);
+size_t nconv_bwd_head_workspace_bytes(const nconv_layer* L);
 
 /* Weight / bias gradients of n (1..16) layers whose nconv_bwd ran with NCONV_BWD_DEFER_REDUCE:
  * layers[k] the descriptor of that call (its weight normaliser wsum is read), workspaces[k] and

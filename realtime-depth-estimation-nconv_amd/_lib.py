@@ -43,6 +43,7 @@ EXPORTED = (
     "nconv_bwd_workspace_bytes",
     "nconv_bwd",
     "nconv_bwd_ex",
+    "nconv_bwd_head_workspace_bytes",
     "nconv_wgrad_reduce",
     "nconv_dense_packed_floats",
     "nconv_dense_pack",
@@ -79,7 +80,10 @@ class NconvLayer(ctypes.Structure):
 
 class NconvBwdIo(ctypes.Structure):
     _fields_ = [(n, ctypes.c_void_p) for n in ("y", "cout", "gy", "gcout", "gxa", "gca", "gxb", "gcb", "gw",
-                                               "gbias", "gy_pool", "gcout_pool", "pool_argmax")]
+                                               "gbias", "gy_pool", "gcout_pool", "pool_argmax")] + [
+        ("head", ctypes.POINTER(NconvLayer)), ("head_workspace", ctypes.c_void_p),
+        ("head_workspace_bytes", ctypes.c_size_t), ("head_gw", ctypes.c_void_p), ("head_gbias", ctypes.c_void_p),
+        ("head_nparts", ctypes.c_int)]
 
 
 class NconvDenseConv(ctypes.Structure):
@@ -143,6 +147,8 @@ def _declare(lib):
     lib.nconv_bwd_ex.restype = ctypes.c_int
     lib.nconv_bwd_ex.argtypes = [ctypes.POINTER(NconvLayer), ctypes.POINTER(NconvBwdIo), P, ctypes.c_size_t,
                                  ctypes.c_uint, P]
+    lib.nconv_bwd_head_workspace_bytes.restype = ctypes.c_size_t
+    lib.nconv_bwd_head_workspace_bytes.argtypes = [ctypes.POINTER(NconvLayer)]
     lib.nconv_wgrad_reduce.restype = ctypes.c_int
     lib.nconv_wgrad_reduce.argtypes = [ctypes.c_int, ctypes.POINTER(NconvLayer), P, P, P, P, P]
     I = ctypes.c_int

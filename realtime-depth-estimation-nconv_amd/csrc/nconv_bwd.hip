@@ -128,15 +128,158 @@ struct VecOf<4> { typedef f4 T; };
 template <>
 struct VecOf<2> { typedef f2 T; };
 
+// ---- fused nconv1 weight gradient (training, exact fp32) ------------------------------------------
+// nconv2's input gradient at a pixel p is nconv1's output gradient there (gy1 = G_xc*c1, gcout1 =
+// G_c + G_xc*y1), and nconv1 (1 -> 8, 5x5, padding 2, on x0 = S, c0 = (S > 0.01)) has
+//     gW1[o][kh][kw] = sum_p gN1[o](p) * S(p + (kh-2, kw-2)) * c0(...) + gD1[o](p) * c0(...)
+// whose terms vanish unless c0 = 1 at the tap: a correlation over the ~5 % of pixels that hold a
+// depth sample. Per tile: {gN1, gD1} of the 16 x 32 pixels (8 channels) into LDS, the samples of the
+// tile's 20 x 36 window listed once (a deterministic block prefix sum), then thread (o, tap) sums
+// over the list; plus the dense sums gb1 = sum gy1 and sum gcout1*cout1 (the normaliser's term).
+// One partial row per workgroup (wgrad_reduce_sum / wgrad_finish reduce them, deferred or not):
+// nconv1's input gradient G[1] is never written to HBM and nconv1 needs no backward kernel.
+constexpr int kHeadNw = 8 * 25, kHeadStride = kHeadNw + 16;
+
+template <int CIN, int TH, int TW>
+struct HeadLds {
+    static constexpr int RH = TH + 4, RW = TW + 4, RN = RH * RW;  // the tile's 5x5-window region
+    static constexpr int F2 = CIN * TH * TW + RN;                // {gN1, gD1} planes + sample list
+};
+
+template <int CIN, int TH, int TW>
+__device__ void head_wgrad_epilogue(const LayerDev& d, const BwdArgs& a, int b, int ih0, int iw0, int ty, int tx,
+                                    const f2 (&acc)[CIN][2], f2* smem) {
+    static_assert(CIN == 8, "nconv1 has 8 output channels");
+    using H = HeadLds<CIN, TH, TW>;
+    constexpr int RW = H::RW, RN = H::RN;
+    f2* gn = smem;                                       // [CIN][TH][TW]
+    f2* qlist = smem + CIN * TH * TW;                    // {row << 8 | col, S} of the samples
+    __shared__ int wtot[4];
+    __shared__ float red[4][2 * CIN];
+    const nconv_layer& L = d.L;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int ih = ih0 + ty, iw = iw0 + tx;
+    const bool pair = ih < L.H && iw + 1 < L.W && (L.W & 1) == 0;  // both pixels in range, 8-byte aligned
+    float sgy[CIN], sgc[CIN];
+#pragma unroll
+    for (int i = 0; i < CIN; ++i) {
+        sgy[i] = sgc[i] = 0.f;
+        const size_t idx = plane_idx(b, i, L.a.C, L.a.H, L.a.W, ih < L.H ? ih : 0, iw < L.W ? iw : 0);
+        float x[2] = {0.f, 0.f}, c[2] = {0.f, 0.f};
+        if (pair) {
+            const f2 xv = *reinterpret_cast<const f2*>(L.a.x + idx), cv = *reinterpret_cast<const f2*>(L.a.c + idx);
+            x[0] = xv.x; x[1] = xv.y; c[0] = cv.x; c[1] = cv.y;
+        } else {
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+                if (ih < L.H && iw + j < L.W) {
+                    x[j] = L.a.x[idx + j];
+                    c[j] = L.a.c[idx + j];
+                }
+        }
+        f2 v[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const bool ok = ih < L.H && iw + j < L.W;
+            const float gy = acc[i][j].x * c[j], gco = acc[i][j].y + acc[i][j].x * x[j];
+            float gN = 0.f, gD = 0.f;
+            if (ok) {
+                if (a.gxa) a.gxa[idx + j] = gy;  // G[1] only when asked for (the input gradient of S)
+                if (a.gca) a.gca[idx + j] = gco;
+                nconv_grad_nd(gy, gco, x[j], c[j], a.heps, a.hb[i], a.hs[i], gN, gD);
+                sgy[i] += gy;
+                sgc[i] = fmaf(gco, c[j], sgc[i]);
+            }
+            v[j] = (f2){gN, gD};
+        }
+        *reinterpret_cast<f4*>(gn + (i * TH + ty) * TW + tx) = (f4){v[0].x, v[0].y, v[1].x, v[1].y};
+    }
+    // the depth samples (c0 = 1) of the window region, listed in (thread, element) order
+    const float* Sp = a.hS + (size_t)b * L.H * L.W;
+    constexpr int NE = (RN + kT - 1) / kT;
+    float sv[NE];
+    int cnt = 0;
+#pragma unroll
+    for (int k = 0; k < NE; ++k) {
+        const int e = tid * NE + k;  // consecutive elements per thread: the list is row-major
+        const int r = e / RW, cc = e - r * RW;
+        const int qr = ih0 - 2 + r, qc = iw0 - 2 + cc;
+        const bool in = e < RN && (unsigned)qr < (unsigned)L.H && (unsigned)qc < (unsigned)L.W;
+        sv[k] = in ? Sp[(size_t)qr * L.W + qc] : 0.f;
+        cnt += sv[k] > a.hthresh ? 1 : 0;
+    }
+    int incl = cnt;  // wave inclusive scan
+#pragma unroll
+    for (int sh = 1; sh < 64; sh <<= 1) {
+        const int t = __shfl_up(incl, sh);
+        if (lane >= sh) incl += t;
+    }
+    if (lane == 63) wtot[wv] = incl;
+    __syncthreads();
+    int off = incl - cnt, total = 0;
+#pragma unroll
+    for (int w2 = 0; w2 < 4; ++w2) {
+        off += w2 < wv ? wtot[w2] : 0;
+        total += wtot[w2];
+    }
+#pragma unroll
+    for (int k = 0; k < NE; ++k) {
+        if (sv[k] > a.hthresh) {
+            const int e = tid * NE + k;
+            qlist[off] = (f2){__builtin_bit_cast(float, ((e / RW) << 8) | (e % RW)), sv[k]};
+            ++off;
+        }
+    }
+    // dense sums: wave butterflies, then the four waves in order
+#pragma unroll
+    for (int i = 0; i < CIN; ++i) {
+#pragma unroll
+        for (int sh = 32; sh > 0; sh >>= 1) {
+            sgy[i] += __shfl_xor(sgy[i], sh);
+            sgc[i] += __shfl_xor(sgc[i], sh);
+        }
+    }
+    if (lane == 0)
+#pragma unroll
+        for (int i = 0; i < CIN; ++i) {
+            red[wv][i] = sgy[i];
+            red[wv][CIN + i] = sgc[i];
+        }
+    __syncthreads();
+    float* out = a.hpart + (size_t)blockIdx.x * kHeadStride;
+    if (tid < kHeadNw) {
+        const int o = tid / 25, tap = tid - o * 25, kh = tap / 5, kw = tap - kh * 5;
+        const f2* g = gn + o * TH * TW;
+        float sn = 0.f, sd = 0.f;
+        for (int n = 0; n < total; ++n) {
+            const f2 q = qlist[n];
+            const int qi = __builtin_bit_cast(int, q.x);
+            const int pr = (qi >> 8) - kh, pc = (qi & 255) - kw;  // p = q - (tap - 2), region origin -2
+            if ((unsigned)pr < (unsigned)TH && (unsigned)pc < (unsigned)TW) {
+                const f2 v = g[pr * TW + pc];
+                sn = fmaf(v.x, q.y, sn);
+                sd += v.y;
+            }
+        }
+        out[tid] = sn + sd;
+    } else if (tid < kHeadNw + 2 * CIN) {
+        const int k = tid - kHeadNw;
+        out[tid] = ((red[0][k] + red[1][k]) + red[2][k]) + red[3][k];
+    }
+}
+
 // One (output channel o, kernel row kh) step per iteration of the inner loop, not unrolled: its
 // Cin*K weights ride SGPRs. The {gN, gD} planes of the output channels are staged one at a time
 // into two LDS buffers, the loads two channels ahead (as the forward's input planes).
-template <int CIN, int COUT, int K, int MODE, bool GP = false>
+template <int CIN, int COUT, int K, int MODE, bool GP = false, bool HW = false>
 __global__ __launch_bounds__(kT) void dgrad_tiled(LayerDev d, BwdArgs a, float* tmp_x, float* tmp_c) {
     using C = DgCfg<CIN, K>;
     using GS = GTileStager<C::OHT, C::OWT, C::OWP, GP>;
     constexpr int P = C::P;
-    __shared__ __attribute__((aligned(16))) f2 tile[2 * GS::PLANE_STRIDE];
+    // with HW the staging planes' LDS is reused by the head epilogue ({gN1, gD1} planes + sample list)
+    constexpr int TILE_F2 = HW && HeadLds<CIN, C::TH, C::TW>::F2 > 2 * GS::PLANE_STRIDE
+                                ? HeadLds<CIN, C::TH, C::TW>::F2 : 2 * GS::PLANE_STRIDE;
+    __shared__ __attribute__((aligned(16))) f2 tile[TILE_F2];
     const nconv_layer& L = d.L;
     const float* __restrict__ wgt = L.weight;
     const TileCoord tcd = xcd_tile((L.W + C::TW - 1) / C::TW, (L.H + C::TH - 1) / C::TH, L.B);
@@ -197,6 +340,12 @@ __global__ __launch_bounds__(kT) void dgrad_tiled(LayerDev d, BwdArgs a, float* 
     }
 
     // ---- epilogue: gx = G_xc*c, gc = G_c + G_xc*x, routed through the glue's backward ----
+    if constexpr (HW) {  // nconv2's input gradient feeds nconv1's weight gradient in-tile
+        static_assert(MODE == NCONV_LOAD_PLAIN && P == 2, "fused head weight gradient: plain 2-pixel tiles");
+        __syncthreads();  // the staging tile is free
+        if constexpr (HW) head_wgrad_epilogue<CIN, C::TH, C::TW>(d, a, b, ih0, iw0, ty, tx, acc, tile);
+        return;
+    }
     const int ih = ih0 + ty;
     if (ih >= L.H) return;
     const int iwb = iw0 + tx;
@@ -1278,6 +1427,12 @@ size_t bwd_workspace_bytes(const LayerDev& d) {
     return bytes;
 }
 
+size_t bwd_head_workspace_bytes(const nconv_layer& L) {
+    using D = DgCfg<8, 5>;
+    const size_t nblk = (size_t)((L.W + D::TW - 1) / D::TW) * ((L.H + D::TH - 1) / D::TH) * L.B;
+    return (nblk + kReduceSplit) * kHeadStride * sizeof(float);
+}
+
 void plan_bwd(const nconv_layer& L, int* dgrad, int* wgrad) {
     if (pick_path(L) == kGeneric) {
         *dgrad = *wgrad = NCONV_KERNEL_GENERIC;
@@ -1293,12 +1448,12 @@ void plan_bwd(const nconv_layer& L, int* dgrad, int* wgrad) {
 // Returns 0, or -EIO when the bf16 weight-gradient grid would not fit the workspace (it cannot:
 // its strips are wider than wgrad_mfma's, for which the workspace is sized; checked anyway, so
 // a bf16 request never silently runs another kernel).
-template <int CIN, int COUT, int K, int MODE, bool GP = false>
+template <int CIN, int COUT, int K, int MODE, bool GP = false, bool HW = false>
 static int go_bwd_tiled(const LayerDev& d, const BwdArgs& a, float* part, float* tx, float* tc,
                         hipStream_t st) {
     const nconv_layer& L = d.L;
     using D = DgCfg<CIN, K>;
-    if (a.gxa || a.gca || a.gxb || a.gcb) {
+    if (HW || a.gxa || a.gca || a.gxb || a.gcb) {
         if (K > 1 && CIN > 1 && L.bwd_math != NCONV_MATH_FP32) {  // split-bf16 matrix cores
             if constexpr (K > 1 && CIN > 1)
                 go_dgrad_bf<CIN, COUT, K, MODE>(d, a, tx, tc, L.bwd_math == NCONV_MATH_BF16X9 ? 3 : 2, st);
@@ -1314,7 +1469,16 @@ static int go_bwd_tiled(const LayerDev& d, const BwdArgs& a, float* part, float*
                     hipLaunchKernelGGL((dgrad_tiled<CIN, COUT, K, MODE>), g, dim3(kT), 0, st, d, a, tx, tc);
                 }
             } else {
-                hipLaunchKernelGGL((dgrad_tiled<CIN, COUT, K, MODE, GP>), g, dim3(kT), 0, st, d, a, tx, tc);
+                hipLaunchKernelGGL((dgrad_tiled<CIN, COUT, K, MODE, GP, HW>), g, dim3(kT), 0, st, d, a, tx, tc);
+                if constexpr (HW) {  // nconv1's weight-gradient partial rows: one per dgrad workgroup
+                    if (a.defer) {
+                        *a.hnparts = (int)g.x;
+                    } else {
+                        const RedJob J{a.hpart, a.hs, a.hgw, a.hgb, (int)g.x, kHeadNw, 8, 25};
+                        const char* why = nullptr;
+                        launch_wgrad_reduce_multi(1, &J, st, &why);
+                    }
+                }
             }
         }
     }
@@ -1396,7 +1560,17 @@ int launch_bwd(const LayerDev& d, const BwdArgs& a, hipStream_t st, const char**
                    "8->8 5x5 stride-1 layer with plain loads";
             return -95;
         }
-        go_bwd_tiled<8, 8, 5, NCONV_LOAD_PLAIN, true>(d, a, part, tx, tc, st);
+        if (a.hpart) go_bwd_tiled<8, 8, 5, NCONV_LOAD_PLAIN, true, true>(d, a, part, tx, tc, st);
+        else go_bwd_tiled<8, 8, 5, NCONV_LOAD_PLAIN, true>(d, a, part, tx, tc, st);
+        return last_err(why);
+    }
+    if (a.hpart) {
+        if (!(path == kTiled && L.Cin == 8 && L.Cout == 8 && L.KH == 5 && L.load_mode == NCONV_LOAD_PLAIN &&
+              L.bwd_math == NCONV_MATH_FP32)) {
+            *why = "fused head weight gradient needs an exact-fp32 8->8 5x5 stride-1 layer with plain loads";
+            return -95;
+        }
+        go_bwd_tiled<8, 8, 5, NCONV_LOAD_PLAIN, false, true>(d, a, part, tx, tc, st);
         return last_err(why);
     }
     if (path == kTiled) {

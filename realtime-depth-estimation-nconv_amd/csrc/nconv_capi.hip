@@ -234,7 +234,12 @@ size_t nconv_bwd_workspace_bytes(const nconv_layer* L) {
     return nconv::bwd_workspace_bytes(make_dev(L));
 }
 
-int nconv_bwd_ex(const nconv_layer* L, const nconv_bwd_io* io, void* workspace, size_t workspace_bytes,
+size_t nconv_bwd_head_workspace_bytes(const nconv_layer* L) {
+    if (!L || validate(L, false)) return 0;
+    return nconv::bwd_head_workspace_bytes(*L);
+}
+
+int nconv_bwd_ex(const nconv_layer* L, nconv_bwd_io* io, void* workspace, size_t workspace_bytes,
                  unsigned flags, void* stream) {
     if (const char* why = validate(L, true)) return fail(-22, "nconv_bwd", why);
     if (!io) return fail(-22, "nconv_bwd", "null io");
@@ -250,6 +255,29 @@ int nconv_bwd_ex(const nconv_layer* L, const nconv_bwd_io* io, void* workspace, 
     nconv::BwdArgs a{io->y, io->cout, io->gy, io->gcout, io->gxa, io->gca, io->gxb, io->gcb, io->gw, io->gbias,
                      (float*)workspace, workspace_bytes, (flags & NCONV_BWD_ACCUMULATE) ? 1 : 0, defer, &nparts,
                      io->gy_pool, io->gcout_pool, io->pool_argmax};
+    io->head_nparts = 0;
+    if (const nconv_layer* H = io->head) {
+        if (const char* why = validate(H, true)) return fail(-22, "nconv_bwd", why);
+        if (H->Cin != 1 || H->Cout != 8 || H->KH != 5 || H->KW != 5 || H->PH != 2 || H->PW != 2 || H->SH != 1 ||
+            H->SW != 1 || H->DH != 1 || H->DW != 1 || H->groups != 1 || H->load_mode != NCONV_LOAD_THRESH)
+            return fail(-22, "nconv_bwd", "head must be a 1->8 5x5 padding-2 threshold layer (nconv1)");
+        if (H->B != L->B || H->Ho != L->H || H->Wo != L->W || L->Cin != 8)
+            return fail(-22, "nconv_bwd", "head output does not match the layer's input");
+        if ((flags & NCONV_BWD_ACCUMULATE) && (io->gxa || io->gca))
+            return fail(-22, "nconv_bwd", "fused head: the head's output gradient is written, not accumulated");
+        if (!io->head_workspace || io->head_workspace_bytes < nconv::bwd_head_workspace_bytes(*L))
+            return fail(-22, "nconv_bwd", "head workspace too small (nconv_bwd_head_workspace_bytes)");
+        if (!defer && !io->head_gw && !io->head_gbias) return fail(-22, "nconv_bwd", "head outputs are NULL");
+        a.hS = H->a.x;
+        a.hb = H->bias;
+        a.hs = H->wsum;
+        a.heps = H->eps;
+        a.hthresh = H->thresh;
+        a.hpart = (float*)io->head_workspace;
+        a.hgw = io->head_gw;
+        a.hgb = io->head_gbias;
+        a.hnparts = &io->head_nparts;
+    }
     const char* why = nullptr;
     int rc = nconv::launch_bwd(d, a, (hipStream_t)stream, &why);
     if (rc) return fail(rc, "nconv_bwd", why);
@@ -259,7 +287,8 @@ int nconv_bwd_ex(const nconv_layer* L, const nconv_bwd_io* io, void* workspace, 
 int nconv_bwd(const nconv_layer* L, const float* y, const float* cout, const float* gy,
               const float* gcout, float* gxa, float* gca, float* gxb, float* gcb, float* gw,
               float* gbias, void* workspace, size_t workspace_bytes, unsigned flags, void* stream) {
-    const nconv_bwd_io io{y, cout, gy, gcout, gxa, gca, gxb, gcb, gw, gbias, nullptr, nullptr, nullptr};
+    nconv_bwd_io io{y, cout, gy, gcout, gxa, gca, gxb, gcb, gw, gbias, nullptr, nullptr, nullptr,
+                    nullptr, nullptr, 0, nullptr, nullptr, 0};
     return nconv_bwd_ex(L, &io, workspace, workspace_bytes, flags, stream);
 }
 

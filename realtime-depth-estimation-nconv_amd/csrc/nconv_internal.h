@@ -45,7 +45,19 @@ struct BwdArgs {
     const float* gpy;
     const float* gpc;
     const unsigned char* parg;
+    // optional fused weight gradient of the producer nconv1 (1 -> 8, 5x5, threshold load, padding 2)
+    // in the input gradient's epilogue: its sparse input S, bias, normaliser, eps, threshold, and
+    // the per-workgroup partial rows (200 weights, 8 sum gy, 8 sum gcout*cout) it writes
+    const float* hS;
+    const float* hb;
+    const float* hs;
+    float heps, hthresh;
+    float* hpart;
+    float* hgw;       // nconv1's gW / gb (undeferred: reduced right after the kernel)
+    float* hgb;
+    int* hnparts;     // out (defer): the number of nconv1 partial rows written
 };
+size_t bwd_head_workspace_bytes(const nconv_layer& L2);
 
 // One layer's deferred weight-gradient reduction (nconv_wgrad_reduce): its workspace's partial rows.
 struct RedJob {

@@ -124,6 +124,15 @@ class DNETFn(torch.autograd.Function):
             bwd(4, 0, 0, gp3, None, src_a=(p3x, p3c), spec=plain[1], pool_grad=(*gp4, a4))  # down2
             gp2 = (e(p2x), e(p2c))
             bwd(3, 0, 0, gp2, None, src_a=(p2x, p2c), spec=plain[0], pool_grad=(*gp3, a3))  # down1
+            if not need[1]:  # nconv2's input gradient feeds nconv1's weight gradient in-tile
+                layer_backward(sp[1], (X[1][0], X[1][1], None, None, *W[1]), X[2][0], X[2][1], *G[2],
+                               (None, None, None, None), gw[1], gb[1], defer=red, pool_grad=(*gp2, a2),
+                               head=(sp[0], S, *W[0], gw[0], gb[0]))
+                red.run(S.device)
+                out = [None, None, None]
+                for i in range(9):
+                    out += [gw[i], gb[i], None]
+                return tuple(out + [None] * ctx.n_extra)
             G[1] = (e(X[1][0]), e(X[1][1]))
             bwd(2, 1, 0, G[1], None, pool_grad=(*gp2, a2))                 # nconv2
         else:

@@ -222,13 +222,15 @@ class NConvLayerFn(torch.autograd.Function):
 
 
 def layer_backward(spec: LayerSpec, inputs, y, co, gy, gco, gin, gw, gb, accumulate=False, defer=None,
-                   pool_grad=None):
+                   pool_grad=None, head=None):
     """nconv_bwd of one fused layer: gin = (gxa, gca, gxb, gcb) (None: skip) overwritten, or added
     into with accumulate=True (NCONV_BWD_ACCUMULATE: a tensor consumed by two layers); gw, gb
     overwritten (None: skip). defer: a WgradReduce collecting the layer's weight-gradient partial
     rows (NCONV_BWD_DEFER_REDUCE): gw / gb are then written by its run(). pool_grad: (gy_pool,
     gcout_pool, argmax) -- the gradient of this layer's 2x2-pooled outputs (the next down layer read
-    layer_forward_pooled's copies), routed into gy / gco by the argmax codes (nconv_bwd_ex)."""
+    layer_forward_pooled's copies), routed into gy / gco by the argmax codes (nconv_bwd_ex). head:
+    (spec, S, weight, bias, wsum, gw, gb) of the producer nconv1, whose weight / bias gradients are
+    then computed inside this layer's input gradient (nconv_bwd_ex head; gin's gxa / gca optional)."""
     xa, ca, xb, cb, weight, bias, wsum = inputs
     gxa, gca, gxb, gcb = gin
     dev = y.device
@@ -247,10 +249,20 @@ def layer_backward(spec: LayerSpec, inputs, y, co, gy, gco, gin, gw, gb, accumul
                     ("gcb", gcb), ("gw", gw), ("gbias", gb), ("gy_pool", gpy), ("gcout_pool", gpc),
                     ("pool_argmax", parg)):
         setattr(io, name, t.data_ptr() if t is not None else None)
+    if head is not None:
+        hspec, S, hw, hb, hs, hgw, hgb = head
+        HL = hspec.descriptor(S, None, None, None, hw, hb, hs)
+        hbytes = lib.nconv_bwd_head_workspace_bytes(_lib.ctypes.byref(L))
+        hws = torch.empty(max(hbytes, 1), dtype=torch.uint8, device=dev)
+        io.head = _lib.ctypes.pointer(HL)
+        io.head_workspace, io.head_workspace_bytes = hws.data_ptr(), hbytes
+        io.head_gw, io.head_gbias = _lib.ptr(hgw), _lib.ptr(hgb)
     rc = lib.nconv_bwd_ex(_lib.ctypes.byref(L), _lib.ctypes.byref(io), _lib.ptr(ws), ws_bytes, flags,
                           _lib.stream_handle(dev))
     if defer is not None and rc >= 0:
         defer.add(L, ws, rc, gw, gb)
+        if head is not None:
+            defer.add(HL, hws, io.head_nparts, hgw, hgb)
         return
     _lib.check(rc, "nconv_bwd")
 

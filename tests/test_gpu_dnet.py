@@ -120,6 +120,22 @@ def test_materialised_pool_matches_pool_on_load(nconv_amd, gpu, H, W, monkeypatc
     for k in pa:
         assert torch.equal(pa[k], pb[k]), k
 
+    # S without gradient: nconv1's weight gradient fused into nconv2's input gradient (sparse
+    # correlation over the depth samples, nconv_bwd_ex head): every other gradient bitwise as
+    # above, nconv1's within fp32 reassociation (normwise 1e-5)
+    monkeypatch.setattr(dnet, "_materialise_pool", lambda S_: True)
+    net = make_net(nconv_amd, "generalized", gpu)
+    out = net(S)
+    nconv_amd.train.calculate_loss(out[0], gt[0], True).backward()
+    pc = {k: v.grad for k, v in net.named_parameters() if v.grad is not None}
+    assert torch.equal(out.detach(), oa) and set(pc) == set(pa)
+    for k in pc:
+        if k.startswith("d_net.nconv1."):
+            rel = ((pc[k] - pa[k]).abs().max() / pa[k].abs().max()).item()
+            assert rel <= 1e-5, (k, rel)
+        else:
+            assert torch.equal(pc[k], pa[k]), k
+
 
 def test_enforcepos_drift(nconv_amd, gpu):
     """Training-mode forward applies softplus(beta=10) to every layer's weight, once per forward."""
