@@ -249,11 +249,30 @@ typedef struct nconv_bwd_io {
     float* head_gw;
     float* head_gbias;
     int head_nparts;                /* out */
+    /* optional: the backward of the 1x1 layer that consumes L's outputs, fused into L's (DNET
+     * training: nconv7, 8 -> 1, 1x1, padding 2, after nconv6). tail = nconv7's descriptor; tail_y,
+     * tail_cout, tail_gy its outputs and their gradient, (B, 1, Ho + 4, Wo + 4); its cout gradient
+     * is taken as 0 (DNET discards nconv7's confidence). L's gy / gcout are then formed in-kernel
+     * from them (gy, gcout above are ignored and may be NULL), so nconv7's input gradient never
+     * reaches HBM; nconv7's weight gradient goes to tail_gw (tail_workspace of
+     * nconv_bwd_tail_workspace_bytes(L) bytes; with NCONV_BWD_DEFER_REDUCE tail_nparts partial rows
+     * for nconv_wgrad_reduce, layer tail). nconv7's bias gradient (the sum of tail_gy) is left to
+     * the caller. L must be nconv6's exact-fp32 geometry (16 -> 8 3x3, padding 0, upsample-first
+     * exactly-2x concat) with gw or gbias requested. */
+    const nconv_layer* tail;
+    const float* tail_y;
+    const float* tail_cout;
+    const float* tail_gy;
+    void* tail_workspace;
+    size_t tail_workspace_bytes;
+    float* tail_gw;
+    int tail_nparts;                /* out */
 } nconv_bwd_io;
 
 int nconv_bwd_ex(const nconv_layer* L, nconv_bwd_io* io, void* workspace, size_t workspace_bytes,
                  unsigned flags, void* stream);
 size_t nconv_bwd_head_workspace_bytes(const nconv_layer* L);
+size_t nconv_bwd_tail_workspace_bytes(const nconv_layer* L);
 
 /* Weight / bias gradients of n (1..16) layers whose nconv_bwd ran with NCONV_BWD_DEFER_REDUCE:
  * layers[k] the descriptor of that call (its weight normaliser wsum is read), workspaces[k] and

@@ -44,6 +44,7 @@ EXPORTED = (
     "nconv_bwd",
     "nconv_bwd_ex",
     "nconv_bwd_head_workspace_bytes",
+    "nconv_bwd_tail_workspace_bytes",
     "nconv_wgrad_reduce",
     "nconv_dense_packed_floats",
     "nconv_dense_pack",
@@ -83,7 +84,9 @@ class NconvBwdIo(ctypes.Structure):
                                                "gbias", "gy_pool", "gcout_pool", "pool_argmax")] + [
         ("head", ctypes.POINTER(NconvLayer)), ("head_workspace", ctypes.c_void_p),
         ("head_workspace_bytes", ctypes.c_size_t), ("head_gw", ctypes.c_void_p), ("head_gbias", ctypes.c_void_p),
-        ("head_nparts", ctypes.c_int)]
+        ("head_nparts", ctypes.c_int), ("tail", ctypes.POINTER(NconvLayer)), ("tail_y", ctypes.c_void_p),
+        ("tail_cout", ctypes.c_void_p), ("tail_gy", ctypes.c_void_p), ("tail_workspace", ctypes.c_void_p),
+        ("tail_workspace_bytes", ctypes.c_size_t), ("tail_gw", ctypes.c_void_p), ("tail_nparts", ctypes.c_int)]
 
 
 class NconvDenseConv(ctypes.Structure):
@@ -149,6 +152,8 @@ def _declare(lib):
                                  ctypes.c_uint, P]
     lib.nconv_bwd_head_workspace_bytes.restype = ctypes.c_size_t
     lib.nconv_bwd_head_workspace_bytes.argtypes = [ctypes.POINTER(NconvLayer)]
+    lib.nconv_bwd_tail_workspace_bytes.restype = ctypes.c_size_t
+    lib.nconv_bwd_tail_workspace_bytes.argtypes = [ctypes.POINTER(NconvLayer)]
     lib.nconv_wgrad_reduce.restype = ctypes.c_int
     lib.nconv_wgrad_reduce.argtypes = [ctypes.c_int, ctypes.POINTER(NconvLayer), P, P, P, P, P]
     I = ctypes.c_int

@@ -32,7 +32,24 @@ constexpr int pick_chunk(int n, int plane_f2, int budget) {
 // padding) is computed once per workgroup; per output channel the four saved planes (gy, gcout,
 // y, cout) are read with buffer loads and {gN, gD} are formed at store time. Elements are dealt
 // to the 256 threads row-major; slots past the tile go to a dump slot after the plane.
-template <int OHT, int OWT, int OWP, bool GP = false>
+// nconv7 (1x1, padding 2) consumer of this layer's outputs fused into its backward (T7): the
+// layer's output gradient at (oh, ow) is nconv7's input gradient there, G_xc = w7[o] gN7, G_c =
+// w7[o] gD7 with {gN7, gD7} from nconv7's (gy, y, cout) at (oh + 2, ow + 2); gy = G_xc * cout,
+// gcout = G_c + G_xc * y (nconv7's dgrad_tiled<8,1,1> epilogue, same operations).
+__device__ __forceinline__ unsigned t7_off(int oh, int ow, int Ho, int Wo, unsigned oob) {
+    return ((unsigned)oh < (unsigned)Ho && (unsigned)ow < (unsigned)Wo) ? (unsigned)((oh + 2) * (Wo + 4) + ow + 2) * 4u
+                                                                          : oob;
+}
+__device__ __forceinline__ void t7_nd(const BwdArgs& a, float gy9, float y9, float co9, float& gN7, float& gD7) {
+    nconv_grad_nd(gy9, 0.f, y9, co9, a.t7eps, a.t7b[0], a.t7s[0], gN7, gD7);
+}
+__device__ __forceinline__ void t7_gy(float w7, float gN7, float gD7, float y, float co, float& gy, float& gco) {
+    const float gxc = fmaf(w7, gN7, 0.f), gc = fmaf(w7, gD7, 0.f);  // the 1x1 dgrad's accumulators
+    gy = gxc * co;
+    gco = fmaf(gxc, y, gc);
+}
+
+template <int OHT, int OWT, int OWP, bool GP = false, bool T7 = false>
 struct GTileStager {
     static constexpr int NT = OHT * OWT;
     static constexpr int NE = (NT + 255) / 256;
@@ -44,6 +61,7 @@ struct GTileStager {
     unsigned go[NE];
     unsigned gpo[GP ? NE : 1];  // pooled element offsets, window slots (GP)
     unsigned gsub[GP ? NE : 1];
+    float t7n[T7 ? NE : 1], t7d[T7 ? NE : 1];  // {gN7, gD7} per element (T7)
 
     __device__ __forceinline__ void init(const nconv_layer& L, int oh0, int ow0, int tid) {
 #pragma unroll
@@ -61,6 +79,31 @@ struct GTileStager {
         }
     }
 
+    // T7: nconv7's (gy, y, cout) of the elements (loads issued here, {gN7, gD7} formed by t7_form)
+    __device__ __forceinline__ void t7_load(const nconv_layer& L, const BwdArgs& a, int b, int oh0, int ow0, int tid,
+                                            float (&v)[3][NE]) const {
+        const int pl7 = (L.Ho + 4) * (L.Wo + 4);
+        const size_t base = (size_t)b * pl7;
+        const __amdgpu_buffer_rsrc_t rg = plane_rsrc(a.t7gy + base, pl7 * 4);
+        const __amdgpu_buffer_rsrc_t ry = plane_rsrc(a.t7y + base, pl7 * 4);
+        const __amdgpu_buffer_rsrc_t rc = plane_rsrc(a.t7co + base, pl7 * 4);
+#pragma unroll
+        for (int k = 0; k < NE; ++k) {
+            const int e = tid + 256 * k;
+            const int r = e / OWT, col = e - r * OWT;
+            const unsigned off = e < NT ? t7_off(oh0 + r, ow0 + col, L.Ho, L.Wo, OOB) : OOB;
+            v[0][k] = ld_f32(rg, off);
+            v[1][k] = ld_f32(ry, off);
+            v[2][k] = ld_f32(rc, off);
+        }
+    }
+    __device__ __forceinline__ void t7_form(const BwdArgs& a, const float (&v)[3][NE]) {
+#pragma unroll
+        for (int k = 0; k < NE; ++k) {
+            if constexpr (T7) t7_nd(a, v[0][k], v[1][k], v[2][k], t7n[k], t7d[k]);
+        }
+    }
+
     // raw (gy, gcout, y, cout [, pooled gy, pooled gcout, code]) of output channel o of image b, no wait
     __device__ __forceinline__ void load(const nconv_layer& L, const BwdArgs& a, int b, int o,
                                          float (&v)[NV][NE]) const {
@@ -69,6 +112,14 @@ struct GTileStager {
         const __amdgpu_buffer_rsrc_t rgy = plane_rsrc(a.gy + base, plane * 4);
         const __amdgpu_buffer_rsrc_t ry = plane_rsrc(a.y + base, plane * 4);
         const __amdgpu_buffer_rsrc_t rco = plane_rsrc(a.co + base, plane * 4);
+        if constexpr (T7) {  // gy / gcout are formed from nconv7's planes at store time
+#pragma unroll
+            for (int k = 0; k < NE; ++k) {
+                v[2][k] = ld_f32(ry, go[k]);
+                v[3][k] = ld_f32(rco, go[k]);
+            }
+            return;
+        }
 #pragma unroll
         for (int k = 0; k < NE; ++k) {
             v[0][k] = ld_f32(rgy, go[k]);
@@ -98,11 +149,19 @@ struct GTileStager {
         }
     }
 
-    __device__ __forceinline__ void store(const nconv_layer& L, int o, const float (&v)[NV][NE], f2* t) const {
+    __device__ __forceinline__ void store(const nconv_layer& L, int o, const float (&v)[NV][NE], f2* t,
+                                          float a_w7 = 0.f) const {
         const float bo = L.bias[o], so = L.wsum[o];
+        const float w7 = T7 ? a_w7 : 0.f;
 #pragma unroll
         for (int k = 0; k < NE; ++k) {
-            float gy = v[0][k], gco = v[1][k];
+            float gy, gco;
+            if constexpr (T7) {
+                t7_gy(w7, t7n[k], t7d[k], v[2][k], v[3][k], gy, gco);
+            } else {
+                gy = v[0][k];
+                gco = v[1][k];
+            }
             if constexpr (GP) pool_route(gy, gco, v[4][k], v[5][k], __builtin_bit_cast(unsigned, v[6][k]), gsub[k]);
             float gN, gD;  // zero padding: gy = gcout = y = cout = 0 gives gN = gD = 0
             nconv_grad_nd(gy, gco, v[2][k], v[3][k], L.eps, bo, so, gN, gD);
@@ -485,10 +544,10 @@ __global__ __launch_bounds__(kT) void box_weights(const float* __restrict__ w, i
     wb[e] = sum;
 }
 
-template <int MODE>
+template <int MODE, bool T7 = false>
 __global__ __launch_bounds__(kT) void dgrad_phase(LayerDev d, BwdArgs a, const float* __restrict__ wbox) {
     using C = DgCfg<16, 3>;
-    using GS = GTileStager<C::OHT, C::OWT, C::OWP>;
+    using GS = GTileStager<C::OHT, C::OWT, C::OWP, false, T7>;
     constexpr int P = C::P, K = 3, CS = 8;
     constexpr int SK0 = (MODE == NCONV_LOAD_UPCAT_SKIP_FIRST) ? 0 : 8;  // first skip channel of W
     static_assert(C::TH % 2 == 0 && C::TW % 2 == 0 && C::OHT >= C::TH + 2 && C::OWT >= C::TW + 2, "low tile");
@@ -556,15 +615,23 @@ __global__ __launch_bounds__(kT) void dgrad_phase(LayerDev d, BwdArgs a, const f
     GS gs;
     gs.init(L, oh0, ow0, tid);
     float va[4][GS::NE], vb[4][GS::NE];
-    gs.load(L, a, b, 0, va);
-    gs.load(L, a, b, 1, vb);
+    if constexpr (T7) {
+        float v7[3][GS::NE];
+        gs.t7_load(L, a, b, oh0, ow0, tid, v7);
+        gs.load(L, a, b, 0, va);
+        gs.load(L, a, b, 1, vb);
+        gs.t7_form(a, v7);
+    } else {
+        gs.load(L, a, b, 0, va);
+        gs.load(L, a, b, 1, vb);
+    }
 #pragma unroll 1
     for (int o = 0; o < 8; o += 2) {
-        gs.store(L, o, va, tile);
+        gs.store(L, o, va, tile, T7 ? a.t7w[o] : 0.f);
         __syncthreads();
         gs.load(L, a, b, o + 2 < 8 ? o + 2 : 7, va);
         fma_plane(o, 0);
-        gs.store(L, o + 1, vb, tile + GS::PLANE_STRIDE);
+        gs.store(L, o + 1, vb, tile + GS::PLANE_STRIDE, T7 ? a.t7w[o + 1] : 0.f);
         __syncthreads();
         gs.load(L, a, b, o + 3 < 8 ? o + 3 : 7, vb);
         fma_plane(o + 1, 1);
@@ -1111,7 +1178,7 @@ struct WmCfg {
 #define NCONV_WM_WAVES 3
 #endif
 #define NCONV_WM_ATTR __attribute__((amdgpu_waves_per_eu(NCONV_WM_WAVES, 8)))
-template <int CIN, int COUT, int K, int MODE, bool GP = false>
+template <int CIN, int COUT, int K, int MODE, bool GP = false, bool T7 = false>
 __global__ __launch_bounds__(kT) NCONV_WM_ATTR void wgrad_mfma(LayerDev d, BwdArgs a, float* part, int nstrip, int nseg,
                                                  int seg_rows) {
     using C = WmCfg<CIN, COUT, K>;
@@ -1153,6 +1220,10 @@ __global__ __launch_bounds__(kT) NCONV_WM_ATTR void wgrad_mfma(LayerDev d, BwdAr
     float px[C::CPW], pc[C::CPW];
     constexpr int NG = GP ? 7 : 4;  // gy, gco, y, cout (+ pooled gy, gcout, argmax code)
     float gq[C::OPW][2][NG];
+    float g7[T7 ? 2 : 1][3];                                     // nconv7's gy, y, cout (T7)
+    float w7n[T7 ? C::OPW : 1], w7d[T7 ? C::OPW : 1];            // nconv7's weight-gradient sums
+#pragma unroll
+    for (int kk = 0; kk < (T7 ? C::OPW : 1); ++kk) w7n[kk] = w7d[kk] = 0.f;
     float gb_acc[C::OPW], gs_acc[C::OPW];
 #pragma unroll
     for (int kk = 0; kk < C::OPW; ++kk) gb_acc[kk] = gs_acc[kk] = 0.f;
@@ -1180,6 +1251,18 @@ __global__ __launch_bounds__(kT) NCONV_WM_ATTR void wgrad_mfma(LayerDev d, BwdAr
     const int plane = L.Ho * L.Wo;
     const int Hp = L.Ho >> 1, Wp = L.Wo >> 1, pplane = Hp * Wp;
     auto load_g = [&](int oh) {
+        if constexpr (T7) {
+            const int pl7 = (L.Ho + 4) * (L.Wo + 4);
+            const size_t base7 = (size_t)b * pl7;
+#pragma unroll
+            for (int p = 0; p < 2; ++p) {
+                const int ow = ow0 - (K - 1) + p * 64 + lane;
+                const unsigned off = (p == 0 || lane < K - 1) ? t7_off(oh, ow, L.Ho, L.Wo, OOB) : OOB;
+                g7[p][0] = ld_f32(plane_rsrc(a.t7gy + base7, pl7 * 4), off);
+                g7[p][1] = ld_f32(plane_rsrc(a.t7y + base7, pl7 * 4), off);
+                g7[p][2] = ld_f32(plane_rsrc(a.t7co + base7, pl7 * 4), off);
+            }
+        }
 #pragma unroll
         for (int kk = 0; kk < C::OPW; ++kk) {
             const int o = w + 4 * kk;
@@ -1193,10 +1276,12 @@ __global__ __launch_bounds__(kT) NCONV_WM_ATTR void wgrad_mfma(LayerDev d, BwdAr
                 const bool in = (p == 0 || lane < K - 1) && (unsigned)oh < (unsigned)L.Ho &&
                                 (unsigned)ow < (unsigned)L.Wo;
                 const unsigned off = in ? (unsigned)(oh * L.Wo + ow) * 4u : OOB;
-                gq[kk][p][0] = ld_f32(rgy, off);
                 gq[kk][p][1] = ld_f32(rco, off);
                 gq[kk][p][2] = ld_f32(ry, off);
-                gq[kk][p][3] = a.gco ? ld_f32(plane_rsrc(a.gco + base, plane * 4), off) : 0.f;
+                if constexpr (!T7) {
+                    gq[kk][p][0] = ld_f32(rgy, off);
+                    gq[kk][p][3] = a.gco ? ld_f32(plane_rsrc(a.gco + base, plane * 4), off) : 0.f;
+                }
                 if constexpr (GP) {
                     const size_t pbase = ((size_t)b * COUT + o) * pplane;
                     const unsigned po = in ? pool_elem_off(oh, ow, Hp, Wp, OOB) : OOB;
@@ -1210,13 +1295,18 @@ __global__ __launch_bounds__(kT) NCONV_WM_ATTR void wgrad_mfma(LayerDev d, BwdAr
     };
     // the wave's output channels' bias and normaliser, read once (not per row: a load right before
     // its use would put a global-memory round trip into every row)
-    float bias_o[C::OPW], wsum_o[C::OPW];
+    float bias_o[C::OPW], wsum_o[C::OPW], w7_o[C::OPW];
 #pragma unroll
     for (int kk = 0; kk < C::OPW; ++kk) {
         bias_o[kk] = L.bias[w + 4 * kk];
         wsum_o[kk] = L.wsum[w + 4 * kk];
+        w7_o[kk] = T7 ? a.t7w[w + 4 * kk] : 0.f;
     }
     auto store_g = [&](int buf, int oh_cur) {
+        float n7[2], d7[2];
+        if constexpr (T7)
+#pragma unroll
+            for (int p = 0; p < 2; ++p) t7_nd(a, g7[p][0], g7[p][1], g7[p][2], n7[p], d7[p]);
 #pragma unroll
         for (int kk = 0; kk < C::OPW; ++kk) {
             const int o = w + 4 * kk;
@@ -1225,7 +1315,17 @@ __global__ __launch_bounds__(kT) NCONV_WM_ATTR void wgrad_mfma(LayerDev d, BwdAr
             for (int p = 0; p < 2; ++p) {
                 const int col = p * 64 + lane;
                 if (p == 1 && lane >= K - 1) continue;
-                float gy = gq[kk][p][0], gco = gq[kk][p][3];
+                float gy, gco;
+                if constexpr (T7) {
+                    t7_gy(w7_o[kk], n7[p], d7[p], gq[kk][p][2], gq[kk][p][1], gy, gco);
+                    if (col >= K - 1) {  // nconv7's weight gradient: corr(x*c, gN7) + corr(c, gD7)
+                        w7n[kk] = fmaf(gq[kk][p][2] * gq[kk][p][1], n7[p], w7n[kk]);
+                        w7d[kk] = fmaf(gq[kk][p][1], d7[p], w7d[kk]);
+                    }
+                } else {
+                    gy = gq[kk][p][0];
+                    gco = gq[kk][p][3];
+                }
                 if constexpr (GP) {
                     const int ow = ow0 - (K - 1) + col;
                     pool_route(gy, gco, gq[kk][p][4], gq[kk][p][5], __builtin_bit_cast(unsigned, gq[kk][p][6]),
@@ -1332,6 +1432,20 @@ __global__ __launch_bounds__(kT) NCONV_WM_ATTR void wgrad_mfma(LayerDev d, BwdAr
             out[NW + COUT + w + 4 * kk] = ss;
         }
     }
+    if constexpr (T7) {  // nconv7's partial row: 8 weights, then its (unused) sum gy / sum gcout*cout slots
+        float* o7 = a.t7part + (size_t)blockIdx.x * 10;
+#pragma unroll
+        for (int kk = 0; kk < C::OPW; ++kk) {
+            float sn = w7n[kk], sd = w7d[kk];
+#pragma unroll
+            for (int sh = 32; sh > 0; sh >>= 1) {
+                sn += __shfl_xor(sn, sh);
+                sd += __shfl_xor(sd, sh);
+            }
+            if (lane == 0) o7[w + 4 * kk] = sn + sd;
+        }
+        if (tid < 2) o7[8 + tid] = 0.f;
+    }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1427,6 +1541,10 @@ size_t bwd_workspace_bytes(const LayerDev& d) {
     return bytes;
 }
 
+size_t bwd_tail_workspace_bytes(const nconv_layer& L) {
+    return (wm_grid(L).nblk + kReduceSplit) * 10 * sizeof(float);
+}
+
 size_t bwd_head_workspace_bytes(const nconv_layer& L) {
     using D = DgCfg<8, 5>;
     const size_t nblk = (size_t)((L.W + D::TW - 1) / D::TW) * ((L.H + D::TH - 1) / D::TH) * L.B;
@@ -1448,7 +1566,7 @@ void plan_bwd(const nconv_layer& L, int* dgrad, int* wgrad) {
 // Returns 0, or -EIO when the bf16 weight-gradient grid would not fit the workspace (it cannot:
 // its strips are wider than wgrad_mfma's, for which the workspace is sized; checked anyway, so
 // a bf16 request never silently runs another kernel).
-template <int CIN, int COUT, int K, int MODE, bool GP = false, bool HW = false>
+template <int CIN, int COUT, int K, int MODE, bool GP = false, bool HW = false, bool T7 = false>
 static int go_bwd_tiled(const LayerDev& d, const BwdArgs& a, float* part, float* tx, float* tc,
                         hipStream_t st) {
     const nconv_layer& L = d.L;
@@ -1464,7 +1582,7 @@ static int go_bwd_tiled(const LayerDev& d, const BwdArgs& a, float* part, float*
                 if (dgrad_phase_ok(L)) {  // box weights into the (then unused) staging planes
                     hipLaunchKernelGGL(box_weights, dim3(1024 / kT), dim3(kT), 0, st, L.weight,
                                        MODE == NCONV_LOAD_UPCAT_SKIP_FIRST ? 8 : 0, tx);
-                    hipLaunchKernelGGL((dgrad_phase<MODE>), g, dim3(kT), 0, st, d, a, tx);
+                    hipLaunchKernelGGL((dgrad_phase<MODE, T7>), g, dim3(kT), 0, st, d, a, tx);
                 } else {
                     hipLaunchKernelGGL((dgrad_tiled<CIN, COUT, K, MODE>), g, dim3(kT), 0, st, d, a, tx, tc);
                 }
@@ -1490,11 +1608,20 @@ static int go_bwd_tiled(const LayerDev& d, const BwdArgs& a, float* part, float*
             const int nw = COUT * CIN * K * K;
             launch_wgrad_reduce(a, part, nblk, nw, COUT, CIN * K * K, L.wsum, st);
         } else if (a.gw || a.gb) {
-            const int per_cu = dev_occupancy((const void*)wgrad_mfma<CIN, COUT, K, MODE, GP>, kT, 0);
+            const int per_cu = dev_occupancy((const void*)wgrad_mfma<CIN, COUT, K, MODE, GP, T7>, kT, 0);
             const int resident = device_cus() * (per_cu < kMfmaMaxPerCu ? per_cu : kMfmaMaxPerCu);
             const WmGrid g = wm_grid(L, kMfmaRounds * resident);
-            hipLaunchKernelGGL((wgrad_mfma<CIN, COUT, K, MODE, GP>), dim3(g.nblk), dim3(kT), 0, st, d, a, part,
+            hipLaunchKernelGGL((wgrad_mfma<CIN, COUT, K, MODE, GP, T7>), dim3(g.nblk), dim3(kT), 0, st, d, a, part,
                                g.nstrip, g.nseg, g.seg_rows);
+            if constexpr (T7) {  // nconv7's weight-gradient partial rows: one per wgrad workgroup
+                if (a.defer) {
+                    *a.t7nparts = (int)g.nblk;
+                } else {
+                    const RedJob J{a.t7part, a.t7s, a.t7gw, nullptr, (int)g.nblk, 8, 1, 8};
+                    const char* why = nullptr;
+                    launch_wgrad_reduce_multi(1, &J, st, &why);
+                }
+            }
             const int nw = COUT * CIN * K * K;
             launch_wgrad_reduce(a, part, (int)g.nblk, nw, COUT, CIN * K * K, L.wsum, st);
         }
@@ -1562,6 +1689,16 @@ int launch_bwd(const LayerDev& d, const BwdArgs& a, hipStream_t st, const char**
         }
         if (a.hpart) go_bwd_tiled<8, 8, 5, NCONV_LOAD_PLAIN, true, true>(d, a, part, tx, tc, st);
         else go_bwd_tiled<8, 8, 5, NCONV_LOAD_PLAIN, true>(d, a, part, tx, tc, st);
+        return last_err(why);
+    }
+    if (a.t7part) {
+        if (!(path == kTiled && dgrad_phase_ok(L) && L.load_mode == NCONV_LOAD_UPCAT_UP_FIRST && L.PH == 0 &&
+              L.PW == 0 && (a.gw || a.gb))) {
+            *why = "fused tail backward needs nconv6's exact-fp32 geometry (16->8 3x3, padding 0, upsample-first "
+                   "exactly-2x concat) with its weight gradient requested";
+            return -95;
+        }
+        go_bwd_tiled<16, 8, 3, NCONV_LOAD_UPCAT_UP_FIRST, false, false, true>(d, a, part, tx, tc, st);
         return last_err(why);
     }
     if (a.hpart) {

@@ -239,11 +239,16 @@ size_t nconv_bwd_head_workspace_bytes(const nconv_layer* L) {
     return nconv::bwd_head_workspace_bytes(*L);
 }
 
+size_t nconv_bwd_tail_workspace_bytes(const nconv_layer* L) {
+    if (!L || validate(L, false)) return 0;
+    return nconv::bwd_tail_workspace_bytes(*L);
+}
+
 int nconv_bwd_ex(const nconv_layer* L, nconv_bwd_io* io, void* workspace, size_t workspace_bytes,
                  unsigned flags, void* stream) {
     if (const char* why = validate(L, true)) return fail(-22, "nconv_bwd", why);
     if (!io) return fail(-22, "nconv_bwd", "null io");
-    if (!io->y || !io->cout || !io->gy) return fail(-22, "nconv_bwd", "null y/cout/gy");
+    if (!io->y || !io->cout || (!io->gy && !io->tail)) return fail(-22, "nconv_bwd", "null y/cout/gy");
     const LayerDev d = make_dev(L);
     const size_t need = nconv::bwd_workspace_bytes(d);
     if (need && (!workspace || workspace_bytes < need)) return fail(-22, "nconv_bwd", "workspace too small");
@@ -278,6 +283,28 @@ int nconv_bwd_ex(const nconv_layer* L, nconv_bwd_io* io, void* workspace, size_t
         a.hgb = io->head_gbias;
         a.hnparts = &io->head_nparts;
     }
+    io->tail_nparts = 0;
+    if (const nconv_layer* T = io->tail) {
+        if (const char* why = validate(T, true)) return fail(-22, "nconv_bwd", why);
+        if (T->Cin != L->Cout || T->Cout != 1 || T->KH != 1 || T->KW != 1 || T->PH != 2 || T->PW != 2 ||
+            T->SH != 1 || T->SW != 1 || T->DH != 1 || T->DW != 1 || T->groups != 1 ||
+            T->load_mode != NCONV_LOAD_PLAIN || T->B != L->B || T->H != L->Ho || T->W != L->Wo)
+            return fail(-22, "nconv_bwd", "tail must be a 1x1 padding-2 layer on this layer's outputs (nconv7)");
+        if (!io->tail_y || !io->tail_cout || !io->tail_gy) return fail(-22, "nconv_bwd", "null tail planes");
+        if (!io->tail_workspace || io->tail_workspace_bytes < nconv::bwd_tail_workspace_bytes(*L))
+            return fail(-22, "nconv_bwd", "tail workspace too small (nconv_bwd_tail_workspace_bytes)");
+        if (!defer && !io->tail_gw) return fail(-22, "nconv_bwd", "tail output is NULL");
+        a.t7w = T->weight;
+        a.t7b = T->bias;
+        a.t7s = T->wsum;
+        a.t7eps = T->eps;
+        a.t7gy = io->tail_gy;
+        a.t7y = io->tail_y;
+        a.t7co = io->tail_cout;
+        a.t7part = (float*)io->tail_workspace;
+        a.t7gw = io->tail_gw;
+        a.t7nparts = &io->tail_nparts;
+    }
     const char* why = nullptr;
     int rc = nconv::launch_bwd(d, a, (hipStream_t)stream, &why);
     if (rc) return fail(rc, "nconv_bwd", why);
@@ -288,7 +315,8 @@ int nconv_bwd(const nconv_layer* L, const float* y, const float* cout, const flo
               const float* gcout, float* gxa, float* gca, float* gxb, float* gcb, float* gw,
               float* gbias, void* workspace, size_t workspace_bytes, unsigned flags, void* stream) {
     nconv_bwd_io io{y, cout, gy, gcout, gxa, gca, gxb, gcb, gw, gbias, nullptr, nullptr, nullptr,
-                    nullptr, nullptr, 0, nullptr, nullptr, 0};
+                    nullptr, nullptr, 0, nullptr, nullptr, 0,
+                    nullptr, nullptr, nullptr, nullptr, nullptr, 0, nullptr, 0};
     return nconv_bwd_ex(L, &io, workspace, workspace_bytes, flags, stream);
 }
 

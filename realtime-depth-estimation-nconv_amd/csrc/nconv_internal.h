@@ -56,7 +56,21 @@ struct BwdArgs {
     float* hgw;       // nconv1's gW / gb (undeferred: reduced right after the kernel)
     float* hgb;
     int* hnparts;     // out (defer): the number of nconv1 partial rows written
+    // optional fused backward of the consumer nconv7 (8 -> 1, 1x1, padding 2) of this layer's
+    // outputs: gy / gco of this layer are formed from nconv7's (gy, y, cout) planes (B, 1, Ho + 4,
+    // Wo + 4) and its weights; nconv7's weight gradient goes to t7part (10-float partial rows)
+    const float* t7w;
+    const float* t7b;
+    const float* t7s;
+    float t7eps;
+    const float* t7gy;
+    const float* t7y;
+    const float* t7co;
+    float* t7part;
+    float* t7gw;
+    int* t7nparts;
 };
+size_t bwd_tail_workspace_bytes(const nconv_layer& L6);
 size_t bwd_head_workspace_bytes(const nconv_layer& L2);
 
 // One layer's deferred weight-gradient reduction (nconv_wgrad_reduce): its workspace's partial rows.

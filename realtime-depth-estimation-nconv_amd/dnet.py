@@ -107,10 +107,22 @@ class DNETFn(torch.autograd.Function):
                            (*(ga or (None, None)), *(gb_ or (None, None))), gw[k - 1], gb[k - 1], accumulate=acc,
                            defer=red, pool_grad=pool_grad)
 
-        G[8] = (e(X[8][0]), e(X[8][1]))
-        bwd(9, 8, 0, G[8], None)                        # nconv7
         G[2], G[7] = (e(X[2][0]), e(X[2][1])), (e(X[7][0]), e(X[7][1]))
-        bwd(8, 2, 7, G[2], G[7])                        # nconv6: nconv2's output (overwrite) + up
+        exact_up = X[2][0].shape[2:] == tuple(2 * v for v in X[7][0].shape[2:])  # nconv6's phase form
+        if FUSE_TAIL_BWD and ctx.pooled and exact_up and gw[8] is not None:  # (c9 is non-differentiable)
+            # nconv7's backward inside nconv6's (nconv_bwd_ex tail): its input gradient never reaches
+            # HBM; its bias gradient is the sum of its output gradient (every output pixel, padding ring
+            # included, as autograd's conv bias gradient)
+            g9c = g9.contiguous()
+            layer_backward(sp[7], (X[2][0], X[2][1], X[7][0], X[7][1], *W[7]), X[8][0], X[8][1], None, None,
+                           (*G[2], *G[7]), gw[7], gb[7], defer=red,
+                           tail=(sp[8], *W[8], X[9][0], X[9][1], g9c, gw[8]))
+            if gb[8] is not None:
+                torch.sum(g9c, dim=(0, 2, 3), out=gb[8])
+        else:
+            G[8] = (e(X[8][0]), e(X[8][1]))
+            bwd(9, 8, 0, G[8], None)                        # nconv7
+            bwd(8, 2, 7, G[2], G[7])                        # nconv6: nconv2's output (overwrite) + up
         G[3], G[6] = (e(X[3][0]), e(X[3][1])), (e(X[6][0]), e(X[6][1]))
         bwd(7, 3, 6, G[3], G[6])                        # nconv5: down1's output + up
         G[4], G[5] = (e(X[4][0]), e(X[4][1])), (e(X[5][0]), e(X[5][1]))
@@ -124,7 +136,7 @@ class DNETFn(torch.autograd.Function):
             bwd(4, 0, 0, gp3, None, src_a=(p3x, p3c), spec=plain[1], pool_grad=(*gp4, a4))  # down2
             gp2 = (e(p2x), e(p2c))
             bwd(3, 0, 0, gp2, None, src_a=(p2x, p2c), spec=plain[0], pool_grad=(*gp3, a3))  # down1
-            if not need[1]:  # nconv2's input gradient feeds nconv1's weight gradient in-tile
+            if FUSE_HEAD_BWD and not need[1]:  # nconv2's input gradient feeds nconv1's weight gradient in-tile
                 layer_backward(sp[1], (X[1][0], X[1][1], None, None, *W[1]), X[2][0], X[2][1], *G[2],
                                (None, None, None, None), gw[1], gb[1], defer=red, pool_grad=(*gp2, a2),
                                head=(sp[0], S, *W[0], gw[0], gb[0]))
@@ -149,6 +161,12 @@ class DNETFn(torch.autograd.Function):
         for i in range(9):
             out += [gw[i], gb[i], None]
         return tuple(out + [None] * ctx.n_extra)
+
+
+# Exact-fp32 training backward (DNETFn, pooled graph): nconv7's backward inside nconv6's and nconv1's
+# weight gradient inside nconv2's input gradient (nconv_bwd_ex tail / head). Switches for tests.
+FUSE_TAIL_BWD = True
+FUSE_HEAD_BWD = True
 
 
 def _materialise_pool(S):

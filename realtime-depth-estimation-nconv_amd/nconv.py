@@ -222,7 +222,7 @@ class NConvLayerFn(torch.autograd.Function):
 
 
 def layer_backward(spec: LayerSpec, inputs, y, co, gy, gco, gin, gw, gb, accumulate=False, defer=None,
-                   pool_grad=None, head=None):
+                   pool_grad=None, head=None, tail=None):
     """nconv_bwd of one fused layer: gin = (gxa, gca, gxb, gcb) (None: skip) overwritten, or added
     into with accumulate=True (NCONV_BWD_ACCUMULATE: a tensor consumed by two layers); gw, gb
     overwritten (None: skip). defer: a WgradReduce collecting the layer's weight-gradient partial
@@ -230,13 +230,16 @@ def layer_backward(spec: LayerSpec, inputs, y, co, gy, gco, gin, gw, gb, accumul
     gcout_pool, argmax) -- the gradient of this layer's 2x2-pooled outputs (the next down layer read
     layer_forward_pooled's copies), routed into gy / gco by the argmax codes (nconv_bwd_ex). head:
     (spec, S, weight, bias, wsum, gw, gb) of the producer nconv1, whose weight / bias gradients are
-    then computed inside this layer's input gradient (nconv_bwd_ex head; gin's gxa / gca optional)."""
+    then computed inside this layer's input gradient (nconv_bwd_ex head; gin's gxa / gca optional).
+    tail: (spec, weight, bias, wsum, y9, cout9, gy9, gw9) of the 1x1 consumer nconv7, whose backward
+    is fused into this layer's (nconv_bwd_ex tail; gy / gco are then unused and may be None; nconv7's
+    bias gradient is the caller's)."""
     xa, ca, xb, cb, weight, bias, wsum = inputs
     gxa, gca, gxb, gcb = gin
     dev = y.device
-    if gy is None:
+    if gy is None and tail is None:
         gy = torch.zeros_like(y)
-    gy = gy.contiguous()
+    gy = gy.contiguous() if gy is not None else None
     gco = gco.contiguous() if gco is not None else None
     L = spec.descriptor(xa, ca, xb, cb, weight, bias, wsum)
     lib = _lib.lib()
@@ -257,12 +260,23 @@ def layer_backward(spec: LayerSpec, inputs, y, co, gy, gco, gin, gw, gb, accumul
         io.head = _lib.ctypes.pointer(HL)
         io.head_workspace, io.head_workspace_bytes = hws.data_ptr(), hbytes
         io.head_gw, io.head_gbias = _lib.ptr(hgw), _lib.ptr(hgb)
+    if tail is not None:
+        tspec, tw, tb, ts, ty, tco, tgy, tgw = tail
+        TL = tspec.descriptor(y, co, None, None, tw, tb, ts)
+        tbytes = lib.nconv_bwd_tail_workspace_bytes(_lib.ctypes.byref(L))
+        tws = torch.empty(max(tbytes, 1), dtype=torch.uint8, device=dev)
+        io.tail = _lib.ctypes.pointer(TL)
+        io.tail_y, io.tail_cout, io.tail_gy = ty.data_ptr(), tco.data_ptr(), tgy.contiguous().data_ptr()
+        io.tail_workspace, io.tail_workspace_bytes = tws.data_ptr(), tbytes
+        io.tail_gw = _lib.ptr(tgw)
     rc = lib.nconv_bwd_ex(_lib.ctypes.byref(L), _lib.ctypes.byref(io), _lib.ptr(ws), ws_bytes, flags,
                           _lib.stream_handle(dev))
     if defer is not None and rc >= 0:
         defer.add(L, ws, rc, gw, gb)
         if head is not None:
             defer.add(HL, hws, io.head_nparts, hgw, hgb)
+        if tail is not None:
+            defer.add(TL, tws, io.tail_nparts, tgw, None)
         return
     _lib.check(rc, "nconv_bwd")
 

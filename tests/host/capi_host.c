@@ -38,7 +38,9 @@ int main(void) {
     F(nconv_bwd_io, gca); F(nconv_bwd_io, gxb); F(nconv_bwd_io, gcb); F(nconv_bwd_io, gw); F(nconv_bwd_io, gbias);
     F(nconv_bwd_io, gy_pool); F(nconv_bwd_io, gcout_pool); F(nconv_bwd_io, pool_argmax); F(nconv_bwd_io, head);
     F(nconv_bwd_io, head_workspace); F(nconv_bwd_io, head_workspace_bytes); F(nconv_bwd_io, head_gw);
-    F(nconv_bwd_io, head_gbias); F(nconv_bwd_io, head_nparts);
+    F(nconv_bwd_io, head_gbias); F(nconv_bwd_io, head_nparts); F(nconv_bwd_io, tail); F(nconv_bwd_io, tail_y);
+    F(nconv_bwd_io, tail_cout); F(nconv_bwd_io, tail_gy); F(nconv_bwd_io, tail_workspace);
+    F(nconv_bwd_io, tail_workspace_bytes); F(nconv_bwd_io, tail_gw); F(nconv_bwd_io, tail_nparts);
     S(nconv_bn_train);
     F(nconv_bn_train, B); F(nconv_bn_train, C); F(nconv_bn_train, H); F(nconv_bn_train, W); F(nconv_bn_train, x);
     F(nconv_bn_train, gamma); F(nconv_bn_train, beta); F(nconv_bn_train, running_mean);

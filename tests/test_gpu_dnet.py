@@ -75,7 +75,8 @@ def test_whole_graph_autograd_matches_per_layer(nconv_amd, gpu, H, W):
     """DNETFn (one autograd node, shared-tensor gradients accumulated in the dgrad kernels) against
     one NConvLayerFn node per layer (PyTorch adds the two consumers' gradients): same kernels, so
     outputs are bitwise equal and gradients agree to fp32 round-off of the accumulation (1e-6
-    relative per tensor); the input gradient of S too."""
+    relative per tensor; 1e-5 for nconv7's, fused into nconv6's backward); the input gradient of S
+    too."""
     g = torch.Generator().manual_seed(21)
     S = sparse_depth(g, 2, H, W).to(gpu)
     gt = (torch.rand(2, 1, H, W, generator=g) * 80).to(gpu)
@@ -91,8 +92,10 @@ def test_whole_graph_autograd_matches_per_layer(nconv_amd, gpu, H, W):
     (oa, ga, pa), (ob, gb, pb) = res
     assert torch.equal(oa, ob)
     assert set(pa) == set(pb) and len(pa) == 18
-    for a, b in [(ga, gb)] + [(pa[k], pb[k]) for k in pa]:
-        assert (a - b).abs().max().item() <= 1e-6 * b.abs().max().item() + 1e-30
+    for k, a, b in [("S", ga, gb)] + [(k, pa[k], pb[k]) for k in pa]:
+        # nconv7's weight gradient is computed inside nconv6's backward by DNETFn (a reassociated sum)
+        tol = 1e-5 if k.startswith("d_net.nconv7.") else 1e-6
+        assert (a - b).abs().max().item() <= tol * b.abs().max().item() + 1e-30, k
 
 
 @pytest.mark.parametrize("H,W", [(64, 96), (45, 67)])
@@ -101,12 +104,15 @@ def test_materialised_pool_matches_pool_on_load(nconv_amd, gpu, H, W, monkeypatc
     argmax codes; pooled-sized down-layer input gradients routed into the producer's {gN, gD} by
     nconv_bwd_ex) against pooling on load with full-resolution accumulation: the same sums in the
     same order, so outputs and every gradient are bitwise equal (odd sizes: rows / columns no
-    window covers get no pooled gradient in both)."""
+    window covers get no pooled gradient in both) -- except the weight gradients the pooled graph
+    computes inside a neighbour's kernel (nconv7's in nconv6's backward, nconv1's in nconv2's when S
+    needs no gradient), which are the same sums reassociated (normwise 1e-5)."""
     g = torch.Generator().manual_seed(22)
     S = sparse_depth(g, 2, H, W).to(gpu)
     gt = (torch.rand(2, 1, H, W, generator=g) * 80).to(gpu)
     dnet = sys.modules[nconv_amd.DNET.__module__]
     res = []
+    monkeypatch.setattr(dnet, "FUSE_TAIL_BWD", False)
     for pooled in (True, False):
         monkeypatch.setattr(dnet, "_materialise_pool", lambda S_, v=pooled: v)
         net = make_net(nconv_amd, "generalized", gpu)
@@ -117,6 +123,11 @@ def test_materialised_pool_matches_pool_on_load(nconv_amd, gpu, H, W, monkeypatc
     (oa, ga, pa), (ob, gb, pb) = res
     assert torch.equal(oa, ob) and torch.equal(ga, gb)
     assert set(pa) == set(pb) and len(pa) == 18
+
+    def close(a, b, k):  # fused-in weight gradients (nconv1, nconv7): fp32 reassociation only
+        rel = ((a - b).abs().max() / b.abs().max()).item()
+        assert rel <= 1e-5, (k, rel)
+
     for k in pa:
         assert torch.equal(pa[k], pb[k]), k
 
@@ -131,10 +142,24 @@ def test_materialised_pool_matches_pool_on_load(nconv_amd, gpu, H, W, monkeypatc
     assert torch.equal(out.detach(), oa) and set(pc) == set(pa)
     for k in pc:
         if k.startswith("d_net.nconv1."):
-            rel = ((pc[k] - pa[k]).abs().max() / pa[k].abs().max()).item()
-            assert rel <= 1e-5, (k, rel)
+            close(pc[k], pa[k], k)
         else:
             assert torch.equal(pc[k], pa[k]), k
+
+    # nconv7's backward fused into nconv6's (nconv_bwd_ex tail, exactly-2x sizes): nconv6's output
+    # gradient formed in-kernel with the 1x1 dgrad's own operations; nconv7's weight gradient
+    # reassociated, its bias gradient a torch sum of its output gradient (normwise 1e-5 each)
+    if H % 8 == 0 and W % 8 == 0:
+        monkeypatch.setattr(dnet, "FUSE_TAIL_BWD", True)
+        net = make_net(nconv_amd, "generalized", gpu)
+        x = S.clone().requires_grad_(True)
+        out = net(x)
+        nconv_amd.train.calculate_loss(out[0], gt[0], True).backward()
+        pt = {k: v.grad for k, v in net.named_parameters() if v.grad is not None}
+        assert torch.equal(out.detach(), oa) and set(pt) == set(pa)
+        close(x.grad, ga, "S")
+        for k in pt:
+            close(pt[k], pa[k], k)
 
 
 def test_enforcepos_drift(nconv_amd, gpu):
