@@ -139,12 +139,13 @@ int nconv_fwd(const nconv_layer* L, float* y, float* cout, void* stream);
  * first maximum wins, NaN propagates) into y_pool, cout_pool (B, Cout, Ho/2, Wo/2): the input of
  * the next down layer (models/step1.py:62-75), which then loads it with NCONV_LOAD_PLAIN instead
  * of re-reading and pooling the full-resolution tensors. Built for the tiled DNET layer shapes
- * (returns -EOPNOTSUPP otherwise). argmax (may be NULL; exact-fp32 tiled layers only): one byte
- * per pooled element, the window slot (2*row + column) of y's first maximum in bits 0-1 and of
- * cout's in bits 2-3 -- what nconv_bwd_ex routes the pooled tensors' gradient by (the indices of
+ * (returns -EOPNOTSUPP otherwise). argmax (may be NULL; exact-fp32 tiled layers only): one 32-bit
+ * word per pooled element (not a byte: the backward's staging then loads it like its float
+ * operands, with no conversion ahead of its use), the window slot (2*row + column) of y's first
+ * maximum in bits 0-1 and of cout's in bits 2-3 -- what nconv_bwd_ex routes the pooled tensors' gradient by (the indices of
  * max_pool2d_with_indices, step1.py:62-75 under autograd). */
 int nconv_fwd_pooled(const nconv_layer* L, float* y, float* cout, float* y_pool, float* cout_pool,
-                     unsigned char* argmax, void* stream);
+                     unsigned int* argmax, void* stream);
 
 /* Inference-only fused head: nconv1 on the thresholded sparse depth (models/step1.py:53-57;
  * L1: Cin 1, Cout 8, 5x5, padding 2, NCONV_LOAD_THRESH) is evaluated while staging nconv2's input
@@ -233,7 +234,7 @@ typedef struct nconv_bwd_io {
     float* gbias;
     const float* gy_pool;           /* optional pooled-output gradient (see above) */
     const float* gcout_pool;
-    const unsigned char* pool_argmax;
+    const unsigned int* pool_argmax;
     /* optional: the weight gradient of the layer that produced L's input, fused into L's input
      * gradient (DNET training: nconv2's backward computes nconv1's gW / gb in-tile, so nconv1's
      * input gradient never reaches HBM and nconv1 needs no nconv_bwd). head = nconv1's descriptor

@@ -126,25 +126,23 @@ struct GTileStager {
             v[2][k] = ld_f32(ry, go[k]);
             v[3][k] = ld_f32(rco, go[k]);
         }
-        if (a.gco) {
-            const __amdgpu_buffer_rsrc_t rgc = plane_rsrc(a.gco + base, plane * 4);
+        // gcout may be absent (= 0): a zero-sized resource then reads 0 -- no branch, since a branch
+        // here makes the compiler wait for all of this stage's loads at the join, i.e. right after
+        // issuing them instead of behind the next plane's FMAs
+        const __amdgpu_buffer_rsrc_t rgc = plane_rsrc(a.gco ? a.gco + base : a.y, a.gco ? plane * 4 : 0);
 #pragma unroll
-            for (int k = 0; k < NE; ++k) v[1][k] = ld_f32(rgc, go[k]);
-        } else {
-#pragma unroll
-            for (int k = 0; k < NE; ++k) v[1][k] = 0.f;
-        }
+        for (int k = 0; k < NE; ++k) v[1][k] = ld_f32(rgc, go[k]);
         if constexpr (GP) {
             const int pplane = (L.Ho >> 1) * (L.Wo >> 1);
             const size_t pbase = ((size_t)b * L.Cout + o) * pplane;
             const __amdgpu_buffer_rsrc_t rpy = plane_rsrc(a.gpy + pbase, pplane * 4);
             const __amdgpu_buffer_rsrc_t rpc = plane_rsrc(a.gpc + pbase, pplane * 4);
-            const __amdgpu_buffer_rsrc_t rpa = plane_rsrc((const float*)(a.parg + pbase), pplane);
+            const __amdgpu_buffer_rsrc_t rpa = plane_rsrc((const float*)(a.parg + pbase), pplane * 4);
 #pragma unroll
             for (int k = 0; k < NE; ++k) {
                 v[4][k] = ld_f32(rpy, gpo[k]);
                 v[5][k] = ld_f32(rpc, gpo[k]);
-                v[6][k] = __builtin_bit_cast(float, ld_u8(rpa, gpo[k] >> 2));
+                v[6][k] = ld_f32(rpa, gpo[k]);  // the code word, carried as raw bits until store
             }
         }
     }
@@ -1280,15 +1278,14 @@ __global__ __launch_bounds__(kT) NCONV_WM_ATTR void wgrad_mfma(LayerDev d, BwdAr
                 gq[kk][p][2] = ld_f32(ry, off);
                 if constexpr (!T7) {
                     gq[kk][p][0] = ld_f32(rgy, off);
-                    gq[kk][p][3] = a.gco ? ld_f32(plane_rsrc(a.gco + base, plane * 4), off) : 0.f;
+                    gq[kk][p][3] = ld_f32(plane_rsrc(a.gco ? a.gco + base : a.y, a.gco ? plane * 4 : 0), off);
                 }
                 if constexpr (GP) {
                     const size_t pbase = ((size_t)b * COUT + o) * pplane;
                     const unsigned po = in ? pool_elem_off(oh, ow, Hp, Wp, OOB) : OOB;
                     gq[kk][p][4] = ld_f32(plane_rsrc(a.gpy + pbase, pplane * 4), po);
                     gq[kk][p][5] = ld_f32(plane_rsrc(a.gpc + pbase, pplane * 4), po);
-                    gq[kk][p][6] = __builtin_bit_cast(
-                        float, ld_u8(plane_rsrc((const float*)(a.parg + pbase), pplane), po >> 2));
+                    gq[kk][p][6] = ld_f32(plane_rsrc((const float*)(a.parg + pbase), pplane * 4), po);
                 }
             }
         }

@@ -129,7 +129,7 @@ int nconv_fwd(const nconv_layer* L, float* y, float* cout, void* stream) {
 }
 
 int nconv_fwd_pooled(const nconv_layer* L, float* y, float* cout, float* y_pool, float* cout_pool,
-                     unsigned char* argmax, void* stream) {
+                     unsigned int* argmax, void* stream) {
     if (const char* why = validate(L, true)) return fail(-22, "nconv_fwd_pooled", why);
     if (!y || !cout || !y_pool || !cout_pool) return fail(-22, "nconv_fwd_pooled", "null output");
     if (L->Ho < 2 || L->Wo < 2) return fail(-22, "nconv_fwd_pooled", "output too small to pool");

@@ -337,10 +337,6 @@ __device__ __forceinline__ float ld_f32s(__amdgpu_buffer_rsrc_t r, unsigned off,
     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, soff, 0));
 }
 
-__device__ __forceinline__ unsigned ld_u8(__amdgpu_buffer_rsrc_t r, unsigned off) {
-    return __builtin_amdgcn_raw_buffer_load_b8(r, off, 0, 0);
-}
-
 // Pooled-gradient routing (training backward of a layer whose outputs feed a 2x2 max-pool that
 // nconv_fwd_pooled materialised with its argmax codes): the output element at window slot `sub`
 // (2*row + column) receives the pooled element's gradient when it is that window's first maximum

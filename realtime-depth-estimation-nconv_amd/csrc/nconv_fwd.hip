@@ -197,21 +197,21 @@ __global__ __launch_bounds__(NTH) void fwd_tiled(LayerDev d, float* __restrict__
                 const __amdgpu_buffer_rsrc_t rpc = plane_rsrc(t.pc + pofs, ppbytes);
                 // with t.parg: each window's first-maximum slots (y in bits 0-1, cout in bits 2-3,
                 // slot = 2*row + column), what the training backward routes the pooled gradient by
-                unsigned char* parg = t.parg ? t.parg + pofs : nullptr;
+                unsigned* parg = t.parg ? t.parg + pofs : nullptr;
                 if constexpr (C::P == 1) {  // the window's right column sits in lane l^1
                     const float ya = shfl_xor1(yv[0]), ca = shfl_xor1(cv[0]);
                     const float yd = shfl_xor1(yb[0]), cd = shfl_xor1(cb[0]);
                     int ay, ac;
                     st_f32(rpy, po[0], pool4(yv[0], ya, yb[0], yd, ay));
                     st_f32(rpc, po[0], pool4(cv[0], ca, cb[0], cd, ac));
-                    if (parg && po[0] != OOB) parg[po[0] >> 2] = (unsigned char)(ay | (ac << 2));
+                    if (parg && po[0] != OOB) parg[po[0] >> 2] = (unsigned)(ay | (ac << 2));
                 } else {
 #pragma unroll
                     for (int h = 0; h < C::P / 2; ++h) {
                         int ay, ac;
                         st_f32(rpy, po[h], pool4(yv[2 * h], yv[2 * h + 1], yb[2 * h], yb[2 * h + 1], ay));
                         st_f32(rpc, po[h], pool4(cv[2 * h], cv[2 * h + 1], cb[2 * h], cb[2 * h + 1], ac));
-                        if (parg && po[h] != OOB) parg[po[h] >> 2] = (unsigned char)(ay | (ac << 2));
+                        if (parg && po[h] != OOB) parg[po[h] >> 2] = (unsigned)(ay | (ac << 2));
                     }
                 }
             }
@@ -419,7 +419,7 @@ int plan_fwd(const nconv_layer& L) {
     return fwd_tiled_shape(L) ? NCONV_KERNEL_TILED_FP32 : NCONV_KERNEL_GENERIC;
 }
 
-int launch_fwd(const LayerDev& d, float* y, float* yc, float* py, float* pc, unsigned char* parg, hipStream_t st,
+int launch_fwd(const LayerDev& d, float* y, float* yc, float* py, float* pc, unsigned* parg, hipStream_t st,
                const char** why) {
     const nconv_layer& L = d.L;
     TailArgs t{};

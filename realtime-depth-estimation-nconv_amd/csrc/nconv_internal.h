@@ -15,7 +15,7 @@ struct TailArgs {
     float* out_c;
     float* py;  // optional 2x2 max-pooled copies of y / cout (non-tail launches), (B,Cout,Ho/2,Wo/2)
     float* pc;
-    unsigned char* parg;  // optional (with py): per pooled element the two first-maximum slots
+    unsigned* parg;  // optional (with py): per pooled element the two first-maximum slots
     // fused head (nconv_fwd_head): nconv1 evaluated while staging nconv2's input
     const float* s_in;  // sparse depth (B, 1, H, W)
     const float* w1;    // nconv1 weight (8, 1, 5, 5), bias, s[o]
@@ -44,7 +44,7 @@ struct BwdArgs {
     // codes (nconv_fwd_pooled), routed into gy / gcout while {gN, gD} are formed (pool_route)
     const float* gpy;
     const float* gpc;
-    const unsigned char* parg;
+    const unsigned* parg;
     // optional fused weight gradient of the producer nconv1 (1 -> 8, 5x5, threshold load, padding 2)
     // in the input gradient's epilogue: its sparse input S, bias, normaliser, eps, threshold, and
     // the per-workgroup partial rows (200 weights, 8 sum gy, 8 sum gcout*cout) it writes
@@ -85,7 +85,7 @@ constexpr int kMaxRedJobs = 16;
 int launch_wgrad_reduce_multi(int n, const RedJob* jobs, hipStream_t st, const char** why);
 
 // Forward. Return 0, or a negative errno with *why set.
-int launch_fwd(const LayerDev& d, float* y, float* yc, float* py, float* pc, unsigned char* parg, hipStream_t st,
+int launch_fwd(const LayerDev& d, float* y, float* yc, float* py, float* pc, unsigned* parg, hipStream_t st,
                const char** why);
 bool fwd_mfma_supported(const nconv_layer& L, bool tail, bool pool);
 bool launch_fwd_mfma(const LayerDev& d, float* y, float* yc, const TailArgs& t, bool tail, hipStream_t st);

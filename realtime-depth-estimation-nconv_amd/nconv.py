@@ -153,13 +153,13 @@ def layer_forward_raw(spec: LayerSpec, xa, ca, xb, cb, weight, bias, wsum, out=N
 
 def layer_forward_pooled(spec: LayerSpec, xa, ca, xb, cb, weight, bias, wsum, out=None, argmax=False):
     """nconv_fwd_pooled: (y, cout, maxpool2x2(y), maxpool2x2(cout)) in one launch (written into
-    `out` if given). With argmax=True also the pooling windows' first-maximum codes (uint8, one per
+    `out` if given). With argmax=True also the pooling windows' first-maximum codes (int32, one per
     pooled element; the training backward routes the pooled tensors' gradient by them) as a fifth
     result. No autograd."""
     L = spec.descriptor(xa, ca, xb, cb, weight, bias, wsum)
     sh, shp = (L.B, L.Cout, L.Ho, L.Wo), (L.B, L.Cout, L.Ho // 2, L.Wo // 2)
     y, co, py, pc = _outputs(out, 4, (sh, sh, shp, shp), xa.device)
-    arg = torch.empty(shp, dtype=torch.uint8, device=xa.device) if argmax else None
+    arg = torch.empty(shp, dtype=torch.int32, device=xa.device) if argmax else None
     rc = _lib.lib().nconv_fwd_pooled(_lib.ctypes.byref(L), _lib.ptr(y), _lib.ptr(co), _lib.ptr(py), _lib.ptr(pc),
                                      _lib.ptr(arg), _lib.stream_handle(xa.device))
     _lib.check(rc, "nconv_fwd_pooled")
