@@ -3,9 +3,9 @@
 // Replaces nn.BatchNorm2d in training mode (batch statistics, running-stat update) followed by
 // nn.ReLU — RGBEncoder (models/step2.py:139-143), Basic2d (:189-191), Basic2dTrans (:207-213) —
 // and the autograd of both. HBM-bound passes over NCHW fp32:
-//   forward : bn_stats (1 read: per-chunk count / mean / M2, Welford-style), bn_finalize (per
-//             channel, chunks combined in a fixed order with Chan's formula: deterministic,
-//             no E[x^2] - E[x]^2 cancellation; running mean / unbiased running var updated),
+//   forward : bn_stats (1 read: per-chunk count / mean / M2, Welford-style), bn_finalize (one
+//             block per channel, chunks combined in a fixed tree order with Chan's formula:
+//             deterministic, no E[x^2] - E[x]^2 cancellation; running mean / unbiased running var),
 //             bn_apply (1 read + 1 write: y = [relu](gamma (x - mean) invstd + beta));
 //   backward: bn_bwd_stats (2 reads: sum g' and sum g' xhat per chunk, g' = g masked by the
 //             recomputed ReLU), bn_bwd_finalize (fixed order), bn_bwd_apply (2 reads + 1 write:
@@ -56,6 +56,21 @@ __device__ __forceinline__ void load_chunk(const float* plane, int hw, int j, bo
     }
 }
 
+__device__ __forceinline__ void store_chunk(float* plane, int hw, int j, bool vec, const float (&v)[kPer]) {
+    const int base = j * kChunk;
+#pragma unroll
+    for (int g = 0; g < kPer / 4; ++g) {
+        const int i0 = base + (g * kBT + threadIdx.x) * 4;
+        if (vec && i0 + 3 < hw) {
+            *reinterpret_cast<f4*>(plane + i0) = (f4){v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]};
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (i0 + k < hw) plane[i0 + k] = v[4 * g + k];
+        }
+    }
+}
+
 // part[(c * nparts + b * ncp + j) * 3 + {0,1,2}] = (count, mean, M2) of chunk j of plane (b, c)
 __global__ __launch_bounds__(kBT) void bn_stats(const float* __restrict__ x, int C, int hw, int ncp, int nparts,
                                                 int vec, float* __restrict__ part) {
@@ -85,26 +100,76 @@ __global__ __launch_bounds__(kBT) void bn_stats(const float* __restrict__ x, int
     }
 }
 
-// One thread per channel: Chan's parallel combination of the chunks in a fixed order.
+// One block per channel: thread t combines a contiguous run of the chunks (Chan's parallel formula,
+// in double), then the 256 runs are combined pairwise in a fixed tree order in LDS -- deterministic,
+// and no longer one thread walking 400+ chunks serially.
+__device__ __forceinline__ void chan_combine(double& n, double& mean, double& m2, double nb, double mb, double m2b) {
+    const double nn = n + nb;
+    if (nn == 0.0) return;
+    const double d = mb - mean;
+    mean += d * nb / nn;
+    m2 += m2b + d * d * n * nb / nn;
+    n = nn;
+}
+
 __global__ __launch_bounds__(kBT) void bn_finalize(const float* __restrict__ part, int C, int nparts, float momentum,
                                                    float eps, float* __restrict__ rmean, float* __restrict__ rvar,
                                                    float* __restrict__ mean_out, float* __restrict__ invstd_out) {
-    const int c = blockIdx.x * kBT + threadIdx.x;
-    if (c >= C) return;
+    __shared__ double sn[kBT], sm[kBT], s2[kBT];
+    const int c = blockIdx.x, t = threadIdx.x;
     const float* p = part + (size_t)c * nparts * 3;
-    double n = 0.0, mean = 0.0, m2 = 0.0;  // 418+ chunks per channel: combine in double
-    for (int k = 0; k < nparts; ++k) {
-        const double nb = p[3 * k], mb = p[3 * k + 1], m2b = p[3 * k + 2];
-        const double nn = n + nb, d = mb - mean;
-        mean += d * nb / nn;
-        m2 += m2b + d * d * n * nb / nn;
-        n = nn;
+    const int per = (nparts + kBT - 1) / kBT, k0 = t * per, k1 = min(nparts, k0 + per);
+    double n = 0.0, mean = 0.0, m2 = 0.0;
+    for (int k = k0; k < k1; ++k) chan_combine(n, mean, m2, p[3 * k], p[3 * k + 1], p[3 * k + 2]);
+    sn[t] = n;
+    sm[t] = mean;
+    s2[t] = m2;
+    __syncthreads();
+    for (int h = kBT / 2; h > 0; h >>= 1) {
+        if (t < h) {
+            double a = sn[t], b = sm[t], q = s2[t];
+            chan_combine(a, b, q, sn[t + h], sm[t + h], s2[t + h]);
+            sn[t] = a;
+            sm[t] = b;
+            s2[t] = q;
+        }
+        __syncthreads();
     }
-    const double var = m2 / n;
-    mean_out[c] = (float)mean;
-    invstd_out[c] = (float)(1.0 / sqrt(var + (double)eps));
-    if (rmean) rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * mean);
-    if (rvar) rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * (n > 1.0 ? m2 / (n - 1.0) : var));
+    if (t == 0) {
+        n = sn[0];
+        mean = sm[0];
+        m2 = s2[0];
+        const double var = m2 / n;
+        mean_out[c] = (float)mean;
+        invstd_out[c] = (float)(1.0 / sqrt(var + (double)eps));
+        if (rmean) rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * mean);
+        if (rvar) rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * (n > 1.0 ? m2 / (n - 1.0) : var));
+    }
+}
+
+// fixed-order block sum of per-thread contiguous runs (double), one block per channel
+template <int NV>
+__device__ __forceinline__ void chan_sums(const float* p, int nparts, double (&out)[NV]) {
+    __shared__ double red[NV][kBT];
+    const int t = threadIdx.x;
+    const int per = (nparts + kBT - 1) / kBT, k0 = t * per, k1 = min(nparts, k0 + per);
+    double v[NV];
+#pragma unroll
+    for (int q = 0; q < NV; ++q) v[q] = 0.0;
+    for (int k = k0; k < k1; ++k)
+#pragma unroll
+        for (int q = 0; q < NV; ++q) v[q] += p[NV * k + q];
+#pragma unroll
+    for (int q = 0; q < NV; ++q) red[q][t] = v[q];
+    __syncthreads();
+    for (int h = kBT / 2; h > 0; h >>= 1) {
+        if (t < h)
+#pragma unroll
+            for (int q = 0; q < NV; ++q) red[q][t] += red[q][t + h];
+        __syncthreads();
+    }
+#pragma unroll
+    for (int q = 0; q < NV; ++q) out[q] = red[q][0];
 }
 
 __device__ __forceinline__ float bn_y(float x, float mu, float is, float g, float bt, bool relu) {
@@ -112,29 +177,21 @@ __device__ __forceinline__ float bn_y(float x, float mu, float is, float g, floa
     return relu ? fmaxf(y, 0.f) : y;
 }
 
+// one block per (chunk, channel, image): the channel's parameters are wave-uniform loads, the
+// chunk's elements go through load_chunk's float4 path (no per-element index division)
 __global__ __launch_bounds__(kBT) void bn_apply(const float* __restrict__ x, float* __restrict__ y, int C, int hw,
-                                                size_t n4, const float* __restrict__ mean,
+                                                int vec, const float* __restrict__ mean,
                                                 const float* __restrict__ invstd, const float* __restrict__ gamma,
                                                 const float* __restrict__ beta, int relu) {
-    // hw % 4 == 0: float4 over the whole tensor (a float4 never crosses a plane)
-    for (size_t i = (size_t)blockIdx.x * kBT + threadIdx.x; i < n4; i += (size_t)gridDim.x * kBT) {
-        const int c = (int)((i * 4 / hw) % C);
-        const float mu = mean[c], is = invstd[c], g = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
-        const f4 q = reinterpret_cast<const f4*>(x)[i];
-        reinterpret_cast<f4*>(y)[i] = (f4){bn_y(q.x, mu, is, g, bt, relu), bn_y(q.y, mu, is, g, bt, relu),
-                                           bn_y(q.z, mu, is, g, bt, relu), bn_y(q.w, mu, is, g, bt, relu)};
-    }
-}
-
-__global__ __launch_bounds__(kBT) void bn_apply_scalar(const float* __restrict__ x, float* __restrict__ y, int C,
-                                                       int hw, size_t n, const float* __restrict__ mean,
-                                                       const float* __restrict__ invstd,
-                                                       const float* __restrict__ gamma,
-                                                       const float* __restrict__ beta, int relu) {
-    for (size_t i = (size_t)blockIdx.x * kBT + threadIdx.x; i < n; i += (size_t)gridDim.x * kBT) {
-        const int c = (int)((i / hw) % C);
-        y[i] = bn_y(x[i], mean[c], invstd[c], gamma ? gamma[c] : 1.f, beta ? beta[c] : 0.f, relu);
-    }
+    const int j = blockIdx.x, c = blockIdx.y, b = blockIdx.z;
+    const size_t off = ((size_t)b * C + c) * hw;
+    const float mu = mean[c], is = invstd[c], g = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+    float v[kPer];
+    bool ok[kPer];
+    load_chunk(x + off, hw, j, vec != 0, v, ok);
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) v[k] = bn_y(v[k], mu, is, g, bt, relu);
+    store_chunk(y + off, hw, j, vec != 0, v);
 }
 
 // part[(c * nparts + b * ncp + j) * 2 + {0,1}] = (sum g', sum g' xhat) of chunk j of plane (b, c)
@@ -171,32 +228,37 @@ __global__ __launch_bounds__(kBT) void bn_bwd_stats(const float* __restrict__ gy
 __global__ __launch_bounds__(kBT) void bn_bwd_finalize(const float* __restrict__ part, int C, int nparts,
                                                        float* __restrict__ sums, float* __restrict__ ggamma,
                                                        float* __restrict__ gbeta) {
-    const int c = blockIdx.x * kBT + threadIdx.x;
-    if (c >= C) return;
-    const float* p = part + (size_t)c * nparts * 2;
-    double s = 0.0, sx = 0.0;
-    for (int k = 0; k < nparts; ++k) {
-        s += p[2 * k];
-        sx += p[2 * k + 1];
+    const int c = blockIdx.x;
+    double v[2];
+    chan_sums<2>(part + (size_t)c * nparts * 2, nparts, v);
+    if (threadIdx.x == 0) {
+        sums[2 * c] = (float)v[0];
+        sums[2 * c + 1] = (float)v[1];
+        if (gbeta) gbeta[c] = (float)v[0];
+        if (ggamma) ggamma[c] = (float)v[1];
     }
-    sums[2 * c] = (float)s;
-    sums[2 * c + 1] = (float)sx;
-    if (gbeta) gbeta[c] = (float)s;
-    if (ggamma) ggamma[c] = (float)sx;
 }
 
 __global__ __launch_bounds__(kBT) void bn_bwd_apply(const float* __restrict__ gy, const float* __restrict__ x,
-                                                    float* __restrict__ gx, int C, int hw, size_t n, float inv_n,
+                                                    float* __restrict__ gx, int C, int hw, int vec, float inv_n,
                                                     const float* __restrict__ mean, const float* __restrict__ invstd,
                                                     const float* __restrict__ gamma, const float* __restrict__ beta,
                                                     int relu, const float* __restrict__ sums) {
-    for (size_t i = (size_t)blockIdx.x * kBT + threadIdx.x; i < n; i += (size_t)gridDim.x * kBT) {
-        const int c = (int)((i / hw) % C);
-        const float mu = mean[c], is = invstd[c], ga = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
-        const float xh = (x[i] - mu) * is;
-        const float gg = (relu && !(fmaf(xh, ga, bt) > 0.f)) ? 0.f : gy[i];
-        gx[i] = ga * is * (gg - sums[2 * c] * inv_n - xh * (sums[2 * c + 1] * inv_n));
+    const int j = blockIdx.x, c = blockIdx.y, b = blockIdx.z;
+    const size_t off = ((size_t)b * C + c) * hw;
+    const float mu = mean[c], is = invstd[c], ga = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+    const float s0 = sums[2 * c] * inv_n, s1 = sums[2 * c + 1] * inv_n, f = ga * is;
+    float g[kPer], v[kPer];
+    bool ok[kPer];
+    load_chunk(gy + off, hw, j, vec != 0, g, ok);
+    load_chunk(x + off, hw, j, vec != 0, v, ok);
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const float xh = (v[k] - mu) * is;
+        const float gg = (relu && !(fmaf(xh, ga, bt) > 0.f)) ? 0.f : g[k];
+        v[k] = f * (gg - s0 - xh * s1);
     }
+    store_chunk(gx + off, hw, j, vec != 0, v);
 }
 
 // ---- ReLU backward + bias gradient of a convolution (the ConvBlock / bias-only layers):
@@ -238,11 +300,10 @@ __global__ __launch_bounds__(kBT) void relu_bias_stats(const float* __restrict__
 
 __global__ __launch_bounds__(kBT) void channel_sum_finalize(const float* __restrict__ part, int C, int nparts,
                                                             float* __restrict__ out) {
-    const int c = blockIdx.x * kBT + threadIdx.x;
-    if (c >= C) return;
-    double s = 0.0;
-    for (int k = 0; k < nparts; ++k) s += part[(size_t)c * nparts + k];
-    out[c] = (float)s;
+    const int c = blockIdx.x;
+    double v[1];
+    chan_sums<1>(part + (size_t)c * nparts, nparts, v);
+    if (threadIdx.x == 0) out[c] = (float)v[0];
 }
 
 size_t relu_bias_workspace_bytes(int B, int C, int H, int W) {
@@ -256,7 +317,7 @@ int launch_relu_bias_bwd(int B, int C, int H, int W, const float* g, const float
                     (!gm || (uintptr_t)gm % 16 == 0);
     hipLaunchKernelGGL(relu_bias_stats, dim3(ncp, C, B), dim3(kBT), 0, st, g, out, gm, C, hw, ncp, nparts, vec, ws);
     if (gbias)
-        hipLaunchKernelGGL(channel_sum_finalize, dim3((C + kBT - 1) / kBT), dim3(kBT), 0, st, ws, C, nparts, gbias);
+        hipLaunchKernelGGL(channel_sum_finalize, dim3(C), dim3(kBT), 0, st, ws, C, nparts, gbias);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         *why = hipGetErrorString(e);
@@ -273,24 +334,15 @@ size_t bn_workspace_bytes(const nconv_bn_train& p) {
     return (nparts * p.C * 3 + 2 * (size_t)p.C) * sizeof(float);
 }
 
-static unsigned elem_blocks(size_t n) {
-    size_t b = (n + kBT - 1) / kBT;
-    return (unsigned)(b > 8192 ? 8192 : (b ? b : 1));
-}
-
 int launch_bn_train_fwd(const nconv_bn_train& p, float* ws, hipStream_t st, const char** why) {
     const int hw = p.H * p.W, ncp = bn_ncp(p), nparts = p.B * ncp;
     const int vec = (hw % 4 == 0) && ((uintptr_t)p.x % 16 == 0);
     hipLaunchKernelGGL(bn_stats, dim3(ncp, p.C, p.B), dim3(kBT), 0, st, p.x, p.C, hw, ncp, nparts, vec, ws);
-    hipLaunchKernelGGL(bn_finalize, dim3((p.C + kBT - 1) / kBT), dim3(kBT), 0, st, ws, p.C, nparts, p.momentum, p.eps,
+    hipLaunchKernelGGL(bn_finalize, dim3(p.C), dim3(kBT), 0, st, ws, p.C, nparts, p.momentum, p.eps,
                        p.running_mean, p.running_var, p.mean, p.invstd);
-    const size_t n = (size_t)p.B * p.C * hw;
-    if (vec && ((uintptr_t)p.y % 16 == 0))
-        hipLaunchKernelGGL(bn_apply, dim3(elem_blocks(n / 4)), dim3(kBT), 0, st, p.x, p.y, p.C, hw, n / 4, p.mean,
-                           p.invstd, p.gamma, p.beta, p.relu);
-    else
-        hipLaunchKernelGGL(bn_apply_scalar, dim3(elem_blocks(n)), dim3(kBT), 0, st, p.x, p.y, p.C, hw, n, p.mean,
-                           p.invstd, p.gamma, p.beta, p.relu);
+    const int vy = vec && ((uintptr_t)p.y % 16 == 0);
+    hipLaunchKernelGGL(bn_apply, dim3(ncp, p.C, p.B), dim3(kBT), 0, st, p.x, p.y, p.C, hw, vy, p.mean, p.invstd,
+                       p.gamma, p.beta, p.relu);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         *why = hipGetErrorString(e);
@@ -306,12 +358,12 @@ int launch_bn_train_bwd(const nconv_bn_train& p, const float* gy, float* gx, flo
     float* sums = ws + (size_t)nparts * p.C * 3;
     hipLaunchKernelGGL(bn_bwd_stats, dim3(ncp, p.C, p.B), dim3(kBT), 0, st, gy, p.x, p.C, hw, ncp, nparts, vec, p.mean,
                        p.invstd, p.gamma, p.beta, p.relu, ws);
-    hipLaunchKernelGGL(bn_bwd_finalize, dim3((p.C + kBT - 1) / kBT), dim3(kBT), 0, st, ws, p.C, nparts, sums, ggamma,
+    hipLaunchKernelGGL(bn_bwd_finalize, dim3(p.C), dim3(kBT), 0, st, ws, p.C, nparts, sums, ggamma,
                        gbeta);
-    const size_t n = (size_t)p.B * p.C * hw;
     if (gx)
-        hipLaunchKernelGGL(bn_bwd_apply, dim3(elem_blocks(n)), dim3(kBT), 0, st, gy, p.x, gx, p.C, hw, n,
-                           1.f / (float)((size_t)p.B * hw), p.mean, p.invstd, p.gamma, p.beta, p.relu, sums);
+        hipLaunchKernelGGL(bn_bwd_apply, dim3(ncp, p.C, p.B), dim3(kBT), 0, st, gy, p.x, gx, p.C, hw,
+                           vec && ((uintptr_t)gx % 16 == 0), 1.f / (float)((size_t)p.B * hw), p.mean, p.invstd,
+                           p.gamma, p.beta, p.relu, sums);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         *why = hipGetErrorString(e);

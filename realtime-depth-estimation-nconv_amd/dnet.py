@@ -82,11 +82,14 @@ class DNETFn(torch.autograd.Function):
         ctx.save_for_backward(S, *p[:27], x1, c1, x2, c2, x3, c3, x4, c4, x5, c5, x6, c6, x7, c7, x8, c8, x9, c9,
                               *pools)
         ctx.mark_non_differentiable(c9)
+        ctx.set_materialize_grads(False)  # no zero-filled gradient for the never-used c9
         return x9, c9
 
     @staticmethod
     def backward(ctx, g9, gc9):
         sv = ctx.saved_tensors
+        if g9 is None:  # (grads are not materialised)
+            g9 = torch.zeros_like(sv[44])
         S, p, acts, pools = sv[0], sv[1:28], sv[28:46], sv[46:]
         W = [p[3 * i:3 * i + 3] for i in range(9)]
         X = [None] + [(acts[2 * i], acts[2 * i + 1]) for i in range(9)]  # X[k] = output of layer k
