@@ -258,8 +258,9 @@ typedef struct nconv_bwd_io {
      * reaches HBM; nconv7's weight gradient goes to tail_gw (tail_workspace of
      * nconv_bwd_tail_workspace_bytes(L) bytes; with NCONV_BWD_DEFER_REDUCE tail_nparts partial rows
      * for nconv_wgrad_reduce, layer tail). nconv7's bias gradient (the sum of tail_gy) is left to
-     * the caller. L must be nconv6's exact-fp32 geometry (16 -> 8 3x3, padding 0, upsample-first
-     * exactly-2x concat) with gw or gbias requested. */
+     * the caller (it is computed by the call that requests L's gw / gbias: a call with only the
+     * input gradients computes none of nconv7's). L must be nconv6's exact-fp32 geometry (16 -> 8
+     * 3x3, padding 0, upsample-first exactly-2x concat). */
     const nconv_layer* tail;
     const float* tail_y;
     const float* tail_cout;

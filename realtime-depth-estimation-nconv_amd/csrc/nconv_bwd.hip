@@ -1690,9 +1690,9 @@ int launch_bwd(const LayerDev& d, const BwdArgs& a, hipStream_t st, const char**
     }
     if (a.t7part) {
         if (!(path == kTiled && dgrad_phase_ok(L) && L.load_mode == NCONV_LOAD_UPCAT_UP_FIRST && L.PH == 0 &&
-              L.PW == 0 && (a.gw || a.gb))) {
+              L.PW == 0)) {
             *why = "fused tail backward needs nconv6's exact-fp32 geometry (16->8 3x3, padding 0, upsample-first "
-                   "exactly-2x concat) with its weight gradient requested";
+                   "exactly-2x concat)";
             return -95;
         }
         go_bwd_tiled<16, 8, 3, NCONV_LOAD_UPCAT_UP_FIRST, false, false, true>(d, a, part, tx, tc, st);

@@ -293,7 +293,7 @@ int nconv_bwd_ex(const nconv_layer* L, nconv_bwd_io* io, void* workspace, size_t
         if (!io->tail_y || !io->tail_cout || !io->tail_gy) return fail(-22, "nconv_bwd", "null tail planes");
         if (!io->tail_workspace || io->tail_workspace_bytes < nconv::bwd_tail_workspace_bytes(*L))
             return fail(-22, "nconv_bwd", "tail workspace too small (nconv_bwd_tail_workspace_bytes)");
-        if (!defer && !io->tail_gw) return fail(-22, "nconv_bwd", "tail output is NULL");
+        if (!defer && !io->tail_gw && (io->gw || io->gbias)) return fail(-22, "nconv_bwd", "tail output is NULL");
         a.t7w = T->weight;
         a.t7b = T->bias;
         a.t7s = T->wsum;

@@ -101,14 +101,35 @@ class DNETFn(torch.autograd.Function):
         G = [None] * 10
         sp = ctx.specs
         red = WgradReduce()  # every layer's weight-gradient reduction in two launches at the end
+        cur = torch.cuda.current_stream(S.device)
+        side = _wgrad_stream(S.device) if (ctx.pooled and WGRAD_STREAM) else None
+
+        def layer_bwd(spec, inputs, y, co, gy, gco, gin, gw_, gb_, **kw):
+            # weight gradient on the side stream, concurrent with this layer's input gradient (and
+            # the next layers' input gradients, which do not depend on it): it needs only tensors
+            # that are complete when this layer's backward starts
+            if side is None or (gw_ is None and gb_ is None):
+                layer_backward(spec, inputs, y, co, gy, gco, gin, gw_, gb_, defer=red, **kw)
+                return
+            side.wait_stream(cur)
+            tail, head = kw.pop("tail", None), kw.pop("head", None)
+            layer_backward(spec, inputs, y, co, gy, gco, gin, None, None, defer=red, head=head,
+                           tail=None if tail is None else tail[:-1] + (None,), **kw)
+            with torch.cuda.stream(side):
+                layer_backward(spec, inputs, y, co, gy, gco, (None,) * 4, gw_, gb_, defer=red, tail=tail, **kw)
 
         def bwd(k, a, b, ga, gb_, acc=False, src_a=None, spec=None, pool_grad=None):
             xa, ca = src_a if src_a is not None else (X[a] if a else (S, None))
             xb, cb = X[b] if b else (None, None)
             gy, gco = G[k] if G[k] is not None else (g9, None)
-            layer_backward(spec or sp[k - 1], (xa, ca, xb, cb, *W[k - 1]), X[k][0], X[k][1], gy, gco,
-                           (*(ga or (None, None)), *(gb_ or (None, None))), gw[k - 1], gb[k - 1], accumulate=acc,
-                           defer=red, pool_grad=pool_grad)
+            layer_bwd(spec or sp[k - 1], (xa, ca, xb, cb, *W[k - 1]), X[k][0], X[k][1], gy, gco,
+                      (*(ga or (None, None)), *(gb_ or (None, None))), gw[k - 1], gb[k - 1], accumulate=acc,
+                      pool_grad=pool_grad)
+
+        def finish():
+            if side is not None:
+                cur.wait_stream(side)
+            red.run(S.device)
 
         G[2], G[7] = (e(X[2][0]), e(X[2][1])), (e(X[7][0]), e(X[7][1]))
         exact_up = X[2][0].shape[2:] == tuple(2 * v for v in X[7][0].shape[2:])  # nconv6's phase form
@@ -117,9 +138,8 @@ class DNETFn(torch.autograd.Function):
             # HBM; its bias gradient is the sum of its output gradient (every output pixel, padding ring
             # included, as autograd's conv bias gradient)
             g9c = g9.contiguous()
-            layer_backward(sp[7], (X[2][0], X[2][1], X[7][0], X[7][1], *W[7]), X[8][0], X[8][1], None, None,
-                           (*G[2], *G[7]), gw[7], gb[7], defer=red,
-                           tail=(sp[8], *W[8], X[9][0], X[9][1], g9c, gw[8]))
+            layer_bwd(sp[7], (X[2][0], X[2][1], X[7][0], X[7][1], *W[7]), X[8][0], X[8][1], None, None,
+                      (*G[2], *G[7]), gw[7], gb[7], tail=(sp[8], *W[8], X[9][0], X[9][1], g9c, gw[8]))
             if gb[8] is not None:
                 torch.sum(g9c, dim=(0, 2, 3), out=gb[8])
         else:
@@ -140,10 +160,10 @@ class DNETFn(torch.autograd.Function):
             gp2 = (e(p2x), e(p2c))
             bwd(3, 0, 0, gp2, None, src_a=(p2x, p2c), spec=plain[0], pool_grad=(*gp3, a3))  # down1
             if FUSE_HEAD_BWD and not need[1]:  # nconv2's input gradient feeds nconv1's weight gradient in-tile
-                layer_backward(sp[1], (X[1][0], X[1][1], None, None, *W[1]), X[2][0], X[2][1], *G[2],
-                               (None, None, None, None), gw[1], gb[1], defer=red, pool_grad=(*gp2, a2),
-                               head=(sp[0], S, *W[0], gw[0], gb[0]))
-                red.run(S.device)
+                layer_bwd(sp[1], (X[1][0], X[1][1], None, None, *W[1]), X[2][0], X[2][1], *G[2],
+                          (None, None, None, None), gw[1], gb[1], pool_grad=(*gp2, a2),
+                          head=(sp[0], S, *W[0], gw[0], gb[0]))
+                finish()
                 out = [None, None, None]
                 for i in range(9):
                     out += [gw[i], gb[i], None]
@@ -157,9 +177,9 @@ class DNETFn(torch.autograd.Function):
             G[1] = (e(X[1][0]), e(X[1][1]))
             bwd(2, 1, 0, G[1], None)                        # nconv2
         gS = e(S) if need[1] else None
-        layer_backward(sp[0], (S, None, None, None, *W[0]), X[1][0], X[1][1], G[1][0], G[1][1],
-                       (gS, None, None, None), gw[0], gb[0], defer=red)  # nconv1 (threshold: c0 has no gradient)
-        red.run(S.device)
+        layer_bwd(sp[0], (S, None, None, None, *W[0]), X[1][0], X[1][1], G[1][0], G[1][1],
+                  (gS, None, None, None), gw[0], gb[0])  # nconv1 (threshold: c0 has no gradient)
+        finish()
         out = [None, None, gS]
         for i in range(9):
             out += [gw[i], gb[i], None]
@@ -167,9 +187,18 @@ class DNETFn(torch.autograd.Function):
 
 
 # Exact-fp32 training backward (DNETFn, pooled graph): nconv7's backward inside nconv6's and nconv1's
-# weight gradient inside nconv2's input gradient (nconv_bwd_ex tail / head). Switches for tests.
+# weight gradient inside nconv2's input gradient (nconv_bwd_ex tail / head); the weight gradients on
+# a second stream, concurrent with the input-gradient chain. Switches for tests.
 FUSE_TAIL_BWD = True
 FUSE_HEAD_BWD = True
+WGRAD_STREAM = True
+_WGRAD_STREAMS = {}
+
+
+def _wgrad_stream(device):
+    if device.index not in _WGRAD_STREAMS:
+        _WGRAD_STREAMS[device.index] = torch.cuda.Stream(device=device)
+    return _WGRAD_STREAMS[device.index]
 
 
 def _materialise_pool(S):
