@@ -73,7 +73,7 @@ struct DcCfg {
 
 typedef float f16v __attribute__((ext_vector_type(16)));
 
-template <int COUT, int KIND, int S, bool SC>
+template <int COUT, int KIND, int S, bool SC, bool STR = false>
 __global__ __launch_bounds__(kDT) void dense_conv_mfma(nconv_dense_conv p, int ntx, int nty, int ncot) {
     using C = DcCfg<COUT, KIND, S>;
     __shared__ __attribute__((aligned(16))) float lds[C::LDS];
@@ -112,26 +112,38 @@ __global__ __launch_bounds__(kDT) void dense_conv_mfma(nconv_dense_conv p, int n
         poff[k] = in ? (unsigned)(ci * HW + iy * p.W + ix) * 4u : OOB;
     }
     const int bytes0 = p.C0 * HW * 4, bytes1 = p.C1 * HW * 4;
-    float pv[C::NP];
+    float pv[C::NP], pv1[STR ? C::NP : 1];
+    unsigned pshift = 0;
     f4 wv[C::NW4], sv[C::NS4];
+    // Branch-free (a branch here made the compiler wait for the chunk's loads at the join, right
+    // after issuing them, instead of behind the chunk's MFMAs): with STR == false (the host found
+    // no chunk straddling the two sources) one load per element from a per-chunk resource chosen
+    // by uniform selects; with STR, two loads per element, the wrong source's out of range.
     auto load_chunk = [&](int ch) {
         const int g0 = ch * kCK;  // first channel of the chunk
-        if (g0 + kCK <= p.C0 || g0 >= p.C0) {  // one source (uniform)
+        if constexpr (!STR) {
             const bool a = g0 < p.C0;
-            const __amdgpu_buffer_rsrc_t rs =
-                a ? plane_rsrc(p.x0 + ((size_t)b * p.C0 + g0) * HW, bytes0 - g0 * HW * 4)
-                  : plane_rsrc(p.x1 + ((size_t)b * p.C1 + (g0 - p.C0)) * HW, bytes1 - (g0 - p.C0) * HW * 4);
+            const float* base = a ? p.x0 + ((size_t)b * p.C0 + g0) * HW
+                                  : p.x1 + ((size_t)b * p.C1 + (g0 - p.C0)) * HW;
+            const int nbytes = a ? bytes0 - g0 * HW * 4 : bytes1 - (g0 - p.C0) * HW * 4;
+            const __amdgpu_buffer_rsrc_t rs = plane_rsrc(base, nbytes);
 #pragma unroll
             for (int k = 0; k < C::NP; ++k) pv[k] = ld_f32(rs, poff[k]);
-        } else {  // the chunk straddles the two sources: both loads, the wrong one out of range
-            const __amdgpu_buffer_rsrc_t r0 = plane_rsrc(p.x0 + ((size_t)b * p.C0 + g0) * HW, bytes0 - g0 * HW * 4);
-            const __amdgpu_buffer_rsrc_t r1 = plane_rsrc(p.x1 + (size_t)b * p.C1 * HW, bytes1);
-            const unsigned shift = (unsigned)(p.C0 - g0) * HW * 4u;  // x1's channel 0 in chunk offsets
+        } else {  // a chunk may straddle the two sources: both loads, the wrong one out of range
+            // x0's part: channels g0 .. C0-1 (none once g0 >= C0); x1's channel 0 sits at chunk
+            // offset `shift` (negative once g0 > C0: the resource then starts at x1's channel g0 - C0)
+            const bool a0 = g0 < p.C0;
+            const __amdgpu_buffer_rsrc_t r0 = plane_rsrc(p.x0 + ((size_t)b * p.C0 + (a0 ? g0 : 0)) * HW,
+                                                         a0 ? bytes0 - g0 * HW * 4 : 0);
+            const int c1 = a0 ? 0 : g0 - p.C0;
+            const __amdgpu_buffer_rsrc_t r1 = plane_rsrc(p.x1 + ((size_t)b * p.C1 + c1) * HW, bytes1 - c1 * HW * 4);
+            const unsigned shift = a0 ? (unsigned)(p.C0 - g0) * HW * 4u : 0u;
+            pshift = shift;  // the two values are selected at store time, not here (no wait)
 #pragma unroll
             for (int k = 0; k < C::NP; ++k) {
                 const bool in1 = poff[k] != OOB && poff[k] >= shift;
-                const float v0 = ld_f32(r0, poff[k]), v1 = ld_f32(r1, in1 ? poff[k] - shift : OOB);
-                pv[k] = in1 ? v1 : v0;
+                pv[k] = ld_f32(r0, poff[k]);
+                pv1[k] = ld_f32(r1, in1 ? poff[k] - shift : OOB);
             }
         }
         const f4* wg = reinterpret_cast<const f4*>(
@@ -154,7 +166,9 @@ __global__ __launch_bounds__(kDT) void dense_conv_mfma(nconv_dense_conv p, int n
 #pragma unroll
         for (int k = 0; k < C::NP; ++k) {
             const int e = tid + kDT * k;
-            if (e < kCK * C::PR * C::PC) lds[e] = pv[k];
+            float v = pv[k];
+            if constexpr (STR) v = (poff[k] != OOB && poff[k] >= pshift) ? pv1[k] : v;
+            if (e < kCK * C::PR * C::PC) lds[e] = v;
         }
 #pragma unroll
         for (int k = 0; k < C::NW4; ++k) {
@@ -642,7 +656,12 @@ static void go_dense(const nconv_dense_conv& p, hipStream_t st) {
     const int ntx = (Wc + C::TW - 1) / C::TW, nty = (Hc + C::TH - 1) / C::TH;
     const int ncot = (p.Cout + COUT - 1) / COUT;
     const int blocks = ntx * nty * ncot * p.B * (C::TR ? 4 : 1);
-    hipLaunchKernelGGL((dense_conv_mfma<COUT, KIND, S, SC>), dim3(blocks), dim3(kDT), 0, st, p, ntx, nty, ncot);
+    if (p.C1 > 0 && p.C0 % kCK != 0)  // a chunk holds channels of both sources
+        hipLaunchKernelGGL((dense_conv_mfma<COUT, KIND, S, SC, true>), dim3(blocks), dim3(kDT), 0, st, p, ntx, nty,
+                           ncot);
+    else
+        hipLaunchKernelGGL((dense_conv_mfma<COUT, KIND, S, SC, false>), dim3(blocks), dim3(kDT), 0, st, p, ntx,
+                           nty, ncot);
 }
 
 int launch_dense_conv(const nconv_dense_conv& p, hipStream_t st, const char** why) {
