@@ -290,7 +290,8 @@ class WgradReduce:
         self.jobs = []
 
     def add(self, L, ws, nparts, gw, gb):
-        self.jobs.append((L, ws, nparts, gw, gb))
+        if nparts > 0 and (gw is not None or gb is not None):  # (input-gradient-only calls add none)
+            self.jobs.append((L, ws, nparts, gw, gb))
 
     def run(self, device):
         for k in range(0, len(self.jobs), 16):
