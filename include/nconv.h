@@ -147,7 +147,7 @@ int nconv_fwd(const nconv_layer* L, float* y, float* cout, void* stream);
 int nconv_fwd_pooled(const nconv_layer* L, float* y, float* cout, float* y_pool, float* cout_pool,
                      unsigned int* argmax, void* stream);
 
-/* Inference-only fused head: nconv1 on the thresholded sparse depth (models/step1.py:53-57;
+/* Fused head: nconv1 on the thresholded sparse depth (models/step1.py:53-57;
  * L1: Cin 1, Cout 8, 5x5, padding 2, NCONV_LOAD_THRESH) is evaluated while staging nconv2's input
  * tile (step1.py:58; L2: 8 -> 8, 5x5, padding 2, stride 1; its sources are not read), so nconv1's
  * 8-channel output never reaches HBM. Writes nconv2's y, cout (B, 8, H, W) and their 2x2 max-pooled
@@ -156,9 +156,12 @@ int nconv_fwd_pooled(const nconv_layer* L, float* y, float* cout, float* y_pool,
  *    window (bitwise its dense sums); nconv2's confidence mass D2 is the 9x9 convolution of the
  *    binary mask c0 with the composed weights sum_i W2[o,i] (x) W1[i] / s1[i] that L2->waux must
  *    hold (nconv_head_weights), except in tiles whose window nconv2's zero padding truncates;
- *  - NCONV_MATH_BF16X3 / BF16X9: the matrix-core head (nconv1 uses the same split). */
+ *  - NCONV_MATH_BF16X3 / BF16X9: the matrix-core head (nconv1 uses the same split).
+ * Training (exact fp32 only; all three or NULL): y1, cout1 (B, 8, H, W) receive nconv1's outputs
+ * (bitwise nconv_fwd's: the nonzero-tap sums are the dense sums) for the backward, argmax the
+ * pooling codes as nconv_fwd_pooled's. */
 int nconv_fwd_head(const nconv_layer* L1, const nconv_layer* L2, float* y, float* cout, float* y_pool,
-                   float* cout_pool, void* stream);
+                   float* cout_pool, unsigned int* argmax, float* y1, float* cout1, void* stream);
 
 /* Auxiliary weights of the exact fused head (L2->waux of nconv_fwd_head): w21 receives 2248 floats,
  * the composed confidence weights w21[(qh * 8 + o) * 9 + qw] = sum_i (1 / s1[i]) sum

@@ -130,7 +130,7 @@ def _declare(lib):
     lib.nconv_fwd_pooled.restype = ctypes.c_int
     lib.nconv_fwd_pooled.argtypes = [ctypes.POINTER(NconvLayer), P, P, P, P, P, P]
     lib.nconv_fwd_head.restype = ctypes.c_int
-    lib.nconv_fwd_head.argtypes = [ctypes.POINTER(NconvLayer), ctypes.POINTER(NconvLayer), P, P, P, P, P]
+    lib.nconv_fwd_head.argtypes = [ctypes.POINTER(NconvLayer), ctypes.POINTER(NconvLayer), P, P, P, P, P, P, P, P]
     lib.nconv_head_weights.restype = ctypes.c_int
     lib.nconv_head_weights.argtypes = [ctypes.POINTER(NconvLayer), ctypes.POINTER(NconvLayer), P, P]
     lib.nconv_fwd_tail.restype = ctypes.c_int

@@ -139,7 +139,7 @@ int nconv_fwd_pooled(const nconv_layer* L, float* y, float* cout, float* y_pool,
 }
 
 int nconv_fwd_head(const nconv_layer* L1, const nconv_layer* L2, float* y, float* cout, float* y_pool,
-                   float* cout_pool, void* stream) {
+                   float* cout_pool, unsigned int* argmax, float* y1, float* cout1, void* stream) {
     const char* fn = "nconv_fwd_head";
     if (const char* why = validate(L1, false)) return fail(-22, fn, why);
     if (!L2) return fail(-22, fn, "null nconv2 descriptor");
@@ -156,6 +156,8 @@ int nconv_fwd_head(const nconv_layer* L1, const nconv_layer* L2, float* y, float
     if (!L2->weight || !L2->bias || !L2->wsum) return fail(-22, fn, "null nconv2 weight/bias/wsum");
     const bool exact = L2->math == NCONV_MATH_FP32;
     if (exact && !L2->waux) return fail(-22, fn, "exact-fp32 head needs nconv2's waux = nconv_head_weights output");
+    if ((argmax || y1 || cout1) && !(exact && argmax && y1 && cout1))
+        return fail(-95, fn, "the training outputs (argmax, y1, cout1: all three) need the exact-fp32 head");
     nconv_layer l2 = *L2;
     l2.load_mode = NCONV_LOAD_PLAIN;
     l2.a = L1->a;  // (the kernel reads the sparse depth through TailArgs)
@@ -168,6 +170,9 @@ int nconv_fwd_head(const nconv_layer* L1, const nconv_layer* L2, float* y, float
     t.s1 = L1->wsum;
     t.eps1 = L1->eps;
     t.thresh1 = L1->thresh;
+    t.parg = argmax;
+    t.y1 = y1;
+    t.c1 = cout1;
     const char* why = nullptr;
     int rc = exact ? nconv::launch_fwd_head_exact(make_dev(&l2), t, y, cout, (hipStream_t)stream, &why)
                    : nconv::launch_fwd_head(make_dev(&l2), t, y, cout, (hipStream_t)stream, &why);

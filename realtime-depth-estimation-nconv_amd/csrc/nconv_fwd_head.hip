@@ -37,6 +37,9 @@ constexpr int kW21 = 9 * 8 * 9;                   // composed weights, then W2 a
 
 typedef const float __attribute__((address_space(4))) cfloat;
 
+// TR (training): nconv1's outputs of the tile's own 16 x 32 pixels also go to HBM (the backward
+// reads them) and the pooled copies come with their argmax words (nconv_fwd_pooled's codes).
+template <bool TR>
 __global__ __launch_bounds__(kHT) void fwd_head_exact(LayerDev d2, TailArgs t, float* __restrict__ y,
                                                       float* __restrict__ yc) {
     const nconv_layer& L = d2.L;  // nconv2 (8 -> 8, 5x5, padding 2); nconv1 through t
@@ -165,12 +168,20 @@ __global__ __launch_bounds__(kHT) void fwd_head_exact(LayerDev d2, TailArgs t, f
             const int dump = 8 * kHPlane * 2;
             const int h0 = (valid && c < kHP) ? (r * kHP + c) * 2 : dump;
             const int h1 = (valid && c >= 16) ? (r * kHP + c - 16) * 2 + 1 : dump;
+            // TR: the tile's own pixels (halo rows / columns 2 .. 17 / 2 .. 33) to nconv1's outputs
+            const unsigned own = (TR && !want_c && in && (unsigned)(r - 2) < (unsigned)kHTH &&
+                                  (unsigned)(c - 2) < (unsigned)kHTW) ? (unsigned)(gr * W + gc) * 4u : 0x80000000u;
 #pragma unroll
             for (int o = 0; o < 8; ++o) {
                 float y1, cc1;
                 nconv_epilogue(acc[o].x, acc[o].y, t.eps1, t.b1[o], t.s1[o], y1, cc1);
                 y1 = in ? y1 : 0.f;  // nconv2's zero padding outside the image
                 cc1 = in ? cc1 : 0.f;
+                if constexpr (TR) {
+                    const size_t po1 = ((size_t)b * 8 + o) * H * W;
+                    st_f32(plane_rsrc(t.y1 + po1, H * W * 4), own, y1);
+                    st_f32(plane_rsrc(t.c1 + po1, H * W * 4), own, cc1);
+                }
                 const float v = want_c ? cc1 : y1 * cc1;  // nconv2's staged x * c, or c
                 float* pl = reinterpret_cast<float*>(hp + o * kHPlane);
                 pl[h0 - (h0 == dump ? o * kHPlane * 2 : 0)] = v;
@@ -256,8 +267,12 @@ __global__ __launch_bounds__(kHT) void fwd_head_exact(LayerDev d2, TailArgs t, f
             // window (r, c) (r, c+1) (r+1, c) (r+1, c+1): lanes l, l^1, l^16, l^17 (torch order)
             const float yb = shfl_xor16(yv[h]), cb = shfl_xor16(cv[h]);
             const float ya = shfl_xor1(yv[h]), yd = shfl_xor1(yb), ca = shfl_xor1(cv[h]), cd = shfl_xor1(cb);
-            st_f32(rpy, po[h], pool4v(yv[h], ya, yb, yd));
-            st_f32(rpc, po[h], pool4v(cv[h], ca, cb, cd));
+            int ay, ac;
+            st_f32(rpy, po[h], pool4(yv[h], ya, yb, yd, ay));
+            st_f32(rpc, po[h], pool4(cv[h], ca, cb, cd, ac));
+            if constexpr (TR)
+                st_f32(plane_rsrc((const float*)(t.parg + pofs), ppbytes), po[h],
+                       __builtin_bit_cast(float, (unsigned)(ay | (ac << 2))));
         }
     }
 }
@@ -299,7 +314,8 @@ int launch_fwd_head_exact(const LayerDev& d2, const TailArgs& t, float* y, float
                           const char** why) {
     const nconv_layer& L = d2.L;
     dim3 grid(((L.Wo + kHTW - 1) / kHTW) * ((L.Ho + kHTH - 1) / kHTH) * L.B);  // see xcd_tile
-    hipLaunchKernelGGL(fwd_head_exact, grid, dim3(kHT), 0, st, d2, t, y, yc);
+    if (t.y1) hipLaunchKernelGGL(fwd_head_exact<true>, grid, dim3(kHT), 0, st, d2, t, y, yc);
+    else hipLaunchKernelGGL(fwd_head_exact<false>, grid, dim3(kHT), 0, st, d2, t, y, yc);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         *why = hipGetErrorString(e);

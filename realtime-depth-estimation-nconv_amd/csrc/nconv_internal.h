@@ -22,6 +22,8 @@ struct TailArgs {
     const float* b1;
     const float* s1;
     float eps1, thresh1;
+    float* y1;  // optional (training): nconv1's outputs (B, 8, H, W) written by the fused head
+    float* c1;
 };
 
 struct BwdArgs {

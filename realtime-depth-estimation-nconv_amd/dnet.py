@@ -55,15 +55,20 @@ class DNETFn(torch.autograd.Function):
         w4, w5, w6 = (None, None, None) if wph is None else tuple(wph)
         sp = specs
         pooled = _materialise_pool(S)
-        x1, c1 = layer_forward_raw(sp[0], S, None, None, None, *W[0])
         if pooled:
             spp = [dataclasses.replace(sp[k], mode=_lib.PLAIN) for k in (2, 3, 4)]
-            x2, c2, p2x, p2c, a2 = layer_forward_pooled(sp[1], x1, c1, None, None, *W[1], argmax=True)
+            if FUSE_HEAD_FWD:  # nconv1 inside nconv2's tile, nconv1's outputs written for the backward
+                w21 = head_weights(sp[0], sp[1], S, *W[0], *W[1])
+                x2, c2, p2x, p2c, a2, x1, c1 = layer_forward_head(sp[0], sp[1], S, *W[0], *W[1], w21, train=True)
+            else:
+                x1, c1 = layer_forward_raw(sp[0], S, None, None, None, *W[0])
+                x2, c2, p2x, p2c, a2 = layer_forward_pooled(sp[1], x1, c1, None, None, *W[1], argmax=True)
             x3, c3, p3x, p3c, a3 = layer_forward_pooled(spp[0], p2x, p2c, None, None, *W[2], argmax=True)
             x4, c4, p4x, p4c, a4 = layer_forward_pooled(spp[1], p3x, p3c, None, None, *W[3], argmax=True)
             x5, c5 = layer_forward_raw(spp[2], p4x, p4c, None, None, *W[4])
             pools = (p2x, p2c, a2, p3x, p3c, a3, p4x, p4c, a4)
         else:
+            x1, c1 = layer_forward_raw(sp[0], S, None, None, None, *W[0])
             x2, c2 = layer_forward_raw(sp[1], x1, c1, None, None, *W[1])
             x3, c3 = layer_forward_raw(sp[2], x2, c2, None, None, *W[2])
             x4, c4 = layer_forward_raw(sp[3], x3, c3, None, None, *W[3])
@@ -186,11 +191,13 @@ class DNETFn(torch.autograd.Function):
         return tuple(out + [None] * ctx.n_extra)
 
 
-# Exact-fp32 training backward (DNETFn, pooled graph): nconv7's backward inside nconv6's and nconv1's
-# weight gradient inside nconv2's input gradient (nconv_bwd_ex tail / head); the weight gradients on
-# a second stream, concurrent with the input-gradient chain. Switches for tests.
+# Exact-fp32 training (DNETFn, pooled graph): the forward's head fused; nconv7's backward inside
+# nconv6's and nconv1's weight gradient inside nconv2's input gradient (nconv_bwd_ex tail / head);
+# the weight gradients on a second stream, concurrent with the input-gradient chain. Switches for
+# tests.
 FUSE_TAIL_BWD = True
 FUSE_HEAD_BWD = True
+FUSE_HEAD_FWD = True  # the training forward's nconv1 + nconv2 as the exact fused head (nconv_fwd_head)
 WGRAD_STREAM = True
 _WGRAD_STREAMS = {}
 

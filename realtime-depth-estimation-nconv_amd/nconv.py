@@ -180,10 +180,12 @@ def head_weights(spec1: LayerSpec, spec2: LayerSpec, S, w1, b1, s1, w2, b2, s2, 
     return out
 
 
-def layer_forward_head(spec1: LayerSpec, spec2: LayerSpec, S, w1, b1, s1, w2, b2, s2, w21=None):
+def layer_forward_head(spec1: LayerSpec, spec2: LayerSpec, S, w1, b1, s1, w2, b2, s2, w21=None, train=False):
     """nconv_fwd_head: nconv2(nconv1(S)) with nconv1 evaluated inside nconv2's staging (its output
     never reaches HBM); returns nconv2's (y, cout, maxpool2x2(y), maxpool2x2(cout)). No autograd.
-    With FORWARD_MATH == exact fp32 the composed weights `w21` (head_weights) are required."""
+    With FORWARD_MATH == exact fp32 the composed weights `w21` (head_weights) are required.
+    train=True (exact fp32): also the pooling argmax codes and nconv1's (y, cout), which the
+    training backward reads -- returns (y, cout, py, pc, argmax, y1, cout1)."""
     L1 = spec1.descriptor(S, None, None, None, w1, b1, s1)
     L2 = spec2.descriptor(S, S, None, None, w2, b2, s2, w21)  # geometry only: the kernel reads S via L1
     B, H, W = S.shape[0], L1.Ho, L1.Wo
@@ -191,10 +193,14 @@ def layer_forward_head(spec1: LayerSpec, spec2: LayerSpec, S, w1, b1, s1, w2, b2
     co = torch.empty_like(y)
     py = torch.empty((B, 8, H // 2, W // 2), device=S.device, dtype=torch.float32)
     pc = torch.empty_like(py)
+    arg = torch.empty(py.shape, device=S.device, dtype=torch.int32) if train else None
+    y1 = torch.empty_like(y) if train else None
+    c1 = torch.empty_like(y) if train else None
     rc = _lib.lib().nconv_fwd_head(_lib.ctypes.byref(L1), _lib.ctypes.byref(L2), _lib.ptr(y), _lib.ptr(co),
-                                   _lib.ptr(py), _lib.ptr(pc), _lib.stream_handle(S.device))
+                                   _lib.ptr(py), _lib.ptr(pc), _lib.ptr(arg), _lib.ptr(y1), _lib.ptr(c1),
+                                   _lib.stream_handle(S.device))
     _lib.check(rc, "nconv_fwd_head")
-    return y, co, py, pc
+    return (y, co, py, pc, arg, y1, c1) if train else (y, co, py, pc)
 
 
 class NConvLayerFn(torch.autograd.Function):

@@ -262,6 +262,18 @@ def test_fwd_head_exact_matches_unfused(nconv_amd, gpu, shape):
     assert torch.equal(py1.nan_to_num(7.0), torch.nn.functional.max_pool2d(y1, 2, 2).nan_to_num(7.0))
     assert torch.equal(pc1, torch.nn.functional.max_pool2d(c1f, 2, 2))
 
+    # training variant: the same nconv2 outputs, nconv1's outputs bitwise the separate nconv1's, and
+    # the argmax words are the first-maximum slots of the head's own outputs (torch's indices)
+    y2, c2, py2, pc2, arg, x1h, c1h = N.layer_forward_head(sp1, sp2, Sg, w1, b1, s1, w2, b2, s2, w21, train=True)
+    torch.cuda.synchronize()
+    for a, r in ((y2, y1), (c2, c1f), (py2, py1), (pc2, pc1), (x1h, x1), (c1h, c1)):
+        assert torch.equal(a.nan_to_num(7.0), r.nan_to_num(7.0)) and torch.equal(torch.isnan(a), torch.isnan(r))
+    Hp, Wp = H // 2, W // 2
+    for plane, bits in ((y2, 0), (c2, 2)):
+        _, idx = torch.nn.functional.max_pool2d(plane, 2, 2, return_indices=True)
+        slot = ((idx // W) % 2) * 2 + (idx % W) % 2
+        assert torch.equal((arg >> bits) & 3, slot.to(torch.int32)), bits
+
 
 @pytest.mark.parametrize("shape", [(2, 48, 128), (1, 37, 70), (1, 352, 1216)])
 def test_fwd_head_matches_unfused(nconv_amd, gpu, shape, monkeypatch):
