@@ -171,15 +171,18 @@ int nconv_fwd_head(const nconv_layer* L1, const nconv_layer* L2, float* y, float
  * window is not truncated by its zero padding. Call after nconv_weight_prep. */
 int nconv_head_weights(const nconv_layer* L1, const nconv_layer* L2, float* w21, void* stream);
 
-/* Inference-only fused tail: the last 3x3 NConv (nconv6, step1.py:88-90) with its 1x1 successor
- * (nconv7, step1.py:92) evaluated in the epilogue, written straight into the cropped output
+/* Fused tail: the last 3x3 NConv (nconv6, step1.py:88-90) with its 1x1 successor (nconv7,
+ * step1.py:92) evaluated in the epilogue, written straight into the (cropped) output
  * (step1.py:94). L6 describes nconv6 (stride 1, no dilation, groups 1). Output pixel (r, c) of
- * `out` (B, 1, out_h, out_w) is nconv7's output at (r + 1, c + 1) of its (Ho6+2*p7) x (Wo6+2*p7)
- * grid, i.e. nconv6 pixel (r + 1 - p7, c + 1 - p7); positions in nconv7's zero border get b7.
- * out_c (nullable) receives the matching output confidence. */
+ * `out` (B, 1, out_h, out_w) is nconv7's output at (r + crop0, c + crop0) of its (Ho6+2*p7) x
+ * (Wo6+2*p7) grid, i.e. nconv6 pixel (r + crop0 - p7, c + crop0 - p7); positions in nconv7's zero
+ * border get b7. crop0 = 1 is DNET's crop; crop0 = 0 with the full grid is nconv7's whole output.
+ * out_c (nullable) receives the matching output confidence. Training (exact fp32, exactly-2x
+ * phase form only; both or NULL): y6, cout6 (B, Cout6, Ho6, Wo6) receive nconv6's outputs, which
+ * the backward reads. */
 int nconv_fwd_tail(const nconv_layer* L6, const float* w7, const float* b7, const float* wsum7,
-                   int cin7, int p7, float eps7, float* out, float* out_c, int out_h, int out_w,
-                   void* stream);
+                   int cin7, int p7, float eps7, float* out, float* out_c, int out_h, int out_w, int crop0,
+                   float* y6, float* cout6, void* stream);
 
 /* Which kernels nconv_fwd (without fused pooling) and nconv_bwd run for L (enum nconv_kernel):
  * the arithmetic a descriptor selects, made observable to hosts and tests. Host-only (no device

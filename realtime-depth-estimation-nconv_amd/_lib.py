@@ -135,7 +135,7 @@ def _declare(lib):
     lib.nconv_head_weights.argtypes = [ctypes.POINTER(NconvLayer), ctypes.POINTER(NconvLayer), P, P]
     lib.nconv_fwd_tail.restype = ctypes.c_int
     lib.nconv_fwd_tail.argtypes = [ctypes.POINTER(NconvLayer), P, P, P, ctypes.c_int, ctypes.c_int,
-                                   ctypes.c_float, P, P, ctypes.c_int, ctypes.c_int, P]
+                                   ctypes.c_float, P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P, P]
     lib.nconv_plan.restype = ctypes.c_int
     lib.nconv_plan.argtypes = [ctypes.POINTER(NconvLayer), P, P, P]
     lib.nconv_phase_weights_floats.restype = ctypes.c_size_t

@@ -192,15 +192,18 @@ int nconv_head_weights(const nconv_layer* L1, const nconv_layer* L2, float* w21,
 }
 
 int nconv_fwd_tail(const nconv_layer* L6, const float* w7, const float* b7, const float* wsum7,
-                   int cin7, int p7, float eps7, float* out, float* out_c, int out_h, int out_w,
-                   void* stream) {
+                   int cin7, int p7, float eps7, float* out, float* out_c, int out_h, int out_w, int crop0,
+                   float* y6, float* cout6, void* stream) {
     if (const char* why = validate(L6, true)) return fail(-22, "nconv_fwd_tail", why);
     if (!w7 || !b7 || !wsum7 || !out) return fail(-22, "nconv_fwd_tail", "null tail pointer");
     if (cin7 != L6->Cout) return fail(-22, "nconv_fwd_tail", "nconv7 Cin must equal nconv6 Cout");
-    if (p7 < 0 || out_h < 0 || out_w < 0) return fail(-22, "nconv_fwd_tail", "bad tail geometry");
-    if (out_h > L6->Ho + 2 * p7 - 1 || out_w > L6->Wo + 2 * p7 - 1)
+    if (p7 < 0 || out_h < 0 || out_w < 0 || crop0 < 0) return fail(-22, "nconv_fwd_tail", "bad tail geometry");
+    if (crop0 + out_h > L6->Ho + 2 * p7 || crop0 + out_w > L6->Wo + 2 * p7)
         return fail(-22, "nconv_fwd_tail", "output crop exceeds nconv7's grid");
-    nconv::TailArgs t{w7, b7, wsum7, eps7, 1 - p7, out_h, out_w, out_c};
+    if ((y6 == nullptr) != (cout6 == nullptr)) return fail(-22, "nconv_fwd_tail", "y6 and cout6: both or neither");
+    nconv::TailArgs t{w7, b7, wsum7, eps7, crop0 - p7, out_h, out_w, out_c};
+    t.y6 = y6;
+    t.c6 = cout6;
     const char* why = nullptr;
     int rc = nconv::launch_fwd_tail(make_dev(L6), t, out, (hipStream_t)stream, &why);
     return rc ? fail(rc, "nconv_fwd_tail", why) : 0;

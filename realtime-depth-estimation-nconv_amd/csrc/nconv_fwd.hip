@@ -486,6 +486,13 @@ int launch_fwd_tail(const LayerDev& d, const TailArgs& t, float* out, hipStream_
         return -95;  // EOPNOTSUPP
     }
     if (t.out_h <= 0 || t.out_w <= 0) return 0;
+    if (t.y6) {  // training outputs: the exact-fp32 phase tail only
+        if (L.math != NCONV_MATH_FP32 || !launch_fwd_phase(d, out, nullptr, t, true, st)) {
+            *why = "nconv6's outputs from the fused tail need the exact-fp32 phase form (exactly-2x upsampling, waux)";
+            return -95;
+        }
+        return last_launch(why);
+    }
     if (launch_fwd_mfma(d, out, nullptr, t, true, st)) return last_launch(why);
     if (launch_fwd_phase(d, out, nullptr, t, true, st)) return last_launch(why);
     go_tiled<16, 8, 3, NCONV_LOAD_UPCAT_UP_FIRST, true>(d, out, nullptr, t, t.out_h, t.out_w, st);

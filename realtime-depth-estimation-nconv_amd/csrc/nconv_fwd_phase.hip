@@ -225,20 +225,49 @@ __global__ __launch_bounds__(kPT) void fwd_phase(LayerDev d, float* __restrict__
         if (r >= t.out_h) return;
         const float b7 = t.b7[0], s7 = t.s7[0];
         float ov[2], oc[2];
+        // nconv6's outputs -> nconv7's sums (o ascending, as nconv7's own kernel); with t.y6
+        // (training) nconv6's outputs are stored too, two pixels per 8-byte store
+        constexpr unsigned OOB = 0x80000000u;
+        const int owb = ow0 + tx;
+        bool inj[2];
+        unsigned so[2];
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-            const int ow = ow0 + tx + j;
-            float N7 = 0.f, D7 = 0.f;
-            if ((unsigned)oh < (unsigned)L.Ho && (unsigned)ow < (unsigned)L.Wo) {
+            inj[j] = (unsigned)oh < (unsigned)L.Ho && (unsigned)(owb + j) < (unsigned)L.Wo;
+            so[j] = inj[j] ? (unsigned)(oh * L.Wo + owb + j) * 4u : OOB;
+        }
+        const bool vec = (L.Wo % 2) == 0 && inj[0] && inj[1];
+        const int pbytes = L.Ho * L.Wo * 4;
+        float N7[2] = {0.f, 0.f}, D7[2] = {0.f, 0.f};
 #pragma unroll
-                for (int o = 0; o < kPCO; ++o) {
-                    float y6, c6;
-                    nconv_epilogue(acc[o][j].x, acc[o][j].y, L.eps, L.bias[o], L.wsum[o], y6, c6);
-                    N7 = fmaf(t.w7[o], y6 * c6, N7);
-                    D7 = fmaf(t.w7[o], c6, D7);
+        for (int o = 0; o < kPCO; ++o) {
+            float y6[2], c6[2];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                nconv_epilogue(acc[o][j].x, acc[o][j].y, L.eps, L.bias[o], L.wsum[o], y6[j], c6[j]);
+                if (inj[j]) {
+                    N7[j] = fmaf(t.w7[o], y6[j] * c6[j], N7[j]);
+                    D7[j] = fmaf(t.w7[o], c6[j], D7[j]);
                 }
             }
-            nconv_epilogue(N7, D7, t.eps7, b7, s7, ov[j], oc[j]);
+            if (t.y6) {  // training: each pixel of nconv6 lies in exactly one tile
+                const size_t ofs = ((size_t)b * kPCO + o) * L.Ho * L.Wo;
+                const __amdgpu_buffer_rsrc_t ry = plane_rsrc(t.y6 + ofs, pbytes), rc = plane_rsrc(t.c6 + ofs, pbytes);
+                if (vec) {
+                    st_f2(ry, so[0], (f2){y6[0], y6[1]});
+                    st_f2(rc, so[0], (f2){c6[0], c6[1]});
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        st_f32(ry, so[j], y6[j]);
+                        st_f32(rc, so[j], c6[j]);
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            nconv_epilogue(N7[j], D7[j], t.eps7, b7, s7, ov[j], oc[j]);
         }
         const size_t base = ((size_t)b * t.out_h + r) * t.out_w + C0 + tx;
 #pragma unroll

@@ -24,6 +24,8 @@ struct TailArgs {
     float eps1, thresh1;
     float* y1;  // optional (training): nconv1's outputs (B, 8, H, W) written by the fused head
     float* c1;
+    float* y6;  // optional (training): nconv6's outputs written by the fused tail (phase kernel)
+    float* c6;
 };
 
 struct BwdArgs {

@@ -76,8 +76,11 @@ class DNETFn(torch.autograd.Function):
             pools = ()
         x6, c6 = layer_forward_raw(sp[5], x4, c4, x5, c5, *W[5], wphase=w4)
         x7, c7 = layer_forward_raw(sp[6], x3, c3, x6, c6, *W[6], wphase=w5)
-        x8, c8 = layer_forward_raw(sp[7], x2, c2, x7, c7, *W[7], wphase=w6)
-        x9, c9 = layer_forward_raw(sp[8], x8, c8, None, None, *W[8])
+        if pooled and FUSE_TAIL_FWD and w6 is not None and x2.shape[2:] == tuple(2 * v for v in x7.shape[2:]):
+            x8, c8, x9, c9 = _tail_train(sp[7], sp[8], x2, c2, x7, c7, W[7], W[8], w6)
+        else:
+            x8, c8 = layer_forward_raw(sp[7], x2, c2, x7, c7, *W[7], wphase=w6)
+            x9, c9 = layer_forward_raw(sp[8], x8, c8, None, None, *W[8])
         if capture is not None:  # the three pooling stages' inputs (DNET.capture)
             capture.update(down1=(x2.detach(), c2.detach()), down2=(x3.detach(), c3.detach()),
                            down3=(x4.detach(), c4.detach()))
@@ -198,6 +201,25 @@ class DNETFn(torch.autograd.Function):
 FUSE_TAIL_BWD = True
 FUSE_HEAD_BWD = True
 FUSE_HEAD_FWD = True  # the training forward's nconv1 + nconv2 as the exact fused head (nconv_fwd_head)
+FUSE_TAIL_FWD = True  # ... and nconv6 + nconv7 as the fused tail (nconv_fwd_tail over nconv7's whole grid)
+
+
+def _tail_train(sp6, sp7, x2, c2, x7, c7, W6, W7, w6):
+    """nconv6 + nconv7 in one phase-tail launch writing nconv6's outputs and nconv7's whole
+    (uncropped) output grid -- what the training backward reads (nconv_fwd_tail, crop0 = 0)."""
+    L = sp6.descriptor(x2, c2, x7, c7, *W6, w6)
+    (w7, b7, s7), p7 = W7, sp7.padding[0]
+    B, dev = x2.shape[0], x2.device
+    x8 = torch.empty((B, sp6.cout, L.Ho, L.Wo), device=dev, dtype=torch.float32)
+    c8 = torch.empty_like(x8)
+    H9, W9 = L.Ho + 2 * p7, L.Wo + 2 * p7
+    x9 = torch.empty((B, 1, H9, W9), device=dev, dtype=torch.float32)
+    c9 = torch.empty_like(x9)
+    rc = _lib.lib().nconv_fwd_tail(_lib.ctypes.byref(L), _lib.ptr(w7), _lib.ptr(b7), _lib.ptr(s7), sp7.cin, p7,
+                                   sp7.eps, _lib.ptr(x9), _lib.ptr(c9), H9, W9, 0, _lib.ptr(x8), _lib.ptr(c8),
+                                   _lib.stream_handle(dev))
+    _lib.check(rc, "nconv_fwd_tail")
+    return x8, c8, x9, c9
 WGRAD_STREAM = True
 _WGRAD_STREAMS = {}
 
@@ -480,7 +502,7 @@ class DNET(nn.Module):
             raise RuntimeError("fused tail needs nconv7 = 1x1, stride 1, square padding")
         rc = _lib.lib().nconv_fwd_tail(
             _lib.ctypes.byref(L), _lib.ptr(l7.weight), _lib.ptr(l7.bias), _lib.ptr(s7), l7.in_channels,
-            l7.padding[0], l7.eps, _lib.ptr(out), None, out_h, out_w, _lib.stream_handle(x1.device))
+            l7.padding[0], l7.eps, _lib.ptr(out), None, out_h, out_w, 1, None, None, _lib.stream_handle(x1.device))
         _lib.check(rc, "nconv_fwd_tail")
         return out
 

@@ -83,6 +83,7 @@ def test_whole_graph_autograd_matches_per_layer(nconv_amd, gpu, H, W, monkeypatc
     # the same forward kernels in both (the fused head's composed D2 rounds differently; it is
     # checked against the oracle in test_dnet_train_gradients and bitwise in the layer tests)
     monkeypatch.setattr(sys.modules[nconv_amd.DNET.__module__], "FUSE_HEAD_FWD", False)
+    monkeypatch.setattr(sys.modules[nconv_amd.DNET.__module__], "FUSE_TAIL_FWD", False)
     res = []
     for whole in (True, False):
         net = make_net(nconv_amd, "generalized", gpu)
@@ -117,6 +118,7 @@ def test_materialised_pool_matches_pool_on_load(nconv_amd, gpu, H, W, monkeypatc
     res = []
     monkeypatch.setattr(dnet, "FUSE_TAIL_BWD", False)
     monkeypatch.setattr(dnet, "FUSE_HEAD_FWD", False)  # (the fused head's D2 rounds differently)
+    monkeypatch.setattr(dnet, "FUSE_TAIL_FWD", False)
     for pooled in (True, False):
         monkeypatch.setattr(dnet, "_materialise_pool", lambda S_, v=pooled: v)
         net = make_net(nconv_amd, "generalized", gpu)
@@ -164,6 +166,36 @@ def test_materialised_pool_matches_pool_on_load(nconv_amd, gpu, H, W, monkeypatc
         close(x.grad, ga, "S")
         for k in pt:
             close(pt[k], pa[k], k)
+
+
+@pytest.mark.parametrize("H,W", [(64, 96), (48, 200)])
+def test_tail_train_matches_layers(nconv_amd, gpu, H, W):
+    """The training forward's fused tail (nconv_fwd_tail over nconv7's whole grid, writing nconv6's
+    outputs too) against nconv6 (phase form) and nconv7 as separate launches: bitwise, the zero
+    border included."""
+    dnet = sys.modules[nconv_amd.DNET.__module__]
+    N = nconv_amd.nconv
+    net = make_net(nconv_amd, "generalized", gpu)
+    d = net.d_net
+    g = torch.Generator().manual_seed(H + W)
+    B = 2
+    x2 = (torch.rand(B, 8, H, W, generator=g) * 5).to(gpu)
+    c2 = torch.rand(B, 8, H, W, generator=g).to(gpu)
+    x7 = (torch.rand(B, 8, H // 2, W // 2, generator=g) * 5).to(gpu)
+    c7 = torch.rand(B, 8, H // 2, W // 2, generator=g).to(gpu)
+    l6, l7 = d.nconv6, d.nconv7
+    s6 = torch.empty(8, device=gpu)
+    s7 = torch.empty(1, device=gpu)
+    N.weight_prep([l6.weight.detach(), l7.weight.detach()], [False, False], [s6, s7])
+    w6 = d._phase_weights(gpu)[2]
+    sp6, sp7 = l6.spec(nconv_amd._lib.UPCAT_UP_FIRST), l7.spec()
+    W6, W7 = (l6.weight.detach(), l6.bias.detach(), s6), (l7.weight.detach(), l7.bias.detach(), s7)
+    x8, c8, x9, c9 = dnet._tail_train(sp6, sp7, x2, c2, x7, c7, W6, W7, w6)
+    r8, rc8 = N.layer_forward_raw(sp6, x2, c2, x7, c7, *W6, wphase=w6)
+    r9, rc9 = N.layer_forward_raw(sp7, r8, rc8, None, None, *W7)
+    torch.cuda.synchronize()
+    for a, r in ((x8, r8), (c8, rc8), (x9, r9), (c9, rc9)):
+        assert a.shape == r.shape and torch.equal(a, r)
 
 
 def test_enforcepos_drift(nconv_amd, gpu):
