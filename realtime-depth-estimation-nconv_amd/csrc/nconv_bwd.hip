@@ -1177,7 +1177,7 @@ struct WmCfg {
 #endif
 #define NCONV_WM_ATTR __attribute__((amdgpu_waves_per_eu(NCONV_WM_WAVES, 8)))
 template <int CIN, int COUT, int K, int MODE, bool GP = false, bool T7 = false>
-__global__ __launch_bounds__(kT) NCONV_WM_ATTR void wgrad_mfma(LayerDev d, BwdArgs a, float* part, int nstrip, int nseg,
+__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(GP ? 4 : NCONV_WM_WAVES, 8))) void wgrad_mfma(LayerDev d, BwdArgs a, float* part, int nstrip, int nseg,
                                                  int seg_rows) {
     using C = WmCfg<CIN, COUT, K>;
     __shared__ __attribute__((aligned(16))) float lds[C::LDS];
