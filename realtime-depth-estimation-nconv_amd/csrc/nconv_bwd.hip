@@ -1175,9 +1175,12 @@ struct WmCfg {
 #ifndef NCONV_WM_WAVES
 #define NCONV_WM_WAVES 3
 #endif
+#ifndef NCONV_WM_GP_WAVES
+#define NCONV_WM_GP_WAVES 3  // the pooled-gradient (training) instantiation (4: 128 VGPRs, 2 spilled)
+#endif
 #define NCONV_WM_ATTR __attribute__((amdgpu_waves_per_eu(NCONV_WM_WAVES, 8)))
 template <int CIN, int COUT, int K, int MODE, bool GP = false, bool T7 = false>
-__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(GP ? 4 : NCONV_WM_WAVES, 8))) void wgrad_mfma(LayerDev d, BwdArgs a, float* part, int nstrip, int nseg,
+__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(GP ? NCONV_WM_GP_WAVES : NCONV_WM_WAVES, 8))) void wgrad_mfma(LayerDev d, BwdArgs a, float* part, int nstrip, int nseg,
                                                  int seg_rows) {
     using C = WmCfg<CIN, COUT, K>;
     __shared__ __attribute__((aligned(16))) float lds[C::LDS];
@@ -1215,14 +1218,24 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(GP ? 4 : NCO
     }
 
     // ---- staging: one input row (CIN x 64 columns) and one g row (COUT x (64+K-1) columns) ----
+    // The g row's 64 + K-1 columns: a main pass (column = lane) for each of the wave's OPW output
+    // channels, and one halo pass over all of them -- lane l < OPW (K-1) takes channel w + 4 (l / (K-1))
+    // at column 64 + l % (K-1) -- instead of a second pass per channel with K-1 of 64 lanes active.
+    // The g tensors are addressed through one resource per image (the channel's plane offset in
+    // soffset for the main pass, in the lane's offset for the halo).
     float px[C::CPW], pc[C::CPW];
     constexpr int NG = GP ? 7 : 4;  // gy, gco, y, cout (+ pooled gy, gcout, argmax code)
-    float gq[C::OPW][2][NG];
-    float g7[T7 ? 2 : 1][3];                                     // nconv7's gy, y, cout (T7)
+    constexpr int NH = C::OPW * (K - 1);
+    static_assert(NH <= 64, "halo lanes");
+    const bool hl = lane < NH;
+    const int hkk = hl ? lane / (K - 1) : 0, hcol = 64 + lane % (K - 1), ho = w + 4 * hkk;
+    float gq[C::OPW][NG], gh[NG];
+    float g7[T7 ? 2 : 1][3];                                     // nconv7's gy, y, cout (T7): main, halo
     float w7n[T7 ? C::OPW : 1], w7d[T7 ? C::OPW : 1];            // nconv7's weight-gradient sums
+    float w7nh = 0.f, w7dh = 0.f;
 #pragma unroll
     for (int kk = 0; kk < (T7 ? C::OPW : 1); ++kk) w7n[kk] = w7d[kk] = 0.f;
-    float gb_acc[C::OPW], gs_acc[C::OPW];
+    float gb_acc[C::OPW], gs_acc[C::OPW], gb_h = 0.f, gs_h = 0.f;
 #pragma unroll
     for (int kk = 0; kk < C::OPW; ++kk) gb_acc[kk] = gs_acc[kk] = 0.f;
 
@@ -1249,45 +1262,67 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(GP ? 4 : NCO
     const int plane = L.Ho * L.Wo;
     const int Hp = L.Ho >> 1, Wp = L.Wo >> 1, pplane = Hp * Wp;
     auto load_g = [&](int oh) {
+        const int ow = ow0 - (K - 1) + lane, owh = ow0 - (K - 1) + hcol;
+        const bool row_in = (unsigned)oh < (unsigned)L.Ho;
+        const bool in = row_in && (unsigned)ow < (unsigned)L.Wo;
+        const bool inh = hl && row_in && (unsigned)owh < (unsigned)L.Wo;
         if constexpr (T7) {
             const int pl7 = (L.Ho + 4) * (L.Wo + 4);
             const size_t base7 = (size_t)b * pl7;
-#pragma unroll
-            for (int p = 0; p < 2; ++p) {
-                const int ow = ow0 - (K - 1) + p * 64 + lane;
-                const unsigned off = (p == 0 || lane < K - 1) ? t7_off(oh, ow, L.Ho, L.Wo, OOB) : OOB;
-                g7[p][0] = ld_f32(plane_rsrc(a.t7gy + base7, pl7 * 4), off);
-                g7[p][1] = ld_f32(plane_rsrc(a.t7y + base7, pl7 * 4), off);
-                g7[p][2] = ld_f32(plane_rsrc(a.t7co + base7, pl7 * 4), off);
-            }
+            const __amdgpu_buffer_rsrc_t r7g = plane_rsrc(a.t7gy + base7, pl7 * 4);
+            const __amdgpu_buffer_rsrc_t r7y = plane_rsrc(a.t7y + base7, pl7 * 4);
+            const __amdgpu_buffer_rsrc_t r7c = plane_rsrc(a.t7co + base7, pl7 * 4);
+            const unsigned o0 = t7_off(oh, ow, L.Ho, L.Wo, OOB), o1 = hl ? t7_off(oh, owh, L.Ho, L.Wo, OOB) : OOB;
+            g7[0][0] = ld_f32(r7g, o0);
+            g7[0][1] = ld_f32(r7y, o0);
+            g7[0][2] = ld_f32(r7c, o0);
+            g7[1][0] = ld_f32(r7g, o1);
+            g7[1][1] = ld_f32(r7y, o1);
+            g7[1][2] = ld_f32(r7c, o1);
         }
+        const size_t base = (size_t)b * COUT * plane;
+        const int bytes = COUT * plane * 4;
+        const __amdgpu_buffer_rsrc_t rgy = plane_rsrc(a.gy + base, bytes);
+        const __amdgpu_buffer_rsrc_t rco = plane_rsrc(a.co + base, bytes);
+        const __amdgpu_buffer_rsrc_t ry = plane_rsrc(a.y + base, bytes);
+        const __amdgpu_buffer_rsrc_t rgc = plane_rsrc(a.gco ? a.gco + base : a.y, a.gco ? bytes : 0);
+        const unsigned off = in ? (unsigned)(oh * L.Wo + ow) * 4u : OOB;
+        const unsigned offh = inh ? (unsigned)((ho * L.Ho + oh) * L.Wo + owh) * 4u : OOB;
 #pragma unroll
         for (int kk = 0; kk < C::OPW; ++kk) {
-            const int o = w + 4 * kk;
-            const size_t base = ((size_t)b * COUT + o) * plane;
-            const __amdgpu_buffer_rsrc_t rgy = plane_rsrc(a.gy + base, plane * 4);
-            const __amdgpu_buffer_rsrc_t rco = plane_rsrc(a.co + base, plane * 4);
-            const __amdgpu_buffer_rsrc_t ry = plane_rsrc(a.y + base, plane * 4);
-#pragma unroll
-            for (int p = 0; p < 2; ++p) {
-                const int ow = ow0 - (K - 1) + p * 64 + lane;
-                const bool in = (p == 0 || lane < K - 1) && (unsigned)oh < (unsigned)L.Ho &&
-                                (unsigned)ow < (unsigned)L.Wo;
-                const unsigned off = in ? (unsigned)(oh * L.Wo + ow) * 4u : OOB;
-                gq[kk][p][1] = ld_f32(rco, off);
-                gq[kk][p][2] = ld_f32(ry, off);
-                if constexpr (!T7) {
-                    gq[kk][p][0] = ld_f32(rgy, off);
-                    gq[kk][p][3] = ld_f32(plane_rsrc(a.gco ? a.gco + base : a.y, a.gco ? plane * 4 : 0), off);
-                }
-                if constexpr (GP) {
-                    const size_t pbase = ((size_t)b * COUT + o) * pplane;
-                    const unsigned po = in ? pool_elem_off(oh, ow, Hp, Wp, OOB) : OOB;
-                    gq[kk][p][4] = ld_f32(plane_rsrc(a.gpy + pbase, pplane * 4), po);
-                    gq[kk][p][5] = ld_f32(plane_rsrc(a.gpc + pbase, pplane * 4), po);
-                    gq[kk][p][6] = ld_f32(plane_rsrc((const float*)(a.parg + pbase), pplane * 4), po);
-                }
+            const int so = (w + 4 * kk) * plane * 4;
+            gq[kk][1] = ld_f32s(rco, off, so);
+            gq[kk][2] = ld_f32s(ry, off, so);
+            if constexpr (!T7) {
+                gq[kk][0] = ld_f32s(rgy, off, so);
+                gq[kk][3] = ld_f32s(rgc, off, so);
             }
+        }
+        gh[1] = ld_f32(rco, offh);
+        gh[2] = ld_f32(ry, offh);
+        if constexpr (!T7) {
+            gh[0] = ld_f32(rgy, offh);
+            gh[3] = ld_f32(rgc, offh);
+        }
+        if constexpr (GP) {
+            const size_t pbase = (size_t)b * COUT * pplane;
+            const int pbytes = COUT * pplane * 4;
+            const __amdgpu_buffer_rsrc_t rpy = plane_rsrc(a.gpy + pbase, pbytes);
+            const __amdgpu_buffer_rsrc_t rpc = plane_rsrc(a.gpc + pbase, pbytes);
+            const __amdgpu_buffer_rsrc_t rpa = plane_rsrc((const float*)(a.parg + pbase), pbytes);
+            const unsigned po = in ? pool_elem_off(oh, ow, Hp, Wp, OOB) : OOB;
+            const unsigned pe = inh ? pool_elem_off(oh, owh, Hp, Wp, OOB) : OOB;
+            const unsigned poh = pe != OOB ? pe + (unsigned)(ho * pplane) * 4u : OOB;
+#pragma unroll
+            for (int kk = 0; kk < C::OPW; ++kk) {
+                const int so = (w + 4 * kk) * pplane * 4;
+                gq[kk][4] = ld_f32s(rpy, po, so);
+                gq[kk][5] = ld_f32s(rpc, po, so);
+                gq[kk][6] = ld_f32s(rpa, po, so);
+            }
+            gh[4] = ld_f32(rpy, poh);
+            gh[5] = ld_f32(rpc, poh);
+            gh[6] = ld_f32(rpa, poh);
         }
     };
     // the wave's output channels' bias and normaliser, read once (not per row: a load right before
@@ -1304,40 +1339,62 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(GP ? 4 : NCO
         if constexpr (T7)
 #pragma unroll
             for (int p = 0; p < 2; ++p) t7_nd(a, g7[p][0], g7[p][1], g7[p][2], n7[p], d7[p]);
+        // the 2x2 window slot of the main / halo column (pooled-gradient routing)
+        const unsigned sub = (unsigned)((oh_cur & 1) << 1), ow_m = (unsigned)(ow0 - (K - 1) + lane);
+        const unsigned ow_h = (unsigned)(ow0 - (K - 1) + hcol);
 #pragma unroll
         for (int kk = 0; kk < C::OPW; ++kk) {
             const int o = w + 4 * kk;
-            const float bo = bias_o[kk], so = wsum_o[kk];
+            float gy, gco;
+            if constexpr (T7) {
+                t7_gy(w7_o[kk], n7[0], d7[0], gq[kk][2], gq[kk][1], gy, gco);
+                if (lane >= K - 1) {  // nconv7's weight gradient: corr(x*c, gN7) + corr(c, gD7)
+                    w7n[kk] = fmaf(gq[kk][2] * gq[kk][1], n7[0], w7n[kk]);
+                    w7d[kk] = fmaf(gq[kk][1], d7[0], w7d[kk]);
+                }
+            } else {
+                gy = gq[kk][0];
+                gco = gq[kk][3];
+            }
+            if constexpr (GP)
+                pool_route(gy, gco, gq[kk][4], gq[kk][5], __builtin_bit_cast(unsigned, gq[kk][6]), sub | (ow_m & 1u));
+            float gN, gD;
+            nconv_grad_nd(gy, gco, gq[kk][2], gq[kk][1], L.eps, bias_o[kk], wsum_o[kk], gN, gD);
+            float* g = lds + C::G_OFF + buf * C::GBUF + o * C::GP + lane;
+            g[0] = gN;
+            g[C::GPART] = gD;
+            if (lane >= K - 1) {  // this strip's own columns: the bias / wsum gradient sums
+                gb_acc[kk] += gy;
+                gs_acc[kk] = fmaf(gco, gq[kk][1], gs_acc[kk]);
+            }
+        }
+        {   // halo pass (columns 64 .. 64+K-2, all the strip's own)
+            float bo = bias_o[0], so = wsum_o[0], w7 = w7_o[0];
 #pragma unroll
-            for (int p = 0; p < 2; ++p) {
-                const int col = p * 64 + lane;
-                if (p == 1 && lane >= K - 1) continue;
-                float gy, gco;
-                if constexpr (T7) {
-                    t7_gy(w7_o[kk], n7[p], d7[p], gq[kk][p][2], gq[kk][p][1], gy, gco);
-                    if (col >= K - 1) {  // nconv7's weight gradient: corr(x*c, gN7) + corr(c, gD7)
-                        w7n[kk] = fmaf(gq[kk][p][2] * gq[kk][p][1], n7[p], w7n[kk]);
-                        w7d[kk] = fmaf(gq[kk][p][1], d7[p], w7d[kk]);
-                    }
-                } else {
-                    gy = gq[kk][p][0];
-                    gco = gq[kk][p][3];
-                }
-                if constexpr (GP) {
-                    const int ow = ow0 - (K - 1) + col;
-                    pool_route(gy, gco, gq[kk][p][4], gq[kk][p][5], __builtin_bit_cast(unsigned, gq[kk][p][6]),
-                               (unsigned)(((oh_cur & 1) << 1) | (ow & 1)));
-                }
-                float gN, gD;
-                nconv_grad_nd(gy, gco, gq[kk][p][2], gq[kk][p][1], L.eps, bo, so, gN, gD);
-                float* g = lds + C::G_OFF + buf * C::GBUF + o * C::GP + col;
+            for (int kk = 1; kk < C::OPW; ++kk) {
+                bo = hkk == kk ? bias_o[kk] : bo;
+                so = hkk == kk ? wsum_o[kk] : so;
+                w7 = hkk == kk ? w7_o[kk] : w7;
+            }
+            float gy, gco;
+            if constexpr (T7) {
+                t7_gy(w7, n7[1], d7[1], gh[2], gh[1], gy, gco);
+                w7nh = fmaf(gh[2] * gh[1], n7[1], w7nh);
+                w7dh = fmaf(gh[1], d7[1], w7dh);
+            } else {
+                gy = gh[0];
+                gco = gh[3];
+            }
+            if constexpr (GP) pool_route(gy, gco, gh[4], gh[5], __builtin_bit_cast(unsigned, gh[6]), sub | (ow_h & 1u));
+            float gN, gD;
+            nconv_grad_nd(gy, gco, gh[2], gh[1], L.eps, bo, so, gN, gD);
+            if (hl) {
+                float* g = lds + C::G_OFF + buf * C::GBUF + ho * C::GP + hcol;
                 g[0] = gN;
                 g[C::GPART] = gD;
-                if (col >= K - 1) {  // this strip's own columns: the bias / wsum gradient sums
-                    gb_acc[kk] += gy;
-                    gs_acc[kk] = fmaf(gco, gq[kk][p][1], gs_acc[kk]);
-                }
             }
+            gb_h += gy;
+            gs_h = fmaf(gco, gh[1], gs_h);
         }
     };
 
@@ -1418,7 +1475,8 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(GP ? 4 : NCO
     }
 #pragma unroll
     for (int kk = 0; kk < C::OPW; ++kk) {
-        float sb = gb_acc[kk], ss = gs_acc[kk];
+        const bool mine = hl && hkk == kk;  // the halo lanes' sums of this channel
+        float sb = gb_acc[kk] + (mine ? gb_h : 0.f), ss = gs_acc[kk] + (mine ? gs_h : 0.f);
 #pragma unroll
         for (int sh = 32; sh > 0; sh >>= 1) {
             sb += __shfl_xor(sb, sh);
@@ -1433,7 +1491,8 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(GP ? 4 : NCO
         float* o7 = a.t7part + (size_t)blockIdx.x * 10;
 #pragma unroll
         for (int kk = 0; kk < C::OPW; ++kk) {
-            float sn = w7n[kk], sd = w7d[kk];
+            const bool mine = hl && hkk == kk;
+            float sn = w7n[kk] + (mine ? w7nh : 0.f), sd = w7d[kk] + (mine ? w7dh : 0.f);
 #pragma unroll
             for (int sh = 32; sh > 0; sh >>= 1) {
                 sn += __shfl_xor(sn, sh);
