@@ -82,11 +82,27 @@ __device__ __forceinline__ LossTile loss_tile(const LossPlane& p) {
     return lt;
 }
 
-// The tile's diff window (rows i0-2 .. i0+kTH+1, columns j0-2 .. j0+kTW+1) into LDS.
+// The tile's diff window (rows i0-2 .. i0+kTH+1, columns j0-2 .. j0+kTW+1) into LDS: every
+// element's t and r loaded first (buffer loads, out-of-plane offsets read 0; r also where t == 0,
+// so no load waits on another), then diff = t - masked_fill(r, t == 0, 0).
 __device__ __forceinline__ void stage_diff(const LossPlane& p, int i0, int j0, float* dw) {
-    for (int e = threadIdx.x; e < kDH * kDW; e += kLT) {
-        const int a = e / kDW, c = e - a * kDW;
-        dw[e] = loss_diff(p, i0 - 2 + a, j0 - 2 + c);
+    constexpr int NS = (kDH * kDW + kLT - 1) / kLT;
+    constexpr unsigned OOB = 0x80000000u;
+    const __amdgpu_buffer_rsrc_t rt = plane_rsrc(p.t, (int)(((long long)(p.H - 1) * p.ts + p.W) * 4));
+    const __amdgpu_buffer_rsrc_t rr = plane_rsrc(p.r, (int)(((long long)(p.H - 1) * p.rs + p.W) * 4));
+    float tv[NS], rv[NS];
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+        const int e = threadIdx.x + kLT * k;
+        const int a = e / kDW, c = e - a * kDW, i = i0 - 2 + a, j = j0 - 2 + c;
+        const bool in = e < kDH * kDW && (unsigned)i < (unsigned)p.H && (unsigned)j < (unsigned)p.W;
+        tv[k] = ld_f32(rt, in ? (unsigned)(i * p.ts + j) * 4u : OOB);
+        rv[k] = ld_f32(rr, in ? (unsigned)(i * p.rs + j) * 4u : OOB);
+    }
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+        const int e = threadIdx.x + kLT * k;
+        if (e < kDH * kDW) dw[e] = tv[k] - (tv[k] == 0.f ? 0.f : rv[k]);
     }
 }
 

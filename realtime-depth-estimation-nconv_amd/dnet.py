@@ -22,7 +22,7 @@ import os
 import torch
 import torch.nn as nn
 
-from . import _lib, export, nconv
+from . import _lib, dense, export, nconv
 from .nconv import (EnforcePos, NConv2d, WgradReduce, _require_device, head_weights, layer_backward,
                     layer_forward_head, layer_forward_pooled, layer_forward_raw, nconv_layer, phase_weights, weight_prep)
 
@@ -148,8 +148,8 @@ class DNETFn(torch.autograd.Function):
             g9c = g9.contiguous()
             layer_bwd(sp[7], (X[2][0], X[2][1], X[7][0], X[7][1], *W[7]), X[8][0], X[8][1], None, None,
                       (*G[2], *G[7]), gw[7], gb[7], tail=(sp[8], *W[8], X[9][0], X[9][1], g9c, gw[8]))
-            if gb[8] is not None:
-                torch.sum(g9c, dim=(0, 2, 3), out=gb[8])
+            if gb[8] is not None:  # (libnconv's per-channel sum)
+                dense.relu_bias_bwd(g9c, None, None, gb[8])
         else:
             G[8] = (e(X[8][0]), e(X[8][1]))
             bwd(9, 8, 0, G[8], None)                        # nconv7
