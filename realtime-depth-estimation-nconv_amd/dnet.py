@@ -220,6 +220,20 @@ def _tail_train(sp6, sp7, x2, c2, x7, c7, W6, W7, w6):
                                    _lib.stream_handle(dev))
     _lib.check(rc, "nconv_fwd_tail")
     return x8, c8, x9, c9
+class CropFn(torch.autograd.Function):
+    """xo[:, :, 1:1+h, 1:1+w] (step1.py:94), a view as there; its backward zero-pads the gradient
+    in one launch (autograd's two slice backwards zero-fill and copy twice)."""
+
+    @staticmethod
+    def forward(ctx, x, h, w):
+        ctx.pad = (1, x.shape[3] - 1 - w, 1, x.shape[2] - 1 - h)
+        return x[:, :, 1:1 + h, 1:1 + w]
+
+    @staticmethod
+    def backward(ctx, g):
+        return torch.nn.functional.pad(g, ctx.pad), None, None
+
+
 WGRAD_STREAM = True
 _WGRAD_STREAMS = {}
 
@@ -329,7 +343,7 @@ class DNET(nn.Module):
             for m_, s_ in zip(layers, wsum):
                 params += [m_.weight, m_.bias, s_]
             xo, _ = DNETFn.apply(specs, self.capture, S, *params, self._phase_weights(S.device))
-            return xo[:, :, 1:1 + out_h, 1:1 + out_w]
+            return CropFn.apply(xo, out_h, out_w)
 
         wph = self._phase_weights(S.device)
         w4, w5, w6 = (None, None, None) if wph is None else tuple(wph)

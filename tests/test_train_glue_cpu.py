@@ -38,3 +38,20 @@ def test_checkpoint_roundtrip_with_module_prefix(nconv_amd, tmp_path):
     nconv_amd.train.load_checkpoint(fresh, os.path.join(tmp_path, "ck.pth.tar"), strict=True)
     for (k, v), (k2, v2) in zip(fresh.state_dict().items(), net.module.state_dict().items()):
         assert k == k2 and torch.equal(v, v2)
+
+
+def test_crop_backward_is_the_slice_backward(nconv_amd):
+    """DNET's training output crop (dnet.CropFn: one zero-pad in the backward) against autograd's
+    slice of step1.py:94, for the literal and generalized crops."""
+    g = torch.Generator().manual_seed(3)
+    for H, W in [(10, 12), (480, 640), (352, 1216)]:
+        for crop in ("literal", "generalized"):
+            h, w = nconv_amd.dnet.crop_hw(H, W, crop)
+            x = torch.randn(1, 1, H + 2, W + 2, generator=g, requires_grad=True)
+            y = nconv_amd.dnet.CropFn.apply(x, h, w)
+            ref = x[:, :, 1:1 + h, 1:1 + w]
+            assert torch.equal(y, ref) and y._is_view()
+            go = torch.randn(ref.shape, generator=g)
+            a, = torch.autograd.grad(y, x, go)
+            b, = torch.autograd.grad(ref, x, go)
+            assert torch.equal(a, b)
