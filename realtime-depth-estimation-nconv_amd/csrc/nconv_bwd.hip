@@ -1239,12 +1239,60 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(GP ? NCONV_W
 #pragma unroll
     for (int kk = 0; kk < C::OPW; ++kk) gb_acc[kk] = gs_acc[kk] = 0.f;
 
-    auto load_in = [&](int ih) {
+    // UpCat inputs: the wave's channel sources, the up plane's column map and one resource per
+    // source image resolved once, not per row (per-row channel resolution cost ~100 SGPR-spill
+    // reloads and a general nearest-index path per row); per row only the row map and two offsets.
+    constexpr bool UPC = MODE == NCONV_LOAD_UPCAT_SKIP_FIRST || MODE == NCONV_LOAD_UPCAT_UP_FIRST;
+    const int iw_in = ow0 - L.PW + lane;
+    const bool col_in = (unsigned)iw_in < (unsigned)L.W;
+    const int sw_up = UPC ? nearest_src(col_in ? iw_in : 0, L.b.W, L.W, d.up_scale_w) : 0;
+    bool up_k[C::CPW];
+    int so_k[C::CPW];
 #pragma unroll
-        for (int kk = 0; kk < C::CPW; ++kk) {
-            const int i = w + 4 * kk;
-            px[kk] = pc[kk] = 0.f;
-            if (i < CIN) load_px<MODE>(d, chan_src<MODE>(d, b, i), ih, ow0 - L.PW + lane, px[kk], pc[kk]);
+    for (int kk = 0; kk < C::CPW; ++kk) {
+        const int i = w + 4 * kk;
+        if constexpr (UPC) {
+            const bool skip_first = MODE == NCONV_LOAD_UPCAT_SKIP_FIRST;
+            const int first_c = skip_first ? L.a.C : L.b.C;
+            const bool from_a = skip_first ? (i < first_c) : (i >= first_c);
+            up_k[kk] = !from_a;
+            so_k[kk] = (from_a ? (skip_first ? i : i - first_c) * L.a.H * L.a.W
+                               : (skip_first ? i - first_c : i) * L.b.H * L.b.W) * 4;
+        } else {
+            up_k[kk] = false;
+            so_k[kk] = 0;
+        }
+    }
+    const int abytes = UPC ? L.a.C * L.a.H * L.a.W * 4 : 0, bbytes = UPC ? L.b.C * L.b.H * L.b.W * 4 : 0;
+    const float* ax_img = UPC ? L.a.x + (size_t)b * L.a.C * L.a.H * L.a.W : nullptr;
+    const float* ac_img = UPC ? L.a.c + (size_t)b * L.a.C * L.a.H * L.a.W : nullptr;
+    const float* bx_img = UPC ? L.b.x + (size_t)b * L.b.C * L.b.H * L.b.W : nullptr;
+    const float* bc_img = UPC ? L.b.c + (size_t)b * L.b.C * L.b.H * L.b.W : nullptr;
+    auto load_in = [&](int ih) {
+        if constexpr (UPC) {
+            const bool in = (unsigned)ih < (unsigned)L.H && col_in;
+            const int sh = nearest_src(in ? ih : 0, L.b.H, L.H, d.up_scale_h);
+            const unsigned od = in ? (unsigned)(ih * L.a.W + iw_in) * 4u : OOB;
+            const unsigned ou = in ? (unsigned)(sh * L.b.W + sw_up) * 4u : OOB;
+#pragma unroll
+            for (int kk = 0; kk < C::CPW; ++kk) {
+                const int i = w + 4 * kk;
+                px[kk] = pc[kk] = 0.f;
+                if (i < CIN) {
+                    const bool up = up_k[kk];
+                    const __amdgpu_buffer_rsrc_t rx = plane_rsrc(up ? bx_img : ax_img, up ? bbytes : abytes);
+                    const __amdgpu_buffer_rsrc_t rc = plane_rsrc(up ? bc_img : ac_img, up ? bbytes : abytes);
+                    px[kk] = ld_f32s(rx, up ? ou : od, so_k[kk]);
+                    pc[kk] = ld_f32s(rc, up ? ou : od, so_k[kk]);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int kk = 0; kk < C::CPW; ++kk) {
+                const int i = w + 4 * kk;
+                px[kk] = pc[kk] = 0.f;
+                if (i < CIN) load_px<MODE>(d, chan_src<MODE>(d, b, i), ih, iw_in, px[kk], pc[kk]);
+            }
         }
     };
     auto store_in = [&](int ih) {
