@@ -20,12 +20,19 @@ reference's F.conv2d; include/nconv.h NCONV_MATH_FP32). Also on the same JSON li
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 8] [--height 352] [--width 1216]
     torchrun --nproc-per-node N bench.py --gpus N ...      # one process per GPU, RCCL
 
+`--gpus N` without a launcher (no WORLD_SIZE in the environment) starts the N rank processes
+itself (launch_ranks: one child per GPU with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1
+set, before this process touches the GPU) and exits with their status; N greater than the visible
+devices is an error. Under torchrun, --gpus must equal WORLD_SIZE.
+
 Multi-GPU: frames are independent units, so each rank runs its own B frames (weak scaling) with
 no collective in the forward; the training step all-reduces gradients over RCCL (one bucket).
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -56,7 +63,8 @@ LAYERS = ("nconv1", "nconv2", "nconv_down1", "nconv_down2", "nconv_down3", "ncon
 
 def parse():
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=None,
+                   help="GPUs (= rank processes, one per GPU); default: WORLD_SIZE under a launcher, else 1")
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--batch", type=int, default=8)
@@ -83,6 +91,48 @@ def parse():
                    help="replay the training step from a hipGraph (1) or eager (0); default: 1 on one GPU, 0 with "
                         "several (the RCCL all-reduce stays outside graph capture)")
     return p.parse_args()
+
+
+def _free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(n, argv, device_count=None, script=None, poll_s=0.2):
+    """Start n rank processes of `script` (default: this file) with `argv`, one per GPU, as
+    torch.distributed.run would (RANK = LOCAL_RANK = r, WORLD_SIZE = n, MASTER_ADDR 127.0.0.1, a free
+    MASTER_PORT), wait for them and return the exit status (the first failing rank's; the others are
+    then terminated, so no rank waits forever in a collective). Called before this process makes
+    any HIP call: torch.cuda.device_count() does not initialise the GPU on this image, and the
+    children are fresh processes (never an exec of a process that touched the GPU)."""
+    ndev = torch.cuda.device_count() if device_count is None else device_count
+    if n > ndev:
+        raise SystemExit(f"bench.py: --gpus {n} but only {ndev} GPU(s) are visible")
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, script or os.path.abspath(__file__)] + list(argv), env=env))
+    status = 0
+    while True:
+        codes = [p.poll() for p in procs]  # (every child polled each round)
+        if all(c is not None for c in codes):
+            break
+        bad = [c for c in codes if c not in (None, 0)]
+        if bad:
+            status = bad[0]
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            break
+        time.sleep(poll_s)
+    for p in procs:
+        rc = p.wait()
+        if rc and not status:
+            status = rc
+    return status if status >= 0 else 128 - status
 
 
 def log(*msg):
@@ -453,7 +503,11 @@ def make_train_step(m, dev, B, H, W, rank, graph=True):
 
 def main():
     a = parse()
+    if "WORLD_SIZE" not in os.environ and (a.gpus or 1) > 1:  # no launcher: start the ranks here
+        sys.exit(launch_ranks(a.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if a.gpus is not None and a.gpus != world:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but the launcher started WORLD_SIZE={world} ranks")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:

@@ -179,7 +179,8 @@ int nconv_head_weights(const nconv_layer* L1, const nconv_layer* L2, float* w21,
  * border get b7. crop0 = 1 is DNET's crop; crop0 = 0 with the full grid is nconv7's whole output.
  * out_c (nullable) receives the matching output confidence. Training (exact fp32, exactly-2x
  * phase form only; both or NULL): y6, cout6 (B, Cout6, Ho6, Wo6) receive nconv6's outputs, which
- * the backward reads. */
+ * the backward reads; the output window must then cover every nconv6 pixel (crop0 <= p7,
+ * crop0 + out_h - p7 >= Ho6, crop0 + out_w - p7 >= Wo6), else -EINVAL. */
 int nconv_fwd_tail(const nconv_layer* L6, const float* w7, const float* b7, const float* wsum7,
                    int cin7, int p7, float eps7, float* out, float* out_c, int out_h, int out_w, int crop0,
                    float* y6, float* cout6, void* stream);
@@ -265,8 +266,8 @@ typedef struct nconv_bwd_io {
      * nconv_bwd_tail_workspace_bytes(L) bytes; with NCONV_BWD_DEFER_REDUCE tail_nparts partial rows
      * for nconv_wgrad_reduce, layer tail). nconv7's bias gradient (the sum of tail_gy) is left to
      * the caller (it is computed by the call that requests L's gw / gbias: a call with only the
-     * input gradients computes none of nconv7's). L must be nconv6's exact-fp32 geometry (16 -> 8
-     * 3x3, padding 0, upsample-first exactly-2x concat). */
+     * input gradients computes none of nconv7's; tail_gw without gw / gbias is -EINVAL). L must
+     * be nconv6's exact-fp32 geometry (16 -> 8 3x3, padding 0, upsample-first exactly-2x concat). */
     const nconv_layer* tail;
     const float* tail_y;
     const float* tail_cout;

@@ -1116,15 +1116,14 @@ int launch_wgrad_reduce_multi(int n, const RedJob* jobs, hipStream_t st, const c
 
 // part: nblk partial rows followed by kReduceSplit rows of slice sums (see bwd_workspace_bytes);
 // with a.defer the rows stay for a later nconv_wgrad_reduce over every layer of the pass
-static void launch_wgrad_reduce(const BwdArgs& a, const float* part, int nblk, int nw, int cout, int fan,
-                                const float* wsum, hipStream_t st) {
+static int launch_wgrad_reduce(const BwdArgs& a, const float* part, int nblk, int nw, int cout, int fan,
+                               const float* wsum, hipStream_t st, const char** why) {
     if (a.defer) {
         *a.nparts = nblk;
-        return;
+        return 0;
     }
     const RedJob J{part, wsum, a.gw, a.gb, nblk, nw, cout, fan};
-    const char* why = nullptr;
-    launch_wgrad_reduce_multi(1, &J, st, &why);
+    return launch_wgrad_reduce_multi(1, &J, st, why);
 }
 
 // ---- wgrad on the matrix cores (fp32 MFMA 16x16x4, exact f32 products) -----------------------------
@@ -1672,7 +1671,7 @@ void plan_bwd(const nconv_layer& L, int* dgrad, int* wgrad) {
 // a bf16 request never silently runs another kernel).
 template <int CIN, int COUT, int K, int MODE, bool GP = false, bool HW = false, bool T7 = false>
 static int go_bwd_tiled(const LayerDev& d, const BwdArgs& a, float* part, float* tx, float* tc,
-                        hipStream_t st) {
+                        hipStream_t st, const char** why) {
     const nconv_layer& L = d.L;
     using D = DgCfg<CIN, K>;
     if (HW || a.gxa || a.gca || a.gxb || a.gcb) {
@@ -1697,8 +1696,7 @@ static int go_bwd_tiled(const LayerDev& d, const BwdArgs& a, float* part, float*
                         *a.hnparts = (int)g.x;
                     } else {
                         const RedJob J{a.hpart, a.hs, a.hgw, a.hgb, (int)g.x, kHeadNw, 8, 25};
-                        const char* why = nullptr;
-                        launch_wgrad_reduce_multi(1, &J, st, &why);
+                        if (int rc = launch_wgrad_reduce_multi(1, &J, st, why)) return rc;
                     }
                 }
             }
@@ -1708,9 +1706,12 @@ static int go_bwd_tiled(const LayerDev& d, const BwdArgs& a, float* part, float*
         if ((a.gw || a.gb) && L.bwd_math != NCONV_MATH_FP32) {  // split-bf16 matrix cores
             const int nblk = go_wgrad_bf<CIN, COUT, K, MODE>(d, a, part, (int)wm_grid(L).nblk,
                                                              L.bwd_math == NCONV_MATH_BF16X9 ? 3 : 2, st);
-            if (nblk < 0) return -5;
+            if (nblk < 0) {
+                *why = "bf16 weight-gradient grid exceeds the workspace";
+                return -5;
+            }
             const int nw = COUT * CIN * K * K;
-            launch_wgrad_reduce(a, part, nblk, nw, COUT, CIN * K * K, L.wsum, st);
+            return launch_wgrad_reduce(a, part, nblk, nw, COUT, CIN * K * K, L.wsum, st, why);
         } else if (a.gw || a.gb) {
             const int per_cu = dev_occupancy((const void*)wgrad_mfma<CIN, COUT, K, MODE, GP, T7>, kT, 0);
             const int resident = device_cus() * (per_cu < kMfmaMaxPerCu ? per_cu : kMfmaMaxPerCu);
@@ -1722,12 +1723,11 @@ static int go_bwd_tiled(const LayerDev& d, const BwdArgs& a, float* part, float*
                     *a.t7nparts = (int)g.nblk;
                 } else {
                     const RedJob J{a.t7part, a.t7s, a.t7gw, nullptr, (int)g.nblk, 8, 1, 8};
-                    const char* why = nullptr;
-                    launch_wgrad_reduce_multi(1, &J, st, &why);
+                    if (int rc = launch_wgrad_reduce_multi(1, &J, st, why)) return rc;
                 }
             }
             const int nw = COUT * CIN * K * K;
-            launch_wgrad_reduce(a, part, (int)g.nblk, nw, COUT, CIN * K * K, L.wsum, st);
+            return launch_wgrad_reduce(a, part, (int)g.nblk, nw, COUT, CIN * K * K, L.wsum, st, why);
         }
     } else if (a.gw || a.gb) {
         using W = WgCfg<CIN, COUT, K>;
@@ -1744,14 +1744,14 @@ static int go_bwd_tiled(const LayerDev& d, const BwdArgs& a, float* part, float*
         const int nblk = nblk_ws < resident ? nblk_ws : resident;
         hipLaunchKernelGGL((wgrad_tiled<CIN, COUT, K, MODE>), dim3(nblk), dim3(kT), lds, st, d, a, part, ntw, nth);
         const int nw = COUT * CIN * K * K;
-        launch_wgrad_reduce(a, part, nblk, nw, COUT, CIN * K * K, L.wsum, st);
+        return launch_wgrad_reduce(a, part, nblk, nw, COUT, CIN * K * K, L.wsum, st, why);
     }
     return 0;
 }
 
 template <int MODE>
-static void go_bwd_generic(const LayerDev& d, const BwdArgs& a, float* part, float* tx, float* tc,
-                           hipStream_t st) {
+static int go_bwd_generic(const LayerDev& d, const BwdArgs& a, float* part, float* tx, float* tc,
+                          hipStream_t st, const char** why) {
     const nconv_layer& L = d.L;
     if (a.gxa || a.gca || a.gxb || a.gcb) {
         const size_t n = (size_t)L.B * L.Cin * L.H * L.W;
@@ -1764,8 +1764,9 @@ static void go_bwd_generic(const LayerDev& d, const BwdArgs& a, float* part, flo
         const int nw = L.Cout * fan;
         const int nchunk = generic_chunks(L);
         hipLaunchKernelGGL(wgrad_generic<MODE>, dim3(nchunk, nw + 2 * L.Cout), dim3(kT), 0, st, d, a, part, nchunk);
-        launch_wgrad_reduce(a, part, nchunk, nw, L.Cout, fan, L.wsum, st);
+        return launch_wgrad_reduce(a, part, nchunk, nw, L.Cout, fan, L.wsum, st, why);
     }
+    return 0;
 }
 
 int launch_bwd(const LayerDev& d, const BwdArgs& a, hipStream_t st, const char** why) {
@@ -1791,9 +1792,9 @@ int launch_bwd(const LayerDev& d, const BwdArgs& a, hipStream_t st, const char**
                    "8->8 5x5 stride-1 layer with plain loads";
             return -95;
         }
-        if (a.hpart) go_bwd_tiled<8, 8, 5, NCONV_LOAD_PLAIN, true, true>(d, a, part, tx, tc, st);
-        else go_bwd_tiled<8, 8, 5, NCONV_LOAD_PLAIN, true>(d, a, part, tx, tc, st);
-        return last_err(why);
+        const int rc = a.hpart ? go_bwd_tiled<8, 8, 5, NCONV_LOAD_PLAIN, true, true>(d, a, part, tx, tc, st, why)
+                               : go_bwd_tiled<8, 8, 5, NCONV_LOAD_PLAIN, true>(d, a, part, tx, tc, st, why);
+        return rc ? rc : last_err(why);
     }
     if (a.t7part) {
         if (!(path == kTiled && dgrad_phase_ok(L) && L.load_mode == NCONV_LOAD_UPCAT_UP_FIRST && L.PH == 0 &&
@@ -1802,8 +1803,8 @@ int launch_bwd(const LayerDev& d, const BwdArgs& a, hipStream_t st, const char**
                    "exactly-2x concat)";
             return -95;
         }
-        go_bwd_tiled<16, 8, 3, NCONV_LOAD_UPCAT_UP_FIRST, false, false, true>(d, a, part, tx, tc, st);
-        return last_err(why);
+        const int rc = go_bwd_tiled<16, 8, 3, NCONV_LOAD_UPCAT_UP_FIRST, false, false, true>(d, a, part, tx, tc, st, why);
+        return rc ? rc : last_err(why);
     }
     if (a.hpart) {
         if (!(path == kTiled && L.Cin == 8 && L.Cout == 8 && L.KH == 5 && L.load_mode == NCONV_LOAD_PLAIN &&
@@ -1811,31 +1812,30 @@ int launch_bwd(const LayerDev& d, const BwdArgs& a, hipStream_t st, const char**
             *why = "fused head weight gradient needs an exact-fp32 8->8 5x5 stride-1 layer with plain loads";
             return -95;
         }
-        go_bwd_tiled<8, 8, 5, NCONV_LOAD_PLAIN, false, true>(d, a, part, tx, tc, st);
-        return last_err(why);
+        const int rc = go_bwd_tiled<8, 8, 5, NCONV_LOAD_PLAIN, false, true>(d, a, part, tx, tc, st, why);
+        return rc ? rc : last_err(why);
     }
     if (path == kTiled) {
         const int m = L.load_mode;
         int rc;
-        if (L.Cin == 1 && m == NCONV_LOAD_THRESH) rc = go_bwd_tiled<1, 8, 5, NCONV_LOAD_THRESH>(d, a, part, tx, tc, st);
-        else if (L.Cin == 8 && L.Cout == 8 && m == NCONV_LOAD_PLAIN) rc = go_bwd_tiled<8, 8, 5, NCONV_LOAD_PLAIN>(d, a, part, tx, tc, st);
-        else if (L.Cin == 8 && L.Cout == 8 && m == NCONV_LOAD_POOL2) rc = go_bwd_tiled<8, 8, 5, NCONV_LOAD_POOL2>(d, a, part, tx, tc, st);
-        else if (m == NCONV_LOAD_UPCAT_SKIP_FIRST) rc = go_bwd_tiled<16, 8, 3, NCONV_LOAD_UPCAT_SKIP_FIRST>(d, a, part, tx, tc, st);
-        else if (m == NCONV_LOAD_UPCAT_UP_FIRST) rc = go_bwd_tiled<16, 8, 3, NCONV_LOAD_UPCAT_UP_FIRST>(d, a, part, tx, tc, st);
-        else rc = go_bwd_tiled<8, 1, 1, NCONV_LOAD_PLAIN>(d, a, part, tx, tc, st);
-        if (rc) {
-            *why = "bf16 weight-gradient grid exceeds the workspace";
-            return rc;
-        }
+        if (L.Cin == 1 && m == NCONV_LOAD_THRESH) rc = go_bwd_tiled<1, 8, 5, NCONV_LOAD_THRESH>(d, a, part, tx, tc, st, why);
+        else if (L.Cin == 8 && L.Cout == 8 && m == NCONV_LOAD_PLAIN) rc = go_bwd_tiled<8, 8, 5, NCONV_LOAD_PLAIN>(d, a, part, tx, tc, st, why);
+        else if (L.Cin == 8 && L.Cout == 8 && m == NCONV_LOAD_POOL2) rc = go_bwd_tiled<8, 8, 5, NCONV_LOAD_POOL2>(d, a, part, tx, tc, st, why);
+        else if (m == NCONV_LOAD_UPCAT_SKIP_FIRST) rc = go_bwd_tiled<16, 8, 3, NCONV_LOAD_UPCAT_SKIP_FIRST>(d, a, part, tx, tc, st, why);
+        else if (m == NCONV_LOAD_UPCAT_UP_FIRST) rc = go_bwd_tiled<16, 8, 3, NCONV_LOAD_UPCAT_UP_FIRST>(d, a, part, tx, tc, st, why);
+        else rc = go_bwd_tiled<8, 1, 1, NCONV_LOAD_PLAIN>(d, a, part, tx, tc, st, why);
+        if (rc) return rc;
     } else {
+        int rc = 0;
         switch (L.load_mode) {
-            case NCONV_LOAD_PLAIN: go_bwd_generic<NCONV_LOAD_PLAIN>(d, a, part, tx, tc, st); break;
-            case NCONV_LOAD_THRESH: go_bwd_generic<NCONV_LOAD_THRESH>(d, a, part, tx, tc, st); break;
-            case NCONV_LOAD_POOL2: go_bwd_generic<NCONV_LOAD_POOL2>(d, a, part, tx, tc, st); break;
-            case NCONV_LOAD_UPCAT_SKIP_FIRST: go_bwd_generic<NCONV_LOAD_UPCAT_SKIP_FIRST>(d, a, part, tx, tc, st); break;
-            case NCONV_LOAD_UPCAT_UP_FIRST: go_bwd_generic<NCONV_LOAD_UPCAT_UP_FIRST>(d, a, part, tx, tc, st); break;
+            case NCONV_LOAD_PLAIN: rc = go_bwd_generic<NCONV_LOAD_PLAIN>(d, a, part, tx, tc, st, why); break;
+            case NCONV_LOAD_THRESH: rc = go_bwd_generic<NCONV_LOAD_THRESH>(d, a, part, tx, tc, st, why); break;
+            case NCONV_LOAD_POOL2: rc = go_bwd_generic<NCONV_LOAD_POOL2>(d, a, part, tx, tc, st, why); break;
+            case NCONV_LOAD_UPCAT_SKIP_FIRST: rc = go_bwd_generic<NCONV_LOAD_UPCAT_SKIP_FIRST>(d, a, part, tx, tc, st, why); break;
+            case NCONV_LOAD_UPCAT_UP_FIRST: rc = go_bwd_generic<NCONV_LOAD_UPCAT_UP_FIRST>(d, a, part, tx, tc, st, why); break;
             default: *why = "unknown load mode"; return -22;
         }
+        if (rc) return rc;
     }
     if (up && (a.gxb || a.gcb) && !(path == kTiled && dgrad_phase_ok(L))) {  // (dgrad_phase writes them itself)
         const size_t n = (size_t)L.B * L.b.C * L.b.H * L.b.W;

@@ -201,6 +201,10 @@ int nconv_fwd_tail(const nconv_layer* L6, const float* w7, const float* b7, cons
     if (crop0 + out_h > L6->Ho + 2 * p7 || crop0 + out_w > L6->Wo + 2 * p7)
         return fail(-22, "nconv_fwd_tail", "output crop exceeds nconv7's grid");
     if ((y6 == nullptr) != (cout6 == nullptr)) return fail(-22, "nconv_fwd_tail", "y6 and cout6: both or neither");
+    // nconv6's outputs are written only where the output window reaches them: with y6 the window
+    // must cover every nconv6 pixel (rows / columns crop0 - p7 .. crop0 - p7 + out - 1 of nconv6)
+    if (y6 && (crop0 > p7 || crop0 + out_h - p7 < L6->Ho || crop0 + out_w - p7 < L6->Wo))
+        return fail(-22, "nconv_fwd_tail", "y6 / cout6 need an output window covering every nconv6 pixel");
     nconv::TailArgs t{w7, b7, wsum7, eps7, crop0 - p7, out_h, out_w, out_c};
     t.y6 = y6;
     t.c6 = cout6;
@@ -302,6 +306,10 @@ int nconv_bwd_ex(const nconv_layer* L, nconv_bwd_io* io, void* workspace, size_t
         if (!io->tail_workspace || io->tail_workspace_bytes < nconv::bwd_tail_workspace_bytes(*L))
             return fail(-22, "nconv_bwd", "tail workspace too small (nconv_bwd_tail_workspace_bytes)");
         if (!defer && !io->tail_gw && (io->gw || io->gbias)) return fail(-22, "nconv_bwd", "tail output is NULL");
+        // nconv7's weight gradient is accumulated inside this layer's weight-gradient pass, which
+        // runs only when gw or gbias is requested
+        if (io->tail_gw && !io->gw && !io->gbias)
+            return fail(-22, "nconv_bwd", "tail_gw needs this layer's weight-gradient pass (gw or gbias)");
         a.t7w = T->weight;
         a.t7b = T->bias;
         a.t7s = T->wsum;

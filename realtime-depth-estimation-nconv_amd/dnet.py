@@ -141,7 +141,10 @@ class DNETFn(torch.autograd.Function):
 
         G[2], G[7] = (e(X[2][0]), e(X[2][1])), (e(X[7][0]), e(X[7][1]))
         exact_up = X[2][0].shape[2:] == tuple(2 * v for v in X[7][0].shape[2:])  # nconv6's phase form
-        if FUSE_TAIL_BWD and ctx.pooled and exact_up and gw[8] is not None:  # (c9 is non-differentiable)
+        # (c9 is non-differentiable; nconv7's weight gradient is accumulated inside nconv6's weight-
+        # gradient pass, so the fused form needs nconv6's gw or gb too)
+        if FUSE_TAIL_BWD and ctx.pooled and exact_up and gw[8] is not None and (gw[7] is not None or
+                                                                             gb[7] is not None):
             # nconv7's backward inside nconv6's (nconv_bwd_ex tail): its input gradient never reaches
             # HBM; its bias gradient is the sum of its output gradient (every output pixel, padding ring
             # included, as autograd's conv bias gradient)
@@ -220,14 +223,18 @@ def _tail_train(sp6, sp7, x2, c2, x7, c7, W6, W7, w6):
                                    _lib.stream_handle(dev))
     _lib.check(rc, "nconv_fwd_tail")
     return x8, c8, x9, c9
+
+
 class CropFn(torch.autograd.Function):
-    """xo[:, :, 1:1+h, 1:1+w] (step1.py:94), a view as there; its backward zero-pads the gradient
-    in one launch (autograd's two slice backwards zero-fill and copy twice)."""
+    """xo[:, :, 1:1+h, 1:1+w] (step1.py:94); its backward zero-pads the gradient in one launch
+    (autograd's two slice backwards zero-fill and copy twice). The crop is returned as a fresh
+    tensor (not a view, as the reference's slice is), so in-place operations on DNET's output
+    (clamp_, masked_fill_, ...) stay legal under autograd; the copy is the output's size only."""
 
     @staticmethod
     def forward(ctx, x, h, w):
         ctx.pad = (1, x.shape[3] - 1 - w, 1, x.shape[2] - 1 - h)
-        return x[:, :, 1:1 + h, 1:1 + w]
+        return x[:, :, 1:1 + h, 1:1 + w].contiguous()
 
     @staticmethod
     def backward(ctx, g):

@@ -71,10 +71,14 @@ class DataParallelRCCL(nn.Module):
 
     @torch.no_grad()
     def allreduce_grads(self):
-        """Average present gradients across ranks in one bucketed all-reduce."""
+        """Average present gradients across ranks in one bucketed all-reduce. Runs whenever a process
+        group is initialised, a one-rank group included (the same RCCL path, so it can be exercised
+        and graph-captured on one GPU); without one it is a no-op."""
+        if not (dist.is_available() and dist.is_initialized()):
+            return
         ws = self.world_size()
         grads = [g for _, g in self.grad_bucket()]
-        if ws <= 1 or not grads:
+        if not grads:
             return
         flat = torch.cat([g.reshape(-1) for g in grads])
         dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.process_group)

@@ -297,9 +297,15 @@ class WgradReduce:
 
     def add(self, L, ws, nparts, gw, gb):
         if nparts > 0 and (gw is not None or gb is not None):  # (input-gradient-only calls add none)
-            self.jobs.append((L, ws, nparts, gw, gb))
+            self.jobs.append((L, ws, nparts, gw, gb, torch.cuda.current_stream(ws.device)))
 
     def run(self, device):
+        cur = torch.cuda.current_stream(device)
+        for j in self.jobs:
+            # a workspace allocated on another stream (the weight-gradient side stream) is read here
+            # by the current one: keep the allocator from reusing it before this reduction ran
+            if j[5] != cur:
+                j[1].record_stream(cur)
         for k in range(0, len(self.jobs), 16):
             jobs = self.jobs[k:k + 16]
             n = len(jobs)

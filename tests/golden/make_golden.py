@@ -20,6 +20,16 @@ Fixtures written (small .npz, float32 unless noted):
   f7_loss.npz     calculate_loss on a (B, 1, H, W) batch (the training loop's call,
                   train_step1.py:63) and on element [0], both loss modes, + autograd gradients
   f8_train_batch.npz  two DNET training steps with the full-batch loss of train_step1.py:63
+  f9_guided_train.npz one SETP2_BP_TRAIN training iteration (train_step2.py:60-66: train mode,
+                  model(rgb, depth, rgb, depth), calculate_loss_multi_resolution without the
+                  gradient loss, backward) at 480x640: the four outputs, the loss, every trainable
+                  gradient and the BatchNorm running statistics after the step
+  f10_train_dense.npz / f11_train_dense_batch.npz  f3 / f8 at 40 %-dense depth: distinct
+                  per-pixel values, so a 2x2 max-pool window's winner is decided by rounding only
+                  where its two largest values happen to lie within fp32 noise (recorded here:
+                  windows with a relative gap < 1e-5, a handful of ~64 k per step, against ~3.5 %
+                  of all windows at f3's 5 % density, where neighbouring outputs repeat one sample);
+                  every gradient tensor is held to the 1e-3 bound against these
 
     python tests/golden/make_golden.py [/root/reference] [f7 f8 ...]   # a subset
 """
@@ -120,10 +130,33 @@ def _ref_calculate_loss():
     return ref_utils
 
 
-def train_fixtures(step1, full_batch=False):
+def _pool_margins(net):
+    """Forward hooks recording, for every 2x2 max-pool the DNET forward applies (the outputs of
+    nconv2, down1 and down2, x and c alike: step1.py:62-75), the smallest relative gap between the
+    largest and second-largest value of a window, the number of windows whose gap is below 1e-5,
+    and the number of windows."""
+    import torch.nn.functional as F
+    gaps = []
+
+    def hook(_m, _inp, out):
+        for t in out:
+            t = t.detach()
+            B, C, H, W = t.shape
+            w = t[:, :, :H // 2 * 2, :W // 2 * 2].reshape(B, C, H // 2, 2, W // 2, 2)
+            w = w.permute(0, 1, 2, 4, 3, 5).reshape(-1, 4)
+            top = w.topk(2, dim=1).values
+            rel = (top[:, 0] - top[:, 1]) / top[:, 0].abs().clamp_min(1e-30)
+            gaps.append((rel.min().item(), int((rel < 1e-5).sum()), rel.numel()))
+    d = net.d_net
+    hs = [m.register_forward_hook(hook) for m in (d.nconv2, d.nconv_down1, d.nconv_down2)]
+    return gaps, hs
+
+
+def train_fixtures(step1, full_batch=False, density=0.05, name=None):
     """F3: two training steps, train_step1.py:59-65 semantics (AdamW lr 1e-2, wd 1e-7), the loss on
     element [0] (the validation loop's call, utils.py:36). F8 (full_batch): the same with the loss on
-    the whole batch, as the training loop calls it (train_step1.py:63)."""
+    the whole batch, as the training loop calls it (train_step1.py:63). density: fraction of valid
+    depth samples (F10 / F11: 0.4, every pooled window's winner decided by a clear margin)."""
     ref_utils = _ref_calculate_loss()
     torch.manual_seed(0)
     net = step1.SETP1_NCONV()
@@ -131,8 +164,9 @@ def train_fixtures(step1, full_batch=False):
     opt = torch.optim.AdamW(net.parameters(), lr=1e-2, weight_decay=1e-7)
     g = torch.Generator().manual_seed(9)
     B, H, W = 2, 64, 96
+    gaps, hooks = _pool_margins(net) if density > 0.05 else ([], [])
     for step in range(2):
-        S = (torch.rand(B, 1, H, W, generator=g) * 79 + 1) * (torch.rand(B, 1, H, W, generator=g) < 0.05)
+        S = (torch.rand(B, 1, H, W, generator=g) * 79 + 1) * (torch.rand(B, 1, H, W, generator=g) < density)
         gt = (torch.rand(B, 1, H + 1, W + 1, generator=g) * 79 + 1) * (torch.rand(B, 1, H + 1, W + 1, generator=g) < 0.3)
         net.train()
         opt.zero_grad()
@@ -151,7 +185,75 @@ def train_fixtures(step1, full_batch=False):
         opt.step()
         for k, p in net.named_parameters():
             out[f"step{step}_after_{k}"] = np32(p)
-    np.savez_compressed(os.path.join(OUT, "f8_train_batch.npz" if full_batch else "f3_train.npz"), **out)
+    for h in hooks:
+        h.remove()
+    if gaps:
+        out["pool_min_margin"] = np.array(min(m for m, _, _ in gaps), np.float64)
+        out["pool_windows_within_1e-5"] = np.array(sum(n for _, n, _ in gaps), np.int64)
+        out["pool_windows"] = np.array(sum(n for _, _, n in gaps), np.int64)
+    name = name or ("f8_train_batch.npz" if full_batch else "f3_train.npz")
+    np.savez_compressed(os.path.join(OUT, name), **out)
+
+
+def _setp2_train_model(step1, step2):
+    """SETP2_BP_TRAIN built as f5 does: step 1 from a temporary reference-format checkpoint of the
+    positive (EnforcePos-applied) seed-0 SETP1_NCONV, the rest from torch.manual_seed(1), and the
+    step-1 call shim (DNET on the batch concatenation, step2.py:62-63)."""
+    net1 = positive_setp1(step1)
+    with tempfile.TemporaryDirectory() as tmp:
+        os.makedirs(os.path.join(tmp, "checkpoints"))
+        torch.save({"epoch": 0, "state_dict": {"module." + k: v for k, v in net1.state_dict().items()},
+                    "stats": None}, os.path.join(tmp, "checkpoints", "s1.pth.tar"))
+        cwd = os.getcwd()
+        os.chdir(tmp)
+        try:
+            torch.manual_seed(1)
+            model = step2.SETP2_BP_TRAIN("s1")
+        finally:
+            os.chdir(cwd)
+    model.step1.forward = lambda d0, d1: model.step1.d_net(torch.cat((d0, d1), 0))
+    return model
+
+
+def guided_train_fixtures(step1, step2):
+    """F9: one training iteration of train_step2.py:60-66 on the reference: model.train(),
+    optim.zero_grad(), estimated_depths, _ = model(rgb, depth, rgb, depth) (the same pair twice, as
+    the script calls it), calculate_loss_multi_resolution(estimated_depths, gt, False)
+    (use_gradient_loss = False, train_step2.py:21; utils.py:63-71), backward, AdamW step (get_optimizer
+    'adam', lr 1e-4, wd 1e-7: train_step2.py:16-17,34). 1 frame at 480x640 (NYU's size: the literal
+    step-1 crop, step1.py:94, matches the RGB branch only there). Stored: inputs (regenerated from
+    torch.Generator().manual_seed(19), sums pinned), the four outputs, the loss, every trainable
+    gradient and the BatchNorm running statistics after the step (train-mode BN updates them in the
+    forward, momentum 0.1). Weights regenerate from the seeds as in f5 (sums pinned)."""
+    ref_utils = _ref_calculate_loss()
+    model = _setp2_train_model(step1, step2)
+    out = {"init_sum_" + k: np.array(v.double().sum().item(), np.float64) for k, v in model.state_dict().items()
+           if v.dtype == torch.float32}
+    optim = ref_utils.get_optimizer(model, "adam", 1e-4, 1e-7)
+    g = torch.Generator().manual_seed(19)
+    H, W = 480, 640
+    rgb = torch.rand(1, 3, H, W, generator=g) * 255
+    depth = (torch.rand(1, 1, H, W, generator=g) * 79 + 1) * (torch.rand(1, 1, H, W, generator=g) < 0.05)
+    gt = (torch.rand(1, 1, H, W, generator=g) * 79 + 1) * (torch.rand(1, 1, H, W, generator=g) < 0.8)
+    for k, v in (("rgb", rgb), ("depth", depth), ("gt", gt)):
+        out[k + "_sum"] = np.array(v.double().sum().item(), np.float64)
+    model.train()
+    optim.zero_grad()
+    est, est1 = model(rgb, depth, rgb, depth)
+    loss = ref_utils.calculate_loss_multi_resolution(est, gt, False)
+    loss.requires_grad_().backward()
+    out["loss"] = np.array(loss.item(), np.float64)
+    for i in range(4):
+        out[f"out0_{i}"] = np32(est[i][0, 0])
+        out[f"out1_{i}_sum"] = np.array(est1[i].double().sum().item(), np.float64)
+    for k, p in model.named_parameters():
+        if p.grad is not None:
+            out["grad_" + k] = np32(p.grad)
+    optim.step()
+    for k, v in model.state_dict().items():
+        if "running_" in k or "num_batches_tracked" in k:
+            out["bn_" + k] = np32(v) if v.dtype == torch.float32 else v.numpy().copy()
+    np.savez_compressed(os.path.join(OUT, "f9_guided_train.npz"), **out)
 
 
 def loss_fixtures():
@@ -261,7 +363,10 @@ def main():
     jobs = {"f1": lambda: layer_fixtures(step1), "f2": lambda: dnet_fixtures(step1),
             "f3": lambda: train_fixtures(step1), "f4": mask_fixtures,
             "f5": lambda: guided_fixtures(step1, step2), "f6": lambda: init_fixtures(step1, step2),
-            "f7": loss_fixtures, "f8": lambda: train_fixtures(step1, full_batch=True)}
+            "f7": loss_fixtures, "f8": lambda: train_fixtures(step1, full_batch=True),
+            "f9": lambda: guided_train_fixtures(step1, step2),
+            "f10": lambda: train_fixtures(step1, density=0.4, name="f10_train_dense.npz"),
+            "f11": lambda: train_fixtures(step1, full_batch=True, density=0.4, name="f11_train_dense_batch.npz")}
     for k, job in jobs.items():
         if not ONLY or k in ONLY:
             job()

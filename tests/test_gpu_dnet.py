@@ -357,3 +357,36 @@ def test_config5_batch16_matches_per_frame(nconv_amd, gpu, fwd_math):
         assert out.shape == (16, 1, 1024, 2048) and torch.isfinite(out).all()
         for i in range(16):
             assert torch.equal(net(S[i:i + 1]), out[i:i + 1]), f"frame {i}"
+
+
+@pytest.mark.parametrize("frozen", [("nconv6.weight", "nconv6.bias"), ("nconv6.weight",), ("nconv6.bias",),
+                                    ("nconv7.weight",)])
+def test_frozen_layers_fused_tail_matches_unfused(nconv_amd, gpu, monkeypatch, frozen):
+    """Individually frozen layers around the fused tail backward (nconv7's backward inside
+    nconv6's): every trainable gradient equals the unfused path's (nconv6 and nconv7 as two
+    backward launches) within 1e-5 normwise -- in particular nconv7's weight gradient when nconv6's
+    weight and bias are both frozen, which the fused form cannot produce (it accumulates nconv7's
+    weight gradient inside nconv6's weight-gradient pass), so DNETFn must not take it then."""
+    g = torch.Generator().manual_seed(91)
+    S = sparse_depth(g, 2, 64, 96).to(gpu)
+    gt = (torch.rand(2, 1, 64, 96, generator=g) * 80).to(gpu)
+    grads = {}
+    for fused in (True, False):
+        monkeypatch.setattr(nconv_amd.dnet, "FUSE_TAIL_BWD", fused)
+        net = make_net(nconv_amd, "generalized", gpu)
+        for n, p in net.d_net.named_parameters():
+            p.requires_grad_(n not in frozen)
+        net.train()
+        out = net(S)
+        nconv_amd.train.calculate_loss(out, gt, True).backward()
+        torch.cuda.synchronize()
+        grads[fused] = {n: (p.grad.detach().clone() if p.grad is not None else None)
+                        for n, p in net.d_net.named_parameters() if "bnorm" not in n}
+    for n, a in grads[True].items():
+        b = grads[False][n]
+        assert (a is None) == (b is None) == (n in frozen), n
+        if a is None:
+            continue
+        assert torch.isfinite(a).all(), n
+        rel = ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
+        assert rel <= 1e-5, f"{n}: {rel:.2e}"

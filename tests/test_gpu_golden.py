@@ -101,8 +101,11 @@ def test_f2_dnet_eval_forward(nconv_amd, gpu, fwd_math, hw):
 
 
 # ---- f3 / f8: two training steps --------------------------------------------------------------------
-@pytest.mark.parametrize("fixture,full_batch", [("f3_train.npz", False), ("f8_train_batch.npz", True)])
-def test_f3_two_training_steps(nconv_amd, gpu, fixture, full_batch):
+@pytest.mark.parametrize("fixture,full_batch,strict", [("f3_train.npz", False, False),
+                                                       ("f8_train_batch.npz", True, False),
+                                                       ("f10_train_dense.npz", False, True),
+                                                       ("f11_train_dense_batch.npz", True, True)])
+def test_f3_two_training_steps(nconv_amd, gpu, fixture, full_batch, strict):
     """train_step1.py:59-65 on the GPU path (train mode: EnforcePos in weight_prep, whole-graph
     DNET autograd node, fused loss kernels, exact-fp32 training forward) from the reference's
     initial weights: per step the weights as used (after the drift), the loss, every gradient and
@@ -111,7 +114,10 @@ def test_f3_two_training_steps(nconv_amd, gpu, fixture, full_batch):
     Tolerances: loss 1e-5 relative; gradients normwise 1e-3, except that around an
     isolated depth sample the 2x2 max-pool winner is decided by fp32 rounding noise (any two fp32
     implementations disagree on ~3.5 % of those windows), which moves some gradient
-    mass by one pixel in the layers below the pools (printed; bounded at 1e-2). Weights: 1e-4
+    mass by one pixel in the layers below the pools (printed; bounded at 1e-2). f10 / f11 (strict)
+    repeat f3 / f8 at 40 %-dense depth, where every pixel's value is distinct and only a few dozen
+    of ~129 k pooled windows lie within 1e-5 of a tie: all 18 gradient tensors of both steps are
+    held to 1e-3 there, no layer excepted. Weights: 1e-4
     relative + 1e-5, except elements whose reference gradient is below 1e-3 of its tensor's
     largest: AdamW's first steps divide by sqrt(v) ~ |g|, so there the update amplifies the
     gradient's rounding difference (bounded by 2 lr; the element is printed and carried to the next
@@ -149,7 +155,7 @@ def test_f3_two_training_steps(nconv_amd, gpu, fixture, full_batch):
             g_ref = T(f[f"step{step}_grad_{k}"])
             rel = normwise(prm.grad, g_ref)
             report.append(f"step {step} {k} grad: {rel:.2e}")
-            assert rel <= 1e-2 and (rel <= 1e-3 or _pool_sensitive(k)), report[-1]
+            assert rel <= 1e-2 and (rel <= 1e-3 or (not strict and _pool_sensitive(k))), report[-1]
             ill[k] = ill.get(k, torch.zeros(g_ref.shape, dtype=torch.bool)) | \
                 (g_ref.abs() <= 1e-3 * g_ref.abs().max())
         opt.step()
@@ -231,11 +237,19 @@ def test_f4_threshold_mask_bit_exact(nconv_amd, gpu, fwd_math):
     y1, co1 = N.layer_forward_raw(sp1, S, None, None, None, w1, b1, s1)
     for o in range(8):
         assert torch.equal(co1[:, o:o + 1].cpu(), c0), f"nconv1 cout channel {o}"
-    if fwd_math != "fp32":  # the fused head (matrix-core maths)
-        sp2, w2, b2, s2 = _center_layer(nconv_amd, gpu, 8, 8, 5, nconv_amd._lib.PLAIN)
-        _, co2, _, _ = N.layer_forward_head(sp1, sp2, S, w1, b1, s1, w2, b2, s2)
+    # the fused head: exact fp32 (fwd_head_exact: nconv1 on the nonzero taps of c0, nconv2's
+    # confidence from the composed 9x9 weights W21 on interior tiles -- here W21 = the centre tap, so
+    # cout2 = c0 exactly) or the matrix-core maths (fwd_mfma<HEAD>)
+    sp2, w2, b2, s2 = _center_layer(nconv_amd, gpu, 8, 8, 5, nconv_amd._lib.PLAIN)
+    w21 = N.head_weights(sp1, sp2, S, w1, b1, s1, w2, b2, s2) if fwd_math == "fp32" else None
+    _, co2, _, _ = N.layer_forward_head(sp1, sp2, S, w1, b1, s1, w2, b2, s2, w21)
+    for o in range(8):
+        assert torch.equal(co2[:, o:o + 1].cpu(), c0), f"fused head channel {o}"
+    if fwd_math == "fp32":  # ... and its training variant (also writes nconv1's outputs)
+        _, co2t, _, _, _, y1t, co1t = N.layer_forward_head(sp1, sp2, S, w1, b1, s1, w2, b2, s2, w21, train=True)
         for o in range(8):
-            assert torch.equal(co2[:, o:o + 1].cpu(), c0), f"fused head channel {o}"
+            assert torch.equal(co2t[:, o:o + 1].cpu(), c0) and torch.equal(co1t[:, o:o + 1].cpu(), c0), o
+        assert torch.equal(y1t, y1)
     Sg = S.clone().requires_grad_(True)
     y, co = N.nconv_layer(sp1, Sg, None, None, None, w1, b1, s1)
     gy = torch.randn(y.shape, generator=torch.Generator().manual_seed(1)).to(gpu)

@@ -52,3 +52,115 @@ def test_guided_generalized_crop_vs_oracle(nconv_amd, gpu, H, W):
     for i in range(4):
         _close(g0[i], r0[i], f"pair0 scale {i}")
         _close(g1[i], r1[i], f"pair1 scale {i}")
+
+
+def test_guided_training_iteration_matches_reference_f9(nconv_amd, gpu):
+    """Golden f9: one SETP2_BP_TRAIN iteration of train_step2.py:60-66 as the reference ran it
+    (train mode: frozen step 1 with its EnforcePos drift, batch-statistics BatchNorm; model(rgb,
+    depth, rgb, depth); calculate_loss_multi_resolution without the gradient loss; backward) on the
+    GPU path. Outputs |gpu - ref| <= 1e-4*|ref| + 1e-3, loss 1e-5 relative, every trainable gradient
+    normwise 1e-3, BatchNorm running statistics after the step 1e-4 relative +
+    1e-5, num_batches_tracked exact."""
+    import os
+    from guided_cases import f9_inputs, grad_rel, trainable_setp2
+    f = np.load(os.path.join(os.path.dirname(__file__), "golden", "f9_guided_train.npz"))
+    model = f5_models(nconv_amd).to(gpu)
+    opt = nconv_amd.train.get_optimizer(model, "adam", 1e-4, 1e-7)
+    rgb, depth, gt = (t.to(gpu) for t in f9_inputs())
+    model.train()
+    opt.zero_grad()
+    est, est1 = model(rgb, depth, rgb, depth)
+    loss = nconv_amd.train.calculate_loss_multi_resolution(est, gt, False)
+    loss.backward()
+    torch.cuda.synchronize()
+    ref_loss = float(f["loss"])
+    assert abs(loss.item() - ref_loss) <= 1e-5 * abs(ref_loss), (loss.item(), ref_loss)
+    for i in range(4):
+        _close(est[i][0, 0].detach(), f[f"out0_{i}"], f"scale {i}")
+        assert est1[i].detach().double().sum().item() == pytest.approx(float(f[f"out1_{i}_sum"]), rel=1e-5)
+    named = dict(model.named_parameters())
+    names = trainable_setp2(None, named.items())
+    assert set(k[5:] for k in f.files if k.startswith("grad_")) == set(names)
+    refs = {k: torch.from_numpy(f["grad_" + k]).double() for k in names}
+    report = [(k, grad_rel(named[k].grad.double().cpu(), refs[k], k, refs)) for k in names]
+    print("\n".join(f"{k}: {r:.2e}" for k, r in report))
+    bad = [f"{k}: {r:.2e}" for k, r in report if r > 1e-3]
+    assert not bad, "\n".join(bad)
+    opt.step()
+    sd = model.state_dict()
+    for k in f.files:
+        if k.startswith("bn_") and "running_" in k:
+            _bn = sd[k[3:]].double().cpu()
+            ref = torch.from_numpy(f[k]).double()
+            assert ((_bn - ref).abs() <= 1e-4 * ref.abs() + 1e-5).all(), k
+        elif k.startswith("bn_"):
+            assert int(sd[k[3:]]) == int(f[k]), k
+
+
+def _kitti_model(nconv_amd, gpu, seed=2):
+    torch.manual_seed(seed)
+    model = nconv_amd.SETP2_BP_TRAIN(None, step1_crop="generalized").to(gpu)
+    with torch.no_grad():  # trained-like positive step-1 weights
+        for n, p in model.step1.named_parameters():
+            if n.endswith("weight") and "bnorm" not in n:
+                p.copy_(torch.nn.functional.softplus(p, beta=10))
+    return model
+
+
+def test_guided_config3_full_size_vs_oracle(nconv_amd, gpu):
+    """Config 3's workload at its own size: 1+1 frames of 352x1216 (KITTI shape, generalized crop)
+    through the eval forward (SETP2_BP_EXPORT's path, hipGraph-able MFMA kernels), all four scales
+    of both pairs against the float64 oracle; and SETP2_BP_EXPORT's border-zeroed output."""
+    model = _kitti_model(nconv_amd, gpu).eval()
+    H, W = 352, 1216
+    rgb0, d0, rgb1, d1 = f5_inputs(H, W)
+    sd = {k: v.detach().double().cpu() for k, v in model.state_dict().items()}
+    with torch.no_grad():
+        g0, g1 = model(rgb0.to(gpu), d0.to(gpu), rgb1.to(gpu), d1.to(gpu))
+        exp = nconv_amd.SETP2_BP_EXPORT(step1_crop="generalized").to(gpu).eval()
+        exp.load_state_dict(model.state_dict(), strict=False)
+        e0, e1 = exp(rgb0.to(gpu), d0.to(gpu), rgb1.to(gpu), d1.to(gpu))
+        r0, r1 = R.setp2_forward(sd, rgb0.double(), d0.double(), rgb1.double(), d1.double(), "generalized", "train")
+    for i in range(4):
+        assert g0[i].shape == r0[i].shape == (1, 1, H >> (3 - i), W >> (3 - i))
+        _close(g0[i], r0[i], f"pair0 scale {i}")
+        _close(g1[i], r1[i], f"pair1 scale {i}")
+    z = r0[3].clone()
+    z[:, :, :45, :] = 0
+    z[:, :, -45:, :] = 0
+    z[:, :, :, :20] = 0
+    _close(e0, z, "export frame 0")
+
+
+def test_guided_config4_full_size_training_vs_oracle(nconv_amd, gpu):
+    """Config 4's per-GPU training step at its own frame size: 1+1 frames of 352x1216, train mode
+    (batch-statistics BatchNorm, frozen drifted step 1), calculate_loss_multi_resolution (MSE),
+    backward: every trainable gradient normwise 1e-3 against the oracle evaluated with the
+    reference's own fp32 CPU ops (float64 at this size takes minutes on the box's host)."""
+    from guided_cases import grad_rel, trainable_setp2
+    model = _kitti_model(nconv_amd, gpu, seed=4)
+    H, W = 352, 1216
+    rgb0, d0, rgb1, d1 = f5_inputs(H, W)
+    g = torch.Generator().manual_seed(12)
+    gt = (torch.rand(1, 1, 480, 640, generator=g) * 79 + 1) * (torch.rand(1, 1, 480, 640, generator=g) < 0.5)
+    sd = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
+    model.train()
+    est, _ = model(rgb0.to(gpu), d0.to(gpu), rgb1.to(gpu), d1.to(gpu))
+    loss = nconv_amd.train.calculate_loss_multi_resolution(est, gt.to(gpu), False)
+    loss.backward()
+    torch.cuda.synchronize()
+    p1 = R.dnet_params_from_state_dict({k: (R.softplus_pos(v) if k.endswith(".weight") and "bnorm" not in k else v)
+                                        for k, v in sd.items()}, "step1.d_net.")
+    named = dict(model.named_parameters())
+    names = trainable_setp2(None, named.items())
+    leaves = {k: sd[k].clone().requires_grad_(True) for k in names}
+    sd.update(leaves)
+    r0, _ = R.setp2_forward(sd, rgb0, d0, rgb1, d1, "generalized", "train", training=True, step1_params=p1)
+    ref_loss = R.calculate_loss_multi_resolution(r0, gt, False)
+    ref_loss.backward()
+    assert abs(loss.item() - ref_loss.item()) <= 1e-4 * abs(ref_loss.item())
+    for i in range(4):
+        _close(est[i].detach(), r0[i].detach(), f"scale {i}")
+    refs = {k: leaves[k].grad.double() for k in names}
+    bad = [f"{k}: {r:.2e}" for k in names if (r := grad_rel(named[k].grad.double().cpu(), refs[k], k, refs)) > 1e-3]
+    assert not bad, "\n".join(bad)

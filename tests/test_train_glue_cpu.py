@@ -50,8 +50,18 @@ def test_crop_backward_is_the_slice_backward(nconv_amd):
             x = torch.randn(1, 1, H + 2, W + 2, generator=g, requires_grad=True)
             y = nconv_amd.dnet.CropFn.apply(x, h, w)
             ref = x[:, :, 1:1 + h, 1:1 + w]
-            assert torch.equal(y, ref) and y._is_view()
+            assert torch.equal(y, ref) and not y._is_view()
             go = torch.randn(ref.shape, generator=g)
             a, = torch.autograd.grad(y, x, go)
             b, = torch.autograd.grad(ref, x, go)
             assert torch.equal(a, b)
+    # in-place operations on the output (a script's clamp_ / masked_fill_) are legal under autograd,
+    # as they are on the reference's slice
+    x = torch.randn(1, 1, 12, 14, generator=g, requires_grad=True)
+    y = nconv_amd.dnet.CropFn.apply(x, 10, 12)
+    y.clamp_(min=0.0)
+    ref = x[:, :, 1:11, 1:13].clone().clamp_(min=0.0)
+    go = torch.randn(ref.shape, generator=g)
+    a, = torch.autograd.grad(y, x, go)
+    b, = torch.autograd.grad(ref, x, go)
+    assert torch.equal(a, b)
