@@ -263,20 +263,38 @@ def pmc_traffic(kernel, math, B, H, W):
         return None
 
 
+def sq_exec(kernel, math, B, H, W):
+    """The kernel's executed VALU work per launch from the committed SQ counters
+    (profiles/sq_exec.json, tools/gpu_runs/r4_sq.sh + tools/sq_report.py), or None."""
+    path = os.path.join(ROOT, "profiles", "sq_exec.json")
+    try:
+        d = json.load(open(path))
+        if tuple(d.get("config", ())) != (B, H, W):
+            return None
+        return d["kernels"][math].get(kernel)
+    except (OSError, ValueError, KeyError, TypeError, AttributeError):
+        return None
+
+
 def roofline(layer_us, costs, math, B, H, W, issued_mfma=None):
     """The roofline object of the dominant (longest) kernel of the forward. Its bound is the roof
     its arithmetic intensity (algorithmic flop per algorithmic byte) meets first:
-    above the fp32 ridge (157.3 TF/s / 8 TB/s = 19.7 flop/B) the compute roof -- "mfma", the dense
-    fp32 matrix peak of MI355X_MICROARCH.md, which the packed-FP32 vector ALU shares (the two peaks
-    are equal and do not add, tools/microbench/fp32_rates.hip) -- with achieved = the reference's
-    algorithmic fp32 flops per launch / the launch time; below it HBM. Both fractions are reported."""
+    above the fp32 ridge (157.3 TF/s / 8 TB/s = 19.7 flop/B) the compute roof -- "fp32-valu" for the
+    exact-fp32 kernels (packed FP32 FMAs on the vector ALU; its peak equals the dense fp32 matrix
+    peak of MI355X_MICROARCH.md and the two do not add, tools/microbench/fp32_rates.hip), "mfma" for
+    the bf16x3 / bf16x9 maths -- with achieved = the reference's algorithmic fp32 flops per launch /
+    the launch time; below it HBM. Both fractions are reported, and, where the committed SQ
+    counters (profiles/sq_exec.json) hold the kernel, the executed rate: the fp32 flops its FMA-class
+    VALU instructions actually performed per launch over the same time."""
     dom = max(layer_us, key=lambda n: layer_us[n])
     byt, fl = costs[dom]
     us = layer_us[dom]
     gbs = byt / (us * 1e-6) / 1e9
     tfs = fl / (us * 1e-6) / 1e12
     compute = fl / byt > FP32_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBS * 1e9)
-    r = {"bound": "mfma" if compute else "hbm",
+    # the compute roof of the exact-fp32 kernels is the packed-FP32 vector ALU ("fp32-valu"); the
+    # bf16x3 / bf16x9 maths run their products on the matrix cores ("mfma")
+    r = {"bound": ("fp32-valu" if math == "fp32" else "mfma") if compute else "hbm",
          "achieved": round(tfs, 2) if compute else round(gbs, 1),
          "peak": FP32_PEAK_TFLOPS if compute else HBM_PEAK_GBS,
          "unit": "TFLOP/s" if compute else "GB/s",
@@ -288,6 +306,13 @@ def roofline(layer_us, costs, math, B, H, W, issued_mfma=None):
                          "which equals the vector peak" if math == "fp32" else f"{math} products on the bf16 matrix cores",
          "hbm_achieved_gbs": round(gbs, 1), "hbm_frac": round(gbs / HBM_PEAK_GBS, 4),
          "fp32_tflops": round(tfs, 2), "fp32_frac": round(tfs / FP32_PEAK_TFLOPS, 4)}
+    ex = sq_exec(dom, math, B, H, W)
+    if ex:  # what the hardware executed: FMA-class VALU instructions x 64 lanes x 4 flop (packed)
+        etf = ex["executed_flops_per_launch"] / (us * 1e-6) / 1e12
+        r["executed"] = {"fp32_flops_per_launch": ex["executed_flops_per_launch"], "tflops": round(etf, 2),
+                         "frac": round(etf / FP32_PEAK_TFLOPS, 4),
+                         "valu_busy_frac": round(ex["valu_cycles_per_simd"] / (us * 1e-6 * 2.4e9), 4),
+                         "source": "profiles/sq_exec.json (SQ_INSTS_VALU_FMA_F32, SQ_INSTS_VALU per launch)"}
     if issued_mfma:
         r["mfma_issued_bf16_tflops"] = round(issued_mfma(dom) / (us * 1e-6) / 1e12, 2)
         r["mfma_bf16_dense_peak_tflops"] = MFMA_BF16_PEAK_TFLOPS

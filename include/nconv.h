@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define NCONV_ABI_VERSION 17
+#define NCONV_ABI_VERSION 18
 
 /* How a layer's input (data x, confidence c) is produced from its source tensors. These are the
  * DNET glue ops fused into the layer's load stage (models/step1.py:53,61-90). */
@@ -339,6 +339,14 @@ int nconv_dense_conv_fwd(const nconv_dense_conv* c, void* stream);
  * (the depth heads `depth + Conv3x3(fout)`, models/step2.py:259,278). */
 int nconv_conv3x3_c1(const float* x, int B, int Cin, int H, int W, const float* w, const float* res,
                      float* out, void* stream);
+
+/* Bilinear resampling with align_corners=True of (B, C, H, W) planes to (B, C, Ho, Wo): the guided
+ * model's depth downsampling F.interpolate(depth, scale_factor=1/k, mode="bilinear",
+ * align_corners=True) (models/step2.py:249,277), with the sampling arithmetic of the reference's
+ * CPU kernel: scale = fp32(H-1) / (Ho-1), source coordinate fp32(scale * o), truncated index,
+ * fp32 lambdas, blend fma(l0h, fma(l0w, a00, l1w*a01), l1h*fma(l0w, a10, l1w*a11)). x and y must
+ * not overlap. */
+int nconv_bilinear_ac(const float* x, int B, int C, int H, int W, float* y, int Ho, int Wo, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Training of the guided model: the weight gradient of a dense convolution.

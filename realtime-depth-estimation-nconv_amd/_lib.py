@@ -13,7 +13,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # NCONV_LIB: an alternative build of the same library (kernel-tuning experiments)
 LIB_PATH = os.environ.get("NCONV_LIB") or os.path.join(_HERE, "libnconv.so")
-ABI_VERSION = 17
+ABI_VERSION = 18
 BWD_ACCUMULATE = 1
 BWD_DEFER_REDUCE = 2
 
@@ -50,6 +50,7 @@ EXPORTED = (
     "nconv_dense_pack",
     "nconv_dense_conv_fwd",
     "nconv_conv3x3_c1",
+    "nconv_bilinear_ac",
     "nconv_dense_wgrad_workspace_bytes",
     "nconv_dense_conv_wgrad",
     "nconv_bn_workspace_bytes",
@@ -165,6 +166,8 @@ def _declare(lib):
     lib.nconv_dense_conv_fwd.argtypes = [ctypes.POINTER(NconvDenseConv), P]
     lib.nconv_conv3x3_c1.restype = I
     lib.nconv_conv3x3_c1.argtypes = [P, I, I, I, I, P, P, P, P]
+    lib.nconv_bilinear_ac.restype = I
+    lib.nconv_bilinear_ac.argtypes = [P, I, I, I, I, P, I, I, P]
     lib.nconv_dense_wgrad_workspace_bytes.restype = ctypes.c_size_t
     lib.nconv_dense_wgrad_workspace_bytes.argtypes = [ctypes.POINTER(NconvDenseWgrad)]
     lib.nconv_dense_conv_wgrad.restype = I

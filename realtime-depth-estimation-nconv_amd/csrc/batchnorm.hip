@@ -7,9 +7,18 @@
 //             block per channel, chunks combined in a fixed tree order with Chan's formula:
 //             deterministic, no E[x^2] - E[x]^2 cancellation; running mean / unbiased running var),
 //             bn_apply (1 read + 1 write: y = [relu](gamma (x - mean) invstd + beta));
-//   backward: bn_bwd_stats (2 reads: sum g' and sum g' xhat per chunk, g' = g masked by the
-//             recomputed ReLU), bn_bwd_finalize (fixed order), bn_bwd_apply (2 reads + 1 write:
-//             gx = gamma invstd (g' - sum g' / N - xhat sum g' xhat / N)).
+//   backward: bn_bwd_stats (2 reads: per chunk sum g', sum g' (x - mean), sum (x - mean), g' = g
+//             masked by the recomputed ReLU), bn_bwd_finalize (fixed order, double), bn_bwd_apply
+//             (2 reads + 1 write: gx = gamma invstd (g' - sum g' / N - xhat sum g' xhat / N), formed
+//             in double per element).
+// Why double in the backward: the saved mean is the batch mean rounded to fp32, so fp32 xhat = (x -
+// mean) invstd sums to N (mean_exact - mean) invstd instead of 0, and sum g' / N rounds likewise;
+// both leave gx with a systematic nonzero sum, which the preceding convolution's weight gradient
+// (sum gx * input, inputs with a large mean such as 0..255 RGB) multiplies by N. At 480x640 that
+// moved the RGB encoder convolutions' weight gradients by ~2e-3 of their size against float64 (as
+// PyTorch's native GPU BatchNorm does); the reference's CPU kernels accumulate in double. Here
+// the backward recovers the exact mean's offset from the fp32 one (sum (x - mean) / N, double) and
+// forms each gx in double, so the only error left per element is its final fp32 rounding.
 // A chunk is kChunk consecutive elements of one (image, channel) plane, 16 per thread (float4
 // loads when the plane size is a multiple of 4).
 #include "nconv_internal.h"
@@ -194,7 +203,8 @@ __global__ __launch_bounds__(kBT) void bn_apply(const float* __restrict__ x, flo
     store_chunk(y + off, hw, j, vec != 0, v);
 }
 
-// part[(c * nparts + b * ncp + j) * 2 + {0,1}] = (sum g', sum g' xhat) of chunk j of plane (b, c)
+// part[(c * nparts + b * ncp + j) * 3 + {0,1,2}] = (sum g', sum g' (x - mean), sum (x - mean)) of
+// chunk j of plane (b, c); mean = the forward's fp32 batch mean
 __global__ __launch_bounds__(kBT) void bn_bwd_stats(const float* __restrict__ gy, const float* __restrict__ x, int C,
                                                     int hw, int ncp, int nparts, int vec,
                                                     const float* __restrict__ mean, const float* __restrict__ invstd,
@@ -208,55 +218,66 @@ __global__ __launch_bounds__(kBT) void bn_bwd_stats(const float* __restrict__ gy
     load_chunk(gy + off, hw, j, vec != 0, g, ok);
     load_chunk(x + off, hw, j, vec != 0, v, ok);
     const float mu = mean[c], is = invstd[c], ga = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
-    float s = 0.f, sx = 0.f;
+    float s = 0.f, sx = 0.f, sd = 0.f;
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
-        const float xh = (v[k] - mu) * is;
-        const float gg = (relu && !(fmaf(xh, ga, bt) > 0.f)) ? 0.f : g[k];  // invalid: g = 0
+        const float d = v[k] - mu;
+        const float gg = (relu && !(fmaf(d * is, ga, bt) > 0.f)) ? 0.f : g[k];  // invalid: g = 0
         s += gg;
-        sx = fmaf(gg, xh, sx);
+        sx = fmaf(gg, d, sx);
+        sd += ok[k] ? d : 0.f;
     }
     s = block_sum(s, red);
     sx = block_sum(sx, red);
+    sd = block_sum(sd, red);
     if (threadIdx.x == 0) {
-        float* o = part + ((size_t)c * nparts + (size_t)b * ncp + j) * 2;
+        float* o = part + ((size_t)c * nparts + (size_t)b * ncp + j) * 3;
         o[0] = s;
         o[1] = sx;
+        o[2] = sd;
     }
 }
 
-__global__ __launch_bounds__(kBT) void bn_bwd_finalize(const float* __restrict__ part, int C, int nparts,
-                                                       float* __restrict__ sums, float* __restrict__ ggamma,
-                                                       float* __restrict__ gbeta) {
+// sums[c] = {s0, a, k} (double) with gx = gamma invstd (g' - s0 - (x - mean - delta) invstd s1) =
+// f (g' - k - a x): delta = sum (x - mean) / N (the exact mean's offset from the fp32 one), s0 =
+// sum g' / N, s1 = sum g' xhat / N with xhat about the exact mean, a = invstd s1, k = s0 - (mean +
+// delta) a; ggamma = sum g' xhat, gbeta = sum g'
+__global__ __launch_bounds__(kBT) void bn_bwd_finalize(const float* __restrict__ part, int C, int nparts, double n,
+                                                       const float* __restrict__ mean,
+                                                       const float* __restrict__ invstd, double* __restrict__ sums,
+                                                       float* __restrict__ ggamma, float* __restrict__ gbeta) {
     const int c = blockIdx.x;
-    double v[2];
-    chan_sums<2>(part + (size_t)c * nparts * 2, nparts, v);
+    double v[3];
+    chan_sums<3>(part + (size_t)c * nparts * 3, nparts, v);
     if (threadIdx.x == 0) {
-        sums[2 * c] = (float)v[0];
-        sums[2 * c + 1] = (float)v[1];
+        const double is = (double)invstd[c], delta = v[2] / n;
+        const double sxh = (v[1] - delta * v[0]) * is;  // sum g' xhat, xhat about the exact mean
+        const double s0 = v[0] / n, a = is * (sxh / n);
+        sums[3 * c] = s0;
+        sums[3 * c + 1] = a;
+        sums[3 * c + 2] = s0 - ((double)mean[c] + delta) * a;
         if (gbeta) gbeta[c] = (float)v[0];
-        if (ggamma) ggamma[c] = (float)v[1];
+        if (ggamma) ggamma[c] = (float)sxh;
     }
 }
 
 __global__ __launch_bounds__(kBT) void bn_bwd_apply(const float* __restrict__ gy, const float* __restrict__ x,
-                                                    float* __restrict__ gx, int C, int hw, int vec, float inv_n,
+                                                    float* __restrict__ gx, int C, int hw, int vec,
                                                     const float* __restrict__ mean, const float* __restrict__ invstd,
                                                     const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                    int relu, const float* __restrict__ sums) {
+                                                    int relu, const double* __restrict__ sums) {
     const int j = blockIdx.x, c = blockIdx.y, b = blockIdx.z;
     const size_t off = ((size_t)b * C + c) * hw;
     const float mu = mean[c], is = invstd[c], ga = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
-    const float s0 = sums[2 * c] * inv_n, s1 = sums[2 * c + 1] * inv_n, f = ga * is;
+    const double f = (double)ga * (double)is, a = sums[3 * c + 1], k0 = sums[3 * c + 2];
     float g[kPer], v[kPer];
     bool ok[kPer];
     load_chunk(gy + off, hw, j, vec != 0, g, ok);
     load_chunk(x + off, hw, j, vec != 0, v, ok);
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
-        const float xh = (v[k] - mu) * is;
-        const float gg = (relu && !(fmaf(xh, ga, bt) > 0.f)) ? 0.f : g[k];
-        v[k] = f * (gg - s0 - xh * s1);
+        const float gg = (relu && !(fmaf((v[k] - mu) * is, ga, bt) > 0.f)) ? 0.f : g[k];  // the forward's mask
+        v[k] = (float)(f * ((double)gg - k0 - a * (double)v[k]));
     }
     store_chunk(gx + off, hw, j, vec != 0, v);
 }
@@ -329,10 +350,13 @@ int launch_relu_bias_bwd(int B, int C, int H, int W, const float* g, const float
 // ------------------------------------------------------------------------------------------------
 static int bn_ncp(const nconv_bn_train& p) { return (p.H * p.W + kChunk - 1) / kChunk; }
 
-size_t bn_workspace_bytes(const nconv_bn_train& p) {
+// per-chunk partials (3 floats each), then the backward's per-channel sums (3 doubles, 8-B aligned)
+static size_t bn_sums_offset(const nconv_bn_train& p) {
     const size_t nparts = (size_t)p.B * bn_ncp(p);
-    return (nparts * p.C * 3 + 2 * (size_t)p.C) * sizeof(float);
+    return (nparts * p.C * 3 * sizeof(float) + 7) & ~(size_t)7;
 }
+
+size_t bn_workspace_bytes(const nconv_bn_train& p) { return bn_sums_offset(p) + 3 * (size_t)p.C * sizeof(double); }
 
 int launch_bn_train_fwd(const nconv_bn_train& p, float* ws, hipStream_t st, const char** why) {
     const int hw = p.H * p.W, ncp = bn_ncp(p), nparts = p.B * ncp;
@@ -355,15 +379,14 @@ int launch_bn_train_bwd(const nconv_bn_train& p, const float* gy, float* gx, flo
                         hipStream_t st, const char** why) {
     const int hw = p.H * p.W, ncp = bn_ncp(p), nparts = p.B * ncp;
     const int vec = (hw % 4 == 0) && ((uintptr_t)p.x % 16 == 0) && ((uintptr_t)gy % 16 == 0);
-    float* sums = ws + (size_t)nparts * p.C * 3;
+    double* sums = reinterpret_cast<double*>(reinterpret_cast<char*>(ws) + bn_sums_offset(p));
     hipLaunchKernelGGL(bn_bwd_stats, dim3(ncp, p.C, p.B), dim3(kBT), 0, st, gy, p.x, p.C, hw, ncp, nparts, vec, p.mean,
                        p.invstd, p.gamma, p.beta, p.relu, ws);
-    hipLaunchKernelGGL(bn_bwd_finalize, dim3(p.C), dim3(kBT), 0, st, ws, p.C, nparts, sums, ggamma,
-                       gbeta);
+    hipLaunchKernelGGL(bn_bwd_finalize, dim3(p.C), dim3(kBT), 0, st, ws, p.C, nparts, (double)((size_t)p.B * hw),
+                       p.mean, p.invstd, sums, ggamma, gbeta);
     if (gx)
         hipLaunchKernelGGL(bn_bwd_apply, dim3(ncp, p.C, p.B), dim3(kBT), 0, st, gy, p.x, gx, p.C, hw,
-                           vec && ((uintptr_t)gx % 16 == 0), 1.f / (float)((size_t)p.B * hw), p.mean, p.invstd,
-                           p.gamma, p.beta, p.relu, sums);
+                           vec && ((uintptr_t)gx % 16 == 0), p.mean, p.invstd, p.gamma, p.beta, p.relu, sums);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         *why = hipGetErrorString(e);

@@ -490,6 +490,16 @@ int nconv_conv3x3_c1(const float* x, int B, int Cin, int H, int W, const float* 
     return rc ? fail(rc, fn, why) : 0;
 }
 
+int nconv_bilinear_ac(const float* x, int B, int C, int H, int W, float* y, int Ho, int Wo, void* stream) {
+    const char* fn = "nconv_bilinear_ac";
+    if (!x || !y) return fail(-22, fn, "null pointer");
+    if (B < 0 || C < 0 || H <= 0 || W <= 0 || Ho <= 0 || Wo <= 0) return fail(-22, fn, "bad geometry");
+    if ((long long)H * W >= (1LL << 31) || (long long)B * C * Ho * Wo >= (1LL << 40)) return fail(-22, fn, "too large");
+    const char* why = nullptr;
+    int rc = nconv::launch_bilinear_ac(x, B, C, H, W, y, Ho, Wo, (hipStream_t)stream, &why);
+    return rc ? fail(rc, fn, why) : 0;
+}
+
 size_t nconv_depth_loss_workspace_bytes(int B, int H, int W) {
     if (B <= 0 || H <= 0 || W <= 0 || (long long)B * H * W > (1LL << 30)) return 0;
     return nconv::loss_workspace_bytes(B, H, W);

@@ -41,9 +41,14 @@ __device__ __forceinline__ float pool4(float v0, float v1, float v2, float v3, i
     return m;
 }
 
+// The pooled value alone (no argmax): the window's maximum, NaN if any element is NaN -- the value
+// max_pool2d returns, as two v_maximum3_f32 (IEEE 754-2019 maximum, NaN-propagating; gfx950)
+// instead of pool4's compare / select chain. Ties need no order for the value; the one difference
+// is the sign of a zero maximum (+0 where a window holds both -0 and +0 in that order), which no
+// consumer distinguishes (w * (+-0) terms leave a sum unchanged).
 __device__ __forceinline__ float pool4v(float v0, float v1, float v2, float v3) {
-    int a;
-    return pool4(v0, v1, v2, v3, a);
+    return __builtin_elementwise_maximum(__builtin_elementwise_maximum(v0, v1),
+                                         __builtin_elementwise_maximum(v2, v3));
 }
 
 // Cross-lane reads without the LDS crossbar (ds_bpermute): xor 1 by a DPP quad permutation,

@@ -201,17 +201,28 @@ __global__ __launch_bounds__(NTH) void fwd_tiled(LayerDev d, float* __restrict__
                 if constexpr (C::P == 1) {  // the window's right column sits in lane l^1
                     const float ya = shfl_xor1(yv[0]), ca = shfl_xor1(cv[0]);
                     const float yd = shfl_xor1(yb[0]), cd = shfl_xor1(cb[0]);
-                    int ay, ac;
-                    st_f32(rpy, po[0], pool4(yv[0], ya, yb[0], yd, ay));
-                    st_f32(rpc, po[0], pool4(cv[0], ca, cb[0], cd, ac));
-                    if (parg && po[0] != OOB) parg[po[0] >> 2] = (unsigned)(ay | (ac << 2));
-                } else {
+                    if (parg) {  // (uniform) training: the first maximum's slot too
+                        int ay, ac;
+                        st_f32(rpy, po[0], pool4(yv[0], ya, yb[0], yd, ay));
+                        st_f32(rpc, po[0], pool4(cv[0], ca, cb[0], cd, ac));
+                        if (po[0] != OOB) parg[po[0] >> 2] = (unsigned)(ay | (ac << 2));
+                    } else {
+                        st_f32(rpy, po[0], pool4v(yv[0], ya, yb[0], yd));
+                        st_f32(rpc, po[0], pool4v(cv[0], ca, cb[0], cd));
+                    }
+                } else if (parg) {
 #pragma unroll
                     for (int h = 0; h < C::P / 2; ++h) {
                         int ay, ac;
                         st_f32(rpy, po[h], pool4(yv[2 * h], yv[2 * h + 1], yb[2 * h], yb[2 * h + 1], ay));
                         st_f32(rpc, po[h], pool4(cv[2 * h], cv[2 * h + 1], cb[2 * h], cb[2 * h + 1], ac));
-                        if (parg && po[h] != OOB) parg[po[h] >> 2] = (unsigned)(ay | (ac << 2));
+                        if (po[h] != OOB) parg[po[h] >> 2] = (unsigned)(ay | (ac << 2));
+                    }
+                } else {
+#pragma unroll
+                    for (int h = 0; h < C::P / 2; ++h) {
+                        st_f32(rpy, po[h], pool4v(yv[2 * h], yv[2 * h + 1], yb[2 * h], yb[2 * h + 1]));
+                        st_f32(rpc, po[h], pool4v(cv[2 * h], cv[2 * h + 1], cb[2 * h], cb[2 * h + 1]));
                     }
                 }
             }

@@ -33,6 +33,7 @@ constexpr int kHH = kHTH + 4, kHW = kHTW + 4;     // nconv1 outputs nconv2 reads
 constexpr int kHP = kHW - 16;                     // halo pair slots per row: (c, c + 16), c < 20
 constexpr int kCP = kSW - 16;                     // mask pair slots per row: c < 24
 constexpr int kHPlane = kHH * kHP;                // f2 per halo pair plane
+constexpr int kHPS = kHPlane + 1;                 // plane stride: each plane ends in its own dump slot
 constexpr int kW21 = 9 * 8 * 9;                   // composed weights, then W2 as [ci][kh][kw][o]
 
 typedef const float __attribute__((address_space(4))) cfloat;
@@ -48,11 +49,11 @@ __global__ __launch_bounds__(kHT) void fwd_head_exact(LayerDev d2, TailArgs t, f
     // masks, and one region holding first the mask pairs of the interior D2, then nconv1's
     // x * c (or, in edge tiles, c) as 8 planes of column pairs
     __shared__ __attribute__((aligned(16))) float sx[kSH * kSW];
-    __shared__ __attribute__((aligned(16))) f2 hp[8 * kHPlane + 1];  // + dump slot
+    __shared__ __attribute__((aligned(16))) f2 hp[8 * kHPS];  // 8 pair planes, each + a dump slot
     __shared__ __attribute__((aligned(16))) float w1t[25 * 8];       // nconv1 weights [tap][o]
     __shared__ unsigned long long rowmask[kSH];
     f2* const c0p = hp;  // {c0(c), c0(c + 16)}, kSH x kCP, until the interior D2 is done
-    static_assert(kSH * kCP <= 8 * kHPlane, "mask pairs fit the plane region");
+    static_assert(kSH * kCP <= 8 * kHPS, "mask pairs fit the plane region");
     const int tid = threadIdx.x;
     const int H = L.Ho, W = L.Wo;
     const TileCoord tc = xcd_tile((W + kHTW - 1) / kHTW, (H + kHTH - 1) / kHTH, L.B);
@@ -163,29 +164,30 @@ __global__ __launch_bounds__(kHT) void fwd_head_exact(LayerDev d2, TailArgs t, f
 #pragma unroll
                 for (int o = 0; o < 8; ++o) acc[o] = __builtin_elementwise_fma((f2){wv[o], wv[o]}, v, acc[o]);
             }
-            // float offsets of this pixel in a pair plane (.x of pair c, .y of pair c - 16), or
-            // the dump slot: every lane stores, no branches
-            const int dump = 8 * kHPlane * 2;
-            const int h0 = (valid && c < kHP) ? (r * kHP + c) * 2 : dump;
-            const int h1 = (valid && c >= 16) ? (r * kHP + c - 16) * 2 + 1 : dump;
+            // float offsets of this pixel in a pair plane (.x of pair c, .y of pair c - 16), or the
+            // plane's own dump slot: every lane stores, no branches, and the channel's plane is a
+            // constant offset (the LDS store's immediate)
+            const int h0 = (valid && c < kHP) ? (r * kHP + c) * 2 : kHPlane * 2;
+            const int h1 = (valid && c >= 16) ? (r * kHP + c - 16) * 2 + 1 : kHPlane * 2 + 1;
+            float* const p0 = reinterpret_cast<float*>(hp) + h0;
+            float* const p1 = reinterpret_cast<float*>(hp) + h1;
             // TR: the tile's own pixels (halo rows / columns 2 .. 17 / 2 .. 33) to nconv1's outputs
             const unsigned own = (TR && !want_c && in && (unsigned)(r - 2) < (unsigned)kHTH &&
                                   (unsigned)(c - 2) < (unsigned)kHTW) ? (unsigned)(gr * W + gc) * 4u : 0x80000000u;
 #pragma unroll
             for (int o = 0; o < 8; ++o) {
+                // outside the image no tap was visited (m = 0): N = D = 0, so cout = 0 and
+                // y * cout = b1 * 0 = +-0 -- nconv2's zero padding without a select
                 float y1, cc1;
                 nconv_epilogue(acc[o].x, acc[o].y, t.eps1, t.b1[o], t.s1[o], y1, cc1);
-                y1 = in ? y1 : 0.f;  // nconv2's zero padding outside the image
-                cc1 = in ? cc1 : 0.f;
                 if constexpr (TR) {
                     const size_t po1 = ((size_t)b * 8 + o) * H * W;
                     st_f32(plane_rsrc(t.y1 + po1, H * W * 4), own, y1);
                     st_f32(plane_rsrc(t.c1 + po1, H * W * 4), own, cc1);
                 }
                 const float v = want_c ? cc1 : y1 * cc1;  // nconv2's staged x * c, or c
-                float* pl = reinterpret_cast<float*>(hp + o * kHPlane);
-                pl[h0 - (h0 == dump ? o * kHPlane * 2 : 0)] = v;
-                pl[h1 - (h1 == dump ? o * kHPlane * 2 : 0)] = v;
+                p0[o * kHPS * 2] = v;
+                p1[o * kHPS * 2] = v;
             }
         }
     };
@@ -199,7 +201,7 @@ __global__ __launch_bounds__(kHT) void fwd_head_exact(LayerDev d2, TailArgs t, f
     auto sum_planes = [&](f2 (&acc)[8]) {
 #pragma unroll 1
         for (int ci = 0; ci < 8; ++ci) {
-            const f2* row = hp + ci * kHPlane + ty * kHP + j;
+            const f2* row = hp + ci * kHPS + ty * kHP + j;
             const cfloat* wr = w2t + ci * 200;
 #pragma unroll 1
             for (int kh = 0; kh < 5; ++kh, row += kHP, wr += 40) {
@@ -267,12 +269,16 @@ __global__ __launch_bounds__(kHT) void fwd_head_exact(LayerDev d2, TailArgs t, f
             // window (r, c) (r, c+1) (r+1, c) (r+1, c+1): lanes l, l^1, l^16, l^17 (torch order)
             const float yb = shfl_xor16(yv[h]), cb = shfl_xor16(cv[h]);
             const float ya = shfl_xor1(yv[h]), yd = shfl_xor1(yb), ca = shfl_xor1(cv[h]), cd = shfl_xor1(cb);
-            int ay, ac;
-            st_f32(rpy, po[h], pool4(yv[h], ya, yb, yd, ay));
-            st_f32(rpc, po[h], pool4(cv[h], ca, cb, cd, ac));
-            if constexpr (TR)
+            if constexpr (TR) {  // the first maximum's slot too (the backward's routing)
+                int ay, ac;
+                st_f32(rpy, po[h], pool4(yv[h], ya, yb, yd, ay));
+                st_f32(rpc, po[h], pool4(cv[h], ca, cb, cd, ac));
                 st_f32(plane_rsrc((const float*)(t.parg + pofs), ppbytes), po[h],
                        __builtin_bit_cast(float, (unsigned)(ay | (ac << 2))));
+            } else {
+                st_f32(rpy, po[h], pool4v(yv[h], ya, yb, yd));
+                st_f32(rpc, po[h], pool4v(cv[h], ca, cb, cd));
+            }
         }
     }
 }

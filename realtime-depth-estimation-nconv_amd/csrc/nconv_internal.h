@@ -134,6 +134,8 @@ size_t dense_packed_floats(int kind, int Cin, int Cout);
 int launch_dense_pack(int kind, int Cin, int Cout, const float* w, const float* scale, float* wp, hipStream_t st,
                       const char** why);
 int launch_dense_conv(const nconv_dense_conv& p, hipStream_t st, const char** why);
+int launch_bilinear_ac(const float* x, int B, int C, int H, int W, float* y, int Ho, int Wo, hipStream_t st,
+                       const char** why);
 int launch_conv3x3_c1(const float* x, int B, int Cin, int H, int W, const float* w, const float* res, float* out,
                       hipStream_t st, const char** why);
 size_t dense_wgrad_workspace_bytes(const nconv_dense_wgrad& g);

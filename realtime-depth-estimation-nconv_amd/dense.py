@@ -12,6 +12,7 @@ Host side of nconv_dense_conv_fwd / nconv_dense_pack / nconv_conv3x3_c1 / nconv_
     on libnconv's nconv_bn_train_* / nconv_relu_bias_bwd kernels (bn_relu).
 """
 import ctypes
+import math
 
 import torch
 
@@ -73,6 +74,24 @@ def conv(x0, kind, stride, wpack, bias, relu, cout, x1=None, wshort=None, out=No
     d.out, d.out_C, d.out_c0 = out.data_ptr(), out.shape[1], out_c0
     _lib.check(_lib.lib().nconv_dense_conv_fwd(ctypes.byref(d), _lib.stream_handle(x0.device)),
                "nconv_dense_conv_fwd")
+    return out
+
+
+def bilinear_down(x, k):
+    """F.interpolate(x, scale_factor=1/k, mode="bilinear", align_corners=True) (models/step2.py:249,
+    277) on libnconv's nconv_bilinear_ac, whose sampling arithmetic is the reference CPU kernel's
+    (fp32 positions: PyTorch-ROCm's own kernel samples KITTI's last column elsewhere, include/nconv.h).
+    Output size floor(H / k) x floor(W / k) as F.interpolate's. A tensor that records autograd (step 1
+    frozen in SETP2, so never on the model's path) goes through F.interpolate for its backward."""
+    if torch.is_grad_enabled() and x.requires_grad:
+        return torch.nn.functional.interpolate(x, scale_factor=1 / k, mode="bilinear", align_corners=True)
+    x = x.contiguous()
+    B, C, H, W = x.shape
+    Ho, Wo = int(math.floor(H * (1.0 / k))), int(math.floor(W * (1.0 / k)))
+    out = torch.empty((B, C, Ho, Wo), device=x.device, dtype=torch.float32)
+    if out.numel():
+        _lib.check(_lib.lib().nconv_bilinear_ac(_lib.ptr(x), B, C, H, W, _lib.ptr(out), Ho, Wo,
+                                                _lib.stream_handle(x.device)), "nconv_bilinear_ac")
     return out
 
 

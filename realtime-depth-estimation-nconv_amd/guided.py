@@ -15,7 +15,8 @@ Training (or any forward that records autograd) on the device: every convolution
 dense.DenseConvFn / dense.HeadFn — forward, input gradient and weight gradient on the same MFMA
 kernels, ReLU after a bias-only convolution fused, torch.cat replaced by two-source loads — and
 training-mode BatchNorm (batch statistics, running-stat updates) + ReLU on libnconv's BN kernels
-(dense.bn_relu); only the bilinear depth downsampling (F.interpolate) stays a PyTorch-ROCm op.
+(dense.bn_relu); the bilinear depth downsampling on nconv_bilinear_ac (the reference CPU kernel's
+sampling arithmetic, dense.bilinear_down).
 `model.dense_kernels = False` runs the dense layers as the plain torch modules — the fp32
 PyTorch reference the GPU tests compare the kernels against (tests/test_gpu_dense.py), not a
 product path (step 1 still runs on libnconv and refuses CPU tensors).
@@ -252,14 +253,13 @@ class FusionResolutionBlock(nn.Module):
 
     def dense_forward(self, rgb, depth, depth_last_step, fusion_festure):
         fout = self.upcat.dense_forward(rgb, fusion_festure, depth_last_step)
-        depth = F.interpolate(depth, scale_factor=1 / self.downsample_factor, mode="bilinear",
-                              align_corners=True).contiguous()
+        depth = D.bilinear_down(depth, self.downsample_factor)
         fout = self.fuse.dense_forward(fout, depth)
         return fout, D.conv3x3_c1(fout, self.conv.weight, depth)
 
     def train_forward(self, rgb, depth, depth_last_step, fusion_festure):
         fout = self.upcat.train_forward(rgb, fusion_festure, depth_last_step)
-        depth = F.interpolate(depth, scale_factor=1 / self.downsample_factor, mode="bilinear", align_corners=True)
+        depth = D.bilinear_down(depth, self.downsample_factor)
         fout = self.fuse.train_forward(fout, depth)
         return fout, D.head_fn(fout, self.conv.weight, depth)
 
@@ -279,13 +279,12 @@ class FusionResolution0(nn.Module):
         return fout, depth + self.conv(fout)
 
     def dense_forward(self, rgb, depth):
-        depth = F.interpolate(depth, scale_factor=1 / self.downsample_factor, mode="bilinear",
-                              align_corners=True).contiguous()
+        depth = D.bilinear_down(depth, self.downsample_factor)
         fout = self.fuse.dense_forward(rgb, depth)
         return fout, D.conv3x3_c1(fout, self.conv.weight, depth)
 
     def train_forward(self, rgb, depth):
-        depth = F.interpolate(depth, scale_factor=1 / self.downsample_factor, mode="bilinear", align_corners=True)
+        depth = D.bilinear_down(depth, self.downsample_factor)
         fout = self.fuse.train_forward(rgb, depth)
         return fout, D.head_fn(fout, self.conv.weight, depth)
 

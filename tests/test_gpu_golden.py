@@ -119,9 +119,10 @@ def test_f3_two_training_steps(nconv_amd, gpu, fixture, full_batch, strict):
     of ~129 k pooled windows lie within 1e-5 of a tie: all 18 gradient tensors of both steps are
     held to 1e-3 there, no layer excepted. Weights: 1e-4
     relative + 1e-5, except elements whose reference gradient is below 1e-3 of its tensor's
-    largest: AdamW's first steps divide by sqrt(v) ~ |g|, so there the update amplifies the
-    gradient's rounding difference (bounded by 2 lr; the element is printed and carried to the next
-    step's check)."""
+    largest or close enough to AdamW's eps that a gradient difference inside the 1e-3 bound moves
+    the update by more than that: AdamW's first steps divide by sqrt(v) ~ |g|, so there the update
+    amplifies the gradient's rounding difference (bounded by 2 lr; the element is printed and
+    carried to the next step's check)."""
     f = load(fixture)
     net = _setp1_from(nconv_amd, gpu, f, prefix="init_")
     lr = 1e-2
@@ -156,8 +157,15 @@ def test_f3_two_training_steps(nconv_amd, gpu, fixture, full_batch, strict):
             rel = normwise(prm.grad, g_ref)
             report.append(f"step {step} {k} grad: {rel:.2e}")
             assert rel <= 1e-2 and (rel <= 1e-3 or (not strict and _pool_sensitive(k))), report[-1]
+            # AdamW's first update is lr g / (|g| + eps), eps = 1e-8: its sensitivity to the gradient
+            # is lr eps / (|g| + eps)^2, so a gradient difference inside the 1e-3 normwise bound
+            # moves the update by more than the weight tolerance wherever |g| is small, relatively
+            # (<= 1e-3 of the tensor's largest) or absolutely (near eps: layers whose gradients are
+            # all ~1e-6, e.g. nconv4's in f10 / f11)
+            gmax = g_ref.abs().max()
+            sens = lr * 1e-8 * (1e-3 * gmax) / (g_ref.abs() + 1e-8) ** 2
             ill[k] = ill.get(k, torch.zeros(g_ref.shape, dtype=torch.bool)) | \
-                (g_ref.abs() <= 1e-3 * g_ref.abs().max())
+                (g_ref.abs() <= 1e-3 * gmax) | (sens > 1e-5)
         opt.step()
         for k, prm in named.items():
             if "bnorm" not in k:
