@@ -54,23 +54,43 @@ def test_guided_generalized_crop_vs_oracle(nconv_amd, gpu, H, W):
         _close(g1[i], r1[i], f"pair1 scale {i}")
 
 
+def _tol64(k):
+    """Normwise gradient bound against the float64 oracle: 2e-3, and 5e-3 for the four RGB-encoder
+    convolutions (each feeds training-mode BatchNorm on inputs of large mean: the most
+    ill-conditioned gradients of the chain; the reference's own fp32 CPU values of these lie up to
+    2.7e-3 from float64 at 480x640, golden f9)."""
+    return 5e-3 if k.startswith("rgb_encoder") and k.endswith("encoder.0.weight") else 2e-3
+
+
+@pytest.mark.timeout(400)
 def test_guided_training_iteration_matches_reference_f9(nconv_amd, gpu):
     """Golden f9: one SETP2_BP_TRAIN iteration of train_step2.py:60-66 as the reference ran it
     (train mode: frozen step 1 with its EnforcePos drift, batch-statistics BatchNorm; model(rgb,
     depth, rgb, depth); calculate_loss_multi_resolution without the gradient loss; backward) on the
-    GPU path. Outputs |gpu - ref| <= 1e-4*|ref| + 1e-3, loss 1e-5 relative, every trainable gradient
-    normwise 1e-3, BatchNorm running statistics after the step 1e-4 relative +
-    1e-5, num_batches_tracked exact."""
+    GPU path, against the reference's own numbers and the float64 oracle of the same iteration.
+
+    Outputs |gpu - ref| <= 1e-4*|ref| + 1e-3, loss 1e-5 relative, BatchNorm running statistics after
+    the step 1e-4 relative + 1e-5, num_batches_tracked exact. Gradients, normwise: within 2e-3 of the
+    float64 oracle (5e-3 for the RGB-encoder convolutions, _tol64) and that + 1e-3 of the reference.
+    Why not 1e-3 here (it holds for every step-1 gradient,
+    tests/test_gpu_golden.py): this chain is ~20 convolution / training-mode BatchNorm layers deep,
+    and a convolution that feeds training-mode BatchNorm has a gradient that is a small difference of
+    large terms (BatchNorm removes the component along the channel mean; condition ~360 for the RGB
+    encoder on 0..255 input), so fp32 rounding anywhere upstream shows there amplified: the
+    reference's own fp32 CPU gradients of the four RGB-encoder convolutions lie 1.5-2.7e-3 from the
+    float64 values, and PyTorch-ROCm's MIOpen and native paths land up to 2.7e-3 away on other
+    tensors of this chain (tools/f9_dump.py). The bound is that spread."""
     import os
     from guided_cases import f9_inputs, grad_rel, trainable_setp2
     f = np.load(os.path.join(os.path.dirname(__file__), "golden", "f9_guided_train.npz"))
     model = f5_models(nconv_amd).to(gpu)
+    sd0 = {k: v.detach().double().cpu().clone() for k, v in model.state_dict().items()}
     opt = nconv_amd.train.get_optimizer(model, "adam", 1e-4, 1e-7)
-    rgb, depth, gt = (t.to(gpu) for t in f9_inputs())
+    rgb, depth, gt = f9_inputs()
     model.train()
     opt.zero_grad()
-    est, est1 = model(rgb, depth, rgb, depth)
-    loss = nconv_amd.train.calculate_loss_multi_resolution(est, gt, False)
+    est, est1 = model(rgb.to(gpu), depth.to(gpu), rgb.to(gpu), depth.to(gpu))
+    loss = nconv_amd.train.calculate_loss_multi_resolution(est, gt.to(gpu), False)
     loss.backward()
     torch.cuda.synchronize()
     ref_loss = float(f["loss"])
@@ -82,19 +102,35 @@ def test_guided_training_iteration_matches_reference_f9(nconv_amd, gpu):
     names = trainable_setp2(None, named.items())
     assert set(k[5:] for k in f.files if k.startswith("grad_")) == set(names)
     refs = {k: torch.from_numpy(f["grad_" + k]).double() for k in names}
-    report = [(k, grad_rel(named[k].grad.double().cpu(), refs[k], k, refs)) for k in names]
-    print("\n".join(f"{k}: {r:.2e}" for k, r in report))
-    bad = [f"{k}: {r:.2e}" for k, r in report if r > 1e-3]
+    # the float64 oracle of the same iteration (step 1 with this forward's EnforcePos drift)
+    sd = dict(sd0)
+    p1 = R.dnet_params_from_state_dict({k: (R.softplus_pos(v) if k.endswith(".weight") and "bnorm" not in k else v)
+                                        for k, v in sd.items()}, "step1.d_net.")
+    leaves = {k: sd[k].clone().requires_grad_(True) for k in names}
+    sd.update(leaves)
+    o0, _ = R.setp2_forward(sd, rgb.double(), depth.double(), rgb.double(), depth.double(), "literal", "train",
+                            training=True, step1_params=p1)
+    R.calculate_loss_multi_resolution(o0, gt.double(), False).backward()
+    g64 = {k: leaves[k].grad for k in names}
+    report, bad = [], []
+    for k in names:
+        got = named[k].grad.double().cpu()
+        e64, eref, ref64 = grad_rel(got, g64[k], k, g64), grad_rel(got, refs[k], k, refs), grad_rel(refs[k], g64[k], k, g64)
+        report.append(f"{k}: vs fp64 {e64:.2e}, vs reference {eref:.2e} (reference vs fp64 {ref64:.2e})")
+        if e64 > _tol64(k) or eref > _tol64(k) + 1e-3:
+            bad.append(report[-1])
+    print("\n".join(report))
+    print(f"{sum(1 for r in report if float(r.split('vs fp64 ')[1][:8]) <= 1e-3)} of {len(names)} within 1e-3 of fp64")
     assert not bad, "\n".join(bad)
     opt.step()
-    sd = model.state_dict()
+    sd1 = model.state_dict()
     for k in f.files:
         if k.startswith("bn_") and "running_" in k:
-            _bn = sd[k[3:]].double().cpu()
+            _bn = sd1[k[3:]].double().cpu()
             ref = torch.from_numpy(f[k]).double()
             assert ((_bn - ref).abs() <= 1e-4 * ref.abs() + 1e-5).all(), k
         elif k.startswith("bn_"):
-            assert int(sd[k[3:]]) == int(f[k]), k
+            assert int(sd1[k[3:]]) == int(f[k]), k
 
 
 def _kitti_model(nconv_amd, gpu, seed=2):
@@ -132,18 +168,20 @@ def test_guided_config3_full_size_vs_oracle(nconv_amd, gpu):
     _close(e0, z, "export frame 0")
 
 
+@pytest.mark.timeout(400)
 def test_guided_config4_full_size_training_vs_oracle(nconv_amd, gpu):
     """Config 4's per-GPU training step at its own frame size: 1+1 frames of 352x1216, train mode
     (batch-statistics BatchNorm, frozen drifted step 1), calculate_loss_multi_resolution (MSE),
-    backward: every trainable gradient normwise 1e-3 against the oracle evaluated with the
-    reference's own fp32 CPU ops (float64 at this size takes minutes on the box's host)."""
+    backward: every trainable gradient normwise within 2e-3 of the float64 oracle (5e-3 for the
+    RGB-encoder convolutions: the fp32 spread of this deep BatchNorm chain, see the f9 test),
+    outputs 1e-4 |ref| + 1e-3."""
     from guided_cases import grad_rel, trainable_setp2
     model = _kitti_model(nconv_amd, gpu, seed=4)
     H, W = 352, 1216
     rgb0, d0, rgb1, d1 = f5_inputs(H, W)
     g = torch.Generator().manual_seed(12)
     gt = (torch.rand(1, 1, 480, 640, generator=g) * 79 + 1) * (torch.rand(1, 1, 480, 640, generator=g) < 0.5)
-    sd = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
+    sd = {k: v.detach().double().cpu().clone() for k, v in model.state_dict().items()}
     model.train()
     est, _ = model(rgb0.to(gpu), d0.to(gpu), rgb1.to(gpu), d1.to(gpu))
     loss = nconv_amd.train.calculate_loss_multi_resolution(est, gt.to(gpu), False)
@@ -155,12 +193,15 @@ def test_guided_config4_full_size_training_vs_oracle(nconv_amd, gpu):
     names = trainable_setp2(None, named.items())
     leaves = {k: sd[k].clone().requires_grad_(True) for k in names}
     sd.update(leaves)
-    r0, _ = R.setp2_forward(sd, rgb0, d0, rgb1, d1, "generalized", "train", training=True, step1_params=p1)
-    ref_loss = R.calculate_loss_multi_resolution(r0, gt, False)
+    r0, _ = R.setp2_forward(sd, rgb0.double(), d0.double(), rgb1.double(), d1.double(), "generalized", "train",
+                            training=True, step1_params=p1)
+    ref_loss = R.calculate_loss_multi_resolution(r0, gt.double(), False)
     ref_loss.backward()
     assert abs(loss.item() - ref_loss.item()) <= 1e-4 * abs(ref_loss.item())
     for i in range(4):
         _close(est[i].detach(), r0[i].detach(), f"scale {i}")
-    refs = {k: leaves[k].grad.double() for k in names}
-    bad = [f"{k}: {r:.2e}" for k in names if (r := grad_rel(named[k].grad.double().cpu(), refs[k], k, refs)) > 1e-3]
+    refs = {k: leaves[k].grad for k in names}
+    rel = {k: grad_rel(named[k].grad.double().cpu(), refs[k], k, refs) for k in names}
+    print("\n".join(f"{k}: {r:.2e}" for k, r in rel.items()))
+    bad = [f"{k}: {r:.2e}" for k, r in rel.items() if r > _tol64(k)]
     assert not bad, "\n".join(bad)
