@@ -155,7 +155,9 @@ int nconv_fwd_pooled(const nconv_layer* L, float* y, float* cout, float* y_pool,
  *  - NCONV_MATH_FP32: exact fp32 (nconv_fwd_head.hip). nconv1 visits only the nonzero taps of each
  *    window (bitwise its dense sums); nconv2's confidence mass D2 is the 9x9 convolution of the
  *    binary mask c0 with the composed weights sum_i W2[o,i] (x) W1[i] / s1[i] that L2->waux must
- *    hold (nconv_head_weights), except in tiles whose window nconv2's zero padding truncates;
+ *    hold (nconv_head_weights), on the bf16 matrix cores with exact products (c0 is 0 or 1, each
+ *    weight the exact sum of three bf16 parts) and fp32 accumulation, except in tiles whose window
+ *    nconv2's zero padding truncates;
  *  - NCONV_MATH_BF16X3 / BF16X9: the matrix-core head (nconv1 uses the same split).
  * Training (exact fp32 only; all three or NULL): y1, cout1 (B, 8, H, W) receive nconv1's outputs
  * (bitwise nconv_fwd's: the nonzero-tap sums are the dense sums) for the backward, argmax the
@@ -163,12 +165,15 @@ int nconv_fwd_pooled(const nconv_layer* L, float* y, float* cout, float* y_pool,
 int nconv_fwd_head(const nconv_layer* L1, const nconv_layer* L2, float* y, float* cout, float* y_pool,
                    float* cout_pool, unsigned int* argmax, float* y1, float* cout1, void* stream);
 
-/* Auxiliary weights of the exact fused head (L2->waux of nconv_fwd_head): w21 receives 2248 floats,
- * the composed confidence weights w21[(qh * 8 + o) * 9 + qw] = sum_i (1 / s1[i]) sum
- * W2[o][i][kh][kw] W1[i][kh'][kw'] over kh + kh' = qh, kw + kw' = qw (fp64, rounded once; s1 =
- * L1->wsum), then nconv2's weights transposed to [i][kh][kw][o] (1600 floats). nconv1's cout = D1 / s1
+/* Auxiliary weights of the exact fused head (L2->waux of nconv_fwd_head): w21 receives
+ * NCONV_HEAD_WEIGHTS_FLOATS floats. First the composed confidence weights W21[o][qh][qw] = sum_i
+ * (1 / s1[i]) sum W2[o][i][kh][kw] W1[i][kh'][kw'] over kh + kh' = qh, kw + kw' = qw (fp64, rounded
+ * once to fp32; s1 = L1->wsum), each split exactly into three bf16 parts and laid out as the A
+ * operands of the head's matrix-core D2 (1536 dwords, nconv_fwd_head.hip kFrag), then nconv2's
+ * weights transposed to [i][kh][kw][o] (1600 floats). nconv1's cout = D1 / s1
  * (models/step1.py:141-147), so nconv2's D2 = sum_i W2[o,i] * c1[i] = W21[o] * c0 wherever nconv2's
  * window is not truncated by its zero padding. Call after nconv_weight_prep. */
+#define NCONV_HEAD_WEIGHTS_FLOATS 3136
 int nconv_head_weights(const nconv_layer* L1, const nconv_layer* L2, float* w21, void* stream);
 
 /* Fused tail: the last 3x3 NConv (nconv6, step1.py:88-90) with its 1x1 successor (nconv7,

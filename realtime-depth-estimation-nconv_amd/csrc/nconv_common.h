@@ -64,6 +64,17 @@ __device__ __forceinline__ float shfl_xor16(float v) {
 }
 __device__ __forceinline__ float shfl_xor17(float v) { return shfl_xor1(shfl_xor16(v)); }
 
+// Vertical 2x2-pool pairs of two values at once: v_permlane16_swap(a, b) swaps a's odd 16-lane rows
+// with b's even rows, leaving {a0, b0, a2, b2} and {a1, b1, a3, b3}; their maximum is a's row-pair
+// maximum in the even rows and b's in the odd rows (IEEE maximum: NaN wins, order-free). The
+// results are copied out of the builtin's vector before the bit casts: hipcc (ROCm 7.2) lowers
+// __builtin_bit_cast of an element of that vector to element 0 whatever the index.
+__device__ __forceinline__ float pair_rows_max(float a, float b) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(int, a), __builtin_bit_cast(int, b), false, false);
+    const int r0 = r[0], r1 = r[1];
+    return __builtin_elementwise_maximum(__builtin_bit_cast(float, r0), __builtin_bit_cast(float, r1));
+}
+
 __device__ __forceinline__ size_t plane_idx(int b, int c, int C, int H, int W, int h, int w) {
     return (((size_t)b * C + c) * H + h) * (size_t)W + w;
 }

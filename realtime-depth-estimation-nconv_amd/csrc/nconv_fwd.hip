@@ -174,10 +174,17 @@ __global__ __launch_bounds__(NTH) void fwd_tiled(LayerDev d, float* __restrict__
         const int ppbytes = (int)(pplane * 4);
         const int pr = oh >> 1, pc0 = ow >> 1;
         const bool pool_row = pool && ((ty & 1) == 0) && pr < Hp;
-        unsigned po[C::P > 1 ? C::P / 2 : 1];
+        constexpr int NPO = C::P > 1 ? C::P / 2 : 1;
+        // po: the window's top-left lane (training, P = 1); pcy / pcc (inference, P even): the pooled
+        // y leaves from the even rows, the pooled cout from the odd rows (see the epilogue)
+        unsigned po[NPO], pcy[NPO], pcc[NPO];
 #pragma unroll
-        for (int h = 0; h < (C::P > 1 ? C::P / 2 : 1); ++h)
+        for (int h = 0; h < NPO; ++h) {
             po[h] = (pool_row && pc0 + h < Wp && (C::P > 1 || (lt & 1) == 0)) ? (unsigned)(pr * Wp + pc0 + h) * 4u : OOB;
+            const unsigned pp = (pool && pr < Hp && pc0 + h < Wp) ? (unsigned)(pr * Wp + pc0 + h) * 4u : OOB;
+            pcy[h] = (ty & 1) == 0 ? pp : OOB;
+            pcc[h] = (ty & 1) ? pp : OOB;
+        }
 #pragma unroll
         for (int oo = 0; oo < CO; ++oo) {
             const int o = og * CO + oo;
@@ -185,7 +192,23 @@ __global__ __launch_bounds__(NTH) void fwd_tiled(LayerDev d, float* __restrict__
             float yv[C::P], cv[C::P];
 #pragma unroll
             for (int j = 0; j < C::P; ++j) nconv_epilogue(acc[oo][j].x, acc[oo][j].y, L.eps, bo, s, yv[j], cv[j]);
-            if (pool) {  // every lane joins the shuffles
+            if (C::P % 2 == 0 && pool && !t.parg) {  // (uniform) inference pooled copy, every lane joins
+                // one v_permlane16_swap of (y, cout) per column leaves rows {y0, c0, y2, c2} and
+                // {y1, c1, y3, c3} (rows oh, oh^1 in lanes l, l^16), so their maximum is y's vertical
+                // pair maximum in the even rows and cout's in the odd rows; the columns are the lane's
+                const size_t pofs = ((size_t)b * COUT + o) * pplane;
+                const __amdgpu_buffer_rsrc_t rpy = plane_rsrc(t.py + pofs, ppbytes);
+                const __amdgpu_buffer_rsrc_t rpc = plane_rsrc(t.pc + pofs, ppbytes);
+                float vm[C::P];
+#pragma unroll
+                for (int j = 0; j < C::P; ++j) vm[j] = pair_rows_max(yv[j], cv[j]);
+#pragma unroll
+                for (int h = 0; h < C::P / 2; ++h) {
+                    const float pm = __builtin_elementwise_maximum(vm[2 * h], vm[2 * h + 1]);
+                    st_f32(rpy, pcy[h], pm);
+                    st_f32(rpc, pcc[h], pm);
+                }
+            } else if (pool) {  // every lane joins the shuffles
                 float yb[C::P], cb[C::P];
 #pragma unroll
                 for (int j = 0; j < C::P; ++j) {

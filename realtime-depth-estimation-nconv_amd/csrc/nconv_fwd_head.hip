@@ -14,11 +14,15 @@
 //  3. nconv2's confidence mass D2 = sum_i W2[o,i] * (W1[i] * c0) / s1[i] (nconv1's cout = D1 / s1,
 //     step1.py:141-147) is one 9x9 convolution of the binary mask c0 with the composed weights
 //     W21[o] = sum_i W2[o,i] (x) W1[i] / s1[i] (nconv_head_weights: fp64, rounded once): 81 taps
-//     instead of 8 x 25. All terms are non-negative (softplus weights, c0 in {0, 1}), so the
-//     regrouping keeps the error inside the fp32 bound of the sum, and D2 is exactly 0 where the
-//     reference's is (no sample in the 9x9 window). Only where nconv2's zero padding truncates its
-//     window (tiles within 2 px of the image edge) is the composition not a plain convolution;
-//     those tiles sum W2 * c1 from nconv1's c1 as the unfused path does.
+//     instead of 8 x 25, and it runs on the bf16 matrix cores without leaving fp32: c0 is 0 or 1
+//     (exact in bf16) and each fp32 W21 is the exact sum of three bf16 parts (hi, mid, lo: 8
+//     significand bits each), so every product is exact and v_mfma_f32_16x16x32_bf16 accumulates
+//     the three part sums in fp32, added in the epilogue. All terms are non-negative (softplus
+//     weights), so the regrouping keeps the error inside the fp32 bound of the sum, and D2 is
+//     exactly 0 where the reference's is (no sample in the 9x9 window). The matrix cores take the
+//     work off the vector ALU, which the rest of the kernel keeps busy. Only where nconv2's zero
+//     padding truncates its window (tiles within 2 px of the image edge) is the composition not a
+//     plain convolution; those tiles sum W2 * c1 from nconv1's c1 as the unfused path does.
 // Interior-tile outputs therefore differ from the unfused exact pair only through D2's rounding;
 // N2, nconv1 and the edge tiles match it bit for bit.
 #include "nconv_internal.h"
@@ -31,17 +35,26 @@ constexpr int kHT = 256, kHTH = 16, kHTW = 32;
 constexpr int kSH = kHTH + 8, kSW = kHTW + 8;     // depth tile: 24 x 40 (two 5x5 halos)
 constexpr int kHH = kHTH + 4, kHW = kHTW + 4;     // nconv1 outputs nconv2 reads: 20 x 36
 constexpr int kHP = kHW - 16;                     // halo pair slots per row: (c, c + 16), c < 20
-constexpr int kCP = kSW - 16;                     // mask pair slots per row: c < 24
 constexpr int kHPlane = kHH * kHP;                // f2 per halo pair plane
 constexpr int kHPS = kHPlane + 1;                 // plane stride: each plane ends in its own dump slot
-constexpr int kW21 = 9 * 8 * 9;                   // composed weights, then W2 as [ci][kh][kw][o]
+// nconv_head_weights' output: the D2 operand fragments (kFrag dwords), then W2 as [ci][kh][kw][o].
+// Fragment (b, ks, lane) of v_mfma_f32_16x16x32_bf16's A: row = lane & 15 = 4 * (o - 4b) + part
+// (part 3 = 0), k = 8 * (lane >> 4) + j over 12 tap chunks 4 ks + (lane >> 4) of 8:
+// chunk q < 9 = taps (q, 0..7), chunk 9 = (0..7, 8), chunk 10 = (8, 8) in j = 0, chunk 11 = none.
+constexpr int kFrag = 2 * 3 * 64 * 4;
+// D2 operand tables in the plane region (bytes): the B fragment of 8 mask bits from a 256-entry
+// table of bf16 {0, 1} octets, the bit octets of each row window (mask rows x columns c..c+7) and
+// of each column window (mask column c + 8, rows r..r+7) at the same pitch
+constexpr int kLut = 0, kW8R = 4096, kW8C = kW8R + kSH * kSW, kTabEnd = kW8C + kHTH * kSW;
+constexpr int kDP = 8 * 64 + 16;                  // D2 transpose: channel pitch (floats)
 
 typedef const float __attribute__((address_space(4))) cfloat;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 // TR (training): nconv1's outputs of the tile's own 16 x 32 pixels also go to HBM (the backward
 // reads them) and the pooled copies come with their argmax words (nconv_fwd_pooled's codes).
 template <bool TR>
-__global__ __launch_bounds__(kHT) void fwd_head_exact(LayerDev d2, TailArgs t, float* __restrict__ y,
+__global__ __launch_bounds__(kHT) __attribute__((amdgpu_waves_per_eu(5, 8))) void fwd_head_exact(LayerDev d2, TailArgs t, float* __restrict__ y,
                                                       float* __restrict__ yc) {
     const nconv_layer& L = d2.L;  // nconv2 (8 -> 8, 5x5, padding 2); nconv1 through t
     // LDS (30.5 KB: five workgroups per CU): the depth tile's S * c0 (c0 = (S * c0 > thresh): S
@@ -51,9 +64,11 @@ __global__ __launch_bounds__(kHT) void fwd_head_exact(LayerDev d2, TailArgs t, f
     __shared__ __attribute__((aligned(16))) float sx[kSH * kSW];
     __shared__ __attribute__((aligned(16))) f2 hp[8 * kHPS];  // 8 pair planes, each + a dump slot
     __shared__ __attribute__((aligned(16))) float w1t[25 * 8];       // nconv1 weights [tap][o]
-    __shared__ unsigned long long rowmask[kSH];
-    f2* const c0p = hp;  // {c0(c), c0(c + 16)}, kSH x kCP, until the interior D2 is done
-    static_assert(kSH * kCP <= 8 * kHPS, "mask pairs fit the plane region");
+    __shared__ unsigned long long rowmask[kSH];  // nonzero taps of nconv1 (x * c0 or c0 nonzero)
+    __shared__ unsigned long long c0row[kSH];    // c0 per mask row (bits = columns)
+    __shared__ unsigned c0col[kSW];              // c0 per mask column (bits = rows)
+    __shared__ int tile_nan;                     // a NaN among the staged S * c0 (S NaN or -inf)
+    static_assert(kTabEnd <= (int)sizeof(hp) && 8 * kDP * 4 <= (int)sizeof(hp), "D2 tables fit the plane region");
     const int tid = threadIdx.x;
     const int H = L.Ho, W = L.Wo;
     const TileCoord tc = xcd_tile((W + kHTW - 1) / kHTW, (H + kHTH - 1) / kHTH, L.B);
@@ -61,7 +76,9 @@ __global__ __launch_bounds__(kHT) void fwd_head_exact(LayerDev d2, TailArgs t, f
     const bool interior = R0 >= 2 && R0 + kHTH + 2 <= H && C0 >= 2 && C0 + kHTW + 2 <= W;
 
     // ---- stage the depth tile (origin R0 - 4, C0 - 4), its nonzero masks and nconv1's weights ----
-    if (tid < kSH) rowmask[tid] = 0ull;
+    if (tid < kSH) rowmask[tid] = c0row[tid] = 0ull;
+    if (tid < kSW) c0col[tid] = 0u;
+    if (tid == 0) tile_nan = 0;
     if (tid < 200) w1t[tid] = t.w1[(tid & 7) * 25 + (tid >> 3)];
     __syncthreads();
     {
@@ -82,9 +99,12 @@ __global__ __launch_bounds__(kHT) void fwd_head_exact(LayerDev d2, TailArgs t, f
                 const float c0 = sv[k] > t.thresh1 ? 1.0f : 0.0f;  // step1.py:53
                 const float xc = sv[k] * c0;
                 sx[e] = xc;
-                if (c < kCP) reinterpret_cast<float*>(c0p)[(r * kCP + c) * 2] = c0;
-                if (c >= 16) reinterpret_cast<float*>(c0p)[(r * kCP + c - 16) * 2 + 1] = c0;
                 if (!(xc == 0.f && c0 == 0.f)) atomicOr(&rowmask[r], 1ull << c);  // NaN counts as nonzero
+                if (xc != xc) tile_nan = 1;
+                if (c0 != 0.f) {
+                    atomicOr(&c0row[r], 1ull << c);
+                    atomicOr(&c0col[c], 1u << r);
+                }
             }
         }
     }
@@ -96,44 +116,59 @@ __global__ __launch_bounds__(kHT) void fwd_head_exact(LayerDev d2, TailArgs t, f
 #pragma unroll
     for (int o = 0; o < 8; ++o) accN[o] = accD[o] = (f2){0.f, 0.f};
 
-#ifdef NCONV_HEAD_PROBE_NO_D2  // timing probe only (wrong results): no interior confidence sums
-    if (false) {
-#else
+    // interior D2 on the matrix cores: wave w's pixels (4w + (nb >> 1), 16 (nb & 1) + n) are the
+    // 16 columns of GEMM block nb; lane (g, n) ends with D2 of channels g (b = 0) and 4 + g (b = 1)
+    float d2v[16];
     if (interior) {
-#endif
-        // D2 = W21 * c0 over the 9 x 9 window (mask tile origin R0 - 4 = output row - 4); rows in
-        // two steps of <= 5 taps: 40 weights in SGPRs at a time, as nconv2's rows
-        const cfloat* w21 = (const cfloat*)L.waux;  // [qh][o][qw]
-#pragma unroll 1
-        for (int qh = 0; qh < 9; ++qh) {
-            const f2* row = c0p + (ty + qh) * kCP + j;
-            const cfloat* wr = w21 + qh * 72;
-            f2 v[9];
+        unsigned char* const tb = reinterpret_cast<unsigned char*>(hp);
+        {   // table entry tid: bf16 1.0 where bit j of tid is set
+            unsigned d[4];
 #pragma unroll
-            for (int qw = 0; qw < 9; ++qw) v[qw] = row[qw];
+            for (int i = 0; i < 4; ++i)
+                d[i] = ((tid >> (2 * i)) & 1u) * 0x3F80u + ((tid >> (2 * i + 1)) & 1u) * 0x3F800000u;
+            reinterpret_cast<uint4*>(tb + kLut)[tid] = make_uint4(d[0], d[1], d[2], d[3]);
+        }
+        for (int e = tid; e < kSH * kSW; e += kHT) {
+            const int r = e / kSW, c = e - r * kSW;
+            tb[kW8R + e] = (unsigned char)(c0row[r] >> c);
+            if (r < kHTH) tb[kW8C + e] = c < kHTW ? (unsigned char)(c0col[c + 8] >> r) : 0;
+        }
+        __syncthreads();
+        const int lane = tid & 63, g = lane >> 4, n = lane & 15;
+        const uint4* fr = reinterpret_cast<const uint4*>(L.waux) + lane;
+        bf16x8 A[2][3];
 #pragma unroll
-            for (int qw = 0; qw < 5; ++qw)
+        for (int bb = 0; bb < 2; ++bb)
 #pragma unroll
-                for (int o = 0; o < 8; ++o) {
-                    const float wv = wr[o * 9 + qw];
-                    accD[o] = __builtin_elementwise_fma((f2){wv, wv}, v[qw], accD[o]);
-                }
-            __builtin_amdgcn_sched_barrier(0);
+            for (int ks = 0; ks < 3; ++ks) A[bb][ks] = __builtin_bit_cast(bf16x8, fr[(bb * 3 + ks) * 64]);
+        // byte offsets of this lane's chunk octets for K step ks (pixel (4w, n) + per-block immediates)
+        const int pb = (tid >> 6) * 4 * kSW + n;
+        const int o0 = kW8R + g * kSW + pb, o1 = kW8R + (4 + g) * kSW + pb;
+        const int o2 = g == 0 ? kW8R + 8 * kSW + pb : (g == 1 ? kW8C + pb : kW8R + 8 * kSW + 8 + pb);
 #pragma unroll
-            for (int qw = 5; qw < 9; ++qw)
+        for (int nb = 0; nb < 8; ++nb) {
+            const int po = (nb >> 1) * kSW + 16 * (nb & 1);
+            const bf16x8 B0 = __builtin_bit_cast(bf16x8, reinterpret_cast<const uint4*>(tb + kLut)[tb[o0 + po]]);
+            const bf16x8 B1 = __builtin_bit_cast(bf16x8, reinterpret_cast<const uint4*>(tb + kLut)[tb[o1 + po]]);
+            const bf16x8 B2 = __builtin_bit_cast(bf16x8, reinterpret_cast<const uint4*>(tb + kLut)[tb[o2 + po]]);
 #pragma unroll
-                for (int o = 0; o < 8; ++o) {
-                    const float wv = wr[o * 9 + qw];
-                    accD[o] = __builtin_elementwise_fma((f2){wv, wv}, v[qw], accD[o]);
-                }
+            for (int bb = 0; bb < 2; ++bb) {
+                f4 acc = (f4){0.f, 0.f, 0.f, 0.f};
+                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[bb][0], B0, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[bb][1], B1, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[bb][2], B2, acc, 0, 0, 0);
+                d2v[bb * 8 + nb] = (acc.x + acc.y) + acc.z;  // hi + mid, then + lo
+            }
         }
     }
-    __syncthreads();  // the mask pairs are dead: the region becomes nconv1's planes
+    __syncthreads();  // the D2 tables are dead: the region becomes nconv1's planes
 
     // ---- nconv1 on the 20 x 36 halo (origin R0 - 2, C0 - 2), nonzero taps only; writes x * c
     //      (want_c false) or c (want_c true, edge tiles' second pass) into the pair planes ----
     constexpr int NH = (kHH * kHW + kHT - 1) / kHT;  // 3 halo pixels per thread (the last partly)
-    auto nconv1_planes = [&](bool want_c) {
+    // exact_c0: c0 formed per visited tap (the tile holds a NaN S * c0); otherwise every visited
+    // tap has c0 = 1 (S * c0 is nonzero only where c0 = 1, or NaN)
+    auto nconv1_pass = [&](bool want_c, auto exact_c0) {
 #pragma unroll 1
         for (int k = 0; k < NH; ++k) {
             const int e = tid + kHT * k;
@@ -141,24 +176,23 @@ __global__ __launch_bounds__(kHT) void fwd_head_exact(LayerDev d2, TailArgs t, f
             const int gr = R0 - 2 + r, gc = C0 - 2 + c;
             const bool valid = e < kHH * kHW;
             const bool in = valid && (unsigned)gr < (unsigned)H && (unsigned)gc < (unsigned)W;
+            unsigned m = 0;
+#ifndef NCONV_HEAD_PROBE_NO_N1  // timing probe only (wrong results): no nconv1 taps
+#pragma unroll
+            for (int kh = 0; kh < 5; ++kh) m |= (unsigned)((rowmask[(valid ? r : 0) + kh] >> c) & 31ull) << (5 * kh);
+#endif
+            m = in ? m : 0u;
+            // tap tp = 5 kh + kw of the window at halo pixel (r, c) is staged at sxb[35 kh + tp]
+            const float* const sxb = sx + r * kSW + c;
             f2 acc[8];
 #pragma unroll
             for (int o = 0; o < 8; ++o) acc[o] = (f2){0.f, 0.f};
-            unsigned m = 0;
-#ifdef NCONV_HEAD_PROBE_NO_N1  // timing probe only (wrong results): no nconv1 taps
-            if (false) {
-#else
-            if (in) {
-#endif
-#pragma unroll
-                for (int kh = 0; kh < 5; ++kh) m |= (unsigned)((rowmask[r + kh] >> c) & 31ull) << (5 * kh);
-            }
             while (m) {
                 const int tp = __builtin_ctz(m);
                 m &= m - 1;
-                const int kh = (tp * 13) >> 6, kw = tp - 5 * kh;  // tp / 5 for tp < 25
-                const float xc = sx[(r + kh) * kSW + c + kw];
-                const f2 v = (f2){xc, xc > t.thresh1 ? 1.0f : 0.0f};  // {S * c0, c0}
+                const int kh = (tp * 13) >> 6;  // tp / 5 for tp < 25
+                const float xc = sxb[kh * (kSW - 5) + tp];
+                const f2 v = (f2){xc, decltype(exact_c0)::value ? (xc > t.thresh1 ? 1.0f : 0.0f) : 1.0f};
                 const f4 wa = reinterpret_cast<const f4*>(w1t)[tp * 2], wb = reinterpret_cast<const f4*>(w1t)[tp * 2 + 1];
                 const float wv[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
 #pragma unroll
@@ -191,12 +225,16 @@ __global__ __launch_bounds__(kHT) void fwd_head_exact(LayerDev d2, TailArgs t, f
             }
         }
     };
+    auto nconv1_planes = [&](bool want_c) {
+        if (tile_nan) nconv1_pass(want_c, std::true_type{});
+        else nconv1_pass(want_c, std::false_type{});
+    };
     nconv1_planes(false);
     __syncthreads();
 
     // nconv2's weights transposed to [ci][kh][kw][o] (nconv_head_weights, after W21): one kernel
     // row's 40 weights are contiguous -- three scalar loads instead of sixteen
-    const cfloat* w2t = (const cfloat*)L.waux + kW21;
+    const cfloat* w2t = (const cfloat*)L.waux + kFrag;
     // N2 (or, for edge tiles, D2 from c1) over the 8 halo pair planes: {N(p), N(p+16)} += w * pair
     auto sum_planes = [&](f2 (&acc)[8]) {
 #pragma unroll 1
@@ -221,13 +259,25 @@ __global__ __launch_bounds__(kHT) void fwd_head_exact(LayerDev d2, TailArgs t, f
 #ifndef NCONV_HEAD_PROBE_NO_N2  // timing probe only (wrong results): no nconv2 data sums
     sum_planes(accN);
 #endif
+    __syncthreads();  // every wave is done reading the x * c planes
     if (!interior) {
         // edge tile: nconv2's zero padding truncates the window -- D2 = W2 * c1 as the unfused
         // path, with c1 from a second nonzero-tap pass of nconv1 into the planes
-        __syncthreads();  // every wave is done reading the x * c planes
         nconv1_planes(true);
         __syncthreads();
         sum_planes(accD);
+    } else {
+        // the matrix-core D2 from GEMM layout to the thread's pixels (ty, j), (ty, j + 16)
+        float* const dt = reinterpret_cast<float*>(hp);
+        const int lane = tid & 63, g = lane >> 4, n = lane & 15, w = tid >> 6;
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb)
+#pragma unroll
+            for (int nb = 0; nb < 8; ++nb)
+                dt[(4 * bb + g) * kDP + (4 * w + (nb >> 1)) * kHTW + 16 * (nb & 1) + n] = d2v[bb * 8 + nb];
+        __syncthreads();
+#pragma unroll
+        for (int o = 0; o < 8; ++o) accD[o] = (f2){dt[o * kDP + ty * kHTW + j], dt[o * kDP + ty * kHTW + j + 16]};
     }
 
     // ---- epilogue: y, cout and their 2x2 max-pooled copies (the input of down1) ----
@@ -238,13 +288,18 @@ __global__ __launch_bounds__(kHT) void fwd_head_exact(LayerDev d2, TailArgs t, f
     const int Hp = H >> 1, Wp = W >> 1;
     const size_t pplane = (size_t)Hp * Wp;
     const int ppbytes = (int)(pplane * 4);
-    unsigned so[2], po[2];
-    const bool pool_lane = ((ty & 1) == 0) && ((j & 1) == 0) && (oh >> 1) < Hp;
+    // training: the pooled pair and argmax leave from the window's top-left lane; inference: the
+    // pooled y from the even rows' even lanes, the pooled cout from the odd rows' (see below)
+    unsigned so[2], po[2], pcy[2], pcc[2];
+    const bool pool_col = ((j & 1) == 0) && (oh >> 1) < Hp;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         const int ow = C0 + j + 16 * h;
         so[h] = (oh < H && ow < W) ? (unsigned)(oh * W + ow) * 4u : OOB;
-        po[h] = (pool_lane && (ow >> 1) < Wp) ? (unsigned)((oh >> 1) * Wp + (ow >> 1)) * 4u : OOB;
+        const unsigned pp = (pool_col && (ow >> 1) < Wp) ? (unsigned)((oh >> 1) * Wp + (ow >> 1)) * 4u : OOB;
+        po[h] = (ty & 1) == 0 ? pp : OOB;
+        pcy[h] = po[h];
+        pcc[h] = (ty & 1) ? pp : OOB;
     }
 #pragma unroll
     for (int o = 0; o < 8; ++o) {
@@ -266,34 +321,56 @@ __global__ __launch_bounds__(kHT) void fwd_head_exact(LayerDev d2, TailArgs t, f
 #ifdef NCONV_HEAD_PROBE_NO_POOL  // timing probe only (wrong results): no pooled copies
             continue;
 #endif
-            // window (r, c) (r, c+1) (r+1, c) (r+1, c+1): lanes l, l^1, l^16, l^17 (torch order)
-            const float yb = shfl_xor16(yv[h]), cb = shfl_xor16(cv[h]);
-            const float ya = shfl_xor1(yv[h]), yd = shfl_xor1(yb), ca = shfl_xor1(cv[h]), cd = shfl_xor1(cb);
             if constexpr (TR) {  // the first maximum's slot too (the backward's routing)
+                // window (r, c) (r, c+1) (r+1, c) (r+1, c+1): lanes l, l^1, l^16, l^17 (torch order)
+                const float yb = shfl_xor16(yv[h]), cb = shfl_xor16(cv[h]);
+                const float ya = shfl_xor1(yv[h]), yd = shfl_xor1(yb), ca = shfl_xor1(cv[h]), cd = shfl_xor1(cb);
                 int ay, ac;
                 st_f32(rpy, po[h], pool4(yv[h], ya, yb, yd, ay));
                 st_f32(rpc, po[h], pool4(cv[h], ca, cb, cd, ac));
                 st_f32(plane_rsrc((const float*)(t.parg + pofs), ppbytes), po[h],
                        __builtin_bit_cast(float, (unsigned)(ay | (ac << 2))));
             } else {
-                st_f32(rpy, po[h], pool4v(yv[h], ya, yb, yd));
-                st_f32(rpc, po[h], pool4v(cv[h], ca, cb, cd));
+                // the value alone: one v_permlane16_swap of (y, cout) leaves rows {y0, c0, y2, c2}
+                // and {y1, c1, y3, c3} (16-lane rows = tile rows), so their maximum is y's vertical
+                // pair maximum in the even rows and cout's in the odd rows; then the column pair
+                const float vm = pair_rows_max(yv[h], cv[h]);
+                const float pm = __builtin_elementwise_maximum(vm, shfl_xor1(vm));
+                st_f32(rpy, pcy[h], pm);
+                st_f32(rpc, pcc[h], pm);
             }
         }
     }
 }
 
-// W21[qh][o][qw] = sum_i (1 / s1[i]) sum_{kh + kh' = qh, kw + kw' = qw} W2[o][i][kh][kw] W1[i][kh'][kw']
-// in fp64, rounded once (s1 = nconv1's weight sums, as the forward's cout = D1 / s1 uses them).
-// One 64-lane block per (qh, qw): lane (o, i) forms channel i's term, the 8 terms of an output
-// are summed over lanes in a fixed butterfly order; block 81 writes W2 transposed to [i][kh][kw][o].
+// W21[o][qh][qw] = sum_i (1 / s1[i]) sum_{kh + kh' = qh, kw + kw' = qw} W2[o][i][kh][kw] W1[i][kh'][kw']
+// in fp64, rounded once to fp32 (s1 = nconv1's weight sums, as the forward's cout = D1 / s1 uses
+// them), then split exactly into bf16 hi + mid + lo (truncations: each remainder is exact in fp32
+// and the last has at most 8 significant bits) and written into the D2 fragments (kFrag). One
+// 64-lane block per (qh, qw): lane (o, i) forms channel i's term, the 8 terms of an output are
+// summed over lanes in a fixed butterfly order; block 81 writes W2 transposed to [i][kh][kw][o],
+// block 82 zeroes the fragment slots no tap fills.
+__device__ __forceinline__ int frag_slot(int o, int part, int chunk, int j) {
+    const int row = 4 * (o & 3) + part, ks = chunk >> 2, g = chunk & 3;
+    return (((o >> 2) * 3 + ks) * 64 + g * 16 + row) * 8 + j;  // bf16 index
+}
+
 __global__ __launch_bounds__(64) void head_weights(const float* __restrict__ w1, const float* __restrict__ s1,
                                                    const float* __restrict__ w2, float* __restrict__ out) {
     const int blk = blockIdx.x, lane = threadIdx.x;
+    unsigned short* const fb = reinterpret_cast<unsigned short*>(out);
     if (blk == 81) {
         for (int e = lane; e < 1600; e += 64) {  // W2t[ci][kh][kw][o] = W2[o][ci][kh][kw]
             const int o = e & 7, kk = (e >> 3) % 25, ci = e / 200;
-            out[kW21 + e] = w2[(o * 8 + ci) * 25 + kk];
+            out[kFrag + e] = w2[(o * 8 + ci) * 25 + kk];
+        }
+        return;
+    }
+    if (blk == 82) {
+        for (int e = lane; e < kFrag * 2; e += 64) {
+            const int j = e & 7, l = (e >> 3) & 63, ks = (e >> 9) % 3;
+            const int part = l & 3, chunk = 4 * ks + (l >> 4);
+            if (part == 3 || chunk == 11 || (chunk == 10 && j != 0)) fb[e] = 0;
         }
         return;
     }
@@ -311,7 +388,18 @@ __global__ __launch_bounds__(64) void head_weights(const float* __restrict__ w1,
     si /= (double)s1[i];
 #pragma unroll
     for (int m = 1; m < 8; m <<= 1) si += __shfl_xor(si, m);
-    if (i == 0) out[(qh * 8 + o) * 9 + qw] = (float)si;
+    if (i == 0) {
+        const float w = (float)si;
+        const float hi = __uint_as_float(__float_as_uint(w) & 0xFFFF0000u);
+        const float r = w - hi;
+        const float mid = __uint_as_float(__float_as_uint(r) & 0xFFFF0000u);
+        const float lo = r - mid;
+        const int chunk = qw < 8 ? qh : (qh < 8 ? 9 : 10);
+        const int j = qw < 8 ? qw : (qh < 8 ? qh : 0);
+        fb[frag_slot(o, 0, chunk, j)] = (unsigned short)(__float_as_uint(hi) >> 16);
+        fb[frag_slot(o, 1, chunk, j)] = (unsigned short)(__float_as_uint(mid) >> 16);
+        fb[frag_slot(o, 2, chunk, j)] = (unsigned short)(__float_as_uint(lo) >> 16);
+    }
 }
 
 }  // namespace
@@ -332,7 +420,7 @@ int launch_fwd_head_exact(const LayerDev& d2, const TailArgs& t, float* y, float
 
 int launch_head_weights(const float* w1, const float* s1, const float* w2, float* out, hipStream_t st,
                         const char** why) {
-    hipLaunchKernelGGL(head_weights, dim3(82), dim3(64), 0, st, w1, s1, w2, out);
+    hipLaunchKernelGGL(head_weights, dim3(83), dim3(64), 0, st, w1, s1, w2, out);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         *why = hipGetErrorString(e);

@@ -166,14 +166,18 @@ def layer_forward_pooled(spec: LayerSpec, xa, ca, xb, cb, weight, bias, wsum, ou
     return (y, co, py, pc, arg) if argmax else (y, co, py, pc)
 
 
+HEAD_WEIGHTS_FLOATS = 3136  # include/nconv.h NCONV_HEAD_WEIGHTS_FLOATS
+
+
 def head_weights(spec1: LayerSpec, spec2: LayerSpec, S, w1, b1, s1, w2, b2, s2, out=None):
-    """nconv_head_weights: the exact fused head's auxiliary weights (2248 floats: the composed
-    confidence weights sum_i W2[o,i] (x) W1[i] / s1[i], then nconv2's weights transposed) from the
-    current weights and nconv1's s[o]; one launch."""
+    """nconv_head_weights: the exact fused head's auxiliary weights (HEAD_WEIGHTS_FLOATS = 3136
+    floats: the composed confidence weights sum_i W2[o,i] (x) W1[i] / s1[i] as exact three-part bf16
+    matrix-core operands, then nconv2's weights transposed) from the current weights and nconv1's
+    s[o]; one launch."""
     L1 = spec1.descriptor(S, None, None, None, w1, b1, s1)
     L2 = spec2.descriptor(S, S, None, None, w2, b2, s2)
     if out is None:
-        out = torch.empty(2248, device=S.device, dtype=torch.float32)
+        out = torch.empty(HEAD_WEIGHTS_FLOATS, device=S.device, dtype=torch.float32)
     rc = _lib.lib().nconv_head_weights(_lib.ctypes.byref(L1), _lib.ctypes.byref(L2), _lib.ptr(out),
                                        _lib.stream_handle(S.device))
     _lib.check(rc, "nconv_head_weights")
