@@ -168,7 +168,7 @@ __global__ __launch_bounds__(kHT) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
     constexpr int NH = (kHH * kHW + kHT - 1) / kHT;  // 3 halo pixels per thread (the last partly)
     // exact_c0: c0 formed per visited tap (the tile holds a NaN S * c0); otherwise every visited
     // tap has c0 = 1 (S * c0 is nonzero only where c0 = 1, or NaN)
-    auto nconv1_pass = [&](bool want_c, auto exact_c0) {
+    auto nconv1_pass = [&](bool want_c, auto exact_c0) __attribute__((always_inline)) {
 #pragma unroll 1
         for (int k = 0; k < NH; ++k) {
             const int e = tid + kHT * k;
@@ -225,7 +225,7 @@ __global__ __launch_bounds__(kHT) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
             }
         }
     };
-    auto nconv1_planes = [&](bool want_c) {
+    auto nconv1_planes = [&](bool want_c) __attribute__((always_inline)) {
         if (tile_nan) nconv1_pass(want_c, std::true_type{});
         else nconv1_pass(want_c, std::false_type{});
     };
@@ -236,7 +236,7 @@ __global__ __launch_bounds__(kHT) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
     // row's 40 weights are contiguous -- three scalar loads instead of sixteen
     const cfloat* w2t = (const cfloat*)L.waux + kFrag;
     // N2 (or, for edge tiles, D2 from c1) over the 8 halo pair planes: {N(p), N(p+16)} += w * pair
-    auto sum_planes = [&](f2 (&acc)[8]) {
+    auto sum_planes = [&](f2 (&acc)[8]) __attribute__((always_inline)) {
 #pragma unroll 1
         for (int ci = 0; ci < 8; ++ci) {
             const f2* row = hp + ci * kHPS + ty * kHP + j;
