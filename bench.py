@@ -85,6 +85,8 @@ def parse():
     p.add_argument("--fused-head", type=int, default=1, help="nconv1 inside nconv2's kernel (nconv_fwd_head)")
     p.add_argument("--inference-streams", type=int, default=None,
                    help="DNET.inference_streams: batch slices on that many streams (default: the module's)")
+    p.add_argument("--inference-shares", default=None, type=lambda v: [float(x) for x in v.split(",")],
+                   help="DNET.inference_shares: relative frames per inference stream, e.g. 5,3")
     p.add_argument("--mid-streams", type=int, default=None,
                    help="DNET.mid_streams: the quarter/eighth-resolution layers on that many batch slices")
     p.add_argument("--train-graph", type=int, default=-1,
@@ -553,6 +555,8 @@ def main():
     net.d_net.fused_head = bool(a.fused_head)
     if a.inference_streams is not None:
         net.d_net.inference_streams = a.inference_streams
+    if a.inference_shares is not None:
+        net.d_net.inference_shares = tuple(a.inference_shares)
     if a.mid_streams is not None:
         net.d_net.mid_streams = a.mid_streams
     g = torch.Generator().manual_seed(1000 + rank)

@@ -385,6 +385,9 @@ __global__ __launch_bounds__(kDT) void conv3x3_c1(const float* __restrict__ x, i
     }
 }
 
+#ifndef NCONV_WGD_GLDS
+#define NCONV_WGD_GLDS 1
+#endif
 // ------------------------------------------------------------------------------------------------
 // Weight gradients (training):  gW[m][n] = sum over images and pixels p of
 //     D[m][p] * P[n / TAPS][patch(p, n % TAPS)]
@@ -498,6 +501,127 @@ __global__ __launch_bounds__(kDT) void dense_wgrad_mfma(WgdArgs a, float* __rest
     // concatenation of the guided model; otherwise that group reads each element from both
     // sources (one out of range) and adds them.
     constexpr unsigned OOB = 0x80000000u;
+#if NCONV_WGD_GLDS
+    // LDS-DMA staging (buffer_load ... lds): every staged element goes from HBM straight into its
+    // LDS slot -- no staging registers, so the weight-gradient accumulators (NT x 16 per lane) and
+    // the rest fit two waves per SIMD, and one workgroup's loads hide behind the other's MFMAs.
+    // A wave's 64 elements of one load are consecutive in the LDS image (the DMA writes wave base
+    // + lane x 4): the patch planes are unpadded and a D row (NPX >= 64 pixels) never splits a wave.
+    typedef __attribute__((address_space(3))) void* lds_ptr_t;
+    auto glds = [&](__amdgpu_buffer_rsrc_t r, float* dst, unsigned off) __attribute__((always_inline)) {
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)dst, 4, off, 0, 0, 0);
+    };
+    const int wb = 64 * w;  // the wave's first element of each load
+    // Per-block constants of the staging (the element -> LDS slot map is the same for every tile):
+    // each patch element's byte offset from its tile's patch origin (channel plane included;
+    // 0x80000000 for the channels past the input, which then reads 0 whatever the tile), and each
+    // D element's pixel offset. An interior tile then costs one add per element; tiles touching
+    // the image border take the general path with per-element bounds.
+    constexpr unsigned OOB_REL = 0x80000000u;
+    unsigned prel[GN][C::NPG];
+    bool gwhole[GN];  // the group's channels come from one source
+#pragma unroll
+    for (int g = 0; g < GN; ++g) {
+        const int gc0 = c_lo + g * C::CPG;
+        const bool hi = a.p1 != nullptr && gc0 >= a.pC0;
+        gwhole[g] = !(a.p1 != nullptr && gc0 < a.pC0 && gc0 + C::CPG > a.pC0);
+        const int cb = hi ? a.pC0 : 0;
+#pragma unroll
+        for (int k = 0; k < C::NPG; ++k) {
+            const int e = tid + kDT * k;
+            const int ci = e / C::PPLANE, rem = e % C::PPLANE;
+            const int r = rem / C::PC, c = rem % C::PC;
+            prel[g][k] = (gc0 + ci < Cp && e < C::CPG * C::PPLANE)
+                             ? ((unsigned)(gc0 + ci - cb) * (unsigned)HWs + (unsigned)(r * C::GS * a.Ws + c * C::GS)) * 4u
+                             : OOB_REL;
+        }
+    }
+    const int dq = tid % C::NPX;
+    const unsigned drel = (unsigned)((dq / C::TW) * a.Wp + dq % C::TW) * 4u;
+    // the block's tiles walk (tx, ty, b) in order from t0
+    int tx_c = (int)(t0 % a.ntx), ty_c = (int)((t0 / a.ntx) % a.nty), b_c = (int)(t0 / ((long long)a.ntx * a.nty));
+    auto stage = [&](int tx, int ty, int b) __attribute__((always_inline)) {
+        int tq = tid;
+        asm volatile("" : "+v"(tq));
+        const int py0 = ty * C::TH, px0 = tx * C::TW;
+        const int iy0 = py0 * C::OS - C::PAD, ix0 = px0 * C::OS - C::PAD;
+        const bool dfull = py0 + C::TH <= a.Hp && px0 + C::TW <= a.Wp;
+        const bool pfull = iy0 >= 0 && ix0 >= 0 && iy0 + (C::PR - 1) * C::GS < a.Hs && ix0 + (C::PC - 1) * C::GS < a.Ws;
+        {
+            unsigned ob;
+            if (dfull) {
+                ob = (unsigned)(py0 * a.Wp + px0) * 4u + drel;
+            } else {
+                const int py = py0 + dq / C::TW, px = px0 + dq % C::TW;
+                ob = (py < a.Hp && px < a.Wp) ? (unsigned)(py * a.Wp + px) * 4u : OOB;
+            }
+            const __amdgpu_buffer_rsrc_t rd0 = plane_rsrc(a.d0 + (size_t)b * a.dC0 * HWp, (int)(a.dC0 * HWp * 4));
+            const __amdgpu_buffer_rsrc_t rd1 =
+                plane_rsrc(a.d1 ? a.d1 + (size_t)b * a.dC1 * HWp : a.d0, (int)((a.d1 ? a.dC1 : 0) * HWp * 4));
+            const int mw = __builtin_amdgcn_readfirstlane(m0 + tid / C::NPX);  // NPX >= 64: per wave
+#pragma unroll
+            for (int k = 0; k < C::NDE; ++k) {
+                const int m = mw + (kDT / C::NPX) * k;
+                const bool s1 = m >= a.dC0;
+                const int mm = s1 ? m - a.dC0 : m;
+                const unsigned off = (m < a.M && ob != OOB) ? (unsigned)(mm * HWp) * 4u + ob : OOB;
+                const int e0 = wb + kDT * k;
+                glds(s1 ? rd1 : rd0, lds + C::D_OFF + (e0 / C::NPX) * C::DP + e0 % C::NPX, off);
+            }
+        }
+        const __amdgpu_buffer_rsrc_t rp0 = plane_rsrc(a.p0 + (size_t)b * a.pC0 * HWs, (int)(a.pC0 * HWs * 4));
+        const __amdgpu_buffer_rsrc_t rp1 =
+            plane_rsrc(a.p1 ? a.p1 + (size_t)b * a.pC1 * HWs : a.p0, (int)((a.p1 ? a.pC1 : 0) * HWs * 4));
+        const unsigned pbase = (unsigned)(iy0 * a.Ws + ix0) * 4u;  // used by interior tiles only
+#pragma unroll
+        for (int g = 0; g < GN; ++g) {
+            const int gc0 = c_lo + g * C::CPG;
+            const bool hi = a.p1 != nullptr && gc0 >= a.pC0;
+            const int cb = hi ? a.pC0 : 0;
+            const __amdgpu_buffer_rsrc_t rp = hi ? rp1 : rp0;
+            if (pfull && gwhole[g]) {
+#pragma unroll
+                for (int k = 0; k < C::NPG; ++k)
+                    if ((k + 1) * kDT <= C::CPG * C::PPLANE || tq + kDT * k < C::CPG * C::PPLANE)
+                        glds(rp, lds + g * C::CPG * C::PPLANE + wb + kDT * k, pbase + prel[g][k]);
+                continue;
+            }
+#pragma unroll
+            for (int k = 0; k < C::NPG; ++k) {
+                const int e = tq + kDT * k;
+                if ((k + 1) * kDT <= C::CPG * C::PPLANE || e < C::CPG * C::PPLANE) {
+                    const int ci = e / C::PPLANE, rem = e % C::PPLANE;
+                    const int r = rem / C::PC, c = rem % C::PC;
+                    const int gc = gc0 + ci, iy = iy0 + r * C::GS, ix = ix0 + c * C::GS;
+                    const bool ok = gc < Cp && (unsigned)iy < (unsigned)a.Hs && (unsigned)ix < (unsigned)a.Ws;
+                    const unsigned pix = (unsigned)(iy * a.Ws + ix);
+                    float* dst = lds + g * C::CPG * C::PPLANE + wb + kDT * k;
+                    if (gwhole[g]) {
+                        glds(rp, dst, ok ? ((unsigned)(gc - cb) * (unsigned)HWs + pix) * 4u : OOB);
+                    } else if (gc < a.pC0) {  // the group's channels come from both sources: each lane one
+                        glds(rp0, dst, ok ? ((unsigned)gc * (unsigned)HWs + pix) * 4u : OOB);
+                    } else {
+                        glds(rp1, dst, ok ? ((unsigned)(gc - a.pC0) * (unsigned)HWs + pix) * 4u : OOB);
+                    }
+                }
+            }
+        }
+    };
+
+#pragma unroll 1
+    for (long long t = t0; t < t1; ++t) {
+        __syncthreads();  // the previous tile's MFMAs are done with the LDS
+        stage(tx_c, ty_c, b_c);
+        if (++tx_c == a.ntx) {
+            tx_c = 0;
+            if (++ty_c == a.nty) {
+                ty_c = 0;
+                ++b_c;
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+#else
     float dv[C::NDE], pv[GN][C::NPG];
     auto load = [&](long long t) {
         // the per-element coordinates below are recomputed per tile (tid made opaque): hoisted
@@ -576,6 +700,7 @@ __global__ __launch_bounds__(kDT) void dense_wgrad_mfma(WgdArgs a, float* __rest
         store();
         __syncthreads();
         if (t + 1 < t1) load(t + 1);
+#endif
         // the wave's pixels in segments of 16 (8 k-steps) inside one tile row
 #pragma unroll 1
         for (int sg = 0; sg < C::PPW / 16; ++sg) {
@@ -757,7 +882,8 @@ static WgdPlan wgrad_plan(const nconv_dense_wgrad& g) {
     // groups per workgroup: pairs along M and N where they divide evenly; the strided 3x3
     // stages tall patches, so it pairs along M only
     pl.gm = (pl.nt > 1 && nmg % 2 == 0) ? 2 : 1;
-    pl.gn = (pl.nt > 1 && nng % 2 == 0 && !(g.kind == NCONV_DENSE_3X3 && g.stride == 2)) ? 2 : 1;
+    // (LDS-DMA staging: one n-group per workgroup, so two workgroups fit a CU's LDS)
+    pl.gn = (!NCONV_WGD_GLDS && pl.nt > 1 && nng % 2 == 0 && !(g.kind == NCONV_DENSE_3X3 && g.stride == 2)) ? 2 : 1;
     pl.rg = 4 / (pl.gm * pl.gn);
     const int th = (tr || (g.kind == NCONV_DENSE_3X3 && g.stride == 2)) ? 2 : 4;
     a.ntx = (a.Wp + 31) / 32;

@@ -394,6 +394,10 @@ class DNET(nn.Module):
     # 0.628 ms), 1 for the matrix-core maths, whose persistent grids are sized to the chip and
     # leave no such gaps (0.507 vs 0.555 ms). A frame's result does not depend on the split.
     inference_streams = None
+    # Frames per stream of the inference split, as relative shares (None = even); an uneven split
+    # staggers the streams' phases so one stream's small quarter / eighth-resolution layers run
+    # beside the other's full-resolution head or tail instead of beside its own small layers.
+    inference_shares = None
 
     def _n_streams(self, B):
         n = self.inference_streams
@@ -417,9 +421,17 @@ class DNET(nn.Module):
         cur = torch.cuda.current_stream(S.device)
         side = self._side_streams(S.device, n - 1)
         bounds = [B * k // n for k in range(n + 1)]
+        sh = self.inference_shares
+        if sh is not None and len(sh) == n:
+            tot, acc = float(sum(sh)), 0.0
+            for k in range(1, n):
+                acc += sh[k - 1]
+                bounds[k] = min(max(int(round(B * acc / tot)), bounds[k - 1]), B)
         for st in side:
             st.wait_stream(cur)
         for k, st in enumerate([cur] + side):
+            if bounds[k + 1] == bounds[k]:
+                continue
             with torch.cuda.stream(st):
                 self._infer(S[bounds[k]:bounds[k + 1]], layers, wsum, out[bounds[k]:bounds[k + 1]], wph, mid=False)
         for st in side:

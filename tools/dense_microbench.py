@@ -35,6 +35,7 @@ def main():
               ("fuse2 upf TR 65->64", 2, 2, 65, 64, 88, 304), ("dgrad TR: C4 32->33", 3, 2, 32, 33, 352, 1216)]
     only = sys.argv[1].split(",") if len(sys.argv) > 1 else None  # name substrings
     fwd_only = os.environ.get("DENSE_FWD_ONLY") == "1"
+    ops = os.environ.get("DENSE_OPS", "fwd,wgrad,dgrad").split(",")  # e.g. DENSE_OPS=wgrad
     for name, kind, s, cin, cout, H, W in shapes:
         if only and not any(o in name for o in only):
             continue
@@ -46,14 +47,17 @@ def main():
         taps = {0: 9, 1: 1, 2: 4, 3: 16}[kind]
         pix = out.shape[0] * out.shape[2] * out.shape[3]
         fl = 2 * cin * cout * taps * pix
-        us = timeit(lambda: D.conv(x, kind, s, wp, None, False, cout, out=out))
-        print(f"fwd   {name:24s} {us:9.1f} us {fl / us / 1e6:7.1f} TF/s", flush=True)
+        if "fwd" in ops:
+            us = timeit(lambda: D.conv(x, kind, s, wp, None, False, cout, out=out))
+            print(f"fwd   {name:24s} {us:9.1f} us {fl / us / 1e6:7.1f} TF/s", flush=True)
         if kind in (0, 2) and not fwd_only:
             g = torch.randn_like(out)
-            us = timeit(lambda: D.wgrad(x, None, g, kind, s, w.shape))
-            print(f"wgrad {name:24s} {us:9.1f} us {fl / us / 1e6:7.1f} TF/s", flush=True)
-            us = timeit(lambda: D.dgrad(g, w, kind, s, x.shape))
-            print(f"dgrad {name:24s} {us:9.1f} us {fl / us / 1e6:7.1f} TF/s", flush=True)
+            if "wgrad" in ops:
+                us = timeit(lambda: D.wgrad(x, None, g, kind, s, w.shape))
+                print(f"wgrad {name:24s} {us:9.1f} us {fl / us / 1e6:7.1f} TF/s", flush=True)
+            if "dgrad" in ops:
+                us = timeit(lambda: D.dgrad(g, w, kind, s, x.shape))
+                print(f"dgrad {name:24s} {us:9.1f} us {fl / us / 1e6:7.1f} TF/s", flush=True)
 
 
 if __name__ == "__main__":
