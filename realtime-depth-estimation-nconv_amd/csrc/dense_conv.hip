@@ -73,6 +73,9 @@ struct DcCfg {
 
 typedef float f16v __attribute__((ext_vector_type(16)));
 
+#ifndef NCONV_DC_PREFETCH
+#define NCONV_DC_PREFETCH 0
+#endif
 template <int COUT, int KIND, int S, bool SC, bool STR = false>
 __global__ __launch_bounds__(kDT) void dense_conv_mfma(nconv_dense_conv p, int ntx, int nty, int ncot) {
     using C = DcCfg<COUT, KIND, S>;
@@ -212,6 +215,52 @@ __global__ __launch_bounds__(kDT) void dense_conv_mfma(nconv_dense_conv p, int n
         store_chunk();
         __syncthreads();
         load_chunk(ch + 1 < nchunk ? ch + 1 : ch);  // next chunk in flight during the MFMAs
+#if NCONV_DC_PREFETCH
+        // taps one per iteration, all of a tap's operand reads issued before its MFMAs (the default
+        // schedule read, waited and issued two MFMAs at a time: an LDS latency per MFMA pair)
+        float av[1][kCK / 2][C::MT], bv[1][kCK / 2][C::RW];
+        auto read_tap = [&](int t, int sl) __attribute__((always_inline)) {
+            const int dr = C::TR ? 1 - t / 2 : t / C::KS;
+            const int dc = C::TR ? 1 - t % 2 : t % C::KS;
+            const float* ap = lds + abase + t * kCK * C::COP;
+            const float* bp = lds + bbase + dr * C::ROW + dc;
+#pragma unroll
+            for (int pp = 0; pp < kCK / 2; ++pp) {
+#pragma unroll
+                for (int m = 0; m < C::MT; ++m) av[sl][pp][m] = ap[2 * pp * C::COP + 32 * m];
+#pragma unroll
+                for (int r = 0; r < C::RW; ++r) bv[sl][pp][r] = bp[2 * pp * C::PLANE + r * C::SP * C::ROW];
+            }
+        };
+        auto mfma_tap = [&](int t, int sl) __attribute__((always_inline)) {
+#pragma unroll
+            for (int pp = 0; pp < kCK / 2; ++pp) {
+#pragma unroll
+                for (int m = 0; m < C::MT; ++m)
+#pragma unroll
+                    for (int r = 0; r < C::RW; ++r)
+                        acc[m][r] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[sl][pp][m], bv[sl][pp][r], acc[m][r], 0, 0, 0);
+                if constexpr (SC) {
+                    if (t == C::CENTER) {
+#pragma unroll
+                        for (int m = 0; m < C::MT; ++m) {
+                            const float sa = lds[sbase + 2 * pp * C::COP + 32 * m];
+#pragma unroll
+                            for (int r = 0; r < C::RW; ++r)
+                                acs[m][r] = __builtin_amdgcn_mfma_f32_32x32x2f32(sa, bv[sl][pp][r], acs[m][r], 0, 0, 0);
+                        }
+                    }
+                }
+            }
+        };
+#pragma unroll 1
+        for (int t = 0; t < C::TAPS; ++t) {
+            read_tap(t, 0);
+            __builtin_amdgcn_sched_barrier(0);  // every operand read of the tap issued before its MFMAs
+            mfma_tap(t, 0);
+        }
+    }
+#else
         // taps one per iteration (not unrolled: unrolling all 9 x 4 k-steps lets the scheduler
         // hoist every operand read of the chunk into registers); the 4 channel pairs unrolled
 #pragma unroll 1
@@ -249,6 +298,7 @@ __global__ __launch_bounds__(kDT) void dense_conv_mfma(nconv_dense_conv p, int n
         }
     }
 
+#endif
     // ---- epilogue: bias, ReLU, shortcut; C[row = co][col = pixel]: col = lane & 31,
     //      row = (q & 3) + 8 (q >> 2) + 4 (lane >> 5) for register q. Stores through one
     //      resource over the image's output channel range: the lane's byte offset (its pixel and
@@ -437,7 +487,7 @@ struct WgdCfg {
     static constexpr int PPLANE = PR * PC;
     static constexpr int DP = NPX + 2;     // D row pitch: rows m, m+1 two banks apart
     static constexpr int D_OFF = (CPB * PPLANE + 3) & ~3;
-    static constexpr int LDS = D_OFF + GM * 32 * DP;
+    static constexpr int LDS = D_OFF + GM * 32 * DP > 4 * 16 * 64 ? D_OFF + GM * 32 * DP : 4 * 16 * 64;  // (+ the wave-partial sums)
     static constexpr int NDE = GM * 32 * NPX / kDT;  // D elements per thread
     static constexpr int NPG = (CPG * PPLANE + kDT - 1) / kDT;  // patch elements per thread and group
     static_assert(PPW % 16 == 0 && (GM * 32 * NPX) % kDT == 0, "wave / thread shares");
@@ -718,16 +768,25 @@ __global__ __launch_bounds__(kDT) void dense_wgrad_mfma(WgdArgs a, float* __rest
         }
     }
 
-    // ---- this wave's partial [32][NT*32] -> slice ks * RG + rg: C[row = m][col = n] ----
-    float* out = part + ((size_t)ks * C::RG + rg) * a.M * a.N;
+    // ---- the block's partial [GM*32][GN*NT*32] -> slice ks: C[row = m][col = n]. The RG waves of
+    //      a group hold the same tile over different pixels: summed here in LDS (fixed order, one
+    //      n-tile at a time), so the block writes one slice, not RG (RG x less partial traffic
+    //      for dense_wgrad_reduce) ----
+    float* out = part + (size_t)ks * a.M * a.N;
 #pragma unroll
     for (int u = 0; u < NT; ++u) {
-        const int n = n0 + gni * C::NCOLS + 32 * u + li;
-        if (n >= a.N) continue;
+        __syncthreads();  // the LDS is free (after the MFMAs / the previous tile)
 #pragma unroll
-        for (int q = 0; q < 16; ++q) {
-            const int m = m0 + gmi * 32 + (q & 3) + 8 * (q >> 2) + 4 * kk;
-            if (m < a.M) out[(size_t)m * a.N + n] = acc[u][q];
+        for (int q = 0; q < 16; ++q) lds[(w * 16 + q) * 64 + lane] = acc[u][q];
+        __syncthreads();
+        for (int e = tid; e < C::GB * 1024; e += kDT) {
+            const int g2 = e >> 10, q = (e >> 6) & 15, l = e & 63;
+            float v = lds[(g2 * 16 + q) * 64 + l];
+#pragma unroll
+            for (int r2 = 1; r2 < C::RG; ++r2) v += lds[((g2 + C::GB * r2) * 16 + q) * 64 + l];
+            const int n = n0 + (g2 / GM) * C::NCOLS + 32 * u + (l & 31);
+            const int m = m0 + (g2 % GM) * 32 + (q & 3) + 8 * (q >> 2) + 4 * (l >> 5);
+            if (n < a.N && m < a.M) out[(size_t)m * a.N + n] = v;
         }
     }
 }
@@ -900,7 +959,7 @@ static WgdPlan wgrad_plan(const nconv_dense_wgrad& g) {
 
 size_t dense_wgrad_workspace_bytes(const nconv_dense_wgrad& g) {
     const WgdPlan pl = wgrad_plan(g);
-    return (size_t)pl.a.nks * pl.rg * pl.a.M * pl.a.N * sizeof(float);
+    return (size_t)pl.a.nks * pl.a.M * pl.a.N * sizeof(float);
 }
 
 template <int KIND, int S, int NT>
@@ -946,7 +1005,7 @@ int launch_dense_wgrad(const nconv_dense_wgrad& g, float* ws, size_t ws_bytes, h
         return -95;
     }
     const int mn = pl.a.M * pl.a.N;
-    hipLaunchKernelGGL(dense_wgrad_reduce, dim3((mn + 63) / 64), dim3(kDT), 0, st, ws, pl.a.nks * pl.rg, mn, g.gw);
+    hipLaunchKernelGGL(dense_wgrad_reduce, dim3((mn + 63) / 64), dim3(kDT), 0, st, ws, pl.a.nks, mn, g.gw);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         *why = hipGetErrorString(e);

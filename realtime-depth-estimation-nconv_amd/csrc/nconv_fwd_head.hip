@@ -184,9 +184,24 @@ __global__ __launch_bounds__(kHT) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
             m = in ? m : 0u;
             // tap tp = 5 kh + kw of the window at halo pixel (r, c) is staged at sxb[35 kh + tp]
             const float* const sxb = sx + r * kSW + c;
+            // the first tap peeled, as a product: acc = w * v is the FMA into +0 the dense order
+            // starts with (bitwise); a window without taps takes v = {0, 0} -- no zero-filled
+            // accumulators (the compiler kept two copies of that fill, one per path into the loop)
             f2 acc[8];
+            {
+                const bool any = m != 0u;
+                const int tp = any ? __builtin_ctz(m) : 0;
+                m &= m - 1u;
+                const int kh = (tp * 13) >> 6;
+                const float xr = sxb[kh * (kSW - 5) + tp];
+                const float xc = any ? xr : 0.f;
+                const float cv = decltype(exact_c0)::value ? (xc > t.thresh1 ? 1.0f : 0.0f) : 1.0f;
+                const f2 v = (f2){xc, any ? cv : 0.f};
+                const f4 wa = reinterpret_cast<const f4*>(w1t)[tp * 2], wb = reinterpret_cast<const f4*>(w1t)[tp * 2 + 1];
+                const float wv[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
 #pragma unroll
-            for (int o = 0; o < 8; ++o) acc[o] = (f2){0.f, 0.f};
+                for (int o = 0; o < 8; ++o) acc[o] = (f2){wv[o], wv[o]} * v;
+            }
             while (m) {
                 const int tp = __builtin_ctz(m);
                 m &= m - 1;

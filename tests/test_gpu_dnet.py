@@ -222,7 +222,7 @@ def bwd_math(request, nconv_amd, monkeypatch):
     return request.param
 
 
-@pytest.mark.parametrize("H,W", [(64, 96), (45, 67)])
+@pytest.mark.parametrize("H,W", [(64, 96), (45, 67), (264, 100)])  # 264: nconv2 on wgrad_mfma2 (>= 256 rows)
 def test_dnet_train_gradients(nconv_amd, gpu, H, W, bwd_math):
     """Step-1 training gradients (EnforcePos + calculate_loss on [0] + backward) vs the fp64 oracle.
 

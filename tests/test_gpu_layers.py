@@ -182,14 +182,15 @@ def test_bwd_accumulate_flag(nconv_amd, gpu, case, bwd_math):
         assert torch.equal(gws[k], gw0) and torch.equal(gbs[k], gb0), "deferred reduction differs"
 
 
-def test_nconv2d_module_train_step(nconv_amd, gpu):
+@pytest.mark.parametrize("H,W", [(30, 44), (262, 70)])  # 262 rows: the two-row 5x5 weight gradient
+def test_nconv2d_module_train_step(nconv_amd, gpu, H, W):
     """Standalone NConv2d (the reference's layer API): EnforcePos pre-hook + forward + backward."""
     from oracle import nconv_ref as R
     torch.manual_seed(3)
     layer = nconv_amd.NConv2d(8, 8, (5, 5), "softplus", "p", padding=(2, 2)).to(gpu)
     w0 = layer.weight.detach().double().cpu().clone()
     g = torch.Generator().manual_seed(5)
-    x, c = rand_pair(g, 2, 8, 30, 44, dtype=torch.float64)
+    x, c = rand_pair(g, 2, 8, H, W, dtype=torch.float64)
     layer.train()
     xg, cg = _gpu(x, gpu, True), _gpu(c, gpu, True)
     y, co = layer(xg, cg)
