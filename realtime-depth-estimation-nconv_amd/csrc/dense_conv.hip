@@ -73,6 +73,9 @@ struct DcCfg {
 
 typedef float f16v __attribute__((ext_vector_type(16)));
 
+// Tap-level operand prefetch (every LDS read of a tap issued before its MFMAs): measured neutral to
+// +9 % slower per instantiation (strided, 32-channel and transposed tiles slower; 64-channel
+// stride-1 within noise: profiles/r4_ab_dense_prefetch.log, r4_ab_phase_lowplanes_prefetch.log).
 #ifndef NCONV_DC_PREFETCH
 #define NCONV_DC_PREFETCH 0
 #endif
