@@ -1,6 +1,7 @@
 // fp32 arithmetic rates on gfx950 (developer microbenchmark, not product code):
 // v_fma_f32, v_pk_fma_f32, v_mfma_f32_16x16x4_f32, v_mfma_f32_32x32x2_f32, and one wave
-// interleaving f32 MFMAs with independent VALU FMAs (are the matrix and vector pipes additive?).
+// interleaving f32 MFMAs with independent VALU FMAs (are the matrix and vector pipes additive?),
+// and split waves of bf16 MFMAs beside packed-FMA waves.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 typedef float f2 __attribute__((ext_vector_type(2)));
@@ -116,6 +117,32 @@ __global__ __launch_bounds__(256) void k(float* out, float a, int iters) {
                 for (int i = 0; i < 16; ++i) acc[i] = __builtin_elementwise_fma(w, acc[i], w);
             for (int i = 0; i < 16; ++i) s += acc[i].x + acc[i].y;
         }
+    } else if constexpr (KIND == 8) {  // wave-specialised: even waves bf16 MFMA 16x16x32, odd v_pk_fma
+        const int wv = threadIdx.x >> 6;
+        if ((wv & 1) == 0 && (NV & 1)) {
+            typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
+            bf8 av, bv;
+            for (int i = 0; i < 8; ++i) {
+                av[i] = (__bf16)(x + i);
+                bv[i] = (__bf16)(a * 0.5f - i);
+            }
+            f4 acc[4];
+            for (int i = 0; i < 4; ++i) acc[i] = (f4){x, x, x, x};
+            for (int it = 0; it < iters; ++it)
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc[i], 0, 0, 0);
+            for (int i = 0; i < 4; ++i) s += acc[i][0] + acc[i][3];
+        } else if ((wv & 1) == 1 && (NV & 2)) {
+            f2 acc[16];
+            for (int i = 0; i < 16; ++i) acc[i] = (f2){x + i, x - i};
+            const f2 w = {a, a};
+            for (int it = 0; it < iters * 8; ++it)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) acc[i] = __builtin_elementwise_fma(w, acc[i], w);
+            for (int i = 0; i < 16; ++i) s += acc[i].x + acc[i].y;
+        }
     }
     out[blockIdx.x * 256 + threadIdx.x] = s;
 }
@@ -178,6 +205,10 @@ int main() {
         run<7, 1>("split waves: MFMA half only", d, blocks, it / 4, 0.5 * 32 * 32.0);
         run<7, 2>("split waves: VALU half only", d, blocks, it / 4, 0.5 * 128 * 4.0);
         run<7, 3>("split waves: both halves", d, blocks, it / 4, 0.5 * 32 * 32.0 + 0.5 * 128 * 4.0);
+        // bf16 16x16x32: 2*16*16*32 flop / 64 lanes = 256 per lane per MFMA
+        run<8, 1>("split: bf16 MFMA half only", d, blocks, it / 4, 0.5 * 32 * 256.0);
+        run<8, 2>("split: VALU half only (bf16 run)", d, blocks, it / 4, 0.5 * 128 * 4.0);
+        run<8, 3>("split: bf16 MFMA + VALU halves", d, blocks, it / 4, 0.5 * 32 * 256.0 + 0.5 * 128 * 4.0);
     }
     {
         const int K = 200;
