@@ -129,6 +129,18 @@ size_t nconv_phase_weights_floats(const nconv_layer* L); /* 0 if L has no phase 
 int nconv_phase_weights(int n, const float* const* weights, const int* cins, const int* up_first,
                         float* const* wphases, void* stream);
 
+/* The inference (eval-mode) weight prologue in ONE launch: the normalisers wsums[i] of n layers
+ * (nconv_weight_prep with apply_softplus all 0: EnforcePos is inactive outside training), the exact
+ * fused head's auxiliary weights (nconv_head_weights of nconv1 head_w1 (8, 1, 5, 5) and nconv2
+ * head_w2 (8, 8, 5, 5) into w21; nconv1's s1 recomputed in-kernel with nconv_weight_prep's
+ * arithmetic; skipped when w21 is NULL) and the phase weights of nphase UpCat layers
+ * (nconv_phase_weights' arguments). Every output is bitwise what the three separate calls write;
+ * the roles read the weights only, so they need no order (replaces three launches per forward). */
+int nconv_weight_prologue(int n, float* const* weights, const int* couts, const int* fan_ins,
+                          float* const* wsums, const float* head_w1, const float* head_w2, float* w21,
+                          int nphase, const float* const* phase_weights, const int* phase_cins,
+                          const int* phase_up_first, float* const* wphases, void* stream);
+
 /* Forward of one NConv2d with fused input glue.
  * Replaces models/step1.py:119-147 (2x F.conv2d, mul, div, bias add, confidence normalisation)
  * plus the glue op that feeds it (step1.py:53 / 62-75 / 78-90).

@@ -40,6 +40,7 @@ EXPORTED = (
     "nconv_plan",
     "nconv_phase_weights_floats",
     "nconv_phase_weights",
+    "nconv_weight_prologue",
     "nconv_bwd_workspace_bytes",
     "nconv_bwd",
     "nconv_bwd_ex",
@@ -143,6 +144,8 @@ def _declare(lib):
     lib.nconv_phase_weights_floats.argtypes = [ctypes.POINTER(NconvLayer)]
     lib.nconv_phase_weights.restype = ctypes.c_int
     lib.nconv_phase_weights.argtypes = [ctypes.c_int, P, P, P, P, P]
+    lib.nconv_weight_prologue.restype = ctypes.c_int
+    lib.nconv_weight_prologue.argtypes = [ctypes.c_int, P, P, P, P, P, P, P, ctypes.c_int, P, P, P, P, P]
     lib.nconv_bwd_workspace_bytes.restype = ctypes.c_size_t
     lib.nconv_bwd_workspace_bytes.argtypes = [ctypes.POINTER(NconvLayer)]
     lib.nconv_bwd.restype = ctypes.c_int

@@ -241,6 +241,30 @@ int nconv_phase_weights(int n, const float* const* weights, const int* cins, con
     return rc ? fail(rc, fn, why) : 0;
 }
 
+int nconv_weight_prologue(int n, float* const* weights, const int* couts, const int* fan_ins,
+                          float* const* wsums, const float* head_w1, const float* head_w2, float* w21,
+                          int nphase, const float* const* phase_weights, const int* phase_cins,
+                          const int* phase_up_first, float* const* wphases, void* stream) {
+    const char* fn = "nconv_weight_prologue";
+    if (n < 0 || nphase < 0) return fail(-22, fn, "negative count");
+    if (n > 0 && (!weights || !couts || !fan_ins || !wsums)) return fail(-22, fn, "null argument");
+    for (int i = 0; i < n; ++i)
+        if (!weights[i] || !wsums[i] || couts[i] <= 0 || fan_ins[i] <= 0) return fail(-22, fn, "bad layer entry");
+    if (w21 && (!head_w1 || !head_w2)) return fail(-22, fn, "head weights need head_w1 and head_w2");
+    if (nphase > 0 && (!phase_weights || !phase_cins || !phase_up_first || !wphases))
+        return fail(-22, fn, "null phase argument");
+    for (int i = 0; i < nphase; ++i) {
+        if (!phase_weights[i] || !wphases[i]) return fail(-22, fn, "null phase weight / output");
+        if (phase_up_first[i] < 0 || phase_up_first[i] + 8 > phase_cins[i])
+            return fail(-22, fn, "upsampled channels outside [0, Cin)");
+    }
+    const char* why = nullptr;
+    int rc = nconv::launch_weight_prologue(n, weights, couts, fan_ins, wsums, head_w1, head_w2, w21, nphase,
+                                           phase_weights, phase_cins, phase_up_first, wphases,
+                                           (hipStream_t)stream, &why);
+    return rc ? fail(rc, fn, why) : 0;
+}
+
 size_t nconv_bwd_workspace_bytes(const nconv_layer* L) {
     if (validate(L, true)) return 0;
     return nconv::bwd_workspace_bytes(make_dev(L));

@@ -16,7 +16,7 @@
 // while staging, so glued tensors never hit HBM. CS = 1 for the full- and half-resolution layers;
 // the small layers split the channels so their few pixels still fill the chip (go_tiled).
 #include <cstdlib>
-#include "nconv_internal.h"
+#include "nconv_prologue.h"
 
 namespace nconv {
 
@@ -341,40 +341,10 @@ __global__ __launch_bounds__(kThreads) void fwd_generic(LayerDev d, float* __res
     }
 }
 
-// EnforcePos (softplus, beta=10, threshold=20; step1.py:190-207) in place + s[o] = sum W[o].
-struct PrepArgs {
-    static constexpr int kMax = 32;
-    float* w[kMax];
-    float* s[kMax];
-    int cout[kMax];
-    int fan_in[kMax];
-    int softplus[kMax];
-};
-
-__global__ __launch_bounds__(kThreads) void weight_prep(PrepArgs a) {
+// EnforcePos + normalisers (PrepArgs, prep_block: nconv_prologue.h), one block per layer.
+__global__ __launch_bounds__(kPrepThreads) void weight_prep(PrepArgs a) {
     const int l = blockIdx.x;
-    float* w = a.w[l];
-    const int n = a.cout[l] * a.fan_in[l];
-    if (a.softplus[l]) {
-        for (int i = threadIdx.x; i < n; i += kThreads) {
-            const float v = w[i];
-            const float bv = v * 10.0f;
-            w[i] = (bv > 20.0f) ? v : log1pf(expf(bv)) / 10.0f;
-        }
-        __syncthreads();
-        __threadfence_block();
-    }
-    // s[o] = sum of row o: one wave per row (lanes stride the row, coalesced; a fixed-order
-    // butterfly combines them), instead of one thread walking ~200 dependent loads (~20 us)
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, fan = a.fan_in[l];
-    for (int o = wave; o < a.cout[l]; o += kThreads / 64) {
-        const float* wr = w + (size_t)o * fan;
-        float s = 0.f;
-        for (int i = lane; i < fan; i += 64) s += wr[i];
-#pragma unroll
-        for (int m = 32; m > 0; m >>= 1) s += __shfl_xor(s, m);
-        if (lane == 0) a.s[l][o] = s;
-    }
+    prep_block(a.w[l], a.s[l], a.cout[l], a.fan_in[l], a.softplus[l]);
 }
 
 }  // namespace nconv
@@ -548,7 +518,7 @@ int launch_weight_prep(int n, float* const* w, const int* cout, const int* fan_i
         a.fan_in[i] = fan_in[i];
         a.softplus[i] = sp ? sp[i] : 0;
     }
-    hipLaunchKernelGGL(weight_prep, dim3(n), dim3(kThreads), 0, st, a);
+    hipLaunchKernelGGL(weight_prep, dim3(n), dim3(kPrepThreads), 0, st, a);
     return last_launch(why);
 }
 

@@ -25,7 +25,7 @@
 //     plain convolution; those tiles sum W2 * c1 from nconv1's c1 as the unfused path does.
 // Interior-tile outputs therefore differ from the unfused exact pair only through D2's rounding;
 // N2, nconv1 and the edge tiles match it bit for bit.
-#include "nconv_internal.h"
+#include "nconv_prologue.h"
 
 namespace nconv {
 
@@ -370,9 +370,12 @@ __device__ __forceinline__ int frag_slot(int o, int part, int chunk, int j) {
     return (((o >> 2) * 3 + ks) * 64 + g * 16 + row) * 8 + j;  // bf16 index
 }
 
-__global__ __launch_bounds__(64) void head_weights(const float* __restrict__ w1, const float* __restrict__ s1,
-                                                   const float* __restrict__ w2, float* __restrict__ out) {
-    const int blk = blockIdx.x, lane = threadIdx.x;
+// One unit of nconv_head_weights per wave: units 0..80 the composed tap (qh, qw) = (u / 9, u % 9),
+// 81 the transposed W2, 82 the zero padding of the fragment table. s1i = s1[lane & 7].
+constexpr int kHeadUnits = 83;
+__device__ __forceinline__ void head_weights_unit(const float* __restrict__ w1, float s1i,
+                                                  const float* __restrict__ w2, float* __restrict__ out,
+                                                  int blk, int lane) {
     unsigned short* const fb = reinterpret_cast<unsigned short*>(out);
     if (blk == 81) {
         for (int e = lane; e < 1600; e += 64) {  // W2t[ci][kh][kw][o] = W2[o][ci][kh][kw]
@@ -400,7 +403,7 @@ __global__ __launch_bounds__(64) void head_weights(const float* __restrict__ w1,
             si += (double)w2[((o * 8 + i) * 5 + kh) * 5 + kw] * (double)w1[(i * 5 + kh1) * 5 + kw1];
         }
     }
-    si /= (double)s1[i];
+    si /= (double)s1i;
 #pragma unroll
     for (int m = 1; m < 8; m <<= 1) si += __shfl_xor(si, m);
     if (i == 0) {
@@ -415,6 +418,42 @@ __global__ __launch_bounds__(64) void head_weights(const float* __restrict__ w1,
         fb[frag_slot(o, 1, chunk, j)] = (unsigned short)(__float_as_uint(mid) >> 16);
         fb[frag_slot(o, 2, chunk, j)] = (unsigned short)(__float_as_uint(lo) >> 16);
     }
+}
+
+__global__ __launch_bounds__(64) void head_weights(const float* __restrict__ w1, const float* __restrict__ s1,
+                                                   const float* __restrict__ w2, float* __restrict__ out) {
+    head_weights_unit(w1, s1[threadIdx.x & 7], w2, out, blockIdx.x, threadIdx.x);
+}
+
+// The inference weight prologue in one launch (nconv_weight_prologue): blocks [0, nprep) the
+// normalisers of the layers (prep_block, no softplus: eval mode), then the head's units four per
+// block (a wave each; nconv1's s1 recomputed by the wave with row_sum_wave, the arithmetic of
+// prep_block, so bitwise the normaliser nconv_weight_prep writes), then one block per phase-weight
+// layer. Every block reads the weights only, so no order between the roles is needed.
+__global__ __launch_bounds__(kPrepThreads) void weight_prologue(PrepArgs prep, int nprep, const float* __restrict__ w1,
+                                                                 const float* __restrict__ w2, float* __restrict__ w21,
+                                                                 PhaseArgs ph, int nphase) {
+    const int nhead = w21 ? (kHeadUnits + 3) / 4 : 0;
+    int blk = blockIdx.x;
+    if (blk < nprep) {
+        prep_block(prep.w[blk], prep.s[blk], prep.cout[blk], prep.fan_in[blk], 0);
+        return;
+    }
+    blk -= nprep;
+    if (blk < nhead) {
+        const int lane = threadIdx.x & 63, unit = 4 * blk + (threadIdx.x >> 6);
+        if (unit >= kHeadUnits) return;
+        float s1i = 0.f;
+#pragma unroll 1
+        for (int r = 0; r < 8; ++r) {
+            const float v = row_sum_wave(w1 + r * 25, 25, lane);
+            if ((lane & 7) == r) s1i = v;
+        }
+        head_weights_unit(w1, s1i, w2, w21, unit, lane);
+        return;
+    }
+    blk -= nhead;
+    if (blk < nphase) phase_block(ph.w[blk], ph.cin[blk], ph.ci0[blk], ph.out[blk]);
 }
 
 }  // namespace
@@ -433,9 +472,42 @@ int launch_fwd_head_exact(const LayerDev& d2, const TailArgs& t, float* y, float
     return 0;
 }
 
+int launch_weight_prologue(int n, float* const* w, const int* cout, const int* fan_in, float* const* s,
+                           const float* w1, const float* w2, float* w21, int nphase, const float* const* pw,
+                           const int* pcin, const int* pup_first, float* const* pout, hipStream_t st,
+                           const char** why) {
+    if (n < 0 || n > PrepArgs::kMax || nphase < 0 || nphase > PhaseArgs::kMax) {
+        *why = "too many layers for one nconv_weight_prologue launch (max 32 normalisers, 8 phase layers)";
+        return -22;
+    }
+    PrepArgs a{};
+    for (int i = 0; i < n; ++i) {
+        a.w[i] = w[i];
+        a.s[i] = s[i];
+        a.cout[i] = cout[i];
+        a.fan_in[i] = fan_in[i];
+    }
+    PhaseArgs p{};
+    for (int i = 0; i < nphase; ++i) {
+        p.w[i] = pw[i];
+        p.out[i] = pout[i];
+        p.ci0[i] = pup_first[i];
+        p.cin[i] = pcin[i];
+    }
+    const int blocks = n + (w21 ? (kHeadUnits + 3) / 4 : 0) + nphase;
+    if (blocks == 0) return 0;
+    hipLaunchKernelGGL(weight_prologue, dim3(blocks), dim3(kPrepThreads), 0, st, a, n, w1, w2, w21, p, nphase);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        *why = hipGetErrorString(e);
+        return -5;
+    }
+    return 0;
+}
+
 int launch_head_weights(const float* w1, const float* s1, const float* w2, float* out, hipStream_t st,
                         const char** why) {
-    hipLaunchKernelGGL(head_weights, dim3(83), dim3(64), 0, st, w1, s1, w2, out);
+    hipLaunchKernelGGL(head_weights, dim3(kHeadUnits), dim3(64), 0, st, w1, s1, w2, out);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         *why = hipGetErrorString(e);

@@ -21,7 +21,7 @@
 // thread), with one difference: a wave owns four rows of one parity (rows w&1, w&1 + 2, ... of its
 // 8-row half), so the phase -- and with it the phase weights -- is wave-uniform and the weights
 // ride the scalar cache.
-#include "nconv_internal.h"
+#include "nconv_prologue.h"
 
 namespace nconv {
 
@@ -279,34 +279,10 @@ __global__ __launch_bounds__(kPT) void fwd_phase(LayerDev d, float* __restrict__
     }
 }
 
-// Phase weights of the upsampled channels of n UPCAT layers, one workgroup per layer:
-// out[((i * 2 + a) * 2 + dh) * 32 + o * 4 + bt * 2 + dw] = sum over kh in S(a, dh), kw in S(bt, dw)
-// of W[o][ci][kh][kw] (kh ascending, then kw), ci = the layer's input channel of up channel i;
-// S(0,0) = {0,1}, S(0,1) = {2}, S(1,0) = {0}, S(1,1) = {1,2}.
-struct PhaseArgs {
-    static constexpr int kMax = 8;
-    const float* w[kMax];
-    float* out[kMax];
-    int ci0[kMax];  // input channel of up channel 0
-    int cin[kMax];
-};
-
-__global__ __launch_bounds__(256) void phase_weights(PhaseArgs a) {
+// Phase weights of n UPCAT layers (PhaseArgs, phase_block: nconv_prologue.h), one block per layer.
+__global__ __launch_bounds__(kPrepThreads) void phase_weights(PhaseArgs a) {
     const int l = blockIdx.x;
-    const float* W = a.w[l];
-    const int cin = a.cin[l];
-    for (int e = threadIdx.x; e < kPCB * 2 * 2 * 32; e += blockDim.x) {
-        const int i = e >> 7, al = (e >> 6) & 1, dh = (e >> 5) & 1, o = (e >> 2) & 7, bt = (e >> 1) & 1, dw = e & 1;
-        const int kh_lo = al == 0 ? (dh == 0 ? 0 : 2) : (dh == 0 ? 0 : 1);
-        const int kh_hi = al == 0 ? (dh == 0 ? 1 : 2) : (dh == 0 ? 0 : 2);
-        const int kw_lo = bt == 0 ? (dw == 0 ? 0 : 2) : (dw == 0 ? 0 : 1);
-        const int kw_hi = bt == 0 ? (dw == 0 ? 1 : 2) : (dw == 0 ? 0 : 2);
-        const float* wo = W + ((size_t)o * cin + a.ci0[l] + i) * 9;
-        float s = 0.f;
-        for (int kh = kh_lo; kh <= kh_hi; ++kh)
-            for (int kw = kw_lo; kw <= kw_hi; ++kw) s += wo[kh * 3 + kw];
-        a.out[l][e] = s;
-    }
+    phase_block(a.w[l], a.cin[l], a.ci0[l], a.out[l]);
 }
 
 }  // namespace
@@ -370,7 +346,7 @@ int launch_phase_weights(int n, const float* const* w, const int* cin, const int
         a.ci0[i] = up_first[i];
         a.cin[i] = cin[i];
     }
-    hipLaunchKernelGGL(phase_weights, dim3(n), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(phase_weights, dim3(n), dim3(kPrepThreads), 0, st, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         *why = hipGetErrorString(e);

@@ -106,6 +106,10 @@ int launch_fwd_head(const LayerDev& d2, const TailArgs& t, float* y, float* yc, 
 // exact-fp32 fused head (nconv_fwd_head.hip); d2.L.waux = the composed confidence weights
 int launch_fwd_head_exact(const LayerDev& d2, const TailArgs& t, float* y, float* yc, hipStream_t st,
                           const char** why);
+int launch_weight_prologue(int n, float* const* w, const int* cout, const int* fan_in, float* const* s,
+                           const float* w1, const float* w2, float* w21, int nphase, const float* const* pw,
+                           const int* pcin, const int* pup_first, float* const* pout, hipStream_t st,
+                           const char** why);
 int launch_head_weights(const float* w1, const float* s1, const float* w2, float* out, hipStream_t st,
                         const char** why);
 int launch_fwd_tail(const LayerDev& d, const TailArgs& t, float* out, hipStream_t st, const char** why);

@@ -1,0 +1,80 @@
+// nconv_prologue.h — bodies of the weight-only prologue kernels, shared by their own launches
+// (nconv_weight_prep, nconv_phase_weights) and by the one-launch inference prologue
+// (nconv_weight_prologue, nconv_fwd_head.hip), so that every output is bitwise the same whichever
+// launch computes it.
+#pragma once
+#include "nconv_internal.h"
+
+namespace nconv {
+
+constexpr int kPrepThreads = 256;  // threads of a prep / phase block
+
+// EnforcePos (softplus, beta=10, threshold=20; step1.py:190-207) in place + s[o] = sum W[o].
+struct PrepArgs {
+    static constexpr int kMax = 32;
+    float* w[kMax];
+    float* s[kMax];
+    int cout[kMax];
+    int fan_in[kMax];
+    int softplus[kMax];
+};
+
+// The normaliser of one weight row (step1.py:141-144) by one wave: lane-strided partial sums, then
+// a fixed-order xor butterfly (every lane ends with the same value).
+__device__ __forceinline__ float row_sum_wave(const float* wr, int fan, int lane) {
+    float s = 0.f;
+    for (int i = lane; i < fan; i += 64) s += wr[i];
+#pragma unroll
+    for (int m = 32; m > 0; m >>= 1) s += __shfl_xor(s, m);
+    return s;
+}
+
+// One layer per 256-thread block: optional in-place softplus, then one wave per row for s[o]
+// (lanes stride the row, coalesced), instead of one thread walking ~200 dependent loads.
+__device__ __forceinline__ void prep_block(float* w, float* s, int cout, int fan, int softplus) {
+    const int n = cout * fan;
+    if (softplus) {
+        for (int i = threadIdx.x; i < n; i += kPrepThreads) {
+            const float v = w[i];
+            const float bv = v * 10.0f;
+            w[i] = (bv > 20.0f) ? v : log1pf(expf(bv)) / 10.0f;
+        }
+        __syncthreads();
+        __threadfence_block();
+    }
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int o = wave; o < cout; o += kPrepThreads / 64) {
+        const float v = row_sum_wave(w + (size_t)o * fan, fan, lane);
+        if (lane == 0) s[o] = v;
+    }
+}
+
+// Phase weights of the upsampled channels of n UPCAT layers (nconv_fwd_phase.hip), one block per
+// layer: out[((i * 2 + a) * 2 + dh) * 32 + o * 4 + bt * 2 + dw] = sum over kh in S(a, dh), kw in
+// S(bt, dw) of W[o][ci][kh][kw] (kh ascending, then kw), ci = the layer's input channel of up
+// channel i; S(0,0) = {0,1}, S(0,1) = {2}, S(1,0) = {0}, S(1,1) = {1,2}.
+struct PhaseArgs {
+    static constexpr int kMax = 8;
+    const float* w[kMax];
+    float* out[kMax];
+    int ci0[kMax];  // input channel of up channel 0
+    int cin[kMax];
+};
+
+__device__ __forceinline__ void phase_block(const float* W, int cin, int ci0, float* out) {
+    constexpr int kUp = 8;  // upsampled input channels (and output channels) of the phase form
+    for (int e = threadIdx.x; e < kUp * 2 * 2 * 32; e += kPrepThreads) {
+        const int i = e >> 7, al = (e >> 6) & 1, dh = (e >> 5) & 1, o = (e >> 2) & 7, bt = (e >> 1) & 1, dw = e & 1;
+        const int kh_lo = al == 0 ? (dh == 0 ? 0 : 2) : (dh == 0 ? 0 : 1);
+        const int kh_hi = al == 0 ? (dh == 0 ? 1 : 2) : (dh == 0 ? 0 : 2);
+        const int kw_lo = bt == 0 ? (dw == 0 ? 0 : 2) : (dw == 0 ? 0 : 1);
+        const int kw_hi = bt == 0 ? (dw == 0 ? 1 : 2) : (dw == 0 ? 0 : 2);
+        const float* wo = W + ((size_t)o * cin + ci0 + i) * 9;
+        float s = 0.f;
+        for (int kh = kh_lo; kh <= kh_hi; ++kh)
+            for (int kw = kw_lo; kw <= kw_hi; ++kw) s += wo[kh * 3 + kw];
+        out[e] = s;
+    }
+}
+
+}  // namespace nconv

@@ -320,6 +320,49 @@ class DNET(nn.Module):
         weight_prep(weights, batched_sp, wsums)
         return wsums
 
+    # The eval-mode forward builds its weight-only prologue -- the normalisers, the exact head's
+    # composed weights and nconv4/5/6's phase weights -- in one launch (nconv_weight_prologue,
+    # bitwise the three separate launches); False: the separate launches.
+    merged_prologue = True
+
+    def _eval_prologue(self, layers, S):
+        """(wsums, phase weights or None, head weights or None) from one nconv_weight_prologue
+        launch, or None where the separate path must run: merged_prologue off, a layer in training
+        mode (EnforcePos then rewrites the weights first), a forward pre-hook other than this
+        package's EnforcePos, or weights that are not contiguous fp32 device tensors."""
+        if not self.merged_prologue:
+            return None
+        for m in layers:
+            hooks = list(m._forward_pre_hooks.values())
+            ours = len(hooks) == 1 and isinstance(hooks[0], EnforcePos) and hooks[0].name == "weight" \
+                and hooks[0].pos_fn.lower() == "softplus"
+            if m.training or not (len(hooks) == 0 or ours):
+                return None
+            w = m.weight
+            if not (w.is_cuda and w.dtype == torch.float32 and w.is_contiguous()):
+                return None
+        dev = S.device
+        weights = [m.weight.data for m in layers]
+        buf = torch.empty(sum(w.shape[0] for w in weights), device=dev, dtype=torch.float32)
+        wsums, off = [], 0
+        for w in weights:
+            wsums.append(buf[off:off + w.shape[0]])
+            off += w.shape[0]
+        head = None
+        l1, l2 = layers[0], layers[1]
+        if nconv.FORWARD_MATH == _lib.MATH_FP32 and self._use_head(l1, l2):
+            head = (l1.weight.data, l2.weight.data,
+                    torch.empty(nconv.HEAD_WEIGHTS_FLOATS, device=dev, dtype=torch.float32))
+        phase, wph = None, None
+        ls = (self.nconv4, self.nconv5, self.nconv6)
+        if self.phase_upcat and nconv.FORWARD_MATH == _lib.MATH_FP32 and all(
+                m.weight.shape[0] == 8 and m.weight.shape[1] == 16 and tuple(m.weight.shape[2:]) == (3, 3)
+                and m.weight.is_contiguous() for m in ls):
+            wph = torch.empty((3, 1024), device=dev, dtype=torch.float32)
+            phase = ([m.weight.data for m in ls], [8, 8, 0], list(wph))
+        nconv.weight_prologue(weights, wsums, head=head, phase=phase)
+        return wsums, wph, (head[2] if head is not None else None)
+
     # -- forward ----------------------------------------------------------------------------------
     def forward(self, S):
         if export.is_exporting():  # the export graph: the reference's own ops (export.py)
@@ -329,18 +372,23 @@ class DNET(nn.Module):
             raise ValueError(f"DNET expects (B, 1, H, W) sparse depth, got {tuple(S.shape)}")
         S = S.contiguous()
         layers = [getattr(self, n) for n in LAYERS]
-        wsum = self._prologue(layers, S)
-        (l1, l2, d1, d2, d3, l4, l5, l6, l7) = layers
-        (s1, s2, sd1, sd2, sd3, s4, s5, s6, s7) = wsum
         grad = torch.is_grad_enabled() and (S.requires_grad or any(p.requires_grad for p in self.parameters()))
         H, W = S.shape[2], S.shape[3]
         out_h, out_w = crop_hw(H, W, self.crop)
-        f = nconv_layer if grad else (lambda spec, *a, wphase=None: layer_forward_raw(spec, *a, wphase=wphase))
-
         if not grad and min(H, W) >= 16:
             out = torch.empty((S.shape[0], 1, out_h, out_w), device=S.device, dtype=torch.float32)
-            self._infer_split(S, layers, wsum, out, self._phase_weights(S.device))
+            pro = self._eval_prologue(layers, S)
+            if pro is None:
+                wsum, wph, w21 = self._prologue(layers, S), self._phase_weights(S.device), None
+            else:
+                wsum, wph, w21 = pro
+            self._infer_split(S, layers, wsum, out, wph, w21)
             return out
+
+        wsum = self._prologue(layers, S)
+        (l1, l2, d1, d2, d3, l4, l5, l6, l7) = layers
+        (s1, s2, sd1, sd2, sd3, s4, s5, s6, s7) = wsum
+        f = nconv_layer if grad else (lambda spec, *a, wphase=None: layer_forward_raw(spec, *a, wphase=wphase))
 
         if grad and self.whole_graph_autograd and S.shape[0] > 0:
             specs = (l1.spec(_lib.THRESH, 0.01), l2.spec(), d1.spec(_lib.POOL2), d2.spec(_lib.POOL2),
@@ -412,11 +460,11 @@ class DNET(nn.Module):
             cache[key] = [torch.cuda.Stream(device=device) for _ in range(n)]
         return cache[key]
 
-    def _infer_split(self, S, layers, wsum, out, wph=None):
+    def _infer_split(self, S, layers, wsum, out, wph=None, w21=None):
         B = S.shape[0]
         n = self._n_streams(B)
         if n == 1:
-            self._infer(S, layers, wsum, out, wph)
+            self._infer(S, layers, wsum, out, wph, w21=w21)
             return
         cur = torch.cuda.current_stream(S.device)
         side = self._side_streams(S.device, n - 1)
@@ -433,15 +481,17 @@ class DNET(nn.Module):
             if bounds[k + 1] == bounds[k]:
                 continue
             with torch.cuda.stream(st):
-                self._infer(S[bounds[k]:bounds[k + 1]], layers, wsum, out[bounds[k]:bounds[k + 1]], wph, mid=False)
+                self._infer(S[bounds[k]:bounds[k + 1]], layers, wsum, out[bounds[k]:bounds[k + 1]], wph, mid=False,
+                            w21=w21)
         for st in side:
             cur.wait_stream(st)
 
-    def _infer(self, S, layers, wsum, out, wph=None, mid=True):
+    def _infer(self, S, layers, wsum, out, wph=None, mid=True, w21=None):
         """The inference chain on the current stream: each producer also writes the pooled input
         of the next down layer, and nconv6+nconv7+crop run as one launch writing `out`. wph: the
         phase weights of nconv4/5/6 (_phase_weights) or None. mid=False (inside an inference
-        split): no nested mid_streams split."""
+        split): no nested mid_streams split. w21: the exact head's weights when the prologue
+        already built them (_eval_prologue), else built here."""
         (l1, l2, d1, d2, d3, l4, l5, l6, l7) = layers
         (s1, s2, sd1, sd2, sd3, s4, s5, s6, s7) = wsum
         w4, w5, w6 = (None, None, None) if wph is None else tuple(wph)
@@ -449,8 +499,7 @@ class DNET(nn.Module):
         if self._use_head(l1, l2):
             # nconv1 inside nconv2's staging: its 8-channel output never reaches HBM
             sp1, sp2 = l1.spec(_lib.THRESH, 0.01), l2.spec()
-            w21 = None
-            if nconv.FORWARD_MATH == _lib.MATH_FP32:  # the exact head's composed confidence weights
+            if w21 is None and nconv.FORWARD_MATH == _lib.MATH_FP32:  # the exact head's composed weights
                 w21 = head_weights(sp1, sp2, S, l1.weight, l1.bias, s1, l2.weight, l2.bias, s2)
             x1, c1, p1, q1 = layer_forward_head(sp1, sp2, S, l1.weight, l1.bias, s1, l2.weight, l2.bias, s2, w21)
         else:

@@ -140,6 +140,32 @@ def phase_weights(weights, up_first, outs):
     _lib.check(rc, "nconv_phase_weights")
 
 
+def weight_prologue(weights, wsums, head=None, phase=None):
+    """nconv_weight_prologue: the eval-mode weight prologue in one launch, bitwise what
+    weight_prep(weights, [False] * n, wsums) + head_weights + phase_weights write.
+    head: (w1, w2, out) -- nconv1 (8, 1, 5, 5), nconv2 (8, 8, 5, 5), HEAD_WEIGHTS_FLOATS out -- or
+    None; phase: (weights, up_first, outs) as phase_weights' arguments, or None."""
+    n = len(weights)
+    w1, w2, w21 = head if head is not None else (None, None, None)
+    pw, pup, pout = phase if phase is not None else ([], [], [])
+    if w21 is not None and (w21.numel() < HEAD_WEIGHTS_FLOATS or not w21.is_contiguous() or
+                            w21.dtype != torch.float32):
+        raise ValueError(f"head-weight buffer needs {HEAD_WEIGHTS_FLOATS} contiguous fp32 elements")
+    for o in pout:
+        if o.numel() < PHASE_WEIGHT_FLOATS or not o.is_contiguous() or o.dtype != torch.float32:
+            raise ValueError(f"phase-weight buffers need {PHASE_WEIGHT_FLOATS} contiguous fp32 elements")
+    m = len(pw)
+    P, I = _lib.ctypes.c_void_p, _lib.ctypes.c_int
+    dev = (weights[0] if n else (w1 if w1 is not None else pw[0])).device
+    rc = _lib.lib().nconv_weight_prologue(
+        n, (P * max(n, 1))(*[w.data_ptr() for w in weights]), (I * max(n, 1))(*[w.shape[0] for w in weights]),
+        (I * max(n, 1))(*[w[0].numel() for w in weights]), (P * max(n, 1))(*[s.data_ptr() for s in wsums]),
+        _lib.ptr(w1), _lib.ptr(w2), _lib.ptr(w21),
+        m, (P * max(m, 1))(*[w.data_ptr() for w in pw]), (I * max(m, 1))(*[w.shape[1] for w in pw]),
+        (I * max(m, 1))(*pup), (P * max(m, 1))(*[o.data_ptr() for o in pout]), _lib.stream_handle(dev))
+    _lib.check(rc, "nconv_weight_prologue")
+
+
 def layer_forward_raw(spec: LayerSpec, xa, ca, xb, cb, weight, bias, wsum, out=None, wphase=None):
     """Enqueue nconv_fwd; returns (y, cout) (written into `out` if given). No autograd. `wphase`:
     the layer's phase weights (UPCAT layers, phase_weights), or None."""

@@ -236,3 +236,25 @@ def test_plan_follows_requested_math(nconv_amd, math, expect):
     assert _plan(nconv_amd, L7) == ("tiled_fp32",) * 3
     # other geometries: the generic kernels whatever the math
     assert _plan(nconv_amd, _layer(nconv_amd, SH=2, SW=2, Ho=8, Wo=8, math=m, bwd_math=m)) == ("generic",) * 3
+
+
+def test_weight_prologue_validation_is_host_only(nconv_amd):
+    """nconv_weight_prologue rejects malformed arguments on the host with -22 before any launch."""
+    lib = nconv_amd._lib.lib()
+    P, I = ctypes.c_void_p, ctypes.c_int
+    p = P(0x1000)
+    w, s = (P * 1)(p), (P * 1)(p)
+    cout, fan = (I * 1)(8), (I * 1)(25)
+    pw, po = (P * 1)(p), (P * 1)(p)
+    cin, up = (I * 1)(16), (I * 1)(8)
+    cases = [
+        ((-1, w, cout, fan, s, None, None, None, 0, None, None, None, None, None), "negative count"),
+        ((1, None, cout, fan, s, None, None, None, 0, None, None, None, None, None), "null argument"),
+        ((1, w, (I * 1)(0), fan, s, None, None, None, 0, None, None, None, None, None), "bad layer entry"),
+        ((1, w, cout, fan, s, None, p, p, 0, None, None, None, None, None), "head_w1 and head_w2"),
+        ((0, None, None, None, None, None, None, None, 1, None, cin, up, po, None), "null phase argument"),
+        ((0, None, None, None, None, None, None, None, 1, pw, cin, (I * 1)(9), po, None), "outside [0, Cin)"),
+    ]
+    for args, msg in cases:
+        assert lib.nconv_weight_prologue(*args) == -22, msg
+        assert msg in lib.nconv_last_error().decode(), msg

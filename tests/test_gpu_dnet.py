@@ -390,3 +390,53 @@ def test_frozen_layers_fused_tail_matches_unfused(nconv_amd, gpu, monkeypatch, f
         assert torch.isfinite(a).all(), n
         rel = ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
         assert rel <= 1e-5, f"{n}: {rel:.2e}"
+
+
+def test_weight_prologue_bitwise_separate_launches(nconv_amd, gpu):
+    """nconv_weight_prologue (one launch) writes bitwise what nconv_weight_prep (no softplus),
+    nconv_head_weights and nconv_phase_weights write as separate launches."""
+    N = nconv_amd.nconv
+    net = make_net(nconv_amd, "generalized", gpu)
+    layers = [getattr(net.d_net, n) for n in nconv_amd.dnet.LAYERS]
+    ws = [m.weight.detach() for m in layers]
+    sa = [torch.empty(w.shape[0], device=gpu) for w in ws]
+    sb = [torch.empty(w.shape[0], device=gpu) for w in ws]
+    N.weight_prep(ws, [False] * len(ws), sa)
+    l1, l2 = layers[0], layers[1]
+    sp1, sp2 = l1.spec(nconv_amd._lib.THRESH, 0.01), l2.spec()
+    S = torch.zeros(1, 1, 32, 32, device=gpu)
+    ha = N.head_weights(sp1, sp2, S, ws[0], l1.bias.detach(), sa[0], ws[1], l2.bias.detach(), sa[1])
+    pws = [ws[5], ws[6], ws[7]]
+    pa = [torch.empty(1024, device=gpu) for _ in range(3)]
+    N.phase_weights(pws, [8, 8, 0], pa)
+    hb = torch.full((N.HEAD_WEIGHTS_FLOATS,), float("nan"), device=gpu)
+    pb = [torch.full((1024,), float("nan"), device=gpu) for _ in range(3)]
+    N.weight_prologue(ws, sb, head=(ws[0], ws[1], hb), phase=(pws, [8, 8, 0], pb))
+    torch.cuda.synchronize()
+    for a, b in zip(sa, sb):
+        assert torch.equal(a, b)
+    assert torch.equal(ha.view(torch.int32), hb.view(torch.int32))
+    for a, b in zip(pa, pb):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("B,H,W", [(2, 64, 96), (8, 352, 1216)])
+def test_dnet_eval_merged_prologue_bitwise(nconv_amd, gpu, B, H, W):
+    """The eval forward with its one-launch weight prologue equals the separate-launch path
+    bitwise, and a weight changed in place between forwards is picked up (no stale prologue)."""
+    net = make_net(nconv_amd, "generalized", gpu)
+    d = net.d_net
+    g = torch.Generator().manual_seed(B * 7 + H)
+    S = sparse_depth(g, B, H, W).to(gpu)
+    with torch.no_grad():
+        d.merged_prologue = False
+        a = net(S)
+        d.merged_prologue = True
+        b = net(S)
+        assert torch.equal(a, b)
+        d.nconv6.weight.mul_(1.5)
+        d.nconv2.weight.mul_(0.75)
+        c = net(S)
+        d.merged_prologue = False
+        e = net(S)
+    assert torch.equal(c, e) and not torch.equal(b, c)

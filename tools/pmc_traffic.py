@@ -69,7 +69,8 @@ ORDER_UNFUSED = ["nconv1", "nconv2"] + ORDER[1:]
 
 def _read(dirpath, counter):
     """Per layer mean of `counter` over the timed inference forwards. Dispatches are taken in
-    order: an inference forward is weight_prep followed by the 7 layer launches of ORDER (8 without
+    order: an inference forward is its weight prologue (weight_prologue; weight_prep before round
+    4's one-launch prologue) followed by the 7 layer launches of ORDER (8 without
     the fused head; the warm-up training forward has 9 and is skipped)."""
     files = glob.glob(os.path.join(dirpath, "**", "*counter_collection.csv"), recursive=True)
     if not files:
@@ -82,7 +83,7 @@ def _read(dirpath, counter):
         if "fwd_tiled<8, 1, 1," in name and int(r["Grid_Size"]) >= 1 << 20:
             calib.append(float(r["Counter_Value"]))
             cur = None
-        elif "weight_prep" in name:
+        elif "weight_prep" in name or "weight_prologue" in name:  # a forward's first launch
             cur = []
             groups.append(cur)
         elif cur is not None and "nconv::" in name and "phase_weights" not in name and "head_weights" not in name:
