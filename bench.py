@@ -315,6 +315,10 @@ def roofline(layer_us, costs, math, B, H, W, issued_mfma=None):
                          "frac": round(etf / FP32_PEAK_TFLOPS, 4),
                          "valu_busy_frac": round(ex["valu_cycles_per_simd"] / (us * 1e-6 * 2.4e9), 4),
                          "source": "profiles/sq_exec.json (SQ_INSTS_VALU_FMA_F32, SQ_INSTS_VALU per launch)"}
+        if ex.get("mfma_insts_per_launch"):  # the head's exact confidence mass on the bf16 matrix cores
+            # v_mfma_f32_16x16x32_bf16: 16384 flop = 16 cycles of one SIMD at the dense bf16 rate
+            r["executed"]["bf16_mfma_busy_frac"] = round(
+                ex["mfma_insts_per_launch"] * 16 / 1024 / (us * 1e-6 * 2.4e9), 4)
     if issued_mfma:
         r["mfma_issued_bf16_tflops"] = round(issued_mfma(dom) / (us * 1e-6) / 1e12, 2)
         r["mfma_bf16_dense_peak_tflops"] = MFMA_BF16_PEAK_TFLOPS
