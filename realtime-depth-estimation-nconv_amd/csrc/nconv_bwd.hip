@@ -1147,15 +1147,25 @@ struct WmCfg {
     static constexpr int TW = 64;
     static constexpr int M = CIN * K, N = COUT * K;
     static constexpr int MT = (M + 15) / 16, NT = (N + 15) / 16;
-    static constexpr int XP = TW + 4;  // staged row pitch: channel rows 4 banks apart
+    // LDS banks of the operand reads (ds_read_b32: bank = dword address mod 32, the two 32-lane
+    // halves separate; a half holds k = lane >> 4 in {0, 1} (or {2, 3}) x 16 rows / columns):
+    // A: row m = (kh, i) at slot(kh) * SLOT + i * XP + k. XP == 2 (mod 32) puts a kernel row's
+    //    channels on 2i + k; for CIN = 8 a 16-row tile holds two kernel rows, in consecutive ring
+    //    slots, and SLOT == 16 (mod 32) puts the second on the other 16 banks (the ring's wrap is an
+    //    odd number of slots back, == 16 too), so every half reads 32 distinct banks.
+    // B: column n = (kw, o) at o * GP + (K-1) - kw + k; lanes with equal o and k - kw read the same
+    //    word (broadcast), so a half holds three words per channel, at 4o + {-1, 0, 1} + const with
+    //    GP == 4 (mod 32): distinct. (Round 3 had pitches 68 / 72 laid out for 64 banks: 2-way on
+    //    A, 4-way on B, ~4.5 K conflict cycles per wave in SQ_LDS_BANK_CONFLICT.)
+    static constexpr int XP = TW + 2;
     static constexpr int SLOTS = K + 1;
-    // slot stride == 4*CIN (mod 64) for CIN < 16, so a 16-row A tile spanning several kernel rows
-    // (consecutive ring slots) still covers 64 distinct banks; 0 for CIN >= 16 (one kh per tile)
-    static constexpr int SKEW = CIN * 4 < 64 ? CIN * 4 : 0;
-    static constexpr int SLOT = CIN * XP + (((SKEW - CIN * XP) % 64) + 64) % 64;
+    static constexpr int SKEW = (2 * CIN) % 32;
+    static constexpr int SLOT = CIN * XP + (((SKEW - CIN * XP) % 32) + 32) % 32;
     static constexpr int GW = TW + K - 1;  // g row incl. the left halo
-    static constexpr int GP = 72;          // == 8 (mod 64): the 8 channels of a B tile 8 banks apart
+    static constexpr int GP = 68;          // == 4 (mod 32), see above
+    static constexpr int ZB = 2;           // padded B columns read the zero row at banks 2, 3 (mod 4): free
     static_assert(GW <= GP, "g row pitch");
+    static_assert(XP % 32 == 2 && GP % 32 == 4 && (CIN >= 16 || SLOT % 32 == 16), "bank layout");
     static_assert(COUT % 4 == 0, "g rows are staged four output channels per pass");
     // LDS (floats): xc ring + its zero row | c ring + its zero row | g [buf][part][COUT + 1 rows][GP]
     // (row COUT of each g part is zero). Padded M / N lanes read the zero rows, whose offsets from
@@ -1213,7 +1223,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(GP ? NCONV_W
 #pragma unroll
     for (int u = 0; u < C::NT; ++u) {
         const int n = 16 * u + ml;
-        b_off[u] = n < C::N ? (n % COUT) * C::GP + (K - 1) - n / COUT + kq : COUT * C::GP + kq;
+        b_off[u] = n < C::N ? (n % COUT) * C::GP + (K - 1) - n / COUT + kq : COUT * C::GP + C::ZB + kq;
     }
 
     // ---- staging: one input row (CIN x 64 columns) and one g row (COUT x (64+K-1) columns) ----
