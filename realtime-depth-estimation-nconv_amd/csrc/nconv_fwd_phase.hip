@@ -201,7 +201,8 @@ __global__ __launch_bounds__(kPT) void fwd_phase(LayerDev d, float* __restrict__
             for (int oo = 0; oo < 2; ++oo)
 #pragma unroll
                 for (int j = 0; j < 3; ++j) a3[oo][j] = (f2){0.f, 0.f};
-            const float* __restrict__ w3 = D.weight + (size_t)(2 * w) * kPCB * 25;
+            const int wu = __builtin_amdgcn_readfirstlane(w);  // wave-uniform: the weights ride s_load
+            const float* __restrict__ w3 = D.weight + (size_t)(2 * wu) * kPCB * 25;
             if (dl) {
 #pragma unroll 1
                 for (int ci = 0; ci < kPCB; ++ci) {
@@ -225,7 +226,7 @@ __global__ __launch_bounds__(kPT) void fwd_phase(LayerDev d, float* __restrict__
                 }
 #pragma unroll
                 for (int oo = 0; oo < 2; ++oo) {
-                    const int o = 2 * w + oo;
+                    const int o = 2 * wu + oo;
                     const float s3 = D.wsum[o], b3 = D.bias[o];
 #pragma unroll
                     for (int j = 0; j < 3; ++j) {
