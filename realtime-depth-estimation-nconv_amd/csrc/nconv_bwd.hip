@@ -1142,6 +1142,9 @@ static int launch_wgrad_reduce(const BwdArgs& a, const float* part, int nblk, in
 // into the block's partial row (then wgrad_reduce_sum / wgrad_finish, as for wgrad_tiled).
 typedef float f4acc __attribute__((ext_vector_type(4)));
 
+#ifndef NCONV_WM_SH
+#define NCONV_WM_SH 1  // 8 -> 8 5x5: 8 MFMA tiles per operand pair (see WmCfg::SH); 0: the plain 3 x 3 tiles
+#endif
 template <int CIN, int COUT, int K>
 struct WmCfg {
     static constexpr int TW = 64;
@@ -1153,7 +1156,7 @@ struct WmCfg {
     // the shifted q range as well, and the staged input row carries one halo column for it); the
     // (third A, third B) tile -- 8 useful of 256 entries -- is not computed: 8 MFMAs per operand pair
     // instead of 9 (1600 useful of 2048 products instead of 2304).
-    static constexpr bool SH = CIN == 8 && K == 5;
+    static constexpr bool SH = NCONV_WM_SH && CIN == 8 && K == 5;
     static_assert(CIN == 8 || CIN == 16, "A tile layout: 8 or 16 input channels");
     // LDS banks of the operand reads (ds_read_b32: bank = dword address mod 32, the two 32-lane
     // halves separate; a half holds k = lane >> 4 in {0, 1} (or {2, 3}) x 16 rows / columns):
