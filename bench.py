@@ -170,9 +170,6 @@ def kernel_costs(B, H, W):
         "nconv_down2": (px(H4, W4) * (16 + 16 + 4) * f4, px(H4, W4) * F5),
         "nconv_down3": (px(H8, W8) * (16 + 16) * f4, px(H8, W8) * F5),
         "nconv4": ((px(H4, W4) * 32 + px(H8, W8) * 16) * f4, px(H4, W4) * F3),
-        # down3 inside nconv4's tiles: down3's input read at eighth resolution, its output never
-        # written (the same bytes as nconv4 alone), both layers' flops counted once
-        "nconv_down3+nconv4": ((px(H4, W4) * 32 + px(H8, W8) * 16) * f4, px(H4, W4) * F3 + px(H8, W8) * F5),
         "nconv5": ((px(H2, W2) * 32 + px(H4, W4) * 16) * f4, px(H2, W2) * F3),
         "nconv6+7_tail": ((px(H, W) * (16 + 1) + px(H2, W2) * 16) * f4,
                           px(H - 2, W - 2) * F3 + px(H + 2, W + 2) * (2 * 2 * 8 + 4)),
@@ -217,18 +214,12 @@ def inference_calls(m, net, S):
                                                  l2.weight, l2.bias, s2, w21)} if head else {
         "nconv1": lambda: fwd(l1.spec(lib.THRESH, 0.01), S, None, None, None, l1.weight, l1.bias, s1),
         "nconv2": lambda: fpool(l2.spec(), x1, c1, None, None, l2.weight, l2.bias, s2)}
-    mid = {
-        "nconv_down3": lambda: fwd(d3.spec(), p3, q3, None, None, d3.weight, d3.bias, sd3),
-        "nconv4": lambda: fwd(l4.spec(lib.UPCAT_SKIP_FIRST), x3, c3, x4, c4, l4.weight, l4.bias, s4, wphase=w4)}
-    if m.dnet.fuse_down_up_ok(d3, l4, x3, p3, w4):  # as DNET._infer: one launch (nconv_fwd_down_up)
-        mid = {"nconv_down3+nconv4": lambda: m.nconv.layer_forward_down_up(
-            d3.spec(), p3, q3, d3.weight, d3.bias, sd3, l4.spec(lib.UPCAT_SKIP_FIRST), x3, c3, l4.weight, l4.bias,
-            s4, w4)}
     return {
         **first,
         "nconv_down1": lambda: fpool(d1.spec(), p1, q1, None, None, d1.weight, d1.bias, sd1),
         "nconv_down2": lambda: fpool(d2.spec(), p2, q2, None, None, d2.weight, d2.bias, sd2),
-        **mid,
+        "nconv_down3": lambda: fwd(d3.spec(), p3, q3, None, None, d3.weight, d3.bias, sd3),
+        "nconv4": lambda: fwd(l4.spec(lib.UPCAT_SKIP_FIRST), x3, c3, x4, c4, l4.weight, l4.bias, s4, wphase=w4),
         "nconv5": lambda: fwd(l5.spec(lib.UPCAT_SKIP_FIRST), x2, c2, x34, c34, l5.weight, l5.bias, s5, wphase=w5),
         "nconv6+7_tail": lambda: d._fused_tail(l6, l7, s6, s7, x1b, c1b, x23, c23, tail_out, w6),
     }

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define NCONV_ABI_VERSION 19
+#define NCONV_ABI_VERSION 18
 
 /* How a layer's input (data x, confidence c) is produced from its source tensors. These are the
  * DNET glue ops fused into the layer's load stage (models/step1.py:53,61-90). */
@@ -201,16 +201,6 @@ int nconv_head_weights(const nconv_layer* L1, const nconv_layer* L2, float* w21,
 int nconv_fwd_tail(const nconv_layer* L6, const float* w7, const float* b7, const float* wsum7,
                    int cin7, int p7, float eps7, float* out, float* out_c, int out_h, int out_w, int crop0,
                    float* y6, float* cout6, void* stream);
-
-/* Fused low-resolution step of DNET's exact-fp32 inference: down3 (step1.py:73-75) evaluated inside
- * nconv4's tiles (step1.py:78-80: cat(x3_ds, nearest-up(down3's output)) -> nconv4), so down3's
- * outputs never reach HBM. `down`: exact fp32, PLAIN, 8 -> 8, 5x5, stride 1, padding 2, no dilation
- * or groups. `up`: exact fp32, UPCAT_SKIP_FIRST, 16 (8 + 8) -> 8, 3x3 with its phase weights in
- * up->waux (nconv_phase_weights); up->b describes down's output -- b.C, b.H, b.W must equal down's
- * Cout, Ho, Wo, with H = 2 b.H and W = 2 b.W -- and b.x / b.c are not read (may be NULL). y, cout:
- * nconv4's outputs (B, 8, Ho, Wo), bitwise those of nconv_fwd(down) followed by nconv_fwd(up).
- * Returns 0, -EINVAL for an invalid descriptor or -EOPNOTSUPP for another geometry. */
-int nconv_fwd_down_up(const nconv_layer* down, const nconv_layer* up, float* y, float* cout, void* stream);
 
 /* Which kernels nconv_fwd (without fused pooling) and nconv_bwd run for L (enum nconv_kernel):
  * the arithmetic a descriptor selects, made observable to hosts and tests. Host-only (no device

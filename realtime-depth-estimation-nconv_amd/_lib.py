@@ -13,7 +13,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # NCONV_LIB: an alternative build of the same library (kernel-tuning experiments)
 LIB_PATH = os.environ.get("NCONV_LIB") or os.path.join(_HERE, "libnconv.so")
-ABI_VERSION = 19
+ABI_VERSION = 18
 BWD_ACCUMULATE = 1
 BWD_DEFER_REDUCE = 2
 
@@ -36,7 +36,6 @@ EXPORTED = (
     "nconv_fwd_pooled",
     "nconv_fwd_tail",
     "nconv_fwd_head",
-    "nconv_fwd_down_up",
     "nconv_head_weights",
     "nconv_plan",
     "nconv_phase_weights_floats",
@@ -139,8 +138,6 @@ def _declare(lib):
     lib.nconv_fwd_tail.restype = ctypes.c_int
     lib.nconv_fwd_tail.argtypes = [ctypes.POINTER(NconvLayer), P, P, P, ctypes.c_int, ctypes.c_int,
                                    ctypes.c_float, P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P, P]
-    lib.nconv_fwd_down_up.restype = ctypes.c_int
-    lib.nconv_fwd_down_up.argtypes = [ctypes.POINTER(NconvLayer), ctypes.POINTER(NconvLayer), P, P, P]
     lib.nconv_plan.restype = ctypes.c_int
     lib.nconv_plan.argtypes = [ctypes.POINTER(NconvLayer), P, P, P]
     lib.nconv_phase_weights_floats.restype = ctypes.c_size_t

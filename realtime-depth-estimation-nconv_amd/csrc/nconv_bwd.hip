@@ -1142,43 +1142,30 @@ static int launch_wgrad_reduce(const BwdArgs& a, const float* part, int nblk, in
 // into the block's partial row (then wgrad_reduce_sum / wgrad_finish, as for wgrad_tiled).
 typedef float f4acc __attribute__((ext_vector_type(4)));
 
-#ifndef NCONV_WM_SH
-#define NCONV_WM_SH 1  // 8 -> 8 5x5: 8 MFMA tiles per operand pair (see WmCfg::SH); 0: the plain 3 x 3 tiles
-#endif
 template <int CIN, int COUT, int K>
 struct WmCfg {
     static constexpr int TW = 64;
     static constexpr int M = CIN * K, N = COUT * K;
     static constexpr int MT = (M + 15) / 16, NT = (N + 15) / 16;
-    // SH (8 -> 8 5x5: M = N = 40, three 16-row / column tiles each): the third A tile holds kernel
-    // row 4 twice, rows 8-15 read one column further right, so with the (kw = 2, 3) B tile they form
-    // kernel row 4's tap kw = 3 + 1 = 4 (summed over the strip shifted one column: the strips tile
-    // the shifted q range as well, and the staged input row carries one halo column for it); the
-    // (third A, third B) tile -- 8 useful of 256 entries -- is not computed: 8 MFMAs per operand pair
-    // instead of 9 (1600 useful of 2048 products instead of 2304).
-    static constexpr bool SH = NCONV_WM_SH && CIN == 8 && K == 5;
-    static_assert(CIN == 8 || CIN == 16, "A tile layout: 8 or 16 input channels");
     // LDS banks of the operand reads (ds_read_b32: bank = dword address mod 32, the two 32-lane
     // halves separate; a half holds k = lane >> 4 in {0, 1} (or {2, 3}) x 16 rows / columns):
-    // A: row m = (kh, i) at slot(kh) * SLOT + i * XP + k (+ 1 for SH's shifted rows).
-    //    CIN = 16: XP == 2 (mod 32), a tile is one kernel row: 2i + k, 32 distinct banks.
-    //    CIN = 8: XP == 4 (mod 32) puts a kernel row's channels on 4i + k; a tile holds two kernel
-    //    rows in consecutive ring slots, and SLOT == 2 (mod 32) puts the second on 4i + 2 + k (the
-    //    ring's wrap, five slots back, == 22 == 2 (mod 4) too); SH's shifted rows read 4i + k + 1,
-    //    the same word as their unshifted neighbour's k + 1 or on bank 4i + 2: no conflicts.
+    // A: row m = (kh, i) at slot(kh) * SLOT + i * XP + k. XP == 2 (mod 32) puts a kernel row's
+    //    channels on 2i + k; for CIN = 8 a 16-row tile holds two kernel rows, in consecutive ring
+    //    slots, and SLOT == 16 (mod 32) puts the second on the other 16 banks (the ring's wrap is an
+    //    odd number of slots back, == 16 too), so every half reads 32 distinct banks.
     // B: column n = (kw, o) at o * GP + (K-1) - kw + k; lanes with equal o and k - kw read the same
     //    word (broadcast), so a half holds three words per channel, at 4o + {-1, 0, 1} + const with
     //    GP == 4 (mod 32): distinct. (Round 3 had pitches 68 / 72 laid out for 64 banks: 2-way on
     //    A, 4-way on B, ~4.5 K conflict cycles per wave in SQ_LDS_BANK_CONFLICT.)
-    static constexpr int XP = CIN == 8 ? TW + 4 : TW + 2;
+    static constexpr int XP = TW + 2;
     static constexpr int SLOTS = K + 1;
-    static constexpr int SKEW = CIN == 8 ? 2 : 0;
+    static constexpr int SKEW = (2 * CIN) % 32;
     static constexpr int SLOT = CIN * XP + (((SKEW - CIN * XP) % 32) + 32) % 32;
     static constexpr int GW = TW + K - 1;  // g row incl. the left halo
     static constexpr int GP = 68;          // == 4 (mod 32), see above
     static constexpr int ZB = 2;           // padded B columns read the zero row at banks 2, 3 (mod 4): free
     static_assert(GW <= GP, "g row pitch");
-    static_assert(XP % 32 == (CIN == 8 ? 4 : 2) && GP % 32 == 4 && (CIN >= 16 || SLOT % 32 == 2), "bank layout");
+    static_assert(XP % 32 == 2 && GP % 32 == 4 && (CIN >= 16 || SLOT % 32 == 16), "bank layout");
     static_assert(COUT % 4 == 0, "g rows are staged four output channels per pass");
     // LDS (floats): xc ring + its zero row | c ring + its zero row | g [buf][part][COUT + 1 rows][GP]
     // (row COUT of each g part is zero). Padded M / N lanes read the zero rows, whose offsets from
@@ -1232,10 +1219,6 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(GP ? NCONV_W
         const int m = 16 * t + ml;
         a_kh[t] = m < C::M ? m / CIN : -1;
         a_ik[t] = (m % CIN) * C::XP + kq;
-        if (C::SH && t == C::MT - 1 && ml >= 8) {  // kernel row 4 again, one column to the right
-            a_kh[t] = K - 1;
-            a_ik[t] = (ml - 8) * C::XP + kq + 1;
-        }
     }
 #pragma unroll
     for (int u = 0; u < C::NT; ++u) {
@@ -1249,7 +1232,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(GP ? NCONV_W
     // at column 64 + l % (K-1) -- instead of a second pass per channel with K-1 of 64 lanes active.
     // The g tensors are addressed through one resource per image (the channel's plane offset in
     // soffset for the main pass, in the lane's offset for the halo).
-    float px[C::CPW], pc[C::CPW], hx[C::CPW], hc[C::CPW];  // hx / hc: SH's halo column (lane 0)
+    float px[C::CPW], pc[C::CPW];
     constexpr int NG = GP ? 7 : 4;  // gy, gco, y, cout (+ pooled gy, gcout, argmax code)
     constexpr int NH = C::OPW * (K - 1);
     static_assert(NH <= 64, "halo lanes");
@@ -1316,12 +1299,8 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(GP ? NCONV_W
 #pragma unroll
             for (int kk = 0; kk < C::CPW; ++kk) {
                 const int i = w + 4 * kk;
-                px[kk] = pc[kk] = hx[kk] = hc[kk] = 0.f;
-                if (i < CIN) {
-                    const ChanSrc src = chan_src<MODE>(d, b, i);
-                    load_px<MODE>(d, src, ih, iw_in, px[kk], pc[kk]);
-                    if constexpr (C::SH) load_px<MODE>(d, src, ih, lane == 0 ? ow0 - L.PW + C::TW : -1, hx[kk], hc[kk]);
-                }
+                px[kk] = pc[kk] = 0.f;
+                if (i < CIN) load_px<MODE>(d, chan_src<MODE>(d, b, i), ih, iw_in, px[kk], pc[kk]);
             }
         }
     };
@@ -1334,10 +1313,6 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(GP ? NCONV_W
                 const float cv = (MODE == NCONV_LOAD_THRESH) ? (px[kk] > L.thresh ? 1.0f : 0.0f) : pc[kk];
                 lds[slot * C::SLOT + i * C::XP + lane] = px[kk] * cv;
                 lds[C::C_OFF + slot * C::SLOT + i * C::XP + lane] = cv;
-                if (C::SH && lane == 0) {
-                    lds[slot * C::SLOT + i * C::XP + C::TW] = hx[kk] * hc[kk];
-                    lds[C::C_OFF + slot * C::SLOT + i * C::XP + C::TW] = hc[kk];
-                }
             }
         }
     };
@@ -1528,8 +1503,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(GP ? NCONV_W
                 for (int t = 0; t < C::MT; ++t)
 #pragma unroll
                     for (int u = 0; u < C::NT; ++u)
-                        if (!(C::SH && t == C::MT - 1 && u == C::NT - 1))
-                            acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(va[t], vb[u], acc[t][u], 0, 0, 0);
+                        acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(va[t], vb[u], acc[t][u], 0, 0, 0);
             }
         }
     }
@@ -1551,11 +1525,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(GP ? NCONV_W
         const int l = e & 63, r = (e >> 6) & 3, tu = e >> 8;
         const int u = tu % C::NT, t = tu / C::NT;
         const int m = 16 * t + (l >> 4) * 4 + r, n = 16 * u + (l & 15);
-        if (C::SH && t == C::MT - 1) {  // kernel row 4: taps 0-3 from rows 0-7, tap 4 from rows 8-15
-            const int mm = m - 16 * t, i = mm & 7, o = n % COUT;
-            if (mm < 8 && u < C::NT - 1) out[((o * CIN + i) * K + K - 1) * K + n / COUT] = v;
-            else if (mm >= 8 && u == 1 && (n & 15) >= 8) out[((o * CIN + i) * K + K - 1) * K + K - 1] = v;
-        } else if (m < C::M && n < C::N) {
+        if (m < C::M && n < C::N) {
             const int kh = m / CIN, i = m % CIN, kw = n / COUT, o = n % COUT;
             out[((o * CIN + i) * K + kh) * K + kw] = v;
         }
@@ -1840,8 +1810,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(NCONV_WM2_WA
                 for (int t = 0; t < C::MT; ++t)
 #pragma unroll
                     for (int u = 0; u < C::NT; ++u)
-                        if (!(C::SH && t == C::MT - 1 && u == C::NT - 1))
-                            acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(va[t], vb[u], acc[t][u], 0, 0, 0);
+                        acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(va[t], vb[u], acc[t][u], 0, 0, 0);
             }
         }
     }

@@ -213,21 +213,6 @@ int nconv_fwd_tail(const nconv_layer* L6, const float* w7, const float* b7, cons
     return rc ? fail(rc, "nconv_fwd_tail", why) : 0;
 }
 
-int nconv_fwd_down_up(const nconv_layer* down, const nconv_layer* up, float* y, float* cout, void* stream) {
-    const char* fn = "nconv_fwd_down_up";
-    if (const char* why = validate(down, true)) return fail(-22, fn, why);
-    if (!up) return fail(-22, fn, "null layer descriptor");
-    nconv_layer u = *up;  // up's source b is down's output, computed in-kernel: only its shape is read
-    if (!u.b.x) u.b.x = u.a.x;
-    if (!u.b.c) u.b.c = u.a.c;
-    if (const char* why = validate(&u, true)) return fail(-22, fn, why);
-    if (!y || !cout) return fail(-22, fn, "null output");
-    if (down->B != u.B) return fail(-22, fn, "down and up must have the same batch");
-    const char* why = nullptr;
-    int rc = nconv::launch_fwd_down_up(make_dev(down), make_dev(&u), y, cout, (hipStream_t)stream, &why);
-    return rc ? fail(rc, fn, why) : 0;
-}
-
 int nconv_plan(const nconv_layer* L, int* fwd_kernel, int* dgrad_kernel, int* wgrad_kernel) {
     if (const char* why = validate(L, false)) return fail(-22, "nconv_plan", why);
     int dg, wg;

@@ -75,29 +75,14 @@ __device__ __forceinline__ ChanSrc native_src(const LayerDev& d, int b, int ca) 
 // PAR = (output-grid origin offset - padding) & 1: the parity of the first input row / column of
 // the windows of even output rows / columns (nconv4 / nconv5: padding 1 -> 1; the tail: nconv6
 // padding 0 computed from grid offset -1 -> 1).
-//
-// FUSED (DNET's down3 -> nconv4, inference): source b -- the low-resolution half -- is the output of
-// the 8 -> 8 5x5 PLAIN layer `dd` (down3), which never reaches HBM: each tile evaluates dd at its
-// 10 x 18 low block (1.4x dd's own pixels, dd's input staged once as 14 x 22 planes), in the same
-// per-element operation order as fwd_tiled (input channel, kernel row, kernel column from zero;
-// nconv_epilogue), and writes {y * cout, cout} -- what LowStager would have staged from dd's stored
-// outputs, {0, 0} outside dd's grid -- into eight resident low planes; the upsampled half then
-// reads them without staging. Outputs are bitwise the two separate launches'.
-constexpr int kDH = kPLH + 4, kDW = kPLW + 4, kDWP = (kDW + 1) & ~1;  // dd's input block: 14 x 22
-using DStager = TileStager<kDH, kDW, kDWP, NCONV_LOAD_PLAIN, kPT>;
-constexpr int kDRows = 6;  // dd's outputs: lane < 60 owns row lane / 6, columns 3 (lane % 6) .. + 2
-
-template <int MODE, bool TAIL, int PAR, bool FUSED = false>
+template <int MODE, bool TAIL, int PAR>
 __global__ __launch_bounds__(kPT) void fwd_phase(LayerDev d, float* __restrict__ y, float* __restrict__ yc,
-                                                 TailArgs t, LayerDev dd) {
+                                                 TailArgs t) {
     using TS = TileStager<kPIH, kPIW, kPIWP, NCONV_LOAD_PLAIN, kPT>;
     constexpr int kStride = TS::PLANE_STRIDE;
     constexpr bool SKIP_FIRST = MODE == NCONV_LOAD_UPCAT_SKIP_FIRST;  // channel order: [a, up(b)]
-    static_assert(!FUSED || (!TAIL && SKIP_FIRST), "fused low planes: nconv4's geometry");
-    constexpr int kTileF2 = FUSED && kPCA * DStager::PLANE_STRIDE > 2 * kStride ? kPCA * DStager::PLANE_STRIDE
-                                                                                 : 2 * kStride;
-    __shared__ __attribute__((aligned(16))) f2 tile[kTileF2];
-    __shared__ __attribute__((aligned(16))) f2 low[(FUSED ? kPCB : 2) * kPLStride];
+    __shared__ __attribute__((aligned(16))) f2 tile[2 * kStride];
+    __shared__ __attribute__((aligned(16))) f2 low[2 * kPLStride];
     const nconv_layer& L = d.L;
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const int gh = TAIL ? t.out_h : L.Ho, gw = TAIL ? t.out_w : L.Wo;
@@ -146,7 +131,7 @@ __global__ __launch_bounds__(kPT) void fwd_phase(LayerDev d, float* __restrict__
     const f2* lowbase = &low[((ty + PAR) >> 1) * kPLP + jx];
     // phase weights: [i][alpha][dh][o][beta][dw] (nconv_phase_weights), 32 floats per (i, alpha, dh)
     const cfloat* wph = (const cfloat*)L.waux;
-    auto fma_up = [&](int cb, int bufi) {  // FUSED: bufi = cb (the resident planes)
+    auto fma_up = [&](int cb, int bufi) {
         const f2* row = lowbase + bufi * kPLStride;
         const cfloat* wr = wph + ((size_t)cb * 2 + alpha) * 2 * 32;
 #pragma unroll 1
@@ -169,80 +154,16 @@ __global__ __launch_bounds__(kPT) void fwd_phase(LayerDev d, float* __restrict__
 
     TS ts;
     ts.init(d, ih0, iw0, tid);
-    const int lr0 = (oh0 - L.PH) >> 1, lc0 = (ow0 - L.PW) >> 1;  // the tile's low block origin
     LowStager ls;
+    ls.init(L, (oh0 - L.PH) >> 1, (ow0 - L.PW) >> 1, tid);
+    // the first two low planes fly during the whole native phase (one element per thread each)
     float lx0, lc0_, lx1, lc1;
-    if constexpr (!FUSED) {
-        ls.init(L, lr0, lc0, tid);
-        // the first two low planes fly during the whole native phase (one element per thread each)
-        ls.load(d, b, 0, lx0, lc0_);
-        ls.load(d, b, 1, lx1, lc1);
-    }
+    ls.load(d, b, 0, lx0, lc0_);
+    ls.load(d, b, 1, lx1, lc1);
     {
         float xa[TS::NE], ca[TS::NE], xb[TS::NE], cb[TS::NE];
-        if constexpr (FUSED) {
-            // ---- dd (down3) at the low block: its input planes, all eight staged at once ----
-            const nconv_layer& D = dd.L;
-            DStager ds;
-            ds.init(dd, lr0 - D.PH, lc0 - D.PW, tid);
-            float dx[kPCB][DStager::NE], dc[kPCB][DStager::NE];
-#pragma unroll
-            for (int i = 0; i < kPCB; ++i) ds.load(chan_src<NCONV_LOAD_PLAIN>(dd, b, i), dx[i], dc[i]);
-            ts.load(native_src<MODE>(d, b, 0), xa, ca);  // nconv4's first native planes fly meanwhile
-            ts.load(native_src<MODE>(d, b, 1), xb, cb);
-#pragma unroll
-            for (int i = 0; i < kPCB; ++i) ds.store(tile + i * DStager::PLANE_STRIDE, dx[i], dc[i], 0.f);
-            __syncthreads();
-            // wave w: dd's output channels 2w, 2w+1; lane < 60: row lane / 6, three columns
-            const int dr = lane / kDRows, dc0 = (lane - dr * kDRows) * 3;
-            const bool dl = lane < kPLH * kDRows;
-            f2 a3[2][3];
-#pragma unroll
-            for (int oo = 0; oo < 2; ++oo)
-#pragma unroll
-                for (int j = 0; j < 3; ++j) a3[oo][j] = (f2){0.f, 0.f};
-            const int wu = __builtin_amdgcn_readfirstlane(w);  // wave-uniform: the weights ride s_load
-            const float* __restrict__ w3 = D.weight + (size_t)(2 * wu) * kPCB * 25;
-            if (dl) {
-#pragma unroll 1
-                for (int ci = 0; ci < kPCB; ++ci) {
-                    const f2* row = tile + ci * DStager::PLANE_STRIDE + dr * kDWP + dc0;
-                    const float* wr = w3 + ci * 25;
-#pragma unroll 1
-                    for (int kh = 0; kh < 5; ++kh, row += kDWP, wr += 5) {
-                        f2 v[7];
-#pragma unroll
-                        for (int m = 0; m < 7; ++m) v[m] = row[m];
-#pragma unroll
-                        for (int kw = 0; kw < 5; ++kw)
-#pragma unroll
-                            for (int oo = 0; oo < 2; ++oo) {
-                                const float wv = wr[oo * kPCB * 25 + kw];
-                                const f2 w2 = (f2){wv, wv};
-#pragma unroll
-                                for (int j = 0; j < 3; ++j) a3[oo][j] = __builtin_elementwise_fma(w2, v[j + kw], a3[oo][j]);
-                            }
-                    }
-                }
-#pragma unroll
-                for (int oo = 0; oo < 2; ++oo) {
-                    const int o = 2 * wu + oo;
-                    const float s3 = D.wsum[o], b3 = D.bias[o];
-#pragma unroll
-                    for (int j = 0; j < 3; ++j) {
-                        const int gr = lr0 + dr, gc = lc0 + dc0 + j;
-                        const bool in = (unsigned)gr < (unsigned)D.Ho && (unsigned)gc < (unsigned)D.Wo;
-                        float yv, cv;
-                        nconv_epilogue(a3[oo][j].x, a3[oo][j].y, D.eps, b3, s3, yv, cv);
-                        low[o * kPLStride + dr * kPLP + dc0 + j] = in ? (f2){yv * cv, cv} : (f2){0.f, 0.f};
-                    }
-                }
-            }
-            __syncthreads();  // the low planes are complete; dd's input block may be overwritten
-        } else {
-            ts.load(native_src<MODE>(d, b, 0), xa, ca);
-            ts.load(native_src<MODE>(d, b, 1), xb, cb);
-        }
+        ts.load(native_src<MODE>(d, b, 0), xa, ca);
+        ts.load(native_src<MODE>(d, b, 1), xb, cb);
 #pragma unroll 1
         for (int ci = 0; ci < kPCA; ci += 2) {
             ts.store(tile, xa, ca, 0.f);
@@ -255,21 +176,16 @@ __global__ __launch_bounds__(kPT) void fwd_phase(LayerDev d, float* __restrict__
             fma_native(ci + 1, 1);
         }
     }
-    if constexpr (FUSED) {
 #pragma unroll 1
-        for (int ci = 0; ci < kPCB; ++ci) fma_up(ci, ci);
-    } else {
-#pragma unroll 1
-        for (int ci = 0; ci < kPCB; ci += 2) {
-            ls.store(low, lx0, lc0_);
-            __syncthreads();
-            ls.load(d, b, ci + 2 < kPCB ? ci + 2 : kPCB - 1, lx0, lc0_);
-            fma_up(ci, 0);
-            ls.store(low + kPLStride, lx1, lc1);
-            __syncthreads();
-            ls.load(d, b, ci + 3 < kPCB ? ci + 3 : kPCB - 1, lx1, lc1);
-            fma_up(ci + 1, 1);
-        }
+    for (int ci = 0; ci < kPCB; ci += 2) {
+        ls.store(low, lx0, lc0_);
+        __syncthreads();
+        ls.load(d, b, ci + 2 < kPCB ? ci + 2 : kPCB - 1, lx0, lc0_);
+        fma_up(ci, 0);
+        ls.store(low + kPLStride, lx1, lc1);
+        __syncthreads();
+        ls.load(d, b, ci + 3 < kPCB ? ci + 3 : kPCB - 1, lx1, lc1);
+        fma_up(ci + 1, 1);
     }
 
     // ---- epilogue ----
@@ -396,9 +312,9 @@ static void go_phase(const LayerDev& d, float* y, float* yc, const TailArgs& t, 
                      hipStream_t st) {
     dim3 grid(((gw + kPTW - 1) / kPTW) * ((gh + kPTH - 1) / kPTH) * d.L.B);  // see xcd_tile
     if (par)
-        hipLaunchKernelGGL((fwd_phase<MODE, TAIL, 1>), grid, dim3(kPT), 0, st, d, y, yc, t, d);
+        hipLaunchKernelGGL((fwd_phase<MODE, TAIL, 1>), grid, dim3(kPT), 0, st, d, y, yc, t);
     else
-        hipLaunchKernelGGL((fwd_phase<MODE, TAIL, 0>), grid, dim3(kPT), 0, st, d, y, yc, t, d);
+        hipLaunchKernelGGL((fwd_phase<MODE, TAIL, 0>), grid, dim3(kPT), 0, st, d, y, yc, t);
 }
 
 bool launch_fwd_phase(const LayerDev& d, float* y, float* yc, const TailArgs& t, bool tail, hipStream_t st) {
@@ -414,40 +330,6 @@ bool launch_fwd_phase(const LayerDev& d, float* y, float* yc, const TailArgs& t,
         else go_phase<NCONV_LOAD_UPCAT_UP_FIRST, false>(d, y, yc, t, gh, gw, par, st);
     }
     return true;
-}
-
-// The layer dd whose outputs are `up`'s source b: exact fp32, PLAIN, 8 -> 8, 5x5, stride 1, no
-// dilation / groups, 'same' padding 2; up.b its output shape (b.x / b.c are not read).
-bool fwd_down_up_supported(const nconv_layer& dn, const nconv_layer& up) {
-    if (up.load_mode != NCONV_LOAD_UPCAT_SKIP_FIRST || !fwd_phase_supported(up, false)) return false;
-    if (dn.load_mode != NCONV_LOAD_PLAIN || dn.math != NCONV_MATH_FP32) return false;
-    if (dn.Cin != kPCB || dn.Cout != kPCB || dn.KH != 5 || dn.KW != 5 || dn.SH != 1 || dn.SW != 1) return false;
-    if (dn.DH != 1 || dn.DW != 1 || dn.groups != 1 || dn.PH != 2 || dn.PW != 2) return false;
-    return up.b.C == dn.Cout && up.b.H == dn.Ho && up.b.W == dn.Wo;
-}
-
-int launch_fwd_down_up(const LayerDev& dn, const LayerDev& up, float* y, float* yc, hipStream_t st,
-                       const char** why) {
-    if (!fwd_down_up_supported(dn.L, up.L)) {
-        *why = "fused down -> up needs an exact-fp32 8->8 5x5 PLAIN layer feeding an exactly-2x "
-               "UPCAT_SKIP_FIRST 16->8 3x3 layer with phase weights (DNET's down3 -> nconv4)";
-        return -95;
-    }
-    const nconv_layer& L = up.L;
-    const TailArgs t{};
-    dim3 grid(((L.Wo + kPTW - 1) / kPTW) * ((L.Ho + kPTH - 1) / kPTH) * L.B);  // see xcd_tile
-    if ((-L.PH) & 1)
-        hipLaunchKernelGGL((fwd_phase<NCONV_LOAD_UPCAT_SKIP_FIRST, false, 1, true>), grid, dim3(kPT), 0, st, up, y,
-                           yc, t, dn);
-    else
-        hipLaunchKernelGGL((fwd_phase<NCONV_LOAD_UPCAT_SKIP_FIRST, false, 0, true>), grid, dim3(kPT), 0, st, up, y,
-                           yc, t, dn);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) {
-        *why = hipGetErrorString(e);
-        return -5;
-    }
-    return 0;
 }
 
 int launch_phase_weights(int n, const float* const* w, const int* cin, const int* up_first, float* const* out,

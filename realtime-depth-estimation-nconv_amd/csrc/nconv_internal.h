@@ -97,10 +97,6 @@ bool launch_fwd_mfma(const LayerDev& d, float* y, float* yc, const TailArgs& t, 
 bool fwd_phase_supported(const nconv_layer& L, bool tail);
 bool launch_fwd_phase(const LayerDev& d, float* y, float* yc, const TailArgs& t, bool tail, hipStream_t st);
 size_t phase_weight_floats(const nconv_layer& L);
-// DNET's down3 -> nconv4 as one launch (the phase kernel evaluating down3 at its low block)
-bool fwd_down_up_supported(const nconv_layer& dn, const nconv_layer& up);
-int launch_fwd_down_up(const LayerDev& dn, const LayerDev& up, float* y, float* yc, hipStream_t st,
-                       const char** why);
 int launch_phase_weights(int n, const float* const* w, const int* cin, const int* up_first, float* const* out,
                          hipStream_t st, const char** why);
 // enum nconv_kernel of the forward / input-gradient / weight-gradient launches (nconv_plan)

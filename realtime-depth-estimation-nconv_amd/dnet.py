@@ -24,8 +24,7 @@ import torch.nn as nn
 
 from . import _lib, dense, export, nconv
 from .nconv import (EnforcePos, NConv2d, WgradReduce, _require_device, head_weights, layer_backward,
-                    layer_forward_down_up, layer_forward_head, layer_forward_pooled, layer_forward_raw, nconv_layer,
-                    phase_weights, weight_prep)
+                    layer_forward_head, layer_forward_pooled, layer_forward_raw, nconv_layer, phase_weights, weight_prep)
 
 LAYERS = ("nconv1", "nconv2", "nconv_down1", "nconv_down2", "nconv_down3", "nconv4", "nconv5",
           "nconv6", "nconv7")
@@ -206,18 +205,6 @@ FUSE_TAIL_BWD = True
 FUSE_HEAD_BWD = True
 FUSE_HEAD_FWD = True  # the training forward's nconv1 + nconv2 as the exact fused head (nconv_fwd_head)
 FUSE_TAIL_FWD = True  # ... and nconv6 + nconv7 as the fused tail (nconv_fwd_tail over nconv7's whole grid)
-FUSE_DOWN_UP = True  # exact-fp32 inference: down3 inside nconv4's tiles (nconv_fwd_down_up)
-
-
-def fuse_down_up_ok(d3, l4, x3, p3, w4):
-    """Whether the inference forward runs down3 inside nconv4's tiles: exact fp32 with nconv4's phase
-    weights, nconv4 'same'-sized over down2's output x3, and down3's output (from its input p3)
-    exactly half of x3 (the phase form's nearest-2x upsampling)."""
-    if not (FUSE_DOWN_UP and w4 is not None and nconv.FORWARD_MATH == _lib.MATH_FP32):
-        return False
-    sp4 = l4.spec(_lib.UPCAT_SKIP_FIRST)
-    h, w = x3.shape[2], x3.shape[3]
-    return sp4.out_hw(h, w) == (h, w) and (h, w) == tuple(2 * v for v in d3.spec().out_hw(p3.shape[2], p3.shape[3]))
 
 
 def _tail_train(sp6, sp7, x2, c2, x7, c7, W6, W7, w6):
@@ -522,14 +509,8 @@ class DNET(nn.Module):
         n = max(1, min(int(self.mid_streams), S.shape[0])) if mid else 1
         if n == 1:
             x3, c3, p3, q3 = fp(d2.spec(), p2, q2, None, None, d2.weight, d2.bias, sd2)
-            sp4 = l4.spec(_lib.UPCAT_SKIP_FIRST)
-            if fuse_down_up_ok(d3, l4, x3, p3, w4):
-                # down3 inside nconv4's tiles: its outputs never reach HBM (nconv_fwd_down_up)
-                x34, c34 = layer_forward_down_up(d3.spec(), p3, q3, d3.weight, d3.bias, sd3, sp4, x3, c3,
-                                                 l4.weight, l4.bias, s4, w4)
-            else:
-                x4, c4 = f(d3.spec(), p3, q3, None, None, d3.weight, d3.bias, sd3)
-                x34, c34 = f(sp4, x3, c3, x4, c4, l4.weight, l4.bias, s4, wphase=w4)
+            x4, c4 = f(d3.spec(), p3, q3, None, None, d3.weight, d3.bias, sd3)
+            x34, c34 = f(l4.spec(_lib.UPCAT_SKIP_FIRST), x3, c3, x4, c4, l4.weight, l4.bias, s4, wphase=w4)
         else:
             x3, c3, p3, q3, x4, c4, x34, c34 = self._mid_split(n, layers, wsum, p2, q2, w4)
         if self.capture is not None:

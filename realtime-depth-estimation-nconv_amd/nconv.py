@@ -177,23 +177,6 @@ def layer_forward_raw(spec: LayerSpec, xa, ca, xb, cb, weight, bias, wsum, out=N
     return y, co
 
 
-def layer_forward_down_up(spec_dn: LayerSpec, x, c, w_dn, b_dn, s_dn, spec_up: LayerSpec, xs, cs, w_up, b_up,
-                          s_up, wphase, out=None):
-    """nconv_fwd_down_up: the PLAIN 8 -> 8 5x5 layer spec_dn on (x, c) evaluated inside the
-    UPCAT_SKIP_FIRST layer spec_up's tiles, whose inputs are cat(skip (xs, cs), nearest-up(spec_dn's
-    output)) -- DNET's down3 -> nconv4 (step1.py:73-80) in one launch; spec_dn's outputs never reach
-    HBM. Returns spec_up's (y, cout), bitwise the two layer_forward_raw calls'. No autograd."""
-    Ld = spec_dn.descriptor(x, c, None, None, w_dn, b_dn, s_dn)
-    Lu = spec_up.descriptor(xs, cs, None, None, w_up, b_up, s_up, wphase)
-    Lu.b.C, Lu.b.H, Lu.b.W = spec_dn.cout, Ld.Ho, Ld.Wo  # source b: the in-kernel output of spec_dn
-    sh = (Lu.B, Lu.Cout, Lu.Ho, Lu.Wo)
-    y, co = _outputs(out, 2, (sh, sh), xs.device)
-    rc = _lib.lib().nconv_fwd_down_up(_lib.ctypes.byref(Ld), _lib.ctypes.byref(Lu), _lib.ptr(y), _lib.ptr(co),
-                                      _lib.stream_handle(xs.device))
-    _lib.check(rc, "nconv_fwd_down_up")
-    return y, co
-
-
 def layer_forward_pooled(spec: LayerSpec, xa, ca, xb, cb, weight, bias, wsum, out=None, argmax=False):
     """nconv_fwd_pooled: (y, cout, maxpool2x2(y), maxpool2x2(cout)) in one launch (written into
     `out` if given). With argmax=True also the pooling windows' first-maximum codes (int32, one per

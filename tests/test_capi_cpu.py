@@ -258,32 +258,3 @@ def test_weight_prologue_validation_is_host_only(nconv_amd):
     for args, msg in cases:
         assert lib.nconv_weight_prologue(*args) == -22, msg
         assert msg in lib.nconv_last_error().decode(), msg
-
-
-def test_fwd_down_up_validation_is_host_only(nconv_amd):
-    """nconv_fwd_down_up rejects malformed descriptors (-22) and other geometries (-95) on the
-    host, before any launch; up's source b may be shape-only (b.x = b.c = NULL)."""
-    lib = nconv_amd._lib.lib()
-    fake = ctypes.c_void_p(0x1000)
-    dn = _layer(nconv_amd, H=8, W=8, Ho=8, Wo=8)
-    dn.a.H = dn.a.W = 8
-    up = _layer(nconv_amd, Cin=16, KH=3, KW=3, PH=1, PW=1, load_mode=nconv_amd._lib.UPCAT_SKIP_FIRST)
-    up.b.C, up.b.H, up.b.W = 8, 8, 8
-    up.waux = 0x1000
-    f = lambda d, u, y=fake, c=fake: lib.nconv_fwd_down_up(d if d is None else ctypes.byref(d),
-                                                          u if u is None else ctypes.byref(u), y, c, None)
-    assert f(None, up) == -22 and "null layer descriptor" in lib.nconv_last_error().decode()
-    assert f(dn, None) == -22
-    assert f(dn, up, y=None) == -22 and "null output" in lib.nconv_last_error().decode()
-    bad = _layer(nconv_amd, Cin=16, KH=3, KW=3, PH=1, PW=1, Ho=15, load_mode=nconv_amd._lib.UPCAT_SKIP_FIRST)
-    assert f(dn, bad) == -22 and "Ho/Wo" in lib.nconv_last_error().decode()
-    other_b = _layer(nconv_amd, H=8, W=8, Ho=8, Wo=8, B=2)
-    other_b.a.H = other_b.a.W = 8
-    assert f(other_b, up) == -22 and "same batch" in lib.nconv_last_error().decode()
-    k3 = _layer(nconv_amd, H=8, W=8, Ho=8, Wo=8, KH=3, KW=3, PH=1, PW=1)
-    k3.a.H = k3.a.W = 8
-    assert f(k3, up) == -95 and "fused down -> up" in lib.nconv_last_error().decode()
-    half = _layer(nconv_amd, Cin=16, KH=3, KW=3, PH=1, PW=1, load_mode=nconv_amd._lib.UPCAT_SKIP_FIRST)
-    half.b.C, half.b.H, half.b.W = 8, 9, 9  # not exactly half of up's 16 x 16
-    half.waux = 0x1000
-    assert f(dn, half) == -95

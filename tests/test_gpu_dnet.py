@@ -440,20 +440,3 @@ def test_dnet_eval_merged_prologue_bitwise(nconv_amd, gpu, B, H, W):
         d.merged_prologue = False
         e = net(S)
     assert torch.equal(c, e) and not torch.equal(b, c)
-
-
-@pytest.mark.parametrize("B,H,W", [(2, 64, 96), (8, 352, 1216), (1, 50, 70)])
-def test_dnet_eval_fused_down_up_bitwise(nconv_amd, gpu, monkeypatch, B, H, W):
-    """The exact-fp32 eval forward with down3 inside nconv4's tiles (nconv_fwd_down_up) equals the
-    separate down3 + nconv4 launches bitwise (50x70: quarter / eighth planes of odd size, where the
-    fused path falls back to the separate launches when nconv4's source is not exactly half size)."""
-    net = make_net(nconv_amd, "generalized", gpu)
-    g = torch.Generator().manual_seed(B * 11 + H)
-    S = sparse_depth(g, B, H, W).to(gpu)
-    with torch.no_grad():
-        monkeypatch.setattr(nconv_amd.dnet, "FUSE_DOWN_UP", False)
-        a = net(S)
-        monkeypatch.setattr(nconv_amd.dnet, "FUSE_DOWN_UP", True)
-        b = net(S)
-    torch.cuda.synchronize()
-    assert torch.equal(a, b)

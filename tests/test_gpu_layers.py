@@ -382,59 +382,3 @@ def test_upcat_phase_backward(nconv_amd, gpu, case):
         ref, got = ref_leaf.grad, got_leaf.grad.double().cpu()
         rel = ((got - ref).abs().max() / ref.abs().max().clamp_min(1e-30)).item()
         assert rel <= 1e-3, f"{name} {lab}: normwise rel err {rel:.3e}"
-
-
-# (down3 input h x w, batch): DNET's B=8 352x1216 eighth-resolution plane, a ragged plane (the low
-# block crosses both image edges in every tile row / column) and one smaller than a tile
-DOWN_UP_CASES = [((44, 152), 8), ((13, 21), 2), ((5, 7), 1)]
-
-
-@pytest.mark.parametrize("hw,B", DOWN_UP_CASES, ids=["dnet_352x1216", "ragged_13x21", "tiny_5x7"])
-def test_fwd_down_up_matches_separate_launches(nconv_amd, gpu, hw, B):
-    """nconv_fwd_down_up (down3 evaluated inside nconv4's tiles, step1.py:73-80) writes bitwise what
-    nconv_fwd(down3) followed by nconv_fwd(nconv4) write, and matches the float64 oracle of the two
-    layers (forward bound of this file)."""
-    N = nconv_amd.nconv
-    h, w = hw
-    g = torch.Generator().manual_seed(31)
-    p3, q3 = rand_pair(g, B, 8, h, w, dtype=torch.float64)        # down3's (pooled) input
-    x3, c3 = rand_pair(g, B, 8, 2 * h, 2 * w, dtype=torch.float64)  # nconv4's skip input
-    wd, w4 = rand_weight(g, 8, 8, 5, 5, torch.float64), rand_weight(g, 8, 16, 3, 3, torch.float64)
-    bd, b4 = (torch.rand(8, generator=g, dtype=torch.float64) * 0.1 for _ in range(2))
-    sd_, s4_ = nconv_amd.LayerSpec(8, 8, (5, 5), (1, 1), (2, 2)), \
-        nconv_amd.LayerSpec(16, 8, (3, 3), (1, 1), (1, 1), mode=nconv_amd._lib.UPCAT_SKIP_FIRST)
-    t = [_gpu(v, gpu) for v in (p3, q3, x3, c3, wd, bd, w4, b4)]
-    sdn, s4 = _wsum(nconv_amd, t[4]), _wsum(nconv_amd, t[6])
-    wph = torch.empty(N.PHASE_WEIGHT_FLOATS, device=gpu)
-    N.phase_weights([t[6]], [8], [wph])
-    x4, c4 = N.layer_forward_raw(sd_, t[0], t[1], None, None, t[4], t[5], sdn)
-    ys, cs = N.layer_forward_raw(s4_, t[2], t[3], x4, c4, t[6], t[7], s4, wphase=wph)
-    yf, cf = N.layer_forward_down_up(sd_, t[0], t[1], t[4], t[5], sdn, s4_, t[2], t[3], t[6], t[7], s4, wph)
-    torch.cuda.synchronize()
-    assert torch.equal(yf, ys) and torch.equal(cf, cs), \
-        f"max |diff| y {(yf - ys).abs().max().item():.3e} cout {(cf - cs).abs().max().item():.3e}"
-    ry4, rc4 = oracle_layer(nconv_amd._lib.PLAIN, p3, q3, None, None, wd, bd, (1, 1), (2, 2))
-    ry, rc = oracle_layer(nconv_amd._lib.UPCAT_SKIP_FIRST, x3, c3, ry4, rc4, w4, b4, (1, 1), (1, 1))
-    for got, ref in ((yf, ry), (cf, rc)):
-        err = (got.double().cpu() - ref).abs()
-        bound = 1e-4 * ref.abs() + 1e-5
-        assert (err <= bound).all(), f"max err {err.max():.3e}, worst ratio {(err / bound).max():.3f}"
-
-
-def test_fwd_down_up_rejects_other_geometry(nconv_amd, gpu):
-    """nconv_fwd_down_up returns -EOPNOTSUPP (not a silent other kernel) for a down layer that is
-    not 8 -> 8 5x5 with padding 2, and for an up layer whose source b is not exactly half size."""
-    N = nconv_amd.nconv
-    r = lambda *s: torch.rand(*s, device=gpu)
-    p3, q3, x3, c3 = r(1, 8, 6, 6), r(1, 8, 6, 6), r(1, 8, 12, 12), r(1, 8, 12, 12)
-    w4, b, s = r(8, 16, 3, 3), r(8), r(8) + 1
-    wph = torch.empty(N.PHASE_WEIGHT_FLOATS, device=gpu)
-    N.phase_weights([w4], [8], [wph])
-    s4 = nconv_amd.LayerSpec(16, 8, (3, 3), (1, 1), (1, 1), mode=nconv_amd._lib.UPCAT_SKIP_FIRST)
-    bad_dn = nconv_amd.LayerSpec(8, 8, (3, 3), (1, 1), (1, 1))
-    with pytest.raises(RuntimeError, match="nconv_fwd_down_up"):
-        N.layer_forward_down_up(bad_dn, p3, q3, r(8, 8, 3, 3), b, s, s4, x3, c3, w4, b, s, wph)
-    ok_dn = nconv_amd.LayerSpec(8, 8, (5, 5), (1, 1), (2, 2))
-    with pytest.raises(RuntimeError, match="nconv_fwd_down_up"):  # skip 14x14: not 2x down's 6x6
-        N.layer_forward_down_up(ok_dn, p3, q3, r(8, 8, 5, 5), b, s, s4, r(1, 8, 14, 14), r(1, 8, 14, 14),
-                                w4, b, s, wph)

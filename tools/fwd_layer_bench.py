@@ -55,17 +55,9 @@ def main():
         spec = m.LayerSpec(16, 8, (3, 3), (1, 1), (1, 1), mode=m._lib.UPCAT_SKIP_FIRST)
         wph = None
         if os.environ.get("NCONV_PHASE", "1") == "1":
-            wph = torch.empty(N.PHASE_WEIGHT_FLOATS, device=dev)
+            wph = torch.empty(1024, device=dev)
             N.phase_weights([w16], [8], [wph])
         fn = lambda: N.layer_forward_raw(spec, xa, ca, xb, cb, w16, b, s16, wphase=wph)
-    elif which == "down3_nconv4":  # down3 inside nconv4's tiles (nconv_fwd_down_up)
-        p3, q3 = r(B, 8, H // 8, W // 8) * 10, r(B, 8, H // 8, W // 8)
-        xa, ca = r(B, 8, H // 4, W // 4) * 10, r(B, 8, H // 4, W // 4)
-        sd = m.LayerSpec(8, 8, (5, 5), (1, 1), (2, 2))
-        spec = m.LayerSpec(16, 8, (3, 3), (1, 1), (1, 1), mode=m._lib.UPCAT_SKIP_FIRST)
-        wph = torch.empty(N.PHASE_WEIGHT_FLOATS, device=dev)
-        N.phase_weights([w16], [8], [wph])
-        fn = lambda: N.layer_forward_down_up(sd, p3, q3, w8, b, s8, spec, xa, ca, w16, b, s16, wph)
     else:  # nconv6 + nconv7 tail
         net = m.DNET(32, crop="generalized").to(dev).eval()
         xa, ca = r(B, 8, H, W) * 10, r(B, 8, H, W)

@@ -65,15 +65,13 @@ CALIB_READ, CALIB_WRITE = B * H * W * 16 * 4, B * H * W * 2 * 4  # bytes per cal
 ORDER = ["nconv1+nconv2_head", "nconv_down1", "nconv_down2", "nconv_down3", "nconv4", "nconv5", "nconv6+7_tail"]
 # (without the fused head: "nconv1", "nconv2", ... as separate launches)
 ORDER_UNFUSED = ["nconv1", "nconv2"] + ORDER[1:]
-# exact fp32 with down3 inside nconv4's tiles (nconv_fwd_down_up): one launch fewer
-ORDER_DOWN_UP = ["nconv1+nconv2_head", "nconv_down1", "nconv_down2", "nconv_down3+nconv4", "nconv5", "nconv6+7_tail"]
 
 
 def _read(dirpath, counter):
     """Per layer mean of `counter` over the timed inference forwards. Dispatches are taken in
     order: an inference forward is its weight prologue (weight_prologue; weight_prep before round
     4's one-launch prologue) followed by the 7 layer launches of ORDER (8 without
-    the fused head, 6 with down3 inside nconv4; the warm-up training forward has 9 and is skipped)."""
+    the fused head; the warm-up training forward has 9 and is skipped)."""
     files = glob.glob(os.path.join(dirpath, "**", "*counter_collection.csv"), recursive=True)
     if not files:
         raise SystemExit(f"no counter_collection.csv under {dirpath}")
@@ -92,7 +90,7 @@ def _read(dirpath, counter):
             cur.append(r)
     per = defaultdict(list)
     for g in groups:
-        order = {len(ORDER): ORDER, len(ORDER_UNFUSED): ORDER_UNFUSED, len(ORDER_DOWN_UP): ORDER_DOWN_UP}.get(len(g))
+        order = {len(ORDER): ORDER, len(ORDER_UNFUSED): ORDER_UNFUSED}.get(len(g))
         if order is None:
             continue
         for name, r in zip(order, g):
