@@ -179,7 +179,6 @@ class GraphedTrainStep:
     def __init__(self, model, optimizer, loss_fn, example_inputs, warmup=3):
         self.model, self.optimizer, self.loss_fn = model, optimizer, loss_fn
         self.static_inputs = [x.detach().clone() for x in example_inputs]
-        self._seed = None  # d loss / d loss, allocated once (outside the graph: no fill kernel per replay)
         tensors = [t for t in list(model.parameters()) + list(model.buffers())]
         tensors += [v for st in optimizer.state.values() for v in st.values() if torch.is_tensor(v)]
         snap = [t.detach().clone() for t in tensors]
@@ -209,9 +208,7 @@ class GraphedTrainStep:
         if zero:
             self.optimizer.zero_grad(set_to_none=True)
         loss = self.loss_fn(self.model, *self.static_inputs)
-        if self._seed is None or self._seed.shape != loss.shape or self._seed.dtype != loss.dtype:
-            self._seed = torch.ones_like(loss)  # (warm-up, before capture)
-        loss.backward(self._seed)
+        loss.backward()
         if hasattr(self.model, "allreduce_grads"):
             self.model.allreduce_grads()
         self.optimizer.step()
