@@ -61,7 +61,7 @@ MATH_ARITH = {
 LAYERS = ("nconv1", "nconv2", "nconv_down1", "nconv_down2", "nconv_down3", "nconv4", "nconv5", "nconv6", "nconv7")
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=None,
                    help="GPUs (= rank processes, one per GPU); default: WORLD_SIZE under a launcher, else 1")
@@ -85,14 +85,32 @@ def parse():
     p.add_argument("--fused-head", type=int, default=1, help="nconv1 inside nconv2's kernel (nconv_fwd_head)")
     p.add_argument("--inference-streams", type=int, default=None,
                    help="DNET.inference_streams: batch slices on that many streams (default: the module's)")
-    p.add_argument("--inference-shares", default=None, type=lambda v: [float(x) for x in v.split(",")],
-                   help="DNET.inference_shares: relative frames per inference stream, e.g. 5,3")
+    p.add_argument("--inference-shares", default=None, type=_shares,
+                   help="DNET.inference_shares: relative frames per inference stream, e.g. 5,3 (one positive "
+                        "number per stream of --inference-streams, default 2)")
     p.add_argument("--mid-streams", type=int, default=None,
                    help="DNET.mid_streams: the quarter/eighth-resolution layers on that many batch slices")
-    p.add_argument("--train-graph", type=int, default=-1,
-                   help="replay the training step from a hipGraph (1) or eager (0); default: 1 on one GPU, 0 with "
-                        "several (the RCCL all-reduce stays outside graph capture)")
-    return p.parse_args()
+    p.add_argument("--head-density", type=float, default=0.40,
+                   help="also time the forward's kernels at this depth density (0: skip); the headline is 5 %%")
+    p.add_argument("--train-graph", type=int, default=1,
+                   help="replay the training step from a hipGraph (1, every world size: the RCCL all-reduce is "
+                        "captured in the graph) or eager (0); on one GPU the eager step is reported beside it")
+    a = p.parse_args(argv)
+    if a.inference_shares is not None and len(a.inference_shares) != (a.inference_streams or 2):
+        p.error(f"--inference-shares has {len(a.inference_shares)} entries for {a.inference_streams or 2} "
+                "inference streams")
+    return a
+
+
+def _shares(v):
+    """--inference-shares: comma list of positive finite numbers."""
+    try:
+        sh = [float(x) for x in v.split(",")]
+    except ValueError:
+        raise argparse.ArgumentTypeError(f"not a comma list of numbers: {v!r}")
+    if not sh or not all(x > 0 and x != float("inf") for x in sh):
+        raise argparse.ArgumentTypeError(f"shares must be positive and finite: {v!r}")
+    return sh
 
 
 def _free_port():
@@ -105,9 +123,10 @@ def launch_ranks(n, argv, device_count=None, script=None, poll_s=0.2):
     """Start n rank processes of `script` (default: this file) with `argv`, one per GPU, as
     torch.distributed.run would (RANK = LOCAL_RANK = r, WORLD_SIZE = n, MASTER_ADDR 127.0.0.1, a free
     MASTER_PORT), wait for them and return the exit status (the first failing rank's; the others are
-    then terminated, so no rank waits forever in a collective). Called before this process makes
-    any HIP call: torch.cuda.device_count() does not initialise the GPU on this image, and the
-    children are fresh processes (never an exec of a process that touched the GPU)."""
+    then terminated, so no rank waits forever in a collective). This parent may load the HIP
+    runtime to count devices (torch.cuda.device_count() falls back to hipGetDeviceCount on builds
+    without amdsmi) but never launches a kernel and is never re-exec'd: the ranks are fresh child
+    processes started with Popen."""
     ndev = torch.cuda.device_count() if device_count is None else device_count
     if n > ndev:
         raise SystemExit(f"bench.py: --gpus {n} but only {ndev} GPU(s) are visible")
@@ -142,10 +161,73 @@ def log(*msg):
     print("[bench]", *msg, file=sys.stderr, flush=True)
 
 
-def sparse_depth(g, B, H, W, device):
+def sparse_depth(g, B, H, W, device, density=0.05):
     d = torch.rand(B, 1, H, W, generator=g) * 79 + 1
-    d = d * (torch.rand(B, 1, H, W, generator=g) < 0.05)
+    d = d * (torch.rand(B, 1, H, W, generator=g) < density)
     return d.to(device)
+
+
+WARMUP_MIN_S = 0.2  # untimed warm-up per leg: at least --warmup calls and at least this long
+
+
+def warm_up(fn, min_calls, min_seconds=WARMUP_MIN_S):
+    """Run fn() at least min_calls times and until min_seconds of device time have passed (synchronised
+    every call after the first few, so the clock is real). A box whose clocks ramp up under load
+    reaches its steady state before the timed region. Returns (calls, seconds)."""
+    n, t0 = 0, time.perf_counter()
+    while True:
+        fn()
+        n += 1
+        if n >= min_calls:
+            torch.cuda.synchronize()
+            el = time.perf_counter() - t0
+            if el >= min_seconds:
+                return n, el
+
+
+def _read(path):
+    try:
+        with open(path) as f:
+            return f.read().strip()
+    except OSError:
+        return None
+
+
+def gpu_state(dev):
+    """The clock / power state the box exposes for this GPU through sysfs (amdgpu: pp_dpm_sclk /
+    pp_dpm_mclk current level -- the line marked '*' --, hwmon power cap / average power / edge
+    temperature), or None where it is not readable (a container may hide /sys/class/drm)."""
+    try:
+        pr = torch.cuda.get_device_properties(dev)
+        bus = f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}"
+    except Exception:  # noqa: BLE001 -- an informational field only
+        bus = None
+    base = None
+    if bus is not None:
+        for cand in (f"/sys/bus/pci/devices/{bus}.0",):
+            if os.path.isdir(cand):
+                base = cand
+    if base is None:
+        return None
+    st = {"pci": bus}
+    for key in ("pp_dpm_sclk", "pp_dpm_mclk", "pp_dpm_fclk"):
+        txt = _read(os.path.join(base, key))
+        if txt:
+            cur = [ln.split(":", 1)[1].strip(" *") for ln in txt.splitlines() if ln.rstrip().endswith("*")]
+            st[key] = cur[0] if cur else txt.splitlines()[-1]
+    st["power_dpm_force_performance_level"] = _read(os.path.join(base, "power_dpm_force_performance_level"))
+    try:
+        hw = os.path.join(base, "hwmon")
+        hw = os.path.join(hw, sorted(os.listdir(hw))[0])
+        for key, name, scale in (("power1_cap", "power_cap_w", 1e-6), ("power1_average", "power_avg_w", 1e-6),
+                                 ("power1_input", "power_w", 1e-6), ("temp1_input", "temp_edge_c", 1e-3),
+                                 ("freq1_input", "sclk_hz", 1.0)):
+            v = _read(os.path.join(hw, key))
+            if v is not None:
+                st[name] = round(float(v) * scale, 1)
+    except (OSError, IndexError, ValueError):
+        pass
+    return st
 
 
 # ---- algorithmic cost per kernel (SURVEY.md 8(d)) -------------------------------------------------
@@ -465,7 +547,7 @@ def guided_forward(m, dev, B, H, W, steps, warmup, rank):
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
             net(rgb0, d0, rgb1, d1)
-        graph.replay()
+        warm_up(graph.replay, 2)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(steps):
@@ -577,9 +659,13 @@ def main():
             return t.item()
         return el
 
+    warm = {}
+    math_key = lambda mth, Sx: f"{mth}:{'x'.join(map(str, Sx.shape))}"
+
     def time_forward(Sx, steps, math):
-        """Warm-up passes (hipGraph capture when --graph), then `steps` timed passes between barrier
-        + synchronize; returns the max over ranks of the timed seconds."""
+        """Warm-up passes (hipGraph capture when --graph; then replays for at least --warmup calls
+        and WARMUP_MIN_S seconds), then `steps` timed passes between barrier + synchronize; returns
+        the max over ranks of the timed seconds."""
         m.nconv.FORWARD_MATH = math
         graph = None
         with torch.no_grad():
@@ -595,18 +681,15 @@ def main():
                 graph = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(graph):
                     net(Sx)
-                for _ in range(a.warmup):
-                    graph.replay()
+            one = graph.replay if graph is not None else (lambda: net(Sx))
+            warm[math_key(math, Sx)] = warm_up(one, a.warmup)
         torch.cuda.synchronize()
         barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         with torch.no_grad():
             for _ in range(steps):
-                if graph is not None:
-                    graph.replay()
-                else:
-                    net(Sx)
+                one()
         torch.cuda.synchronize()
         barrier()
         el = time.perf_counter() - t0
@@ -620,15 +703,25 @@ def main():
 
     # ---- headline: config 2 forward ----
     log(f"config 2 forward, {a.math}")
+    state0 = gpu_state(dev)
     t_fwd = time_forward(S, a.steps, HEAD)
+    state1 = gpu_state(dev)
     fps = world * B * a.steps / t_fwd
     # per-kernel times of each forward right after its timed run (rank 0), so the roofline's kernel
     # time is taken in the same conditions as the headline, not after the heavier legs below
     lt_of = {}
+    head_density = None
     if rank == 0:
         log("per-kernel times")
         m.nconv.FORWARD_MATH = HEAD
         lt_of[a.math] = time_layers(m, net, S)
+        if a.head_density > 0 and a.math == "fp32":
+            # the exact head skips nconv1's zero taps, so its time depends on the input density: the
+            # same forward's kernels at f10's 40 % (golden fixture density) beside the 5 % headline
+            log(f"per-kernel times at density {a.head_density}")
+            S40 = sparse_depth(torch.Generator().manual_seed(1100 + rank), B, H, W, dev, a.head_density)
+            lt_of["density"] = time_layers(m, net, S40)
+            del S40
 
     # ---- the same forward in the other arithmetics ----
     alt = {}
@@ -668,25 +761,36 @@ def main():
     train = None
     if not a.no_train:
         log("config 4b training step")
-        tg = (world == 1) if a.train_graph < 0 else bool(a.train_graph)
-        step = make_train_step(m, dev, B, H, W, rank, graph=tg)
+        tg = a.train_graph != 0
         ks = a.train_steps or a.steps
-        for _ in range(max(a.warmup, 1)):
-            step()
-        torch.cuda.synchronize()
-        barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(ks):
-            step()
-        torch.cuda.synchronize()
-        barrier()
-        tt = max_over_ranks(time.perf_counter() - t0)
+
+        def time_train(graphed):
+            step = make_train_step(m, dev, B, H, W, rank, graph=graphed)
+            wn, ws = warm_up(step, max(a.warmup, 1))
+            torch.cuda.synchronize()
+            barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(ks):
+                step()
+            torch.cuda.synchronize()
+            barrier()
+            el = max_over_ranks(time.perf_counter() - t0)
+            del step
+            return el, wn, ws
+        tt, wn, ws = time_train(tg)
         ms = tt / ks * 1e3
+        eager = None
+        if tg and world == 1:  # the same step eager, so a 1 -> N curve can be read in either mode
+            log("config 4b training step, eager")
+            te, _, _ = time_train(False)
+            eager = {"frames_per_sec": round(world * B * ks / te, 2), "ms_per_step": round(te / ks * 1e3, 4)}
         fl = (PASS_FLOPS_PER_FRAME + BWD_FLOPS_PER_FRAME) * B * (H * W) / (352 * 1216)
         by = (PASS_BYTES_PER_FRAME + BWD_BYTES_PER_FRAME) * B * (H * W) / (352 * 1216)
         train = {"frames_per_sec": round(world * B * ks / tt, 2), "ms_per_step": round(ms, 4), "steps": ks,
-                 "hipgraph": tg, "loss": "calculate_loss(est, gt) on the whole batch (train_step1.py:63)",
+                 "mode": "hipgraph" if tg else "eager", "hipgraph": tg, "eager": eager,
+                 "warmup_calls": wn, "warmup_s": round(ws, 3),
+                 "loss": "calculate_loss(est, gt) on the whole batch (train_step1.py:63)",
                  "forward_math": "exact fp32 (training forward), exact fp32 backward",
                  "roofline": {"bound": "fp32", "flops_per_step": fl, "bytes_per_step": by,
                               "achieved_tflops": round(fl / (ms * 1e-3) / 1e12, 2), "peak_tflops": FP32_PEAK_TFLOPS,
@@ -694,7 +798,6 @@ def main():
                               "hbm_frac": round(by / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                               "basis": "SURVEY.md 8(d): forward 6.62 GFLOP / 238.4 MB + backward 12.79 GFLOP / "
                                        "373.9 MB per 352x1216 frame"}}
-        del step
         torch.cuda.empty_cache()
 
     # ---- config 3: guided forward ----
@@ -717,8 +820,7 @@ def main():
         log("config 4 guided training step")
         gts = max(3, a.steps // 10)
         st = make_guided_train_step(m, dev, B, H, W, rank)
-        for _ in range(max(min(a.warmup, 2), 1)):
-            st()
+        warm_up(st, max(min(a.warmup, 2), 1))
         torch.cuda.synchronize()
         barrier()
         t0 = time.perf_counter()
@@ -732,6 +834,7 @@ def main():
         guided_train = {"frames_per_sec": round(world * B * gts / tt, 2), "ms_per_step": round(tt / gts * 1e3, 3),
                         "steps": gts, "frames_per_step": B * world,
                         "workload": "config4: SETP2_BP_TRAIN fwd+bwd+AdamW, B/2+B/2 frames per GPU, eager",
+                        "mode": "eager",
                         "fp32_tflops": round(fl / (tt / gts) / 1e12, 2),
                         "fp32_mfma_frac": round(fl / (tt / gts) / 1e12 / FP32_PEAK_TFLOPS, 4)}
         del st
@@ -744,6 +847,22 @@ def main():
         issued = (lambda k: mfma_issued_flops(k, B, H, W, a.math)) if a.math in MFMA_TERMS else None
         roof = roofline(lt, costs, a.math, B, H, W, issued_mfma=issued)
         roof["whole_pass_hbm_frac"] = pass_frac(t_fwd, a.steps)
+        if "density" in lt_of:
+            dom = roof["kernel"]
+            head_density = {}
+            for dens, lt_d in ((0.05, lt), (a.head_density, lt_of["density"])):
+                r_d = roofline({dom: lt_d[dom]}, costs, a.math, B, H, W)
+                ex = sq_exec(dom if dens == 0.05 else f"{dom}@{dens:.2f}", a.math, B, H, W)
+                ent = {"kernel_us": r_d["kernel_us"], "reference_flop_frac": r_d["fp32_frac"],
+                       "executed_frac": None, "layer_us": {k: round(v, 2) for k, v in lt_d.items()}}
+                if ex:
+                    ent["executed_frac"] = round(ex["executed_flops_per_launch"] / (lt_d[dom] * 1e-6) / 1e12
+                                                 / FP32_PEAK_TFLOPS, 4)
+                    ent["executed_fp32_flops_per_launch"] = ex["executed_flops_per_launch"]
+                head_density[f"{dens:.2f}"] = ent
+            head_density["note"] = ("reference_flop_frac counts nconv1 + nconv2 densely (the reference's flops); "
+                                    "executed_frac = the fp32 flops the kernel's FMA instructions performed "
+                                    "(SQ counters at that density, profiles/sq_exec.json) over the same time")
         for name, rec in alt.items():
             lt_a = lt_of[name]
             rec["layer_us"] = {k: round(v, 2) for k, v in lt_a.items()}
@@ -773,6 +892,9 @@ def main():
             "arith": MATH_ARITH[a.math],
             "layer_us": {k: round(v, 2) for k, v in lt.items()},
             "roofline": roof,
+            "head_density": head_density,
+            "warmup_replays": {k: {"calls": n, "seconds": round(t, 3)} for k, (n, t) in warm.items()},
+            "gpu_state": {"before": state0, "after_forward": state1},
             "fwd_other_arith": alt,
             "config5": c5,
             "train_fwd_bwd_adamw": train,

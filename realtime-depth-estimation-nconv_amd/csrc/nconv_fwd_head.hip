@@ -184,9 +184,11 @@ __global__ __launch_bounds__(kHT) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
             m = in ? m : 0u;
             // tap tp = 5 kh + kw of the window at halo pixel (r, c) is staged at sxb[35 kh + tp]
             const float* const sxb = sx + r * kSW + c;
-            // the first tap peeled, as a product: acc = w * v is the FMA into +0 the dense order
-            // starts with (bitwise); a window without taps takes v = {0, 0} -- no zero-filled
-            // accumulators (the compiler kept two copies of that fill, one per path into the loop)
+            // the first tap peeled: acc = fma(w, v, +0), the FMA into +0 the dense order starts
+            // with (bitwise, the sign of zero included: a window without taps takes v = {0, 0}, and
+            // a plain product w * 0 would give -0 for a negative eval-mode weight); no zero-filled
+            // accumulators carried into the loop (the compiler kept two copies of that fill, one
+            // per path into it)
             f2 acc[8];
             {
                 const bool any = m != 0u;
@@ -200,7 +202,7 @@ __global__ __launch_bounds__(kHT) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
                 const f4 wa = reinterpret_cast<const f4*>(w1t)[tp * 2], wb = reinterpret_cast<const f4*>(w1t)[tp * 2 + 1];
                 const float wv[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
 #pragma unroll
-                for (int o = 0; o < 8; ++o) acc[o] = (f2){wv[o], wv[o]} * v;
+                for (int o = 0; o < 8; ++o) acc[o] = __builtin_elementwise_fma((f2){wv[o], wv[o]}, v, (f2){0.f, 0.f});
             }
             while (m) {
                 const int tp = __builtin_ctz(m);

@@ -17,6 +17,7 @@ mode, before any layer runs (the reference applies each right before its layer; 
 no weights, so the results are identical).
 """
 import dataclasses
+import math
 import os
 
 import torch
@@ -448,10 +449,37 @@ class DNET(nn.Module):
     inference_shares = None
 
     def _n_streams(self, B):
+        return max(1, min(self._configured_streams(), B))
+
+    def _configured_streams(self):
         n = self.inference_streams
         if n is None:
             n = 2 if nconv.FORWARD_MATH == _lib.MATH_FP32 else 1
-        return max(1, min(int(n), B))
+        return int(n)
+
+    @staticmethod
+    def split_bounds(B, n, shares=None, configured=None):
+        """Frame bounds [b0 = 0, b1, ..., bn = B] of an n-way inference split: even, or by the
+        relative `shares` (one positive finite number per configured stream). Shares whose count
+        differs from the configured stream count, or that are not all positive and finite, raise
+        ValueError; when the batch is smaller than the configured count (n clamped to B) the split
+        is even."""
+        bounds = [B * k // n for k in range(n + 1)]
+        if shares is None:
+            return bounds
+        sh = [float(v) for v in shares]
+        want = n if configured is None else configured
+        if len(sh) != want:
+            raise ValueError(f"inference_shares has {len(sh)} entries for {want} inference streams")
+        if not all(math.isfinite(v) and v > 0 for v in sh):
+            raise ValueError(f"inference_shares must be positive and finite, got {tuple(shares)}")
+        if len(sh) != n:  # batch smaller than the configured streams: even split
+            return bounds
+        tot, acc = sum(sh), 0.0
+        for k in range(1, n):
+            acc += sh[k - 1]
+            bounds[k] = min(max(int(round(B * acc / tot)), bounds[k - 1]), B)
+        return bounds
 
     def _side_streams(self, device, n):
         key = (device.index, n)
@@ -463,18 +491,12 @@ class DNET(nn.Module):
     def _infer_split(self, S, layers, wsum, out, wph=None, w21=None):
         B = S.shape[0]
         n = self._n_streams(B)
+        bounds = self.split_bounds(B, n, self.inference_shares, self._configured_streams())
         if n == 1:
             self._infer(S, layers, wsum, out, wph, w21=w21)
             return
         cur = torch.cuda.current_stream(S.device)
         side = self._side_streams(S.device, n - 1)
-        bounds = [B * k // n for k in range(n + 1)]
-        sh = self.inference_shares
-        if sh is not None and len(sh) == n:
-            tot, acc = float(sum(sh)), 0.0
-            for k in range(1, n):
-                acc += sh[k - 1]
-                bounds[k] = min(max(int(round(B * acc / tot)), bounds[k - 1]), B)
         for st in side:
             st.wait_stream(cur)
         for k, st in enumerate([cur] + side):

@@ -183,7 +183,9 @@ def test_guided_training_step_matches_oracle(nconv_amd, gpu, H, W):
     assert named["rgb_encoder4.encoder.0.weight"].grad is None  # unused in forward (step2.py:46)
 
 
-@pytest.mark.parametrize("B,C,H,W,relu", [(2, 32, 19, 45, True), (3, 64, 8, 10, False), (1, 33, 100, 130, True)])
+@pytest.mark.parametrize("B,C,H,W,relu", [(2, 32, 19, 45, True), (3, 64, 8, 10, False), (1, 33, 100, 130, True),
+                                          # the bench's guided batch (4 frames per pair) at decoder sizes
+                                          (4, 32, 352, 1216, True), (4, 128, 44, 152, False)])
 def test_batchnorm_relu_train(nconv_amd, gpu, B, C, H, W, relu):
     """Training-mode BatchNorm2d (+ ReLU) against nn.BatchNorm2d in float64: output, running-stat
     update (momentum 0.1, unbiased variance), num_batches_tracked, and the three gradients."""

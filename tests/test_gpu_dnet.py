@@ -222,6 +222,55 @@ def bwd_math(request, nconv_amd, monkeypatch):
     return request.param
 
 
+def _train_gradients_vs_oracle(nconv_amd, gpu, B, H, W, crop, whole_batch_loss, seed=11):
+    """One step-1 training forward + calculate_loss + backward on the GPU and the same in the fp64
+    oracle on the GPU's pool branch (see test_dnet_train_gradients); returns the per-tensor report
+    lines (normwise errors, 'FAIL' past 1e-3) after checking the EnforcePos-drifted weights."""
+    net = make_net(nconv_amd, crop, gpu)
+    net.train()
+    g = torch.Generator().manual_seed(seed)
+    S = sparse_depth(g, B, H, W)
+    params0 = oracle_params(net)  # the forward below applies EnforcePos once more
+    net.d_net.capture = {}
+    out = net(S.to(gpu))
+    cap, net.d_net.capture = net.d_net.capture, None
+    idx = {k: tuple(torch.nn.functional.max_pool2d(t, 2, 2, return_indices=True)[1].cpu() for t in v)
+           for k, v in cap.items()}
+
+    params = {n: (R.softplus_pos(w).detach().requires_grad_(True), b.detach().requires_grad_(True))
+              for n, (w, b) in params0.items()}
+    ref = R.dnet_forward(S.double(), params, crop, pool_idx=idx)
+    gt = torch.rand(ref.shape, generator=g, dtype=torch.float64) * 80
+    gt = gt * (torch.rand(ref.shape, generator=g, dtype=torch.float64) < 0.3)
+    sel = (lambda t: t) if whole_batch_loss else (lambda t: t[0])
+    R.calculate_loss(sel(ref), sel(gt), True).backward()
+    nconv_amd.train.calculate_loss(sel(out), sel(gt).to(gpu, torch.float32), True).backward()
+    torch.cuda.synchronize()
+    named = dict(net.named_parameters())
+    report = []
+    for n, (w, b) in params.items():
+        for lab, ref_t in (("weight", w), ("bias", b)):
+            got = named[f"d_net.{n}.{lab}"].grad.double().cpu()
+            rel = ((got - ref_t.grad).abs().max() / ref_t.grad.abs().max().clamp_min(1e-30)).item()
+            report.append(f"{n}.{lab}: {rel:.2e}" + ("" if rel <= 1e-3 else "  <-- FAIL"))
+        torch.testing.assert_close(named[f"d_net.{n}.weight"].detach().double().cpu(), w.detach(),
+                                   rtol=2e-6, atol=2e-7)
+    return report
+
+
+@pytest.mark.timeout(300)
+def test_dnet_train_gradients_config4b_full_size(nconv_amd, gpu):
+    """The bench's training leg at its own batch (config 4b: B=8 352x1216, generalized crop,
+    calculate_loss on the whole batch as train_step1.py:63, exact fp32 backward -- the deferred
+    split-K weight-gradient reduction over 3.4 M pixels, the fused nconv1 / nconv7 gradients, the
+    materialised pools): all 18 gradients normwise within 1e-3 of the fp64 oracle on the GPU's
+    pool branch."""
+    report = _train_gradients_vs_oracle(nconv_amd, gpu, 8, 352, 1216, "generalized", True, seed=13)
+    print("\n".join(report))
+    assert len(report) == 18
+    assert not any(r.endswith("FAIL") for r in report), "\n".join(report)
+
+
 @pytest.mark.parametrize("H,W", [(64, 96), (45, 67), (264, 100)])  # 264: nconv2 on wgrad_mfma2 (>= 256 rows)
 def test_dnet_train_gradients(nconv_amd, gpu, H, W, bwd_math):
     """Step-1 training gradients (EnforcePos + calculate_loss on [0] + backward) vs the fp64 oracle.
@@ -233,34 +282,7 @@ def test_dnet_train_gradients(nconv_amd, gpu, H, W, bwd_math):
     the branch the GPU took: its pool winners are forced to the GPU's (computed by torch's own
     max_pool2d on the GPU's activations). Tie-breaking itself is tested bit-exactly elsewhere
     (test_gpu_layers, integer-valued pooling cases). Tolerance: normwise 1e-3 per tensor."""
-    net = make_net(nconv_amd, "literal", gpu)
-    net.train()
-    g = torch.Generator().manual_seed(11)
-    S = sparse_depth(g, 2, H, W)
-    params0 = oracle_params(net)  # the forward below applies EnforcePos once more
-    net.d_net.capture = {}
-    out = net(S.to(gpu))
-    cap, net.d_net.capture = net.d_net.capture, None
-    idx = {k: tuple(torch.nn.functional.max_pool2d(t, 2, 2, return_indices=True)[1].cpu() for t in v)
-           for k, v in cap.items()}
-
-    params = {n: (R.softplus_pos(w).detach().requires_grad_(True), b.detach().requires_grad_(True))
-              for n, (w, b) in params0.items()}
-    ref = R.dnet_forward(S.double(), params, "literal", pool_idx=idx)
-    gt = torch.rand(ref.shape, generator=g, dtype=torch.float64) * 80
-    gt = gt * (torch.rand(ref.shape, generator=g, dtype=torch.float64) < 0.3)
-    R.calculate_loss(ref[0], gt[0], True).backward()
-    R.calculate_loss(out[0], gt[0].to(gpu, torch.float32), True).backward()
-    torch.cuda.synchronize()
-    named = dict(net.named_parameters())
-    report = []
-    for n, (w, b) in params.items():
-        for lab, ref_t in (("weight", w), ("bias", b)):
-            got = named[f"d_net.{n}.{lab}"].grad.double().cpu()
-            rel = ((got - ref_t.grad).abs().max() / ref_t.grad.abs().max().clamp_min(1e-30)).item()
-            report.append(f"{n}.{lab}: {rel:.2e}" + ("" if rel <= 1e-3 else "  <-- FAIL"))
-        torch.testing.assert_close(named[f"d_net.{n}.weight"].detach().double().cpu(), w.detach(),
-                                   rtol=2e-6, atol=2e-7)
+    report = _train_gradients_vs_oracle(nconv_amd, gpu, 2, H, W, "literal", False)
     print("\n".join(report))
     assert not any(r.endswith("FAIL") for r in report), "\n".join(report)
 

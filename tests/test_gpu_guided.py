@@ -143,44 +143,53 @@ def _kitti_model(nconv_amd, gpu, seed=2):
     return model
 
 
+@pytest.mark.timeout(600)
 def test_guided_config3_full_size_vs_oracle(nconv_amd, gpu):
-    """Config 3's workload at its own size: 1+1 frames of 352x1216 (KITTI shape, generalized crop)
-    through the eval forward (SETP2_BP_EXPORT's path, hipGraph-able MFMA kernels), all four scales
-    of both pairs against the float64 oracle; and SETP2_BP_EXPORT's border-zeroed output."""
+    """Config 3's per-GPU workload at its own batch and size: 4+4 frames of 352x1216 (KITTI shape,
+    generalized crop; bench.py guided_forward's B/2 + B/2 at B=8) through the eval forward
+    (SETP2_BP_EXPORT's path, hipGraph-able MFMA kernels), all four scales of both pairs against the
+    float64 oracle -- every one of the 2n frames (the module itself returns batch slices [0:1] and
+    [1:2], step2.py:77) -- and SETP2_BP_EXPORT's border-zeroed output."""
     model = _kitti_model(nconv_amd, gpu).eval()
-    H, W = 352, 1216
-    rgb0, d0, rgb1, d1 = f5_inputs(H, W)
+    H, W, n = 352, 1216, 4
+    rgb0, d0, rgb1, d1 = f5_inputs(H, W, n)
     sd = {k: v.detach().double().cpu() for k, v in model.state_dict().items()}
+    ins = [t.to(gpu) for t in (rgb0, d0, rgb1, d1)]
     with torch.no_grad():
-        g0, g1 = model(rgb0.to(gpu), d0.to(gpu), rgb1.to(gpu), d1.to(gpu))
+        g0, g1 = model(*ins)
+        ga = nconv_amd.guided._guided_forward(model, *ins)  # all 2n frames (the module returns [0:1], [1:2])
         exp = nconv_amd.SETP2_BP_EXPORT(step1_crop="generalized").to(gpu).eval()
         exp.load_state_dict(model.state_dict(), strict=False)
-        e0, e1 = exp(rgb0.to(gpu), d0.to(gpu), rgb1.to(gpu), d1.to(gpu))
-        r0, r1 = R.setp2_forward(sd, rgb0.double(), d0.double(), rgb1.double(), d1.double(), "generalized", "train")
+        e0, e1 = exp(*ins)
+        ra = R.setp2_forward(sd, rgb0.double(), d0.double(), rgb1.double(), d1.double(), "generalized", "all")
+    r0, r1 = [o[0:1] for o in ra], [o[1:2] for o in ra]
     for i in range(4):
-        assert g0[i].shape == r0[i].shape == (1, 1, H >> (3 - i), W >> (3 - i))
+        assert g0[i].shape == r0[i].shape == (1, 1, H >> (3 - i), W >> (3 - i))  # step2.py:77's slices
+        assert ga[i].shape == ra[i].shape == (2 * n, 1, H >> (3 - i), W >> (3 - i))
+        _close(ga[i], ra[i], f"all {2 * n} frames, scale {i}")
         _close(g0[i], r0[i], f"pair0 scale {i}")
         _close(g1[i], r1[i], f"pair1 scale {i}")
     z = r0[3].clone()
     z[:, :, :45, :] = 0
     z[:, :, -45:, :] = 0
     z[:, :, :, :20] = 0
-    _close(e0, z, "export frame 0")
+    _close(e0, z, "export pair 0")
 
 
-@pytest.mark.timeout(400)
+@pytest.mark.timeout(600)
 def test_guided_config4_full_size_training_vs_oracle(nconv_amd, gpu):
-    """Config 4's per-GPU training step at its own frame size: 1+1 frames of 352x1216, train mode
-    (batch-statistics BatchNorm, frozen drifted step 1), calculate_loss_multi_resolution (MSE),
-    backward: every trainable gradient normwise within 2e-3 of the float64 oracle (5e-3 for the
-    RGB-encoder convolutions: the fp32 spread of this deep BatchNorm chain, see the f9 test),
-    outputs 1e-4 |ref| + 1e-3."""
+    """Config 4's per-GPU training step at its own batch and frame size: 4+4 frames of 352x1216
+    (bench.py make_guided_train_step's B/2 + B/2 at B=8), train mode (batch-statistics BatchNorm over
+    the 4-frame batch, frozen drifted step 1), calculate_loss_multi_resolution (MSE, on element [0]
+    as utils.py:63-71), backward: every trainable gradient normwise within 2e-3 of the float64 oracle
+    (5e-3 for the RGB-encoder convolutions: the fp32 spread of this deep BatchNorm chain, see the f9
+    test), outputs 1e-4 |ref| + 1e-3."""
     from guided_cases import grad_rel, trainable_setp2
     model = _kitti_model(nconv_amd, gpu, seed=4)
-    H, W = 352, 1216
-    rgb0, d0, rgb1, d1 = f5_inputs(H, W)
+    H, W, n = 352, 1216, 4
+    rgb0, d0, rgb1, d1 = f5_inputs(H, W, n)
     g = torch.Generator().manual_seed(12)
-    gt = (torch.rand(1, 1, 480, 640, generator=g) * 79 + 1) * (torch.rand(1, 1, 480, 640, generator=g) < 0.5)
+    gt = (torch.rand(n, 1, 480, 640, generator=g) * 79 + 1) * (torch.rand(n, 1, 480, 640, generator=g) < 0.5)
     sd = {k: v.detach().double().cpu().clone() for k, v in model.state_dict().items()}
     model.train()
     est, _ = model(rgb0.to(gpu), d0.to(gpu), rgb1.to(gpu), d1.to(gpu))
@@ -199,6 +208,7 @@ def test_guided_config4_full_size_training_vs_oracle(nconv_amd, gpu):
     ref_loss.backward()
     assert abs(loss.item() - ref_loss.item()) <= 1e-4 * abs(ref_loss.item())
     for i in range(4):
+        assert est[i].shape == r0[i].shape == (1, 1, H >> (3 - i), W >> (3 - i))
         _close(est[i].detach(), r0[i].detach(), f"scale {i}")
     refs = {k: leaves[k].grad for k in names}
     rel = {k: grad_rel(named[k].grad.double().cpu(), refs[k], k, refs) for k in names}

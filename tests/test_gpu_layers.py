@@ -209,6 +209,38 @@ def test_nconv2d_module_train_step(nconv_amd, gpu, H, W):
         assert rel <= 1e-3, rel
 
 
+def test_fwd_head_negative_weights_sign_of_zero(nconv_amd, gpu):
+    """Eval mode (no EnforcePos) allows negative nconv1 weights. A window without depth samples then
+    sums only zero products; the dense order (an FMA chain from +0, like the reference's
+    convolution) gives +0, so the fused head's nconv1 (nonzero taps only, first tap peeled) must
+    give +0 too, not w * 0 = -0: nconv1's outputs bitwise, sign of zero included, against the
+    separate nconv1 launch, and nconv2's edge-tile outputs likewise."""
+    B, H, W = 2, 48, 96
+    g = torch.Generator().manual_seed(4242)
+    S = (torch.rand(B, 1, H, W, generator=g) * 79 + 1) * (torch.rand(B, 1, H, W, generator=g) < 0.02)
+    w1 = _gpu(-rand_weight(g, 8, 1, 5, 5), gpu)
+    w2 = _gpu(rand_weight(g, 8, 8, 5, 5), gpu)
+    b1 = _gpu(torch.zeros(8), gpu)
+    b2 = _gpu(torch.rand(8, generator=g) * 0.1, gpu)
+    s1, s2 = _wsum(nconv_amd, w1), _wsum(nconv_amd, w2)
+    sp1 = nconv_amd.LayerSpec(1, 8, (5, 5), (1, 1), (2, 2), mode=THRESH)
+    sp2 = nconv_amd.LayerSpec(8, 8, (5, 5), (1, 1), (2, 2))
+    Sg = S.to(gpu)
+    N = nconv_amd.nconv
+    x1, c1 = N.layer_forward_raw(sp1, Sg, None, None, None, w1, b1, s1)
+    y0, c0 = N.layer_forward_raw(sp2, x1, c1, None, None, w2, b2, s2)
+    w21 = N.head_weights(sp1, sp2, Sg, w1, b1, s1, w2, b2, s2)
+    y2, c2, _, _, _, x1h, c1h = N.layer_forward_head(sp1, sp2, Sg, w1, b1, s1, w2, b2, s2, w21, train=True)
+    torch.cuda.synchronize()
+    bits = lambda t: t.contiguous().view(torch.int32)
+    assert (x1 == 0).any() and (c1 == 0).any()  # sample-free windows exist
+    assert torch.equal(bits(x1h), bits(x1)) and torch.equal(bits(c1h), bits(c1))
+    # (cout = D / s1 with D = +0 and s1 < 0 is -0 in those windows; the old peeled product gave
+    # D = -0 and so cout = +0)
+    assert torch.signbit(c1[c1 == 0]).all()
+    assert torch.equal(bits(y2[:, :, :16]), bits(y0[:, :, :16])) and torch.equal(bits(c2[:, :, :16]), bits(c0[:, :, :16]))
+
+
 @pytest.mark.parametrize("shape", [(2, 8, 48, 128), (2, 8, 37, 71), (1, 8, 20, 66)])
 def test_fwd_pooled_outputs(nconv_amd, gpu, shape):
     """nconv_fwd_pooled: identical y/cout to nconv_fwd, and pooled copies bit-equal to torch's
