@@ -195,7 +195,7 @@ struct VecOf<2> { typedef f2 T; };
 // over the list; plus the dense sums gb1 = sum gy1 and sum gcout1*cout1 (the normaliser's term).
 // One partial row per workgroup (wgrad_reduce_sum / wgrad_finish reduce them, deferred or not):
 // nconv1's input gradient G[1] is never written to HBM and nconv1 needs no backward kernel.
-constexpr int kHeadNw = 8 * 25, kHeadStride = kHeadNw + 16;
+// (kHeadNw, kHeadStride: nconv_internal.h)
 
 template <int CIN, int TH, int TW>
 struct HeadLds {
@@ -2116,6 +2116,32 @@ int launch_bwd(const LayerDev& d, const BwdArgs& a, hipStream_t st, const char**
             *why = "pooled-output gradient needs gy_pool, gcout_pool and the argmax codes, on an exact-fp32 "
                    "8->8 5x5 stride-1 layer with plain loads";
             return -95;
+        }
+        // input and weight gradient requested: one kernel for both (nconv_bwd_fused.hip) unless the
+        // caller asked for the separate kernels
+        const bool want_in = a.hpart || a.gxa || a.gca;
+        if (!a.separate && want_in && (a.gw || a.gb) && fused_bwd_ok(L)) {
+            // partial rows: at most what the layer's workspace (wm_grid) and, with the head, the head
+            // workspace (one row per dgrad_tiled tile, bwd_head_workspace_bytes) hold
+            int maxb = (int)wm_grid(L).nblk;
+            if (a.hpart) {
+                using D = DgCfg<8, 5>;
+                const int hb = ((L.W + D::TW - 1) / D::TW) * ((L.H + D::TH - 1) / D::TH) * L.B;
+                maxb = hb < maxb ? hb : maxb;
+            }
+            const int nb = launch_bwd_fused(d, a, part, maxb, true, a.hpart != nullptr, st);
+            if (nb > 0) {
+                if (a.hpart) {
+                    if (a.defer) {
+                        *a.hnparts = nb;
+                    } else {
+                        const RedJob J{a.hpart, a.hs, a.hgw, a.hgb, nb, kHeadNw, 8, 25};
+                        if (int rc = launch_wgrad_reduce_multi(1, &J, st, why)) return rc;
+                    }
+                }
+                const int rc = launch_wgrad_reduce(a, part, nb, 8 * 8 * 25, 8, 8 * 25, L.wsum, st, why);
+                return rc ? rc : last_err(why);
+            }
         }
         const int rc = a.hpart ? go_bwd_tiled<8, 8, 5, NCONV_LOAD_PLAIN, true, true>(d, a, part, tx, tc, st, why)
                                : go_bwd_tiled<8, 8, 5, NCONV_LOAD_PLAIN, true>(d, a, part, tx, tc, st, why);

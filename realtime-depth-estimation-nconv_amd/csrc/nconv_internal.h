@@ -73,6 +73,7 @@ struct BwdArgs {
     float* t7part;
     float* t7gw;
     int* t7nparts;
+    int separate;  // NCONV_BWD_SEPARATE: no one-kernel backward (input and weight gradient as two kernels)
 };
 size_t bwd_tail_workspace_bytes(const nconv_layer& L6);
 size_t bwd_head_workspace_bytes(const nconv_layer& L2);
@@ -131,6 +132,19 @@ int go_wgrad_bf(const LayerDev& d, const BwdArgs& a, float* part, int max_blocks
 template <int CIN, int COUT, int K, int MODE>
 void go_dgrad_bf(const LayerDev& d, const BwdArgs& a, float* tmp_x, float* tmp_c, int np, hipStream_t st);
 int launch_bwd(const LayerDev& d, const BwdArgs& a, hipStream_t st, const char** why);
+// nconv1's weight-gradient partial rows of the fused head (200 weights, 8 sum gy, 8 sum gcout*cout)
+constexpr int kHeadNw = 8 * 25, kHeadStride = kHeadNw + 16;
+// One-kernel backward of an exact-fp32 8 -> 8 5x5 stride-1 layer with plain loads (input and weight
+// gradient together, nconv_bwd_fused.hip): the grid (64-column strips x row segments x images) and
+// its launch, with the pooled-output gradient (gp) and / or the fused nconv1 weight gradient (hw);
+// returns the number of partial rows written (<= max_blocks), or -1 when they would not fit.
+struct FusedGrid {
+    int nstrip, nseg, seg_rows, nblk;
+};
+FusedGrid fused_grid(const nconv_layer& L, int max_blocks);
+bool fused_bwd_ok(const nconv_layer& L);
+int launch_bwd_fused(const LayerDev& d, const BwdArgs& a, float* part, int max_blocks, bool gp, bool hw,
+                     hipStream_t st);
 
 // Dense convolutions (RGB-guided model).
 int dense_cout_tile(int Cout);

@@ -113,12 +113,14 @@ class DNETFn(torch.autograd.Function):
         cur = torch.cuda.current_stream(S.device)
         side = _wgrad_stream(S.device) if (ctx.pooled and WGRAD_STREAM) else None
 
-        def layer_bwd(spec, inputs, y, co, gy, gco, gin, gw_, gb_, **kw):
-            # weight gradient on the side stream, concurrent with this layer's input gradient (and
-            # the next layers' input gradients, which do not depend on it): it needs only tensors
-            # that are complete when this layer's backward starts
-            if side is None or (gw_ is None and gb_ is None):
-                layer_backward(spec, inputs, y, co, gy, gco, gin, gw_, gb_, defer=red, **kw)
+        def layer_bwd(spec, inputs, y, co, gy, gco, gin, gw_, gb_, fused=False, **kw):
+            # fused: one call (one kernel) for the input and the weight gradient (the exact-fp32 8 -> 8
+            # 5x5 layers with a pooled-output gradient, nconv_bwd_fused.hip). Otherwise the weight
+            # gradient runs on the side stream, concurrent with this layer's input gradient (and the
+            # next layers' input gradients, which do not depend on it): it needs only tensors that are
+            # complete when this layer's backward starts
+            if side is None or (gw_ is None and gb_ is None) or fused:
+                layer_backward(spec, inputs, y, co, gy, gco, gin, gw_, gb_, defer=red, separate=not fused, **kw)
                 return
             side.wait_stream(cur)
             tail, head = kw.pop("tail", None), kw.pop("head", None)
@@ -133,7 +135,7 @@ class DNETFn(torch.autograd.Function):
             gy, gco = G[k] if G[k] is not None else (g9, None)
             layer_bwd(spec or sp[k - 1], (xa, ca, xb, cb, *W[k - 1]), X[k][0], X[k][1], gy, gco,
                       (*(ga or (None, None)), *(gb_ or (None, None))), gw[k - 1], gb[k - 1], accumulate=acc,
-                      pool_grad=pool_grad)
+                      pool_grad=pool_grad, fused=pool_grad is not None and LAYERS[k - 1] in FUSED_BWD)
 
         def finish():
             if side is not None:
@@ -174,7 +176,7 @@ class DNETFn(torch.autograd.Function):
             if FUSE_HEAD_BWD and not need[1]:  # nconv2's input gradient feeds nconv1's weight gradient in-tile
                 layer_bwd(sp[1], (X[1][0], X[1][1], None, None, *W[1]), X[2][0], X[2][1], *G[2],
                           (None, None, None, None), gw[1], gb[1], pool_grad=(*gp2, a2),
-                          head=(sp[0], S, *W[0], gw[0], gb[0]))
+                          head=(sp[0], S, *W[0], gw[0], gb[0]), fused="nconv2" in FUSED_BWD)
                 finish()
                 out = [None, None, None]
                 for i in range(9):
@@ -206,6 +208,9 @@ FUSE_TAIL_BWD = True
 FUSE_HEAD_BWD = True
 FUSE_HEAD_FWD = True  # the training forward's nconv1 + nconv2 as the exact fused head (nconv_fwd_head)
 FUSE_TAIL_FWD = True  # ... and nconv6 + nconv7 as the fused tail (nconv_fwd_tail over nconv7's whole grid)
+# Layers whose backward (with the pooled-output gradient) runs the input and the weight gradient as
+# ONE kernel (nconv_bwd_fused.hip) instead of two on two streams
+FUSED_BWD = frozenset(os.environ.get("NCONV_FUSED_BWD", "").split(",")) - {""}
 
 
 def _tail_train(sp6, sp7, x2, c2, x7, c7, W6, W7, w6):

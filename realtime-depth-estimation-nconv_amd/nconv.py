@@ -258,7 +258,7 @@ class NConvLayerFn(torch.autograd.Function):
 
 
 def layer_backward(spec: LayerSpec, inputs, y, co, gy, gco, gin, gw, gb, accumulate=False, defer=None,
-                   pool_grad=None, head=None, tail=None):
+                   pool_grad=None, head=None, tail=None, separate=False):
     """nconv_bwd of one fused layer: gin = (gxa, gca, gxb, gcb) (None: skip) overwritten, or added
     into with accumulate=True (NCONV_BWD_ACCUMULATE: a tensor consumed by two layers); gw, gb
     overwritten (None: skip). defer: a WgradReduce collecting the layer's weight-gradient partial
@@ -269,7 +269,9 @@ def layer_backward(spec: LayerSpec, inputs, y, co, gy, gco, gin, gw, gb, accumul
     then computed inside this layer's input gradient (nconv_bwd_ex head; gin's gxa / gca optional).
     tail: (spec, weight, bias, wsum, y9, cout9, gy9, gw9) of the 1x1 consumer nconv7, whose backward
     is fused into this layer's (nconv_bwd_ex tail; gy / gco are then unused and may be None; nconv7's
-    bias gradient is the caller's)."""
+    bias gradient is the caller's). With pool_grad and both an input gradient (or head) and gw / gb
+    requested, an exact-fp32 8 -> 8 5x5 layer runs one kernel for both gradients (include/nconv.h
+    NCONV_BWD_SEPARATE); separate=True runs the input- and weight-gradient kernels instead."""
     xa, ca, xb, cb, weight, bias, wsum = inputs
     gxa, gca, gxb, gcb = gin
     dev = y.device
@@ -281,7 +283,8 @@ def layer_backward(spec: LayerSpec, inputs, y, co, gy, gco, gin, gw, gb, accumul
     lib = _lib.lib()
     ws_bytes = lib.nconv_bwd_workspace_bytes(_lib.ctypes.byref(L))
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
-    flags = (_lib.BWD_ACCUMULATE if accumulate else 0) | (_lib.BWD_DEFER_REDUCE if defer is not None else 0)
+    flags = (_lib.BWD_ACCUMULATE if accumulate else 0) | (_lib.BWD_DEFER_REDUCE if defer is not None else 0) | \
+        (_lib.BWD_SEPARATE if separate else 0)
     io = _lib.NconvBwdIo()
     gpy, gpc, parg = pool_grad if pool_grad is not None else (None, None, None)
     for name, t in (("y", y), ("cout", co), ("gy", gy), ("gcout", gco), ("gxa", gxa), ("gca", gca), ("gxb", gxb),

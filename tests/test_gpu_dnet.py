@@ -84,6 +84,8 @@ def test_whole_graph_autograd_matches_per_layer(nconv_amd, gpu, H, W, monkeypatc
     # checked against the oracle in test_dnet_train_gradients and bitwise in the layer tests)
     monkeypatch.setattr(sys.modules[nconv_amd.DNET.__module__], "FUSE_HEAD_FWD", False)
     monkeypatch.setattr(sys.modules[nconv_amd.DNET.__module__], "FUSE_TAIL_FWD", False)
+    # (the per-layer path has no pooled-gradient one-kernel backward: compare like with like)
+    monkeypatch.setattr(sys.modules[nconv_amd.DNET.__module__], "FUSED_BWD", frozenset())
     res = []
     for whole in (True, False):
         net = make_net(nconv_amd, "generalized", gpu)
@@ -117,6 +119,7 @@ def test_materialised_pool_matches_pool_on_load(nconv_amd, gpu, H, W, monkeypatc
     dnet = sys.modules[nconv_amd.DNET.__module__]
     res = []
     monkeypatch.setattr(dnet, "FUSE_TAIL_BWD", False)
+    monkeypatch.setattr(dnet, "FUSED_BWD", frozenset())  # the two-kernel backward (one-kernel: test_gpu_fused_bwd)
     monkeypatch.setattr(dnet, "FUSE_HEAD_FWD", False)  # (the fused head's D2 rounds differently)
     monkeypatch.setattr(dnet, "FUSE_TAIL_FWD", False)
     for pooled in (True, False):
