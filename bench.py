@@ -90,6 +90,8 @@ def parse(argv=None):
                         "number per stream of --inference-streams, default 2)")
     p.add_argument("--mid-streams", type=int, default=None,
                    help="DNET.mid_streams: the quarter/eighth-resolution layers on that many batch slices")
+    p.add_argument("--guided-train-graph", type=int, default=1,
+                   help="replay the config-4 guided training step from a hipGraph (1) or eager (0)")
     p.add_argument("--head-density", type=float, default=0.40,
                    help="also time the forward's kernels at this depth density (0: skip); the headline is 5 %%")
     p.add_argument("--train-graph", type=int, default=1,
@@ -557,15 +559,16 @@ def guided_forward(m, dev, B, H, W, steps, warmup, rank):
     return el
 
 
-def make_guided_train_step(m, dev, B, H, W, rank):
+def make_guided_train_step(m, dev, B, H, W, rank, graph=True):
     """Config 4 per GPU: one SETP2_BP_TRAIN iteration as train_step2.py:60-66 (train mode, frozen
     step 1 still EnforcePos-drifted, batch-statistics BatchNorm), forward on B/2 + B/2 frames,
     calculate_loss_multi_resolution (MSE, train_step2.py:21), backward, RCCL all-reduce with
-    several ranks, AdamW lr 1e-4 / wd 1e-7."""
+    several ranks, AdamW lr 1e-4 / wd 1e-7. graph=True replays the iteration from a hipGraph
+    (train.GraphedTrainStep; fused capturable AdamW, the same update rule)."""
     torch.manual_seed(1)
     model = m.SETP2_BP_TRAIN(None, step1_crop="generalized").to(dev)
     net = m.dp.DataParallelRCCL(model)
-    opt = m.train.get_optimizer(net, "adam", 1e-4, 1e-7)
+    opt = m.train.get_optimizer(net, "adam", 1e-4, 1e-7, capturable=graph, fused=graph)
     g = torch.Generator().manual_seed(4000 + rank)
     h = B // 2
     rgb0 = (torch.rand(h, 3, H, W, generator=g) * 255).to(dev)
@@ -575,10 +578,17 @@ def make_guided_train_step(m, dev, B, H, W, rank):
     gt = sparse_depth(g, h, 480, 640, dev)
     net.train()
 
+    def loss_fn(model_, rgb0_, d0_, rgb1_, d1_, gt_):
+        est, _ = model_(rgb0_, d0_, rgb1_, d1_)
+        return m.train.calculate_loss_multi_resolution(est, gt_, False)
+
+    if graph:
+        gstep = m.train.GraphedTrainStep(net, opt, loss_fn, (rgb0, d0, rgb1, d1, gt))
+        return lambda: gstep()
+
     def step():
         opt.zero_grad()
-        est, _ = net(rgb0, d0, rgb1, d1)
-        loss = m.train.calculate_loss_multi_resolution(est, gt, False)
+        loss = loss_fn(net, rgb0, d0, rgb1, d1, gt)
         loss.backward()
         net.allreduce_grads()
         opt.step()
@@ -819,26 +829,37 @@ def main():
     if not a.no_guided_train:
         log("config 4 guided training step")
         gts = max(3, a.steps // 10)
-        st = make_guided_train_step(m, dev, B, H, W, rank)
-        warm_up(st, max(min(a.warmup, 2), 1))
-        torch.cuda.synchronize()
-        barrier()
-        t0 = time.perf_counter()
-        for _ in range(gts):
-            st()
-        torch.cuda.synchronize()
-        barrier()
-        tt = max_over_ranks(time.perf_counter() - t0)
         # forward + input gradient + weight gradient of every dense conv; frozen step 1 forward only
         fl = (3 * GUIDED_DENSE_FLOPS_PER_FRAME + PASS_FLOPS_PER_FRAME) * B * (H * W) / (352 * 1216)
+
+        def time_guided_train(graphed):
+            st = make_guided_train_step(m, dev, B, H, W, rank, graph=graphed)
+            warm_up(st, max(min(a.warmup, 2), 1))
+            torch.cuda.synchronize()
+            barrier()
+            t0 = time.perf_counter()
+            for _ in range(gts):
+                st()
+            torch.cuda.synchronize()
+            barrier()
+            el = max_over_ranks(time.perf_counter() - t0)
+            del st
+            torch.cuda.empty_cache()
+            return el
+        gmode = a.guided_train_graph != 0
+        tt = time_guided_train(gmode)
         guided_train = {"frames_per_sec": round(world * B * gts / tt, 2), "ms_per_step": round(tt / gts * 1e3, 3),
                         "steps": gts, "frames_per_step": B * world,
-                        "workload": "config4: SETP2_BP_TRAIN fwd+bwd+AdamW, B/2+B/2 frames per GPU, eager",
-                        "mode": "eager",
+                        "workload": "config4: SETP2_BP_TRAIN fwd+bwd+AdamW, B/2+B/2 frames per GPU, "
+                                    + ("hipGraph" if gmode else "eager"),
+                        "mode": "hipgraph" if gmode else "eager",
                         "fp32_tflops": round(fl / (tt / gts) / 1e12, 2),
                         "fp32_mfma_frac": round(fl / (tt / gts) / 1e12 / FP32_PEAK_TFLOPS, 4)}
-        del st
-        torch.cuda.empty_cache()
+        if gmode and world == 1:  # the eager step beside it
+            log("config 4 guided training step, eager")
+            te = time_guided_train(False)
+            guided_train["eager"] = {"frames_per_sec": round(world * B * gts / te, 2),
+                                     "ms_per_step": round(te / gts * 1e3, 3)}
 
     # ---- per-kernel times, rooflines, CPU baseline (rank 0) ----
     if rank == 0:

@@ -36,18 +36,7 @@ constexpr int pick_chunk(int n, int plane_f2, int budget) {
 // layer's output gradient at (oh, ow) is nconv7's input gradient there, G_xc = w7[o] gN7, G_c =
 // w7[o] gD7 with {gN7, gD7} from nconv7's (gy, y, cout) at (oh + 2, ow + 2); gy = G_xc * cout,
 // gcout = G_c + G_xc * y (nconv7's dgrad_tiled<8,1,1> epilogue, same operations).
-__device__ __forceinline__ unsigned t7_off(int oh, int ow, int Ho, int Wo, unsigned oob) {
-    return ((unsigned)oh < (unsigned)Ho && (unsigned)ow < (unsigned)Wo) ? (unsigned)((oh + 2) * (Wo + 4) + ow + 2) * 4u
-                                                                          : oob;
-}
-__device__ __forceinline__ void t7_nd(const BwdArgs& a, float gy9, float y9, float co9, float& gN7, float& gD7) {
-    nconv_grad_nd(gy9, 0.f, y9, co9, a.t7eps, a.t7b[0], a.t7s[0], gN7, gD7);
-}
-__device__ __forceinline__ void t7_gy(float w7, float gN7, float gD7, float y, float co, float& gy, float& gco) {
-    const float gxc = fmaf(w7, gN7, 0.f), gc = fmaf(w7, gD7, 0.f);  // the 1x1 dgrad's accumulators
-    gy = gxc * co;
-    gco = fmaf(gxc, y, gc);
-}
+// (t7_off, t7_nd, t7_gy: nconv_internal.h)
 
 template <int OHT, int OWT, int OWP, bool GP = false, bool T7 = false>
 struct GTileStager {
@@ -2153,6 +2142,20 @@ int launch_bwd(const LayerDev& d, const BwdArgs& a, hipStream_t st, const char**
             *why = "fused tail backward needs nconv6's exact-fp32 geometry (16->8 3x3, padding 0, upsample-first "
                    "exactly-2x concat)";
             return -95;
+        }
+        if (!a.separate && (a.gxa || a.gca || a.gxb || a.gcb) && (a.gw || a.gb) && fused_tail_bwd_ok(L)) {
+            // input and weight gradient (and nconv7's) in one kernel (nconv_bwd_fused.hip)
+            const int nb = launch_bwd_fused_tail(d, a, part, (int)wm_grid(L).nblk, st);
+            if (nb > 0) {
+                if (a.defer) {
+                    *a.t7nparts = nb;
+                } else {
+                    const RedJob J{a.t7part, a.t7s, a.t7gw, nullptr, nb, 8, 1, 8};
+                    if (int rc = launch_wgrad_reduce_multi(1, &J, st, why)) return rc;
+                }
+                const int rc = launch_wgrad_reduce(a, part, nb, 8 * 16 * 9, 8, 16 * 9, L.wsum, st, why);
+                return rc ? rc : last_err(why);
+            }
         }
         const int rc = go_bwd_tiled<16, 8, 3, NCONV_LOAD_UPCAT_UP_FIRST, false, false, true>(d, a, part, tx, tc, st, why);
         return rc ? rc : last_err(why);

@@ -482,4 +482,441 @@ int launch_bwd_fused(const LayerDev& d, const BwdArgs& a, float* part, int max_b
     return g.nblk;
 }
 
+
+
+// ================================================================================================
+// nconv6 + nconv7 (the training tail) in one backward kernel.
+//
+// nconv6 is 16 -> 8, 3x3, padding 0 over cat(up2x(x23) [channels 0..7], x2 [8..15]) (step1.py:88-90,
+// UP_FIRST), and its output feeds nconv7 (1x1, padding 2), whose backward is folded in as in
+// dgrad_phase<T7> / wgrad_mfma<T7>: nconv6's (gy, gcout) are formed from nconv7's (gy, y, cout) while
+// {gN, gD} are staged, nconv7's weight gradient is summed beside nconv6's. Row-streaming strips as
+// bwd_fused (input rows s of a 64-column strip, segments of an even number of rows):
+//   * weight gradient of output row s (lane = (o, i8): the upsampled channel i8 and the skip channel
+//     8 + i8, 9 taps each; the input rows s .. s+2 staged at full resolution, the upsampled half
+//     expanded from its low plane at staging);
+//   * skip-channel input gradient of input row s (g rows s-2 .. s; lane = column, wave = output-
+//     channel pair, the four waves' partials summed in a fixed order);
+//   * after each odd row s = 2p + 1, the upsampled channels' gradient of low row p straight into the
+//     low-resolution producer: the nearest-upsample backward sums a 2x2 block, which is a 4x4
+//     correlation of {gN, gD} (g rows 2p-2 .. 2p+1) with box-summed weights (dgrad_phase's form;
+//     lane = (low column, channel half), box weights broadcast from LDS).
+namespace ft {
+constexpr int kT = 256;
+constexpr int CO = 8, CI = 16, TW = 64, LW = TW / 2;
+constexpr int GW = TW + 2;               // g columns c0-2 .. c0+63
+constexpr int XP = 136, GPT = 136;       // channel-row pitches (floats), 8 * pitch distinct mod 64
+constexpr int NSX = 3, NSG = 4;
+constexpr int XSLOT = CI * XP, GSLOT = CO * GPT;
+constexpr int X_OFF = 0;
+constexpr int G_OFF = X_OFF + NSX * XSLOT;
+constexpr int RS_OFF = G_OFF + NSG * GSLOT;      // skip partials [4][8][64] f2
+constexpr int RU_OFF = RS_OFF + 4 * 8 * 2 * TW;  // upsampled partials [4][8][32] f2
+constexpr int WB_OFF = RU_OFF + 4 * 8 * 2 * LW;  // box weights [o][t][u][i]
+constexpr int LDS_MAIN = WB_OFF + CO * 16 * 8;
+constexpr int FIN = 4 * 36 * 64;
+constexpr int LDS = LDS_MAIN > FIN ? LDS_MAIN : FIN;
+constexpr int NW = CO * CI * 9;          // 1152 weights
+constexpr unsigned OOB = 0x80000000u;
+static_assert(XP >= 2 * TW && GPT >= 2 * GW, "pitches");
+}  // namespace ft
+
+__global__ __launch_bounds__(ft::kT) __attribute__((amdgpu_waves_per_eu(2, 2))) void bwd_fused_tail(
+    LayerDev d, BwdArgs a, float* part, int nstrip, int nseg, int seg_rows) {
+    using namespace ft;
+    __shared__ __attribute__((aligned(16))) float lds[LDS];
+    const nconv_layer& L = d.L;
+    const cfloat* wgt = (const cfloat*)L.weight;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const TileCoord tc = xcd_tile(nstrip, nseg, L.B);
+    const int b = tc.b, c0 = tc.tx * TW;
+    const int H = L.H, W = L.W, Ho = L.Ho, Wo = L.Wo, Hl = L.b.H, Wl = L.b.W;
+    const int r0 = tc.ty * seg_rows, r1 = min(H, r0 + seg_rows);
+    const int plane = H * W, lplane = Hl * Wl, oplane = Ho * Wo;
+
+    // box weights [o][t][u][i] (t, u = 0..3 collect the taps S(0) = {2}, S(1) = {1, 2}, S(2) = {0, 1},
+    // S(3) = {0}; dgrad_phase / box_weights), from the upsampled channels' weights (0..7)
+    for (int e = tid; e < CO * 16 * 8; e += kT) {
+        const int i = e & 7, u = (e >> 3) & 3, t = (e >> 5) & 3, o = e >> 7;
+        const cfloat* wk = wgt + ((size_t)o * CI + i) * 9;
+        const int h0 = t == 0 ? 2 : (t == 1 ? 1 : 0), nh = (t == 1 || t == 2) ? 2 : 1;
+        const int w0 = u == 0 ? 2 : (u == 1 ? 1 : 0), nw = (u == 1 || u == 2) ? 2 : 1;
+        float sum = 0.f;
+        for (int r = 0; r < nh; ++r)
+            for (int c = 0; c < nw; ++c) sum += wk[(h0 + r) * 3 + w0 + c];
+        lds[WB_OFF + e] = sum;
+    }
+
+    // ---- resources ----
+    const __amdgpu_buffer_rsrc_t rax = plane_rsrc(L.a.x + (size_t)b * 8 * plane, 8 * plane * 4);
+    const __amdgpu_buffer_rsrc_t rac = plane_rsrc(L.a.c + (size_t)b * 8 * plane, 8 * plane * 4);
+    const __amdgpu_buffer_rsrc_t rbx = plane_rsrc(L.b.x + (size_t)b * 8 * lplane, 8 * lplane * 4);
+    const __amdgpu_buffer_rsrc_t rbc = plane_rsrc(L.b.c + (size_t)b * 8 * lplane, 8 * lplane * 4);
+    const __amdgpu_buffer_rsrc_t ry = plane_rsrc(a.y + (size_t)b * CO * oplane, CO * oplane * 4);
+    const __amdgpu_buffer_rsrc_t rco = plane_rsrc(a.co + (size_t)b * CO * oplane, CO * oplane * 4);
+    const int pl7 = (Ho + 4) * (Wo + 4);
+    const __amdgpu_buffer_rsrc_t r7g = plane_rsrc(a.t7gy + (size_t)b * pl7, pl7 * 4);
+    const __amdgpu_buffer_rsrc_t r7y = plane_rsrc(a.t7y + (size_t)b * pl7, pl7 * 4);
+    const __amdgpu_buffer_rsrc_t r7c = plane_rsrc(a.t7co + (size_t)b * pl7, pl7 * 4);
+
+    // ---- input rows: wave w stages the upsampled channels w, w + 4 and the skip channels 8 + w, 12 + w ----
+    float px[4], pc[4];
+    const int iwl = c0 + lane;
+    auto load_x = [&](int ih) {
+        const bool in = (unsigned)ih < (unsigned)H && iwl < W;
+        const unsigned off = in ? (unsigned)(ih * W + iwl) * 4u : OOB;
+        const unsigned offl = in ? (unsigned)((ih >> 1) * Wl + (iwl >> 1)) * 4u : OOB;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            px[k] = ld_f32s(rbx, offl, (w + 4 * k) * lplane * 4);
+            pc[k] = ld_f32s(rbc, offl, (w + 4 * k) * lplane * 4);
+            px[2 + k] = ld_f32s(rax, off, (w + 4 * k) * plane * 4);
+            pc[2 + k] = ld_f32s(rac, off, (w + 4 * k) * plane * 4);
+        }
+    };
+    auto store_x = [&](int ih) {
+        float* xs = lds + X_OFF + ring(ih, NSX) * XSLOT + 2 * lane;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int ch = (k < 2 ? 0 : 8) + w + 4 * (k & 1);
+            *reinterpret_cast<f2*>(xs + ch * XP) = (f2){px[k] * pc[k], pc[k]};
+        }
+    };
+
+    // ---- g rows (nconv6's output row oh, columns c0-2+m, m = 0..65): {gN, gD} of channels w, w+4 from
+    //      nconv7's planes; main pass m = lane, halo lanes 0..3: channel w + 4 (lane >> 1), m = 64 + (lane & 1) ----
+    float g7[2][3], gv[2][2], gvh[2];
+    const bool hl = lane < 4;
+    const int hk = (lane >> 1) & 1, ho = w + 4 * hk;
+    const int owm = c0 - 2 + lane, owh = c0 + 62 + (lane & 1);
+    auto load_g = [&](int oh) {
+        const unsigned o7 = t7_off(oh, owm, Ho, Wo, OOB), o7h = hl ? t7_off(oh, owh, Ho, Wo, OOB) : OOB;
+        g7[0][0] = ld_f32(r7g, o7);
+        g7[0][1] = ld_f32(r7y, o7);
+        g7[0][2] = ld_f32(r7c, o7);
+        g7[1][0] = ld_f32(r7g, o7h);
+        g7[1][1] = ld_f32(r7y, o7h);
+        g7[1][2] = ld_f32(r7c, o7h);
+        const bool in = (unsigned)oh < (unsigned)Ho && (unsigned)owm < (unsigned)Wo;
+        const bool inh = hl && (unsigned)oh < (unsigned)Ho && (unsigned)owh < (unsigned)Wo;
+        const unsigned off = in ? (unsigned)(oh * Wo + owm) * 4u : OOB;
+        const unsigned offh = inh ? (unsigned)((ho * Ho + oh) * Wo + owh) * 4u : OOB;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            gv[k][0] = ld_f32s(ry, off, (w + 4 * k) * oplane * 4);
+            gv[k][1] = ld_f32s(rco, off, (w + 4 * k) * oplane * 4);
+        }
+        gvh[0] = ld_f32(ry, offh);
+        gvh[1] = ld_f32(rco, offh);
+    };
+    float bias_o[2], wsum_o[2], w7_o[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        bias_o[k] = L.bias[w + 4 * k];
+        wsum_o[k] = L.wsum[w + 4 * k];
+        w7_o[k] = a.t7w[w + 4 * k];
+    }
+    const float bias_h = hk ? bias_o[1] : bias_o[0], wsum_h = hk ? wsum_o[1] : wsum_o[0], w7_h = hk ? w7_o[1] : w7_o[0];
+    float gb_acc[2] = {0.f, 0.f}, gs_acc[2] = {0.f, 0.f}, gb_h = 0.f, gs_h = 0.f;
+    float w7n[2] = {0.f, 0.f}, w7d[2] = {0.f, 0.f}, w7nh = 0.f, w7dh = 0.f;
+    auto store_g = [&](int oh, bool count) {
+        float* gs = lds + G_OFF + ring(oh, NSG) * GSLOT;
+        float n7, d7, n7h, d7h;
+        t7_nd(a, g7[0][0], g7[0][1], g7[0][2], n7, d7);
+        t7_nd(a, g7[1][0], g7[1][1], g7[1][2], n7h, d7h);
+        const bool own = count && lane >= 2;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            float gy, gco, gN, gD;
+            t7_gy(w7_o[k], n7, d7, gv[k][0], gv[k][1], gy, gco);
+            nconv_grad_nd(gy, gco, gv[k][0], gv[k][1], L.eps, bias_o[k], wsum_o[k], gN, gD);
+            *reinterpret_cast<f2*>(gs + (w + 4 * k) * GPT + 2 * lane) = (f2){gN, gD};
+            if (own) {
+                gb_acc[k] += gy;
+                gs_acc[k] = fmaf(gco, gv[k][1], gs_acc[k]);
+                w7n[k] = fmaf(gv[k][0] * gv[k][1], n7, w7n[k]);  // nconv7: corr(x*c, gN7) + corr(c, gD7)
+                w7d[k] = fmaf(gv[k][1], d7, w7d[k]);
+            }
+        }
+        float gy, gco, gN, gD;
+        t7_gy(w7_h, n7h, d7h, gvh[0], gvh[1], gy, gco);
+        nconv_grad_nd(gy, gco, gvh[0], gvh[1], L.eps, bias_h, wsum_h, gN, gD);
+        if (hl) {
+            *reinterpret_cast<f2*>(gs + ho * GPT + 2 * (64 + (lane & 1))) = (f2){gN, gD};
+            if (count) {
+                gb_h += gy;
+                gs_h = fmaf(gco, gvh[1], gs_h);
+                w7nh = fmaf(gvh[0] * gvh[1], n7h, w7nh);
+                w7dh = fmaf(gvh[1], d7h, w7dh);
+            }
+        }
+    };
+    // epilogue inputs: the skip row's (x, c) for channels 2w, 2w+1 at column c0 + lane; the low row's
+    // (x, c) of channel i = tid >> 5 at low column c0/2 + (tid & 31)
+    float ex[2], ec[2], ux = 0.f, uc = 0.f;
+    auto load_e = [&](int ih) {
+        const bool in = (unsigned)ih < (unsigned)H && iwl < W;
+        const unsigned off = in ? (unsigned)(ih * W + iwl) * 4u : OOB;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            ex[k] = ld_f32s(rax, off, (2 * w + k) * plane * 4);
+            ec[k] = ld_f32s(rac, off, (2 * w + k) * plane * 4);
+        }
+    };
+    const int uq = tid & 31, ui = tid >> 5, uql = (c0 >> 1) + uq;
+    auto load_u = [&](int p) {
+        const bool in = (unsigned)p < (unsigned)Hl && uql < Wl;
+        // (the channel differs between the wave's two 32-lane halves: its plane offset rides the
+        // per-lane offset, not soffset, which must be wave-uniform)
+        const unsigned off = (in ? (unsigned)(p * Wl + uql) * 4u : OOB) + (unsigned)(ui * lplane * 4);
+        ux = ld_f32(rbx, off);
+        uc = ld_f32(rbc, off);
+    };
+
+    f2 wu[3][3], wsk[3][3];  // weight-gradient accumulators: lane (o, i8), upsampled i8 / skip 8 + i8
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) wu[kh][kw] = wsk[kh][kw] = (f2){0.f, 0.f};
+    const int wo = lane >> 3, wi = lane & 7;
+
+    if (r0 < r1) {
+        for (int r = r0; r < r0 + 2; ++r) {  // prologue: input rows r0, r0+1; g rows r0-2, r0-1
+            load_x(r);
+            store_x(r);
+        }
+        for (int r = r0 - 2; r < r0; ++r) {
+            load_g(r);
+            store_g(r, false);
+        }
+        load_x(r0 + 2);
+        load_g(r0);
+        load_e(r0);
+        load_u(r0 >> 1);
+    }
+    const bool accm = a.accumulate != 0;
+#pragma unroll 1
+    for (int s = r0; s < r1; ++s) {
+        const bool up = (s & 1) != 0;  // low row (s - 1) / 2 complete after this row
+        store_x(s + 2);
+        store_g(s, true);
+        const float exc[2] = {ex[0], ex[1]}, ecc[2] = {ec[0], ec[1]};
+        const float uxc = ux, ucc = uc;
+        __syncthreads();
+        {
+            const int nx = min(s + 3, r1 + 1);  // (rows past the segment clamped: staged, unused)
+            load_x(nx);
+            load_g(min(s + 1, r1));
+            load_e(min(s + 1, r1 - 1));
+            if (up) load_u(min((s + 1) >> 1, (r1 >> 1) - 1) + 0);  // next odd row's low row
+        }
+        if (s < Ho) {  // ---- weight gradient of output row s: columns 16w .. 16w+15 ----
+            const float* gr = lds + G_OFF + ring(s, NSG) * GSLOT + wo * GPT;
+            const float* xu[3];
+            const float* xk[3];
+#pragma unroll
+            for (int kh = 0; kh < 3; ++kh) {
+                xu[kh] = lds + X_OFF + ring(s + kh, NSX) * XSLOT + wi * XP;
+                xk[kh] = xu[kh] + 8 * XP;
+            }
+            const int j0 = 16 * w;
+            f2 gwin[3];  // gwin[k] = g at local column j + k  (ow = iw - 2 + k, i.e. kw = 2 - k)
+#pragma unroll
+            for (int k = 0; k < 2; ++k) gwin[k] = *reinterpret_cast<const f2*>(gr + 2 * (j0 + k));
+#pragma unroll
+            for (int t = 0; t < 16; ++t) {
+                const int j = j0 + t;
+                gwin[2] = *reinterpret_cast<const f2*>(gr + 2 * (j + 2));
+                f2 vu[3], vk[3];
+#pragma unroll
+                for (int kh = 0; kh < 3; ++kh) {
+                    vu[kh] = *reinterpret_cast<const f2*>(xu[kh] + 2 * j);
+                    vk[kh] = *reinterpret_cast<const f2*>(xk[kh] + 2 * j);
+                }
+#pragma unroll
+                for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+                    for (int kw = 0; kw < 3; ++kw) {
+                        wu[kh][kw] = __builtin_elementwise_fma(vu[kh], gwin[2 - kw], wu[kh][kw]);
+                        wsk[kh][kw] = __builtin_elementwise_fma(vk[kh], gwin[2 - kw], wsk[kh][kw]);
+                    }
+                gwin[0] = gwin[1];
+                gwin[1] = gwin[2];
+            }
+        }
+        {   // ---- skip-channel input gradient of input row s: output channels 2w, 2w + 1 ----
+            f2 acc[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) acc[i] = (f2){0.f, 0.f};
+#pragma unroll 1
+            for (int oo = 0; oo < 2; ++oo) {
+                const int o = 2 * w + oo;
+#pragma unroll
+                for (int kh = 0; kh < 3; ++kh) {  // g row s - kh, columns iw - kw -> local j + 2 - kw
+                    const float* gr = lds + G_OFF + ring(s - kh, NSG) * GSLOT + o * GPT + 2 * lane;
+                    f2 v[3];
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) v[k] = *reinterpret_cast<const f2*>(gr + 2 * k);
+                    const cfloat* wr = wgt + ((size_t)o * CI + 8) * 9 + kh * 3;
+#pragma unroll
+                    for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+                        for (int i = 0; i < 8; ++i) {
+                            const float wv = wr[i * 9 + kw];
+                            acc[i] = __builtin_elementwise_fma((f2){wv, wv}, v[2 - kw], acc[i]);
+                        }
+                }
+            }
+            float* rp = lds + RS_OFF + w * (8 * 2 * TW) + 2 * lane;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) *reinterpret_cast<f2*>(rp + i * 2 * TW) = acc[i];
+        }
+        if (up) {  // ---- upsampled channels of low row p = (s - 1) / 2: g rows 2p-2 .. 2p+1 = s-3 .. s ----
+            const int q = lane & 31, ih4 = lane >> 5;  // low column, channel half (4 ih4 .. 4 ih4 + 3)
+            f2 au[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) au[c] = (f2){0.f, 0.f};
+#pragma unroll 1
+            for (int oo = 0; oo < 2; ++oo) {
+                const int o = 2 * w + oo;
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const float* gr = lds + G_OFF + ring(s - 3 + t, NSG) * GSLOT + o * GPT + 4 * q;
+                    const f4 q0 = *reinterpret_cast<const f4*>(gr), q1 = *reinterpret_cast<const f4*>(gr + 4);
+                    const f2 g[4] = {q0.xy, q0.zw, q1.xy, q1.zw};
+                    const float* wb = lds + WB_OFF + (o * 16 + t * 4) * 8 + 4 * ih4;
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const f4 wv = *reinterpret_cast<const f4*>(wb + u * 8);
+#pragma unroll
+                        for (int c = 0; c < 4; ++c) au[c] = __builtin_elementwise_fma((f2){wv[c], wv[c]}, g[u], au[c]);
+                    }
+                }
+            }
+            float* rp = lds + RU_OFF + w * (8 * 2 * LW) + 2 * q;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) *reinterpret_cast<f2*>(rp + (4 * ih4 + c) * 2 * LW) = au[c];
+        }
+        __syncthreads();
+        {   // ---- skip epilogue: input row s, channels 2w, 2w + 1 -> gxa / gca ----
+            const bool ok = iwl < W;
+            const unsigned eoff = ok ? (unsigned)(s * W + iwl) * 4u : OOB;
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const int i = 2 * w + k;
+                const float* rp = lds + RS_OFF + i * 2 * TW + 2 * lane;
+                constexpr int WS = 8 * 2 * TW;
+                const f2 G = ((*reinterpret_cast<const f2*>(rp) + *reinterpret_cast<const f2*>(rp + WS)) +
+                              *reinterpret_cast<const f2*>(rp + 2 * WS)) + *reinterpret_cast<const f2*>(rp + 3 * WS);
+                const float gx = G.x * ecc[k], gc = G.y + G.x * exc[k];
+                const unsigned o = eoff + (unsigned)(i * plane * 4);
+                if (a.gxa) {
+                    const __amdgpu_buffer_rsrc_t r = plane_rsrc(a.gxa + (size_t)b * 8 * plane, 8 * plane * 4);
+                    const float prev = accm ? ld_f32(r, o) : 0.f;
+                    if (ok) st_f32(r, o, accm ? prev + gx : gx);
+                }
+                if (a.gca) {
+                    const __amdgpu_buffer_rsrc_t r = plane_rsrc(a.gca + (size_t)b * 8 * plane, 8 * plane * 4);
+                    const float prev = accm ? ld_f32(r, o) : 0.f;
+                    if (ok) st_f32(r, o, accm ? prev + gc : gc);
+                }
+            }
+        }
+        if (up) {  // ---- upsampled epilogue: low row p, channel ui, low column c0/2 + uq -> gxb / gcb ----
+            const int p = (s - 1) >> 1;
+            const bool ok = p < Hl && uql < Wl;
+            const float* rp = lds + RU_OFF + ui * 2 * LW + 2 * uq;
+            constexpr int WS = 8 * 2 * LW;
+            const f2 G = ((*reinterpret_cast<const f2*>(rp) + *reinterpret_cast<const f2*>(rp + WS)) +
+                          *reinterpret_cast<const f2*>(rp + 2 * WS)) + *reinterpret_cast<const f2*>(rp + 3 * WS);
+            const float gx = G.x * ucc, gc = G.y + G.x * uxc;
+            const unsigned o = ok ? (unsigned)((ui * Hl + p) * Wl + uql) * 4u : OOB;
+            if (a.gxb) {
+                const __amdgpu_buffer_rsrc_t r = plane_rsrc(a.gxb + (size_t)b * 8 * lplane, 8 * lplane * 4);
+                const float prev = accm ? ld_f32(r, o) : 0.f;
+                if (ok) st_f32(r, o, accm ? prev + gx : gx);
+            }
+            if (a.gcb) {
+                const __amdgpu_buffer_rsrc_t r = plane_rsrc(a.gcb + (size_t)b * 8 * lplane, 8 * lplane * 4);
+                const float prev = accm ? ld_f32(r, o) : 0.f;
+                if (ok) st_f32(r, o, accm ? prev + gc : gc);
+            }
+        }
+    }
+
+    // ---- partial rows ----
+    __syncthreads();
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+            const int e = (kh * 3 + kw) * 2;
+            lds[(w * 36 + e) * 64 + lane] = wu[kh][kw].x;
+            lds[(w * 36 + e + 1) * 64 + lane] = wu[kh][kw].y;
+            lds[(w * 36 + 18 + e) * 64 + lane] = wsk[kh][kw].x;
+            lds[(w * 36 + 18 + e + 1) * 64 + lane] = wsk[kh][kw].y;
+        }
+    __syncthreads();
+    float* out = part + (size_t)blockIdx.x * (NW + 2 * CO);
+    for (int idx = tid; idx < NW; idx += kT) {  // gW[o][i][kh][kw], i < 8 upsampled, 8.. skip
+        const int o = idx / 144, i = (idx / 9) % 16, tap = idx % 9;
+        const int src = o * 8 + (i & 7), e = (i < 8 ? 0 : 18) + tap * 2;
+        float v[2];
+#pragma unroll
+        for (int pp = 0; pp < 2; ++pp)
+            v[pp] = ((lds[(0 * 36 + e + pp) * 64 + src] + lds[(1 * 36 + e + pp) * 64 + src]) +
+                     lds[(2 * 36 + e + pp) * 64 + src]) + lds[(3 * 36 + e + pp) * 64 + src];
+        out[idx] = v[0] + v[1];
+    }
+    float* o7 = a.t7part + (size_t)blockIdx.x * 10;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const bool mine = hl && hk == k;
+        float sb = gb_acc[k] + (mine ? gb_h : 0.f), ss = gs_acc[k] + (mine ? gs_h : 0.f);
+        float sn = w7n[k] + (mine ? w7nh : 0.f), sd = w7d[k] + (mine ? w7dh : 0.f);
+#pragma unroll
+        for (int sh = 32; sh > 0; sh >>= 1) {
+            sb += __shfl_xor(sb, sh);
+            ss += __shfl_xor(ss, sh);
+            sn += __shfl_xor(sn, sh);
+            sd += __shfl_xor(sd, sh);
+        }
+        if (lane == 0) {
+            out[NW + w + 4 * k] = sb;
+            out[NW + CO + w + 4 * k] = ss;
+            o7[w + 4 * k] = sn + sd;
+        }
+    }
+    if (tid < 2) o7[8 + tid] = 0.f;
+}
+
+bool fused_tail_bwd_ok(const nconv_layer& L) {
+    return L.Cin == 16 && L.Cout == 8 && L.a.C == 8 && L.b.C == 8 && L.KH == 3 && L.KW == 3 && L.PH == 0 &&
+           L.PW == 0 && L.SH == 1 && L.SW == 1 && L.DH == 1 && L.DW == 1 && L.groups == 1 &&
+           L.load_mode == NCONV_LOAD_UPCAT_UP_FIRST && L.bwd_math == NCONV_MATH_FP32 && L.a.H == L.H &&
+           L.a.W == L.W && L.H == 2 * L.b.H && L.W == 2 * L.b.W && L.Ho == L.H - 2 && L.Wo == L.W - 2 && L.H >= 2;
+}
+
+int launch_bwd_fused_tail(const LayerDev& d, const BwdArgs& a, float* part, int max_blocks, hipStream_t st) {
+    const nconv_layer& L = d.L;
+    const int nstrip = (L.W + ft::TW - 1) / ft::TW, per_img = nstrip * L.B;
+    static int rounds = [] {
+        const char* e = getenv("NCONV_FB_ROUNDS");
+        const int r = e ? atoi(e) : 3;
+        return r > 0 ? r : 3;
+    }();
+    int target = rounds * dev_cus() * 2;
+    if (target > max_blocks) target = max_blocks;
+    int nseg = target / per_img;
+    nseg = nseg < 1 ? 1 : (nseg > L.H / 2 ? L.H / 2 : nseg);
+    int seg_rows = (L.H + nseg - 1) / nseg;
+    seg_rows += seg_rows & 1;  // even: a low row's two full-resolution rows in one segment
+    nseg = (L.H + seg_rows - 1) / seg_rows;
+    const int nblk = nstrip * nseg * L.B;
+    if (nblk > max_blocks || nblk <= 0) return -1;
+    hipLaunchKernelGGL(bwd_fused_tail, dim3(nblk), dim3(ft::kT), 0, st, d, a, part, nstrip, nseg, seg_rows);
+    return nblk;
+}
+
 }  // namespace nconv

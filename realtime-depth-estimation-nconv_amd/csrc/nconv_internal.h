@@ -75,6 +75,22 @@ struct BwdArgs {
     int* t7nparts;
     int separate;  // NCONV_BWD_SEPARATE: no one-kernel backward (input and weight gradient as two kernels)
 };
+// nconv7 (1x1, padding 2) consumer fused into its producer's backward (T7): byte offset of nconv6
+// pixel (oh, ow) in nconv7's (Ho + 4) x (Wo + 4) grid, or oob outside nconv6's grid; nconv7's {gN7,
+// gD7} from its (gy, y, cout) (its cout gradient is 0); nconv6's (gy, gcout) from them and w7[o] as
+// nconv7's own 1x1 input gradient forms them (dgrad_tiled<8,1,1>'s epilogue, same operations)
+__device__ __forceinline__ unsigned t7_off(int oh, int ow, int Ho, int Wo, unsigned oob) {
+    return ((unsigned)oh < (unsigned)Ho && (unsigned)ow < (unsigned)Wo) ? (unsigned)((oh + 2) * (Wo + 4) + ow + 2) * 4u
+                                                                          : oob;
+}
+__device__ __forceinline__ void t7_nd(const BwdArgs& a, float gy9, float y9, float co9, float& gN7, float& gD7) {
+    nconv_grad_nd(gy9, 0.f, y9, co9, a.t7eps, a.t7b[0], a.t7s[0], gN7, gD7);
+}
+__device__ __forceinline__ void t7_gy(float w7, float gN7, float gD7, float y, float co, float& gy, float& gco) {
+    const float gxc = fmaf(w7, gN7, 0.f), gc = fmaf(w7, gD7, 0.f);  // the 1x1 dgrad's accumulators
+    gy = gxc * co;
+    gco = fmaf(gxc, y, gc);
+}
 size_t bwd_tail_workspace_bytes(const nconv_layer& L6);
 size_t bwd_head_workspace_bytes(const nconv_layer& L2);
 
@@ -145,6 +161,11 @@ FusedGrid fused_grid(const nconv_layer& L, int max_blocks);
 bool fused_bwd_ok(const nconv_layer& L);
 int launch_bwd_fused(const LayerDev& d, const BwdArgs& a, float* part, int max_blocks, bool gp, bool hw,
                      hipStream_t st);
+// The same for nconv6 with nconv7's backward fused (T7: 16 -> 8 3x3, padding 0, upsample-first
+// exactly-2x concat): skip-channel input gradient at full resolution, upsampled-channel gradient
+// straight to the low-resolution producer (box weights), weight gradient, nconv7's weight gradient
+bool fused_tail_bwd_ok(const nconv_layer& L);
+int launch_bwd_fused_tail(const LayerDev& d, const BwdArgs& a, float* part, int max_blocks, hipStream_t st);
 
 // Dense convolutions (RGB-guided model).
 int dense_cout_tile(int Cout);

@@ -153,7 +153,8 @@ class DNETFn(torch.autograd.Function):
             # included, as autograd's conv bias gradient)
             g9c = g9.contiguous()
             layer_bwd(sp[7], (X[2][0], X[2][1], X[7][0], X[7][1], *W[7]), X[8][0], X[8][1], None, None,
-                      (*G[2], *G[7]), gw[7], gb[7], tail=(sp[8], *W[8], X[9][0], X[9][1], g9c, gw[8]))
+                      (*G[2], *G[7]), gw[7], gb[7], tail=(sp[8], *W[8], X[9][0], X[9][1], g9c, gw[8]),
+                      fused="nconv6" in FUSED_BWD)
             if gb[8] is not None:  # (libnconv's per-channel sum)
                 dense.relu_bias_bwd(g9c, None, None, gb[8])
         else:

@@ -91,11 +91,13 @@ def test_fused_bwd_deterministic(nconv_amd, gpu):
         assert torch.equal(a[k], b[k]), k
 
 
-@pytest.mark.parametrize("layers", [("nconv2",), ("nconv2", "nconv_down1", "nconv_down2")])
+@pytest.mark.parametrize("layers", [("nconv2",), ("nconv6",), ("nconv2", "nconv6"),
+                                    ("nconv2", "nconv_down1", "nconv_down2", "nconv6")])
 def test_dnet_fused_bwd_matches_two_kernel(nconv_amd, gpu, monkeypatch, layers):
-    """The DNET training backward with the one-kernel form on nconv2 (default) or on every pooled
-    8 -> 8 5x5 layer against the two-kernel form: outputs bitwise, every gradient within 1e-5
-    normwise (nconv1's, fused into nconv2's backward in both, too)."""
+    """The DNET training backward with the one-kernel forms (nconv2, the pooled 8 -> 8 5x5 down
+    layers, nconv6 + nconv7) against the two-kernel forms: outputs bitwise, every gradient within
+    1e-5 normwise (nconv1's, fused into nconv2's backward in both, and nconv7's, fused into
+    nconv6's, too)."""
     dnet = sys.modules[nconv_amd.DNET.__module__]
     g = torch.Generator().manual_seed(77)
     B, H, W = 2, 96, 200
@@ -116,3 +118,66 @@ def test_dnet_fused_bwd_matches_two_kernel(nconv_amd, gpu, monkeypatch, layers):
     assert set(ga) == set(gb) and len(ga) == 18
     bad = [(k, _rel(gb[k], ga[k])) for k in ga if _rel(gb[k], ga[k]) > 1e-5]
     assert not bad, bad
+
+
+def _tail_setup(nconv_amd, gpu, B, H, W, seed):
+    """nconv6 (16 -> 8 3x3 padding 0 on cat(up2x(x7), x2)) + nconv7 (1x1 padding 2) as DNET's training
+    tail builds them, with random inputs and a random gradient of nconv7's output."""
+    dnet = sys.modules[nconv_amd.DNET.__module__]
+    N = nconv_amd.nconv
+    torch.manual_seed(seed)
+    net = nconv_amd.SETP1_NCONV(crop="generalized").to(gpu)
+    d = net.d_net
+    with torch.no_grad():  # trained-like positive weights
+        for m in (d.nconv6, d.nconv7):
+            m.weight.copy_(torch.nn.functional.softplus(m.weight, beta=10))
+    g = torch.Generator().manual_seed(seed)
+    x2 = (torch.rand(B, 8, H, W, generator=g) * 5).to(gpu)
+    c2 = torch.rand(B, 8, H, W, generator=g).to(gpu)
+    x7 = (torch.rand(B, 8, H // 2, W // 2, generator=g) * 5).to(gpu)
+    c7 = torch.rand(B, 8, H // 2, W // 2, generator=g).to(gpu)
+    l6, l7 = d.nconv6, d.nconv7
+    s6, s7 = torch.empty(8, device=gpu), torch.empty(1, device=gpu)
+    N.weight_prep([l6.weight.detach(), l7.weight.detach()], [False, False], [s6, s7])
+    w6 = d._phase_weights(gpu)[2]
+    sp6, sp7 = l6.spec(nconv_amd._lib.UPCAT_UP_FIRST), l7.spec()
+    W6 = (l6.weight.detach(), l6.bias.detach(), s6)
+    W7 = (l7.weight.detach(), l7.bias.detach(), s7)
+    x8, c8, x9, c9 = dnet._tail_train(sp6, sp7, x2, c2, x7, c7, W6, W7, w6)
+    g9 = torch.randn(x9.shape, generator=g).to(gpu)
+    return dict(sp6=sp6, sp7=sp7, x2=x2, c2=c2, x7=x7, c7=c7, W6=W6, W7=W7, x8=x8, c8=c8, x9=x9, c9=c9, g9=g9)
+
+
+def _tail_run(nconv_amd, t, separate):
+    N = nconv_amd.nconv
+    out = dict(gxa=torch.empty_like(t["x2"]), gca=torch.empty_like(t["c2"]), gxb=torch.empty_like(t["x7"]),
+               gcb=torch.empty_like(t["c7"]), gw=torch.empty_like(t["W6"][0]), gb=torch.empty_like(t["W6"][1]),
+               gw7=torch.empty_like(t["W7"][0]))
+    N.layer_backward(t["sp6"], (t["x2"], t["c2"], t["x7"], t["c7"], *t["W6"]), t["x8"], t["c8"], None, None,
+                     (out["gxa"], out["gca"], out["gxb"], out["gcb"]), out["gw"], out["gb"],
+                     tail=(t["sp7"], *t["W7"], t["x9"], t["c9"], t["g9"], out["gw7"]), separate=separate)
+    torch.cuda.synchronize()
+    return out
+
+
+@pytest.mark.parametrize("B,H,W", [(2, 64, 128), (1, 48, 200), (3, 20, 66), (2, 100, 130), (8, 352, 1216)])
+def test_fused_tail_bwd_matches_separate(nconv_amd, gpu, B, H, W):
+    """nconv6 + nconv7 backward in one kernel against dgrad_phase<T7> + wgrad_mfma<T7>: the skip
+    channels' gradient, the upsampled channels' (low-resolution) gradient, nconv6's and nconv7's
+    weight gradients and nconv6's bias gradient within 1e-5 normwise (fp32 reassociation)."""
+    t = _tail_setup(nconv_amd, gpu, B, H, W, seed=B * 100 + H + W)
+    a = _tail_run(nconv_amd, t, separate=True)
+    b = _tail_run(nconv_amd, t, separate=False)
+    rels = {k: _rel(b[k], a[k]) for k in a}
+    print(B, H, W, {k: f"{v:.2e}" for k, v in rels.items()})
+    for k in a:
+        assert torch.isfinite(b[k]).all(), k
+        assert rels[k] <= 1e-5, (k, rels[k])
+
+
+def test_fused_tail_bwd_deterministic(nconv_amd, gpu):
+    t = _tail_setup(nconv_amd, gpu, 2, 96, 160, seed=3)
+    a = _tail_run(nconv_amd, t, separate=False)
+    b = _tail_run(nconv_amd, t, separate=False)
+    for k in a:
+        assert torch.equal(a[k], b[k]), k

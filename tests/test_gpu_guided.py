@@ -215,3 +215,46 @@ def test_guided_config4_full_size_training_vs_oracle(nconv_amd, gpu):
     print("\n".join(f"{k}: {r:.2e}" for k, r in rel.items()))
     bad = [f"{k}: {r:.2e}" for k, r in rel.items() if r > _tol64(k)]
     assert not bad, "\n".join(bad)
+
+
+@pytest.mark.timeout(300)
+def test_guided_graphed_train_step_matches_eager(nconv_amd, gpu):
+    """Config 4's training iteration (SETP2_BP_TRAIN train mode, calculate_loss_multi_resolution,
+    backward, fused capturable AdamW) replayed from a hipGraph (train.GraphedTrainStep, bench.py's
+    default) against the same iterations run eagerly: same kernels in the same order, so the losses
+    and every parameter / BatchNorm buffer after three steps agree to fp32 round-off (1e-5 relative
+    + 1e-7 absolute), and constructing the graphed step leaves the model untouched."""
+    H, W = 64, 96
+    rgb0, d0, rgb1, d1 = [t.to(gpu) for t in f5_inputs(H, W)]
+    g = torch.Generator().manual_seed(31)
+    gt = ((torch.rand(1, 1, 480, 640, generator=g) * 79 + 1) * (torch.rand(1, 1, 480, 640, generator=g) < 0.5)).to(gpu)
+
+    def fn(model, a0, b0, a1, b1, t):
+        est, _ = model(a0, b0, a1, b1)
+        return nconv_amd.train.calculate_loss_multi_resolution(est, t, False)
+
+    def setup():
+        torch.manual_seed(1)
+        net = nconv_amd.SETP2_BP_TRAIN(None, step1_crop="generalized").to(gpu)
+        net.train()
+        return net, nconv_amd.train.get_optimizer(net, "adam", 1e-4, 1e-7, capturable=True, fused=True)
+
+    net_e, opt_e = setup()
+    net_g, opt_g = setup()
+    before = {k: v.clone() for k, v in net_g.state_dict().items()}
+    step = nconv_amd.train.GraphedTrainStep(net_g, opt_g, fn, (rgb0, d0, rgb1, d1, gt))
+    for k, v in net_g.state_dict().items():
+        assert torch.equal(v, before[k]), f"GraphedTrainStep construction changed {k}"
+    le, lg = [], []
+    for _ in range(3):
+        opt_e.zero_grad(set_to_none=True)
+        loss = fn(net_e, rgb0, d0, rgb1, d1, gt)
+        loss.backward()
+        opt_e.step()
+        le.append(loss.item())
+        lg.append(step().item())
+    torch.cuda.synchronize()
+    assert lg == pytest.approx(le, rel=1e-5)
+    sd_e, sd_g = net_e.state_dict(), net_g.state_dict()
+    for k in sd_e:
+        torch.testing.assert_close(sd_g[k], sd_e[k], rtol=1e-5, atol=1e-7, msg=k)
