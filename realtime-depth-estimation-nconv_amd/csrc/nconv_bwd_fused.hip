@@ -50,10 +50,14 @@ constexpr int XSLOT = C * XP, GSLOT = C * GPT;
 constexpr int X_OFF = 0;
 constexpr int G_OFF = X_OFF + NSX * XSLOT;
 constexpr int R_OFF = G_OFF + NSG * GSLOT;   // the input gradient's per-wave partials [4][8][64] f2
-constexpr int H_OFF = R_OFF + 4 * C * 2 * TW;  // nconv1's {gN1, gD1} of the row, [8][64] f2
+constexpr int H_OFF = R_OFF + 4 * C * 2 * TW;  // nconv1's {gN1, gD1} of a row, [2 (row parity)][8][64] f2
 constexpr int SL = 2 + 2 * GW;               // per S row: count (+ pad), then (column, S) of the samples
-constexpr int S_OFF = H_OFF + 2 * C * TW;
-constexpr int LDS_MAIN = S_OFF + NSS * SL;
+constexpr int S_OFF = H_OFF + 2 * 2 * C * TW;
+#ifndef NCONV_FB_LDSW
+#define NCONV_FB_LDSW 0  // 1: the input gradient's weights from LDS ([o][kh][kw][i], broadcast reads)
+#endif
+constexpr int W_OFF = S_OFF + NSS * SL;
+constexpr int LDS_MAIN = W_OFF + (NCONV_FB_LDSW ? C * C * 25 : 0);
 constexpr int FIN = 4 * 50 * 64;             // the waves' weight-gradient accumulators, summed at the end
 constexpr int LDS = LDS_MAIN > FIN ? LDS_MAIN : FIN;
 constexpr int NW = C * C * 25;               // 1600 weights
@@ -81,6 +85,12 @@ __global__ __launch_bounds__(fb::kT) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     const int r0 = tc.ty * seg_rows, r1 = min(H, r0 + seg_rows);
     const int plane = H * W;
 
+#if NCONV_FB_LDSW
+    for (int e = tid; e < C * C * 25; e += kT) {  // [o][kh][kw][i] <- weight[o][i][kh][kw]
+        const int o = e / 200, r = e - o * 200, kh = r / 40, kw = (r >> 3) % 5, i = r & 7;
+        lds[W_OFF + e] = wgt[((o * C + i) * 5 + kh) * 5 + kw];
+    }
+#endif
     // ---- per-image resources (one per saved tensor: the channel plane rides soffset) ----
     const size_t img = (size_t)b * C * plane;
     const int ibytes = C * plane * 4;
@@ -241,37 +251,65 @@ __global__ __launch_bounds__(fb::kT) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     float hn_acc = 0.f, hd_acc = 0.f;          // fused head: thread (o1, tap) < 200
     float sgy[2] = {0.f, 0.f}, sgc[2] = {0.f, 0.f};  // fused head: sum gy1, sum gcout1*c1 of channels 2w, 2w+1
 
+    // Step s computes from the rings and stages the NEXT step's rows at its end: the loads are
+    // issued at the top of step s (in flight under its FMAs) and stored to LDS after its epilogue,
+    // inside the same iteration -- no loaded register lives across the loop back-edge (the
+    // compiler would copy it there and wait for the load at the copy). The epilogue's (x, c) loads
+    // go first: loads return in order, so waiting for them does not wait for the row loads.
     if (r0 < r1) {
-        for (int r = r0 - 2; r < r0 + 2; ++r) {  // prologue: input rows r0-2 .. r0+1, g rows r0-2, r0-1
+        for (int r = r0 - 2; r <= r0 + 2; ++r) {  // prologue: input rows r0-2 .. r0+2, g rows r0-2 .. r0
             load_x(r);
             store_x(r);
         }
-        for (int r = r0 - 2; r < r0; ++r) {
+        for (int r = r0 - 2; r <= r0; ++r) {
             load_g(r);
-            store_g(r, false);
+            store_g(r, r >= r0);
             load_s(r);
             store_s(r);
         }
-        load_x(r0 + 2);
-        load_g(r0);
-        load_s(r0);
-        load_e(r0 - 2);
+        __syncthreads();
     }
     const int last = r1 + 1;  // the last staged row (g rows up to r1 + 1 feed input-gradient rows r1-2, r1-1)
+    float hbk[2], hsk[2];      // fused head: nconv1's bias / normaliser of channels 2w, 2w + 1
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        hbk[k] = HW ? a.hb[2 * w + k] : 0.f;
+        hsk[k] = HW ? a.hs[2 * w + k] : 1.f;
+    }
+    // fused head: nconv1's weight-gradient sums of input row ih (its {gN1, gD1} row in the parity
+    // buffer the epilogue wrote), thread (o1, tap) over the samples of S row ih + kh - 2; run at the
+    // top of the NEXT step (beside the other waves' FMAs, no barrier of its own)
+    auto head_list = [&](int ih) {
+        if constexpr (HW) {
+            if (tid < 200) {
+                const int o1 = tid / 25, tap = tid - o1 * 25, kh = tap / 5, kw = tap - kh * 5;
+                const float* lst = lds + S_OFF + ring(ih + kh - 2, NSS) * SL;
+                const int n = __builtin_bit_cast(int, lst[0]);
+                const f2* ent = reinterpret_cast<const f2*>(lst + 2);
+                const f2* hn = reinterpret_cast<const f2*>(lds + H_OFF + ((ih & 1) * C + o1) * 2 * TW);
+                for (int e = 0; e < n; ++e) {
+                    const f2 q = ent[e];
+                    const int jj = __builtin_bit_cast(int, q.x) - kw;  // strip column of the output pixel
+                    if ((unsigned)jj < (unsigned)TW) {
+                        const f2 h = hn[jj];
+                        hn_acc = fmaf(h.x, q.y, hn_acc);
+                        hd_acc += h.y;
+                    }
+                }
+            }
+        }
+    };
 #pragma unroll 1
     for (int s = r0; s < r1 + 2; ++s) {
         const bool wg = s < r1, dg = s >= r0 + 2;
-        store_x(s + 2);
-        store_g(s, wg);
-        store_s(s);
-        const float exc[2] = {ex[0], ex[1]}, ecc[2] = {ec[0], ec[1]};
-        __syncthreads();
-        {   // the next step's loads, in flight under this step's FMAs (rows past the segment clamped)
-            load_x(min(s + 3, last));
-            load_g(min(s + 1, last));
-            load_s(min(s + 1, last));
-            load_e(s - 1);
-        }
+        const int nx = min(s + 1, last);  // the next step's g / S row (clamped: the last step re-loads)
+        load_e(s - 2);
+        load_x(min(s + 3, last));
+        load_g(nx);
+        load_s(nx);
+        const float* exc = ex;
+        const float* ecc = ec;
+        if (s >= r0 + 3) head_list(s - 3);  // the previous step's input-gradient row
         if (wg) {  // ---- weight gradient of output row s: columns 16w .. 16w+15 of the strip ----
             const float* gr = lds + G_OFF + ring(s, NSG) * GSLOT + wo * GPT;
             const float* xr[5];
@@ -309,6 +347,17 @@ __global__ __launch_bounds__(fb::kT) __attribute__((amdgpu_waves_per_eu(2, 2))) 
                     f2 v[5];
 #pragma unroll
                     for (int k = 0; k < 5; ++k) v[k] = *reinterpret_cast<const f2*>(gr + 2 * k);
+#if NCONV_FB_LDSW
+                    const float* wl = lds + W_OFF + (o * 5 + kh) * 40;
+#pragma unroll
+                    for (int kw = 0; kw < 5; ++kw) {
+                        const f4 wa = *reinterpret_cast<const f4*>(wl + kw * 8), wb = *reinterpret_cast<const f4*>(wl + kw * 8 + 4);
+                        const float wv8[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
+#pragma unroll
+                        for (int i = 0; i < C; ++i)
+                            acc[i] = __builtin_elementwise_fma((f2){wv8[i], wv8[i]}, v[4 - kw], acc[i]);
+                    }
+#else
                     const cfloat* wr = wgt + (o * C) * 25 + kh * 5;
 #pragma unroll
                     for (int kw = 0; kw < 5; ++kw)
@@ -317,6 +366,7 @@ __global__ __launch_bounds__(fb::kT) __attribute__((amdgpu_waves_per_eu(2, 2))) 
                             const float wv = wr[i * 25 + kw];
                             acc[i] = __builtin_elementwise_fma((f2){wv, wv}, v[4 - kw], acc[i]);
                         }
+#endif
                 }
             }
             float* rp = lds + R_OFF + w * (C * 2 * TW) + 2 * lane;
@@ -346,11 +396,11 @@ __global__ __launch_bounds__(fb::kT) __attribute__((amdgpu_waves_per_eu(2, 2))) 
                     if (a.gca) st_f32(plane_rsrc(a.gca + img, ibytes), eoff + so, gco);
                     float gN1 = 0.f, gD1 = 0.f;
                     if (ok) {
-                        nconv_grad_nd(gy, gco, exc[k], ecc[k], a.heps, a.hb[i], a.hs[i], gN1, gD1);
+                        nconv_grad_nd(gy, gco, exc[k], ecc[k], a.heps, hbk[k], hsk[k], gN1, gD1);
                         sgy[k] += gy;
                         sgc[k] = fmaf(gco, ecc[k], sgc[k]);
                     }
-                    *reinterpret_cast<f2*>(lds + H_OFF + i * 2 * TW + 2 * lane) = (f2){gN1, gD1};
+                    *reinterpret_cast<f2*>(lds + H_OFF + ((ih & 1) * C + i) * 2 * TW + 2 * lane) = (f2){gN1, gD1};
                 } else {
                     // gcout of a thresholded source has no gradient path; PLAIN here (host checks)
                     if (a.gxa) {
@@ -365,27 +415,15 @@ __global__ __launch_bounds__(fb::kT) __attribute__((amdgpu_waves_per_eu(2, 2))) 
                     }
                 }
             }
-            if constexpr (HW) {
-                __syncthreads();
-                if (tid < 200) {  // thread (o1, tap): sum over the samples of S row ih + kh - 2
-                    const int o1 = tid / 25, tap = tid - o1 * 25, kh = tap / 5, kw = tap - kh * 5;
-                    const float* lst = lds + S_OFF + ring(ih + kh - 2, NSS) * SL;
-                    const int n = __builtin_bit_cast(int, lst[0]);
-                    const f2* ent = reinterpret_cast<const f2*>(lst + 2);
-                    const f2* hn = reinterpret_cast<const f2*>(lds + H_OFF + o1 * 2 * TW);
-                    for (int e = 0; e < n; ++e) {
-                        const f2 q = ent[e];
-                        const int jj = __builtin_bit_cast(int, q.x) - kw;  // strip column of the output pixel
-                        if ((unsigned)jj < (unsigned)TW) {
-                            const f2 h = hn[jj];
-                            hn_acc = fmaf(h.x, q.y, hn_acc);
-                            hd_acc += h.y;
-                        }
-                    }
-                }
-            }
         }
+        if (s + 1 < r1 + 2) {  // stage the next step's rows (their slots' previous rows are done)
+            store_x(s + 3);
+            store_g(s + 1, s + 1 < r1);
+            store_s(s + 1);
+        }
+        __syncthreads();
     }
+    if (r0 < r1) head_list(r1 - 1);  // the last input-gradient row
 
     // ---- partial rows: the four waves' weight-gradient accumulators summed in a fixed order ----
     __syncthreads();
@@ -681,36 +719,30 @@ __global__ __launch_bounds__(ft::kT) __attribute__((amdgpu_waves_per_eu(2, 2))) 
         for (int kw = 0; kw < 3; ++kw) wu[kh][kw] = wsk[kh][kw] = (f2){0.f, 0.f};
     const int wo = lane >> 3, wi = lane & 7;
 
+    // as bwd_fused: the next step's rows are loaded at the top of step s and staged at its end (no
+    // loaded register across the back-edge); the epilogues' loads are issued first
     if (r0 < r1) {
-        for (int r = r0; r < r0 + 2; ++r) {  // prologue: input rows r0, r0+1; g rows r0-2, r0-1
+        for (int r = r0; r <= r0 + 2; ++r) {  // prologue: input rows r0 .. r0+2; g rows r0-2 .. r0
             load_x(r);
             store_x(r);
         }
-        for (int r = r0 - 2; r < r0; ++r) {
+        for (int r = r0 - 2; r <= r0; ++r) {
             load_g(r);
-            store_g(r, false);
+            store_g(r, r >= r0);
         }
-        load_x(r0 + 2);
-        load_g(r0);
-        load_e(r0);
-        load_u(r0 >> 1);
+        __syncthreads();
     }
     const bool accm = a.accumulate != 0;
 #pragma unroll 1
     for (int s = r0; s < r1; ++s) {
         const bool up = (s & 1) != 0;  // low row (s - 1) / 2 complete after this row
-        store_x(s + 2);
-        store_g(s, true);
-        const float exc[2] = {ex[0], ex[1]}, ecc[2] = {ec[0], ec[1]};
+        load_e(s);
+        load_u(s >> 1);
+        load_x(min(s + 3, r1 + 1));  // (rows past the segment clamped: staged, unused)
+        load_g(min(s + 1, r1));
+        const float* exc = ex;
+        const float* ecc = ec;
         const float uxc = ux, ucc = uc;
-        __syncthreads();
-        {
-            const int nx = min(s + 3, r1 + 1);  // (rows past the segment clamped: staged, unused)
-            load_x(nx);
-            load_g(min(s + 1, r1));
-            load_e(min(s + 1, r1 - 1));
-            if (up) load_u(min((s + 1) >> 1, (r1 >> 1) - 1) + 0);  // next odd row's low row
-        }
         if (s < Ho) {  // ---- weight gradient of output row s: columns 16w .. 16w+15 ----
             const float* gr = lds + G_OFF + ring(s, NSG) * GSLOT + wo * GPT;
             const float* xu[3];
@@ -752,7 +784,7 @@ __global__ __launch_bounds__(ft::kT) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 #pragma unroll 1
             for (int oo = 0; oo < 2; ++oo) {
                 const int o = 2 * w + oo;
-#pragma unroll
+#pragma unroll 1
                 for (int kh = 0; kh < 3; ++kh) {  // g row s - kh, columns iw - kw -> local j + 2 - kw
                     const float* gr = lds + G_OFF + ring(s - kh, NSG) * GSLOT + o * GPT + 2 * lane;
                     f2 v[3];
@@ -843,6 +875,11 @@ __global__ __launch_bounds__(ft::kT) __attribute__((amdgpu_waves_per_eu(2, 2))) 
                 if (ok) st_f32(r, o, accm ? prev + gc : gc);
             }
         }
+        if (s + 1 < r1) {  // stage the next step's rows (their slots' previous rows are done)
+            store_x(s + 3);
+            store_g(s + 1, true);
+        }
+        __syncthreads();
     }
 
     // ---- partial rows ----

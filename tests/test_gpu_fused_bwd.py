@@ -172,7 +172,9 @@ def test_fused_tail_bwd_matches_separate(nconv_amd, gpu, B, H, W):
     print(B, H, W, {k: f"{v:.2e}" for k, v in rels.items()})
     for k in a:
         assert torch.isfinite(b[k]).all(), k
-        assert rels[k] <= 1e-5, (k, rels[k])
+        # nconv7's 8 weights are each one sum over every nconv6 pixel of the batch (3.4 M terms at
+        # B=8 352x1216): the two forms' summation orders differ by ~1e-5 of its largest entry there
+        assert rels[k] <= (3e-5 if k == "gw7" else 1e-5), (k, rels[k])
 
 
 def test_fused_tail_bwd_deterministic(nconv_amd, gpu):

@@ -46,6 +46,21 @@ def main():
             res["separate" if sep else "fused"] = e0.elapsed_time(e1) / reps * 1e3
         print(f"B={B} {H}x{W} head={head}: two kernels {res['separate']:.1f} us, one kernel {res['fused']:.1f} us",
               flush=True)
+    # nconv6 + nconv7 (the training tail)
+    from test_gpu_fused_bwd import _tail_run, _tail_setup
+    t = _tail_setup(m, dev, 8, 352, 1216, seed=1)
+    res = {}
+    for sep in (True, False):
+        for _ in range(3):
+            _tail_run(m, t, sep)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            _tail_run(m, t, sep)
+        e1.record()
+        e1.synchronize()
+        res["separate" if sep else "fused"] = e0.elapsed_time(e1) / reps * 1e3
+    print(f"tail B=8 352x1216: two kernels {res['separate']:.1f} us, one kernel {res['fused']:.1f} us", flush=True)
 
 
 if __name__ == "__main__":

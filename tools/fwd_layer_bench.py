@@ -35,8 +35,8 @@ def main():
         s1 = w1.sum((1, 2, 3)).contiguous()
         spec = m.LayerSpec(1, 8, (5, 5), (1, 1), (2, 2), mode=m._lib.THRESH)
         fn = lambda: N.layer_forward_raw(spec, S, None, None, None, w1, b, s1)
-    elif which == "head":  # nconv1 inside nconv2 (nconv_fwd_head)
-        S = (r(B, 1, H, W) * 79 + 1) * (r(B, 1, H, W) < 0.05)
+    elif which == "head":  # nconv1 inside nconv2 (nconv_fwd_head); NCONV_DENSITY: depth density (0.05)
+        S = (r(B, 1, H, W) * 79 + 1) * (r(B, 1, H, W) < float(os.environ.get("NCONV_DENSITY", "0.05")))
         w1 = r(8, 1, 5, 5) + 0.05
         s1 = w1.sum((1, 2, 3)).contiguous()
         sp1 = m.LayerSpec(1, 8, (5, 5), (1, 1), (2, 2), mode=m._lib.THRESH)

@@ -12,6 +12,18 @@ case $rc in 0|1) ;; *) exit $rc;; esac
 timeout -k 10 120 python3 -u tools/fused_bwd_bench.py 20 > gpurun_out/fbench_$tag.log 2>&1
 brc=$?; echo "fbench rc=$brc"; tail -6 gpurun_out/fbench_$tag.log
 case $brc in 0) ;; *) exit $brc;; esac
+timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/fprof_$tag -o run -- \
+    python3 tools/fused_bwd_bench.py 5 > gpurun_out/fprof_$tag.log 2>&1
+prc=$?; echo "fprof rc=$prc"
+case $prc in 0) ;; *) exit $prc;; esac
+f=$(ls gpurun_out/fprof_$tag/*/run_kernel_stats.csv gpurun_out/fprof_$tag/run_kernel_stats.csv 2>/dev/null | head -1)
+[ -n "$f" ] && python3 -c "
+import csv,sys
+for r in csv.DictReader(open(sys.argv[1])):
+    n=r['Name']
+    if any(k in n for k in ('bwd_fused','dgrad','wgrad_mfma','wgrad_reduce','box_weights')):
+        print(f\"{float(r['AverageNs'])/1e3:9.1f} us x{r['Calls']:>4}  {n[:90]}\")
+" "$f"
 for F in "" nconv2 nconv6 "nconv2,nconv6" "nconv2,nconv_down1,nconv_down2,nconv6"; do
   NCONV_FUSED_BWD="$F" timeout -k 10 200 python3 -u bench.py --no-config5 --no-guided --no-guided-train \
       --no-cpu-baseline --alt-math "" --head-density 0 > gpurun_out/btrain_${tag}_${F//,/_}.json 2> gpurun_out/btrain_${tag}_${F//,/_}.err
