@@ -73,12 +73,6 @@ struct DcCfg {
 
 typedef float f16v __attribute__((ext_vector_type(16)));
 
-// Tap-level operand prefetch (every LDS read of a tap issued before its MFMAs): measured neutral to
-// +9 % slower per instantiation (strided, 32-channel and transposed tiles slower; 64-channel
-// stride-1 within noise: profiles/r4_ab_dense_prefetch.log, r4_ab_phase_lowplanes_prefetch.log).
-#ifndef NCONV_DC_PREFETCH
-#define NCONV_DC_PREFETCH 0
-#endif
 template <int COUT, int KIND, int S, bool SC, bool STR = false>
 __global__ __launch_bounds__(kDT) void dense_conv_mfma(nconv_dense_conv p, int ntx, int nty, int ncot) {
     using C = DcCfg<COUT, KIND, S>;
@@ -218,52 +212,6 @@ __global__ __launch_bounds__(kDT) void dense_conv_mfma(nconv_dense_conv p, int n
         store_chunk();
         __syncthreads();
         load_chunk(ch + 1 < nchunk ? ch + 1 : ch);  // next chunk in flight during the MFMAs
-#if NCONV_DC_PREFETCH
-        // taps one per iteration, all of a tap's operand reads issued before its MFMAs (the default
-        // schedule read, waited and issued two MFMAs at a time: an LDS latency per MFMA pair)
-        float av[1][kCK / 2][C::MT], bv[1][kCK / 2][C::RW];
-        auto read_tap = [&](int t, int sl) __attribute__((always_inline)) {
-            const int dr = C::TR ? 1 - t / 2 : t / C::KS;
-            const int dc = C::TR ? 1 - t % 2 : t % C::KS;
-            const float* ap = lds + abase + t * kCK * C::COP;
-            const float* bp = lds + bbase + dr * C::ROW + dc;
-#pragma unroll
-            for (int pp = 0; pp < kCK / 2; ++pp) {
-#pragma unroll
-                for (int m = 0; m < C::MT; ++m) av[sl][pp][m] = ap[2 * pp * C::COP + 32 * m];
-#pragma unroll
-                for (int r = 0; r < C::RW; ++r) bv[sl][pp][r] = bp[2 * pp * C::PLANE + r * C::SP * C::ROW];
-            }
-        };
-        auto mfma_tap = [&](int t, int sl) __attribute__((always_inline)) {
-#pragma unroll
-            for (int pp = 0; pp < kCK / 2; ++pp) {
-#pragma unroll
-                for (int m = 0; m < C::MT; ++m)
-#pragma unroll
-                    for (int r = 0; r < C::RW; ++r)
-                        acc[m][r] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[sl][pp][m], bv[sl][pp][r], acc[m][r], 0, 0, 0);
-                if constexpr (SC) {
-                    if (t == C::CENTER) {
-#pragma unroll
-                        for (int m = 0; m < C::MT; ++m) {
-                            const float sa = lds[sbase + 2 * pp * C::COP + 32 * m];
-#pragma unroll
-                            for (int r = 0; r < C::RW; ++r)
-                                acs[m][r] = __builtin_amdgcn_mfma_f32_32x32x2f32(sa, bv[sl][pp][r], acs[m][r], 0, 0, 0);
-                        }
-                    }
-                }
-            }
-        };
-#pragma unroll 1
-        for (int t = 0; t < C::TAPS; ++t) {
-            read_tap(t, 0);
-            __builtin_amdgcn_sched_barrier(0);  // every operand read of the tap issued before its MFMAs
-            mfma_tap(t, 0);
-        }
-    }
-#else
         // taps one per iteration (not unrolled: unrolling all 9 x 4 k-steps lets the scheduler
         // hoist every operand read of the chunk into registers); the 4 channel pairs unrolled
 #pragma unroll 1
@@ -300,8 +248,6 @@ __global__ __launch_bounds__(kDT) void dense_conv_mfma(nconv_dense_conv p, int n
             }
         }
     }
-
-#endif
     // ---- epilogue: bias, ReLU, shortcut; C[row = co][col = pixel]: col = lane & 31,
     //      row = (q & 3) + 8 (q >> 2) + 4 (lane >> 5) for register q. Stores through one
     //      resource over the image's output channel range: the lane's byte offset (its pixel and

@@ -1550,306 +1550,6 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(GP ? NCONV_W
     }
 }
 
-// Measured (graphed training step, same box, two repetitions each): wgrad_mfma2 on every 5x5
-// layer 2.334 / 2.324 ms, on nconv2 only 2.363 / 2.369, off 2.318 / 2.338 -- nconv2's weight
-// gradient alone drops 509 -> 347 us, but the backward stage is bound by the sum of the concurrent
-// input- and weight-gradient work (fp32 MFMA and VALU do not overlap) and the two-row kernel runs
-// at two waves per SIMD. Off by default; -DNCONV_WM2=1 builds it in.
-#ifndef NCONV_WM2
-#define NCONV_WM2 0  // the 8 -> 8 5x5 weight gradients two output rows per step (wgrad_mfma2)
-#endif
-#ifndef NCONV_WM2_MIN_ROWS
-#define NCONV_WM2_MIN_ROWS 256
-#endif
-#ifndef NCONV_WM2_WAVES
-#define NCONV_WM2_WAVES 2  // 3 spills the two rows' staging registers to scratch (V170 cap)
-#endif
-// ---- wgrad of the 8 -> 8, 5x5 layers (nconv2, down1-3), two output rows per step ---------------
-// wgrad_mfma's GEMM per output row is M = (kh, i) = 40 by N = (kw, o) = 40, padded to 48 x 48 (69 %
-// of its MFMA work useful). Two output rows oh, oh + 1 at a time read input rows oh - PH .. oh - PH
-// + 5, so with M = (input row ir 0..5, i) = 48 and N = (kw, row r 0..1, o) = 80 both tile exactly
-// (3 x 5 tiles of 16): C[(ir, i)][(kw, r, o)] adds to gW[o][i][ir - r][kw] where 0 <= ir - r <= 4,
-// and only the pairs (ir, r) = (5, 0), (0, 1) are wasted -- 83 % useful, 15 MFMAs per operand pair
-// and k-step for two rows instead of 2 x 9. Operands as wgrad_mfma's: A = the staged input row of
-// ir (x*c, then c), B = the {gN, gD} row of r shifted by kw (its K-1 column halo); ring of six input
-// rows, two new ones per step, two barriers per step (one per row, as wgrad_mfma). The last step
-// of an odd segment stages its second g row as zero (no contribution).
-template <int MODE, bool GP>
-struct Wm2Cfg {
-    static constexpr int CIN = 8, COUT = 8, K = 5, TW = 64;
-    static constexpr int XP = TW + 4;
-    static constexpr int SLOTS = 6;
-    static constexpr int SLOT = CIN * XP;              // == 32 (mod 64): neighbouring ir rows 32 banks apart
-    static constexpr int C_OFF = SLOTS * SLOT;         // c ring after the x*c ring
-    static constexpr int GP_ = 72;                     // g row pitch (64 + K-1 halo), == 8 (mod 64)
-    static constexpr int GPART = COUT * GP_;           // one part (gN or gD) of one g row
-    static constexpr int GROW = 2 * GPART;             // both parts of one g row
-    static constexpr int G_OFF = 2 * C_OFF;
-    static constexpr int STAGE = G_OFF + 2 * GROW;
-    static constexpr int MT = 3, NT = 5;               // 48 x 80
-    static constexpr int RED = 4 * NT * 256;           // one A-tile row of the four waves' tiles
-    static constexpr int OUT_OFF = RED;                // the layer's 1600 weights, accumulated
-    static constexpr int LDS = STAGE > OUT_OFF + CIN * COUT * K * K ? STAGE : OUT_OFF + CIN * COUT * K * K;
-    static constexpr int CPW = CIN / 4, OPW = COUT / 4;
-};
-
-template <int MODE, bool GP>
-__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(NCONV_WM2_WAVES, 8))) void wgrad_mfma2(
-    LayerDev d, BwdArgs a, float* part, int nstrip, int nseg, int seg_rows) {
-    using C = Wm2Cfg<MODE, GP>;
-    constexpr int CIN = C::CIN, COUT = C::COUT, K = C::K;
-    __shared__ __attribute__((aligned(16))) float lds[C::LDS];
-    const nconv_layer& L = d.L;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    int blk = blockIdx.x;
-    const int strip = blk % nstrip;
-    blk /= nstrip;
-    const int seg = blk % nseg, b = blk / nseg;
-    const int ow0 = strip * C::TW;
-    const int r0 = seg * seg_rows, r1 = min(L.Ho, r0 + seg_rows);
-    constexpr unsigned OOB = 0x80000000u;
-
-    // per-lane operand offsets: A[m = lane&15][k = lane>>4], B[k][n = lane&15]
-    const int kq = lane >> 4, ml = lane & 15;
-    int a_ir[C::MT], a_i[C::MT], b_off[C::NT];
-#pragma unroll
-    for (int t = 0; t < C::MT; ++t) {
-        const int m = 16 * t + ml;
-        a_ir[t] = m / CIN;
-        a_i[t] = (m % CIN) * C::XP + kq;
-    }
-#pragma unroll
-    for (int u = 0; u < C::NT; ++u) {  // n = 16 kw + 8 r + o: tile u is kw = u
-        const int r = ml >> 3, o = ml & 7;
-        b_off[u] = C::G_OFF + r * C::GROW + o * C::GP_ + (K - 1) - u + kq;
-    }
-
-    // ---- staging (as wgrad_mfma): input row = CIN x 64 columns, g row = COUT x (64 + K-1) ----
-    constexpr int NG = GP ? 7 : 4;
-    constexpr int NH = C::OPW * (K - 1);
-    const bool hl = lane < NH;
-    const int hkk = hl ? lane / (K - 1) : 0, hcol = 64 + lane % (K - 1), ho = w + 4 * hkk;
-    const int iw_in = ow0 - L.PW + lane;
-    float px[2][C::CPW], pc[2][C::CPW];
-    float gq[2][C::OPW][NG], gh[2][NG];
-    float gb_acc[C::OPW], gs_acc[C::OPW], gb_h = 0.f, gs_h = 0.f;
-#pragma unroll
-    for (int kk = 0; kk < C::OPW; ++kk) gb_acc[kk] = gs_acc[kk] = 0.f;
-    float bias_o[C::OPW], wsum_o[C::OPW];
-#pragma unroll
-    for (int kk = 0; kk < C::OPW; ++kk) {
-        bias_o[kk] = L.bias[w + 4 * kk];
-        wsum_o[kk] = L.wsum[w + 4 * kk];
-    }
-    auto load_in = [&](int j, int ih) __attribute__((always_inline)) {
-#pragma unroll
-        for (int kk = 0; kk < C::CPW; ++kk) {
-            px[j][kk] = pc[j][kk] = 0.f;
-            load_px<MODE>(d, chan_src<MODE>(d, b, w + 4 * kk), ih, iw_in, px[j][kk], pc[j][kk]);
-        }
-    };
-    auto store_in = [&](int j, int ih) __attribute__((always_inline)) {
-        const int slot = ((ih % C::SLOTS) + C::SLOTS) % C::SLOTS;
-#pragma unroll
-        for (int kk = 0; kk < C::CPW; ++kk) {
-            const int i = w + 4 * kk;
-            lds[slot * C::SLOT + i * C::XP + lane] = px[j][kk] * pc[j][kk];
-            lds[C::C_OFF + slot * C::SLOT + i * C::XP + lane] = pc[j][kk];
-        }
-    };
-    const int plane = L.Ho * L.Wo;
-    const int Hp = L.Ho >> 1, Wp = L.Wo >> 1, pplane = Hp * Wp;
-    // row oh of the segment (oh >= r1: a zero row)
-    auto load_g = [&](int j, int oh) __attribute__((always_inline)) {
-        const int ow = ow0 - (K - 1) + lane, owh = ow0 - (K - 1) + hcol;
-        const bool row_in = oh < r1;
-        const bool in = row_in && (unsigned)ow < (unsigned)L.Wo;
-        const bool inh = hl && row_in && (unsigned)owh < (unsigned)L.Wo;
-        const size_t base = (size_t)b * COUT * plane;
-        const int bytes = COUT * plane * 4;
-        const __amdgpu_buffer_rsrc_t rgy = plane_rsrc(a.gy + base, bytes);
-        const __amdgpu_buffer_rsrc_t rco = plane_rsrc(a.co + base, bytes);
-        const __amdgpu_buffer_rsrc_t ry = plane_rsrc(a.y + base, bytes);
-        const __amdgpu_buffer_rsrc_t rgc = plane_rsrc(a.gco ? a.gco + base : a.y, a.gco ? bytes : 0);
-        const unsigned off = in ? (unsigned)(oh * L.Wo + ow) * 4u : OOB;
-        const unsigned offh = inh ? (unsigned)((ho * L.Ho + oh) * L.Wo + owh) * 4u : OOB;
-#pragma unroll
-        for (int kk = 0; kk < C::OPW; ++kk) {
-            const int so = (w + 4 * kk) * plane * 4;
-            gq[j][kk][0] = ld_f32s(rgy, off, so);
-            gq[j][kk][1] = ld_f32s(rco, off, so);
-            gq[j][kk][2] = ld_f32s(ry, off, so);
-            gq[j][kk][3] = ld_f32s(rgc, off, so);
-        }
-        gh[j][0] = ld_f32(rgy, offh);
-        gh[j][1] = ld_f32(rco, offh);
-        gh[j][2] = ld_f32(ry, offh);
-        gh[j][3] = ld_f32(rgc, offh);
-        if constexpr (GP) {
-            const size_t pbase = (size_t)b * COUT * pplane;
-            const int pbytes = COUT * pplane * 4;
-            const __amdgpu_buffer_rsrc_t rpy = plane_rsrc(a.gpy + pbase, pbytes);
-            const __amdgpu_buffer_rsrc_t rpc = plane_rsrc(a.gpc + pbase, pbytes);
-            const __amdgpu_buffer_rsrc_t rpa = plane_rsrc((const float*)(a.parg + pbase), pbytes);
-            const unsigned po = in ? pool_elem_off(oh, ow, Hp, Wp, OOB) : OOB;
-            const unsigned pe = inh ? pool_elem_off(oh, owh, Hp, Wp, OOB) : OOB;
-            const unsigned poh = pe != OOB ? pe + (unsigned)(ho * pplane) * 4u : OOB;
-#pragma unroll
-            for (int kk = 0; kk < C::OPW; ++kk) {
-                const int so = (w + 4 * kk) * pplane * 4;
-                gq[j][kk][4] = ld_f32s(rpy, po, so);
-                gq[j][kk][5] = ld_f32s(rpc, po, so);
-                gq[j][kk][6] = ld_f32s(rpa, po, so);
-            }
-            gh[j][4] = ld_f32(rpy, poh);
-            gh[j][5] = ld_f32(rpc, poh);
-            gh[j][6] = ld_f32(rpa, poh);
-        }
-    };
-    auto store_g = [&](int j, int oh_cur) __attribute__((always_inline)) {
-        const unsigned sub = (unsigned)((oh_cur & 1) << 1), ow_m = (unsigned)(ow0 - (K - 1) + lane);
-        const unsigned ow_h = (unsigned)(ow0 - (K - 1) + hcol);
-        float* const grow = lds + C::G_OFF + j * C::GROW;
-#pragma unroll
-        for (int kk = 0; kk < C::OPW; ++kk) {
-            const int o = w + 4 * kk;
-            float gy = gq[j][kk][0], gco = gq[j][kk][3];
-            if constexpr (GP)
-                pool_route(gy, gco, gq[j][kk][4], gq[j][kk][5], __builtin_bit_cast(unsigned, gq[j][kk][6]),
-                           sub | (ow_m & 1u));
-            float gN, gD;
-            nconv_grad_nd(gy, gco, gq[j][kk][2], gq[j][kk][1], L.eps, bias_o[kk], wsum_o[kk], gN, gD);
-            grow[o * C::GP_ + lane] = gN;
-            grow[C::GPART + o * C::GP_ + lane] = gD;
-            if (lane >= K - 1) {  // this strip's own columns: the bias / wsum gradient sums
-                gb_acc[kk] += gy;
-                gs_acc[kk] = fmaf(gco, gq[j][kk][1], gs_acc[kk]);
-            }
-        }
-        {   // halo pass (columns 64 .. 64+K-2, all the strip's own)
-            float bo = bias_o[0], so = wsum_o[0];
-#pragma unroll
-            for (int kk = 1; kk < C::OPW; ++kk) {
-                bo = hkk == kk ? bias_o[kk] : bo;
-                so = hkk == kk ? wsum_o[kk] : so;
-            }
-            float gy = gh[j][0], gco = gh[j][3];
-            if constexpr (GP) pool_route(gy, gco, gh[j][4], gh[j][5], __builtin_bit_cast(unsigned, gh[j][6]), sub | (ow_h & 1u));
-            float gN, gD;
-            nconv_grad_nd(gy, gco, gh[j][2], gh[j][1], L.eps, bo, so, gN, gD);
-            if (hl) {
-                grow[ho * C::GP_ + hcol] = gN;
-                grow[C::GPART + ho * C::GP_ + hcol] = gD;
-            }
-            gb_h += gy;
-            gs_h = fmaf(gco, gh[j][1], gs_h);
-        }
-    };
-
-    f4acc acc[C::MT][C::NT];
-#pragma unroll
-    for (int t = 0; t < C::MT; ++t)
-#pragma unroll
-        for (int u = 0; u < C::NT; ++u) acc[t][u] = (f4acc){0.f, 0.f, 0.f, 0.f};
-
-    if (r0 < r1) {
-        for (int ir = 0; ir < 4; ++ir) {  // prologue: the first step's input rows 0..3
-            load_in(0, r0 - L.PH + ir);
-            store_in(0, r0 - L.PH + ir);
-        }
-        load_in(0, r0 - L.PH + 4);
-        load_in(1, r0 - L.PH + 5);
-        load_g(0, r0);
-        load_g(1, r0 + 1);
-    }
-#pragma unroll 1
-    for (int oh = r0; oh < r1; oh += 2) {
-        if (oh > r0) __syncthreads();  // every wave is done with the previous step's rows
-        store_in(0, oh - L.PH + 4);
-        store_in(1, oh - L.PH + 5);
-        store_g(0, oh);
-        store_g(1, oh + 1);
-        __syncthreads();
-        {   // the next step's loads in flight during this step's MFMAs (past the segment: zero g rows,
-            // input rows that are never used)
-            load_in(0, oh + 2 - L.PH + 4);
-            load_in(1, oh + 2 - L.PH + 5);
-            load_g(0, oh + 2);
-            load_g(1, oh + 3);
-        }
-        int ax[C::MT];
-#pragma unroll
-        for (int t = 0; t < C::MT; ++t) {
-            const int ih = oh - L.PH + a_ir[t];
-            const int slot = ((ih % C::SLOTS) + C::SLOTS) % C::SLOTS;
-            ax[t] = slot * C::SLOT + a_i[t];
-        }
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            const int q0 = 16 * w + 4 * s;
-#pragma unroll
-            for (int prt = 0; prt < 2; ++prt) {  // {x*c, gN} then {c, gD}
-                float va[C::MT], vb[C::NT];
-#pragma unroll
-                for (int t = 0; t < C::MT; ++t) va[t] = lds[ax[t] + prt * C::C_OFF + q0];
-#pragma unroll
-                for (int u = 0; u < C::NT; ++u) vb[u] = lds[b_off[u] + prt * C::GPART + q0];
-#pragma unroll
-                for (int t = 0; t < C::MT; ++t)
-#pragma unroll
-                    for (int u = 0; u < C::NT; ++u)
-                        acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(va[t], vb[u], acc[t][u], 0, 0, 0);
-            }
-        }
-    }
-
-    // ---- the four waves' tiles, one A-tile row at a time, summed in a fixed order; each weight gets
-    //      its (ir = kh, r = 0) term, then its (kh + 1, 1) term (rows t = kh / 2 <= (kh + 1) / 2) ----
-    constexpr int NW = COUT * CIN * K * K;
-    float* out = part + (size_t)blockIdx.x * (NW + 2 * COUT);
-    float* const acc_w = lds + C::OUT_OFF;
-    __syncthreads();
-    for (int e = tid; e < NW; e += kT) acc_w[e] = 0.f;
-#pragma unroll
-    for (int t = 0; t < C::MT; ++t) {
-        __syncthreads();
-#pragma unroll
-        for (int u = 0; u < C::NT; ++u)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) lds[w * C::NT * 256 + u * 256 + r * 64 + lane] = acc[t][u][r];
-        __syncthreads();
-#pragma unroll
-        for (int rr = 0; rr < 2; ++rr) {
-            for (int e = tid; e < C::NT * 256; e += kT) {
-                const int l = e & 63, q = (e >> 6) & 3, u = e >> 8;
-                const int r = (l >> 3) & 1;
-                if (r != rr) continue;
-                const float v = ((lds[e] + lds[C::NT * 256 + e]) + lds[2 * C::NT * 256 + e]) + lds[3 * C::NT * 256 + e];
-                const int m = 16 * t + (l >> 4) * 4 + q;
-                const int ir = m / CIN, i = m % CIN, o = l & 7, kw = u, kh = ir - r;
-                if (kh >= 0 && kh < K) acc_w[((o * CIN + i) * K + kh) * K + kw] += v;
-            }
-            __syncthreads();
-        }
-    }
-    for (int e = tid; e < NW; e += kT) out[e] = acc_w[e];
-#pragma unroll
-    for (int kk = 0; kk < C::OPW; ++kk) {
-        const bool mine = hl && hkk == kk;  // the halo lanes' sums of this channel
-        float sb = gb_acc[kk] + (mine ? gb_h : 0.f), ss = gs_acc[kk] + (mine ? gs_h : 0.f);
-#pragma unroll
-        for (int sh = 32; sh > 0; sh >>= 1) {
-            sb += __shfl_xor(sb, sh);
-            ss += __shfl_xor(ss, sh);
-        }
-        if (lane == 0) {
-            out[NW + w + 4 * kk] = sb;
-            out[NW + COUT + w + 4 * kk] = ss;
-        }
-    }
-}
-
 // ------------------------------------------------------------------------------------------------
 // Launchers
 // ------------------------------------------------------------------------------------------------
@@ -2012,21 +1712,6 @@ static int go_bwd_tiled(const LayerDev& d, const BwdArgs& a, float* part, float*
             const int nw = COUT * CIN * K * K;
             return launch_wgrad_reduce(a, part, nblk, nw, COUT, CIN * K * K, L.wsum, st, why);
         } else if (a.gw || a.gb) {
-#if NCONV_WM2
-            // (on the full-resolution layer only: the quarter / eighth-resolution segments are too
-            // short for its two-row prologue and three-round epilogue at two waves per SIMD)
-            if constexpr (CIN == 8 && COUT == 8 && K == 5 && !T7 &&
-                          (MODE == NCONV_LOAD_PLAIN || MODE == NCONV_LOAD_POOL2))
-                if (L.Ho >= NCONV_WM2_MIN_ROWS) {
-                const int per_cu = dev_occupancy((const void*)wgrad_mfma2<MODE, GP>, kT, 0);
-                const int resident = device_cus() * (per_cu < kMfmaMaxPerCu ? per_cu : kMfmaMaxPerCu);
-                const WmGrid g = wm_grid(L, kMfmaRounds * resident);
-                hipLaunchKernelGGL((wgrad_mfma2<MODE, GP>), dim3(g.nblk), dim3(kT), 0, st, d, a, part, g.nstrip,
-                                   g.nseg, g.seg_rows);
-                const int nw = COUT * CIN * K * K;
-                return launch_wgrad_reduce(a, part, (int)g.nblk, nw, COUT, CIN * K * K, L.wsum, st, why);
-                }
-#endif
             const int per_cu = dev_occupancy((const void*)wgrad_mfma<CIN, COUT, K, MODE, GP, T7>, kT, 0);
             const int resident = device_cus() * (per_cu < kMfmaMaxPerCu ? per_cu : kMfmaMaxPerCu);
             const WmGrid g = wm_grid(L, kMfmaRounds * resident);

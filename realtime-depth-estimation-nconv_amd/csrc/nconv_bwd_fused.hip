@@ -53,11 +53,8 @@ constexpr int R_OFF = G_OFF + NSG * GSLOT;   // the input gradient's per-wave pa
 constexpr int H_OFF = R_OFF + 4 * C * 2 * TW;  // nconv1's {gN1, gD1} of a row, [2 (row parity)][8][64] f2
 constexpr int SL = 2 + 2 * GW;               // per S row: count (+ pad), then (column, S) of the samples
 constexpr int S_OFF = H_OFF + 2 * 2 * C * TW;
-#ifndef NCONV_FB_LDSW
-#define NCONV_FB_LDSW 0  // 1: the input gradient's weights from LDS ([o][kh][kw][i], broadcast reads)
-#endif
 constexpr int W_OFF = S_OFF + NSS * SL;
-constexpr int LDS_MAIN = W_OFF + (NCONV_FB_LDSW ? C * C * 25 : 0);
+constexpr int LDS_MAIN = W_OFF;
 constexpr int FIN = 4 * 50 * 64;             // the waves' weight-gradient accumulators, summed at the end
 constexpr int LDS = LDS_MAIN > FIN ? LDS_MAIN : FIN;
 constexpr int NW = C * C * 25;               // 1600 weights
@@ -85,12 +82,6 @@ __global__ __launch_bounds__(fb::kT) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     const int r0 = tc.ty * seg_rows, r1 = min(H, r0 + seg_rows);
     const int plane = H * W;
 
-#if NCONV_FB_LDSW
-    for (int e = tid; e < C * C * 25; e += kT) {  // [o][kh][kw][i] <- weight[o][i][kh][kw]
-        const int o = e / 200, r = e - o * 200, kh = r / 40, kw = (r >> 3) % 5, i = r & 7;
-        lds[W_OFF + e] = wgt[((o * C + i) * 5 + kh) * 5 + kw];
-    }
-#endif
     // ---- per-image resources (one per saved tensor: the channel plane rides soffset) ----
     const size_t img = (size_t)b * C * plane;
     const int ibytes = C * plane * 4;
@@ -347,17 +338,6 @@ __global__ __launch_bounds__(fb::kT) __attribute__((amdgpu_waves_per_eu(2, 2))) 
                     f2 v[5];
 #pragma unroll
                     for (int k = 0; k < 5; ++k) v[k] = *reinterpret_cast<const f2*>(gr + 2 * k);
-#if NCONV_FB_LDSW
-                    const float* wl = lds + W_OFF + (o * 5 + kh) * 40;
-#pragma unroll
-                    for (int kw = 0; kw < 5; ++kw) {
-                        const f4 wa = *reinterpret_cast<const f4*>(wl + kw * 8), wb = *reinterpret_cast<const f4*>(wl + kw * 8 + 4);
-                        const float wv8[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
-#pragma unroll
-                        for (int i = 0; i < C; ++i)
-                            acc[i] = __builtin_elementwise_fma((f2){wv8[i], wv8[i]}, v[4 - kw], acc[i]);
-                    }
-#else
                     const cfloat* wr = wgt + (o * C) * 25 + kh * 5;
 #pragma unroll
                     for (int kw = 0; kw < 5; ++kw)
@@ -366,7 +346,6 @@ __global__ __launch_bounds__(fb::kT) __attribute__((amdgpu_waves_per_eu(2, 2))) 
                             const float wv = wr[i * 25 + kw];
                             acc[i] = __builtin_elementwise_fma((f2){wv, wv}, v[4 - kw], acc[i]);
                         }
-#endif
                 }
             }
             float* rp = lds + R_OFF + w * (C * 2 * TW) + 2 * lane;

@@ -23,10 +23,6 @@
 // ride the scalar cache.
 #include "nconv_prologue.h"
 
-#ifndef NCONV_PHASE_UNROLL
-#define NCONV_PHASE_UNROLL 0  // 1: a channel's kernel rows unrolled (their weight / LDS loads issued together)
-#endif
-
 namespace nconv {
 
 namespace {
@@ -112,11 +108,7 @@ __global__ __launch_bounds__(kPT) void fwd_phase(LayerDev d, float* __restrict__
     auto fma_native = [&](int ca, int bufi) {
         const f2* row = rowbase + bufi * kStride;
         const float* wr = wgt + (size_t)(cbase_a + ca) * kPK * kPK;
-#if NCONV_PHASE_UNROLL
-#pragma unroll
-#else
 #pragma unroll 1
-#endif
         for (int q = 0; q < kPK; ++q, row += kPIWP, wr += kPK) {
             f2 v[4];
             const f4 q0 = reinterpret_cast<const f4*>(row)[0], q1 = reinterpret_cast<const f4*>(row)[1];
@@ -142,11 +134,7 @@ __global__ __launch_bounds__(kPT) void fwd_phase(LayerDev d, float* __restrict__
     auto fma_up = [&](int cb, int bufi) {
         const f2* row = lowbase + bufi * kPLStride;
         const cfloat* wr = wph + ((size_t)cb * 2 + alpha) * 2 * 32;
-#if NCONV_PHASE_UNROLL
-#pragma unroll
-#else
 #pragma unroll 1
-#endif
         for (int dh = 0; dh < 2; ++dh, row += kPLP, wr += 32) {
             f2 v[3];
             v[0] = row[0];

@@ -274,7 +274,7 @@ def test_dnet_train_gradients_config4b_full_size(nconv_amd, gpu):
     assert not any(r.endswith("FAIL") for r in report), "\n".join(report)
 
 
-@pytest.mark.parametrize("H,W", [(64, 96), (45, 67), (264, 100)])  # 264: nconv2 on wgrad_mfma2 (>= 256 rows)
+@pytest.mark.parametrize("H,W", [(64, 96), (45, 67), (264, 100)])  # 264: full-height rows (>= 256)
 def test_dnet_train_gradients(nconv_amd, gpu, H, W, bwd_math):
     """Step-1 training gradients (EnforcePos + calculate_loss on [0] + backward) vs the fp64 oracle.
 
