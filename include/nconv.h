@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define NCONV_ABI_VERSION 19
+#define NCONV_ABI_VERSION 20
 
 /* How a layer's input (data x, confidence c) is produced from its source tensors. These are the
  * DNET glue ops fused into the layer's load stage (models/step1.py:53,61-90). */
@@ -140,6 +140,23 @@ int nconv_weight_prologue(int n, float* const* weights, const int* couts, const 
                           float* const* wsums, const float* head_w1, const float* head_w2, float* w21,
                           int nphase, const float* const* phase_weights, const int* phase_cins,
                           const int* phase_up_first, float* const* wphases, void* stream);
+
+/* The training pass's weight prologue in one launch (replaces models/step1.py:190-207's EnforcePos
+ * pre-hooks of DNET's nine layers, whose forward then needs the normalisers and the auxiliaries
+ * below: five launches -- nconv_weight_prep, nconv_head_weights, nconv_phase_weights and the three
+ * backward box-weight builds -- become one). Layer i (weights[i], couts[i] x fan_ins[i]) gets
+ * EnforcePos's softplus in place when softplus[i] (softplus may be NULL: none) and its normalisers
+ * in wsums[i]. With w21 != NULL, layers head1 / head2 are nconv1 (8 x 1 x 5 x 5) and nconv2 (8 x 8 x
+ * 5 x 5) and w21 receives the exact head's weights (nconv_head_weights, NCONV_HEAD_WEIGHTS_FLOATS).
+ * Phase layer k is layer phase_layers[k] (8 x 16 x 3 x 3, upsampled channels from phase_up_first[k]
+ * = 0 or 8): wphases[k] receives its phase weights (nconv_phase_weights) and, when wboxes and
+ * wboxes[k] are non-NULL, wboxes[k] its 1,024 box weights for the phase-form input gradient
+ * (nconv_bwd_io.box_weights). Each output is bitwise what the separate calls write after
+ * nconv_weight_prep. Each layer is read by one workgroup, which applies the softplus while staging
+ * and writes it back, so the roles need no order between them. Returns 0 or -EINVAL. */
+int nconv_train_prologue(int n, float* const* weights, const int* couts, const int* fan_ins, const int* softplus,
+                         float* const* wsums, int head1, int head2, float* w21, int nphase, const int* phase_layers,
+                         const int* phase_up_first, float* const* wphases, float* const* wboxes, void* stream);
 
 /* Forward of one NConv2d with fused input glue.
  * Replaces models/step1.py:119-147 (2x F.conv2d, mul, div, bias add, confidence normalisation)
@@ -300,6 +317,16 @@ typedef struct nconv_bwd_io {
     size_t tail_workspace_bytes;
     float* tail_gw;
     int tail_nparts;                /* out */
+    /* ABI 20. optional: the box weights of an exactly-2x UPCAT layer's phase-form input gradient
+     * (nconv_train_prologue wboxes), else built by a launch of this call. */
+    const float* box_weights;
+    /* ABI 20. The tail planes' extent: all zero = nconv7's whole (Ho + 4) x (Wo + 4) grid;
+     * otherwise (B, 1, tail_h, tail_w) holding the grid from row / column tail_crop0 (DNET's crop,
+     * step1.py:94: the training output written cropped by nconv_fwd_tail); gradient outside the
+     * window is 0. */
+    int tail_crop0;
+    int tail_h;
+    int tail_w;
 } nconv_bwd_io;
 
 int nconv_bwd_ex(const nconv_layer* L, nconv_bwd_io* io, void* workspace, size_t workspace_bytes,
@@ -313,6 +340,16 @@ size_t nconv_bwd_tail_workspace_bytes(const nconv_layer* L);
  * layers with nparts[k] == 0 are skipped). Two launches on `stream`. Returns 0 or -EINVAL. */
 int nconv_wgrad_reduce(int n, const nconv_layer* layers, void* const* workspaces, const int* nparts,
                        float* const* gw, float* const* gbias, void* stream);
+
+/* nconv_wgrad_reduce plus nsum plain sums in the same two launches (n + nsum in 1..16): sum_out[k]
+ * = the sum of sum_x[k][0 .. sum_n[k]) in a fixed order (bitwise deterministic; DNET training:
+ * nconv7's bias gradient, the sum of its output gradient, without two launches of its own).
+ * sum_workspace: nconv_sum_workspace_bytes(nsum) bytes. n may be 0. Returns 0 or -EINVAL. */
+int nconv_wgrad_reduce_ex(int n, const nconv_layer* layers, void* const* workspaces, const int* nparts,
+                          float* const* gw, float* const* gbias, int nsum, const float* const* sum_x,
+                          const long long* sum_n, float* const* sum_out, void* sum_workspace,
+                          size_t sum_workspace_bytes, void* stream);
+size_t nconv_sum_workspace_bytes(int nsum);
 
 /* ------------------------------------------------------------------------------------------
  * Dense convolutions of the RGB-guided model on the matrix cores (fp32 MFMA, exact f32 products).

@@ -13,7 +13,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # NCONV_LIB: an alternative build of the same library (kernel-tuning experiments)
 LIB_PATH = os.environ.get("NCONV_LIB") or os.path.join(_HERE, "libnconv.so")
-ABI_VERSION = 19
+ABI_VERSION = 20
 BWD_ACCUMULATE = 1
 BWD_DEFER_REDUCE = 2
 BWD_SEPARATE = 4
@@ -42,12 +42,15 @@ EXPORTED = (
     "nconv_phase_weights_floats",
     "nconv_phase_weights",
     "nconv_weight_prologue",
+    "nconv_train_prologue",
     "nconv_bwd_workspace_bytes",
     "nconv_bwd",
     "nconv_bwd_ex",
     "nconv_bwd_head_workspace_bytes",
     "nconv_bwd_tail_workspace_bytes",
     "nconv_wgrad_reduce",
+    "nconv_wgrad_reduce_ex",
+    "nconv_sum_workspace_bytes",
     "nconv_dense_packed_floats",
     "nconv_dense_pack",
     "nconv_dense_conv_fwd",
@@ -89,7 +92,9 @@ class NconvBwdIo(ctypes.Structure):
         ("head_workspace_bytes", ctypes.c_size_t), ("head_gw", ctypes.c_void_p), ("head_gbias", ctypes.c_void_p),
         ("head_nparts", ctypes.c_int), ("tail", ctypes.POINTER(NconvLayer)), ("tail_y", ctypes.c_void_p),
         ("tail_cout", ctypes.c_void_p), ("tail_gy", ctypes.c_void_p), ("tail_workspace", ctypes.c_void_p),
-        ("tail_workspace_bytes", ctypes.c_size_t), ("tail_gw", ctypes.c_void_p), ("tail_nparts", ctypes.c_int)]
+        ("tail_workspace_bytes", ctypes.c_size_t), ("tail_gw", ctypes.c_void_p), ("tail_nparts", ctypes.c_int),
+        ("box_weights", ctypes.c_void_p), ("tail_crop0", ctypes.c_int), ("tail_h", ctypes.c_int),
+        ("tail_w", ctypes.c_int)]
 
 
 class NconvDenseConv(ctypes.Structure):
@@ -161,6 +166,14 @@ def _declare(lib):
     lib.nconv_bwd_tail_workspace_bytes.argtypes = [ctypes.POINTER(NconvLayer)]
     lib.nconv_wgrad_reduce.restype = ctypes.c_int
     lib.nconv_wgrad_reduce.argtypes = [ctypes.c_int, ctypes.POINTER(NconvLayer), P, P, P, P, P]
+    lib.nconv_wgrad_reduce_ex.restype = ctypes.c_int
+    lib.nconv_wgrad_reduce_ex.argtypes = [ctypes.c_int, ctypes.POINTER(NconvLayer), P, P, P, P, ctypes.c_int, P, P,
+                                          P, P, ctypes.c_size_t, P]
+    lib.nconv_sum_workspace_bytes.restype = ctypes.c_size_t
+    lib.nconv_sum_workspace_bytes.argtypes = [ctypes.c_int]
+    lib.nconv_train_prologue.restype = ctypes.c_int
+    lib.nconv_train_prologue.argtypes = [ctypes.c_int, P, P, P, P, P, ctypes.c_int, ctypes.c_int, P, ctypes.c_int,
+                                         P, P, P, P, P]
     I = ctypes.c_int
     lib.nconv_dense_packed_floats.restype = ctypes.c_size_t
     lib.nconv_dense_packed_floats.argtypes = [I, I, I]

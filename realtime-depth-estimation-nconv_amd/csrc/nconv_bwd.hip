@@ -15,6 +15,7 @@
 // kernel reduces them in a fixed order (bitwise deterministic, no float atomics).
 #include "nconv_internal.h"
 #include "nconv_route.h"
+#include "nconv_prologue.h"
 
 namespace nconv {
 
@@ -71,7 +72,7 @@ struct GTileStager {
     // T7: nconv7's (gy, y, cout) of the elements (loads issued here, {gN7, gD7} formed by t7_form)
     __device__ __forceinline__ void t7_load(const nconv_layer& L, const BwdArgs& a, int b, int oh0, int ow0, int tid,
                                             float (&v)[3][NE]) const {
-        const int pl7 = (L.Ho + 4) * (L.Wo + 4);
+        const int pl7 = a.t7ph * a.t7pw;
         const size_t base = (size_t)b * pl7;
         const __amdgpu_buffer_rsrc_t rg = plane_rsrc(a.t7gy + base, pl7 * 4);
         const __amdgpu_buffer_rsrc_t ry = plane_rsrc(a.t7y + base, pl7 * 4);
@@ -80,7 +81,7 @@ struct GTileStager {
         for (int k = 0; k < NE; ++k) {
             const int e = tid + 256 * k;
             const int r = e / OWT, col = e - r * OWT;
-            const unsigned off = e < NT ? t7_off(oh0 + r, ow0 + col, L.Ho, L.Wo, OOB) : OOB;
+            const unsigned off = e < NT ? t7_off(a, oh0 + r, ow0 + col, L.Ho, L.Wo, OOB) : OOB;
             v[0][k] = ld_f32(rg, off);
             v[1][k] = ld_f32(ry, off);
             v[2][k] = ld_f32(rc, off);
@@ -520,15 +521,7 @@ __global__ __launch_bounds__(kT) void dgrad_tiled(LayerDev d, BwdArgs a, float* 
 // wave-uniform (waves 0-1 / 2-3) so the box weights stay scalar.
 __global__ __launch_bounds__(kT) void box_weights(const float* __restrict__ w, int first_up, float* __restrict__ wb) {
     const int e = blockIdx.x * kT + threadIdx.x;  // [o][i][t][u], 8 x 8 x 4 x 4
-    if (e >= 1024) return;
-    const int u = e & 3, t = (e >> 2) & 3, i = (e >> 4) & 7, o = e >> 7;
-    const float* wk = w + ((size_t)o * 16 + first_up + i) * 9;
-    const int h0 = t == 0 ? 2 : (t == 1 ? 1 : 0), nh = (t == 1 || t == 2) ? 2 : 1;
-    const int w0 = u == 0 ? 2 : (u == 1 ? 1 : 0), nw = (u == 1 || u == 2) ? 2 : 1;
-    float sum = 0.f;
-    for (int r = 0; r < nh; ++r)
-        for (int c = 0; c < nw; ++c) sum += wk[(h0 + r) * 3 + w0 + c];
-    wb[e] = sum;
+    if (e < 1024) wb[e] = box_weight(w, first_up, e);
 }
 
 template <int MODE, bool T7 = false>
@@ -1031,10 +1024,33 @@ __device__ __forceinline__ int red_job(const int* first, int n, int blk) {
     return k;
 }
 
+// A flat job's chunk sum (nconv_wgrad_reduce_ex): chunk c of kSumChunks contiguous chunks of the
+// vector, lane-strided partial sums, then a fixed-order LDS tree.
+__device__ __forceinline__ float block_tree_sum(float* red, float s) {
+    red[threadIdx.x] = s;
+    __syncthreads();
+#pragma unroll
+    for (int h = kT / 2; h > 0; h >>= 1) {
+        if ((int)threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
+        __syncthreads();
+    }
+    return red[0];
+}
+
 __global__ __launch_bounds__(kT) void wgrad_reduce_sum(const RedTable T) {
     __shared__ float red[kT];
     const int k = red_job(T.x0, T.n, blockIdx.x);
     const RedJob& J = T.j[k];
+    if (J.flat) {
+        const int c = (blockIdx.x - T.x0[k]) * kReduceSplit + blockIdx.y;
+        const long long n = J.nblk, per = (n + kSumChunks - 1) / kSumChunks;
+        const long long e0 = c * per, e1 = e0 + per < n ? e0 + per : n;
+        float s = 0.f;
+        for (long long e = e0 + threadIdx.x; e < e1; e += kT) s += J.part[e];
+        const float t = block_tree_sum(red, s);
+        if (threadIdx.x == 0) J.sub[c] = t;
+        return;
+    }
     const int stride = J.nw + 2 * J.cout, nblk = J.nblk;
     const float* part = J.part;
     float* sub = const_cast<float*>(J.part) + (size_t)nblk * stride;
@@ -1070,8 +1086,17 @@ __device__ __forceinline__ float slice_total(const float* sub, int stride, int e
 }
 
 __global__ __launch_bounds__(kT) void wgrad_finish(const RedTable T) {
+    __shared__ float red[kT];
     const int k = red_job(T.f0, T.n, blockIdx.x);
     const RedJob& J = T.j[k];
+    if (J.flat) {  // the kSumChunks chunk sums: kSumChunks / kT per thread in order, then the tree
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < kSumChunks / kT; ++i) s += J.sub[threadIdx.x * (kSumChunks / kT) + i];
+        const float t = block_tree_sum(red, s);
+        if (threadIdx.x == 0) J.gb[0] = t;
+        return;
+    }
     const int nw = J.nw, cout = J.cout, stride = nw + 2 * cout;
     const float* sub = J.part + (size_t)J.nblk * stride;
     const int w = (blockIdx.x - T.f0[k]) * kT + threadIdx.x;
@@ -1091,11 +1116,12 @@ int launch_wgrad_reduce_multi(int n, const RedJob* jobs, hipStream_t st, const c
     RedTable T;
     T.n = n;
     T.x0[0] = T.f0[0] = 0;
+    static_assert(kSumChunks % kReduceSplit == 0 && kSumChunks % kT == 0, "flat chunks");
     for (int k = 0; k < n; ++k) {
         T.j[k] = jobs[k];
         const int stride = jobs[k].nw + 2 * jobs[k].cout;
-        T.x0[k + 1] = T.x0[k] + (stride + 63) / 64;
-        T.f0[k + 1] = T.f0[k] + (jobs[k].nw + jobs[k].cout + kT - 1) / kT;
+        T.x0[k + 1] = T.x0[k] + (jobs[k].flat ? kSumChunks / kReduceSplit : (stride + 63) / 64);
+        T.f0[k + 1] = T.f0[k] + (jobs[k].flat ? 1 : (jobs[k].nw + jobs[k].cout + kT - 1) / kT);
     }
     for (int k = n + 1; k <= kMaxRedJobs; ++k) T.x0[k] = T.f0[k] = 0;
     hipLaunchKernelGGL(wgrad_reduce_sum, dim3(T.x0[n], kReduceSplit), dim3(kT), 0, st, T);
@@ -1313,12 +1339,12 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(GP ? NCONV_W
         const bool in = row_in && (unsigned)ow < (unsigned)L.Wo;
         const bool inh = hl && row_in && (unsigned)owh < (unsigned)L.Wo;
         if constexpr (T7) {
-            const int pl7 = (L.Ho + 4) * (L.Wo + 4);
+            const int pl7 = a.t7ph * a.t7pw;
             const size_t base7 = (size_t)b * pl7;
             const __amdgpu_buffer_rsrc_t r7g = plane_rsrc(a.t7gy + base7, pl7 * 4);
             const __amdgpu_buffer_rsrc_t r7y = plane_rsrc(a.t7y + base7, pl7 * 4);
             const __amdgpu_buffer_rsrc_t r7c = plane_rsrc(a.t7co + base7, pl7 * 4);
-            const unsigned o0 = t7_off(oh, ow, L.Ho, L.Wo, OOB), o1 = hl ? t7_off(oh, owh, L.Ho, L.Wo, OOB) : OOB;
+            const unsigned o0 = t7_off(a, oh, ow, L.Ho, L.Wo, OOB), o1 = hl ? t7_off(a, oh, owh, L.Ho, L.Wo, OOB) : OOB;
             g7[0][0] = ld_f32(r7g, o0);
             g7[0][1] = ld_f32(r7y, o0);
             g7[0][2] = ld_f32(r7c, o0);
@@ -1681,10 +1707,14 @@ static int go_bwd_tiled(const LayerDev& d, const BwdArgs& a, float* part, float*
             dim3 g(((L.W + D::TW - 1) / D::TW) * ((L.H + D::TH - 1) / D::TH) * L.B);  // see xcd_tile
             constexpr bool up = MODE == NCONV_LOAD_UPCAT_SKIP_FIRST || MODE == NCONV_LOAD_UPCAT_UP_FIRST;
             if constexpr (up && CIN == 16 && COUT == 8 && K == 3) {
-                if (dgrad_phase_ok(L)) {  // box weights into the (then unused) staging planes
-                    hipLaunchKernelGGL(box_weights, dim3(1024 / kT), dim3(kT), 0, st, L.weight,
-                                       MODE == NCONV_LOAD_UPCAT_SKIP_FIRST ? 8 : 0, tx);
-                    hipLaunchKernelGGL((dgrad_phase<MODE, T7>), g, dim3(kT), 0, st, d, a, tx);
+                if (dgrad_phase_ok(L)) {  // box weights: the caller's, or into the (then unused) staging planes
+                    const float* wb = a.box;
+                    if (!wb) {
+                        hipLaunchKernelGGL(box_weights, dim3(1024 / kT), dim3(kT), 0, st, L.weight,
+                                           MODE == NCONV_LOAD_UPCAT_SKIP_FIRST ? 8 : 0, tx);
+                        wb = tx;
+                    }
+                    hipLaunchKernelGGL((dgrad_phase<MODE, T7>), g, dim3(kT), 0, st, d, a, wb);
                 } else {
                     hipLaunchKernelGGL((dgrad_tiled<CIN, COUT, K, MODE>), g, dim3(kT), 0, st, d, a, tx, tc);
                 }

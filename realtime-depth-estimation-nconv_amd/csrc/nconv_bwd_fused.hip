@@ -572,7 +572,7 @@ __global__ __launch_bounds__(ft::kT) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     const __amdgpu_buffer_rsrc_t rbc = plane_rsrc(L.b.c + (size_t)b * 8 * lplane, 8 * lplane * 4);
     const __amdgpu_buffer_rsrc_t ry = plane_rsrc(a.y + (size_t)b * CO * oplane, CO * oplane * 4);
     const __amdgpu_buffer_rsrc_t rco = plane_rsrc(a.co + (size_t)b * CO * oplane, CO * oplane * 4);
-    const int pl7 = (Ho + 4) * (Wo + 4);
+    const int pl7 = a.t7ph * a.t7pw;
     const __amdgpu_buffer_rsrc_t r7g = plane_rsrc(a.t7gy + (size_t)b * pl7, pl7 * 4);
     const __amdgpu_buffer_rsrc_t r7y = plane_rsrc(a.t7y + (size_t)b * pl7, pl7 * 4);
     const __amdgpu_buffer_rsrc_t r7c = plane_rsrc(a.t7co + (size_t)b * pl7, pl7 * 4);
@@ -608,7 +608,7 @@ __global__ __launch_bounds__(ft::kT) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     const int hk = (lane >> 1) & 1, ho = w + 4 * hk;
     const int owm = c0 - 2 + lane, owh = c0 + 62 + (lane & 1);
     auto load_g = [&](int oh) {
-        const unsigned o7 = t7_off(oh, owm, Ho, Wo, OOB), o7h = hl ? t7_off(oh, owh, Ho, Wo, OOB) : OOB;
+        const unsigned o7 = t7_off(a, oh, owm, Ho, Wo, OOB), o7h = hl ? t7_off(a, oh, owh, Ho, Wo, OOB) : OOB;
         g7[0][0] = ld_f32(r7g, o7);
         g7[0][1] = ld_f32(r7y, o7);
         g7[0][2] = ld_f32(r7c, o7);

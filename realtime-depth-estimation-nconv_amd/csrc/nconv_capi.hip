@@ -241,6 +241,36 @@ int nconv_phase_weights(int n, const float* const* weights, const int* cins, con
     return rc ? fail(rc, fn, why) : 0;
 }
 
+int nconv_train_prologue(int n, float* const* weights, const int* couts, const int* fan_ins, const int* softplus,
+                         float* const* wsums, int head1, int head2, float* w21, int nphase, const int* phase_layers,
+                         const int* phase_up_first, float* const* wphases, float* const* wboxes, void* stream) {
+    const char* fn = "nconv_train_prologue";
+    if (n < 0 || nphase < 0) return fail(-22, fn, "negative count");
+    if (n > 0 && (!weights || !couts || !fan_ins || !wsums)) return fail(-22, fn, "null argument");
+    for (int i = 0; i < n; ++i)
+        if (!weights[i] || !wsums[i] || couts[i] <= 0 || fan_ins[i] <= 0) return fail(-22, fn, "bad layer entry");
+    if (w21) {
+        if (head1 < 0 || head1 >= n || head2 < 0 || head2 >= n || head1 == head2)
+            return fail(-22, fn, "head layers must be two distinct layer indices");
+        if (couts[head1] != 8 || fan_ins[head1] != 25 || couts[head2] != 8 || fan_ins[head2] != 200)
+            return fail(-22, fn, "head layers must be nconv1 (8 x 1 x 5 x 5) and nconv2 (8 x 8 x 5 x 5)");
+    }
+    if (nphase > 0 && (!phase_layers || !phase_up_first || !wphases)) return fail(-22, fn, "null phase argument");
+    for (int k = 0; k < nphase; ++k) {
+        const int i = phase_layers[k];
+        if (i < 0 || i >= n || !wphases[k]) return fail(-22, fn, "bad phase entry");
+        if (couts[i] != 8 || fan_ins[i] != 144) return fail(-22, fn, "phase layers must be 8 x 16 x 3 x 3");
+        if (phase_up_first[k] != 0 && phase_up_first[k] != 8) return fail(-22, fn, "up_first must be 0 or 8");
+        if (w21 && (i == head1 || i == head2)) return fail(-22, fn, "a layer is both a head and a phase layer");
+        for (int j = 0; j < k; ++j)
+            if (phase_layers[j] == i) return fail(-22, fn, "a phase layer is listed twice");
+    }
+    const char* why = nullptr;
+    int rc = nconv::launch_train_prologue(n, weights, couts, fan_ins, softplus, wsums, head1, head2, w21, nphase,
+                                          phase_layers, phase_up_first, wphases, wboxes, (hipStream_t)stream, &why);
+    return rc ? fail(rc, fn, why) : 0;
+}
+
 int nconv_weight_prologue(int n, float* const* weights, const int* couts, const int* fan_ins,
                           float* const* wsums, const float* head_w1, const float* head_w2, float* w21,
                           int nphase, const float* const* phase_weights, const int* phase_cins,
@@ -297,6 +327,7 @@ int nconv_bwd_ex(const nconv_layer* L, nconv_bwd_io* io, void* workspace, size_t
                      (float*)workspace, workspace_bytes, (flags & NCONV_BWD_ACCUMULATE) ? 1 : 0, defer, &nparts,
                      io->gy_pool, io->gcout_pool, io->pool_argmax};
     a.separate = (flags & NCONV_BWD_SEPARATE) ? 1 : 0;
+    a.box = io->box_weights;
     io->head_nparts = 0;
     if (const nconv_layer* H = io->head) {
         if (const char* why = validate(H, true)) return fail(-22, "nconv_bwd", why);
@@ -328,6 +359,15 @@ int nconv_bwd_ex(const nconv_layer* L, nconv_bwd_io* io, void* workspace, size_t
             T->load_mode != NCONV_LOAD_PLAIN || T->B != L->B || T->H != L->Ho || T->W != L->Wo)
             return fail(-22, "nconv_bwd", "tail must be a 1x1 padding-2 layer on this layer's outputs (nconv7)");
         if (!io->tail_y || !io->tail_cout || !io->tail_gy) return fail(-22, "nconv_bwd", "null tail planes");
+        // nconv7's planes: its whole (Ho + 4) x (Wo + 4) grid (tail_h = 0), or a window of it
+        if (io->tail_h == 0 && io->tail_w == 0 && io->tail_crop0 == 0) {
+            a.t7ph = L->Ho + 4, a.t7pw = L->Wo + 4, a.t7pc0 = 0;
+        } else {
+            if (io->tail_h <= 0 || io->tail_w <= 0 || io->tail_crop0 < 0 || io->tail_crop0 + io->tail_h > L->Ho + 4 ||
+                io->tail_crop0 + io->tail_w > L->Wo + 4)
+                return fail(-22, "nconv_bwd", "tail window outside nconv7's grid");
+            a.t7ph = io->tail_h, a.t7pw = io->tail_w, a.t7pc0 = io->tail_crop0;
+        }
         if (!io->tail_workspace || io->tail_workspace_bytes < nconv::bwd_tail_workspace_bytes(*L))
             return fail(-22, "nconv_bwd", "tail workspace too small (nconv_bwd_tail_workspace_bytes)");
         if (!defer && !io->tail_gw && (io->gw || io->gbias)) return fail(-22, "nconv_bwd", "tail output is NULL");
@@ -355,17 +395,31 @@ int nconv_bwd_ex(const nconv_layer* L, nconv_bwd_io* io, void* workspace, size_t
 int nconv_bwd(const nconv_layer* L, const float* y, const float* cout, const float* gy,
               const float* gcout, float* gxa, float* gca, float* gxb, float* gcb, float* gw,
               float* gbias, void* workspace, size_t workspace_bytes, unsigned flags, void* stream) {
-    nconv_bwd_io io{y, cout, gy, gcout, gxa, gca, gxb, gcb, gw, gbias, nullptr, nullptr, nullptr,
-                    nullptr, nullptr, 0, nullptr, nullptr, 0,
-                    nullptr, nullptr, nullptr, nullptr, nullptr, 0, nullptr, 0};
+    nconv_bwd_io io{};
+    io.y = y, io.cout = cout, io.gy = gy, io.gcout = gcout;
+    io.gxa = gxa, io.gca = gca, io.gxb = gxb, io.gcb = gcb, io.gw = gw, io.gbias = gbias;
     return nconv_bwd_ex(L, &io, workspace, workspace_bytes, flags, stream);
 }
 
 int nconv_wgrad_reduce(int n, const nconv_layer* layers, void* const* workspaces, const int* nparts,
                        float* const* gw, float* const* gbias, void* stream) {
+    return nconv_wgrad_reduce_ex(n, layers, workspaces, nparts, gw, gbias, 0, nullptr, nullptr, nullptr, nullptr, 0,
+                                 stream);
+}
+
+size_t nconv_sum_workspace_bytes(int nsum) { return nsum > 0 ? (size_t)nsum * nconv::kSumChunks * sizeof(float) : 0; }
+
+int nconv_wgrad_reduce_ex(int n, const nconv_layer* layers, void* const* workspaces, const int* nparts,
+                          float* const* gw, float* const* gbias, int nsum, const float* const* sum_x,
+                          const long long* sum_n, float* const* sum_out, void* sum_workspace,
+                          size_t sum_workspace_bytes, void* stream) {
     const char* fn = "nconv_wgrad_reduce";
-    if (n < 1 || n > nconv::kMaxRedJobs) return fail(-22, fn, "n must be 1..16");
-    if (!layers || !workspaces || !nparts || !gw || !gbias) return fail(-22, fn, "null array");
+    if (n < 0 || nsum < 0 || n + nsum < 1 || n + nsum > nconv::kMaxRedJobs)
+        return fail(-22, fn, "1..16 layers and sums together");
+    if (n > 0 && (!layers || !workspaces || !nparts || !gw || !gbias)) return fail(-22, fn, "null array");
+    if (nsum > 0 && (!sum_x || !sum_n || !sum_out)) return fail(-22, fn, "null sum array");
+    if (nsum > 0 && (!sum_workspace || sum_workspace_bytes < nconv_sum_workspace_bytes(nsum)))
+        return fail(-22, fn, "sum workspace too small (nconv_sum_workspace_bytes)");
     nconv::RedJob jobs[nconv::kMaxRedJobs];
     int m = 0;
     for (int k = 0; k < n; ++k) {
@@ -378,6 +432,12 @@ int nconv_wgrad_reduce(int n, const nconv_layer* layers, void* const* workspaces
         const int fan = (L->Cin / L->groups) * L->KH * L->KW;
         jobs[m++] = nconv::RedJob{(const float*)workspaces[k], L->wsum, gw[k], gbias[k], nparts[k],
                                   L->Cout * fan, L->Cout, fan};
+    }
+    for (int k = 0; k < nsum; ++k) {
+        if (!sum_out[k] || sum_n[k] < 0 || sum_n[k] > 0x7fffffffLL || (sum_n[k] > 0 && !sum_x[k]))
+            return fail(-22, fn, "bad sum entry");
+        float* sub = (float*)sum_workspace + (size_t)k * nconv::kSumChunks;
+        jobs[m++] = nconv::RedJob{sum_x[k], nullptr, nullptr, sum_out[k], (int)sum_n[k], 0, 1, 0, 1, sub};
     }
     if (m == 0) return 0;
     const char* why = nullptr;

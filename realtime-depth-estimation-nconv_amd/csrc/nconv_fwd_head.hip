@@ -458,6 +458,80 @@ __global__ __launch_bounds__(kPrepThreads) void weight_prologue(PrepArgs prep, i
     if (blk < nphase) phase_block(ph.w[blk], ph.cin[blk], ph.ci0[blk], ph.out[blk]);
 }
 
+// The training weight prologue in one launch (nconv_train_prologue): EnforcePos in place and every
+// weight-only input of the training pass formed from the transformed weights. A layer read by
+// several roles would need an order between a writer and its readers, so each layer has exactly
+// one block that reads it: blocks [0, nprep) the other layers (prep_block: softplus in place, then
+// the normalisers), then the head block (nconv1 + nconv2: both staged into LDS through
+// enforce_pos, written back, their normalisers by prep_block's wave sums over the staged rows,
+// then the 83 head units over its 8 waves), then one block per phase layer (staged the same way;
+// normalisers, phase weights, box weights). Every output is bitwise what weight_prep +
+// head_weights + phase_weights + box_weights write. 512 threads per block (1024 caps a lane at
+// 128 VGPRs, and the head units' fp64 sums then spill); the prep and phase roles use the first 256
+// (the others leave before any barrier).
+constexpr int kTrainProThreads = 512;
+__global__ __launch_bounds__(kTrainProThreads) void train_prologue(PrepArgs prep, int nprep, float* w1, float* w2,
+                                                                   float* s1, float* s2, int sp1, int sp2,
+                                                                   float* w21, TrainPhaseArgs ph, int nphase) {
+    __shared__ float lw[1800 + 8];  // head: W1 (200), W2 (1600), s1 (8); phase: W (1152)
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    int blk = blockIdx.x;
+    if (blk < nprep) {
+        if (tid < kPrepThreads) prep_block(prep.w[blk], prep.s[blk], prep.cout[blk], prep.fan_in[blk], prep.softplus[blk]);
+        return;
+    }
+    blk -= nprep;
+    if (w21) {
+        if (blk == 0) {
+            for (int e = tid; e < 1800; e += kTrainProThreads) {
+                const bool one = e < 200;
+                const float v = one ? w1[e] : w2[e - 200];
+                lw[e] = (one ? sp1 : sp2) ? enforce_pos(v) : v;
+            }
+            __syncthreads();
+            for (int e = tid; e < 1800; e += kTrainProThreads) {
+                if (e < 200) {
+                    if (sp1) w1[e] = lw[e];
+                } else if (sp2) {
+                    w2[e - 200] = lw[e];
+                }
+            }
+            for (int r = wave; r < 16; r += kTrainProThreads / 64) {  // s1 (8 rows of 25), s2 (8 of 200)
+                const float v = r < 8 ? row_sum_wave(lw + r * 25, 25, lane)
+                                      : row_sum_wave(lw + 200 + (r - 8) * 200, 200, lane);
+                if (lane == 0) {
+                    if (r < 8) {
+                        s1[r] = v;
+                        lw[1800 + r] = v;
+                    } else {
+                        s2[r - 8] = v;
+                    }
+                }
+            }
+            __syncthreads();
+            const float s1i = lw[1800 + (lane & 7)];
+            for (int u = wave; u < kHeadUnits; u += kTrainProThreads / 64) head_weights_unit(lw, s1i, lw + 200, w21, u, lane);
+            return;
+        }
+        --blk;
+    }
+    if (blk < nphase && tid < kPrepThreads) {
+        float* W = ph.w[blk];
+        const int sp = ph.sp[blk];
+        for (int e = tid; e < 1152; e += kPrepThreads) lw[e] = sp ? enforce_pos(W[e]) : W[e];
+        __syncthreads();
+        if (sp)
+            for (int e = tid; e < 1152; e += kPrepThreads) W[e] = lw[e];
+        for (int o = wave; o < 8; o += kPrepThreads / 64) {
+            const float v = row_sum_wave(lw + o * 144, 144, lane);
+            if (lane == 0) ph.s[blk][o] = v;
+        }
+        phase_block(lw, 16, ph.ci0[blk], ph.out[blk]);
+        if (float* bx = ph.box[blk])
+            for (int e = tid; e < 1024; e += kPrepThreads) bx[e] = box_weight(lw, ph.ci0[blk], e);
+    }
+}
+
 }  // namespace
 
 int launch_fwd_head_exact(const LayerDev& d2, const TailArgs& t, float* y, float* yc, hipStream_t st,
@@ -510,6 +584,55 @@ int launch_weight_prologue(int n, float* const* w, const int* cout, const int* f
 int launch_head_weights(const float* w1, const float* s1, const float* w2, float* out, hipStream_t st,
                         const char** why) {
     hipLaunchKernelGGL(head_weights, dim3(kHeadUnits), dim3(64), 0, st, w1, s1, w2, out);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        *why = hipGetErrorString(e);
+        return -5;
+    }
+    return 0;
+}
+
+int launch_train_prologue(int n, float* const* w, const int* cout, const int* fan_in, const int* sp,
+                          float* const* s, int head1, int head2, float* w21, int nphase, const int* players,
+                          const int* pup_first, float* const* pout, float* const* pbox, hipStream_t st,
+                          const char** why) {
+    if (n < 0 || n > PrepArgs::kMax || nphase < 0 || nphase > TrainPhaseArgs::kMax) {
+        *why = "too many layers for one nconv_train_prologue launch (max 32 layers, 8 phase layers)";
+        return -22;
+    }
+    PrepArgs a{};
+    TrainPhaseArgs p{};
+    int nprep = 0;
+    for (int i = 0; i < n; ++i) {
+        bool own = w21 && (i == head1 || i == head2);
+        for (int k = 0; k < nphase; ++k) own = own || players[k] == i;
+        if (own) continue;
+        a.w[nprep] = w[i];
+        a.s[nprep] = s[i];
+        a.cout[nprep] = cout[i];
+        a.fan_in[nprep] = fan_in[i];
+        a.softplus[nprep] = sp ? sp[i] : 0;
+        ++nprep;
+    }
+    for (int k = 0; k < nphase; ++k) {
+        const int i = players[k];
+        p.w[k] = w[i];
+        p.s[k] = s[i];
+        p.out[k] = pout[k];
+        p.box[k] = pbox ? pbox[k] : nullptr;
+        p.sp[k] = sp ? sp[i] : 0;
+        p.ci0[k] = pup_first[k];
+    }
+    float *w1 = nullptr, *w2 = nullptr, *s1 = nullptr, *s2 = nullptr;
+    int sp1 = 0, sp2 = 0;
+    if (w21) {
+        w1 = w[head1], w2 = w[head2], s1 = s[head1], s2 = s[head2];
+        sp1 = sp ? sp[head1] : 0, sp2 = sp ? sp[head2] : 0;
+    }
+    const int blocks = nprep + (w21 ? 1 : 0) + nphase;
+    if (blocks == 0) return 0;
+    hipLaunchKernelGGL(train_prologue, dim3(blocks), dim3(kTrainProThreads), 0, st, a, nprep, w1, w2, s1, s2, sp1, sp2,
+                       w21, p, nphase);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         *why = hipGetErrorString(e);

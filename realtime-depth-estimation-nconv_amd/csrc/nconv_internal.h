@@ -73,15 +73,22 @@ struct BwdArgs {
     float* t7part;
     float* t7gw;
     int* t7nparts;
+    int t7ph, t7pw, t7pc0;  // nconv7's planes: (t7ph, t7pw) holding its grid from row / column t7pc0
     int separate;  // NCONV_BWD_SEPARATE: no one-kernel backward (input and weight gradient as two kernels)
+    const float* box;  // optional precomputed box weights of an exactly-2x UPCAT layer (dgrad_phase)
 };
 // nconv7 (1x1, padding 2) consumer fused into its producer's backward (T7): byte offset of nconv6
-// pixel (oh, ow) in nconv7's (Ho + 4) x (Wo + 4) grid, or oob outside nconv6's grid; nconv7's {gN7,
-// gD7} from its (gy, y, cout) (its cout gradient is 0); nconv6's (gy, gcout) from them and w7[o] as
-// nconv7's own 1x1 input gradient forms them (dgrad_tiled<8,1,1>'s epilogue, same operations)
-__device__ __forceinline__ unsigned t7_off(int oh, int ow, int Ho, int Wo, unsigned oob) {
-    return ((unsigned)oh < (unsigned)Ho && (unsigned)ow < (unsigned)Wo) ? (unsigned)((oh + 2) * (Wo + 4) + ow + 2) * 4u
-                                                                          : oob;
+// pixel (oh, ow) in nconv7's planes -- its (Ho + 4) x (Wo + 4) grid, or the window of it that DNET's
+// crop keeps (t7ph x t7pw from row / column t7pc0) -- or oob outside nconv6's grid or the window (a
+// zero gradient there); nconv7's {gN7, gD7} from its (gy, y, cout) (its cout gradient is 0);
+// nconv6's (gy, gcout) from them and w7[o] as nconv7's own 1x1 input gradient forms them
+// (dgrad_tiled<8,1,1>'s epilogue, same operations)
+__device__ __forceinline__ unsigned t7_off(const BwdArgs& a, int oh, int ow, int Ho, int Wo, unsigned oob) {
+    const int r = oh + 2 - a.t7pc0, c = ow + 2 - a.t7pc0;
+    return ((unsigned)oh < (unsigned)Ho && (unsigned)ow < (unsigned)Wo && (unsigned)r < (unsigned)a.t7ph &&
+            (unsigned)c < (unsigned)a.t7pw)
+               ? (unsigned)(r * a.t7pw + c) * 4u
+               : oob;
 }
 __device__ __forceinline__ void t7_nd(const BwdArgs& a, float gy9, float y9, float co9, float& gN7, float& gD7) {
     nconv_grad_nd(gy9, 0.f, y9, co9, a.t7eps, a.t7b[0], a.t7s[0], gN7, gD7);
@@ -101,8 +108,13 @@ struct RedJob {
     float* gw;
     float* gb;
     int nblk, nw, cout, fan;
+    // flat (nconv_wgrad_reduce_ex sums): gb[0] = the sum of part[0 .. nblk) (nw = 0, cout = 1) in a
+    // fixed order -- kSumChunks chunk sums into sub, then their tree
+    int flat;
+    float* sub;
 };
 constexpr int kMaxRedJobs = 16;
+constexpr int kSumChunks = 1024;
 int launch_wgrad_reduce_multi(int n, const RedJob* jobs, hipStream_t st, const char** why);
 
 // Forward. Return 0, or a negative errno with *why set.
@@ -127,6 +139,10 @@ int launch_weight_prologue(int n, float* const* w, const int* cout, const int* f
                            const float* w1, const float* w2, float* w21, int nphase, const float* const* pw,
                            const int* pcin, const int* pup_first, float* const* pout, hipStream_t st,
                            const char** why);
+int launch_train_prologue(int n, float* const* w, const int* cout, const int* fan_in, const int* sp,
+                          float* const* s, int head1, int head2, float* w21, int nphase, const int* players,
+                          const int* pup_first, float* const* pout, float* const* pbox, hipStream_t st,
+                          const char** why);
 int launch_head_weights(const float* w1, const float* s1, const float* w2, float* out, hipStream_t st,
                         const char** why);
 int launch_fwd_tail(const LayerDev& d, const TailArgs& t, float* out, hipStream_t st, const char** why);

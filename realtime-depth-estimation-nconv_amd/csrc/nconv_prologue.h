@@ -29,16 +29,19 @@ __device__ __forceinline__ float row_sum_wave(const float* wr, int fan, int lane
     return s;
 }
 
+// EnforcePos's softplus of one weight. Not inlined: every launch that applies it (weight_prep,
+// the training prologue's staging) runs this one instruction sequence, so all agree bitwise.
+__device__ __attribute__((noinline)) float enforce_pos(float v) {
+    const float bv = v * 10.0f;
+    return (bv > 20.0f) ? v : log1pf(expf(bv)) / 10.0f;
+}
+
 // One layer per 256-thread block: optional in-place softplus, then one wave per row for s[o]
 // (lanes stride the row, coalesced), instead of one thread walking ~200 dependent loads.
 __device__ __forceinline__ void prep_block(float* w, float* s, int cout, int fan, int softplus) {
     const int n = cout * fan;
     if (softplus) {
-        for (int i = threadIdx.x; i < n; i += kPrepThreads) {
-            const float v = w[i];
-            const float bv = v * 10.0f;
-            w[i] = (bv > 20.0f) ? v : log1pf(expf(bv)) / 10.0f;
-        }
+        for (int i = threadIdx.x; i < n; i += kPrepThreads) w[i] = enforce_pos(w[i]);
         __syncthreads();
         __threadfence_block();
     }
@@ -59,6 +62,33 @@ struct PhaseArgs {
     float* out[kMax];
     int ci0[kMax];  // input channel of up channel 0
     int cin[kMax];
+};
+
+// Box weights of an exactly-2x UPCAT layer's upsampled half for the phase-form input gradient
+// (dgrad_phase, nconv_bwd.hip): entry e = [o][i][t][u] (8 x 8 x 4 x 4) = the sum of W[o][first_up +
+// i][kh][kw] over kh in S(t), kw in S(u), S(0) = {2}, S(1) = {1, 2}, S(2) = {0, 1}, S(3) = {0}
+// (row-major order). Shared by the box_weights launch and the training prologue (bitwise equal).
+__device__ __forceinline__ float box_weight(const float* w, int first_up, int e) {
+    const int u = e & 3, t = (e >> 2) & 3, i = (e >> 4) & 7, o = e >> 7;
+    const float* wk = w + ((size_t)o * 16 + first_up + i) * 9;
+    const int h0 = t == 0 ? 2 : (t == 1 ? 1 : 0), nh = (t == 1 || t == 2) ? 2 : 1;
+    const int w0 = u == 0 ? 2 : (u == 1 ? 1 : 0), nw = (u == 1 || u == 2) ? 2 : 1;
+    float sum = 0.f;
+    for (int r = 0; r < nh; ++r)
+        for (int c = 0; c < nw; ++c) sum += wk[(h0 + r) * 3 + w0 + c];
+    return sum;
+}
+
+// Training prologue (nconv_train_prologue): per phase layer (16 -> 8 3x3) its weight (EnforcePos
+// applied in place when sp), normalisers, phase weights and optional box weights.
+struct TrainPhaseArgs {
+    static constexpr int kMax = 8;
+    float* w[kMax];
+    float* s[kMax];
+    float* out[kMax];
+    float* box[kMax];
+    int sp[kMax];
+    int ci0[kMax];
 };
 
 __device__ __forceinline__ void phase_block(const float* W, int cin, int ci0, float* out) {

@@ -25,7 +25,8 @@ import torch.nn as nn
 
 from . import _lib, dense, export, nconv
 from .nconv import (EnforcePos, NConv2d, WgradReduce, _require_device, head_weights, layer_backward,
-                    layer_forward_head, layer_forward_pooled, layer_forward_raw, nconv_layer, phase_weights, weight_prep)
+                    layer_forward_head, layer_forward_pooled, layer_forward_raw, nconv_layer, phase_weights,
+                    train_prologue, weight_prep)
 
 LAYERS = ("nconv1", "nconv2", "nconv_down1", "nconv_down2", "nconv_down3", "nconv4", "nconv5",
           "nconv6", "nconv7")
@@ -36,6 +37,11 @@ class DNETFn(torch.autograd.Function):
     backwards in reverse order itself. Inputs: specs, capture (dict or None), S, then (weight, bias,
     s[o]) of each layer in LAYERS order, then the phase weights; outputs: nconv7's (uncropped) y,
     cout.
+
+    crop: None, or DNET's output size (h, w) when the fused training tail writes nconv7's output
+    already cropped (DNET._tail_crop): the outputs are then the cropped (y, cout), and the backward
+    reads their gradient through the window (nconv_bwd_io tail_crop0), with no crop copy and no
+    zero-padded gradient.
 
     Three tensors are read by two layers each (nconv2's output: down1 through the 2x2 max-pool and
     nconv6; down1's: down2 and nconv5; down2's: down3 and nconv4). With exact-fp32 forward and
@@ -48,18 +54,23 @@ class DNETFn(torch.autograd.Function):
     into the full-resolution gradient (NCONV_BWD_ACCUMULATE)."""
 
     @staticmethod
-    def forward(ctx, specs, capture, S, *p):
+    def forward(ctx, specs, capture, crop, S, *p):
         """p: (weight, bias, s[o]) of each layer, then the phase weights of nconv4/5/6 (a (3, 1024)
-        tensor, DNET._phase_weights) or None."""
+        tensor, DNET._phase_weights) or None, then optionally the exact head's weights (None: built
+        here) and the box weights of nconv4/5/6 (a (3, 1024) tensor, None: built by the backward),
+        both from DNET._train_prologue."""
         W = [p[3 * i:3 * i + 3] for i in range(9)]
         wph = p[27] if len(p) > 27 and p[27] is not None else None
+        w21 = p[28] if len(p) > 28 else None
+        ctx.wbox = p[29] if len(p) > 29 else None
         w4, w5, w6 = (None, None, None) if wph is None else tuple(wph)
         sp = specs
         pooled = _materialise_pool(S)
         if pooled:
             spp = [dataclasses.replace(sp[k], mode=_lib.PLAIN) for k in (2, 3, 4)]
             if FUSE_HEAD_FWD:  # nconv1 inside nconv2's tile, nconv1's outputs written for the backward
-                w21 = head_weights(sp[0], sp[1], S, *W[0], *W[1])
+                if w21 is None:
+                    w21 = head_weights(sp[0], sp[1], S, *W[0], *W[1])
                 x2, c2, p2x, p2c, a2, x1, c1 = layer_forward_head(sp[0], sp[1], S, *W[0], *W[1], w21, train=True)
             else:
                 x1, c1 = layer_forward_raw(sp[0], S, None, None, None, *W[0])
@@ -77,8 +88,11 @@ class DNETFn(torch.autograd.Function):
             pools = ()
         x6, c6 = layer_forward_raw(sp[5], x4, c4, x5, c5, *W[5], wphase=w4)
         x7, c7 = layer_forward_raw(sp[6], x3, c3, x6, c6, *W[6], wphase=w5)
+        ctx.crop = crop
         if pooled and FUSE_TAIL_FWD and w6 is not None and x2.shape[2:] == tuple(2 * v for v in x7.shape[2:]):
-            x8, c8, x9, c9 = _tail_train(sp[7], sp[8], x2, c2, x7, c7, W[7], W[8], w6)
+            x8, c8, x9, c9 = _tail_train(sp[7], sp[8], x2, c2, x7, c7, W[7], W[8], w6, crop)
+        elif crop is not None:
+            raise RuntimeError("DNETFn: a cropped output needs the fused training tail")
         else:
             x8, c8 = layer_forward_raw(sp[7], x2, c2, x7, c7, *W[7], wphase=w6)
             x9, c9 = layer_forward_raw(sp[8], x8, c8, None, None, *W[8])
@@ -100,9 +114,10 @@ class DNETFn(torch.autograd.Function):
         if g9 is None:  # (grads are not materialised)
             g9 = torch.zeros_like(sv[44])
         S, p, acts, pools = sv[0], sv[1:28], sv[28:46], sv[46:]
+        wbox = (None, None, None) if ctx.wbox is None else tuple(ctx.wbox)
         W = [p[3 * i:3 * i + 3] for i in range(9)]
         X = [None] + [(acts[2 * i], acts[2 * i + 1]) for i in range(9)]  # X[k] = output of layer k
-        need = ctx.needs_input_grad[1:]  # (capture, S, w1, b1, s1, ...)
+        need = ctx.needs_input_grad[2:]  # (capture, S, w1, b1, s1, ...)
         gw = [torch.empty_like(W[i][0]) if need[2 + 3 * i] else None for i in range(9)]
         gb = [torch.empty_like(W[i][1]) if need[3 + 3 * i] else None for i in range(9)]
         e = torch.empty_like
@@ -129,13 +144,13 @@ class DNETFn(torch.autograd.Function):
             with torch.cuda.stream(side):
                 layer_backward(spec, inputs, y, co, gy, gco, (None,) * 4, gw_, gb_, defer=red, tail=tail, **kw)
 
-        def bwd(k, a, b, ga, gb_, acc=False, src_a=None, spec=None, pool_grad=None):
+        def bwd(k, a, b, ga, gb_, acc=False, src_a=None, spec=None, pool_grad=None, box=None):
             xa, ca = src_a if src_a is not None else (X[a] if a else (S, None))
             xb, cb = X[b] if b else (None, None)
             gy, gco = G[k] if G[k] is not None else (g9, None)
             layer_bwd(spec or sp[k - 1], (xa, ca, xb, cb, *W[k - 1]), X[k][0], X[k][1], gy, gco,
                       (*(ga or (None, None)), *(gb_ or (None, None))), gw[k - 1], gb[k - 1], accumulate=acc,
-                      pool_grad=pool_grad, fused=pool_grad is not None and LAYERS[k - 1] in FUSED_BWD)
+                      pool_grad=pool_grad, fused=pool_grad is not None and LAYERS[k - 1] in FUSED_BWD, box=box)
 
         def finish():
             if side is not None:
@@ -146,25 +161,28 @@ class DNETFn(torch.autograd.Function):
         exact_up = X[2][0].shape[2:] == tuple(2 * v for v in X[7][0].shape[2:])  # nconv6's phase form
         # (c9 is non-differentiable; nconv7's weight gradient is accumulated inside nconv6's weight-
         # gradient pass, so the fused form needs nconv6's gw or gb too)
-        if FUSE_TAIL_BWD and ctx.pooled and exact_up and gw[8] is not None and (gw[7] is not None or
-                                                                             gb[7] is not None):
+        if ctx.crop is not None or (FUSE_TAIL_BWD and ctx.pooled and exact_up and gw[8] is not None and
+                                    (gw[7] is not None or gb[7] is not None)):
             # nconv7's backward inside nconv6's (nconv_bwd_ex tail): its input gradient never reaches
             # HBM; its bias gradient is the sum of its output gradient (every output pixel, padding ring
-            # included, as autograd's conv bias gradient)
+            # included, as autograd's conv bias gradient), summed by the batched reduction. With the
+            # cropped output nconv7's planes are the crop window from grid row / column 1
+            # (step1.py:94); the gradient outside it is 0
             g9c = g9.contiguous()
             layer_bwd(sp[7], (X[2][0], X[2][1], X[7][0], X[7][1], *W[7]), X[8][0], X[8][1], None, None,
-                      (*G[2], *G[7]), gw[7], gb[7], tail=(sp[8], *W[8], X[9][0], X[9][1], g9c, gw[8]),
-                      fused="nconv6" in FUSED_BWD)
-            if gb[8] is not None:  # (libnconv's per-channel sum)
-                dense.relu_bias_bwd(g9c, None, None, gb[8])
+                      (*G[2], *G[7]), gw[7], gb[7],
+                      tail=(sp[8], *W[8], X[9][0], X[9][1], g9c, gw[8], None if ctx.crop is None else 1),
+                      fused="nconv6" in FUSED_BWD, box=wbox[2])
+            if gb[8] is not None:
+                red.add_sum(g9c, gb[8])
         else:
             G[8] = (e(X[8][0]), e(X[8][1]))
             bwd(9, 8, 0, G[8], None)                        # nconv7
             bwd(8, 2, 7, G[2], G[7])                        # nconv6: nconv2's output (overwrite) + up
         G[3], G[6] = (e(X[3][0]), e(X[3][1])), (e(X[6][0]), e(X[6][1]))
-        bwd(7, 3, 6, G[3], G[6])                        # nconv5: down1's output + up
+        bwd(7, 3, 6, G[3], G[6], box=wbox[1])           # nconv5: down1's output + up
         G[4], G[5] = (e(X[4][0]), e(X[4][1])), (e(X[5][0]), e(X[5][1]))
-        bwd(6, 4, 5, G[4], G[5])                        # nconv4: down2's output + up
+        bwd(6, 4, 5, G[4], G[5], box=wbox[0])           # nconv4: down2's output + up
         if ctx.pooled:
             p2x, p2c, a2, p3x, p3c, a3, p4x, p4c, a4 = pools
             plain = [dataclasses.replace(sp[k], mode=_lib.PLAIN) for k in (2, 3, 4)]
@@ -179,7 +197,7 @@ class DNETFn(torch.autograd.Function):
                           (None, None, None, None), gw[1], gb[1], pool_grad=(*gp2, a2),
                           head=(sp[0], S, *W[0], gw[0], gb[0]), fused="nconv2" in FUSED_BWD)
                 finish()
-                out = [None, None, None]
+                out = [None, None, None, None]
                 for i in range(9):
                     out += [gw[i], gb[i], None]
                 return tuple(out + [None] * ctx.n_extra)
@@ -195,7 +213,7 @@ class DNETFn(torch.autograd.Function):
         layer_bwd(sp[0], (S, None, None, None, *W[0]), X[1][0], X[1][1], G[1][0], G[1][1],
                   (gS, None, None, None), gw[0], gb[0])  # nconv1 (threshold: c0 has no gradient)
         finish()
-        out = [None, None, gS]
+        out = [None, None, None, gS]
         for i in range(9):
             out += [gw[i], gb[i], None]
         return tuple(out + [None] * ctx.n_extra)
@@ -214,19 +232,20 @@ FUSE_TAIL_FWD = True  # ... and nconv6 + nconv7 as the fused tail (nconv_fwd_tai
 FUSED_BWD = frozenset(os.environ.get("NCONV_FUSED_BWD", "").split(",")) - {""}
 
 
-def _tail_train(sp6, sp7, x2, c2, x7, c7, W6, W7, w6):
+def _tail_train(sp6, sp7, x2, c2, x7, c7, W6, W7, w6, crop=None):
     """nconv6 + nconv7 in one phase-tail launch writing nconv6's outputs and nconv7's whole
-    (uncropped) output grid -- what the training backward reads (nconv_fwd_tail, crop0 = 0)."""
+    (uncropped) output grid -- what the training backward reads (nconv_fwd_tail, crop0 = 0) -- or,
+    with crop = (h, w), nconv7's output cropped as step1.py:94 (crop0 = 1)."""
     L = sp6.descriptor(x2, c2, x7, c7, *W6, w6)
     (w7, b7, s7), p7 = W7, sp7.padding[0]
     B, dev = x2.shape[0], x2.device
     x8 = torch.empty((B, sp6.cout, L.Ho, L.Wo), device=dev, dtype=torch.float32)
     c8 = torch.empty_like(x8)
-    H9, W9 = L.Ho + 2 * p7, L.Wo + 2 * p7
+    (H9, W9), crop0 = ((L.Ho + 2 * p7, L.Wo + 2 * p7), 0) if crop is None else (tuple(crop), 1)
     x9 = torch.empty((B, 1, H9, W9), device=dev, dtype=torch.float32)
     c9 = torch.empty_like(x9)
     rc = _lib.lib().nconv_fwd_tail(_lib.ctypes.byref(L), _lib.ptr(w7), _lib.ptr(b7), _lib.ptr(s7), sp7.cin, p7,
-                                   sp7.eps, _lib.ptr(x9), _lib.ptr(c9), H9, W9, 0, _lib.ptr(x8), _lib.ptr(c8),
+                                   sp7.eps, _lib.ptr(x9), _lib.ptr(c9), H9, W9, crop0, _lib.ptr(x8), _lib.ptr(c8),
                                    _lib.stream_handle(dev))
     _lib.check(rc, "nconv_fwd_tail")
     return x8, c8, x9, c9
@@ -327,6 +346,66 @@ class DNET(nn.Module):
         weight_prep(weights, batched_sp, wsums)
         return wsums
 
+    def _train_prologue(self, layers, S):
+        """(wsums, phase weights, head weights, box weights) of the whole-graph training pass from
+        one nconv_train_prologue launch (EnforcePos applied in place first, as the hooks would),
+        or None where the separate path must run: merged_prologue off, a forward pre-hook other
+        than this package's softplus EnforcePos, weights that are not contiguous fp32 device
+        tensors, or a matrix-core arithmetic. Phase / box weights are None when phase_upcat is off
+        or the UpCat layers do not have the phase form's geometry; head weights None when the
+        fused training head is off."""
+        if not self.merged_prologue or nconv.FORWARD_MATH != _lib.MATH_FP32 or not _materialise_pool(S):
+            return None
+        sp = []
+        for m in layers:
+            hooks = list(m._forward_pre_hooks.values())
+            ours = len(hooks) == 1 and isinstance(hooks[0], EnforcePos) and hooks[0].name == "weight" \
+                and hooks[0].pos_fn.lower() == "softplus"
+            if not (len(hooks) == 0 or ours):
+                return None
+            w = m.weight
+            if not (w.is_cuda and w.dtype == torch.float32 and w.is_contiguous()):
+                return None
+            sp.append(ours and m.training)
+        dev = S.device
+        weights = [m.weight.data for m in layers]
+        buf = torch.empty(sum(w.shape[0] for w in weights), device=dev, dtype=torch.float32)
+        wsums, off = [], 0
+        for w in weights:
+            wsums.append(buf[off:off + w.shape[0]])
+            off += w.shape[0]
+        head, w21 = None, None
+        if FUSE_HEAD_FWD and self._head_shapes(layers[0], layers[1]):
+            w21 = torch.empty(nconv.HEAD_WEIGHTS_FLOATS, device=dev, dtype=torch.float32)
+            head = (0, 1, w21)
+        phase, wph, wbox = None, None, None
+        ls = (self.nconv4, self.nconv5, self.nconv6)
+        if self.phase_upcat and all(m.weight.shape[0] == 8 and m.weight.shape[1] == 16 and
+                                    tuple(m.weight.shape[2:]) == (3, 3) for m in ls):
+            wph = torch.empty((3, 1024), device=dev, dtype=torch.float32)
+            wbox = torch.empty((3, nconv.BOX_WEIGHT_FLOATS), device=dev, dtype=torch.float32)
+            phase = ([5, 6, 7], [8, 8, 0], list(wph), list(wbox))
+        train_prologue(weights, sp, wsums, head=head, phase=phase)
+        return wsums, wph, w21, wbox
+
+    # The whole-graph training pass writes DNET's cropped output from the fused tail where it can
+    # (_tail_crop); False: nconv7's whole grid, then CropFn (tests compare the two).
+    crop_in_tail = True
+
+    def _tail_crop(self, S, wph):
+        """Whether the whole-graph training pass writes DNET's cropped output straight from the
+        fused tail (no crop copy, no zero-padded gradient): the pooled graph with the fused
+        training tail and its backward, exactly-2x UpCat, a crop window covering every nconv6 pixel
+        (crop0 = 1 <= nconv7's padding, the window at least (H - 1) x (W - 1): the generalized crop,
+        or the literal one up to 481 x 641), and nconv7's weight gradient only with nconv6's
+        (it is accumulated in nconv6's weight-gradient pass)."""
+        H, W = S.shape[2], S.shape[3]
+        oh, ow = crop_hw(H, W, self.crop)
+        l6, l7 = self.nconv6, self.nconv7
+        return (self.crop_in_tail and wph is not None and FUSE_TAIL_FWD and FUSE_TAIL_BWD and _materialise_pool(S) and H % 2 == 0
+                and W % 2 == 0 and tuple(l7.padding) == (2, 2) and oh >= H - 1 and ow >= W - 1
+                and (not l7.weight.requires_grad or l6.weight.requires_grad or l6.bias.requires_grad))
+
     # The eval-mode forward builds its weight-only prologue -- the normalisers, the exact head's
     # composed weights and nconv4/5/6's phase weights -- in one launch (nconv_weight_prologue,
     # bitwise the three separate launches); False: the separate launches.
@@ -392,20 +471,28 @@ class DNET(nn.Module):
             self._infer_split(S, layers, wsum, out, wph, w21)
             return out
 
-        wsum = self._prologue(layers, S)
         (l1, l2, d1, d2, d3, l4, l5, l6, l7) = layers
-        (s1, s2, sd1, sd2, sd3, s4, s5, s6, s7) = wsum
-        f = nconv_layer if grad else (lambda spec, *a, wphase=None: layer_forward_raw(spec, *a, wphase=wphase))
-
         if grad and self.whole_graph_autograd and S.shape[0] > 0:
             specs = (l1.spec(_lib.THRESH, 0.01), l2.spec(), d1.spec(_lib.POOL2), d2.spec(_lib.POOL2),
                      d3.spec(_lib.POOL2), l4.spec(_lib.UPCAT_SKIP_FIRST), l5.spec(_lib.UPCAT_SKIP_FIRST),
                      l6.spec(_lib.UPCAT_UP_FIRST), l7.spec())
+            pro = self._train_prologue(layers, S)
+            if pro is None:
+                wsum = self._prologue(layers, S)
+                extra = (self._phase_weights(S.device),)
+            else:
+                wsum, wph, w21, wbox = pro
+                extra = (wph, w21, wbox)
             params = []
             for m_, s_ in zip(layers, wsum):
                 params += [m_.weight, m_.bias, s_]
-            xo, _ = DNETFn.apply(specs, self.capture, S, *params, self._phase_weights(S.device))
-            return CropFn.apply(xo, out_h, out_w)
+            crop = (out_h, out_w) if self._tail_crop(S, extra[0]) else None
+            xo, _ = DNETFn.apply(specs, self.capture, crop, S, *params, *extra)
+            return xo if crop is not None else CropFn.apply(xo, out_h, out_w)
+
+        wsum = self._prologue(layers, S)
+        (s1, s2, sd1, sd2, sd3, s4, s5, s6, s7) = wsum
+        f = nconv_layer if grad else (lambda spec, *a, wphase=None: layer_forward_raw(spec, *a, wphase=wphase))
 
         wph = self._phase_weights(S.device)
         w4, w5, w6 = (None, None, None) if wph is None else tuple(wph)

@@ -166,6 +166,37 @@ def weight_prologue(weights, wsums, head=None, phase=None):
     _lib.check(rc, "nconv_weight_prologue")
 
 
+def train_prologue(weights, softplus, wsums, head=None, phase=None):
+    """nconv_train_prologue: the training pass's weight prologue in one launch -- EnforcePos's
+    softplus in place on the layers flagged in `softplus`, every layer's normalisers into wsums, and
+    from the transformed weights: head = (i1, i2, w21) the exact head's weights of layers i1 (nconv1)
+    / i2 (nconv2), or None; phase = (layer indices, up_first, phase outs, box outs or None) as
+    phase_weights' outputs plus the backward's box weights (BOX_WEIGHT_FLOATS each). Bitwise what
+    weight_prep + head_weights + phase_weights + the backward's box-weight builds write."""
+    n = len(weights)
+    i1, i2, w21 = head if head is not None else (-1, -1, None)
+    pl, pup, pout, pbox = phase if phase is not None else ([], [], [], None)
+    if w21 is not None and (w21.numel() < HEAD_WEIGHTS_FLOATS or not w21.is_contiguous() or
+                            w21.dtype != torch.float32):
+        raise ValueError(f"head-weight buffer needs {HEAD_WEIGHTS_FLOATS} contiguous fp32 elements")
+    for o in list(pout) + list(pbox or []):
+        if o.numel() < PHASE_WEIGHT_FLOATS or not o.is_contiguous() or o.dtype != torch.float32:
+            raise ValueError(f"phase / box buffers need {PHASE_WEIGHT_FLOATS} contiguous fp32 elements")
+    m = len(pl)
+    P, I = _lib.ctypes.c_void_p, _lib.ctypes.c_int
+    rc = _lib.lib().nconv_train_prologue(
+        n, (P * max(n, 1))(*[w.data_ptr() for w in weights]), (I * max(n, 1))(*[w.shape[0] for w in weights]),
+        (I * max(n, 1))(*[w[0].numel() for w in weights]), (I * max(n, 1))(*[int(bool(v)) for v in softplus]),
+        (P * max(n, 1))(*[s.data_ptr() for s in wsums]), i1, i2, _lib.ptr(w21), m, (I * max(m, 1))(*pl),
+        (I * max(m, 1))(*pup), (P * max(m, 1))(*[o.data_ptr() for o in pout]),
+        (P * max(m, 1))(*[o.data_ptr() for o in pbox]) if pbox is not None else None,
+        _lib.stream_handle(weights[0].device))
+    _lib.check(rc, "nconv_train_prologue")
+
+
+BOX_WEIGHT_FLOATS = 1024  # (8, 8, 4, 4) box weights of an exactly-2x UPCAT layer (nconv_bwd_io.box_weights)
+
+
 def layer_forward_raw(spec: LayerSpec, xa, ca, xb, cb, weight, bias, wsum, out=None, wphase=None):
     """Enqueue nconv_fwd; returns (y, cout) (written into `out` if given). No autograd. `wphase`:
     the layer's phase weights (UPCAT layers, phase_weights), or None."""
@@ -258,7 +289,7 @@ class NConvLayerFn(torch.autograd.Function):
 
 
 def layer_backward(spec: LayerSpec, inputs, y, co, gy, gco, gin, gw, gb, accumulate=False, defer=None,
-                   pool_grad=None, head=None, tail=None, separate=False):
+                   pool_grad=None, head=None, tail=None, separate=False, box=None):
     """nconv_bwd of one fused layer: gin = (gxa, gca, gxb, gcb) (None: skip) overwritten, or added
     into with accumulate=True (NCONV_BWD_ACCUMULATE: a tensor consumed by two layers); gw, gb
     overwritten (None: skip). defer: a WgradReduce collecting the layer's weight-gradient partial
@@ -271,7 +302,10 @@ def layer_backward(spec: LayerSpec, inputs, y, co, gy, gco, gin, gw, gb, accumul
     is fused into this layer's (nconv_bwd_ex tail; gy / gco are then unused and may be None; nconv7's
     bias gradient is the caller's). With pool_grad and both an input gradient (or head) and gw / gb
     requested, an exact-fp32 8 -> 8 5x5 layer runs one kernel for both gradients (include/nconv.h
-    NCONV_BWD_SEPARATE); separate=True runs the input- and weight-gradient kernels instead."""
+    NCONV_BWD_SEPARATE); separate=True runs the input- and weight-gradient kernels instead. tail may
+    carry a 9th element, the crop origin of nconv7's planes when they hold a window of its grid
+    (DNET's crop: nconv_bwd_io tail_crop0 / tail_h / tail_w). box: an exactly-2x UPCAT layer's box
+    weights (train_prologue), else built by this call."""
     xa, ca, xb, cb, weight, bias, wsum = inputs
     gxa, gca, gxb, gcb = gin
     dev = y.device
@@ -299,8 +333,11 @@ def layer_backward(spec: LayerSpec, inputs, y, co, gy, gco, gin, gw, gb, accumul
         io.head = _lib.ctypes.pointer(HL)
         io.head_workspace, io.head_workspace_bytes = hws.data_ptr(), hbytes
         io.head_gw, io.head_gbias = _lib.ptr(hgw), _lib.ptr(hgb)
+    io.box_weights = _lib.ptr(box)
     if tail is not None:
-        tspec, tw, tb, ts, ty, tco, tgy, tgw = tail
+        tspec, tw, tb, ts, ty, tco, tgy, tgw = tail[:8]
+        if len(tail) > 8 and tail[8] is not None:  # the planes hold a window of nconv7's grid
+            io.tail_crop0, io.tail_h, io.tail_w = int(tail[8]), ty.shape[2], ty.shape[3]
         TL = tspec.descriptor(y, co, None, None, tw, tb, ts)
         tbytes = lib.nconv_bwd_tail_workspace_bytes(_lib.ctypes.byref(L))
         tws = torch.empty(max(tbytes, 1), dtype=torch.uint8, device=dev)
@@ -327,10 +364,15 @@ class WgradReduce:
 
     def __init__(self):
         self.jobs = []
+        self.sums = []
 
     def add(self, L, ws, nparts, gw, gb):
         if nparts > 0 and (gw is not None or gb is not None):  # (input-gradient-only calls add none)
             self.jobs.append((L, ws, nparts, gw, gb, torch.cuda.current_stream(ws.device)))
+
+    def add_sum(self, x, out):
+        """out[0] = x.sum() in the same two launches (nconv_wgrad_reduce_ex; fixed order)."""
+        self.sums.append((x.contiguous(), out, torch.cuda.current_stream(x.device)))
 
     def run(self, device):
         cur = torch.cuda.current_stream(device)
@@ -339,18 +381,31 @@ class WgradReduce:
             # by the current one: keep the allocator from reusing it before this reduction ran
             if j[5] != cur:
                 j[1].record_stream(cur)
-        for k in range(0, len(self.jobs), 16):
-            jobs = self.jobs[k:k + 16]
-            n = len(jobs)
-            layers = (_lib.NconvLayer * n)(*[j[0] for j in jobs])
-            VP = _lib.ctypes.c_void_p * n
+        for j in self.sums:
+            if j[2] != cur:
+                j[0].record_stream(cur)
+        items = [("job", j) for j in self.jobs] + [("sum", j) for j in self.sums]
+        lib = _lib.lib()
+        for k in range(0, len(items), 16):
+            jobs = [j for t, j in items[k:k + 16] if t == "job"]
+            sums = [j for t, j in items[k:k + 16] if t == "sum"]
+            n, ns = len(jobs), len(sums)
+            VP = _lib.ctypes.c_void_p * max(n, 1)
+            layers = (_lib.NconvLayer * max(n, 1))(*[j[0] for j in jobs])
             wss = VP(*[j[1].data_ptr() for j in jobs])
-            nparts = (_lib.ctypes.c_int * n)(*[j[2] for j in jobs])
+            nparts = (_lib.ctypes.c_int * max(n, 1))(*[j[2] for j in jobs])
             gws = VP(*[(j[3].data_ptr() if j[3] is not None else None) for j in jobs])
             gbs = VP(*[(j[4].data_ptr() if j[4] is not None else None) for j in jobs])
-            rc = _lib.lib().nconv_wgrad_reduce(n, layers, wss, nparts, gws, gbs, _lib.stream_handle(device))
+            SP = _lib.ctypes.c_void_p * max(ns, 1)
+            sws_bytes = lib.nconv_sum_workspace_bytes(ns)
+            sws = torch.empty(max(sws_bytes, 4), dtype=torch.uint8, device=device) if ns else None
+            rc = lib.nconv_wgrad_reduce_ex(n, layers, wss, nparts, gws, gbs, ns, SP(*[j[0].data_ptr() for j in sums]),
+                                           (_lib.ctypes.c_longlong * max(ns, 1))(*[j[0].numel() for j in sums]),
+                                           SP(*[j[1].data_ptr() for j in sums]), _lib.ptr(sws), sws_bytes,
+                                           _lib.stream_handle(device))
             _lib.check(rc, "nconv_wgrad_reduce")
         self.jobs = []
+        self.sums = []
 
 
 def kernel_plan(spec: LayerSpec, xa, ca, xb, cb, weight, bias, wsum):

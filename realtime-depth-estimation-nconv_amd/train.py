@@ -208,7 +208,11 @@ class GraphedTrainStep:
         if zero:
             self.optimizer.zero_grad(set_to_none=True)
         loss = self.loss_fn(self.model, *self.static_inputs)
-        loss.backward()
+        # d loss / d loss from a persistent tensor made during the warm-up (outside the capture):
+        # loss.backward() would fill a fresh one with a launch of its own every replay
+        if getattr(self, "_seed", None) is None or self._seed.shape != loss.shape:
+            self._seed = torch.ones_like(loss)
+        loss.backward(self._seed)
         if hasattr(self.model, "allreduce_grads"):
             self.model.allreduce_grads()
         self.optimizer.step()

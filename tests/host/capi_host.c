@@ -41,6 +41,7 @@ int main(void) {
     F(nconv_bwd_io, head_gbias); F(nconv_bwd_io, head_nparts); F(nconv_bwd_io, tail); F(nconv_bwd_io, tail_y);
     F(nconv_bwd_io, tail_cout); F(nconv_bwd_io, tail_gy); F(nconv_bwd_io, tail_workspace);
     F(nconv_bwd_io, tail_workspace_bytes); F(nconv_bwd_io, tail_gw); F(nconv_bwd_io, tail_nparts);
+    F(nconv_bwd_io, box_weights); F(nconv_bwd_io, tail_crop0); F(nconv_bwd_io, tail_h); F(nconv_bwd_io, tail_w);
     S(nconv_bn_train);
     F(nconv_bn_train, B); F(nconv_bn_train, C); F(nconv_bn_train, H); F(nconv_bn_train, W); F(nconv_bn_train, x);
     F(nconv_bn_train, gamma); F(nconv_bn_train, beta); F(nconv_bn_train, running_mean);

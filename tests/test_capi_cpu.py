@@ -258,3 +258,50 @@ def test_weight_prologue_validation_is_host_only(nconv_amd):
     for args, msg in cases:
         assert lib.nconv_weight_prologue(*args) == -22, msg
         assert msg in lib.nconv_last_error().decode(), msg
+
+
+def test_train_prologue_validation_is_host_only(nconv_amd):
+    """nconv_train_prologue rejects malformed arguments on the host with -22 before any launch."""
+    lib = nconv_amd._lib.lib()
+    P, I = ctypes.c_void_p, ctypes.c_int
+    p = P(0x1000)
+    w2, s2 = (P * 2)(p, p), (P * 2)(p, p)
+    cout2, fan2, sp2 = (I * 2)(8, 8), (I * 2)(25, 200), (I * 2)(1, 1)
+    w1, s1, cout1, fan1 = (P * 1)(p), (P * 1)(p), (I * 1)(8), (I * 1)(144)
+    pl, up, po = (I * 1)(0), (I * 1)(8), (P * 1)(p)
+    cases = [
+        ((-1, w2, cout2, fan2, sp2, s2, 0, 1, None, 0, None, None, None, None), "negative count"),
+        ((2, None, cout2, fan2, sp2, s2, 0, 1, None, 0, None, None, None, None), "null argument"),
+        ((2, w2, cout2, fan2, sp2, s2, 0, 0, p, 0, None, None, None, None), "two distinct layer indices"),
+        ((2, w2, cout2, (I * 2)(25, 144), sp2, s2, 0, 1, p, 0, None, None, None, None), "must be nconv1"),
+        ((1, w1, cout1, fan1, None, s1, -1, -1, None, 1, None, up, po, None), "null phase argument"),
+        ((1, w1, cout1, fan1, None, s1, -1, -1, None, 1, (I * 1)(3), up, po, None), "bad phase entry"),
+        ((1, w1, cout1, (I * 1)(200), None, s1, -1, -1, None, 1, pl, up, po, None), "8 x 16 x 3 x 3"),
+        ((1, w1, cout1, fan1, None, s1, -1, -1, None, 1, pl, (I * 1)(4), po, None), "up_first must be 0 or 8"),
+        ((2, (P * 2)(p, p), (I * 2)(8, 8), (I * 2)(144, 144), None, s2, -1, -1, None, 2, (I * 2)(1, 1),
+          (I * 2)(8, 8), (P * 2)(p, p), None), "listed twice"),
+    ]
+    for args, msg in cases:
+        assert lib.nconv_train_prologue(*args, None) == -22, msg
+        assert msg in lib.nconv_last_error().decode(), msg
+
+
+def test_wgrad_reduce_ex_validation_is_host_only(nconv_amd):
+    """nconv_wgrad_reduce_ex (layers + plain sums) rejects malformed arguments on the host."""
+    lib = nconv_amd._lib.lib()
+    P = ctypes.c_void_p
+    p = P(0x1000)
+    x, out, n = (P * 1)(p), (P * 1)(p), (ctypes.c_longlong * 1)(100)
+    nbytes = lib.nconv_sum_workspace_bytes(1)
+    assert nbytes == 1024 * 4 and lib.nconv_sum_workspace_bytes(0) == 0
+    cases = [
+        ((0, None, None, None, None, None, 0, None, None, None, None, 0), "1..16 layers and sums"),
+        ((0, None, None, None, None, None, 17, x, n, out, p, 17 * nbytes), "1..16 layers and sums"),
+        ((0, None, None, None, None, None, 1, None, n, out, p, nbytes), "null sum array"),
+        ((0, None, None, None, None, None, 1, x, n, out, p, nbytes - 4), "sum workspace too small"),
+        ((0, None, None, None, None, None, 1, x, (ctypes.c_longlong * 1)(-1), out, p, nbytes), "bad sum entry"),
+        ((0, None, None, None, None, None, 1, (P * 1)(None), n, out, p, nbytes), "bad sum entry"),
+    ]
+    for args, msg in cases:
+        assert lib.nconv_wgrad_reduce_ex(*args, None) == -22, msg
+        assert msg in lib.nconv_last_error().decode(), msg

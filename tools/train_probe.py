@@ -24,8 +24,11 @@ def main():
         del args[i:i + 2]
     for a in args:
         k, v = a.split("=")
-        assert hasattr(m.dnet, k), k
-        setattr(m.dnet, k, bool(int(v)))
+        obj = m.dnet
+        if k.startswith("DNET."):  # a DNET class attribute (merged_prologue, crop_in_tail, ...)
+            obj, k = m.DNET, k[5:]
+        assert hasattr(obj, k), k
+        setattr(obj, k, bool(int(v)))
     dev = torch.device("cuda:0")
     step = bench.make_train_step(m, dev, 8, 352, 1216, 0, graph=True)
     for _ in range(3):
