@@ -140,7 +140,7 @@ class DNETFn(torch.autograd.Function):
             side.wait_stream(cur)
             tail, head = kw.pop("tail", None), kw.pop("head", None)
             layer_backward(spec, inputs, y, co, gy, gco, gin, None, None, defer=red, head=head,
-                           tail=None if tail is None else tail[:-1] + (None,), **kw)
+                           tail=None if tail is None else tail[:7] + (None,) + tail[8:], **kw)  # (no gw7)
             with torch.cuda.stream(side):
                 layer_backward(spec, inputs, y, co, gy, gco, (None,) * 4, gw_, gb_, defer=red, tail=tail, **kw)
 
