@@ -395,14 +395,19 @@ __device__ __forceinline__ void head_weights_unit(const float* __restrict__ w1, 
         return;
     }
     const int qh = blk / 9, qw = blk % 9, o = lane >> 3, i = lane & 7;
+    // all 25 (kh, kw) unrolled, the valid ones accumulated in (kh, kw) order by explicit fp64 FMAs:
+    // every load of the unit is issued up front (a loop with data-dependent bounds waited on each)
     double si = 0.0;
+#pragma unroll
     for (int kh = 0; kh < 5; ++kh) {
         const int kh1 = qh - kh;
-        if (kh1 < 0 || kh1 > 4) continue;
+#pragma unroll
         for (int kw = 0; kw < 5; ++kw) {
             const int kw1 = qw - kw;
-            if (kw1 < 0 || kw1 > 4) continue;
-            si += (double)w2[((o * 8 + i) * 5 + kh) * 5 + kw] * (double)w1[(i * 5 + kh1) * 5 + kw1];
+            const bool v = kh1 >= 0 && kh1 <= 4 && kw1 >= 0 && kw1 <= 4;
+            const double a = (double)w2[((o * 8 + i) * 5 + kh) * 5 + kw];
+            const double b = (double)w1[v ? (i * 5 + kh1) * 5 + kw1 : 0];
+            si = v ? __builtin_fma(a, b, si) : si;
         }
     }
     si /= (double)s1i;

@@ -4,8 +4,8 @@
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 timeout -k 10 900 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu \
-    tests/test_gpu_train_launches.py tests/test_gpu_dnet.py tests/test_gpu_golden.py tests/test_gpu_fused_bwd.py \
-    tests/test_gpu_dp.py tests/test_gpu_train_graph.py > gpurun_out/r5_launch_pytest.log 2>&1
+    ${R5_TESTS:-tests/test_gpu_train_launches.py tests/test_gpu_dnet.py tests/test_gpu_golden.py tests/test_gpu_fused_bwd.py} \
+    ${R5_TESTS2-tests/test_gpu_dp.py tests/test_gpu_train_graph.py} > gpurun_out/r5_launch_pytest.log 2>&1
 rc=$?; tail -3 gpurun_out/r5_launch_pytest.log; [ $rc -eq 0 ] || exit $rc
 for a in "" "DNET.merged_prologue=0 DNET.crop_in_tail=0" "" "DNET.merged_prologue=0 DNET.crop_in_tail=0"; do
     timeout -k 10 120 python3 tools/train_probe.py $a --steps 50 || exit $?
