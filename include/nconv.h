@@ -147,16 +147,20 @@ int nconv_weight_prologue(int n, float* const* weights, const int* couts, const 
  * backward box-weight builds -- become one). Layer i (weights[i], couts[i] x fan_ins[i]) gets
  * EnforcePos's softplus in place when softplus[i] (softplus may be NULL: none) and its normalisers
  * in wsums[i]. With w21 != NULL, layers head1 / head2 are nconv1 (8 x 1 x 5 x 5) and nconv2 (8 x 8 x
- * 5 x 5) and w21 receives the exact head's weights (nconv_head_weights, NCONV_HEAD_WEIGHTS_FLOATS).
+ * 5 x 5) and w21 receives the exact head's weights (nconv_head_weights, NCONV_HEAD_WEIGHTS_FLOATS);
+ * `sync` is then a device counter that is 0 before the call and is left 0 by it (the head's
+ * workgroups write nconv1 / nconv2 back once all of them have staged them: one counter per stream
+ * that runs this concurrently).
  * Phase layer k is layer phase_layers[k] (8 x 16 x 3 x 3, upsampled channels from phase_up_first[k]
  * = 0 or 8): wphases[k] receives its phase weights (nconv_phase_weights) and, when wboxes and
  * wboxes[k] are non-NULL, wboxes[k] its 1,024 box weights for the phase-form input gradient
  * (nconv_bwd_io.box_weights). Each output is bitwise what the separate calls write after
- * nconv_weight_prep. Each layer is read by one workgroup, which applies the softplus while staging
- * and writes it back, so the roles need no order between them. Returns 0 or -EINVAL. */
+ * nconv_weight_prep. Every role applies the softplus while staging; a layer is written back by its
+ * only reader, or by the last head workgroup. Returns 0 or -EINVAL. */
 int nconv_train_prologue(int n, float* const* weights, const int* couts, const int* fan_ins, const int* softplus,
-                         float* const* wsums, int head1, int head2, float* w21, int nphase, const int* phase_layers,
-                         const int* phase_up_first, float* const* wphases, float* const* wboxes, void* stream);
+                         float* const* wsums, int head1, int head2, float* w21, unsigned int* sync, int nphase,
+                         const int* phase_layers, const int* phase_up_first, float* const* wphases,
+                         float* const* wboxes, void* stream);
 
 /* Forward of one NConv2d with fused input glue.
  * Replaces models/step1.py:119-147 (2x F.conv2d, mul, div, bias add, confidence normalisation)

@@ -172,8 +172,8 @@ def _declare(lib):
     lib.nconv_sum_workspace_bytes.restype = ctypes.c_size_t
     lib.nconv_sum_workspace_bytes.argtypes = [ctypes.c_int]
     lib.nconv_train_prologue.restype = ctypes.c_int
-    lib.nconv_train_prologue.argtypes = [ctypes.c_int, P, P, P, P, P, ctypes.c_int, ctypes.c_int, P, ctypes.c_int,
-                                         P, P, P, P, P]
+    lib.nconv_train_prologue.argtypes = [ctypes.c_int, P, P, P, P, P, ctypes.c_int, ctypes.c_int, P, P,
+                                         ctypes.c_int, P, P, P, P, P]
     I = ctypes.c_int
     lib.nconv_dense_packed_floats.restype = ctypes.c_size_t
     lib.nconv_dense_packed_floats.argtypes = [I, I, I]

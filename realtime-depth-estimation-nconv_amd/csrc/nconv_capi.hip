@@ -242,8 +242,9 @@ int nconv_phase_weights(int n, const float* const* weights, const int* cins, con
 }
 
 int nconv_train_prologue(int n, float* const* weights, const int* couts, const int* fan_ins, const int* softplus,
-                         float* const* wsums, int head1, int head2, float* w21, int nphase, const int* phase_layers,
-                         const int* phase_up_first, float* const* wphases, float* const* wboxes, void* stream) {
+                         float* const* wsums, int head1, int head2, float* w21, unsigned int* sync, int nphase,
+                         const int* phase_layers, const int* phase_up_first, float* const* wphases,
+                         float* const* wboxes, void* stream) {
     const char* fn = "nconv_train_prologue";
     if (n < 0 || nphase < 0) return fail(-22, fn, "negative count");
     if (n > 0 && (!weights || !couts || !fan_ins || !wsums)) return fail(-22, fn, "null argument");
@@ -254,6 +255,7 @@ int nconv_train_prologue(int n, float* const* weights, const int* couts, const i
             return fail(-22, fn, "head layers must be two distinct layer indices");
         if (couts[head1] != 8 || fan_ins[head1] != 25 || couts[head2] != 8 || fan_ins[head2] != 200)
             return fail(-22, fn, "head layers must be nconv1 (8 x 1 x 5 x 5) and nconv2 (8 x 8 x 5 x 5)");
+        if (!sync) return fail(-22, fn, "head weights need the sync counter");
     }
     if (nphase > 0 && (!phase_layers || !phase_up_first || !wphases)) return fail(-22, fn, "null phase argument");
     for (int k = 0; k < nphase; ++k) {
@@ -266,8 +268,9 @@ int nconv_train_prologue(int n, float* const* weights, const int* couts, const i
             if (phase_layers[j] == i) return fail(-22, fn, "a phase layer is listed twice");
     }
     const char* why = nullptr;
-    int rc = nconv::launch_train_prologue(n, weights, couts, fan_ins, softplus, wsums, head1, head2, w21, nphase,
-                                          phase_layers, phase_up_first, wphases, wboxes, (hipStream_t)stream, &why);
+    int rc = nconv::launch_train_prologue(n, weights, couts, fan_ins, softplus, wsums, head1, head2, w21, sync,
+                                          nphase, phase_layers, phase_up_first, wphases, wboxes, (hipStream_t)stream,
+                                          &why);
     return rc ? fail(rc, fn, why) : 0;
 }
 

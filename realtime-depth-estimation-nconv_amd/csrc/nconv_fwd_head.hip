@@ -464,63 +464,71 @@ __global__ __launch_bounds__(kPrepThreads) void weight_prologue(PrepArgs prep, i
 }
 
 // The training weight prologue in one launch (nconv_train_prologue): EnforcePos in place and every
-// weight-only input of the training pass formed from the transformed weights. A layer read by
-// several roles would need an order between a writer and its readers, so each layer has exactly
-// one block that reads it: blocks [0, nprep) the other layers (prep_block: softplus in place, then
-// the normalisers), then the head block (nconv1 + nconv2: both staged into LDS through
-// enforce_pos, written back, their normalisers by prep_block's wave sums over the staged rows,
-// then the 83 head units over its 8 waves), then one block per phase layer (staged the same way;
-// normalisers, phase weights, box weights). Every output is bitwise what weight_prep +
-// head_weights + phase_weights + box_weights write. 512 threads per block (1024 caps a lane at
-// 128 VGPRs, and the head units' fp64 sums then spill); the prep and phase roles use the first 256
-// (the others leave before any barrier).
-constexpr int kTrainProThreads = 512;
-__global__ __launch_bounds__(kTrainProThreads) void train_prologue(PrepArgs prep, int nprep, float* w1, float* w2,
-                                                                   float* s1, float* s2, int sp1, int sp2,
-                                                                   float* w21, TrainPhaseArgs ph, int nphase) {
+// weight-only input of the training pass formed from the transformed weights. Blocks [0, nprep):
+// the layers no other role reads (prep_block: softplus in place, then the normalisers). Then
+// kTrainHeadBlocks head blocks, four head units each (a wave per unit): each stages nconv1's and
+// nconv2's weights into LDS through enforce_pos and works from there; the writes of the
+// transformed weights (and the normalisers) wait for every head block's staging reads, so the
+// block that finishes last (a counter in *sync, left at 0 for the next call) writes them. Then
+// one block per phase layer, the layer's only reader: staged the same way, written back, its
+// normalisers, phase weights and box weights. Every output is bitwise what weight_prep +
+// head_weights + phase_weights + box_weights write (the same device functions on the same values).
+constexpr int kTrainHeadBlocks = (kHeadUnits + 3) / 4;
+__global__ __launch_bounds__(kPrepThreads) void train_prologue(PrepArgs prep, int nprep, float* w1, float* w2,
+                                                               float* s1, float* s2, int sp1, int sp2,
+                                                               float* w21, unsigned* sync, TrainPhaseArgs ph,
+                                                               int nphase) {
     __shared__ float lw[1800 + 8];  // head: W1 (200), W2 (1600), s1 (8); phase: W (1152)
+    __shared__ int last;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     int blk = blockIdx.x;
     if (blk < nprep) {
-        if (tid < kPrepThreads) prep_block(prep.w[blk], prep.s[blk], prep.cout[blk], prep.fan_in[blk], prep.softplus[blk]);
+        prep_block(prep.w[blk], prep.s[blk], prep.cout[blk], prep.fan_in[blk], prep.softplus[blk]);
         return;
     }
     blk -= nprep;
     if (w21) {
-        if (blk == 0) {
-            for (int e = tid; e < 1800; e += kTrainProThreads) {
+        if (blk < kTrainHeadBlocks) {
+            for (int e = tid; e < 1800; e += kPrepThreads) {
                 const bool one = e < 200;
                 const float v = one ? w1[e] : w2[e - 200];
                 lw[e] = (one ? sp1 : sp2) ? enforce_pos(v) : v;
             }
             __syncthreads();
-            for (int e = tid; e < 1800; e += kTrainProThreads) {
+            for (int r = wave; r < 8; r += kPrepThreads / 64) {  // s1: prep_block's wave sums
+                const float v = row_sum_wave(lw + r * 25, 25, lane);
+                if (lane == 0) lw[1800 + r] = v;
+            }
+            __syncthreads();
+            const int u = 4 * blk + wave;
+            if (u < kHeadUnits) head_weights_unit(lw, lw[1800 + (lane & 7)], lw + 200, w21, u, lane);
+            // every head block's reads of w1 / w2 are done before it counts itself
+            __syncthreads();
+            if (tid == 0) {
+                __threadfence();
+                last = atomicAdd(sync, 1u) == (unsigned)(kTrainHeadBlocks - 1);
+            }
+            __syncthreads();
+            if (!last) return;
+            __threadfence();
+            for (int e = tid; e < 1800; e += kPrepThreads) {
                 if (e < 200) {
                     if (sp1) w1[e] = lw[e];
                 } else if (sp2) {
                     w2[e - 200] = lw[e];
                 }
             }
-            for (int r = wave; r < 16; r += kTrainProThreads / 64) {  // s1 (8 rows of 25), s2 (8 of 200)
-                const float v = r < 8 ? row_sum_wave(lw + r * 25, 25, lane)
-                                      : row_sum_wave(lw + 200 + (r - 8) * 200, 200, lane);
-                if (lane == 0) {
-                    if (r < 8) {
-                        s1[r] = v;
-                        lw[1800 + r] = v;
-                    } else {
-                        s2[r - 8] = v;
-                    }
-                }
+            if (tid < 8) s1[tid] = lw[1800 + tid];
+            for (int r = wave; r < 8; r += kPrepThreads / 64) {  // s2 (rows of 200)
+                const float v = row_sum_wave(lw + 200 + r * 200, 200, lane);
+                if (lane == 0) s2[r] = v;
             }
-            __syncthreads();
-            const float s1i = lw[1800 + (lane & 7)];
-            for (int u = wave; u < kHeadUnits; u += kTrainProThreads / 64) head_weights_unit(lw, s1i, lw + 200, w21, u, lane);
+            if (tid == 0) atomicExch(sync, 0u);
             return;
         }
-        --blk;
+        blk -= kTrainHeadBlocks;
     }
-    if (blk < nphase && tid < kPrepThreads) {
+    if (blk < nphase) {
         float* W = ph.w[blk];
         const int sp = ph.sp[blk];
         for (int e = tid; e < 1152; e += kPrepThreads) lw[e] = sp ? enforce_pos(W[e]) : W[e];
@@ -598,9 +606,9 @@ int launch_head_weights(const float* w1, const float* s1, const float* w2, float
 }
 
 int launch_train_prologue(int n, float* const* w, const int* cout, const int* fan_in, const int* sp,
-                          float* const* s, int head1, int head2, float* w21, int nphase, const int* players,
-                          const int* pup_first, float* const* pout, float* const* pbox, hipStream_t st,
-                          const char** why) {
+                          float* const* s, int head1, int head2, float* w21, unsigned* sync, int nphase,
+                          const int* players, const int* pup_first, float* const* pout, float* const* pbox,
+                          hipStream_t st, const char** why) {
     if (n < 0 || n > PrepArgs::kMax || nphase < 0 || nphase > TrainPhaseArgs::kMax) {
         *why = "too many layers for one nconv_train_prologue launch (max 32 layers, 8 phase layers)";
         return -22;
@@ -634,10 +642,10 @@ int launch_train_prologue(int n, float* const* w, const int* cout, const int* fa
         w1 = w[head1], w2 = w[head2], s1 = s[head1], s2 = s[head2];
         sp1 = sp ? sp[head1] : 0, sp2 = sp ? sp[head2] : 0;
     }
-    const int blocks = nprep + (w21 ? 1 : 0) + nphase;
+    const int blocks = nprep + (w21 ? kTrainHeadBlocks : 0) + nphase;
     if (blocks == 0) return 0;
-    hipLaunchKernelGGL(train_prologue, dim3(blocks), dim3(kTrainProThreads), 0, st, a, nprep, w1, w2, s1, s2, sp1, sp2,
-                       w21, p, nphase);
+    hipLaunchKernelGGL(train_prologue, dim3(blocks), dim3(kPrepThreads), 0, st, a, nprep, w1, w2, s1, s2, sp1, sp2,
+                       w21, sync, p, nphase);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         *why = hipGetErrorString(e);

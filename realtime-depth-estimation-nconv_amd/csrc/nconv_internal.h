@@ -140,9 +140,9 @@ int launch_weight_prologue(int n, float* const* w, const int* cout, const int* f
                            const int* pcin, const int* pup_first, float* const* pout, hipStream_t st,
                            const char** why);
 int launch_train_prologue(int n, float* const* w, const int* cout, const int* fan_in, const int* sp,
-                          float* const* s, int head1, int head2, float* w21, int nphase, const int* players,
-                          const int* pup_first, float* const* pout, float* const* pbox, hipStream_t st,
-                          const char** why);
+                          float* const* s, int head1, int head2, float* w21, unsigned* sync, int nphase,
+                          const int* players, const int* pup_first, float* const* pout, float* const* pbox,
+                          hipStream_t st, const char** why);
 int launch_head_weights(const float* w1, const float* s1, const float* w2, float* out, hipStream_t st,
                         const char** why);
 int launch_fwd_tail(const LayerDev& d, const TailArgs& t, float* out, hipStream_t st, const char** why);

@@ -377,7 +377,7 @@ class DNET(nn.Module):
         head, w21 = None, None
         if FUSE_HEAD_FWD and self._head_shapes(layers[0], layers[1]):
             w21 = torch.empty(nconv.HEAD_WEIGHTS_FLOATS, device=dev, dtype=torch.float32)
-            head = (0, 1, w21)
+            head = (0, 1, w21, nconv.sync_counter(dev))
         phase, wph, wbox = None, None, None
         ls = (self.nconv4, self.nconv5, self.nconv6)
         if self.phase_upcat and all(m.weight.shape[0] == 8 and m.weight.shape[1] == 16 and

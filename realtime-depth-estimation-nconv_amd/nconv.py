@@ -169,12 +169,15 @@ def weight_prologue(weights, wsums, head=None, phase=None):
 def train_prologue(weights, softplus, wsums, head=None, phase=None):
     """nconv_train_prologue: the training pass's weight prologue in one launch -- EnforcePos's
     softplus in place on the layers flagged in `softplus`, every layer's normalisers into wsums, and
-    from the transformed weights: head = (i1, i2, w21) the exact head's weights of layers i1 (nconv1)
-    / i2 (nconv2), or None; phase = (layer indices, up_first, phase outs, box outs or None) as
+    from the transformed weights: head = (i1, i2, w21, sync) the exact head's weights of layers i1
+    (nconv1) / i2 (nconv2) and a zero int32 device counter the call leaves at zero (sync_counter), or
+    None; phase = (layer indices, up_first, phase outs, box outs or None) as
     phase_weights' outputs plus the backward's box weights (BOX_WEIGHT_FLOATS each). Bitwise what
     weight_prep + head_weights + phase_weights + the backward's box-weight builds write."""
     n = len(weights)
-    i1, i2, w21 = head if head is not None else (-1, -1, None)
+    i1, i2, w21, sync = head if head is not None else (-1, -1, None, None)
+    if w21 is not None and (sync is None or sync.dtype != torch.int32 or sync.numel() < 1):
+        raise ValueError("the head weights need a zero int32 sync counter (sync_counter)")
     pl, pup, pout, pbox = phase if phase is not None else ([], [], [], None)
     if w21 is not None and (w21.numel() < HEAD_WEIGHTS_FLOATS or not w21.is_contiguous() or
                             w21.dtype != torch.float32):
@@ -187,11 +190,24 @@ def train_prologue(weights, softplus, wsums, head=None, phase=None):
     rc = _lib.lib().nconv_train_prologue(
         n, (P * max(n, 1))(*[w.data_ptr() for w in weights]), (I * max(n, 1))(*[w.shape[0] for w in weights]),
         (I * max(n, 1))(*[w[0].numel() for w in weights]), (I * max(n, 1))(*[int(bool(v)) for v in softplus]),
-        (P * max(n, 1))(*[s.data_ptr() for s in wsums]), i1, i2, _lib.ptr(w21), m, (I * max(m, 1))(*pl),
+        (P * max(n, 1))(*[s.data_ptr() for s in wsums]), i1, i2, _lib.ptr(w21), _lib.ptr(sync), m,
+        (I * max(m, 1))(*pl),
         (I * max(m, 1))(*pup), (P * max(m, 1))(*[o.data_ptr() for o in pout]),
         (P * max(m, 1))(*[o.data_ptr() for o in pbox]) if pbox is not None else None,
         _lib.stream_handle(weights[0].device))
     _lib.check(rc, "nconv_train_prologue")
+
+
+_SYNC = {}
+
+
+def sync_counter(device):
+    """The device's zero int32 counter for train_prologue (made once, zero-filled; every call
+    leaves it at zero)."""
+    key = torch.device(device).index
+    if key not in _SYNC:
+        _SYNC[key] = torch.zeros(1, dtype=torch.int32, device=device)
+    return _SYNC[key]
 
 
 BOX_WEIGHT_FLOATS = 1024  # (8, 8, 4, 4) box weights of an exactly-2x UPCAT layer (nconv_bwd_io.box_weights)

@@ -269,16 +269,18 @@ def test_train_prologue_validation_is_host_only(nconv_amd):
     cout2, fan2, sp2 = (I * 2)(8, 8), (I * 2)(25, 200), (I * 2)(1, 1)
     w1, s1, cout1, fan1 = (P * 1)(p), (P * 1)(p), (I * 1)(8), (I * 1)(144)
     pl, up, po = (I * 1)(0), (I * 1)(8), (P * 1)(p)
+    SYNC = p
     cases = [
-        ((-1, w2, cout2, fan2, sp2, s2, 0, 1, None, 0, None, None, None, None), "negative count"),
-        ((2, None, cout2, fan2, sp2, s2, 0, 1, None, 0, None, None, None, None), "null argument"),
-        ((2, w2, cout2, fan2, sp2, s2, 0, 0, p, 0, None, None, None, None), "two distinct layer indices"),
-        ((2, w2, cout2, (I * 2)(25, 144), sp2, s2, 0, 1, p, 0, None, None, None, None), "must be nconv1"),
-        ((1, w1, cout1, fan1, None, s1, -1, -1, None, 1, None, up, po, None), "null phase argument"),
-        ((1, w1, cout1, fan1, None, s1, -1, -1, None, 1, (I * 1)(3), up, po, None), "bad phase entry"),
-        ((1, w1, cout1, (I * 1)(200), None, s1, -1, -1, None, 1, pl, up, po, None), "8 x 16 x 3 x 3"),
-        ((1, w1, cout1, fan1, None, s1, -1, -1, None, 1, pl, (I * 1)(4), po, None), "up_first must be 0 or 8"),
-        ((2, (P * 2)(p, p), (I * 2)(8, 8), (I * 2)(144, 144), None, s2, -1, -1, None, 2, (I * 2)(1, 1),
+        ((-1, w2, cout2, fan2, sp2, s2, 0, 1, None, SYNC, 0, None, None, None, None), "negative count"),
+        ((2, None, cout2, fan2, sp2, s2, 0, 1, None, SYNC, 0, None, None, None, None), "null argument"),
+        ((2, w2, cout2, fan2, sp2, s2, 0, 0, p, SYNC, 0, None, None, None, None), "two distinct layer indices"),
+        ((2, w2, cout2, (I * 2)(25, 144), sp2, s2, 0, 1, p, SYNC, 0, None, None, None, None), "must be nconv1"),
+        ((2, w2, cout2, fan2, sp2, s2, 0, 1, p, None, 0, None, None, None, None), "need the sync counter"),
+        ((1, w1, cout1, fan1, None, s1, -1, -1, None, SYNC, 1, None, up, po, None), "null phase argument"),
+        ((1, w1, cout1, fan1, None, s1, -1, -1, None, SYNC, 1, (I * 1)(3), up, po, None), "bad phase entry"),
+        ((1, w1, cout1, (I * 1)(200), None, s1, -1, -1, None, SYNC, 1, pl, up, po, None), "8 x 16 x 3 x 3"),
+        ((1, w1, cout1, fan1, None, s1, -1, -1, None, SYNC, 1, pl, (I * 1)(4), po, None), "up_first must be 0 or 8"),
+        ((2, (P * 2)(p, p), (I * 2)(8, 8), (I * 2)(144, 144), None, s2, -1, -1, None, SYNC, 2, (I * 2)(1, 1),
           (I * 2)(8, 8), (P * 2)(p, p), None), "listed twice"),
     ]
     for args, msg in cases:

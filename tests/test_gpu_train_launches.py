@@ -70,7 +70,8 @@ def test_train_prologue_bitwise_separate_launches(nconv_amd, gpu):
     N.weight_prep([wa[2], wa[6]], [False, False], [sa[2], sa[6]])
     pa[1] = torch.empty(1024, device=gpu)
     N.phase_weights([wa[6]], [8], [pa[1]])
-    N.train_prologue(wb, sp, sb, head=(0, 1, hb), phase=([5, 6, 7], [8, 8, 0], pb, bb))
+    sync = torch.zeros(1, dtype=torch.int32, device=gpu)
+    N.train_prologue(wb, sp, sb, head=(0, 1, hb, sync), phase=([5, 6, 7], [8, 8, 0], pb, bb))
     torch.cuda.synchronize()
     for k, (a, b) in enumerate(zip(wa, wb)):
         assert torch.equal(a.view(torch.int32), b.view(torch.int32)), k
@@ -81,6 +82,16 @@ def test_train_prologue_bitwise_separate_launches(nconv_amd, gpu):
         assert torch.equal(a, b)
     for k, (li, up) in enumerate(((5, 8), (6, 8), (7, 0))):
         assert torch.equal(bb[k].cpu(), _box_ref(wb[li], up)), k
+    assert sync.item() == 0  # (left at zero for the next call)
+    # repeated calls on the same counter (as graph replays run them): same outputs each time
+    hc = torch.full_like(hb, float("nan"))
+    for _ in range(3):
+        N.train_prologue([w.clone() for w in wb], [False] * 9, [torch.empty_like(v) for v in sb],
+                         head=(0, 1, hc, sync))
+    torch.cuda.synchronize()
+    assert sync.item() == 0
+    hd = N.head_weights(sp1, sp2, S, wb[0], l1.bias.detach(), sb[0], wb[1], l2.bias.detach(), sb[1])
+    assert torch.equal(hc.view(torch.int32), hd.view(torch.int32))
 
 
 def test_train_prologue_without_head_or_phase(nconv_amd, gpu):
