@@ -466,15 +466,17 @@ __global__ __launch_bounds__(kPrepThreads) void weight_prologue(PrepArgs prep, i
 // The training weight prologue in one launch (nconv_train_prologue): EnforcePos in place and every
 // weight-only input of the training pass formed from the transformed weights. Blocks [0, nprep):
 // the layers no other role reads (prep_block: softplus in place, then the normalisers). Then
-// kTrainHeadBlocks head blocks, four head units each (a wave per unit): each stages nconv1's and
+// kTrainHeadBlocks head blocks, eight head units each (a wave per unit): each stages nconv1's and
 // nconv2's weights into LDS through enforce_pos and works from there; the writes of the
 // transformed weights (and the normalisers) wait for every head block's staging reads, so the
 // block that finishes last (a counter in *sync, left at 0 for the next call) writes them. Then
 // one block per phase layer, the layer's only reader: staged the same way, written back, its
 // normalisers, phase weights and box weights. Every output is bitwise what weight_prep +
 // head_weights + phase_weights + box_weights write (the same device functions on the same values).
-constexpr int kTrainHeadBlocks = (kHeadUnits + 3) / 4;
-__global__ __launch_bounds__(kPrepThreads) void train_prologue(PrepArgs prep, int nprep, float* w1, float* w2,
+// 512 threads per workgroup: eight head units per head workgroup; the prep and phase roles use
+// the first 256 (the others leave before any barrier).
+constexpr int kTrainProThreads = 512, kTrainHeadBlocks = (kHeadUnits + 7) / 8;
+__global__ __launch_bounds__(kTrainProThreads) void train_prologue(PrepArgs prep, int nprep, float* w1, float* w2,
                                                                float* s1, float* s2, int sp1, int sp2,
                                                                float* w21, unsigned* sync, TrainPhaseArgs ph,
                                                                int nphase) {
@@ -483,24 +485,24 @@ __global__ __launch_bounds__(kPrepThreads) void train_prologue(PrepArgs prep, in
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     int blk = blockIdx.x;
     if (blk < nprep) {
-        prep_block(prep.w[blk], prep.s[blk], prep.cout[blk], prep.fan_in[blk], prep.softplus[blk]);
+        if (tid < kPrepThreads) prep_block(prep.w[blk], prep.s[blk], prep.cout[blk], prep.fan_in[blk], prep.softplus[blk]);
         return;
     }
     blk -= nprep;
     if (w21) {
         if (blk < kTrainHeadBlocks) {
-            for (int e = tid; e < 1800; e += kPrepThreads) {
+            for (int e = tid; e < 1800; e += kTrainProThreads) {
                 const bool one = e < 200;
                 const float v = one ? w1[e] : w2[e - 200];
                 lw[e] = (one ? sp1 : sp2) ? enforce_pos(v) : v;
             }
             __syncthreads();
-            for (int r = wave; r < 8; r += kPrepThreads / 64) {  // s1: prep_block's wave sums
-                const float v = row_sum_wave(lw + r * 25, 25, lane);
-                if (lane == 0) lw[1800 + r] = v;
+            {  // s1: prep_block's wave sums (a wave per row)
+                const float v = row_sum_wave(lw + wave * 25, 25, lane);
+                if (lane == 0) lw[1800 + wave] = v;
             }
             __syncthreads();
-            const int u = 4 * blk + wave;
+            const int u = 8 * blk + wave;
             if (u < kHeadUnits) head_weights_unit(lw, lw[1800 + (lane & 7)], lw + 200, w21, u, lane);
             // every head block's reads of w1 / w2 are done before it counts itself
             __syncthreads();
@@ -511,7 +513,7 @@ __global__ __launch_bounds__(kPrepThreads) void train_prologue(PrepArgs prep, in
             __syncthreads();
             if (!last) return;
             __threadfence();
-            for (int e = tid; e < 1800; e += kPrepThreads) {
+            for (int e = tid; e < 1800; e += kTrainProThreads) {
                 if (e < 200) {
                     if (sp1) w1[e] = lw[e];
                 } else if (sp2) {
@@ -519,16 +521,16 @@ __global__ __launch_bounds__(kPrepThreads) void train_prologue(PrepArgs prep, in
                 }
             }
             if (tid < 8) s1[tid] = lw[1800 + tid];
-            for (int r = wave; r < 8; r += kPrepThreads / 64) {  // s2 (rows of 200)
-                const float v = row_sum_wave(lw + 200 + r * 200, 200, lane);
-                if (lane == 0) s2[r] = v;
+            {  // s2 (rows of 200)
+                const float v = row_sum_wave(lw + 200 + wave * 200, 200, lane);
+                if (lane == 0) s2[wave] = v;
             }
             if (tid == 0) atomicExch(sync, 0u);
             return;
         }
         blk -= kTrainHeadBlocks;
     }
-    if (blk < nphase) {
+    if (blk < nphase && tid < kPrepThreads) {
         float* W = ph.w[blk];
         const int sp = ph.sp[blk];
         for (int e = tid; e < 1152; e += kPrepThreads) lw[e] = sp ? enforce_pos(W[e]) : W[e];
@@ -644,7 +646,8 @@ int launch_train_prologue(int n, float* const* w, const int* cout, const int* fa
     }
     const int blocks = nprep + (w21 ? kTrainHeadBlocks : 0) + nphase;
     if (blocks == 0) return 0;
-    hipLaunchKernelGGL(train_prologue, dim3(blocks), dim3(kPrepThreads), 0, st, a, nprep, w1, w2, s1, s2, sp1, sp2,
+    static_assert(kTrainProThreads / 64 == 8, "a wave per nconv1 / nconv2 row");
+    hipLaunchKernelGGL(train_prologue, dim3(blocks), dim3(kTrainProThreads), 0, st, a, nprep, w1, w2, s1, s2, sp1, sp2,
                        w21, sync, p, nphase);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
