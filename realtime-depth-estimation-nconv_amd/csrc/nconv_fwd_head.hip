@@ -450,11 +450,19 @@ __global__ __launch_bounds__(kPrepThreads) void weight_prologue(PrepArgs prep, i
     if (blk < nhead) {
         const int lane = threadIdx.x & 63, unit = 4 * blk + (threadIdx.x >> 6);
         if (unit >= kHeadUnits) return;
+        // s1 as row_sum_wave sums each row (lane-strided terms from +0, then the butterfly), the
+        // eight rows' loads issued together (one row after another waited on each)
+        float v[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) v[r] = lane < 25 ? w1[r * 25 + lane] : 0.f;
         float s1i = 0.f;
-#pragma unroll 1
+#pragma unroll
         for (int r = 0; r < 8; ++r) {
-            const float v = row_sum_wave(w1 + r * 25, 25, lane);
-            if ((lane & 7) == r) s1i = v;
+            float sr = 0.f;
+            if (lane < 25) sr += v[r];
+#pragma unroll
+            for (int m = 32; m > 0; m >>= 1) sr += __shfl_xor(sr, m);
+            if ((lane & 7) == r) s1i = sr;
         }
         head_weights_unit(w1, s1i, w2, w21, unit, lane);
         return;

@@ -23,7 +23,16 @@ struct PrepArgs {
 // a fixed-order xor butterfly (every lane ends with the same value).
 __device__ __forceinline__ float row_sum_wave(const float* wr, int fan, int lane) {
     float s = 0.f;
-    for (int i = lane; i < fan; i += 64) s += wr[i];
+    if (fan <= 256) {  // (every DNET layer) the lane's loads issued together, added in the same order
+        float v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = wr[lane + 64 * k < fan ? lane + 64 * k : 0];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (lane + 64 * k < fan) s += v[k];
+    } else {
+        for (int i = lane; i < fan; i += 64) s += wr[i];
+    }
 #pragma unroll
     for (int m = 32; m > 0; m >>= 1) s += __shfl_xor(s, m);
     return s;

@@ -45,6 +45,8 @@ def main():
         "prep only (9 layers)": lambda: N.train_prologue(ws, nosp, s),
         "head only": lambda: N.train_prologue(ws[:2], nosp[:2], s[:2], head=(0, 1, w21, N.sync_counter(dev))),
         "phase only": lambda: N.train_prologue(ws[5:8], nosp[:3], s[5:8], phase=([0, 1, 2], [8, 8, 0], ph, bx)),
+        "eval weight_prologue": lambda: N.weight_prologue(ws, s, head=(ws[0], ws[1], w21),
+                                                          phase=([ws[5], ws[6], ws[7]], [8, 8, 0], ph)),
         "weight_prep (9)": lambda: N.weight_prep(ws, nosp, s),
         "head_weights": lambda: N.head_weights(layers[0].spec(m._lib.THRESH, 0.01), layers[1].spec(),
                                                torch.zeros(1, 1, 32, 32, device=dev), ws[0], layers[0].bias, s[0],
