@@ -411,22 +411,33 @@ class DNET(nn.Module):
     # bitwise the three separate launches); False: the separate launches.
     merged_prologue = True
 
-    def _eval_prologue(self, layers, S):
-        """(wsums, phase weights or None, head weights or None) from one nconv_weight_prologue
-        launch, or None where the separate path must run: merged_prologue off, a layer in training
-        mode (EnforcePos then rewrites the weights first), a forward pre-hook other than this
-        package's EnforcePos, or weights that are not contiguous fp32 device tensors."""
+    # Inference split over streams (inference_streams > 1): each stream builds its own copy of the
+    # weight prologue (one small launch), so the side streams start with the main one instead of
+    # waiting for its prologue across streams; False: one shared prologue before the fork.
+    stream_prologue = True
+
+    def _eval_prologue_ok(self, layers):
+        """Whether the one-launch eval prologue applies (see _eval_prologue)."""
         if not self.merged_prologue:
-            return None
+            return False
         for m in layers:
             hooks = list(m._forward_pre_hooks.values())
             ours = len(hooks) == 1 and isinstance(hooks[0], EnforcePos) and hooks[0].name == "weight" \
                 and hooks[0].pos_fn.lower() == "softplus"
             if m.training or not (len(hooks) == 0 or ours):
-                return None
+                return False
             w = m.weight
             if not (w.is_cuda and w.dtype == torch.float32 and w.is_contiguous()):
-                return None
+                return False
+        return True
+
+    def _eval_prologue(self, layers, S):
+        """(wsums, phase weights or None, head weights or None) from one nconv_weight_prologue
+        launch, or None where the separate path must run: merged_prologue off, a layer in training
+        mode (EnforcePos then rewrites the weights first), a forward pre-hook other than this
+        package's EnforcePos, or weights that are not contiguous fp32 device tensors."""
+        if not self._eval_prologue_ok(layers):
+            return None
         dev = S.device
         weights = [m.weight.data for m in layers]
         buf = torch.empty(sum(w.shape[0] for w in weights), device=dev, dtype=torch.float32)
@@ -463,6 +474,9 @@ class DNET(nn.Module):
         out_h, out_w = crop_hw(H, W, self.crop)
         if not grad and min(H, W) >= 16:
             out = torch.empty((S.shape[0], 1, out_h, out_w), device=S.device, dtype=torch.float32)
+            if self.stream_prologue and self._n_streams(S.shape[0]) > 1 and self._eval_prologue_ok(layers):
+                self._infer_split(S, layers, None, out, per_stream_prologue=True)
+                return out
             pro = self._eval_prologue(layers, S)
             if pro is None:
                 wsum, wph, w21 = self._prologue(layers, S), self._phase_weights(S.device), None
@@ -581,7 +595,10 @@ class DNET(nn.Module):
             cache[key] = [torch.cuda.Stream(device=device) for _ in range(n)]
         return cache[key]
 
-    def _infer_split(self, S, layers, wsum, out, wph=None, w21=None):
+    def _infer_split(self, S, layers, wsum, out, wph=None, w21=None, per_stream_prologue=False):
+        """The inference chain on batch slices, one stream each. per_stream_prologue: each stream
+        runs its own eval prologue (wsum / wph / w21 unused) -- the outputs are the same (the
+        prologue is a deterministic function of the weights)."""
         B = S.shape[0]
         n = self._n_streams(B)
         bounds = self.split_bounds(B, n, self.inference_shares, self._configured_streams())
@@ -596,8 +613,10 @@ class DNET(nn.Module):
             if bounds[k + 1] == bounds[k]:
                 continue
             with torch.cuda.stream(st):
-                self._infer(S[bounds[k]:bounds[k + 1]], layers, wsum, out[bounds[k]:bounds[k + 1]], wph, mid=False,
-                            w21=w21)
+                Sk = S[bounds[k]:bounds[k + 1]]
+                if per_stream_prologue:
+                    wsum, wph, w21 = self._eval_prologue(layers, Sk)
+                self._infer(Sk, layers, wsum, out[bounds[k]:bounds[k + 1]], wph, mid=False, w21=w21)
         for st in side:
             cur.wait_stream(st)
 

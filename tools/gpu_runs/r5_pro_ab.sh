@@ -4,7 +4,7 @@
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out/proab
 timeout -k 10 300 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu \
-    tests/test_gpu_train_launches.py tests/test_gpu_dnet.py -k "prologue or launches" > gpurun_out/proab/pytest.log 2>&1
+    tests/test_gpu_train_launches.py tests/test_gpu_dnet.py -k "prologue or launches or stream" > gpurun_out/proab/pytest.log 2>    tests/test_gpu_train_launches.py tests/test_gpu_dnet.py -k "prologue or launches" > gpurun_out/proab/pytest.log 2>&11
 rc=$?; tail -1 gpurun_out/proab/pytest.log; [ $rc -eq 0 ] || exit $rc
 for V in new prev; do
   lib=""; [ $V = prev ] && lib=$PWD/variants/prev/libnconv.so
