@@ -414,7 +414,7 @@ class DNET(nn.Module):
     # Inference split over streams (inference_streams > 1): each stream builds its own copy of the
     # weight prologue (one small launch), so the side streams start with the main one instead of
     # waiting for its prologue across streams; False: one shared prologue before the fork.
-    stream_prologue = True
+    stream_prologue = os.environ.get("NCONV_STREAM_PROLOGUE", "1") == "1"
 
     def _eval_prologue_ok(self, layers):
         """Whether the one-launch eval prologue applies (see _eval_prologue)."""
