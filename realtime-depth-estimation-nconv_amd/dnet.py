@@ -411,10 +411,12 @@ class DNET(nn.Module):
     # bitwise the three separate launches); False: the separate launches.
     merged_prologue = True
 
-    # Inference split over streams (inference_streams > 1): each stream builds its own copy of the
-    # weight prologue (one small launch), so the side streams start with the main one instead of
-    # waiting for its prologue across streams; False: one shared prologue before the fork.
-    stream_prologue = os.environ.get("NCONV_STREAM_PROLOGUE", "1") == "1"
+    # Inference split over streams (inference_streams > 1): True = each stream builds its own copy
+    # of the weight prologue (one small launch), so the side streams start with the main one
+    # instead of waiting for its prologue across streams. Measured slower at B=8 352x1216 (16.3-16.5
+    # k against 16.9-17.2 k frames/s, same box, three alternations: profiles/r5_ab_stream_prologue.log):
+    # the side stream's ~6 us later start staggers the two halves' kernels usefully. Off by default.
+    stream_prologue = os.environ.get("NCONV_STREAM_PROLOGUE", "0") == "1"
 
     def _eval_prologue_ok(self, layers):
         """Whether the one-launch eval prologue applies (see _eval_prologue)."""
