@@ -384,9 +384,6 @@ __global__ __launch_bounds__(kDT) void conv3x3_c1(const float* __restrict__ x, i
     }
 }
 
-#ifndef NCONV_WGD_GLDS
-#define NCONV_WGD_GLDS 1
-#endif
 // ------------------------------------------------------------------------------------------------
 // Weight gradients (training):  gW[m][n] = sum over images and pixels p of
 //     D[m][p] * P[n / TAPS][patch(p, n % TAPS)]
@@ -413,7 +410,7 @@ __host__ __device__ constexpr int wgd_ntb(int kind) {
 // (the 1- and 3-channel inputs of depth_conv / rgb_encoder0, a 1x1 of <= 32 channels)
 constexpr int wgd_nt(int kind, int N) { return N <= 32 ? 1 : wgd_ntb(kind); }
 
-template <int KIND, int S, int NT, int GM, int GN>
+template <int KIND, int S, int NT, int GM, int GN, bool DB>
 struct WgdCfg {
     static constexpr bool TR = KIND == NCONV_DENSE_TRANSPOSED_4X4;
     static constexpr int TAPS = KIND == NCONV_DENSE_3X3 ? 9 : (KIND == NCONV_DENSE_1X1 ? 1 : 16);
@@ -436,7 +433,9 @@ struct WgdCfg {
     static constexpr int PPLANE = PR * PC;
     static constexpr int DP = NPX + 2;     // D row pitch: rows m, m+1 two banks apart
     static constexpr int D_OFF = (CPB * PPLANE + 3) & ~3;
-    static constexpr int LDS = D_OFF + GM * 32 * DP > 4 * 16 * 64 ? D_OFF + GM * 32 * DP : 4 * 16 * 64;  // (+ the wave-partial sums)
+    static constexpr int BUF = (D_OFF + GM * 32 * DP + 3) & ~3;  // one tile's staging (patch, then D)
+    static constexpr int STG = DB ? 2 * BUF : BUF;               // DB: two tiles, the next one in flight
+    static constexpr int LDS = STG > 4 * 16 * 64 ? STG : 4 * 16 * 64;  // (+ the wave-partial sums)
     static constexpr int NDE = GM * 32 * NPX / kDT;  // D elements per thread
     static constexpr int NPG = (CPG * PPLANE + kDT - 1) / kDT;  // patch elements per thread and group
     static_assert(PPW % 16 == 0 && (GM * 32 * NPX) % kDT == 0, "wave / thread shares");
@@ -456,9 +455,9 @@ struct WgdArgs {
     long long ntiles;
 };
 
-template <int KIND, int S, int NT, int GM, int GN>
+template <int KIND, int S, int NT, int GM, int GN, bool DB>
 __global__ __launch_bounds__(kDT) void dense_wgrad_mfma(WgdArgs a, float* __restrict__ part) {
-    using C = WgdCfg<KIND, S, NT, GM, GN>;
+    using C = WgdCfg<KIND, S, NT, GM, GN, DB>;
     __shared__ __attribute__((aligned(16))) float lds[C::LDS];
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -500,7 +499,6 @@ __global__ __launch_bounds__(kDT) void dense_wgrad_mfma(WgdArgs a, float* __rest
     // concatenation of the guided model; otherwise that group reads each element from both
     // sources (one out of range) and adds them.
     constexpr unsigned OOB = 0x80000000u;
-#if NCONV_WGD_GLDS
     // LDS-DMA staging (buffer_load ... lds): every staged element goes from HBM straight into its
     // LDS slot -- no staging registers, so the weight-gradient accumulators (NT x 16 per lane) and
     // the rest fit two waves per SIMD, and one workgroup's loads hide behind the other's MFMAs.
@@ -539,7 +537,7 @@ __global__ __launch_bounds__(kDT) void dense_wgrad_mfma(WgdArgs a, float* __rest
     const unsigned drel = (unsigned)((dq / C::TW) * a.Wp + dq % C::TW) * 4u;
     // the block's tiles walk (tx, ty, b) in order from t0
     int tx_c = (int)(t0 % a.ntx), ty_c = (int)((t0 / a.ntx) % a.nty), b_c = (int)(t0 / ((long long)a.ntx * a.nty));
-    auto stage = [&](int tx, int ty, int b) __attribute__((always_inline)) {
+    auto stage = [&](int tx, int ty, int b, float* lds) __attribute__((always_inline)) {
         int tq = tid;
         asm volatile("" : "+v"(tq));
         const int py0 = ty * C::TH, px0 = tx * C::TW;
@@ -607,10 +605,7 @@ __global__ __launch_bounds__(kDT) void dense_wgrad_mfma(WgdArgs a, float* __rest
         }
     };
 
-#pragma unroll 1
-    for (long long t = t0; t < t1; ++t) {
-        __syncthreads();  // the previous tile's MFMAs are done with the LDS
-        stage(tx_c, ty_c, b_c);
+    auto next_tile = [&]() __attribute__((always_inline)) {
         if (++tx_c == a.ntx) {
             tx_c = 0;
             if (++ty_c == a.nty) {
@@ -618,88 +613,32 @@ __global__ __launch_bounds__(kDT) void dense_wgrad_mfma(WgdArgs a, float* __rest
                 ++b_c;
             }
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-#else
-    float dv[C::NDE], pv[GN][C::NPG];
-    auto load = [&](long long t) {
-        // the per-element coordinates below are recomputed per tile (tid made opaque): hoisted
-        // out of the tile loop they would pin ~4 registers per staged element
-        int tq = tid;
-        asm volatile("" : "+v"(tq));
-        const int tx = (int)(t % a.ntx);
-        const long long rr = t / a.ntx;
-        const int ty = (int)(rr % a.nty), b = (int)(rr / a.nty);
-        const int py0 = ty * C::TH, px0 = tx * C::TW;
-        {   // D: element k of a thread is row m0 + tid / NPX + k * (256 / NPX), pixel tid % NPX
-            const int q = tq % C::NPX;
-            const int py = py0 + q / C::TW, px = px0 + q % C::TW;
-            const unsigned ob = (py < a.Hp && px < a.Wp) ? (unsigned)(py * a.Wp + px) * 4u : OOB;
-            const __amdgpu_buffer_rsrc_t rd0 = plane_rsrc(a.d0 + (size_t)b * a.dC0 * HWp, (int)(a.dC0 * HWp * 4));
-            const __amdgpu_buffer_rsrc_t rd1 =
-                plane_rsrc(a.d1 ? a.d1 + (size_t)b * a.dC1 * HWp : a.d0, (int)((a.d1 ? a.dC1 : 0) * HWp * 4));
-            const int mw = __builtin_amdgcn_readfirstlane(m0 + tid / C::NPX);  // NPX >= 64: per wave
-#pragma unroll
-            for (int k = 0; k < C::NDE; ++k) {
-                const int m = mw + (kDT / C::NPX) * k;
-                const bool s1 = m >= a.dC0;
-                const int mm = s1 ? m - a.dC0 : m;
-                const unsigned off = (m < a.M && ob != OOB) ? (unsigned)(mm * HWp) * 4u + ob : OOB;
-                dv[k] = ld_f32(s1 ? rd1 : rd0, off);
-            }
-        }
-        const int iy0 = py0 * C::OS - C::PAD, ix0 = px0 * C::OS - C::PAD;
-        const __amdgpu_buffer_rsrc_t rp0 = plane_rsrc(a.p0 + (size_t)b * a.pC0 * HWs, (int)(a.pC0 * HWs * 4));
-        const __amdgpu_buffer_rsrc_t rp1 =
-            plane_rsrc(a.p1 ? a.p1 + (size_t)b * a.pC1 * HWs : a.p0, (int)((a.p1 ? a.pC1 : 0) * HWs * 4));
-#pragma unroll
-        for (int g = 0; g < GN; ++g) {
-            const int gc0 = c_lo + g * C::CPG;  // the group's first channel
-            const bool hi = a.p1 != nullptr && gc0 >= a.pC0;
-            const bool straddle = a.p1 != nullptr && gc0 < a.pC0 && gc0 + C::CPG > a.pC0;
-            const int cb = hi ? a.pC0 : 0;
-#pragma unroll
-            for (int k = 0; k < C::NPG; ++k) {
-                const int e = tq + kDT * k;
-                const int ci = e / C::PPLANE, rem = e % C::PPLANE;
-                const int r = rem / C::PC, c = rem % C::PC;
-                const int gc = gc0 + ci, iy = iy0 + r * C::GS, ix = ix0 + c * C::GS;
-                const bool ok = e < C::CPG * C::PPLANE && gc < Cp && (unsigned)iy < (unsigned)a.Hs &&
-                                (unsigned)ix < (unsigned)a.Ws;
-                const unsigned pix = (unsigned)(iy * a.Ws + ix);
-                if (!straddle) {
-                    pv[g][k] = ld_f32(hi ? rp1 : rp0, ok ? ((unsigned)(gc - cb) * (unsigned)HWs + pix) * 4u : OOB);
-                } else {
-                    pv[g][k] = ld_f32(rp0, ok && gc < a.pC0 ? ((unsigned)gc * (unsigned)HWs + pix) * 4u : OOB) +
-                               ld_f32(rp1, ok && gc >= a.pC0 ? ((unsigned)(gc - a.pC0) * (unsigned)HWs + pix) * 4u
-                                                              : OOB);
-                }
-            }
-        }
     };
-    auto store = [&]() {
-#pragma unroll
-        for (int k = 0; k < C::NDE; ++k) {
-            const int e = tid + kDT * k;
-            lds[C::D_OFF + (e / C::NPX) * C::DP + e % C::NPX] = dv[k];
-        }
-#pragma unroll
-        for (int g = 0; g < GN; ++g)
-#pragma unroll
-            for (int k = 0; k < C::NPG; ++k) {
-                const int e = tid + kDT * k;
-                if (e < C::CPG * C::PPLANE) lds[g * C::CPG * C::PPLANE + e] = pv[g][k];
-            }
-    };
-
-    if (t0 < t1) load(t0);
+    // DB: tile t + 1's DMA goes into the other buffer right after tile t's barrier and lands during
+    // tile t's MFMAs (one workgroup per CU keeps the matrix cores busy by itself); otherwise one
+    // buffer, and the loads of one workgroup hide behind the MFMAs of the CU's other workgroup
+    if (DB && t0 < t1) {
+        stage(tx_c, ty_c, b_c, lds);
+        next_tile();
+    }
 #pragma unroll 1
     for (long long t = t0; t < t1; ++t) {
-        __syncthreads();  // the previous tile's MFMAs are done with the LDS
-        store();
-        __syncthreads();
-        if (t + 1 < t1) load(t + 1);
-#endif
+        const float* lb = lds;
+        if constexpr (DB) {
+            lb = lds + ((t - t0) & 1) * C::BUF;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this tile's DMA (issued one tile ago)
+            __syncthreads();  // ... from every wave; and every wave is done with the other buffer
+            if (t + 1 < t1) {
+                stage(tx_c, ty_c, b_c, lds + ((t + 1 - t0) & 1) * C::BUF);
+                next_tile();
+            }
+        } else {
+            __syncthreads();  // the previous tile's MFMAs are done with the LDS
+            stage(tx_c, ty_c, b_c, lds);
+            next_tile();
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+        }
         // the wave's pixels in segments of 16 (8 k-steps) inside one tile row
 #pragma unroll 1
         for (int sg = 0; sg < C::PPW / 16; ++sg) {
@@ -707,10 +646,10 @@ __global__ __launch_bounds__(kDT) void dense_wgrad_mfma(WgdArgs a, float* __rest
             const int aoff = abase + q, boff = r * C::LS * C::PC + c * C::LS;
 #pragma unroll 2
             for (int j = 0; j < 8; ++j) {
-                const float av = lds[aoff + 2 * j];
+                const float av = lb[aoff + 2 * j];
 #pragma unroll
                 for (int u = 0; u < NT; ++u) {
-                    const float bv = lds[bbase[u] + boff + 2 * j * C::LS];
+                    const float bv = lb[bbase[u] + boff + 2 * j * C::LS];
                     acc[u] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[u], 0, 0, 0);
                 }
             }
@@ -847,7 +786,17 @@ int launch_conv3x3_c1(const float* x, int B, int Cin, int H, int W, const float*
 struct WgdPlan {
     WgdArgs a;
     int nt, gm, gn, rg;
+    bool db;  // double-buffered staging, one workgroup per CU (dense_wgrad_mfma DB)
 };
+
+// NCONV_WGD_DB=0: the single-buffer weight gradient (two workgroups per CU), for A/B timing
+static bool wgd_db() {
+    static const bool v = [] {
+        const char* e = getenv("NCONV_WGD_DB");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
 
 static WgdPlan wgrad_plan(const nconv_dense_wgrad& g) {
     WgdPlan pl{};
@@ -891,7 +840,7 @@ static WgdPlan wgrad_plan(const nconv_dense_wgrad& g) {
     // stages tall patches, so it pairs along M only
     pl.gm = (pl.nt > 1 && nmg % 2 == 0) ? 2 : 1;
     // (LDS-DMA staging: one n-group per workgroup, so two workgroups fit a CU's LDS)
-    pl.gn = (!NCONV_WGD_GLDS && pl.nt > 1 && nng % 2 == 0 && !(g.kind == NCONV_DENSE_3X3 && g.stride == 2)) ? 2 : 1;
+    pl.gn = 1;
     pl.rg = 4 / (pl.gm * pl.gn);
     const int th = (tr || (g.kind == NCONV_DENSE_3X3 && g.stride == 2)) ? 2 : 4;
     a.ntx = (a.Wp + 31) / 32;
@@ -899,7 +848,8 @@ static WgdPlan wgrad_plan(const nconv_dense_wgrad& g) {
     a.ntiles = (long long)g.B * a.ntx * a.nty;
     a.nbm = nmg / pl.gm;
     a.nbn = nng / pl.gn;
-    long long nks = 512 / (a.nbm * a.nbn);  // about two workgroups per CU
+    pl.db = wgd_db() && pl.nt > 1;  // (the one-tile groups are small and occupancy-bound: single buffer)
+    long long nks = (pl.db ? 256 : 512) / (a.nbm * a.nbn);  // one (DB) or two workgroups per CU
     if (nks < 1) nks = 1;
     if (nks > a.ntiles) nks = a.ntiles;
     a.nks = (int)nks;
@@ -911,26 +861,22 @@ size_t dense_wgrad_workspace_bytes(const nconv_dense_wgrad& g) {
     return (size_t)pl.a.nks * pl.a.M * pl.a.N * sizeof(float);
 }
 
+template <int KIND, int S, int NT, bool DB>
+static bool go_wgrad_db(const WgdPlan& pl, float* ws, hipStream_t st) {
+    const dim3 grid(pl.a.nbm * pl.a.nbn * pl.a.nks), blk(kDT);
+    if (pl.gn != 1) return false;  // (one n-group per workgroup: LDS-DMA staging)
+    if (pl.gm == 1)
+        hipLaunchKernelGGL((dense_wgrad_mfma<KIND, S, NT, 1, 1, DB>), grid, blk, 0, st, pl.a, ws);
+    else if constexpr (NT > 1)
+        hipLaunchKernelGGL((dense_wgrad_mfma<KIND, S, NT, 2, 1, DB>), grid, blk, 0, st, pl.a, ws);
+    else
+        return false;
+    return true;
+}
+
 template <int KIND, int S, int NT>
 static bool go_wgrad(const WgdPlan& pl, float* ws, hipStream_t st) {
-    const dim3 grid(pl.a.nbm * pl.a.nbn * pl.a.nks), blk(kDT);
-    if (pl.gm == 1 && pl.gn == 1)
-        hipLaunchKernelGGL((dense_wgrad_mfma<KIND, S, NT, 1, 1>), grid, blk, 0, st, pl.a, ws);
-    else if constexpr (NT > 1) {
-        if (pl.gm == 2 && pl.gn == 1)
-            hipLaunchKernelGGL((dense_wgrad_mfma<KIND, S, NT, 2, 1>), grid, blk, 0, st, pl.a, ws);
-        else if constexpr (!(KIND == NCONV_DENSE_3X3 && S == 2) && KIND != NCONV_DENSE_1X1) {
-            if (pl.gm == 1 && pl.gn == 2)
-                hipLaunchKernelGGL((dense_wgrad_mfma<KIND, S, NT, 1, 2>), grid, blk, 0, st, pl.a, ws);
-            else
-                hipLaunchKernelGGL((dense_wgrad_mfma<KIND, S, NT, 2, 2>), grid, blk, 0, st, pl.a, ws);
-        } else {
-            return false;
-        }
-    } else {
-        return false;
-    }
-    return true;
+    return pl.db ? go_wgrad_db<KIND, S, NT, true>(pl, ws, st) : go_wgrad_db<KIND, S, NT, false>(pl, ws, st);
 }
 
 int launch_dense_wgrad(const nconv_dense_wgrad& g, float* ws, size_t ws_bytes, hipStream_t st, const char** why) {
