@@ -789,11 +789,13 @@ struct WgdPlan {
     bool db;  // double-buffered staging, one workgroup per CU (dense_wgrad_mfma DB)
 };
 
-// NCONV_WGD_DB=0: the single-buffer weight gradient (two workgroups per CU), for A/B timing
+// NCONV_WGD_DB=1: the double-buffered weight gradient (one workgroup per CU). Measured slower than
+// two single-buffer workgroups per CU: the config-4 step 47.1 against 45.0-45.3 ms, the 32-channel
+// 3x3 weight gradient 704.6 against 614.0 us (profiles/r5_ab_dense_wgrad_db.log), so opt-in only.
 static bool wgd_db() {
     static const bool v = [] {
         const char* e = getenv("NCONV_WGD_DB");
-        return !(e && e[0] == '0');
+        return e && e[0] == '1';
     }();
     return v;
 }
