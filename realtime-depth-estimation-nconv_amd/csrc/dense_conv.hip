@@ -793,11 +793,8 @@ struct WgdPlan {
 // two single-buffer workgroups per CU: the config-4 step 47.1 against 45.0-45.3 ms, the 32-channel
 // 3x3 weight gradient 704.6 against 614.0 us (profiles/r5_ab_dense_wgrad_db.log), so opt-in only.
 static bool wgd_db() {
-    static const bool v = [] {
-        const char* e = getenv("NCONV_WGD_DB");
-        return e && e[0] == '1';
-    }();
-    return v;
+    const char* e = getenv("NCONV_WGD_DB");  // (read per call: tests switch it inside one process)
+    return e && e[0] == '1';
 }
 
 static WgdPlan wgrad_plan(const nconv_dense_wgrad& g) {
