@@ -696,6 +696,88 @@ __global__ __launch_bounds__(kDT) void dense_wgrad_reduce(const float* __restric
     if (ph == 0 && e < mn) gw[e] = ((red[0][col] + red[1][col]) + red[2][col]) + red[3][col];
 }
 
+// ---- the transposed convolution's weight-gradient rows of the few channels concatenated beside
+//      whole 32-channel groups (UpCat's depth channel and 32 / 64 features, step2.py:173) ----
+// On the matrix cores those rows would take a whole 32-row m-tile each (M = 33 / 65 padded to 64 /
+// 96: half or a third of the tile work wasted); here they are a small GEMV on the vector ALU:
+//   out[j][co*16 + kh*4 + kw] = sum over (b, oy, ox) with oy + 1 - kh, ox + 1 - kw even of
+//       gy[b][co][oy][ox] * x1[b][j][(oy + 1 - kh) / 2][(ox + 1 - kw) / 2]
+// Persistent workgroups over 16 x 32 tiles of gy; thread = (co of a group of 16, tap); per tile and
+// co group the 16 gy planes and the x1 window (10 x 18 per channel) are staged in LDS and each
+// thread sums its tap's parity class (8 x 16 pixels). Per-workgroup partial rows, reduced in a
+// fixed order by dense_wgrad_reduce (deterministic).
+constexpr int kTrTH = 16, kTrTW = 32, kTrGP = kTrTH * kTrTW + 1;  // gy plane pitch (+1: banks)
+constexpr int kTrXH = kTrTH / 2 + 2, kTrXW = kTrTW / 2 + 2;        // x1 window
+constexpr int kTrMaxC1 = 2, kTrMaxG = 6;                            // channels, co groups (Cout <= 96)
+__global__ __launch_bounds__(256) void dense_wgrad_tr_rows(const float* __restrict__ x1, int C1, int H, int W,
+                                                           const float* __restrict__ gy, int Cout, int Ho, int Wo,
+                                                           int ntx, int nty, long long ntiles,
+                                                           float* __restrict__ part) {
+    __shared__ float sg[16 * kTrGP];
+    __shared__ float sx[kTrMaxC1 * kTrXH * kTrXW];
+    const int tid = threadIdx.x, col = tid >> 4, tap = tid & 15, kh = tap >> 2, kw = tap & 3;
+    const int ng = Cout / 16, N = Cout * 16;
+    float acc[kTrMaxG][kTrMaxC1];
+#pragma unroll
+    for (int g = 0; g < kTrMaxG; ++g)
+#pragma unroll
+        for (int j = 0; j < kTrMaxC1; ++j) acc[g][j] = 0.f;
+    // this tap's pixels: rows ry = pr + 2 a, columns rx = pc + 2 c (oy + 1 - kh even: tile origins even)
+    const int pr = (kh + 1) & 1, pc = (kw + 1) & 1;
+    for (long long t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const int tx = (int)(t % ntx), ty = (int)((t / ntx) % nty), b = (int)(t / ((long long)ntx * nty));
+        const int r0 = ty * kTrTH, c0 = tx * kTrTW;
+        const int iy0 = r0 / 2 - 1, ix0 = c0 / 2 - 1;  // x1 window origin
+        __syncthreads();  // the previous tile is done with sx
+        for (int e = tid; e < C1 * kTrXH * kTrXW; e += 256) {
+            const int j = e / (kTrXH * kTrXW), r = (e / kTrXW) % kTrXH, c = e % kTrXW;
+            const int iy = iy0 + r, ix = ix0 + c;
+            sx[e] = ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
+                        ? x1[(((size_t)b * C1 + j) * H + iy) * W + ix] : 0.f;
+        }
+        for (int g = 0; g < ng; ++g) {
+            __syncthreads();  // (sx staged; the previous group is done with sg)
+            for (int e = tid; e < 16 * kTrTH * kTrTW; e += 256) {
+                const int cl = e / (kTrTH * kTrTW), r = (e / kTrTW) % kTrTH, c = e % kTrTW;
+                const int oy = r0 + r, ox = c0 + c;
+                sg[cl * kTrGP + r * kTrTW + c] = (oy < Ho && ox < Wo)
+                    ? gy[(((size_t)b * Cout + g * 16 + cl) * Ho + oy) * Wo + ox] : 0.f;
+            }
+            __syncthreads();
+            float a[kTrMaxC1];
+#pragma unroll
+            for (int j = 0; j < kTrMaxC1; ++j) a[j] = 0.f;
+#pragma unroll 2
+            for (int ra = 0; ra < kTrTH / 2; ++ra) {
+                const int ry = pr + 2 * ra;
+                const int xr = (r0 + ry + 1 - kh) / 2 - iy0;  // x1 window row
+                const float* gr = sg + col * kTrGP + ry * kTrTW + pc;
+#pragma unroll
+                for (int ca = 0; ca < kTrTW / 2; ++ca) {
+                    const float v = gr[2 * ca];
+                    const int xc = (c0 + pc + 2 * ca + 1 - kw) / 2 - ix0;
+#pragma unroll
+                    for (int j = 0; j < kTrMaxC1; ++j)
+                        if (j < C1) a[j] = fmaf(v, sx[(j * kTrXH + xr) * kTrXW + xc], a[j]);
+                }
+            }
+#pragma unroll
+            for (int gg = 0; gg < kTrMaxG; ++gg)
+                if (gg == g) {
+#pragma unroll
+                    for (int j = 0; j < kTrMaxC1; ++j) acc[gg][j] += a[j];
+                }
+        }
+    }
+    // partial row of this workgroup: [C1][N]
+    float* out = part + (size_t)blockIdx.x * C1 * N;
+#pragma unroll
+    for (int g = 0; g < kTrMaxG; ++g)
+#pragma unroll
+        for (int j = 0; j < kTrMaxC1; ++j)
+            if (g < ng && j < C1) out[(size_t)j * N + (g * 16 + col) * 16 + tap] = acc[g][j];
+}
+
 // ------------------------------------------------------------------------------------------------
 // Launchers
 // ------------------------------------------------------------------------------------------------
@@ -855,9 +937,55 @@ static WgdPlan wgrad_plan(const nconv_dense_wgrad& g) {
     return pl;
 }
 
-size_t dense_wgrad_workspace_bytes(const nconv_dense_wgrad& g) {
+// The transposed kind with one source of a few channels beside one of whole 32-channel groups:
+// the matrix cores take the large source's rows, dense_wgrad_tr_rows the small one's
+// (NCONV_WGD_TR_ROWS=0: all on the matrix cores). Returns 0 (no split), 1 (x1 small), 2 (x0 small).
+static int tr_rows_split(const nconv_dense_wgrad& g) {
+    const char* e = getenv("NCONV_WGD_TR_ROWS");
+    if ((e && e[0] == '0') || g.kind != NCONV_DENSE_TRANSPOSED_4X4 || !g.x1 || g.C0 <= 0 || g.C1 <= 0 ||
+        g.Cout % 16 != 0 || g.Cout > 16 * kTrMaxG)
+        return 0;
+    if (g.C1 <= kTrMaxC1 && g.C0 % 32 == 0) return 1;
+    if (g.C0 <= kTrMaxC1 && g.C1 % 32 == 0) return 2;
+    return 0;
+}
+// the large source alone, its gradient rows where they sit in gw
+static nconv_dense_wgrad tr_rows_main(const nconv_dense_wgrad& g) {
+    nconv_dense_wgrad m = g;
+    if (tr_rows_split(g) == 2) {
+        m.x0 = g.x1;
+        m.C0 = g.C1;
+        m.gw = g.gw + (size_t)g.C0 * g.Cout * 16;
+    }
+    m.x1 = nullptr;
+    m.C1 = 0;
+    return m;
+}
+constexpr int kTrBlocks = 1024;
+struct TrRowsGrid {
+    int ntx, nty;
+    long long ntiles;
+    int nblk;
+};
+static TrRowsGrid tr_rows_grid(const nconv_dense_wgrad& g) {
+    TrRowsGrid r;
+    r.ntx = (g.Wo + kTrTW - 1) / kTrTW;
+    r.nty = (g.Ho + kTrTH - 1) / kTrTH;
+    r.ntiles = (long long)g.B * r.ntx * r.nty;
+    r.nblk = (int)(r.ntiles < kTrBlocks ? r.ntiles : kTrBlocks);
+    return r;
+}
+
+static size_t main_wgrad_bytes(const nconv_dense_wgrad& g) {
     const WgdPlan pl = wgrad_plan(g);
     return (size_t)pl.a.nks * pl.a.M * pl.a.N * sizeof(float);
+}
+
+size_t dense_wgrad_workspace_bytes(const nconv_dense_wgrad& g) {
+    if (!tr_rows_split(g)) return main_wgrad_bytes(g);
+    const size_t a = (main_wgrad_bytes(tr_rows_main(g)) + 255) & ~(size_t)255;
+    const int cs = tr_rows_split(g) == 1 ? g.C1 : g.C0;
+    return a + (size_t)tr_rows_grid(g).nblk * cs * g.Cout * 16 * sizeof(float);
 }
 
 template <int KIND, int S, int NT, bool DB>
@@ -878,12 +1006,36 @@ static bool go_wgrad(const WgdPlan& pl, float* ws, hipStream_t st) {
     return pl.db ? go_wgrad_db<KIND, S, NT, true>(pl, ws, st) : go_wgrad_db<KIND, S, NT, false>(pl, ws, st);
 }
 
+static int launch_dense_wgrad_main(const nconv_dense_wgrad& g, float* ws, hipStream_t st, const char** why);
+
 int launch_dense_wgrad(const nconv_dense_wgrad& g, float* ws, size_t ws_bytes, hipStream_t st, const char** why) {
-    const WgdPlan pl = wgrad_plan(g);
     if (ws_bytes < dense_wgrad_workspace_bytes(g)) {
         *why = "workspace too small (see nconv_dense_wgrad_workspace_bytes)";
         return -22;
     }
+    const int sp = tr_rows_split(g);
+    if (!sp) return launch_dense_wgrad_main(g, ws, st, why);
+    const nconv_dense_wgrad m = tr_rows_main(g);  // the large source's rows
+    if (int rc = launch_dense_wgrad_main(m, ws, st, why)) return rc;
+    const TrRowsGrid r = tr_rows_grid(g);
+    float* part = ws + ((main_wgrad_bytes(m) + 255) & ~(size_t)255) / sizeof(float);
+    const float* xs = sp == 1 ? g.x1 : g.x0;
+    const int cs = sp == 1 ? g.C1 : g.C0;
+    hipLaunchKernelGGL(dense_wgrad_tr_rows, dim3(r.nblk), dim3(256), 0, st, xs, cs, g.H, g.W, g.gy, g.Cout, g.Ho,
+                       g.Wo, r.ntx, r.nty, r.ntiles, part);
+    const int mn = cs * g.Cout * 16;
+    hipLaunchKernelGGL(dense_wgrad_reduce, dim3((mn + 63) / 64), dim3(kDT), 0, st, part, r.nblk, mn,
+                       sp == 1 ? g.gw + (size_t)g.C0 * g.Cout * 16 : g.gw);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        *why = hipGetErrorString(e);
+        return -5;
+    }
+    return 0;
+}
+
+static int launch_dense_wgrad_main(const nconv_dense_wgrad& g, float* ws, hipStream_t st, const char** why) {
+    const WgdPlan pl = wgrad_plan(g);
     bool ok = false;
 #define NCONV_WG(KIND_, S_)                                                                     \
     if (g.kind == KIND_ && g.stride == S_)                                                     \

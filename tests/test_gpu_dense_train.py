@@ -242,3 +242,30 @@ def test_relu_bias_bwd(nconv_amd, gpu, B, C, H, W, relu):
     if relu:
         assert torch.equal(gm.cpu(), ref)
     _close(gb, ref.double().sum(dim=(0, 2, 3)), "gbias", 1e-5)
+
+
+@pytest.mark.parametrize("c0,c1,cout,H,W", [(1, 32, 32, 9, 19), (1, 64, 64, 7, 20), (32, 1, 32, 12, 33),
+                                            (64, 1, 64, 5, 17), (2, 32, 32, 20, 41), (1, 32, 32, 44, 152)])
+def test_transposed_wgrad_row_split(nconv_amd, gpu, c0, c1, cout, H, W, monkeypatch):
+    """ConvTranspose2d weight gradient with the few channels beside whole 32-channel groups on the
+    vector ALU (dense_wgrad_tr_rows; UpCat's cat(depth, features)): against float64 autograd (1e-4
+    normwise) and against every row on the matrix cores (NCONV_WGD_TR_ROWS=0, 1e-5)."""
+    D = nconv_amd.dense
+    g = torch.Generator().manual_seed(c0 * 100 + c1 + H)
+    B = 2
+    x0 = torch.randn(B, c0, H, W, generator=g, dtype=torch.float64)
+    x1 = torch.randn(B, c1, H, W, generator=g, dtype=torch.float64)
+    w = torch.randn(c0 + c1, cout, 4, 4, generator=g, dtype=torch.float64) * 0.1
+    gy = torch.randn(B, cout, 2 * H, 2 * W, generator=g, dtype=torch.float64)
+    r = w.clone().requires_grad_(True)
+    F.conv_transpose2d(torch.cat([x0, x1], 1), r, None, 2, 1).backward(gy)
+    grads = {}
+    for split in ("1", "0"):
+        monkeypatch.setenv("NCONV_WGD_TR_ROWS", split)
+        q = w.to(gpu, torch.float32).requires_grad_(True)
+        y = D.conv_fn(x0.to(gpu, torch.float32), q, None, 2, 2, x1=x1.to(gpu, torch.float32))
+        y.backward(gy.to(gpu, torch.float32))
+        torch.cuda.synchronize()
+        grads[split] = q.grad.detach().double().cpu()
+        _close(grads[split], r.grad, f"weight gradient (split={split})", 1e-4)
+    _close(grads["1"], grads["0"], "split vs matrix cores", 1e-5)
