@@ -699,83 +699,90 @@ __global__ __launch_bounds__(kDT) void dense_wgrad_reduce(const float* __restric
 // ---- the transposed convolution's weight-gradient rows of the few channels concatenated beside
 //      whole 32-channel groups (UpCat's depth channel and 32 / 64 features, step2.py:173) ----
 // On the matrix cores those rows would take a whole 32-row m-tile each (M = 33 / 65 padded to 64 /
-// 96: half or a third of the tile work wasted); here they are a small GEMV on the vector ALU:
+// 96: half or a third of the tile work wasted); here they are a GEMV on the vector ALU that
+// streams dL/dy once:
 //   out[j][co*16 + kh*4 + kw] = sum over (b, oy, ox) with oy + 1 - kh, ox + 1 - kw even of
 //       gy[b][co][oy][ox] * x1[b][j][(oy + 1 - kh) / 2][(ox + 1 - kw) / 2]
-// Persistent workgroups over 16 x 32 tiles of gy; thread = (co of a group of 16, tap); per tile and
-// co group the 16 gy planes and the x1 window (10 x 18 per channel) are staged in LDS and each
-// thread sums its tap's parity class (8 x 16 pixels). Per-workgroup partial rows, reduced in a
-// fixed order by dense_wgrad_reduce (deterministic).
-constexpr int kTrTH = 16, kTrTW = 32, kTrGP = kTrTH * kTrTW + 1;  // gy plane pitch (+1: banks)
-constexpr int kTrXH = kTrTH / 2 + 2, kTrXW = kTrTW / 2 + 2;        // x1 window
-constexpr int kTrMaxC1 = 2, kTrMaxG = 6;                            // channels, co groups (Cout <= 96)
+// Each dL/dy element meets two kernel rows (kh of its row parity) and two columns. Workgroup =
+// one channel co of one image over a 16-row x 256-column block of dL/dy: thread = column, its 16
+// rows read coalesced, the x1 window (10 rows x 130 columns per channel) staged in LDS; the 16
+// tap sums of the workgroup reduced over its threads in a fixed order into its partial slot
+// part[slice][co * 16 + tap], slice = (image, row block, column block); dense_wgrad_reduce adds
+// the slices in a fixed order (deterministic).
+constexpr int kTrRows = 16, kTrCols = 256;
+constexpr int kTrXH = kTrRows / 2 + 2, kTrXW = kTrCols / 2 + 2;  // x1 window
+constexpr int kTrMaxC1 = 2, kTrMaxG = 6;                          // channels; Cout <= 16 * kTrMaxG
 __global__ __launch_bounds__(256) void dense_wgrad_tr_rows(const float* __restrict__ x1, int C1, int H, int W,
                                                            const float* __restrict__ gy, int Cout, int Ho, int Wo,
-                                                           int ntx, int nty, long long ntiles,
-                                                           float* __restrict__ part) {
-    __shared__ float sg[16 * kTrGP];
+                                                           int nry, int nrx, float* __restrict__ part) {
     __shared__ float sx[kTrMaxC1 * kTrXH * kTrXW];
-    const int tid = threadIdx.x, col = tid >> 4, tap = tid & 15, kh = tap >> 2, kw = tap & 3;
-    const int ng = Cout / 16, N = Cout * 16;
-    float acc[kTrMaxG][kTrMaxC1];
+    __shared__ float red[4][kTrMaxC1 * 16];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    int blk = blockIdx.x;
+    const int co = blk % Cout;
+    blk /= Cout;
+    const int rx = blk % nrx;
+    blk /= nrx;
+    const int ry = blk % nry, b = blk / nry;
+    const int oy0 = ry * kTrRows, ox0 = rx * kTrCols;
+    const int iy0 = oy0 / 2 - 1, ix0 = ox0 / 2 - 1;
+    for (int e = tid; e < C1 * kTrXH * kTrXW; e += 256) {
+        const int j = e / (kTrXH * kTrXW), r = (e / kTrXW) % kTrXH, c = e % kTrXW;
+        const int iy = iy0 + r, ix = ix0 + c;
+        sx[e] = ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W) ? x1[(((size_t)b * C1 + j) * H + iy) * W + ix]
+                                                                         : 0.f;
+    }
+    const int ox = ox0 + tid;
+    float gv[kTrRows];
+    const float* gp = gy + (((size_t)b * Cout + co) * Ho + oy0) * Wo + ox;
 #pragma unroll
-    for (int g = 0; g < kTrMaxG; ++g)
+    for (int r = 0; r < kTrRows; ++r) gv[r] = (ox < Wo && oy0 + r < Ho) ? gp[(size_t)r * Wo] : 0.f;
+    __syncthreads();
+    // this column's two kernel columns (kw of the parity of ox + 1) and their x1 columns
+    const int kwa = (ox + 1) & 1;                  // kw in {kwa, kwa + 2}
+    const int xca = (ox + 1 - kwa) / 2 - ix0;      // x1 column of kw = kwa; kw = kwa + 2: xca - 1
+    // acc[j][kh][i]: kernel column kw = kwa + 2 i (the thread's column parity; kh is the row's,
+    // known per unrolled row since the block's first row is even)
+    float acc[kTrMaxC1][4][2];
 #pragma unroll
-        for (int j = 0; j < kTrMaxC1; ++j) acc[g][j] = 0.f;
-    // this tap's pixels: rows ry = pr + 2 a, columns rx = pc + 2 c (oy + 1 - kh even: tile origins even)
-    const int pr = (kh + 1) & 1, pc = (kw + 1) & 1;
-    for (long long t = blockIdx.x; t < ntiles; t += gridDim.x) {
-        const int tx = (int)(t % ntx), ty = (int)((t / ntx) % nty), b = (int)(t / ((long long)ntx * nty));
-        const int r0 = ty * kTrTH, c0 = tx * kTrTW;
-        const int iy0 = r0 / 2 - 1, ix0 = c0 / 2 - 1;  // x1 window origin
-        __syncthreads();  // the previous tile is done with sx
-        for (int e = tid; e < C1 * kTrXH * kTrXW; e += 256) {
-            const int j = e / (kTrXH * kTrXW), r = (e / kTrXW) % kTrXH, c = e % kTrXW;
-            const int iy = iy0 + r, ix = ix0 + c;
-            sx[e] = ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
-                        ? x1[(((size_t)b * C1 + j) * H + iy) * W + ix] : 0.f;
-        }
-        for (int g = 0; g < ng; ++g) {
-            __syncthreads();  // (sx staged; the previous group is done with sg)
-            for (int e = tid; e < 16 * kTrTH * kTrTW; e += 256) {
-                const int cl = e / (kTrTH * kTrTW), r = (e / kTrTW) % kTrTH, c = e % kTrTW;
-                const int oy = r0 + r, ox = c0 + c;
-                sg[cl * kTrGP + r * kTrTW + c] = (oy < Ho && ox < Wo)
-                    ? gy[(((size_t)b * Cout + g * 16 + cl) * Ho + oy) * Wo + ox] : 0.f;
-            }
-            __syncthreads();
-            float a[kTrMaxC1];
+    for (int j = 0; j < kTrMaxC1; ++j)
 #pragma unroll
-            for (int j = 0; j < kTrMaxC1; ++j) a[j] = 0.f;
-#pragma unroll 2
-            for (int ra = 0; ra < kTrTH / 2; ++ra) {
-                const int ry = pr + 2 * ra;
-                const int xr = (r0 + ry + 1 - kh) / 2 - iy0;  // x1 window row
-                const float* gr = sg + col * kTrGP + ry * kTrTW + pc;
+        for (int t = 0; t < 4; ++t) acc[j][t][0] = acc[j][t][1] = 0.f;
 #pragma unroll
-                for (int ca = 0; ca < kTrTW / 2; ++ca) {
-                    const float v = gr[2 * ca];
-                    const int xc = (c0 + pc + 2 * ca + 1 - kw) / 2 - ix0;
+    for (int r = 0; r < kTrRows; ++r) {
+        const int kha = (r + 1) & 1;                    // oy0 even: kh in {kha, kha + 2}
+        const int xra = (oy0 + r + 1 - kha) / 2 - iy0;  // x1 row of kh = kha; kh = kha + 2: xra - 1
 #pragma unroll
-                    for (int j = 0; j < kTrMaxC1; ++j)
-                        if (j < C1) a[j] = fmaf(v, sx[(j * kTrXH + xr) * kTrXW + xc], a[j]);
-                }
-            }
-#pragma unroll
-            for (int gg = 0; gg < kTrMaxG; ++gg)
-                if (gg == g) {
-#pragma unroll
-                    for (int j = 0; j < kTrMaxC1; ++j) acc[gg][j] += a[j];
-                }
+        for (int j = 0; j < kTrMaxC1; ++j) {
+            if (j >= C1) continue;
+            const float* xs = sx + j * kTrXH * kTrXW;
+            const float x00 = xs[xra * kTrXW + xca], x01 = xs[xra * kTrXW + xca - 1];
+            const float x10 = xs[(xra - 1) * kTrXW + xca], x11 = xs[(xra - 1) * kTrXW + xca - 1];
+            acc[j][kha][0] = fmaf(gv[r], x00, acc[j][kha][0]);
+            acc[j][kha][1] = fmaf(gv[r], x01, acc[j][kha][1]);
+            acc[j][kha + 2][0] = fmaf(gv[r], x10, acc[j][kha + 2][0]);
+            acc[j][kha + 2][1] = fmaf(gv[r], x11, acc[j][kha + 2][1]);
         }
     }
-    // partial row of this workgroup: [C1][N]
-    float* out = part + (size_t)blockIdx.x * C1 * N;
+    // the workgroup's 16 (x C1) tap sums: wave butterflies, then the four waves in order
 #pragma unroll
-    for (int g = 0; g < kTrMaxG; ++g)
+    for (int j = 0; j < kTrMaxC1; ++j) {
+        if (j >= C1) continue;
 #pragma unroll
-        for (int j = 0; j < kTrMaxC1; ++j)
-            if (g < ng && j < C1) out[(size_t)j * N + (g * 16 + col) * 16 + tap] = acc[g][j];
+        for (int t = 0; t < 16; ++t) {
+            const int kh = t >> 2, kw = t & 3;
+            float v = (kw & 1) == kwa ? acc[j][kh][kw >> 1] : 0.f;
+#pragma unroll
+            for (int m = 32; m > 0; m >>= 1) v += __shfl_xor(v, m);
+            if (lane == 0) red[wv][j * 16 + t] = v;
+        }
+    }
+    __syncthreads();
+    if (tid < C1 * 16) {
+        const int j = tid >> 4, t = tid & 15;
+        const size_t slice = ((size_t)b * nry + ry) * nrx + rx;
+        part[(slice * C1 + j) * (size_t)(Cout * 16) + co * 16 + t] = ((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid];
+    }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -961,18 +968,14 @@ static nconv_dense_wgrad tr_rows_main(const nconv_dense_wgrad& g) {
     m.C1 = 0;
     return m;
 }
-constexpr int kTrBlocks = 1024;
 struct TrRowsGrid {
-    int ntx, nty;
-    long long ntiles;
-    int nblk;
+    int nry, nrx, nslice;
 };
 static TrRowsGrid tr_rows_grid(const nconv_dense_wgrad& g) {
     TrRowsGrid r;
-    r.ntx = (g.Wo + kTrTW - 1) / kTrTW;
-    r.nty = (g.Ho + kTrTH - 1) / kTrTH;
-    r.ntiles = (long long)g.B * r.ntx * r.nty;
-    r.nblk = (int)(r.ntiles < kTrBlocks ? r.ntiles : kTrBlocks);
+    r.nry = (g.Ho + kTrRows - 1) / kTrRows;
+    r.nrx = (g.Wo + kTrCols - 1) / kTrCols;
+    r.nslice = g.B * r.nry * r.nrx;
     return r;
 }
 
@@ -985,7 +988,7 @@ size_t dense_wgrad_workspace_bytes(const nconv_dense_wgrad& g) {
     if (!tr_rows_split(g)) return main_wgrad_bytes(g);
     const size_t a = (main_wgrad_bytes(tr_rows_main(g)) + 255) & ~(size_t)255;
     const int cs = tr_rows_split(g) == 1 ? g.C1 : g.C0;
-    return a + (size_t)tr_rows_grid(g).nblk * cs * g.Cout * 16 * sizeof(float);
+    return a + (size_t)tr_rows_grid(g).nslice * cs * g.Cout * 16 * sizeof(float);
 }
 
 template <int KIND, int S, int NT, bool DB>
@@ -1021,10 +1024,10 @@ int launch_dense_wgrad(const nconv_dense_wgrad& g, float* ws, size_t ws_bytes, h
     float* part = ws + ((main_wgrad_bytes(m) + 255) & ~(size_t)255) / sizeof(float);
     const float* xs = sp == 1 ? g.x1 : g.x0;
     const int cs = sp == 1 ? g.C1 : g.C0;
-    hipLaunchKernelGGL(dense_wgrad_tr_rows, dim3(r.nblk), dim3(256), 0, st, xs, cs, g.H, g.W, g.gy, g.Cout, g.Ho,
-                       g.Wo, r.ntx, r.nty, r.ntiles, part);
+    hipLaunchKernelGGL(dense_wgrad_tr_rows, dim3(r.nslice * g.Cout), dim3(256), 0, st, xs, cs, g.H, g.W, g.gy, g.Cout,
+                       g.Ho, g.Wo, r.nry, r.nrx, part);
     const int mn = cs * g.Cout * 16;
-    hipLaunchKernelGGL(dense_wgrad_reduce, dim3((mn + 63) / 64), dim3(kDT), 0, st, part, r.nblk, mn,
+    hipLaunchKernelGGL(dense_wgrad_reduce, dim3((mn + 63) / 64), dim3(kDT), 0, st, part, r.nslice, mn,
                        sp == 1 ? g.gw + (size_t)g.C0 * g.Cout * 16 : g.gw);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
