@@ -430,19 +430,14 @@ struct WgdCfg {
     static constexpr int OS = TR ? 2 : S;
     static constexpr int PAD = KIND == NCONV_DENSE_1X1 ? 0 : 1;
     static constexpr int PR = (TH - 1) * LS + KS, PC = (TW - 1) * LS + KS;
-    // LDS image of the patch, padded for ds_read_b32's banks (bank = dword mod 32 per 32-lane half):
-    // B column n = (ci, tap = kh * KS + kw) reads ci * PPP + kh * PCP + kw + const, which is
-    // TAPS * ci + tap = n (mod 32) when PCP = KS and PPP = TAPS (mod 32) -- 32 consecutive columns,
-    // 32 banks. The A rows (one per lane) sit DP = 1 (mod 32) apart likewise.
-    static constexpr int PCP = PC + ((KS - PC) % 32 + 32) % 32;
-    static constexpr int PPP = PR * PCP + ((TAPS - PR * PCP) % 32 + 32) % 32;
-    static constexpr int DP = NPX + 1;     // D row pitch
-    static constexpr int D_OFF = (CPB * PPP + 3) & ~3;
+    static constexpr int PPLANE = PR * PC;
+    static constexpr int DP = NPX + 2;     // D row pitch: rows m, m+1 two banks apart
+    static constexpr int D_OFF = (CPB * PPLANE + 3) & ~3;
     static constexpr int BUF = (D_OFF + GM * 32 * DP + 3) & ~3;  // one tile's staging (patch, then D)
     static constexpr int STG = DB ? 2 * BUF : BUF;               // DB: two tiles, the next one in flight
     static constexpr int LDS = STG > 4 * 16 * 64 ? STG : 4 * 16 * 64;  // (+ the wave-partial sums)
     static constexpr int NDE = GM * 32 * NPX / kDT;  // D elements per thread
-    static constexpr int NPG = (CPG * PPP + kDT - 1) / kDT;  // patch slots per thread and group
+    static constexpr int NPG = (CPG * PPLANE + kDT - 1) / kDT;  // patch elements per thread and group
     static_assert(PPW % 16 == 0 && (GM * 32 * NPX) % kDT == 0, "wave / thread shares");
 };
 
@@ -489,7 +484,7 @@ __global__ __launch_bounds__(kDT) void dense_wgrad_mfma(WgdArgs a, float* __rest
         const int nl = gni * C::NCOLS + 32 * u + li;  // column within the workgroup
         const int ci = nl / C::TAPS, tap = nl % C::TAPS;
         const int kh = tap / C::KS, kw = tap % C::KS;
-        bbase[u] = ci * C::PPP + kh * C::PCP + kw + kk * C::LS;  // + r*LS*PCP + c*LS
+        bbase[u] = ci * C::PPLANE + kh * C::PC + kw + kk * C::LS;  // + r*LS*PC + c*LS
     }
 
     f16v acc[NT];
@@ -531,9 +526,9 @@ __global__ __launch_bounds__(kDT) void dense_wgrad_mfma(WgdArgs a, float* __rest
 #pragma unroll
         for (int k = 0; k < C::NPG; ++k) {
             const int e = tid + kDT * k;
-            const int ci = e / C::PPP, rem = e % C::PPP;
-            const int r = rem / C::PCP, c = rem % C::PCP;
-            prel[g][k] = (gc0 + ci < Cp && e < C::CPG * C::PPP && r < C::PR && c < C::PC)
+            const int ci = e / C::PPLANE, rem = e % C::PPLANE;
+            const int r = rem / C::PC, c = rem % C::PC;
+            prel[g][k] = (gc0 + ci < Cp && e < C::CPG * C::PPLANE)
                              ? ((unsigned)(gc0 + ci - cb) * (unsigned)HWs + (unsigned)(r * C::GS * a.Ws + c * C::GS)) * 4u
                              : OOB_REL;
         }
@@ -584,21 +579,20 @@ __global__ __launch_bounds__(kDT) void dense_wgrad_mfma(WgdArgs a, float* __rest
             if (pfull && gwhole[g]) {
 #pragma unroll
                 for (int k = 0; k < C::NPG; ++k)
-                    if ((k + 1) * kDT <= C::CPG * C::PPP || tq + kDT * k < C::CPG * C::PPP)
-                        glds(rp, lds + g * C::CPG * C::PPP + wb + kDT * k, pbase + prel[g][k]);
+                    if ((k + 1) * kDT <= C::CPG * C::PPLANE || tq + kDT * k < C::CPG * C::PPLANE)
+                        glds(rp, lds + g * C::CPG * C::PPLANE + wb + kDT * k, pbase + prel[g][k]);
                 continue;
             }
 #pragma unroll
             for (int k = 0; k < C::NPG; ++k) {
                 const int e = tq + kDT * k;
-                if ((k + 1) * kDT <= C::CPG * C::PPP || e < C::CPG * C::PPP) {
-                    const int ci = e / C::PPP, rem = e % C::PPP;
-                    const int r = rem / C::PCP, c = rem % C::PCP;
+                if ((k + 1) * kDT <= C::CPG * C::PPLANE || e < C::CPG * C::PPLANE) {
+                    const int ci = e / C::PPLANE, rem = e % C::PPLANE;
+                    const int r = rem / C::PC, c = rem % C::PC;
                     const int gc = gc0 + ci, iy = iy0 + r * C::GS, ix = ix0 + c * C::GS;
-                    const bool ok = gc < Cp && r < C::PR && c < C::PC && (unsigned)iy < (unsigned)a.Hs &&
-                                    (unsigned)ix < (unsigned)a.Ws;  // (padding slots read 0)
+                    const bool ok = gc < Cp && (unsigned)iy < (unsigned)a.Hs && (unsigned)ix < (unsigned)a.Ws;
                     const unsigned pix = (unsigned)(iy * a.Ws + ix);
-                    float* dst = lds + g * C::CPG * C::PPP + wb + kDT * k;
+                    float* dst = lds + g * C::CPG * C::PPLANE + wb + kDT * k;
                     if (gwhole[g]) {
                         glds(rp, dst, ok ? ((unsigned)(gc - cb) * (unsigned)HWs + pix) * 4u : OOB);
                     } else if (gc < a.pC0) {  // the group's channels come from both sources: each lane one
@@ -649,7 +643,7 @@ __global__ __launch_bounds__(kDT) void dense_wgrad_mfma(WgdArgs a, float* __rest
 #pragma unroll 1
         for (int sg = 0; sg < C::PPW / 16; ++sg) {
             const int q = q0 + 16 * sg, r = q / C::TW, c = q % C::TW;
-            const int aoff = abase + q, boff = r * C::LS * C::PCP + c * C::LS;
+            const int aoff = abase + q, boff = r * C::LS * C::PC + c * C::LS;
 #pragma unroll 2
             for (int j = 0; j < 8; ++j) {
                 const float av = lb[aoff + 2 * j];
