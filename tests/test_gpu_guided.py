@@ -1,6 +1,9 @@
 """GPU: the RGB-guided model (SETP2_BP_TRAIN / EXPORT) with step 1 on libnconv, against the reference's
 golden outputs (480x640, f5) and against the oracle at KITTI-like shapes with the generalized crop.
-Tolerance: |gpu - ref| <= 1e-4*|ref| + 1e-3 (fp32 conv stacks of depth ~15 on values up to ~80)."""
+Tolerance: |gpu - ref| <= 1e-4*|ref| + 1e-5 (fp32 conv stacks of depth ~15 on values up to ~80): the
+north star's 1e-4 relative down to 0.1 m of depth. Measured on the GPU (round 5, every comparison
+of this file, NCONV_TOL_REPORT): max |gpu - ref| 5.0e-5, and at most 6.7e-7 beyond 1e-4*|ref|
+(profiles/r5_guided_output_error_margins.tsv) -- the absolute term has a 15x margin (was 1e-3)."""
 import os
 
 import numpy as np
@@ -17,7 +20,7 @@ def _close(got, ref, what):
     got = got.double().cpu()
     ref = torch.as_tensor(np.asarray(ref)).double() if not torch.is_tensor(ref) else ref.double().cpu()
     err = (got - ref).abs()
-    bound = 1e-4 * ref.abs() + 1e-3
+    bound = 1e-4 * ref.abs() + 1e-5
     rep = os.environ.get("NCONV_TOL_REPORT")
     if rep:  # (tolerance study) the absolute term each comparison needs beside 1e-4 relative
         with open(rep, "a") as fh:
