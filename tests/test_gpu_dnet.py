@@ -2,8 +2,10 @@
 models/step1.py:51-94) — forward at several sizes and both crops, training-mode EnforcePos drift,
 and the fwd+bwd gradients of a step-1 training loss.
 
-Tolerances: forward elementwise |gpu-ref| <= 1e-4*|ref| + 1e-4 (fp32 kernels vs fp64 oracle; the
-absolute term covers outputs near 0); gradients normwise max|gpu-ref|/max|ref| <= 1e-3.
+Tolerances: forward elementwise |gpu-ref| <= 1e-4*|ref| + 1e-6 (fp32 kernels vs fp64 oracle: the
+north star's 1e-4 relative; measured in round 5 every element of every case, bf16x3 included, lies
+below 1e-4*|ref| - 1e-6, profiles/r5_dnet_output_error_margins.tsv; the absolute term was 1e-4);
+gradients normwise max|gpu-ref|/max|ref| <= 1e-3.
 """
 import os
 import sys
@@ -59,7 +61,7 @@ def test_dnet_eval_forward(nconv_amd, gpu, crop, B, H, W):
     assert out.shape == ref.shape, (out.shape, ref.shape)
     err = (out - ref).abs()
     _report(f"eval {crop} {B}x{H}x{W}", err, ref)
-    bound = 1e-4 * ref.abs() + 1e-4
+    bound = 1e-4 * ref.abs() + 1e-6
     assert (err <= bound).all(), f"max err {err.max():.3e} ratio {(err / bound).max():.3f}"
 
 
@@ -379,7 +381,7 @@ def test_dnet_full_size_vs_oracle(nconv_amd, gpu, fwd_math, B, H, W, crop):
     assert out.shape == ref.shape == (B, 1) + ((H, W) if crop == "generalized" else (min(480, H + 1), min(640, W + 1)))
     err = (out - ref).abs()
     _report(f"full {fwd_math} {crop} {B}x{H}x{W}", err, ref)
-    bound = 1e-4 * ref.abs() + 1e-4
+    bound = 1e-4 * ref.abs() + 1e-6
     assert (err <= bound).all(), f"max err {err.max():.3e} ratio {(err / bound).max():.3f}"
 
 
