@@ -403,6 +403,16 @@ __global__ __launch_bounds__(kDT) void conv3x3_c1(const float* __restrict__ x, i
 // from a per-wave base. Each wave writes its partial [32][NT*32] to slice ks * RG + row-group;
 // dense_wgrad_reduce adds the slices in a fixed order (deterministic, no float atomics).
 // ------------------------------------------------------------------------------------------------
+#ifndef NCONV_WGD_TALL
+#define NCONV_WGD_TALL 1
+#endif
+// pixel tile rows of the weight gradient: 4 x 32 (2 x 32 where the strided patch is tall: 3x3 s2,
+// transposed); the stride-1 3x3 with one m-tile per workgroup takes 8 x 32 (half the staging
+// instructions per MFMA; two workgroups still share a CU's LDS)
+__host__ __device__ constexpr int wgd_th(int kind, int s, int gm) {
+    return (kind == NCONV_DENSE_TRANSPOSED_4X4 || (kind == NCONV_DENSE_3X3 && s == 2)) ? 2
+           : (NCONV_WGD_TALL && kind == NCONV_DENSE_3X3 && gm == 1) ? 8 : 4;
+}
 __host__ __device__ constexpr int wgd_ntb(int kind) {
     return kind == NCONV_DENSE_3X3 ? 9 : (kind == NCONV_DENSE_1X1 ? 2 : 8);
 }
@@ -420,8 +430,8 @@ struct WgdCfg {
     static constexpr int CPG = NCOLS % TAPS == 0 ? NCOLS / TAPS : (NCOLS - 1) / TAPS + 2;
     static constexpr int CPB = GN * CPG;   // patch channels staged per workgroup
     static constexpr int GB = GM * GN, RG = 4 / GB;  // groups per workgroup, row-groups (waves per group)
-    // pixel tile: 4 x 32 (2 x 32 where the strided patch is tall: 3x3 s2, transposed)
-    static constexpr int TH = (TR || (KIND == NCONV_DENSE_3X3 && S == 2)) ? 2 : 4, TW = 32, NPX = TH * TW;
+    // pixel tile: wgd_th x 32
+    static constexpr int TH = wgd_th(KIND, S, GM), TW = 32, NPX = TH * TW;
     static constexpr int PPW = NPX / RG;   // pixels per wave per tile (a multiple of 16)
     // patch geometry: LDS step between neighbouring pixels (1x1 stages only the sampled
     // positions), global step between neighbouring LDS columns, patch origin = pixel * OS - PAD
@@ -930,7 +940,7 @@ static WgdPlan wgrad_plan(const nconv_dense_wgrad& g) {
     // (LDS-DMA staging: one n-group per workgroup, so two workgroups fit a CU's LDS)
     pl.gn = 1;
     pl.rg = 4 / (pl.gm * pl.gn);
-    const int th = (tr || (g.kind == NCONV_DENSE_3X3 && g.stride == 2)) ? 2 : 4;
+    const int th = wgd_th(g.kind, g.stride, pl.gm);
     a.ntx = (a.Wp + 31) / 32;
     a.nty = (a.Hp + th - 1) / th;
     a.ntiles = (long long)g.B * a.ntx * a.nty;
