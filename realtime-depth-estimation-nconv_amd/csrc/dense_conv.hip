@@ -403,15 +403,11 @@ __global__ __launch_bounds__(kDT) void conv3x3_c1(const float* __restrict__ x, i
 // from a per-wave base. Each wave writes its partial [32][NT*32] to slice ks * RG + row-group;
 // dense_wgrad_reduce adds the slices in a fixed order (deterministic, no float atomics).
 // ------------------------------------------------------------------------------------------------
-#ifndef NCONV_WGD_TALL
-#define NCONV_WGD_TALL 1
-#endif
-// pixel tile rows of the weight gradient: 4 x 32 (2 x 32 where the strided patch is tall: 3x3 s2,
-// transposed); the stride-1 3x3 with one m-tile per workgroup takes 8 x 32 (half the staging
-// instructions per MFMA; two workgroups still share a CU's LDS)
-__host__ __device__ constexpr int wgd_th(int kind, int s, int gm) {
-    return (kind == NCONV_DENSE_TRANSPOSED_4X4 || (kind == NCONV_DENSE_3X3 && s == 2)) ? 2
-           : (NCONV_WGD_TALL && kind == NCONV_DENSE_3X3 && gm == 1) ? 8 : 4;
+// pixel tile rows of the weight gradient: 4 x 32, 2 x 32 where the strided patch is tall (3x3 s2,
+// transposed). (8 x 32 for the stride-1 3x3 with one m-tile per workgroup measured 1-2 % slower:
+// profiles/r5_ab_dense_wgrad_tall_tiles.log)
+__host__ __device__ constexpr int wgd_th(int kind, int s, int) {
+    return (kind == NCONV_DENSE_TRANSPOSED_4X4 || (kind == NCONV_DENSE_3X3 && s == 2)) ? 2 : 4;
 }
 __host__ __device__ constexpr int wgd_ntb(int kind) {
     return kind == NCONV_DENSE_3X3 ? 9 : (kind == NCONV_DENSE_1X1 ? 2 : 8);
