@@ -190,7 +190,8 @@ struct VecOf<2> { typedef f2 T; };
 template <int CIN, int TH, int TW>
 struct HeadLds {
     static constexpr int RH = TH + 4, RW = TW + 4, RN = RH * RW;  // the tile's 5x5-window region
-    static constexpr int F2 = CIN * TH * TW + RN;                // {gN1, gD1} planes + sample list
+    static constexpr int NPL = CIN / 2;  // {gN1, gD1} planes held at once (22 KB of LDS, not 38)
+    static constexpr int F2 = NPL * TH * TW + RN;                 // {gN1, gD1} planes + sample list
 };
 
 template <int CIN, int TH, int TW>
@@ -199,8 +200,10 @@ __device__ void head_wgrad_epilogue(const LayerDev& d, const BwdArgs& a, int b, 
     static_assert(CIN == 8, "nconv1 has 8 output channels");
     using H = HeadLds<CIN, TH, TW>;
     constexpr int RW = H::RW, RN = H::RN;
-    f2* gn = smem;                                       // [CIN][TH][TW]
-    f2* qlist = smem + CIN * TH * TW;                    // {row << 8 | col, S} of the samples
+    constexpr int NPL = H::NPL;
+    f2* gn = smem;                                       // [NPL][TH][TW]
+    f2* qlist = smem + NPL * TH * TW;                    // {row << 8 | col, S} of the samples
+    f4 vh[CIN - NPL > 0 ? CIN - NPL : 1];                // the second half's {gN1, gD1} (NPL < CIN)
     __shared__ int wtot[4];
     __shared__ float red[4][2 * CIN];
     const nconv_layer& L = d.L;
@@ -239,7 +242,8 @@ __device__ void head_wgrad_epilogue(const LayerDev& d, const BwdArgs& a, int b, 
             }
             v[j] = (f2){gN, gD};
         }
-        *reinterpret_cast<f4*>(gn + (i * TH + ty) * TW + tx) = (f4){v[0].x, v[0].y, v[1].x, v[1].y};
+        if (i < NPL) *reinterpret_cast<f4*>(gn + (i * TH + ty) * TW + tx) = (f4){v[0].x, v[0].y, v[1].x, v[1].y};
+        else vh[i - NPL] = (f4){v[0].x, v[0].y, v[1].x, v[1].y};
     }
     // the depth samples (c0 = 1) of the window region, listed in (thread, element) order
     const float* Sp = a.hS + (size_t)b * L.H * L.W;
@@ -294,24 +298,38 @@ __device__ void head_wgrad_epilogue(const LayerDev& d, const BwdArgs& a, int b, 
         }
     __syncthreads();
     float* out = a.hpart + (size_t)blockIdx.x * kHeadStride;
-    if (tid < kHeadNw) {
-        const int o = tid / 25, tap = tid - o * 25, kh = tap / 5, kw = tap - kh * 5;
-        const f2* g = gn + o * TH * TW;
-        float sn = 0.f, sd = 0.f;
-        for (int n = 0; n < total; ++n) {
-            const f2 q = qlist[n];
-            const int qi = __builtin_bit_cast(int, q.x);
-            const int pr = (qi >> 8) - kh, pc = (qi & 255) - kw;  // p = q - (tap - 2), region origin -2
-            if ((unsigned)pr < (unsigned)TH && (unsigned)pc < (unsigned)TW) {
-                const f2 v = g[pr * TW + pc];
-                sn = fmaf(v.x, q.y, sn);
-                sd += v.y;
+    // thread (o, tap) sums its tap over the sample list; with NPL < CIN one half of the channels
+    // at a time (the LDS of four planes instead of eight: more workgroups per CU)
+    auto tap_sums = [&](int o0) __attribute__((always_inline)) {
+        const int t = tid;
+        if (t < NPL * 25) {
+            const int ol = t / 25, tap = t - ol * 25, kh = tap / 5, kw = tap - kh * 5;
+            const f2* g = gn + ol * TH * TW;
+            float sn = 0.f, sd = 0.f;
+            for (int n = 0; n < total; ++n) {
+                const f2 q = qlist[n];
+                const int qi = __builtin_bit_cast(int, q.x);
+                const int pr = (qi >> 8) - kh, pc = (qi & 255) - kw;  // p = q - (tap - 2), region origin -2
+                if ((unsigned)pr < (unsigned)TH && (unsigned)pc < (unsigned)TW) {
+                    const f2 v = g[pr * TW + pc];
+                    sn = fmaf(v.x, q.y, sn);
+                    sd += v.y;
+                }
             }
+            out[o0 * 25 + t] = sn + sd;
         }
-        out[tid] = sn + sd;
-    } else if (tid < kHeadNw + 2 * CIN) {
+    };
+    tap_sums(0);
+    if (tid >= kHeadNw && tid < kHeadNw + 2 * CIN) {
         const int k = tid - kHeadNw;
         out[tid] = ((red[0][k] + red[1][k]) + red[2][k]) + red[3][k];
+    }
+    if constexpr (NPL < CIN) {
+        __syncthreads();  // every tap sum of the first half is done with its planes
+#pragma unroll
+        for (int i = NPL; i < CIN; ++i) *reinterpret_cast<f4*>(gn + ((i - NPL) * TH + ty) * TW + tx) = vh[i - NPL];
+        __syncthreads();
+        tap_sums(NPL);
     }
 }
 
@@ -369,8 +387,23 @@ __global__ __launch_bounds__(kT) void dgrad_tiled(LayerDev d, BwdArgs a, float* 
 
     GS gs;
     gs.init(L, oh0, ow0, tid);
-    float va[GS::NV][GS::NE], vb[GS::NV][GS::NE];
+    constexpr bool ONE = GP;
+    float va[GS::NV][GS::NE], vb[ONE ? 1 : GS::NV][GS::NE];
     gs.load(L, a, b, 0, va);
+    if constexpr (ONE) {
+        // pooled stager (seven values per element): one plane ahead, one register set -- 85
+        // instead of 105 VGPRs, five waves per SIMD instead of four (with the head epilogue's
+        // 22 KB of LDS); nconv2's input gradient 353 -> 332 us alone, the graphed step within
+        // noise (the weight gradients share the CUs), profiles/r5_ab_dgrad_occupancy.log
+#pragma unroll 1
+        for (int o = 0; o < COUT; ++o) {
+            const int bufi = o & 1;
+            gs.store(L, o, va, tile + bufi * GS::PLANE_STRIDE);
+            __syncthreads();
+            gs.load(L, a, b, o + 1 < COUT ? o + 1 : COUT - 1, va);
+            fma_plane(o, bufi);
+        }
+    } else {
     if (COUT > 1) gs.load(L, a, b, 1, vb);
 #pragma unroll 1
     for (int o = 0; o < COUT; o += 2) {
@@ -384,6 +417,7 @@ __global__ __launch_bounds__(kT) void dgrad_tiled(LayerDev d, BwdArgs a, float* 
             gs.load(L, a, b, o + 3 < COUT ? o + 3 : COUT - 1, vb);
             fma_plane(o + 1, 1);
         }
+    }
     }
 
     // ---- epilogue: gx = G_xc*c, gc = G_c + G_xc*x, routed through the glue's backward ----
