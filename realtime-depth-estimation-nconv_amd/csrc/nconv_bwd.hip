@@ -628,17 +628,31 @@ __global__ __launch_bounds__(kT) void dgrad_phase(LayerDev d, BwdArgs a, const f
 
     GS gs;
     gs.init(L, oh0, ow0, tid);
-    float va[4][GS::NE], vb[4][GS::NE];
+    // one plane ahead with one register set (as dgrad_tiled's pooled stager): 79 instead of 109
+    // VGPRs, six waves per SIMD instead of four; the tail's input gradient 235 -> 200 us alone
+    // (profiles/r5_ab_dgrad_phase_one_ahead.log)
+    constexpr bool ONE = true;
+    float va[4][GS::NE], vb[ONE ? 1 : 4][GS::NE];
     if constexpr (T7) {
         float v7[3][GS::NE];
         gs.t7_load(L, a, b, oh0, ow0, tid, v7);
         gs.load(L, a, b, 0, va);
-        gs.load(L, a, b, 1, vb);
+        if constexpr (!ONE) gs.load(L, a, b, 1, vb);
         gs.t7_form(a, v7);
     } else {
         gs.load(L, a, b, 0, va);
-        gs.load(L, a, b, 1, vb);
+        if constexpr (!ONE) gs.load(L, a, b, 1, vb);
     }
+    if constexpr (ONE) {
+#pragma unroll 1
+        for (int o = 0; o < 8; ++o) {
+            const int bufi = o & 1;
+            gs.store(L, o, va, tile + bufi * GS::PLANE_STRIDE, T7 ? a.t7w[o] : 0.f);
+            __syncthreads();
+            gs.load(L, a, b, o + 1 < 8 ? o + 1 : 7, va);
+            fma_plane(o, bufi);
+        }
+    } else {
 #pragma unroll 1
     for (int o = 0; o < 8; o += 2) {
         gs.store(L, o, va, tile, T7 ? a.t7w[o] : 0.f);
@@ -649,6 +663,7 @@ __global__ __launch_bounds__(kT) void dgrad_phase(LayerDev d, BwdArgs a, const f
         __syncthreads();
         gs.load(L, a, b, o + 3 < 8 ? o + 3 : 7, vb);
         fma_plane(o + 1, 1);
+    }
     }
 
     const bool accm = a.accumulate != 0;

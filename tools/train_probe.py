@@ -22,15 +22,18 @@ def main():
         i = args.index("--steps")
         steps = int(args[i + 1])
         del args[i:i + 2]
+    eager = "--eager" in args
+    if eager:
+        args.remove("--eager")
     for a in args:
         k, v = a.split("=")
         obj = m.dnet
         if k.startswith("DNET."):  # a DNET class attribute (merged_prologue, crop_in_tail, ...)
             obj, k = m.DNET, k[5:]
         assert hasattr(obj, k), k
-        setattr(obj, k, bool(int(v)))
+        setattr(obj, k, bool(int(v)) if isinstance(getattr(obj, k), bool) else int(v))
     dev = torch.device("cuda:0")
-    step = bench.make_train_step(m, dev, 8, 352, 1216, 0, graph=True)
+    step = bench.make_train_step(m, dev, 8, 352, 1216, 0, graph=not eager)
     for _ in range(3):
         step()
     torch.cuda.synchronize()
@@ -40,7 +43,7 @@ def main():
         step()
     e1.record()
     e1.synchronize()
-    print(f"train step {' '.join(args) or 'default'}: {e0.elapsed_time(e1) / steps:.3f} ms", flush=True)
+    print(f"train step{' eager' if eager else ''} {' '.join(args) or 'default'}: {e0.elapsed_time(e1) / steps:.3f} ms", flush=True)
 
 
 if __name__ == "__main__":
