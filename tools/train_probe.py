@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """Training-step probe (developer tool, GPU): the bench's graphed config-2 training step
 (B=8 352x1216) with dnet's module switches set from the command line, e.g.
-    python3 tools/train_probe.py WGRAD_STREAM=0 FUSE_HEAD_BWD=0 [--steps 20]
-prints ms per step; run under rocprofv3 --kernel-trace for the per-kernel split."""
+    python3 tools/train_probe.py WGRAD_STREAM=0 FUSE_HEAD_BWD=0 [--steps 20] [--eager]
+prints ms per step (hipGraph-replayed; --eager: the eager step); run under rocprofv3 --kernel-trace
+for the per-kernel split."""
 import os
 import sys
 
