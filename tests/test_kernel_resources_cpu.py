@@ -67,3 +67,36 @@ def test_exact_head_has_no_scratch_and_few_spills(tmp_path):
         assert v.get("private_segment_fixed_size", 0) == 0, (k, v)
         assert v.get("vgpr_spill_count", 0) == 0, (k, v)
         assert v.get("sgpr_spill_count", 0) <= 24, (k, v)
+
+
+def _kernel_blocks(obj, tmp):
+    """{kernel name: {field: int}} from the code object's metadata, split per kernel entry (fields
+    that sort before .name, such as .group_segment_fixed_size, stay with their own kernel)."""
+    fat, co = os.path.join(tmp, "f.bin"), os.path.join(tmp, "k.co")
+    subprocess.run([f"{LLVM}/llvm-objcopy", "-O", "binary", "--only-section=.hip_fatbin", obj, fat], check=True)
+    subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o",
+                    "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--input={fat}", f"--output={co}"], check=True)
+    notes = subprocess.run([f"{LLVM}/llvm-readelf", "--notes", co], capture_output=True, text=True, check=True).stdout
+    out = {}
+    for blk in re.split(r"\n\s+- \.agpr_count", notes):
+        m = re.search(r"\.name:\s+(\S+)", blk)
+        if m:
+            out[m.group(1)] = {k: int(v) for k, v in re.findall(r"\.(\w+):\s+(\d+)\s*$", blk, re.M)}
+    return out
+
+
+@pytest.mark.skipif(not glob.glob(os.path.join(BUILD, "*.o")) or not shutil.which(f"{LLVM}/llvm-readelf"),
+                    reason="needs the built objects (build.py) and the ROCm llvm tools")
+def test_training_input_gradients_occupancy(tmp_path):
+    """nconv2's input gradient (dgrad_tiled, pooled stager + fused nconv1 weight gradient) at five
+    waves per SIMD and the tail's (dgrad_phase) at six: the one-plane-ahead stagers' register budgets
+    and the head epilogue's halved LDS (profiles/r5_ab_dgrad_occupancy.log,
+    r5_ab_dgrad_phase_one_ahead.log). A change that pushes them back to four waves shows here."""
+    md = _kernel_blocks(os.path.join(BUILD, "nconv_bwd.hip.o"), str(tmp_path))
+    head = [v for k, v in md.items() if "dgrad_tiledILi8ELi8ELi5ELi0ELb1ELb1E" in k]
+    phase = [v for k, v in md.items() if "dgrad_phaseILi4ELb1E" in k]
+    assert len(head) == 1 and len(phase) == 1, sorted(md)
+    assert head[0]["vgpr_count"] <= 96 and head[0]["group_segment_fixed_size"] <= 160 * 1024 // 5, head[0]
+    assert phase[0]["vgpr_count"] <= 80 and phase[0]["group_segment_fixed_size"] <= 160 * 1024 // 6, phase[0]
+    for v in head + phase:
+        assert v.get("private_segment_fixed_size", 0) == 0, v
