@@ -72,11 +72,7 @@ __global__ __launch_bounds__(NTH) void fwd_tiled(LayerDev d, float* __restrict__
     // SGPRs (s_load) right before use. Unrolling lets the compiler hoist every weight of the plane
     // into SGPRs, which spills them through v_writelane.
     const f2* rowbase = &tile[ty * C::IWP + tx];
-    auto fma_plane = [&](int ci, int bufi) {
-        const f2* row = rowbase + bufi * kStride;
-        const float* wr = wgt + (size_t)ci * K * K;  // weights of (ci, kh) are K contiguous floats
-#pragma unroll 1
-        for (int q = 0; q < K; ++q, row += C::IWP, wr += K) {
+    auto row_step = [&](const f2* row, const float* wr) __attribute__((always_inline)) {
             f2 v[C::NV];
             if constexpr (C::P % 2 == 0) {  // even pixel offset: 16-B aligned ds_read_b128
 #pragma unroll
@@ -99,6 +95,21 @@ __global__ __launch_bounds__(NTH) void fwd_tiled(LayerDev d, float* __restrict__
 #pragma unroll
                     for (int j = 0; j < C::P; ++j) acc[o][j] = __builtin_elementwise_fma(w2, v[j + kw], acc[o][j]);
                 }
+    };
+#ifndef NCONV_TILED_UNROLL_SMALL
+#define NCONV_TILED_UNROLL_SMALL 0
+#endif
+    auto fma_plane = [&](int ci, int bufi) {
+        const f2* row = rowbase + bufi * kStride;
+        const float* wr = wgt + (size_t)ci * K * K;  // weights of (ci, kh) are K contiguous floats
+        if constexpr (NCONV_TILED_UNROLL_SMALL && CO <= 2) {
+            // two output channels per thread (the channel-split small layers): the plane's 2 K*K
+            // weights fit the SGPRs, so the rows are unrolled and every weight load issued up front
+#pragma unroll
+            for (int q = 0; q < K; ++q) row_step(row + q * C::IWP, wr + q * K);
+        } else {
+#pragma unroll 1
+            for (int q = 0; q < K; ++q, row += C::IWP, wr += K) row_step(row, wr);
         }
     };
 
