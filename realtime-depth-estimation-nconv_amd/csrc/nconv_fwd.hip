@@ -96,15 +96,17 @@ __global__ __launch_bounds__(NTH) void fwd_tiled(LayerDev d, float* __restrict__
                     for (int j = 0; j < C::P; ++j) acc[o][j] = __builtin_elementwise_fma(w2, v[j + kw], acc[o][j]);
                 }
     };
-#ifndef NCONV_TILED_UNROLL_SMALL
-#define NCONV_TILED_UNROLL_SMALL 0
+#ifndef NCONV_TILED_UNROLL_CO
+#define NCONV_TILED_UNROLL_CO 2
 #endif
     auto fma_plane = [&](int ci, int bufi) {
         const f2* row = rowbase + bufi * kStride;
         const float* wr = wgt + (size_t)ci * K * K;  // weights of (ci, kh) are K contiguous floats
-        if constexpr (NCONV_TILED_UNROLL_SMALL && CO <= 2) {
+        if constexpr (CO <= NCONV_TILED_UNROLL_CO) {
             // two output channels per thread (the channel-split small layers): the plane's 2 K*K
             // weights fit the SGPRs, so the rows are unrolled and every weight load issued up front
+            // (their latency was exposed: < 1 wave per SIMD at the eighth resolution); down3 17 ->
+            // 13 us, down2 26.6 -> 24.6, forward +1.1 % (profiles/r5_ab_small_layers_unrolled.log)
 #pragma unroll
             for (int q = 0; q < K; ++q) row_step(row + q * C::IWP, wr + q * K);
         } else {
