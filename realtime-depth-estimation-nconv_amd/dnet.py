@@ -32,6 +32,62 @@ LAYERS = ("nconv1", "nconv2", "nconv_down1", "nconv_down2", "nconv_down3", "ncon
           "nconv6", "nconv7")
 
 
+# Training forward in batch slices on this many streams (DNETFn.forward): the exact-fp32 pooled
+# graph with the fused head and tail only; 1 = one launch per layer over the whole batch
+TRAIN_FWD_STREAMS = int(os.environ.get("NCONV_TRAIN_FWD_STREAMS", "2"))
+_TRAIN_FWD_STREAMS = {}
+
+
+def _train_fwd_streams(device, n):
+    key = (device.index, n)
+    if key not in _TRAIN_FWD_STREAMS:
+        _TRAIN_FWD_STREAMS[key] = [torch.cuda.Stream(device=device) for _ in range(n)]
+    return _TRAIN_FWD_STREAMS[key]
+
+
+def _tail_exact_up(sp, S):
+    """nconv6's skip input (nconv2's grid, S's) is exactly twice nconv5's grid (the pooled one)."""
+    return S.shape[2] % 2 == 0 and S.shape[3] % 2 == 0
+
+
+def _train_fwd_chain(sp, W, S, w21, wph, crop, out, pooled=True):
+    """DNETFn's forward launches over S's frames; out: None (fresh tensors) or a callable handing
+    out each launch's output tensors (nconv._outputs). Returns x1, c1, ..., x9, c9, then the pooled
+    copies and argmax codes (pooled graph)."""
+    w4, w5, w6 = (None, None, None) if wph is None else tuple(wph)
+    if pooled:
+        spp = [dataclasses.replace(sp[k], mode=_lib.PLAIN) for k in (2, 3, 4)]
+        if FUSE_HEAD_FWD:  # nconv1 inside nconv2's tile, nconv1's outputs written for the backward
+            if w21 is None:
+                w21 = head_weights(sp[0], sp[1], S, *W[0], *W[1])
+            x2, c2, p2x, p2c, a2, x1, c1 = layer_forward_head(sp[0], sp[1], S, *W[0], *W[1], w21, train=True,
+                                                              out=out)
+        else:
+            x1, c1 = layer_forward_raw(sp[0], S, None, None, None, *W[0], out=out)
+            x2, c2, p2x, p2c, a2 = layer_forward_pooled(sp[1], x1, c1, None, None, *W[1], out=out, argmax=True)
+        x3, c3, p3x, p3c, a3 = layer_forward_pooled(spp[0], p2x, p2c, None, None, *W[2], out=out, argmax=True)
+        x4, c4, p4x, p4c, a4 = layer_forward_pooled(spp[1], p3x, p3c, None, None, *W[3], out=out, argmax=True)
+        x5, c5 = layer_forward_raw(spp[2], p4x, p4c, None, None, *W[4], out=out)
+        pools = (p2x, p2c, a2, p3x, p3c, a3, p4x, p4c, a4)
+    else:
+        x1, c1 = layer_forward_raw(sp[0], S, None, None, None, *W[0], out=out)
+        x2, c2 = layer_forward_raw(sp[1], x1, c1, None, None, *W[1], out=out)
+        x3, c3 = layer_forward_raw(sp[2], x2, c2, None, None, *W[2], out=out)
+        x4, c4 = layer_forward_raw(sp[3], x3, c3, None, None, *W[3], out=out)
+        x5, c5 = layer_forward_raw(sp[4], x4, c4, None, None, *W[4], out=out)
+        pools = ()
+    x6, c6 = layer_forward_raw(sp[5], x4, c4, x5, c5, *W[5], out=out, wphase=w4)
+    x7, c7 = layer_forward_raw(sp[6], x3, c3, x6, c6, *W[6], out=out, wphase=w5)
+    if pooled and FUSE_TAIL_FWD and w6 is not None and x2.shape[2:] == tuple(2 * v for v in x7.shape[2:]):
+        x8, c8, x9, c9 = _tail_train(sp[7], sp[8], x2, c2, x7, c7, W[7], W[8], w6, crop, out=out)
+    elif crop is not None:
+        raise RuntimeError("DNETFn: a cropped output needs the fused training tail")
+    else:
+        x8, c8 = layer_forward_raw(sp[7], x2, c2, x7, c7, *W[7], out=out, wphase=w6)
+        x9, c9 = layer_forward_raw(sp[8], x8, c8, None, None, *W[8], out=out)
+    return (x1, c1, x2, c2, x3, c3, x4, c4, x5, c5, x6, c6, x7, c7, x8, c8, x9, c9, *pools)
+
+
 class DNETFn(torch.autograd.Function):
     """Autograd node of the whole 9-layer DNET graph (training path). The backward runs the layer
     backwards in reverse order itself. Inputs: specs, capture (dict or None), S, then (weight, bias,
@@ -63,39 +119,49 @@ class DNETFn(torch.autograd.Function):
         wph = p[27] if len(p) > 27 and p[27] is not None else None
         w21 = p[28] if len(p) > 28 else None
         ctx.wbox = p[29] if len(p) > 29 else None
-        w4, w5, w6 = (None, None, None) if wph is None else tuple(wph)
+        w6 = None if wph is None else wph[2]
         sp = specs
         pooled = _materialise_pool(S)
-        if pooled:
-            spp = [dataclasses.replace(sp[k], mode=_lib.PLAIN) for k in (2, 3, 4)]
-            if FUSE_HEAD_FWD:  # nconv1 inside nconv2's tile, nconv1's outputs written for the backward
-                if w21 is None:
-                    w21 = head_weights(sp[0], sp[1], S, *W[0], *W[1])
-                x2, c2, p2x, p2c, a2, x1, c1 = layer_forward_head(sp[0], sp[1], S, *W[0], *W[1], w21, train=True)
-            else:
-                x1, c1 = layer_forward_raw(sp[0], S, None, None, None, *W[0])
-                x2, c2, p2x, p2c, a2 = layer_forward_pooled(sp[1], x1, c1, None, None, *W[1], argmax=True)
-            x3, c3, p3x, p3c, a3 = layer_forward_pooled(spp[0], p2x, p2c, None, None, *W[2], argmax=True)
-            x4, c4, p4x, p4c, a4 = layer_forward_pooled(spp[1], p3x, p3c, None, None, *W[3], argmax=True)
-            x5, c5 = layer_forward_raw(spp[2], p4x, p4c, None, None, *W[4])
-            pools = (p2x, p2c, a2, p3x, p3c, a3, p4x, p4c, a4)
-        else:
-            x1, c1 = layer_forward_raw(sp[0], S, None, None, None, *W[0])
-            x2, c2 = layer_forward_raw(sp[1], x1, c1, None, None, *W[1])
-            x3, c3 = layer_forward_raw(sp[2], x2, c2, None, None, *W[2])
-            x4, c4 = layer_forward_raw(sp[3], x3, c3, None, None, *W[3])
-            x5, c5 = layer_forward_raw(sp[4], x4, c4, None, None, *W[4])
-            pools = ()
-        x6, c6 = layer_forward_raw(sp[5], x4, c4, x5, c5, *W[5], wphase=w4)
-        x7, c7 = layer_forward_raw(sp[6], x3, c3, x6, c6, *W[6], wphase=w5)
         ctx.crop = crop
-        if pooled and FUSE_TAIL_FWD and w6 is not None and x2.shape[2:] == tuple(2 * v for v in x7.shape[2:]):
-            x8, c8, x9, c9 = _tail_train(sp[7], sp[8], x2, c2, x7, c7, W[7], W[8], w6, crop)
-        elif crop is not None:
-            raise RuntimeError("DNETFn: a cropped output needs the fused training tail")
+        B = S.shape[0]
+        nst = max(1, min(int(TRAIN_FWD_STREAMS), B))
+        if (pooled and FUSE_HEAD_FWD and FUSE_TAIL_FWD and w6 is not None and nst > 1 and
+                _tail_exact_up(sp, S)):
+            # the batch in nst slices, one stream each, every launch writing its rows of full-batch
+            # tensors (allocated by the first slice's launches): the slices' kernels overlap as the
+            # inference split's do; each frame's arithmetic is unchanged (bitwise the one-stream pass)
+            if w21 is None:
+                w21 = head_weights(sp[0], sp[1], S, *W[0], *W[1])
+            bounds = [B * k // nst for k in range(nst + 1)]
+            full = []
+            cur = torch.cuda.current_stream(S.device)
+            side = _train_fwd_streams(S.device, nst - 1)
+            for st in side:
+                st.wait_stream(cur)
+            res = None
+            for k, st in enumerate([cur] + side):
+                b0, b1 = bounds[k], bounds[k + 1]
+                it = iter(range(1 << 30))
+
+                def rows(shapes, dtypes, device, b0=b0, b1=b1, it=it):
+                    out = []
+                    for sh, dt in zip(shapes, dtypes):
+                        i = next(it)
+                        if i == len(full):
+                            full.append(torch.empty((B,) + tuple(sh[1:]), device=device, dtype=dt))
+                        out.append(full[i][b0:b1])
+                    return out
+                with torch.cuda.stream(st):
+                    r = _train_fwd_chain(sp, W, S[b0:b1], w21, wph, crop, rows)
+                res = r if res is None else res
+            for st in side:
+                cur.wait_stream(st)
+            base = {t.data_ptr(): t for t in full}
+            (x1, c1, x2, c2, x3, c3, x4, c4, x5, c5, x6, c6, x7, c7, x8, c8, x9, c9, *pools) = [
+                base[t.data_ptr()] for t in res]
         else:
-            x8, c8 = layer_forward_raw(sp[7], x2, c2, x7, c7, *W[7], wphase=w6)
-            x9, c9 = layer_forward_raw(sp[8], x8, c8, None, None, *W[8])
+            (x1, c1, x2, c2, x3, c3, x4, c4, x5, c5, x6, c6, x7, c7, x8, c8, x9, c9, *pools) = \
+                _train_fwd_chain(sp, W, S, w21, wph, crop, None, pooled=pooled)
         if capture is not None:  # the three pooling stages' inputs (DNET.capture)
             capture.update(down1=(x2.detach(), c2.detach()), down2=(x3.detach(), c3.detach()),
                            down3=(x4.detach(), c4.detach()))
@@ -232,18 +298,17 @@ FUSE_TAIL_FWD = True  # ... and nconv6 + nconv7 as the fused tail (nconv_fwd_tai
 FUSED_BWD = frozenset(os.environ.get("NCONV_FUSED_BWD", "").split(",")) - {""}
 
 
-def _tail_train(sp6, sp7, x2, c2, x7, c7, W6, W7, w6, crop=None):
+def _tail_train(sp6, sp7, x2, c2, x7, c7, W6, W7, w6, crop=None, out=None):
     """nconv6 + nconv7 in one phase-tail launch writing nconv6's outputs and nconv7's whole
     (uncropped) output grid -- what the training backward reads (nconv_fwd_tail, crop0 = 0) -- or,
-    with crop = (h, w), nconv7's output cropped as step1.py:94 (crop0 = 1)."""
+    with crop = (h, w), nconv7's output cropped as step1.py:94 (crop0 = 1). out: None or a callable
+    as nconv._outputs takes."""
     L = sp6.descriptor(x2, c2, x7, c7, *W6, w6)
     (w7, b7, s7), p7 = W7, sp7.padding[0]
     B, dev = x2.shape[0], x2.device
-    x8 = torch.empty((B, sp6.cout, L.Ho, L.Wo), device=dev, dtype=torch.float32)
-    c8 = torch.empty_like(x8)
     (H9, W9), crop0 = ((L.Ho + 2 * p7, L.Wo + 2 * p7), 0) if crop is None else (tuple(crop), 1)
-    x9 = torch.empty((B, 1, H9, W9), device=dev, dtype=torch.float32)
-    c9 = torch.empty_like(x9)
+    sh8, sh9 = (B, sp6.cout, L.Ho, L.Wo), (B, 1, H9, W9)
+    x8, c8, x9, c9 = nconv._outputs(out, 4, (sh8, sh8, sh9, sh9), dev)
     rc = _lib.lib().nconv_fwd_tail(_lib.ctypes.byref(L), _lib.ptr(w7), _lib.ptr(b7), _lib.ptr(s7), sp7.cin, p7,
                                    sp7.eps, _lib.ptr(x9), _lib.ptr(c9), H9, W9, crop0, _lib.ptr(x8), _lib.ptr(c8),
                                    _lib.stream_handle(dev))

@@ -111,9 +111,15 @@ def weight_prep(weights, softplus_flags, wsums):
     _lib.check(rc, "nconv_weight_prep")
 
 
-def _outputs(out, n, shapes, device):
+def _outputs(out, n, shapes, device, dtypes=None):
+    """The launch's output tensors: fresh (out None), the caller's (a sequence), or from a callable
+    out(shapes, dtypes, device) -> tensors (e.g. batch rows of full-batch tensors, dnet's split
+    training forward)."""
+    dtypes = dtypes or [torch.float32] * n
     if out is None:
-        return [torch.empty(sh, device=device, dtype=torch.float32) for sh in shapes]
+        return [torch.empty(sh, device=device, dtype=dt) for sh, dt in zip(shapes, dtypes)]
+    if callable(out):
+        return list(out(shapes, dtypes, device))
     if len(out) != n or any(tuple(t.shape) != tuple(sh) or not t.is_contiguous() or t.dtype != torch.float32
                             for t, sh in zip(out, shapes)):
         raise ValueError("out= tensors must be contiguous fp32 of the layer's output shapes")
@@ -231,8 +237,11 @@ def layer_forward_pooled(spec: LayerSpec, xa, ca, xb, cb, weight, bias, wsum, ou
     result. No autograd."""
     L = spec.descriptor(xa, ca, xb, cb, weight, bias, wsum)
     sh, shp = (L.B, L.Cout, L.Ho, L.Wo), (L.B, L.Cout, L.Ho // 2, L.Wo // 2)
-    y, co, py, pc = _outputs(out, 4, (sh, sh, shp, shp), xa.device)
-    arg = torch.empty(shp, dtype=torch.int32, device=xa.device) if argmax else None
+    if callable(out) and argmax:
+        y, co, py, pc, arg = _outputs(out, 5, (sh, sh, shp, shp, shp), xa.device, [torch.float32] * 4 + [torch.int32])
+    else:
+        y, co, py, pc = _outputs(out, 4, (sh, sh, shp, shp), xa.device)
+        arg = torch.empty(shp, dtype=torch.int32, device=xa.device) if argmax else None
     rc = _lib.lib().nconv_fwd_pooled(_lib.ctypes.byref(L), _lib.ptr(y), _lib.ptr(co), _lib.ptr(py), _lib.ptr(pc),
                                      _lib.ptr(arg), _lib.stream_handle(xa.device))
     _lib.check(rc, "nconv_fwd_pooled")
@@ -257,22 +266,24 @@ def head_weights(spec1: LayerSpec, spec2: LayerSpec, S, w1, b1, s1, w2, b2, s2, 
     return out
 
 
-def layer_forward_head(spec1: LayerSpec, spec2: LayerSpec, S, w1, b1, s1, w2, b2, s2, w21=None, train=False):
+def layer_forward_head(spec1: LayerSpec, spec2: LayerSpec, S, w1, b1, s1, w2, b2, s2, w21=None, train=False,
+                       out=None):
     """nconv_fwd_head: nconv2(nconv1(S)) with nconv1 evaluated inside nconv2's staging (its output
     never reaches HBM); returns nconv2's (y, cout, maxpool2x2(y), maxpool2x2(cout)). No autograd.
     With FORWARD_MATH == exact fp32 the composed weights `w21` (head_weights) are required.
     train=True (exact fp32): also the pooling argmax codes and nconv1's (y, cout), which the
-    training backward reads -- returns (y, cout, py, pc, argmax, y1, cout1)."""
+    training backward reads -- returns (y, cout, py, pc, argmax, y1, cout1). out: None (fresh
+    tensors) or a callable as _outputs takes."""
     L1 = spec1.descriptor(S, None, None, None, w1, b1, s1)
     L2 = spec2.descriptor(S, S, None, None, w2, b2, s2, w21)  # geometry only: the kernel reads S via L1
     B, H, W = S.shape[0], L1.Ho, L1.Wo
-    y = torch.empty((B, 8, H, W), device=S.device, dtype=torch.float32)
-    co = torch.empty_like(y)
-    py = torch.empty((B, 8, H // 2, W // 2), device=S.device, dtype=torch.float32)
-    pc = torch.empty_like(py)
-    arg = torch.empty(py.shape, device=S.device, dtype=torch.int32) if train else None
-    y1 = torch.empty_like(y) if train else None
-    c1 = torch.empty_like(y) if train else None
+    sh, shp, f32 = (B, 8, H, W), (B, 8, H // 2, W // 2), torch.float32
+    if train:
+        y, co, py, pc, arg, y1, c1 = _outputs(out, 7, (sh, sh, shp, shp, shp, sh, sh), S.device,
+                                              [f32] * 4 + [torch.int32, f32, f32])
+    else:
+        y, co, py, pc = _outputs(out, 4, (sh, sh, shp, shp), S.device)
+        arg = y1 = c1 = None
     rc = _lib.lib().nconv_fwd_head(_lib.ctypes.byref(L1), _lib.ctypes.byref(L2), _lib.ptr(y), _lib.ptr(co),
                                    _lib.ptr(py), _lib.ptr(pc), _lib.ptr(arg), _lib.ptr(y1), _lib.ptr(c1),
                                    _lib.stream_handle(S.device))

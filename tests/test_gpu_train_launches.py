@@ -109,7 +109,9 @@ def test_train_prologue_without_head_or_phase(nconv_amd, gpu):
         assert torch.equal(a, b)
 
 
-def _train_iteration(nconv_amd, gpu, B, H, W, crop, merged=True, in_tail=True, seed=31):
+def _train_iteration(nconv_amd, gpu, B, H, W, crop, merged=True, in_tail=True, seed=31, fwd_streams=None):
+    if fwd_streams is not None:
+        nconv_amd.dnet.TRAIN_FWD_STREAMS = fwd_streams
     g = torch.Generator().manual_seed(seed)
     S = sparse_depth(g, B, H, W).to(gpu)
     net = make_net(nconv_amd, crop, gpu)
@@ -209,3 +211,23 @@ def test_dnet_eval_stream_prologue_bitwise(nconv_amd, gpu, B, H, W):
         d.stream_prologue = False
         e = net(S)
     assert torch.equal(c, e) and not torch.equal(b, c)
+
+
+@pytest.mark.parametrize("B,H,W,crop", [(2, 64, 96, "generalized"), (3, 48, 200, "literal"),
+                                        (8, 352, 1216, "generalized")])
+def test_dnet_train_forward_streams_bitwise(nconv_amd, gpu, B, H, W, crop):
+    """The training forward in batch slices on two streams (dnet.TRAIN_FWD_STREAMS, each launch
+    writing its rows of full-batch tensors) equals the one-stream pass bitwise: output, weights
+    after the drift and every gradient (B = 3: uneven slices 1 + 2)."""
+    keep = nconv_amd.dnet.TRAIN_FWD_STREAMS
+    try:
+        oa, wa, ga = _train_iteration(nconv_amd, gpu, B, H, W, crop, fwd_streams=2)
+        ob, wb, gb = _train_iteration(nconv_amd, gpu, B, H, W, crop, fwd_streams=1)
+    finally:
+        nconv_amd.dnet.TRAIN_FWD_STREAMS = keep
+    assert torch.equal(oa, ob)
+    for k in wa:
+        assert torch.equal(wa[k], wb[k]), k
+    assert set(ga) == set(gb) and len(ga) == 18
+    for k in ga:
+        assert torch.equal(ga[k], gb[k]), k
