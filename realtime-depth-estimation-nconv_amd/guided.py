@@ -21,6 +21,7 @@ sampling arithmetic, dense.bilinear_down).
 PyTorch reference the GPU tests compare the kernels against (tests/test_gpu_dense.py), not a
 product path (step 1 still runs on libnconv and refuses CPU tensors).
 """
+import os
 from collections import OrderedDict
 
 import torch
@@ -314,9 +315,13 @@ def _use_dense(m, x):
     return not (torch.is_grad_enabled() and any(p.requires_grad for p in m.parameters()))
 
 
-def _guided_forward_dense(m, rgb0, depth0, rgb1, depth1):
-    sparse = m.step1(depth0, depth1).contiguous()
-    rgb = torch.cat((rgb0, rgb1), dim=0).contiguous()
+# The eval (dense) forward's encoders and decoder in this many batch slices, one stream each (every
+# frame's arithmetic is per frame: bitwise the one-stream pass); 1 = one launch per layer
+GUIDED_STREAMS = int(os.environ.get("NCONV_GUIDED_STREAMS", "2"))
+_GUIDED_STREAMS = {}
+
+
+def _dense_chain(m, rgb, sparse):
     e0 = m.rgb_encoder0.dense_forward(rgb)
     e1 = m.rgb_encoder1.dense_forward(e0)
     e2 = m.rgb_encoder2.dense_forward(e1)
@@ -326,6 +331,34 @@ def _guided_forward_dense(m, rgb0, depth0, rgb1, depth1):
     f2, d2 = m.fuse2.dense_forward(e1, sparse, f1, d1)
     f3, d3 = m.fuse3.dense_forward(e0, sparse, f2, d2)
     return d0, d1, d2, d3
+
+
+def _guided_forward_dense(m, rgb0, depth0, rgb1, depth1):
+    sparse = m.step1(depth0, depth1).contiguous()
+    rgb = torch.cat((rgb0, rgb1), dim=0).contiguous()
+    B = rgb.shape[0]
+    n = max(1, min(int(GUIDED_STREAMS), B))
+    if n == 1:
+        return _dense_chain(m, rgb, sparse)
+    dev = rgb.device
+    if (dev.index, n) not in _GUIDED_STREAMS:
+        _GUIDED_STREAMS[(dev.index, n)] = [torch.cuda.Stream(device=dev) for _ in range(n - 1)]
+    side = _GUIDED_STREAMS[(dev.index, n)]
+    cur = torch.cuda.current_stream(dev)
+    for st in side:
+        st.wait_stream(cur)
+    bounds = [B * k // n for k in range(n + 1)]
+    parts = []
+    for k, st in enumerate([cur] + side):
+        with torch.cuda.stream(st):
+            parts.append(_dense_chain(m, rgb[bounds[k]:bounds[k + 1]], sparse[bounds[k]:bounds[k + 1]]))
+    for st in side:
+        cur.wait_stream(st)
+    if not torch.cuda.is_current_stream_capturing():  # the side streams' outputs are read on cur
+        for part in parts[1:]:
+            for t in part:
+                t.record_stream(cur)
+    return tuple(torch.cat([part[i] for part in parts], dim=0) for i in range(4))
 
 
 def _guided_forward_train(m, rgb0, depth0, rgb1, depth1):

@@ -268,3 +268,24 @@ def test_guided_graphed_train_step_matches_eager(nconv_amd, gpu):
     sd_e, sd_g = net_e.state_dict(), net_g.state_dict()
     for k in sd_e:
         torch.testing.assert_close(sd_g[k], sd_e[k], rtol=1e-5, atol=1e-7, msg=k)
+
+
+@pytest.mark.parametrize("H,W,n", [(64, 96, 1), (72, 200, 3), (352, 1216, 4)])
+def test_guided_eval_streams_bitwise(nconv_amd, gpu, H, W, n):
+    """The eval (dense) forward's encoders + decoder in batch slices on two streams
+    (guided.GUIDED_STREAMS) equals the one-stream pass bitwise at every scale (n = 3: 6 frames)."""
+    model = _kitti_model(nconv_amd, gpu).eval()
+    ins = [t.to(gpu) for t in f5_inputs(H, W, n)]
+    G = nconv_amd.guided
+    keep = G.GUIDED_STREAMS
+    try:
+        with torch.no_grad():
+            G.GUIDED_STREAMS = 2
+            a = G._guided_forward(model, *ins)
+            G.GUIDED_STREAMS = 1
+            b = G._guided_forward(model, *ins)
+    finally:
+        G.GUIDED_STREAMS = keep
+    for i in range(4):
+        assert a[i].shape == b[i].shape == (2 * n, 1, H >> (3 - i), W >> (3 - i))
+        assert torch.equal(a[i], b[i]), i
