@@ -13,6 +13,7 @@ Host side of nconv_dense_conv_fwd / nconv_dense_pack / nconv_conv3x3_c1 / nconv_
 """
 import ctypes
 import math
+import os
 
 import torch
 
@@ -166,6 +167,18 @@ def relu_bias_bwd(g, out, g_masked, gbias):
                                      _lib.ptr(ws), nb, _lib.stream_handle(g.device)), "nconv_relu_bias_bwd")
 
 
+# The training backward's weight gradient on a side stream, concurrent with the same layer's input
+# gradient(s) (both matrix-core kernels; joined before the node returns)
+WGRAD_STREAM = int(os.environ.get("NCONV_DENSE_WGRAD_STREAM", "1"))
+_WGRAD_STREAMS = {}
+
+
+def _wgrad_stream(device):
+    if device.index not in _WGRAD_STREAMS:
+        _WGRAD_STREAMS[device.index] = torch.cuda.Stream(device=device)
+    return _WGRAD_STREAMS[device.index]
+
+
 class DenseConvFn(torch.autograd.Function):
     """y = [relu](conv(cat(x0, x1); weight) + bias) for Conv2d 3x3 pad 1 / 1x1 (stride 1 | 2) and
     ConvTranspose2d 4x4 s2 p1 — nn.Conv2d / nn.ConvTranspose2d (+ ReLU, + the torch.cat before
@@ -202,12 +215,22 @@ class DenseConvFn(torch.autograd.Function):
         co = ctx.c0
         tr = ctx.kind == DENSE_TRANSPOSED_4X4
         w = weight.detach()
+        side = None
+        if need[2] and WGRAD_STREAM and (need[0] or (x1 is not None and need[1])):
+            cur, side = torch.cuda.current_stream(g.device), _wgrad_stream(g.device)
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                gw = wgrad(x0, x1, g, ctx.kind, ctx.stride, weight.shape)
         if need[0]:
             w0 = w if x1 is None else (w[:co] if tr else w[:, :co])
             gx0 = dgrad(g, w0, ctx.kind, ctx.stride, x0.shape)
         if x1 is not None and need[1]:
             gx1 = dgrad(g, w[co:] if tr else w[:, co:], ctx.kind, ctx.stride, x1.shape)
-        if need[2]:
+        if side is not None:
+            cur.wait_stream(side)
+            if not torch.cuda.is_current_stream_capturing():
+                gw.record_stream(cur)  # (made on the side stream, read on this one)
+        elif need[2]:
             gw = wgrad(x0, x1, g, ctx.kind, ctx.stride, weight.shape)
         return gx0, gx1, gw, gb, None, None, None
 
