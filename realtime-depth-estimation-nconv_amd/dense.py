@@ -168,15 +168,32 @@ def relu_bias_bwd(g, out, g_masked, gbias):
 
 
 # The training backward's weight gradient on a side stream, concurrent with the same layer's input
-# gradient(s) (both matrix-core kernels; joined before the node returns)
+# gradient(s): 1 = joined before the node returns; 2 = joined once, when the backward pass ends
+# (autograd's end-of-pass callback), so it also runs under the next layers' BatchNorm / ReLU
+# backward passes -- only when the parameter's .grad is unset (autograd then takes the tensor as is,
+# no accumulation kernel reads it before the join); 0 = serial
 WGRAD_STREAM = int(os.environ.get("NCONV_DENSE_WGRAD_STREAM", "1"))
 _WGRAD_STREAMS = {}
+_JOIN_QUEUED = set()
 
 
 def _wgrad_stream(device):
     if device.index not in _WGRAD_STREAMS:
         _WGRAD_STREAMS[device.index] = torch.cuda.Stream(device=device)
     return _WGRAD_STREAMS[device.index]
+
+
+def _join_at_backward_end(cur, side):
+    """cur waits for the side stream when the running backward pass ends (once per pass)."""
+    key = (cur.device.index, cur.stream_id)
+    if key in _JOIN_QUEUED:
+        return
+
+    def join():
+        _JOIN_QUEUED.discard(key)
+        cur.wait_stream(side)
+    _JOIN_QUEUED.add(key)
+    torch.autograd.Variable._execution_engine.queue_callback(join)
 
 
 class DenseConvFn(torch.autograd.Function):
@@ -194,6 +211,7 @@ class DenseConvFn(torch.autograd.Function):
         b = bias.detach().contiguous() if bias is not None else None
         out = conv(x0, kind, stride, wp, b, relu, cout, x1=x1)
         ctx.kind, ctx.stride, ctx.relu, ctx.c0 = kind, stride, relu, x0.shape[1]
+        ctx.wparam = weight  # (its .grad decides whether the weight gradient's join may wait)
         ctx.has_bias = bias is not None
         ctx.save_for_backward(x0, x1, weight, out if relu else None)
         return out
@@ -227,9 +245,15 @@ class DenseConvFn(torch.autograd.Function):
         if x1 is not None and need[1]:
             gx1 = dgrad(g, w[co:] if tr else w[:, co:], ctx.kind, ctx.stride, x1.shape)
         if side is not None:
-            cur.wait_stream(side)
-            if not torch.cuda.is_current_stream_capturing():
-                gw.record_stream(cur)  # (made on the side stream, read on this one)
+            if WGRAD_STREAM == 2 and ctx.wparam.grad is None:
+                # the side stream still reads g, x0, x1: their memory is not reused before it is done
+                for t in (g, x0, x1):
+                    if t is not None:
+                        t.record_stream(side)
+                _join_at_backward_end(cur, side)
+            else:
+                cur.wait_stream(side)
+            gw.record_stream(cur)  # (made on the side stream, read on this one)
         elif need[2]:
             gw = wgrad(x0, x1, g, ctx.kind, ctx.stride, weight.shape)
         return gx0, gx1, gw, gb, None, None, None

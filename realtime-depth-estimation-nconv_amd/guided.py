@@ -354,10 +354,9 @@ def _guided_forward_dense(m, rgb0, depth0, rgb1, depth1):
             parts.append(_dense_chain(m, rgb[bounds[k]:bounds[k + 1]], sparse[bounds[k]:bounds[k + 1]]))
     for st in side:
         cur.wait_stream(st)
-    if not torch.cuda.is_current_stream_capturing():  # the side streams' outputs are read on cur
-        for part in parts[1:]:
-            for t in part:
-                t.record_stream(cur)
+    for part in parts[1:]:  # the side streams' outputs are read on cur (under capture the
+        for t in part:      # allocator holds such blocks until the capture ends)
+            t.record_stream(cur)
     return tuple(torch.cat([part[i] for part in parts], dim=0) for i in range(4))
 
 
