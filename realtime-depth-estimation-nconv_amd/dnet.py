@@ -192,7 +192,9 @@ class DNETFn(torch.autograd.Function):
         sp = ctx.specs
         red = WgradReduce()  # every layer's weight-gradient reduction in two launches at the end
         cur = torch.cuda.current_stream(S.device)
-        side = _wgrad_stream(S.device) if (ctx.pooled and WGRAD_STREAM) else None
+        sides = _wgrad_streams(S.device, WGRAD_STREAMS_N) if (ctx.pooled and WGRAD_STREAM) else []
+        side = sides[0] if sides else None
+        turn = [0]
 
         def layer_bwd(spec, inputs, y, co, gy, gco, gin, gw_, gb_, fused=False, **kw):
             # fused: one call (one kernel) for the input and the weight gradient (the exact-fp32 8 -> 8
@@ -203,11 +205,13 @@ class DNETFn(torch.autograd.Function):
             if side is None or (gw_ is None and gb_ is None) or fused:
                 layer_backward(spec, inputs, y, co, gy, gco, gin, gw_, gb_, defer=red, separate=not fused, **kw)
                 return
-            side.wait_stream(cur)
+            st = sides[turn[0] % len(sides)]  # (several weight-gradient streams: round robin)
+            turn[0] += 1
+            st.wait_stream(cur)
             tail, head = kw.pop("tail", None), kw.pop("head", None)
             layer_backward(spec, inputs, y, co, gy, gco, gin, None, None, defer=red, head=head,
                            tail=None if tail is None else tail[:7] + (None,) + tail[8:], **kw)  # (no gw7)
-            with torch.cuda.stream(side):
+            with torch.cuda.stream(st):
                 layer_backward(spec, inputs, y, co, gy, gco, (None,) * 4, gw_, gb_, defer=red, tail=tail, **kw)
 
         def bwd(k, a, b, ga, gb_, acc=False, src_a=None, spec=None, pool_grad=None, box=None):
@@ -219,8 +223,8 @@ class DNETFn(torch.autograd.Function):
                       pool_grad=pool_grad, fused=pool_grad is not None and LAYERS[k - 1] in FUSED_BWD, box=box)
 
         def finish():
-            if side is not None:
-                cur.wait_stream(side)
+            for st in sides:
+                cur.wait_stream(st)
             red.run(S.device)
 
         G[2], G[7] = (e(X[2][0]), e(X[2][1])), (e(X[7][0]), e(X[7][1]))
@@ -337,9 +341,18 @@ _WGRAD_STREAMS = {}
 
 
 def _wgrad_stream(device):
-    if device.index not in _WGRAD_STREAMS:
-        _WGRAD_STREAMS[device.index] = torch.cuda.Stream(device=device)
-    return _WGRAD_STREAMS[device.index]
+    return _wgrad_streams(device, 1)[0]
+
+
+# weight-gradient streams of the training backward (layers round-robin over them)
+WGRAD_STREAMS_N = int(os.environ.get("NCONV_WGRAD_STREAMS", "1"))
+
+
+def _wgrad_streams(device, n):
+    have = _WGRAD_STREAMS.setdefault(device.index, [])
+    while len(have) < max(1, n):
+        have.append(torch.cuda.Stream(device=device))
+    return have[:max(1, n)]
 
 
 def _materialise_pool(S):
