@@ -51,6 +51,38 @@ def cached(mod, name, tensors, build):
     return ent[1]
 
 
+# Training convolutions (DenseConvFn's forward) in this many batch slices, one stream each, every
+# slice writing its rows of the output (per-frame arithmetic: bitwise the one-launch result)
+TRAIN_SLICES = int(os.environ.get("NCONV_DENSE_TRAIN_SLICES", "1"))
+_SLICE_STREAMS = {}
+
+
+def conv_sliced(x0, kind, stride, wpack, bias, relu, cout, x1=None, n=2):
+    """conv() over n batch slices on n streams into one output tensor."""
+    B = x0.shape[0]
+    n = max(1, min(int(n), B))
+    if n == 1:
+        return conv(x0, kind, stride, wpack, bias, relu, cout, x1=x1)
+    out = conv(x0[:0], kind, stride, wpack, bias, relu, cout, x1=None if x1 is None else x1[:0])  # shape only
+    out = torch.empty((B,) + tuple(out.shape[1:]), device=x0.device, dtype=torch.float32)
+    dev = x0.device
+    if (dev.index, n) not in _SLICE_STREAMS:
+        _SLICE_STREAMS[(dev.index, n)] = [torch.cuda.Stream(device=dev) for _ in range(n - 1)]
+    side = _SLICE_STREAMS[(dev.index, n)]
+    cur = torch.cuda.current_stream(dev)
+    for st in side:
+        st.wait_stream(cur)
+    bounds = [B * k // n for k in range(n + 1)]
+    for k, st in enumerate([cur] + side):
+        with torch.cuda.stream(st):
+            b0, b1 = bounds[k], bounds[k + 1]
+            conv(x0[b0:b1], kind, stride, wpack, bias, relu, cout, x1=None if x1 is None else x1[b0:b1],
+                 out=out[b0:b1])
+    for st in side:
+        cur.wait_stream(st)
+    return out
+
+
 def conv(x0, kind, stride, wpack, bias, relu, cout, x1=None, wshort=None, out=None, out_c0=0):
     """[relu](conv(cat(x0, x1)) + bias) [+ shortcut]; written to out[:, out_c0:out_c0+cout] if out is given."""
     B, C0, H, W = x0.shape
@@ -73,6 +105,8 @@ def conv(x0, kind, stride, wpack, bias, relu, cout, x1=None, wshort=None, out=No
     d.relu = 1 if relu else 0
     d.wshort = wshort.data_ptr() if wshort is not None else None
     d.out, d.out_C, d.out_c0 = out.data_ptr(), out.shape[1], out_c0
+    if B == 0:
+        return out
     _lib.check(_lib.lib().nconv_dense_conv_fwd(ctypes.byref(d), _lib.stream_handle(x0.device)),
                "nconv_dense_conv_fwd")
     return out
@@ -209,7 +243,10 @@ class DenseConvFn(torch.autograd.Function):
         cout = weight.shape[1] if kind == DENSE_TRANSPOSED_4X4 else weight.shape[0]
         wp = pack(kind, weight, cin, cout)
         b = bias.detach().contiguous() if bias is not None else None
-        out = conv(x0, kind, stride, wp, b, relu, cout, x1=x1)
+        if TRAIN_SLICES > 1:
+            out = conv_sliced(x0, kind, stride, wp, b, relu, cout, x1=x1, n=TRAIN_SLICES)
+        else:
+            out = conv(x0, kind, stride, wp, b, relu, cout, x1=x1)
         ctx.kind, ctx.stride, ctx.relu, ctx.c0 = kind, stride, relu, x0.shape[1]
         ctx.wparam = weight  # (its .grad decides whether the weight gradient's join may wait)
         ctx.has_bias = bias is not None

@@ -289,3 +289,37 @@ def test_guided_eval_streams_bitwise(nconv_amd, gpu, H, W, n):
     for i in range(4):
         assert a[i].shape == b[i].shape == (2 * n, 1, H >> (3 - i), W >> (3 - i))
         assert torch.equal(a[i], b[i]), i
+
+
+@pytest.mark.parametrize("H,W,n", [(64, 96, 1), (72, 200, 3)])
+def test_guided_train_sliced_convs_bitwise(nconv_amd, gpu, H, W, n):
+    """The training convolutions' forward in two batch slices on two streams (dense.TRAIN_SLICES,
+    each slice writing its rows of the output) equals the one-launch pass bitwise: estimate, loss
+    and every parameter gradient of one config-4 iteration (n = 3: 6 frames, slices 3 + 3)."""
+    Dm = nconv_amd.dense
+    g = torch.Generator().manual_seed(41)
+    gt = ((torch.rand(n, 1, 480, 640, generator=g) * 79 + 1) * (torch.rand(n, 1, 480, 640, generator=g) < 0.5)).to(gpu)
+    ins = [t.to(gpu) for t in f5_inputs(H, W, n)]
+
+    def run(slices):
+        Dm.TRAIN_SLICES = slices
+        torch.manual_seed(2)
+        net = nconv_amd.SETP2_BP_TRAIN(None, step1_crop="generalized").to(gpu).train()
+        est, _ = net(*ins)
+        loss = nconv_amd.train.calculate_loss_multi_resolution(est, gt, False)
+        loss.backward()
+        torch.cuda.synchronize()
+        return [e.detach() for e in est], loss.detach(), {k: p.grad for k, p in net.named_parameters()
+                                                          if p.grad is not None}
+    keep = Dm.TRAIN_SLICES
+    try:
+        ea, la, ga = run(2)
+        eb, lb, gb = run(1)
+    finally:
+        Dm.TRAIN_SLICES = keep
+    assert torch.equal(la, lb)
+    for a, b in zip(ea, eb):
+        assert torch.equal(a, b)
+    assert set(ga) == set(gb) and ga
+    for k in ga:
+        assert torch.equal(ga[k], gb[k]), k
