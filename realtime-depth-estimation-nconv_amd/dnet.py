@@ -17,6 +17,7 @@ mode, before any layer runs (the reference applies each right before its layer; 
 no weights, so the results are identical).
 """
 import dataclasses
+import itertools
 import math
 import os
 
@@ -141,9 +142,9 @@ class DNETFn(torch.autograd.Function):
             res = None
             for k, st in enumerate([cur] + side):
                 b0, b1 = bounds[k], bounds[k + 1]
-                it = iter(range(1 << 30))
 
-                def rows(shapes, dtypes, device, b0=b0, b1=b1, it=it):
+                def rows(shapes, dtypes, device, b0=b0, b1=b1, it=itertools.count()):
+                    # the i-th output of this slice's launches = rows b0:b1 of full-batch tensor i
                     out = []
                     for sh, dt in zip(shapes, dtypes):
                         i = next(it)
