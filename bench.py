@@ -29,12 +29,15 @@ Multi-GPU: frames are independent units, so each rank runs its own B frames (wea
 no collective in the forward; the training step all-reduces gradients over RCCL (one bucket).
 """
 import argparse
+import faulthandler
 import json
 import os
 import socket
 import subprocess
 import sys
 import time
+
+faulthandler.enable()  # a host fault (SIGSEGV / SIGABRT) leaves every thread's Python stack on stderr
 
 import torch
 import torch.distributed as dist
@@ -88,8 +91,6 @@ def parse(argv=None):
     p.add_argument("--inference-shares", default=None, type=_shares,
                    help="DNET.inference_shares: relative frames per inference stream, e.g. 5,3 (one positive "
                         "number per stream of --inference-streams, default 2)")
-    p.add_argument("--mid-streams", type=int, default=None,
-                   help="DNET.mid_streams: the quarter/eighth-resolution layers on that many batch slices")
     p.add_argument("--guided-train-graph", type=int, default=1,
                    help="replay the config-4 guided training step from a hipGraph (1) or eager (0)")
     p.add_argument("--head-density", type=float, default=0.40,
@@ -329,6 +330,35 @@ def time_layers(m, net, S, reps=20):
                 ev[name].append((e0, e1))
     torch.cuda.synchronize()
     return {name: sum(e0.elapsed_time(e1) for e0, e1 in pairs) / len(pairs) * 1e3 for name, pairs in ev.items()}
+
+
+def time_concurrent_halves(m, net, S, name, reps=20):
+    """Device span (us) of kernel `name`'s two B/2 launches run concurrently on two streams -- the
+    launch shape the replayed headline graph runs (DNET's two-stream inference split), as opposed to
+    time_layers' isolated B launch on one stream: HIP events on the current stream around the fork
+    (side stream waits for it), the two launches, and the join."""
+    B = S.shape[0]
+    if B < 2:
+        return None
+    h = B // 2
+    ca, cb = inference_calls(m, net, S[:h])[name], inference_calls(m, net, S[h:])[name]
+    cur = torch.cuda.current_stream()
+    side = torch.cuda.Stream()
+    spans = []
+    with torch.no_grad():
+        for it in range(reps + 2):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(cur)
+            side.wait_stream(cur)
+            ca()
+            with torch.cuda.stream(side):
+                cb()
+            cur.wait_stream(side)
+            e1.record(cur)
+            if it >= 2:
+                spans.append((e0, e1))
+    torch.cuda.synchronize()
+    return sum(e0.elapsed_time(e1) for e0, e1 in spans) / len(spans) * 1e3
 
 
 def pmc_traffic(kernel, math, B, H, W):
@@ -653,8 +683,6 @@ def main():
         net.d_net.inference_streams = a.inference_streams
     if a.inference_shares is not None:
         net.d_net.inference_shares = tuple(a.inference_shares)
-    if a.mid_streams is not None:
-        net.d_net.mid_streams = a.mid_streams
     g = torch.Generator().manual_seed(1000 + rank)
     S = sparse_depth(g, B, H, W, dev)
 
@@ -725,6 +753,8 @@ def main():
         log("per-kernel times")
         m.nconv.FORWARD_MATH = HEAD
         lt_of[a.math] = time_layers(m, net, S)
+        dom = max(lt_of[a.math], key=lambda n: lt_of[a.math][n])
+        lt_of["replayed_shape"] = time_concurrent_halves(m, net, S, dom)
         if a.head_density > 0 and a.math == "fp32":
             # the exact head skips nconv1's zero taps, so its time depends on the input density: the
             # same forward's kernels at f10's 40 % (golden fixture density) beside the 5 % headline
@@ -868,6 +898,13 @@ def main():
         issued = (lambda k: mfma_issued_flops(k, B, H, W, a.math)) if a.math in MFMA_TERMS else None
         roof = roofline(lt, costs, a.math, B, H, W, issued_mfma=issued)
         roof["whole_pass_hbm_frac"] = pass_frac(t_fwd, a.steps)
+        roof["launch"] = f"kernel_us: one isolated B={B} launch on one stream (HIP events, outside the graph)"
+        if lt_of.get("replayed_shape"):
+            span = lt_of["replayed_shape"]
+            fl_dom = costs[roof["kernel"]][1]
+            roof["replayed_shape"] = {
+                "launches": f"two concurrent B={B // 2} launches on two streams (the headline graph's split)",
+                "span_us": round(span, 2), "reference_flop_frac": round(fl_dom / (span * 1e-6) / 1e12 / FP32_PEAK_TFLOPS, 4)}
         if "density" in lt_of:
             dom = roof["kernel"]
             head_density = {}

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define NCONV_ABI_VERSION 20
+#define NCONV_ABI_VERSION 21
 
 /* How a layer's input (data x, confidence c) is produced from its source tensors. These are the
  * DNET glue ops fused into the layer's load stage (models/step1.py:53,61-90). */
@@ -253,12 +253,8 @@ size_t nconv_bwd_workspace_bytes(const nconv_layer* L);
  * launches instead of two per layer. Same sums, same fixed order: the result is bitwise that of
  * the undeferred call. */
 #define NCONV_BWD_DEFER_REDUCE 2u
-/* An exact-fp32 8 -> 8 5x5 stride-1 layer with plain loads and the pooled-output gradient (nconv_bwd_ex
- * gy_pool / gcout_pool / pool_argmax: DNET's nconv2, down1, down2 in training) whose call asks for both
- * an input gradient (gxa / gca, or the fused head) and the weight gradient runs ONE kernel for both:
- * {gN, gD} formed once per element, the weight gradient on the vector ALU beside the input gradient
- * (same sums as the two-kernel form up to fp32 reassociation). (flags & NCONV_BWD_SEPARATE) runs the
- * two kernels instead (tests, A/B timing). */
+/* Accepted and ignored since ABI 21: the input and the weight gradient always run as two kernels
+ * (the one-kernel form of ABI 19-20 measured slower and was removed). */
 #define NCONV_BWD_SEPARATE 4u
 
 int nconv_bwd(const nconv_layer* L, const float* y, const float* cout, const float* gy,

@@ -13,10 +13,10 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # NCONV_LIB: an alternative build of the same library (kernel-tuning experiments)
 LIB_PATH = os.environ.get("NCONV_LIB") or os.path.join(_HERE, "libnconv.so")
-ABI_VERSION = 20
+ABI_VERSION = 21
 BWD_ACCUMULATE = 1
 BWD_DEFER_REDUCE = 2
-BWD_SEPARATE = 4
+BWD_SEPARATE = 4  # accepted and ignored since ABI 21 (include/nconv.h)
 
 # enum nconv_load_mode
 PLAIN, THRESH, POOL2, UPCAT_SKIP_FIRST, UPCAT_UP_FIRST = 0, 1, 2, 3, 4

@@ -416,7 +416,7 @@ __host__ __device__ constexpr int wgd_ntb(int kind) {
 // (the 1- and 3-channel inputs of depth_conv / rgb_encoder0, a 1x1 of <= 32 channels)
 constexpr int wgd_nt(int kind, int N) { return N <= 32 ? 1 : wgd_ntb(kind); }
 
-template <int KIND, int S, int NT, int GM, int GN, bool DB>
+template <int KIND, int S, int NT, int GM, int GN>
 struct WgdCfg {
     static constexpr bool TR = KIND == NCONV_DENSE_TRANSPOSED_4X4;
     static constexpr int TAPS = KIND == NCONV_DENSE_3X3 ? 9 : (KIND == NCONV_DENSE_1X1 ? 1 : 16);
@@ -440,8 +440,7 @@ struct WgdCfg {
     static constexpr int DP = NPX + 2;     // D row pitch: rows m, m+1 two banks apart
     static constexpr int D_OFF = (CPB * PPLANE + 3) & ~3;
     static constexpr int BUF = (D_OFF + GM * 32 * DP + 3) & ~3;  // one tile's staging (patch, then D)
-    static constexpr int STG = DB ? 2 * BUF : BUF;               // DB: two tiles, the next one in flight
-    static constexpr int LDS = STG > 4 * 16 * 64 ? STG : 4 * 16 * 64;  // (+ the wave-partial sums)
+    static constexpr int LDS = BUF > 4 * 16 * 64 ? BUF : 4 * 16 * 64;  // (+ the wave-partial sums)
     static constexpr int NDE = GM * 32 * NPX / kDT;  // D elements per thread
     static constexpr int NPG = (CPG * PPLANE + kDT - 1) / kDT;  // patch elements per thread and group
     static_assert(PPW % 16 == 0 && (GM * 32 * NPX) % kDT == 0, "wave / thread shares");
@@ -461,9 +460,9 @@ struct WgdArgs {
     long long ntiles;
 };
 
-template <int KIND, int S, int NT, int GM, int GN, bool DB>
+template <int KIND, int S, int NT, int GM, int GN>
 __global__ __launch_bounds__(kDT) void dense_wgrad_mfma(WgdArgs a, float* __restrict__ part) {
-    using C = WgdCfg<KIND, S, NT, GM, GN, DB>;
+    using C = WgdCfg<KIND, S, NT, GM, GN>;
     __shared__ __attribute__((aligned(16))) float lds[C::LDS];
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -620,31 +619,17 @@ __global__ __launch_bounds__(kDT) void dense_wgrad_mfma(WgdArgs a, float* __rest
             }
         }
     };
-    // DB: tile t + 1's DMA goes into the other buffer right after tile t's barrier and lands during
-    // tile t's MFMAs (one workgroup per CU keeps the matrix cores busy by itself); otherwise one
-    // buffer, and the loads of one workgroup hide behind the MFMAs of the CU's other workgroup
-    if (DB && t0 < t1) {
-        stage(tx_c, ty_c, b_c, lds);
-        next_tile();
-    }
+    // one buffer: the loads of one workgroup hide behind the MFMAs of the CU's other workgroup (a
+    // double-buffered single workgroup per CU measured slower, 704.6 against 614.0 us for the
+    // 32-channel 3x3: profiles/r5_ab_dense_wgrad_db.log; removed in round 6)
 #pragma unroll 1
     for (long long t = t0; t < t1; ++t) {
         const float* lb = lds;
-        if constexpr (DB) {
-            lb = lds + ((t - t0) & 1) * C::BUF;
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this tile's DMA (issued one tile ago)
-            __syncthreads();  // ... from every wave; and every wave is done with the other buffer
-            if (t + 1 < t1) {
-                stage(tx_c, ty_c, b_c, lds + ((t + 1 - t0) & 1) * C::BUF);
-                next_tile();
-            }
-        } else {
-            __syncthreads();  // the previous tile's MFMAs are done with the LDS
-            stage(tx_c, ty_c, b_c, lds);
-            next_tile();
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-        }
+        __syncthreads();  // the previous tile's MFMAs are done with the LDS
+        stage(tx_c, ty_c, b_c, lds);
+        next_tile();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
         // the wave's pixels in segments of 16 (8 k-steps) inside one tile row
 #pragma unroll 1
         for (int sg = 0; sg < C::PPW / 16; ++sg) {
@@ -881,16 +866,7 @@ int launch_conv3x3_c1(const float* x, int B, int Cin, int H, int W, const float*
 struct WgdPlan {
     WgdArgs a;
     int nt, gm, gn, rg;
-    bool db;  // double-buffered staging, one workgroup per CU (dense_wgrad_mfma DB)
 };
-
-// NCONV_WGD_DB=1: the double-buffered weight gradient (one workgroup per CU). Measured slower than
-// two single-buffer workgroups per CU: the config-4 step 47.1 against 45.0-45.3 ms, the 32-channel
-// 3x3 weight gradient 704.6 against 614.0 us (profiles/r5_ab_dense_wgrad_db.log), so opt-in only.
-static bool wgd_db() {
-    const char* e = getenv("NCONV_WGD_DB");  // (read per call: tests switch it inside one process)
-    return e && e[0] == '1';
-}
 
 static WgdPlan wgrad_plan(const nconv_dense_wgrad& g) {
     WgdPlan pl{};
@@ -942,8 +918,7 @@ static WgdPlan wgrad_plan(const nconv_dense_wgrad& g) {
     a.ntiles = (long long)g.B * a.ntx * a.nty;
     a.nbm = nmg / pl.gm;
     a.nbn = nng / pl.gn;
-    pl.db = wgd_db() && pl.nt > 1;  // (the one-tile groups are small and occupancy-bound: single buffer)
-    long long nks = (pl.db ? 256 : 512) / (a.nbm * a.nbn);  // one (DB) or two workgroups per CU
+    long long nks = 512 / (a.nbm * a.nbn);  // two workgroups per CU
     if (nks < 1) nks = 1;
     if (nks > a.ntiles) nks = a.ntiles;
     a.nks = (int)nks;
@@ -997,22 +972,17 @@ size_t dense_wgrad_workspace_bytes(const nconv_dense_wgrad& g) {
     return a + (size_t)tr_rows_grid(g).nslice * cs * g.Cout * 16 * sizeof(float);
 }
 
-template <int KIND, int S, int NT, bool DB>
-static bool go_wgrad_db(const WgdPlan& pl, float* ws, hipStream_t st) {
+template <int KIND, int S, int NT>
+static bool go_wgrad(const WgdPlan& pl, float* ws, hipStream_t st) {
     const dim3 grid(pl.a.nbm * pl.a.nbn * pl.a.nks), blk(kDT);
     if (pl.gn != 1) return false;  // (one n-group per workgroup: LDS-DMA staging)
     if (pl.gm == 1)
-        hipLaunchKernelGGL((dense_wgrad_mfma<KIND, S, NT, 1, 1, DB>), grid, blk, 0, st, pl.a, ws);
+        hipLaunchKernelGGL((dense_wgrad_mfma<KIND, S, NT, 1, 1>), grid, blk, 0, st, pl.a, ws);
     else if constexpr (NT > 1)
-        hipLaunchKernelGGL((dense_wgrad_mfma<KIND, S, NT, 2, 1, DB>), grid, blk, 0, st, pl.a, ws);
+        hipLaunchKernelGGL((dense_wgrad_mfma<KIND, S, NT, 2, 1>), grid, blk, 0, st, pl.a, ws);
     else
         return false;
     return true;
-}
-
-template <int KIND, int S, int NT>
-static bool go_wgrad(const WgdPlan& pl, float* ws, hipStream_t st) {
-    return pl.db ? go_wgrad_db<KIND, S, NT, true>(pl, ws, st) : go_wgrad_db<KIND, S, NT, false>(pl, ws, st);
 }
 
 static int launch_dense_wgrad_main(const nconv_dense_wgrad& g, float* ws, hipStream_t st, const char** why);

@@ -1870,32 +1870,6 @@ int launch_bwd(const LayerDev& d, const BwdArgs& a, hipStream_t st, const char**
                    "8->8 5x5 stride-1 layer with plain loads";
             return -95;
         }
-        // input and weight gradient requested: one kernel for both (nconv_bwd_fused.hip) unless the
-        // caller asked for the separate kernels
-        const bool want_in = a.hpart || a.gxa || a.gca;
-        if (!a.separate && want_in && (a.gw || a.gb) && fused_bwd_ok(L)) {
-            // partial rows: at most what the layer's workspace (wm_grid) and, with the head, the head
-            // workspace (one row per dgrad_tiled tile, bwd_head_workspace_bytes) hold
-            int maxb = (int)wm_grid(L).nblk;
-            if (a.hpart) {
-                using D = DgCfg<8, 5>;
-                const int hb = ((L.W + D::TW - 1) / D::TW) * ((L.H + D::TH - 1) / D::TH) * L.B;
-                maxb = hb < maxb ? hb : maxb;
-            }
-            const int nb = launch_bwd_fused(d, a, part, maxb, true, a.hpart != nullptr, st);
-            if (nb > 0) {
-                if (a.hpart) {
-                    if (a.defer) {
-                        *a.hnparts = nb;
-                    } else {
-                        const RedJob J{a.hpart, a.hs, a.hgw, a.hgb, nb, kHeadNw, 8, 25};
-                        if (int rc = launch_wgrad_reduce_multi(1, &J, st, why)) return rc;
-                    }
-                }
-                const int rc = launch_wgrad_reduce(a, part, nb, 8 * 8 * 25, 8, 8 * 25, L.wsum, st, why);
-                return rc ? rc : last_err(why);
-            }
-        }
         const int rc = a.hpart ? go_bwd_tiled<8, 8, 5, NCONV_LOAD_PLAIN, true, true>(d, a, part, tx, tc, st, why)
                                : go_bwd_tiled<8, 8, 5, NCONV_LOAD_PLAIN, true>(d, a, part, tx, tc, st, why);
         return rc ? rc : last_err(why);
@@ -1906,20 +1880,6 @@ int launch_bwd(const LayerDev& d, const BwdArgs& a, hipStream_t st, const char**
             *why = "fused tail backward needs nconv6's exact-fp32 geometry (16->8 3x3, padding 0, upsample-first "
                    "exactly-2x concat)";
             return -95;
-        }
-        if (!a.separate && (a.gxa || a.gca || a.gxb || a.gcb) && (a.gw || a.gb) && fused_tail_bwd_ok(L)) {
-            // input and weight gradient (and nconv7's) in one kernel (nconv_bwd_fused.hip)
-            const int nb = launch_bwd_fused_tail(d, a, part, (int)wm_grid(L).nblk, st);
-            if (nb > 0) {
-                if (a.defer) {
-                    *a.t7nparts = nb;
-                } else {
-                    const RedJob J{a.t7part, a.t7s, a.t7gw, nullptr, nb, 8, 1, 8};
-                    if (int rc = launch_wgrad_reduce_multi(1, &J, st, why)) return rc;
-                }
-                const int rc = launch_wgrad_reduce(a, part, nb, 8 * 16 * 9, 8, 16 * 9, L.wsum, st, why);
-                return rc ? rc : last_err(why);
-            }
         }
         const int rc = go_bwd_tiled<16, 8, 3, NCONV_LOAD_UPCAT_UP_FIRST, false, false, true>(d, a, part, tx, tc, st, why);
         return rc ? rc : last_err(why);

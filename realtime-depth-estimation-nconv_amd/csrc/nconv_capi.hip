@@ -329,7 +329,6 @@ int nconv_bwd_ex(const nconv_layer* L, nconv_bwd_io* io, void* workspace, size_t
     nconv::BwdArgs a{io->y, io->cout, io->gy, io->gcout, io->gxa, io->gca, io->gxb, io->gcb, io->gw, io->gbias,
                      (float*)workspace, workspace_bytes, (flags & NCONV_BWD_ACCUMULATE) ? 1 : 0, defer, &nparts,
                      io->gy_pool, io->gcout_pool, io->pool_argmax};
-    a.separate = (flags & NCONV_BWD_SEPARATE) ? 1 : 0;
     a.box = io->box_weights;
     io->head_nparts = 0;
     if (const nconv_layer* H = io->head) {

@@ -74,7 +74,6 @@ struct BwdArgs {
     float* t7gw;
     int* t7nparts;
     int t7ph, t7pw, t7pc0;  // nconv7's planes: (t7ph, t7pw) holding its grid from row / column t7pc0
-    int separate;  // NCONV_BWD_SEPARATE: no one-kernel backward (input and weight gradient as two kernels)
     const float* box;  // optional precomputed box weights of an exactly-2x UPCAT layer (dgrad_phase)
 };
 // nconv7 (1x1, padding 2) consumer fused into its producer's backward (T7): byte offset of nconv6
@@ -166,23 +165,6 @@ void go_dgrad_bf(const LayerDev& d, const BwdArgs& a, float* tmp_x, float* tmp_c
 int launch_bwd(const LayerDev& d, const BwdArgs& a, hipStream_t st, const char** why);
 // nconv1's weight-gradient partial rows of the fused head (200 weights, 8 sum gy, 8 sum gcout*cout)
 constexpr int kHeadNw = 8 * 25, kHeadStride = kHeadNw + 16;
-// One-kernel backward of an exact-fp32 8 -> 8 5x5 stride-1 layer with plain loads (input and weight
-// gradient together, nconv_bwd_fused.hip): the grid (64-column strips x row segments x images) and
-// its launch, with the pooled-output gradient (gp) and / or the fused nconv1 weight gradient (hw);
-// returns the number of partial rows written (<= max_blocks), or -1 when they would not fit.
-struct FusedGrid {
-    int nstrip, nseg, seg_rows, nblk;
-};
-FusedGrid fused_grid(const nconv_layer& L, int max_blocks);
-bool fused_bwd_ok(const nconv_layer& L);
-int launch_bwd_fused(const LayerDev& d, const BwdArgs& a, float* part, int max_blocks, bool gp, bool hw,
-                     hipStream_t st);
-// The same for nconv6 with nconv7's backward fused (T7: 16 -> 8 3x3, padding 0, upsample-first
-// exactly-2x concat): skip-channel input gradient at full resolution, upsampled-channel gradient
-// straight to the low-resolution producer (box weights), weight gradient, nconv7's weight gradient
-bool fused_tail_bwd_ok(const nconv_layer& L);
-int launch_bwd_fused_tail(const LayerDev& d, const BwdArgs& a, float* part, int max_blocks, hipStream_t st);
-
 // Dense convolutions (RGB-guided model).
 int dense_cout_tile(int Cout);
 size_t dense_packed_floats(int kind, int Cin, int Cout);

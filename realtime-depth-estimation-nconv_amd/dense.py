@@ -51,38 +51,6 @@ def cached(mod, name, tensors, build):
     return ent[1]
 
 
-# Training convolutions (DenseConvFn's forward) in this many batch slices, one stream each, every
-# slice writing its rows of the output (per-frame arithmetic: bitwise the one-launch result)
-TRAIN_SLICES = int(os.environ.get("NCONV_DENSE_TRAIN_SLICES", "1"))
-_SLICE_STREAMS = {}
-
-
-def conv_sliced(x0, kind, stride, wpack, bias, relu, cout, x1=None, n=2):
-    """conv() over n batch slices on n streams into one output tensor."""
-    B = x0.shape[0]
-    n = max(1, min(int(n), B))
-    if n == 1:
-        return conv(x0, kind, stride, wpack, bias, relu, cout, x1=x1)
-    out = conv(x0[:0], kind, stride, wpack, bias, relu, cout, x1=None if x1 is None else x1[:0])  # shape only
-    out = torch.empty((B,) + tuple(out.shape[1:]), device=x0.device, dtype=torch.float32)
-    dev = x0.device
-    if (dev.index, n) not in _SLICE_STREAMS:
-        _SLICE_STREAMS[(dev.index, n)] = [torch.cuda.Stream(device=dev) for _ in range(n - 1)]
-    side = _SLICE_STREAMS[(dev.index, n)]
-    cur = torch.cuda.current_stream(dev)
-    for st in side:
-        st.wait_stream(cur)
-    bounds = [B * k // n for k in range(n + 1)]
-    for k, st in enumerate([cur] + side):
-        with torch.cuda.stream(st):
-            b0, b1 = bounds[k], bounds[k + 1]
-            conv(x0[b0:b1], kind, stride, wpack, bias, relu, cout, x1=None if x1 is None else x1[b0:b1],
-                 out=out[b0:b1])
-    for st in side:
-        cur.wait_stream(st)
-    return out
-
-
 def conv(x0, kind, stride, wpack, bias, relu, cout, x1=None, wshort=None, out=None, out_c0=0):
     """[relu](conv(cat(x0, x1)) + bias) [+ shortcut]; written to out[:, out_c0:out_c0+cout] if out is given."""
     B, C0, H, W = x0.shape
@@ -202,32 +170,16 @@ def relu_bias_bwd(g, out, g_masked, gbias):
 
 
 # The training backward's weight gradient on a side stream, concurrent with the same layer's input
-# gradient(s): 1 = joined before the node returns; 2 = joined once, when the backward pass ends
-# (autograd's end-of-pass callback), so it also runs under the next layers' BatchNorm / ReLU
-# backward passes -- only when the parameter's .grad is unset (autograd then takes the tensor as is,
-# no accumulation kernel reads it before the join); 0 = serial
+# gradient(s), joined before the node returns (1; 0 = serial). Joining once at the end of the
+# backward pass measured slower (43.3 -> 44.0 ms per guided step, profiles/r5_ab_guided_wgrad_join.log)
 WGRAD_STREAM = int(os.environ.get("NCONV_DENSE_WGRAD_STREAM", "1"))
 _WGRAD_STREAMS = {}
-_JOIN_QUEUED = set()
 
 
 def _wgrad_stream(device):
     if device.index not in _WGRAD_STREAMS:
         _WGRAD_STREAMS[device.index] = torch.cuda.Stream(device=device)
     return _WGRAD_STREAMS[device.index]
-
-
-def _join_at_backward_end(cur, side):
-    """cur waits for the side stream when the running backward pass ends (once per pass)."""
-    key = (cur.device.index, cur.stream_id)
-    if key in _JOIN_QUEUED:
-        return
-
-    def join():
-        _JOIN_QUEUED.discard(key)
-        cur.wait_stream(side)
-    _JOIN_QUEUED.add(key)
-    torch.autograd.Variable._execution_engine.queue_callback(join)
 
 
 class DenseConvFn(torch.autograd.Function):
@@ -243,12 +195,8 @@ class DenseConvFn(torch.autograd.Function):
         cout = weight.shape[1] if kind == DENSE_TRANSPOSED_4X4 else weight.shape[0]
         wp = pack(kind, weight, cin, cout)
         b = bias.detach().contiguous() if bias is not None else None
-        if TRAIN_SLICES > 1:
-            out = conv_sliced(x0, kind, stride, wp, b, relu, cout, x1=x1, n=TRAIN_SLICES)
-        else:
-            out = conv(x0, kind, stride, wp, b, relu, cout, x1=x1)
+        out = conv(x0, kind, stride, wp, b, relu, cout, x1=x1)
         ctx.kind, ctx.stride, ctx.relu, ctx.c0 = kind, stride, relu, x0.shape[1]
-        ctx.wparam = weight  # (its .grad decides whether the weight gradient's join may wait)
         ctx.has_bias = bias is not None
         ctx.save_for_backward(x0, x1, weight, out if relu else None)
         return out
@@ -282,14 +230,7 @@ class DenseConvFn(torch.autograd.Function):
         if x1 is not None and need[1]:
             gx1 = dgrad(g, w[co:] if tr else w[:, co:], ctx.kind, ctx.stride, x1.shape)
         if side is not None:
-            if WGRAD_STREAM == 2 and ctx.wparam.grad is None:
-                # the side stream still reads g, x0, x1: their memory is not reused before it is done
-                for t in (g, x0, x1):
-                    if t is not None:
-                        t.record_stream(side)
-                _join_at_backward_end(cur, side)
-            else:
-                cur.wait_stream(side)
+            cur.wait_stream(side)
             gw.record_stream(cur)  # (made on the side stream, read on this one)
         elif need[2]:
             gw = wgrad(x0, x1, g, ctx.kind, ctx.stride, weight.shape)

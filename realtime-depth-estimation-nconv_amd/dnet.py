@@ -193,21 +193,16 @@ class DNETFn(torch.autograd.Function):
         sp = ctx.specs
         red = WgradReduce()  # every layer's weight-gradient reduction in two launches at the end
         cur = torch.cuda.current_stream(S.device)
-        sides = _wgrad_streams(S.device, WGRAD_STREAMS_N) if (ctx.pooled and WGRAD_STREAM) else []
-        side = sides[0] if sides else None
-        turn = [0]
+        side = _wgrad_stream(S.device) if (ctx.pooled and WGRAD_STREAM) else None
 
-        def layer_bwd(spec, inputs, y, co, gy, gco, gin, gw_, gb_, fused=False, **kw):
-            # fused: one call (one kernel) for the input and the weight gradient (the exact-fp32 8 -> 8
-            # 5x5 layers with a pooled-output gradient, nconv_bwd_fused.hip). Otherwise the weight
-            # gradient runs on the side stream, concurrent with this layer's input gradient (and the
-            # next layers' input gradients, which do not depend on it): it needs only tensors that are
-            # complete when this layer's backward starts
-            if side is None or (gw_ is None and gb_ is None) or fused:
-                layer_backward(spec, inputs, y, co, gy, gco, gin, gw_, gb_, defer=red, separate=not fused, **kw)
+        def layer_bwd(spec, inputs, y, co, gy, gco, gin, gw_, gb_, **kw):
+            # the weight gradient runs on the side stream, concurrent with this layer's input gradient
+            # (and the next layers' input gradients, which do not depend on it): it needs only tensors
+            # that are complete when this layer's backward starts
+            if side is None or (gw_ is None and gb_ is None):
+                layer_backward(spec, inputs, y, co, gy, gco, gin, gw_, gb_, defer=red, **kw)
                 return
-            st = sides[turn[0] % len(sides)]  # (several weight-gradient streams: round robin)
-            turn[0] += 1
+            st = side
             st.wait_stream(cur)
             tail, head = kw.pop("tail", None), kw.pop("head", None)
             layer_backward(spec, inputs, y, co, gy, gco, gin, None, None, defer=red, head=head,
@@ -221,11 +216,11 @@ class DNETFn(torch.autograd.Function):
             gy, gco = G[k] if G[k] is not None else (g9, None)
             layer_bwd(spec or sp[k - 1], (xa, ca, xb, cb, *W[k - 1]), X[k][0], X[k][1], gy, gco,
                       (*(ga or (None, None)), *(gb_ or (None, None))), gw[k - 1], gb[k - 1], accumulate=acc,
-                      pool_grad=pool_grad, fused=pool_grad is not None and LAYERS[k - 1] in FUSED_BWD, box=box)
+                      pool_grad=pool_grad, box=box)
 
         def finish():
-            for st in sides:
-                cur.wait_stream(st)
+            if side is not None:
+                cur.wait_stream(side)
             red.run(S.device)
 
         G[2], G[7] = (e(X[2][0]), e(X[2][1])), (e(X[7][0]), e(X[7][1]))
@@ -243,7 +238,7 @@ class DNETFn(torch.autograd.Function):
             layer_bwd(sp[7], (X[2][0], X[2][1], X[7][0], X[7][1], *W[7]), X[8][0], X[8][1], None, None,
                       (*G[2], *G[7]), gw[7], gb[7],
                       tail=(sp[8], *W[8], X[9][0], X[9][1], g9c, gw[8], None if ctx.crop is None else 1),
-                      fused="nconv6" in FUSED_BWD, box=wbox[2])
+                      box=wbox[2])
             if gb[8] is not None:
                 red.add_sum(g9c, gb[8])
         else:
@@ -266,7 +261,7 @@ class DNETFn(torch.autograd.Function):
             if FUSE_HEAD_BWD and not need[1]:  # nconv2's input gradient feeds nconv1's weight gradient in-tile
                 layer_bwd(sp[1], (X[1][0], X[1][1], None, None, *W[1]), X[2][0], X[2][1], *G[2],
                           (None, None, None, None), gw[1], gb[1], pool_grad=(*gp2, a2),
-                          head=(sp[0], S, *W[0], gw[0], gb[0]), fused="nconv2" in FUSED_BWD)
+                          head=(sp[0], S, *W[0], gw[0], gb[0]))
                 finish()
                 out = [None, None, None, None]
                 for i in range(9):
@@ -298,9 +293,6 @@ FUSE_TAIL_BWD = True
 FUSE_HEAD_BWD = True
 FUSE_HEAD_FWD = True  # the training forward's nconv1 + nconv2 as the exact fused head (nconv_fwd_head)
 FUSE_TAIL_FWD = True  # ... and nconv6 + nconv7 as the fused tail (nconv_fwd_tail over nconv7's whole grid)
-# Layers whose backward (with the pooled-output gradient) runs the input and the weight gradient as
-# ONE kernel (nconv_bwd_fused.hip) instead of two on two streams
-FUSED_BWD = frozenset(os.environ.get("NCONV_FUSED_BWD", "").split(",")) - {""}
 
 
 def _tail_train(sp6, sp7, x2, c2, x7, c7, W6, W7, w6, crop=None, out=None):
@@ -337,23 +329,16 @@ class CropFn(torch.autograd.Function):
         return torch.nn.functional.pad(g, ctx.pad), None, None
 
 
+# The training backward's weight gradients on one side stream (two round-robin streams measured
+# slower: 2.20 -> 2.26 ms per graphed step, profiles/r5_ab_two_wgrad_streams.log)
 WGRAD_STREAM = True
 _WGRAD_STREAMS = {}
 
 
 def _wgrad_stream(device):
-    return _wgrad_streams(device, 1)[0]
-
-
-# weight-gradient streams of the training backward (layers round-robin over them)
-WGRAD_STREAMS_N = int(os.environ.get("NCONV_WGRAD_STREAMS", "1"))
-
-
-def _wgrad_streams(device, n):
-    have = _WGRAD_STREAMS.setdefault(device.index, [])
-    while len(have) < max(1, n):
-        have.append(torch.cuda.Stream(device=device))
-    return have[:max(1, n)]
+    if device.index not in _WGRAD_STREAMS:
+        _WGRAD_STREAMS[device.index] = torch.cuda.Stream(device=device)
+    return _WGRAD_STREAMS[device.index]
 
 
 def _materialise_pool(S):
@@ -490,13 +475,6 @@ class DNET(nn.Module):
     # bitwise the three separate launches); False: the separate launches.
     merged_prologue = True
 
-    # Inference split over streams (inference_streams > 1): True = each stream builds its own copy
-    # of the weight prologue (one small launch), so the side streams start with the main one
-    # instead of waiting for its prologue across streams. Measured slower at B=8 352x1216 (16.3-16.5
-    # k against 16.9-17.2 k frames/s, same box, three alternations: profiles/r5_ab_stream_prologue.log):
-    # the side stream's ~6 us later start staggers the two halves' kernels usefully. Off by default.
-    stream_prologue = os.environ.get("NCONV_STREAM_PROLOGUE", "0") == "1"
-
     def _eval_prologue_ok(self, layers):
         """Whether the one-launch eval prologue applies (see _eval_prologue)."""
         if not self.merged_prologue:
@@ -555,9 +533,6 @@ class DNET(nn.Module):
         out_h, out_w = crop_hw(H, W, self.crop)
         if not grad and min(H, W) >= 16:
             out = torch.empty((S.shape[0], 1, out_h, out_w), device=S.device, dtype=torch.float32)
-            if self.stream_prologue and self._n_streams(S.shape[0]) > 1 and self._eval_prologue_ok(layers):
-                self._infer_split(S, layers, None, out, per_stream_prologue=True)
-                return out
             pro = self._eval_prologue(layers, S)
             if pro is None:
                 wsum, wph, w21 = self._prologue(layers, S), self._phase_weights(S.device), None
@@ -676,10 +651,10 @@ class DNET(nn.Module):
             cache[key] = [torch.cuda.Stream(device=device) for _ in range(n)]
         return cache[key]
 
-    def _infer_split(self, S, layers, wsum, out, wph=None, w21=None, per_stream_prologue=False):
-        """The inference chain on batch slices, one stream each. per_stream_prologue: each stream
-        runs its own eval prologue (wsum / wph / w21 unused) -- the outputs are the same (the
-        prologue is a deterministic function of the weights)."""
+    def _infer_split(self, S, layers, wsum, out, wph=None, w21=None):
+        """The inference chain on batch slices, one stream each (the weight prologue once, on the
+        current stream, before the fork: a prologue per stream measured slower, 16.3-16.5 k against
+        16.9-17.2 k frames/s, profiles/r5_ab_stream_prologue.log)."""
         B = S.shape[0]
         n = self._n_streams(B)
         bounds = self.split_bounds(B, n, self.inference_shares, self._configured_streams())
@@ -695,18 +670,15 @@ class DNET(nn.Module):
                 continue
             with torch.cuda.stream(st):
                 Sk = S[bounds[k]:bounds[k + 1]]
-                if per_stream_prologue:
-                    wsum, wph, w21 = self._eval_prologue(layers, Sk)
-                self._infer(Sk, layers, wsum, out[bounds[k]:bounds[k + 1]], wph, mid=False, w21=w21)
+                self._infer(Sk, layers, wsum, out[bounds[k]:bounds[k + 1]], wph, w21=w21)
         for st in side:
             cur.wait_stream(st)
 
-    def _infer(self, S, layers, wsum, out, wph=None, mid=True, w21=None):
+    def _infer(self, S, layers, wsum, out, wph=None, w21=None):
         """The inference chain on the current stream: each producer also writes the pooled input
         of the next down layer, and nconv6+nconv7+crop run as one launch writing `out`. wph: the
-        phase weights of nconv4/5/6 (_phase_weights) or None. mid=False (inside an inference
-        split): no nested mid_streams split. w21: the exact head's weights when the prologue
-        already built them (_eval_prologue), else built here."""
+        phase weights of nconv4/5/6 (_phase_weights) or None. w21: the exact head's weights when
+        the prologue already built them (_eval_prologue), else built here."""
         (l1, l2, d1, d2, d3, l4, l5, l6, l7) = layers
         (s1, s2, sd1, sd2, sd3, s4, s5, s6, s7) = wsum
         w4, w5, w6 = (None, None, None) if wph is None else tuple(wph)
@@ -721,57 +693,13 @@ class DNET(nn.Module):
             x1, c1 = f(l1.spec(_lib.THRESH, 0.01), S, None, None, None, l1.weight, l1.bias, s1)
             x1, c1, p1, q1 = fp(l2.spec(), x1, c1, None, None, l2.weight, l2.bias, s2)
         x2, c2, p2, q2 = fp(d1.spec(), p1, q1, None, None, d1.weight, d1.bias, sd1)
-        n = max(1, min(int(self.mid_streams), S.shape[0])) if mid else 1
-        if n == 1:
-            x3, c3, p3, q3 = fp(d2.spec(), p2, q2, None, None, d2.weight, d2.bias, sd2)
-            x4, c4 = f(d3.spec(), p3, q3, None, None, d3.weight, d3.bias, sd3)
-            x34, c34 = f(l4.spec(_lib.UPCAT_SKIP_FIRST), x3, c3, x4, c4, l4.weight, l4.bias, s4, wphase=w4)
-        else:
-            x3, c3, p3, q3, x4, c4, x34, c34 = self._mid_split(n, layers, wsum, p2, q2, w4)
+        x3, c3, p3, q3 = fp(d2.spec(), p2, q2, None, None, d2.weight, d2.bias, sd2)
+        x4, c4 = f(d3.spec(), p3, q3, None, None, d3.weight, d3.bias, sd3)
+        x34, c34 = f(l4.spec(_lib.UPCAT_SKIP_FIRST), x3, c3, x4, c4, l4.weight, l4.bias, s4, wphase=w4)
         if self.capture is not None:
             self.capture.update(down1=(x1, c1), down2=(x2, c2), down3=(x3, c3))
         x23, c23 = f(l5.spec(_lib.UPCAT_SKIP_FIRST), x2, c2, x34, c34, l5.weight, l5.bias, s5, wphase=w5)
         self._fused_tail(l6, l7, s6, s7, x1, c1, x23, c23, out, w6)
-
-    # The quarter- and eighth-resolution layers (down2, down3, nconv4) have too few tiles to fill
-    # the chip evenly (e.g. 836 tiles of down2 on 768 resident workgroups: a second, nearly empty
-    # round). With mid_streams = n > 1 they run on n batch slices in n streams, so one slice's
-    # next layer fills the other's partial round; outputs land in full-batch tensors (no copies).
-    # Measured slower at B=8 352x1216 (19.1-19.4 k vs 18.7-18.8 k frames/s with 2 slices, 16.7-16.9 k
-    # with 4: each slice's persistent grid is sized to the whole chip), so the default is 1.
-    mid_streams = int(os.environ.get("NCONV_MID_STREAMS", "1"))
-
-    def _mid_split(self, n, layers, wsum, p2, q2, w4=None):
-        (l1, l2, d1, d2, d3, l4, l5, l6, l7) = layers
-        (s1, s2, sd1, sd2, sd3, s4, s5, s6, s7) = wsum
-        B, C, H4, W4 = p2.shape
-        dev = p2.device
-        e = lambda *sh: torch.empty(sh, device=dev, dtype=torch.float32)
-        H8, W8 = d2.spec().out_hw(H4, W4)
-        x3, c3 = e(B, 8, H8, W8), e(B, 8, H8, W8)
-        p3, q3 = e(B, 8, H8 // 2, W8 // 2), e(B, 8, H8 // 2, W8 // 2)
-        H16, W16 = d3.spec().out_hw(H8 // 2, W8 // 2)
-        x4, c4 = e(B, 8, H16, W16), e(B, 8, H16, W16)
-        sp4 = l4.spec(_lib.UPCAT_SKIP_FIRST)
-        H34, W34 = sp4.out_hw(*sp4.in_hw((B, 8, H8, W8), (B, 8, H16, W16)))
-        x34, c34 = e(B, 8, H34, W34), e(B, 8, H34, W34)
-        cur = torch.cuda.current_stream(dev)
-        side = self._side_streams(dev, n - 1)
-        for st in side:
-            st.wait_stream(cur)
-        bounds = [B * k // n for k in range(n + 1)]
-        for k, st in enumerate([cur] + side):
-            sl = slice(bounds[k], bounds[k + 1])
-            with torch.cuda.stream(st):
-                layer_forward_pooled(d2.spec(), p2[sl], q2[sl], None, None, d2.weight, d2.bias, sd2,
-                                     out=(x3[sl], c3[sl], p3[sl], q3[sl]))
-                layer_forward_raw(d3.spec(), p3[sl], q3[sl], None, None, d3.weight, d3.bias, sd3,
-                                  out=(x4[sl], c4[sl]))
-                layer_forward_raw(sp4, x3[sl], c3[sl], x4[sl], c4[sl], l4.weight, l4.bias, s4,
-                                  out=(x34[sl], c34[sl]), wphase=w4)
-        for st in side:
-            cur.wait_stream(st)
-        return x3, c3, p3, q3, x4, c4, x34, c34
 
     # Inference evaluates nconv1 inside nconv2's kernel (nconv_fwd_head) when the layers have
     # DNET's geometry -- in exact fp32 with nconv1 on the nonzero taps only and nconv2's confidence

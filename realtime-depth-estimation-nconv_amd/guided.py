@@ -65,15 +65,20 @@ class RGBEncoder(nn.Module):
     def forward(self, x):
         return self.encoder(x) + self.downsample(x)
 
-    def dense_forward(self, x):
+    def dense_plans(self):
+        """(packed 3x3 weights with eval BN folded, shift, packed shortcut), cached (dense.cached)."""
         conv, bn, sc = self.encoder[0], self.encoder[1], self.downsample[0]
 
         def build():
             scale, shift = D.bn_fold(bn, conv.bias)
             return (D.pack(D.DENSE_3X3, conv.weight, conv.in_channels, conv.out_channels, scale), shift,
                     D.pack(D.DENSE_1X1, sc.weight, sc.in_channels, sc.out_channels))
-        wp, bias, ws = D.cached(self, "enc", [conv.weight, conv.bias, bn.weight, bn.bias, bn.running_mean,
-                                              bn.running_var, sc.weight], build)
+        return D.cached(self, "enc", [conv.weight, conv.bias, bn.weight, bn.bias, bn.running_mean,
+                                      bn.running_var, sc.weight], build)
+
+    def dense_forward(self, x):
+        conv = self.encoder[0]
+        wp, bias, ws = self.dense_plans()
         return D.conv(x, D.DENSE_3X3, conv.stride[0], wp, bias, True, conv.out_channels, wshort=ws)
 
     def train_forward(self, x):
@@ -98,7 +103,7 @@ class Basic2d(nn.Module):
     def forward(self, x):
         return self.conv(x)
 
-    def dense_forward(self, x0, x1=None, out=None, out_c0=0):
+    def dense_plans(self):
         conv = self.conv.conv
         bn = getattr(self.conv, "bn", None)
         if conv.kernel_size != (3, 3) or conv.padding != (1, 1) or not isinstance(self.conv.relu, nn.ReLU):
@@ -112,7 +117,11 @@ class Basic2d(nn.Module):
             return D.pack(D.DENSE_3X3, conv.weight, conv.in_channels, conv.out_channels, scale), shift
         ts = [conv.weight] + ([conv.bias] if conv.bias is not None else []) + \
             ([bn.weight, bn.bias, bn.running_mean, bn.running_var] if bn is not None else [])
-        wp, bias = D.cached(self, "conv", ts, build)
+        return D.cached(self, "conv", ts, build)
+
+    def dense_forward(self, x0, x1=None, out=None, out_c0=0):
+        conv = self.conv.conv
+        wp, bias = self.dense_plans()
         return D.conv(x0, D.DENSE_3X3, conv.stride[0], wp, bias, True, conv.out_channels, x1=x1, out=out,
                       out_c0=out_c0)
 
@@ -139,7 +148,7 @@ class Basic2dTrans(nn.Module):
     def forward(self, x):
         return self.relu(self.bn(self.conv(x.contiguous())))
 
-    def dense_forward(self, x0, x1=None):
+    def dense_plans(self):
         conv, bn = self.conv, self.bn
 
         def build():
@@ -151,9 +160,12 @@ class Basic2dTrans(nn.Module):
             return D.pack(D.DENSE_TRANSPOSED_4X4, conv.weight, conv.in_channels, conv.out_channels, scale), shift
         ts = [conv.weight] + ([conv.bias] if conv.bias is not None else []) + \
             ([bn.weight, bn.bias, bn.running_mean, bn.running_var] if isinstance(bn, nn.BatchNorm2d) else [])
-        wp, bias = D.cached(self, "convT", ts, build)
+        return D.cached(self, "convT", ts, build)
+
+    def dense_forward(self, x0, x1=None):
+        wp, bias = self.dense_plans()
         return D.conv(x0, D.DENSE_TRANSPOSED_4X4, 2, wp, bias, isinstance(self.relu, nn.ReLU),
-                      conv.out_channels, x1=x1)
+                      self.conv.out_channels, x1=x1)
 
     def train_forward(self, x0, x1=None):
         y = D.conv_fn(x0, self.conv.weight, self.conv.bias, D.DENSE_TRANSPOSED_4X4, 2, x1=x1)
@@ -193,12 +205,16 @@ class ConvBlock(nn.Module):
     def forward(self, x):
         return self.relu(self.conv(x))
 
-    def dense_forward(self, x, out=None, out_c0=0):
+    def dense_plans(self):
         conv = self.conv
 
         def build():
             return D.pack(D.DENSE_3X3, conv.weight, conv.in_channels, conv.out_channels), conv.bias.detach().contiguous()
-        wp, bias = D.cached(self, "conv", [conv.weight, conv.bias], build)
+        return D.cached(self, "conv", [conv.weight, conv.bias], build)
+
+    def dense_forward(self, x, out=None, out_c0=0):
+        conv = self.conv
+        wp, bias = self.dense_plans()
         return D.conv(x, D.DENSE_3X3, conv.stride[0], wp, bias, True, conv.out_channels, out=out, out_c0=out_c0)
 
     def train_forward(self, x0, x1=None):
@@ -333,6 +349,22 @@ def _dense_chain(m, rgb, sparse):
     return d0, d1, d2, d3
 
 
+_DENSE_CHAIN = ("rgb_encoder0", "rgb_encoder1", "rgb_encoder2", "rgb_encoder3", "fuse0", "fuse1", "fuse2", "fuse3")
+
+
+def prepare_dense_plans(m):
+    """Build (or validate) every packed-weight plan the eval chain reads, on the current stream.
+    The batch-sliced forward calls this before forking: a plan built lazily inside one slice's
+    chain would be launched on that slice's stream, and the other slices -- which find it cached --
+    would read it with no ordering after the pack launch (a cold cache, or any weight / BatchNorm
+    change bumping a version counter)."""
+    for name in _DENSE_CHAIN:
+        for mod in getattr(m, name).modules():
+            plans = getattr(mod, "dense_plans", None)
+            if plans is not None:
+                plans()
+
+
 def _guided_forward_dense(m, rgb0, depth0, rgb1, depth1):
     sparse = m.step1(depth0, depth1).contiguous()
     rgb = torch.cat((rgb0, rgb1), dim=0).contiguous()
@@ -341,6 +373,7 @@ def _guided_forward_dense(m, rgb0, depth0, rgb1, depth1):
     if n == 1:
         return _dense_chain(m, rgb, sparse)
     dev = rgb.device
+    prepare_dense_plans(m)  # on cur, before the side streams' wait_stream(cur)
     if (dev.index, n) not in _GUIDED_STREAMS:
         _GUIDED_STREAMS[(dev.index, n)] = [torch.cuda.Stream(device=dev) for _ in range(n - 1)]
     side = _GUIDED_STREAMS[(dev.index, n)]

@@ -208,9 +208,11 @@ _SYNC = {}
 
 
 def sync_counter(device):
-    """The device's zero int32 counter for train_prologue (made once, zero-filled; every call
-    leaves it at zero)."""
-    key = torch.device(device).index
+    """A zero int32 counter for train_prologue (made once, zero-filled; every call leaves it at
+    zero), one per (device, current stream): two prologues running concurrently on different
+    streams must not count their last-block arrivals on one counter."""
+    device = torch.device(device)
+    key = (device.index, torch.cuda.current_stream(device).stream_id)
     if key not in _SYNC:
         _SYNC[key] = torch.zeros(1, dtype=torch.int32, device=device)
     return _SYNC[key]
@@ -316,7 +318,7 @@ class NConvLayerFn(torch.autograd.Function):
 
 
 def layer_backward(spec: LayerSpec, inputs, y, co, gy, gco, gin, gw, gb, accumulate=False, defer=None,
-                   pool_grad=None, head=None, tail=None, separate=False, box=None):
+                   pool_grad=None, head=None, tail=None, box=None):
     """nconv_bwd of one fused layer: gin = (gxa, gca, gxb, gcb) (None: skip) overwritten, or added
     into with accumulate=True (NCONV_BWD_ACCUMULATE: a tensor consumed by two layers); gw, gb
     overwritten (None: skip). defer: a WgradReduce collecting the layer's weight-gradient partial
@@ -327,9 +329,7 @@ def layer_backward(spec: LayerSpec, inputs, y, co, gy, gco, gin, gw, gb, accumul
     then computed inside this layer's input gradient (nconv_bwd_ex head; gin's gxa / gca optional).
     tail: (spec, weight, bias, wsum, y9, cout9, gy9, gw9) of the 1x1 consumer nconv7, whose backward
     is fused into this layer's (nconv_bwd_ex tail; gy / gco are then unused and may be None; nconv7's
-    bias gradient is the caller's). With pool_grad and both an input gradient (or head) and gw / gb
-    requested, an exact-fp32 8 -> 8 5x5 layer runs one kernel for both gradients (include/nconv.h
-    NCONV_BWD_SEPARATE); separate=True runs the input- and weight-gradient kernels instead. tail may
+    bias gradient is the caller's). The input and the weight gradient are separate kernels. tail may
     carry a 9th element, the crop origin of nconv7's planes when they hold a window of its grid
     (DNET's crop: nconv_bwd_io tail_crop0 / tail_h / tail_w). box: an exactly-2x UPCAT layer's box
     weights (train_prologue), else built by this call."""
@@ -344,8 +344,7 @@ def layer_backward(spec: LayerSpec, inputs, y, co, gy, gco, gin, gw, gb, accumul
     lib = _lib.lib()
     ws_bytes = lib.nconv_bwd_workspace_bytes(_lib.ctypes.byref(L))
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
-    flags = (_lib.BWD_ACCUMULATE if accumulate else 0) | (_lib.BWD_DEFER_REDUCE if defer is not None else 0) | \
-        (_lib.BWD_SEPARATE if separate else 0)
+    flags = (_lib.BWD_ACCUMULATE if accumulate else 0) | (_lib.BWD_DEFER_REDUCE if defer is not None else 0)
     io = _lib.NconvBwdIo()
     gpy, gpc, parg = pool_grad if pool_grad is not None else (None, None, None)
     for name, t in (("y", y), ("cout", co), ("gy", gy), ("gcout", gco), ("gxa", gxa), ("gca", gca), ("gxb", gxb),

@@ -1,7 +1,10 @@
+import faulthandler
 import os
 import sys
 
 import pytest
+
+faulthandler.enable()  # a host fault under a test leaves the Python stacks of every thread in the log
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:

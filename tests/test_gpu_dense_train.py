@@ -40,11 +40,8 @@ CASES = [
 ]
 
 
-@pytest.mark.parametrize("db", ["0", "1"])  # NCONV_WGD_DB: the opt-in double-buffered weight gradient
 @pytest.mark.parametrize("kind,stride,c0,c1,cout,H,W,relu,bias", CASES)
-def test_dense_conv_fn_forward_backward(nconv_amd, gpu, kind, stride, c0, c1, cout, H, W, relu, bias, db,
-                                        monkeypatch):
-    monkeypatch.setenv("NCONV_WGD_DB", db)
+def test_dense_conv_fn_forward_backward(nconv_amd, gpu, kind, stride, c0, c1, cout, H, W, relu, bias):
     D = nconv_amd.dense
     g = torch.Generator().manual_seed(kind * 1000 + c0 * 10 + cout + H)
     B, cin = 2, c0 + c1

@@ -98,8 +98,6 @@ def test_whole_graph_autograd_matches_per_layer(nconv_amd, gpu, H, W, monkeypatc
     # checked against the oracle in test_dnet_train_gradients and bitwise in the layer tests)
     monkeypatch.setattr(sys.modules[nconv_amd.DNET.__module__], "FUSE_HEAD_FWD", False)
     monkeypatch.setattr(sys.modules[nconv_amd.DNET.__module__], "FUSE_TAIL_FWD", False)
-    # (the per-layer path has no pooled-gradient one-kernel backward: compare like with like)
-    monkeypatch.setattr(sys.modules[nconv_amd.DNET.__module__], "FUSED_BWD", frozenset())
     res = []
     for whole in (True, False):
         net = make_net(nconv_amd, "generalized", gpu)
@@ -133,7 +131,6 @@ def test_materialised_pool_matches_pool_on_load(nconv_amd, gpu, H, W, monkeypatc
     dnet = sys.modules[nconv_amd.DNET.__module__]
     res = []
     monkeypatch.setattr(dnet, "FUSE_TAIL_BWD", False)
-    monkeypatch.setattr(dnet, "FUSED_BWD", frozenset())  # the two-kernel backward (one-kernel: test_gpu_fused_bwd)
     monkeypatch.setattr(dnet, "FUSE_HEAD_FWD", False)  # (the fused head's D2 rounds differently)
     monkeypatch.setattr(dnet, "FUSE_TAIL_FWD", False)
     for pooled in (True, False):
@@ -302,28 +299,6 @@ def test_dnet_train_gradients(nconv_amd, gpu, H, W, bwd_math):
     report = _train_gradients_vs_oracle(nconv_amd, gpu, 2, H, W, "literal", False)
     print("\n".join(report))
     assert not any(r.endswith("FAIL") for r in report), "\n".join(report)
-
-
-@pytest.mark.parametrize("n", [2, 3])
-def test_mid_streams_split_matches_one_stream(nconv_amd, gpu, n):
-    """Inference with down2/down3/nconv4 run on batch slices in several streams (DNET.mid_streams)
-    writes the same bits as the one-stream chain (same kernels per frame), eager and graphed."""
-    net = make_net(nconv_amd, "generalized", gpu)
-    net.d_net.inference_streams = 1  # (mid_streams applies to an unsplit chain)
-    g = torch.Generator().manual_seed(31)
-    S = sparse_depth(g, 5, 96, 160).to(gpu)
-    with torch.no_grad():
-        net.d_net.mid_streams = 1
-        a = net(S)
-        net.d_net.mid_streams = n
-        b = net(S)
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            c = net(S)
-        graph.replay()
-        torch.cuda.synchronize()
-        net.d_net.mid_streams = 1
-    assert torch.equal(a, b) and torch.equal(a, c)
 
 
 @pytest.mark.parametrize("n", [2, 3, 8])

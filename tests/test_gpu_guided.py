@@ -64,12 +64,20 @@ def test_guided_generalized_crop_vs_oracle(nconv_amd, gpu, H, W):
         _close(g1[i], r1[i], f"pair1 scale {i}")
 
 
+_SPREAD = None
+
+
 def _tol64(k):
-    """Normwise gradient bound against the float64 oracle: 2e-3, and 5e-3 for the four RGB-encoder
-    convolutions (each feeds training-mode BatchNorm on inputs of large mean: the most
-    ill-conditioned gradients of the chain; the reference's own fp32 CPU values of these lie up to
-    2.7e-3 from float64 at 480x640, golden f9)."""
-    return 5e-3 if k.startswith("rgb_encoder") and k.endswith("encoder.0.weight") else 2e-3
+    """Normwise gradient bound against the float64 oracle, per tensor: max(1e-3, 1.5 x the
+    reference's own fp32 error on that tensor in golden f9's iteration (tests/golden/f9_ref_spread.json,
+    tools/f9_spread.py: the reference's fp32 CPU gradient vs the float64 oracle). 1e-3 is SURVEY
+    8(c)'s gradient bound; only the four RGB-encoder convolutions feeding training-mode BatchNorm on
+    0..255 input (the reference itself 1.5-2.7e-3 from float64) get more."""
+    global _SPREAD
+    if _SPREAD is None:
+        import json
+        _SPREAD = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "f9_ref_spread.json")))["spread"]
+    return max(1e-3, 1.5 * _SPREAD[k])
 
 
 @pytest.mark.timeout(400)
@@ -80,10 +88,10 @@ def test_guided_training_iteration_matches_reference_f9(nconv_amd, gpu):
     GPU path, against the reference's own numbers and the float64 oracle of the same iteration.
 
     Outputs |gpu - ref| <= 1e-4*|ref| + 1e-5, loss 1e-5 relative, BatchNorm running statistics after
-    the step 1e-4 relative + 1e-5, num_batches_tracked exact. Gradients, normwise: within 2e-3 of the
-    float64 oracle (5e-3 for the RGB-encoder convolutions, _tol64) and that + 1e-3 of the reference.
-    Why not 1e-3 here (it holds for every step-1 gradient,
-    tests/test_gpu_golden.py): this chain is ~20 convolution / training-mode BatchNorm layers deep,
+    the step 1e-4 relative + 1e-5, num_batches_tracked exact. Gradients, normwise: within
+    max(1e-3, 1.5 x the reference's own fp32 spread on that tensor) of the float64 oracle (_tol64)
+    and that + 1e-3 of the reference. Why more than 1e-3 on a few tensors (1e-3 holds for every
+    step-1 gradient, tests/test_gpu_golden.py): this chain is ~20 convolution / training-mode BatchNorm layers deep,
     and a convolution that feeds training-mode BatchNorm has a gradient that is a small difference of
     large terms (BatchNorm removes the component along the channel mean; condition ~360 for the RGB
     encoder on 0..255 input), so fp32 rounding anywhere upstream shows there amplified: the
@@ -126,7 +134,8 @@ def test_guided_training_iteration_matches_reference_f9(nconv_amd, gpu):
     for k in names:
         got = named[k].grad.double().cpu()
         e64, eref, ref64 = grad_rel(got, g64[k], k, g64), grad_rel(got, refs[k], k, refs), grad_rel(refs[k], g64[k], k, g64)
-        report.append(f"{k}: vs fp64 {e64:.2e}, vs reference {eref:.2e} (reference vs fp64 {ref64:.2e})")
+        report.append(f"{k}: vs fp64 {e64:.2e}, vs reference {eref:.2e} (reference vs fp64 {ref64:.2e}, "
+                      f"bound {_tol64(k):.2e})")
         if e64 > _tol64(k) or eref > _tol64(k) + 1e-3:
             bad.append(report[-1])
     print("\n".join(report))
@@ -191,9 +200,8 @@ def test_guided_config4_full_size_training_vs_oracle(nconv_amd, gpu):
     """Config 4's per-GPU training step at its own batch and frame size: 4+4 frames of 352x1216
     (bench.py make_guided_train_step's B/2 + B/2 at B=8), train mode (batch-statistics BatchNorm over
     the 4-frame batch, frozen drifted step 1), calculate_loss_multi_resolution (MSE, on element [0]
-    as utils.py:63-71), backward: every trainable gradient normwise within 2e-3 of the float64 oracle
-    (5e-3 for the RGB-encoder convolutions: the fp32 spread of this deep BatchNorm chain, see the f9
-    test), outputs 1e-4 |ref| + 1e-5."""
+    as utils.py:63-71), backward: every trainable gradient normwise within _tol64 of the float64
+    oracle (max(1e-3, 1.5 x the reference's fp32 spread on that tensor in f9), outputs 1e-4 |ref| + 1e-5."""
     from guided_cases import grad_rel, trainable_setp2
     model = _kitti_model(nconv_amd, gpu, seed=4)
     H, W, n = 352, 1216, 4
@@ -222,7 +230,7 @@ def test_guided_config4_full_size_training_vs_oracle(nconv_amd, gpu):
         _close(est[i].detach(), r0[i].detach(), f"scale {i}")
     refs = {k: leaves[k].grad for k in names}
     rel = {k: grad_rel(named[k].grad.double().cpu(), refs[k], k, refs) for k in names}
-    print("\n".join(f"{k}: {r:.2e}" for k, r in rel.items()))
+    print("\n".join(f"{k}: {r:.2e} (bound {_tol64(k):.2e})" for k, r in rel.items()))
     bad = [f"{k}: {r:.2e}" for k, r in rel.items() if r > _tol64(k)]
     assert not bad, "\n".join(bad)
 
@@ -291,35 +299,40 @@ def test_guided_eval_streams_bitwise(nconv_amd, gpu, H, W, n):
         assert torch.equal(a[i], b[i]), i
 
 
-@pytest.mark.parametrize("H,W,n", [(64, 96, 1), (72, 200, 3)])
-def test_guided_train_sliced_convs_bitwise(nconv_amd, gpu, H, W, n):
-    """The training convolutions' forward in two batch slices on two streams (dense.TRAIN_SLICES,
-    each slice writing its rows of the output) equals the one-launch pass bitwise: estimate, loss
-    and every parameter gradient of one config-4 iteration (n = 3: 6 frames, slices 3 + 3)."""
-    Dm = nconv_amd.dense
-    g = torch.Generator().manual_seed(41)
-    gt = ((torch.rand(n, 1, 480, 640, generator=g) * 79 + 1) * (torch.rand(n, 1, 480, 640, generator=g) < 0.5)).to(gpu)
-    ins = [t.to(gpu) for t in f5_inputs(H, W, n)]
+def test_guided_eval_streams_plans_built_before_fork(nconv_amd, gpu):
+    """The batch-sliced eval forward builds every packed-weight plan on the current stream before
+    the side streams fork (guided.prepare_dense_plans): after weights and BatchNorm statistics are
+    changed in place between two calls, every plan is current at the fork (no slice builds one), and
+    the sliced pass equals the one-stream pass bitwise."""
+    model = _kitti_model(nconv_amd, gpu).eval()
+    ins = [t.to(gpu) for t in f5_inputs(64, 96, 2)]
+    G = nconv_amd.guided
+    keep = G.GUIDED_STREAMS
+    built = []
+    D = nconv_amd.dense
+    orig = D.cached
 
-    def run(slices):
-        Dm.TRAIN_SLICES = slices
-        torch.manual_seed(2)
-        net = nconv_amd.SETP2_BP_TRAIN(None, step1_crop="generalized").to(gpu).train()
-        est, _ = net(*ins)
-        loss = nconv_amd.train.calculate_loss_multi_resolution(est, gt, False)
-        loss.backward()
-        torch.cuda.synchronize()
-        return [e.detach() for e in est], loss.detach(), {k: p.grad for k, p in net.named_parameters()
-                                                          if p.grad is not None}
-    keep = Dm.TRAIN_SLICES
+    def spy(mod, name, tensors, build):
+        def b():
+            built.append((id(mod), name, torch.cuda.current_stream(gpu).stream_id))
+            return build()
+        return orig(mod, name, tensors, b)
     try:
-        ea, la, ga = run(2)
-        eb, lb, gb = run(1)
+        with torch.no_grad():
+            G.GUIDED_STREAMS = 2
+            G._guided_forward(model, *ins)
+            model.fuse3.fuse.fuse_conv2.conv.weight.mul_(1.125)
+            model.rgb_encoder1.encoder[1].running_var.mul_(0.75)
+            model.fuse2.upcat.upf.conv.weight.add_(0.01)
+            D.cached = spy
+            cur = torch.cuda.current_stream(gpu).stream_id
+            a = G._guided_forward(model, *ins)
+            D.cached = orig
+            assert len(built) == 3 and all(s == cur for _, _, s in built), built
+            G.GUIDED_STREAMS = 1
+            b = G._guided_forward(model, *ins)
     finally:
-        Dm.TRAIN_SLICES = keep
-    assert torch.equal(la, lb)
-    for a, b in zip(ea, eb):
-        assert torch.equal(a, b)
-    assert set(ga) == set(gb) and ga
-    for k in ga:
-        assert torch.equal(ga[k], gb[k]), k
+        D.cached = orig
+        G.GUIDED_STREAMS = keep
+    for i in range(4):
+        assert torch.equal(a[i], b[i]), i

@@ -192,27 +192,6 @@ def test_wgrad_reduce_sum_empty(nconv_amd, gpu):
     assert o.item() == 0.0
 
 
-@pytest.mark.parametrize("B,H,W", [(2, 64, 96), (8, 352, 1216)])
-def test_dnet_eval_stream_prologue_bitwise(nconv_amd, gpu, B, H, W):
-    """The inference split with a weight prologue per stream (no cross-stream wait at the fork)
-    equals the shared prologue bitwise, and picks up weights changed in place."""
-    net = make_net(nconv_amd, "generalized", gpu)
-    d = net.d_net
-    g = torch.Generator().manual_seed(B + H)
-    S = sparse_depth(g, B, H, W).to(gpu)
-    with torch.no_grad():
-        d.stream_prologue = False
-        a = net(S)
-        d.stream_prologue = True
-        b = net(S)
-        assert torch.equal(a, b)
-        d.nconv4.weight.mul_(1.25)
-        c = net(S)
-        d.stream_prologue = False
-        e = net(S)
-    assert torch.equal(c, e) and not torch.equal(b, c)
-
-
 @pytest.mark.parametrize("B,H,W,crop", [(2, 64, 96, "generalized"), (3, 48, 200, "literal"),
                                         (8, 352, 1216, "generalized")])
 def test_dnet_train_forward_streams_bitwise(nconv_amd, gpu, B, H, W, crop):
