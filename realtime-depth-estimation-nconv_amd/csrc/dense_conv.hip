@@ -687,6 +687,22 @@ __global__ __launch_bounds__(kDT) void dense_wgrad_reduce(const float* __restric
     if (ph == 0 && e < mn) gw[e] = ((red[0][col] + red[1][col]) + red[2][col]) + red[3][col];
 }
 
+// dense_wgrad_reduce over fp64 partials (dense_wgrad_tr_rows), summed in fp64, rounded once.
+__global__ __launch_bounds__(kDT) void dense_wgrad_reduce_d(const double* __restrict__ part, int nsl, int mn,
+                                                            float* __restrict__ gw) {
+    __shared__ double red[4][64];
+    const int col = threadIdx.x & 63, ph = threadIdx.x >> 6;
+    const int e = blockIdx.x * 64 + col;
+    double s = 0.0;
+    if (e < mn) {
+#pragma unroll 8
+        for (int k = ph; k < nsl; k += 4) s += part[(size_t)k * mn + e];
+    }
+    red[ph][col] = s;
+    __syncthreads();
+    if (ph == 0 && e < mn) gw[e] = (float)(((red[0][col] + red[1][col]) + red[2][col]) + red[3][col]);
+}
+
 // ---- the transposed convolution's weight-gradient rows of the few channels concatenated beside
 //      whole 32-channel groups (UpCat's depth channel and 32 / 64 features, step2.py:173) ----
 // On the matrix cores those rows would take a whole 32-row m-tile each (M = 33 / 65 padded to 64 /
@@ -705,9 +721,9 @@ constexpr int kTrXH = kTrRows / 2 + 2, kTrXW = kTrCols / 2 + 2;  // x1 window
 constexpr int kTrMaxC1 = 2, kTrMaxG = 6;                          // channels; Cout <= 16 * kTrMaxG
 __global__ __launch_bounds__(256) void dense_wgrad_tr_rows(const float* __restrict__ x1, int C1, int H, int W,
                                                            const float* __restrict__ gy, int Cout, int Ho, int Wo,
-                                                           int nry, int nrx, float* __restrict__ part) {
+                                                           int nry, int nrx, double* __restrict__ part) {
     __shared__ float sx[kTrMaxC1 * kTrXH * kTrXW];
-    __shared__ float red[4][kTrMaxC1 * 16];
+    __shared__ double red[4][kTrMaxC1 * 16];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     int blk = blockIdx.x;
     const int co = blk % Cout;
@@ -733,12 +749,16 @@ __global__ __launch_bounds__(256) void dense_wgrad_tr_rows(const float* __restri
     const int kwa = (ox + 1) & 1;                  // kw in {kwa, kwa + 2}
     const int xca = (ox + 1 - kwa) / 2 - ix0;      // x1 column of kw = kwa; kw = kwa + 2: xca - 1
     // acc[j][kh][i]: kernel column kw = kwa + 2 i (the thread's column parity; kh is the row's,
-    // known per unrolled row since the block's first row is even)
-    float acc[kTrMaxC1][4][2];
+    // known per unrolled row since the block's first row is even). Exact products summed in fp64,
+    // the partials kept in fp64 down to the final reduction: dL/dy of the BatchNorm after this
+    // convolution has zero mean per channel while the depth channel has a large mean (0..80 m), so
+    // the sum is a small difference of large terms -- in fp32 its rounding reached 1.4e-3 of the
+    // largest gradient (golden f9, fuse1.upcat.upf.conv.weight; the reference's own: 5e-6)
+    double acc[kTrMaxC1][4][2];
 #pragma unroll
     for (int j = 0; j < kTrMaxC1; ++j)
 #pragma unroll
-        for (int t = 0; t < 4; ++t) acc[j][t][0] = acc[j][t][1] = 0.f;
+        for (int t = 0; t < 4; ++t) acc[j][t][0] = acc[j][t][1] = 0.0;
 #pragma unroll
     for (int r = 0; r < kTrRows; ++r) {
         const int kha = (r + 1) & 1;                    // oy0 even: kh in {kha, kha + 2}
@@ -749,10 +769,11 @@ __global__ __launch_bounds__(256) void dense_wgrad_tr_rows(const float* __restri
             const float* xs = sx + j * kTrXH * kTrXW;
             const float x00 = xs[xra * kTrXW + xca], x01 = xs[xra * kTrXW + xca - 1];
             const float x10 = xs[(xra - 1) * kTrXW + xca], x11 = xs[(xra - 1) * kTrXW + xca - 1];
-            acc[j][kha][0] = fmaf(gv[r], x00, acc[j][kha][0]);
-            acc[j][kha][1] = fmaf(gv[r], x01, acc[j][kha][1]);
-            acc[j][kha + 2][0] = fmaf(gv[r], x10, acc[j][kha + 2][0]);
-            acc[j][kha + 2][1] = fmaf(gv[r], x11, acc[j][kha + 2][1]);
+            const double g = (double)gv[r];
+            acc[j][kha][0] = __builtin_fma(g, (double)x00, acc[j][kha][0]);
+            acc[j][kha][1] = __builtin_fma(g, (double)x01, acc[j][kha][1]);
+            acc[j][kha + 2][0] = __builtin_fma(g, (double)x10, acc[j][kha + 2][0]);
+            acc[j][kha + 2][1] = __builtin_fma(g, (double)x11, acc[j][kha + 2][1]);
         }
     }
     // the workgroup's 16 (x C1) tap sums: wave butterflies, then the four waves in order
@@ -762,7 +783,7 @@ __global__ __launch_bounds__(256) void dense_wgrad_tr_rows(const float* __restri
 #pragma unroll
         for (int t = 0; t < 16; ++t) {
             const int kh = t >> 2, kw = t & 3;
-            float v = (kw & 1) == kwa ? acc[j][kh][kw >> 1] : 0.f;
+            double v = (kw & 1) == kwa ? acc[j][kh][kw >> 1] : 0.0;
 #pragma unroll
             for (int m = 32; m > 0; m >>= 1) v += __shfl_xor(v, m);
             if (lane == 0) red[wv][j * 16 + t] = v;
@@ -969,7 +990,7 @@ size_t dense_wgrad_workspace_bytes(const nconv_dense_wgrad& g) {
     if (!tr_rows_split(g)) return main_wgrad_bytes(g);
     const size_t a = (main_wgrad_bytes(tr_rows_main(g)) + 255) & ~(size_t)255;
     const int cs = tr_rows_split(g) == 1 ? g.C1 : g.C0;
-    return a + (size_t)tr_rows_grid(g).nslice * cs * g.Cout * 16 * sizeof(float);
+    return a + (size_t)tr_rows_grid(g).nslice * cs * g.Cout * 16 * sizeof(double);
 }
 
 template <int KIND, int S, int NT>
@@ -997,13 +1018,13 @@ int launch_dense_wgrad(const nconv_dense_wgrad& g, float* ws, size_t ws_bytes, h
     const nconv_dense_wgrad m = tr_rows_main(g);  // the large source's rows
     if (int rc = launch_dense_wgrad_main(m, ws, st, why)) return rc;
     const TrRowsGrid r = tr_rows_grid(g);
-    float* part = ws + ((main_wgrad_bytes(m) + 255) & ~(size_t)255) / sizeof(float);
+    double* part = reinterpret_cast<double*>(ws + ((main_wgrad_bytes(m) + 255) & ~(size_t)255) / sizeof(float));
     const float* xs = sp == 1 ? g.x1 : g.x0;
     const int cs = sp == 1 ? g.C1 : g.C0;
     hipLaunchKernelGGL(dense_wgrad_tr_rows, dim3(r.nslice * g.Cout), dim3(256), 0, st, xs, cs, g.H, g.W, g.gy, g.Cout,
                        g.Ho, g.Wo, r.nry, r.nrx, part);
     const int mn = cs * g.Cout * 16;
-    hipLaunchKernelGGL(dense_wgrad_reduce, dim3((mn + 63) / 64), dim3(kDT), 0, st, part, r.nslice, mn,
+    hipLaunchKernelGGL(dense_wgrad_reduce_d, dim3((mn + 63) / 64), dim3(kDT), 0, st, part, r.nslice, mn,
                        sp == 1 ? g.gw + (size_t)g.C0 * g.Cout * 16 : g.gw);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {

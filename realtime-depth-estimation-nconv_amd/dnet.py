@@ -26,8 +26,8 @@ import torch.nn as nn
 
 from . import _lib, dense, export, nconv
 from .nconv import (EnforcePos, NConv2d, WgradReduce, _require_device, head_weights, layer_backward,
-                    layer_forward_head, layer_forward_pooled, layer_forward_raw, nconv_layer, phase_weights,
-                    train_prologue, weight_prep)
+                    layer_forward_head, layer_forward_head_xc, layer_forward_pooled, layer_forward_raw, nconv_layer,
+                    phase_weights, tail_weights, train_prologue, weight_prep)
 
 LAYERS = ("nconv1", "nconv2", "nconv_down1", "nconv_down2", "nconv_down3", "nconv4", "nconv5",
           "nconv6", "nconv7")
@@ -491,10 +491,11 @@ class DNET(nn.Module):
         return True
 
     def _eval_prologue(self, layers, S):
-        """(wsums, phase weights or None, head weights or None) from one nconv_weight_prologue
-        launch, or None where the separate path must run: merged_prologue off, a layer in training
-        mode (EnforcePos then rewrites the weights first), a forward pre-hook other than this
-        package's EnforcePos, or weights that are not contiguous fp32 device tensors."""
+        """(wsums, phase weights or None, head weights or None, tail weights or None) from one
+        nconv_weight_prologue launch, or None where the separate path must run: merged_prologue off,
+        a layer in training mode (EnforcePos then rewrites the weights first), a forward pre-hook
+        other than this package's EnforcePos, or weights that are not contiguous fp32 device
+        tensors."""
         if not self._eval_prologue_ok(layers):
             return None
         dev = S.device
@@ -516,8 +517,23 @@ class DNET(nn.Module):
                 and m.weight.is_contiguous() for m in ls):
             wph = torch.empty((3, 1024), device=dev, dtype=torch.float32)
             phase = ([m.weight.data for m in ls], [8, 8, 0], list(wph))
-        nconv.weight_prologue(weights, wsums, head=head, phase=phase)
-        return wsums, wph, (head[2] if head is not None else None)
+        tail = None
+        if head is not None and phase is not None and self._use_tail_comp(layers, S):
+            tail = (self.nconv6.weight.data, torch.empty(nconv.TAIL_WEIGHTS_FLOATS, device=dev, dtype=torch.float32))
+        nconv.weight_prologue(weights, wsums, head=head, phase=phase, tail=tail)
+        return wsums, wph, (head[2] if head is not None else None), (tail[1] if tail is not None else None)
+
+    # Exact-fp32 inference evaluates nconv6's skip-half confidence mass composed back to nconv1's
+    # thresholded input on the bf16 matrix cores (nconv_fwd_tail_comp), the head writing nconv2's y *
+    # cout for it (nconv_fwd_head_xc); False: the phase tail over nconv2's y and cout.
+    compose_tail = True
+
+    def _use_tail_comp(self, layers, S):
+        l1, l2, l6 = layers[0], layers[1], layers[7]
+        return (self.compose_tail and self.phase_upcat and nconv.FORWARD_MATH == _lib.MATH_FP32 and
+                self._use_head(l1, l2) and S.shape[2] % 2 == 0 and S.shape[3] % 2 == 0 and
+                (l6.in_channels, l6.out_channels, tuple(l6.kernel_size), tuple(l6.padding), tuple(l6.stride),
+                 tuple(l6.dilation), l6.groups) == (16, 8, (3, 3), (0, 0), (1, 1), (1, 1), 1))
 
     # -- forward ----------------------------------------------------------------------------------
     def forward(self, S):
@@ -535,10 +551,10 @@ class DNET(nn.Module):
             out = torch.empty((S.shape[0], 1, out_h, out_w), device=S.device, dtype=torch.float32)
             pro = self._eval_prologue(layers, S)
             if pro is None:
-                wsum, wph, w21 = self._prologue(layers, S), self._phase_weights(S.device), None
+                wsum, wph, w21, wt = self._prologue(layers, S), self._phase_weights(S.device), None, None
             else:
-                wsum, wph, w21 = pro
-            self._infer_split(S, layers, wsum, out, wph, w21)
+                wsum, wph, w21, wt = pro
+            self._infer_split(S, layers, wsum, out, wph, w21, wt)
             return out
 
         (l1, l2, d1, d2, d3, l4, l5, l6, l7) = layers
@@ -651,7 +667,7 @@ class DNET(nn.Module):
             cache[key] = [torch.cuda.Stream(device=device) for _ in range(n)]
         return cache[key]
 
-    def _infer_split(self, S, layers, wsum, out, wph=None, w21=None):
+    def _infer_split(self, S, layers, wsum, out, wph=None, w21=None, wt=None):
         """The inference chain on batch slices, one stream each (the weight prologue once, on the
         current stream, before the fork: a prologue per stream measured slower, 16.3-16.5 k against
         16.9-17.2 k frames/s, profiles/r5_ab_stream_prologue.log)."""
@@ -659,7 +675,7 @@ class DNET(nn.Module):
         n = self._n_streams(B)
         bounds = self.split_bounds(B, n, self.inference_shares, self._configured_streams())
         if n == 1:
-            self._infer(S, layers, wsum, out, wph, w21=w21)
+            self._infer(S, layers, wsum, out, wph, w21=w21, wt=wt)
             return
         cur = torch.cuda.current_stream(S.device)
         side = self._side_streams(S.device, n - 1)
@@ -670,25 +686,35 @@ class DNET(nn.Module):
                 continue
             with torch.cuda.stream(st):
                 Sk = S[bounds[k]:bounds[k + 1]]
-                self._infer(Sk, layers, wsum, out[bounds[k]:bounds[k + 1]], wph, w21=w21)
+                self._infer(Sk, layers, wsum, out[bounds[k]:bounds[k + 1]], wph, w21=w21, wt=wt)
         for st in side:
             cur.wait_stream(st)
 
-    def _infer(self, S, layers, wsum, out, wph=None, w21=None):
+    def _infer(self, S, layers, wsum, out, wph=None, w21=None, wt=None):
         """The inference chain on the current stream: each producer also writes the pooled input
         of the next down layer, and nconv6+nconv7+crop run as one launch writing `out`. wph: the
         phase weights of nconv4/5/6 (_phase_weights) or None. w21: the exact head's weights when
-        the prologue already built them (_eval_prologue), else built here."""
+        the prologue already built them (_eval_prologue), else built here. wt: the composed tail's
+        weights (_eval_prologue), else built here when the composed tail applies."""
         (l1, l2, d1, d2, d3, l4, l5, l6, l7) = layers
         (s1, s2, sd1, sd2, sd3, s4, s5, s6, s7) = wsum
         w4, w5, w6 = (None, None, None) if wph is None else tuple(wph)
         f, fp = layer_forward_raw, layer_forward_pooled
+        comp = wph is not None and self._use_tail_comp(layers, S)
         if self._use_head(l1, l2):
             # nconv1 inside nconv2's staging: its 8-channel output never reaches HBM
             sp1, sp2 = l1.spec(_lib.THRESH, 0.01), l2.spec()
             if w21 is None and nconv.FORWARD_MATH == _lib.MATH_FP32:  # the exact head's composed weights
                 w21 = head_weights(sp1, sp2, S, l1.weight, l1.bias, s1, l2.weight, l2.bias, s2)
-            x1, c1, p1, q1 = layer_forward_head(sp1, sp2, S, l1.weight, l1.bias, s1, l2.weight, l2.bias, s2, w21)
+            if comp:  # nconv2's y * cout (what the composed tail stages) in place of y
+                if wt is None:
+                    wt = tail_weights(sp1, sp2, l6.spec(_lib.UPCAT_UP_FIRST), S, l1.weight, s1, l2.weight, s2,
+                                      l6.weight)
+                x1, c1, p1, q1 = layer_forward_head_xc(sp1, sp2, S, l1.weight, l1.bias, s1, l2.weight, l2.bias, s2,
+                                                       w21)
+            else:
+                x1, c1, p1, q1 = layer_forward_head(sp1, sp2, S, l1.weight, l1.bias, s1, l2.weight, l2.bias, s2,
+                                                    w21)
         else:
             x1, c1 = f(l1.spec(_lib.THRESH, 0.01), S, None, None, None, l1.weight, l1.bias, s1)
             x1, c1, p1, q1 = fp(l2.spec(), x1, c1, None, None, l2.weight, l2.bias, s2)
@@ -699,7 +725,8 @@ class DNET(nn.Module):
         if self.capture is not None:
             self.capture.update(down1=(x1, c1), down2=(x2, c2), down3=(x3, c3))
         x23, c23 = f(l5.spec(_lib.UPCAT_SKIP_FIRST), x2, c2, x34, c34, l5.weight, l5.bias, s5, wphase=w5)
-        self._fused_tail(l6, l7, s6, s7, x1, c1, x23, c23, out, w6)
+        self._fused_tail(l6, l7, s6, s7, x1, c1, x23, c23, out, w6,
+                         comp=(S, l1.spec(_lib.THRESH, 0.01).thresh, wt) if comp and self._use_head(l1, l2) else None)
 
     # Inference evaluates nconv1 inside nconv2's kernel (nconv_fwd_head) when the layers have
     # DNET's geometry -- in exact fp32 with nconv1 on the nonzero taps only and nconv2's confidence
@@ -718,13 +745,25 @@ class DNET(nn.Module):
             (8, 8, (5, 5), (2, 2), (1, 1)) and tuple(l1.dilation) == (1, 1) and tuple(l2.dilation) == (1, 1) \
             and l1.groups == 1 and l2.groups == 1
 
-    def _fused_tail(self, l6, l7, s6, s7, x1, c1, x23, c23, out, w6=None):
+    def _fused_tail(self, l6, l7, s6, s7, x1, c1, x23, c23, out, w6=None, comp=None):
+        """nconv6 + nconv7 + crop into `out`; comp = (S, thresh, tail weights): the composed tail
+        (nconv_fwd_tail_comp; x1 then holds nconv2's y * cout, nconv_fwd_head_xc)."""
         out_h, out_w = out.shape[2], out.shape[3]
         if out_h == 0 or out_w == 0 or out.shape[0] == 0:
             return out
         L = l6.spec(_lib.UPCAT_UP_FIRST).descriptor(x1, c1, x23, c23, l6.weight, l6.bias, s6, w6)
         if tuple(l7.kernel_size) != (1, 1) or l7.padding[0] != l7.padding[1] or tuple(l7.stride) != (1, 1):
             raise RuntimeError("fused tail needs nconv7 = 1x1, stride 1, square padding")
+        if comp is not None:
+            S, thresh, wt = comp
+            tc = _lib.NconvTailComp()
+            tc.s_in, tc.thresh, tc.weights, tc.a_product = S.data_ptr(), thresh, wt.data_ptr(), 1
+            rc = _lib.lib().nconv_fwd_tail_comp(
+                _lib.ctypes.byref(L), _lib.ptr(l7.weight), _lib.ptr(l7.bias), _lib.ptr(s7), l7.in_channels,
+                l7.padding[0], l7.eps, _lib.ptr(out), None, out_h, out_w, 1, _lib.ctypes.byref(tc),
+                _lib.stream_handle(x1.device))
+            _lib.check(rc, "nconv_fwd_tail_comp")
+            return out
         rc = _lib.lib().nconv_fwd_tail(
             _lib.ctypes.byref(L), _lib.ptr(l7.weight), _lib.ptr(l7.bias), _lib.ptr(s7), l7.in_channels,
             l7.padding[0], l7.eps, _lib.ptr(out), None, out_h, out_w, 1, None, None, _lib.stream_handle(x1.device))
