@@ -256,8 +256,8 @@ int nconv_tail_weights(const nconv_layer* L1, const nconv_layer* L2, const nconv
  * sum W6 * c2 on the vector ALU as nconv_fwd_tail does. L6 as nconv_fwd_tail's, restricted to DNET's
  * nconv6 (16 -> 8 = 8 upsampled + 8 skip channels, upsampled first, 3x3, padding 0, stride 1,
  * exactly-2x upsampling, exact fp32, phase weights in L6->waux; -EOPNOTSUPP otherwise), whose skip
- * source L6->a is nconv2's output on the grid of comp->s_in (B, 1, L6->H, L6->W); no y6 / cout6
- * (inference). */
+ * source L6->a is nconv2's output on the grid of comp->s_in (B, 1, L6->H, L6->W). y6 / cout6 as
+ * nconv_fwd_tail's (training: nconv6's outputs for the backward, with a_product = 0). */
 typedef struct nconv_tail_comp {
     const float* s_in;      /* DNET's sparse input S: nconv1's c0 = (S > thresh)                       */
     float thresh;           /* nconv1's threshold (0.01, step1.py:53)                                 */
@@ -265,8 +265,8 @@ typedef struct nconv_tail_comp {
     int a_product;          /* 1: L6->a.x holds nconv2's y * cout (nconv_fwd_head_xc); 0: y           */
 } nconv_tail_comp;
 int nconv_fwd_tail_comp(const nconv_layer* L6, const float* w7, const float* b7, const float* wsum7, int cin7,
-                        int p7, float eps7, float* out, float* out_c, int out_h, int out_w, int crop0,
-                        const nconv_tail_comp* comp, void* stream);
+                        int p7, float eps7, float* out, float* out_c, int out_h, int out_w, int crop0, float* y6,
+                        float* cout6, const nconv_tail_comp* comp, void* stream);
 
 /* Which kernels nconv_fwd (without fused pooling) and nconv_bwd run for L (enum nconv_kernel):
  * the arithmetic a descriptor selects, made observable to hosts and tests. Host-only (no device

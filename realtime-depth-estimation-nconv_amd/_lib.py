@@ -167,7 +167,7 @@ def _declare(lib):
                                        ctypes.POINTER(NconvLayer), P, P]
     lib.nconv_fwd_tail_comp.restype = ctypes.c_int
     lib.nconv_fwd_tail_comp.argtypes = [ctypes.POINTER(NconvLayer), P, P, P, ctypes.c_int, ctypes.c_int,
-                                        ctypes.c_float, P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                        ctypes.c_float, P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P,
                                         ctypes.POINTER(NconvTailComp), P]
     lib.nconv_bwd_workspace_bytes.restype = ctypes.c_size_t
     lib.nconv_bwd_workspace_bytes.argtypes = [ctypes.POINTER(NconvLayer)]

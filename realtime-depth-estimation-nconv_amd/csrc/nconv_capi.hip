@@ -243,8 +243,8 @@ int nconv_tail_weights(const nconv_layer* L1, const nconv_layer* L2, const nconv
 }
 
 int nconv_fwd_tail_comp(const nconv_layer* L6, const float* w7, const float* b7, const float* wsum7, int cin7,
-                        int p7, float eps7, float* out, float* out_c, int out_h, int out_w, int crop0,
-                        const nconv_tail_comp* comp, void* stream) {
+                        int p7, float eps7, float* out, float* out_c, int out_h, int out_w, int crop0, float* y6,
+                        float* cout6, const nconv_tail_comp* comp, void* stream) {
     const char* fn = "nconv_fwd_tail_comp";
     if (const char* why = validate(L6, true)) return fail(-22, fn, why);
     if (!w7 || !b7 || !wsum7 || !out || !comp || !comp->s_in || !comp->weights)
@@ -256,8 +256,13 @@ int nconv_fwd_tail_comp(const nconv_layer* L6, const float* w7, const float* b7,
     if (!nconv::fwd_tail_comp_supported(*L6))
         return fail(-95, fn, "the composed tail is built for DNET's nconv6 (16 -> 8 = up + skip, 3x3, padding 0, "
                               "exactly-2x upsampling, exact fp32, phase weights in waux)");
+    if ((y6 == nullptr) != (cout6 == nullptr)) return fail(-22, fn, "y6 and cout6: both or neither");
+    if (y6 && (crop0 > p7 || crop0 + out_h - p7 < L6->Ho || crop0 + out_w - p7 < L6->Wo))
+        return fail(-22, fn, "y6 / cout6 need an output window covering every nconv6 pixel");
     if (out_h == 0 || out_w == 0 || L6->B == 0) return 0;
     nconv::TailArgs t{w7, b7, wsum7, eps7, crop0 - p7, out_h, out_w, out_c};
+    t.y6 = y6;
+    t.c6 = cout6;
     const char* why = nullptr;
     int rc = nconv::launch_fwd_tail_comp(make_dev(L6), t, out, comp->s_in, comp->thresh, comp->weights,
                                          comp->a_product != 0, (hipStream_t)stream, &why);

@@ -51,10 +51,11 @@ def _tail_exact_up(sp, S):
     return S.shape[2] % 2 == 0 and S.shape[3] % 2 == 0
 
 
-def _train_fwd_chain(sp, W, S, w21, wph, crop, out, pooled=True):
+def _train_fwd_chain(sp, W, S, w21, wph, crop, out, pooled=True, wt=None):
     """DNETFn's forward launches over S's frames; out: None (fresh tensors) or a callable handing
     out each launch's output tensors (nconv._outputs). Returns x1, c1, ..., x9, c9, then the pooled
-    copies and argmax codes (pooled graph)."""
+    copies and argmax codes (pooled graph). wt: the composed tail's weights (the training tail then
+    composes nconv6's skip-half confidence mass, nconv_fwd_tail_comp), or None."""
     w4, w5, w6 = (None, None, None) if wph is None else tuple(wph)
     if pooled:
         spp = [dataclasses.replace(sp[k], mode=_lib.PLAIN) for k in (2, 3, 4)]
@@ -80,7 +81,8 @@ def _train_fwd_chain(sp, W, S, w21, wph, crop, out, pooled=True):
     x6, c6 = layer_forward_raw(sp[5], x4, c4, x5, c5, *W[5], out=out, wphase=w4)
     x7, c7 = layer_forward_raw(sp[6], x3, c3, x6, c6, *W[6], out=out, wphase=w5)
     if pooled and FUSE_TAIL_FWD and w6 is not None and x2.shape[2:] == tuple(2 * v for v in x7.shape[2:]):
-        x8, c8, x9, c9 = _tail_train(sp[7], sp[8], x2, c2, x7, c7, W[7], W[8], w6, crop, out=out)
+        x8, c8, x9, c9 = _tail_train(sp[7], sp[8], x2, c2, x7, c7, W[7], W[8], w6, crop, out=out,
+                                     comp=None if wt is None else (S, sp[0].thresh, wt))
     elif crop is not None:
         raise RuntimeError("DNETFn: a cropped output needs the fused training tail")
     else:
@@ -120,6 +122,7 @@ class DNETFn(torch.autograd.Function):
         wph = p[27] if len(p) > 27 and p[27] is not None else None
         w21 = p[28] if len(p) > 28 else None
         ctx.wbox = p[29] if len(p) > 29 else None
+        wt = p[30] if len(p) > 30 else None  # the composed tail's weights (DNET._train_tail_weights)
         w6 = None if wph is None else wph[2]
         sp = specs
         pooled = _materialise_pool(S)
@@ -153,7 +156,7 @@ class DNETFn(torch.autograd.Function):
                         out.append(full[i][b0:b1])
                     return out
                 with torch.cuda.stream(st):
-                    r = _train_fwd_chain(sp, W, S[b0:b1], w21, wph, crop, rows)
+                    r = _train_fwd_chain(sp, W, S[b0:b1], w21, wph, crop, rows, wt=wt)
                 res = r if res is None else res
             for st in side:
                 cur.wait_stream(st)
@@ -162,7 +165,7 @@ class DNETFn(torch.autograd.Function):
                 base[t.data_ptr()] for t in res]
         else:
             (x1, c1, x2, c2, x3, c3, x4, c4, x5, c5, x6, c6, x7, c7, x8, c8, x9, c9, *pools) = \
-                _train_fwd_chain(sp, W, S, w21, wph, crop, None, pooled=pooled)
+                _train_fwd_chain(sp, W, S, w21, wph, crop, None, pooled=pooled, wt=wt if pooled else None)
         if capture is not None:  # the three pooling stages' inputs (DNET.capture)
             capture.update(down1=(x2.detach(), c2.detach()), down2=(x3.detach(), c3.detach()),
                            down3=(x4.detach(), c4.detach()))
@@ -295,17 +298,27 @@ FUSE_HEAD_FWD = True  # the training forward's nconv1 + nconv2 as the exact fuse
 FUSE_TAIL_FWD = True  # ... and nconv6 + nconv7 as the fused tail (nconv_fwd_tail over nconv7's whole grid)
 
 
-def _tail_train(sp6, sp7, x2, c2, x7, c7, W6, W7, w6, crop=None, out=None):
+def _tail_train(sp6, sp7, x2, c2, x7, c7, W6, W7, w6, crop=None, out=None, comp=None):
     """nconv6 + nconv7 in one phase-tail launch writing nconv6's outputs and nconv7's whole
     (uncropped) output grid -- what the training backward reads (nconv_fwd_tail, crop0 = 0) -- or,
     with crop = (h, w), nconv7's output cropped as step1.py:94 (crop0 = 1). out: None or a callable
-    as nconv._outputs takes."""
+    as nconv._outputs takes. comp = (S, thresh, tail weights): the composed tail
+    (nconv_fwd_tail_comp over nconv2's y and cout, a_product = 0)."""
     L = sp6.descriptor(x2, c2, x7, c7, *W6, w6)
     (w7, b7, s7), p7 = W7, sp7.padding[0]
     B, dev = x2.shape[0], x2.device
     (H9, W9), crop0 = ((L.Ho + 2 * p7, L.Wo + 2 * p7), 0) if crop is None else (tuple(crop), 1)
     sh8, sh9 = (B, sp6.cout, L.Ho, L.Wo), (B, 1, H9, W9)
     x8, c8, x9, c9 = nconv._outputs(out, 4, (sh8, sh8, sh9, sh9), dev)
+    if comp is not None:
+        S, thresh, wt = comp
+        tc = _lib.NconvTailComp()
+        tc.s_in, tc.thresh, tc.weights, tc.a_product = S.data_ptr(), thresh, wt.data_ptr(), 0
+        rc = _lib.lib().nconv_fwd_tail_comp(_lib.ctypes.byref(L), _lib.ptr(w7), _lib.ptr(b7), _lib.ptr(s7), sp7.cin,
+                                            p7, sp7.eps, _lib.ptr(x9), _lib.ptr(c9), H9, W9, crop0, _lib.ptr(x8),
+                                            _lib.ptr(c8), _lib.ctypes.byref(tc), _lib.stream_handle(dev))
+        _lib.check(rc, "nconv_fwd_tail_comp")
+        return x8, c8, x9, c9
     rc = _lib.lib().nconv_fwd_tail(_lib.ctypes.byref(L), _lib.ptr(w7), _lib.ptr(b7), _lib.ptr(s7), sp7.cin, p7,
                                    sp7.eps, _lib.ptr(x9), _lib.ptr(c9), H9, W9, crop0, _lib.ptr(x8), _lib.ptr(c8),
                                    _lib.stream_handle(dev))
@@ -528,10 +541,22 @@ class DNET(nn.Module):
     # cout for it (nconv_fwd_head_xc); False: the phase tail over nconv2's y and cout.
     compose_tail = True
 
-    def _use_tail_comp(self, layers, S):
+    def _train_tail_weights(self, layers, S, specs, wsum, wph):
+        """The composed training tail's weights (nconv_tail_weights of the current, transformed
+        weights and normalisers), or None where the training pass keeps the phase tail."""
+        if wph is None or not (FUSE_TAIL_FWD and _materialise_pool(S) and self._use_tail_comp(layers, S, head=False)):
+            return None
+        return tail_weights(specs[0], specs[1], specs[7], S, layers[0].weight, wsum[0], layers[1].weight, wsum[1],
+                            layers[7].weight)
+
+    def _use_tail_comp(self, layers, S, head=True):
+        """Whether the composed tail applies: exact fp32, phase form, DNET's nconv1 / nconv2 / nconv6
+        geometry, even H and W (exactly-2x UpCat); inference also needs the fused head (whose
+        product planes it reads)."""
         l1, l2, l6 = layers[0], layers[1], layers[7]
         return (self.compose_tail and self.phase_upcat and nconv.FORWARD_MATH == _lib.MATH_FP32 and
-                self._use_head(l1, l2) and S.shape[2] % 2 == 0 and S.shape[3] % 2 == 0 and
+                (self._use_head(l1, l2) if head else self._head_shapes(l1, l2)) and
+                S.shape[2] % 2 == 0 and S.shape[3] % 2 == 0 and
                 (l6.in_channels, l6.out_channels, tuple(l6.kernel_size), tuple(l6.padding), tuple(l6.stride),
                  tuple(l6.dilation), l6.groups) == (16, 8, (3, 3), (0, 0), (1, 1), (1, 1), 1))
 
@@ -565,10 +590,11 @@ class DNET(nn.Module):
             pro = self._train_prologue(layers, S)
             if pro is None:
                 wsum = self._prologue(layers, S)
-                extra = (self._phase_weights(S.device),)
+                wph = self._phase_weights(S.device)
+                extra = (wph, None, None, self._train_tail_weights(layers, S, specs, wsum, wph))
             else:
                 wsum, wph, w21, wbox = pro
-                extra = (wph, w21, wbox)
+                extra = (wph, w21, wbox, self._train_tail_weights(layers, S, specs, wsum, wph))
             params = []
             for m_, s_ in zip(layers, wsum):
                 params += [m_.weight, m_.bias, s_]
@@ -760,7 +786,7 @@ class DNET(nn.Module):
             tc.s_in, tc.thresh, tc.weights, tc.a_product = S.data_ptr(), thresh, wt.data_ptr(), 1
             rc = _lib.lib().nconv_fwd_tail_comp(
                 _lib.ctypes.byref(L), _lib.ptr(l7.weight), _lib.ptr(l7.bias), _lib.ptr(s7), l7.in_channels,
-                l7.padding[0], l7.eps, _lib.ptr(out), None, out_h, out_w, 1, _lib.ctypes.byref(tc),
+                l7.padding[0], l7.eps, _lib.ptr(out), None, out_h, out_w, 1, None, None, _lib.ctypes.byref(tc),
                 _lib.stream_handle(x1.device))
             _lib.check(rc, "nconv_fwd_tail_comp")
             return out

@@ -83,7 +83,7 @@ int main(void) {
     nconv_layer l6 = L;
     l6.Cin = 16; l6.KH = l6.KW = 3; l6.PH = l6.PW = 1; l6.Ho = 16; l6.Wo = 16;
     l6.load_mode = NCONV_LOAD_UPCAT_UP_FIRST; l6.b = l6.a; l6.b.H = 8; l6.b.W = 8; l6.waux = fake;
-    rc = nconv_fwd_tail_comp(&l6, fake, fake, fake, 8, 2, 1e-7f, out, NULL, 16, 16, 1, &tc, NULL);
+    rc = nconv_fwd_tail_comp(&l6, fake, fake, fake, 8, 2, 1e-7f, out, NULL, 16, 16, 1, NULL, NULL, &tc, NULL);
     printf("\"rc_tail_comp_pad1\": [%d, \"%s\"],\n", rc, nconv_last_error());
     printf("\"abi\": [%d, %d]\n}\n", nconv_abi_version(), NCONV_ABI_VERSION);
     return 0;
