@@ -282,13 +282,6 @@ def inference_calls(m, net, S):
     if head and m.nconv.FORWARD_MATH == lib.MATH_FP32:
         w21 = m.nconv.head_weights(l1.spec(lib.THRESH, 0.01), l2.spec(), S, l1.weight, l1.bias, s1, l2.weight,
                                    l2.bias, s2)
-    # the composed tail (DNET._infer): the head then writes nconv2's y * cout, the tail reads it
-    comp = wph is not None and d._use_tail_comp(layers, S)
-    wt = None
-    if comp:
-        fhead = m.nconv.layer_forward_head_xc
-        wt = m.nconv.tail_weights(l1.spec(lib.THRESH, 0.01), l2.spec(), l6.spec(lib.UPCAT_UP_FIRST), S, l1.weight,
-                                  s1, l2.weight, s2, l6.weight)
     with torch.no_grad():
         if head:
             x1b, c1b, p1, q1 = fhead(l1.spec(lib.THRESH, 0.01), l2.spec(), S, l1.weight, l1.bias, s1, l2.weight,
@@ -313,8 +306,7 @@ def inference_calls(m, net, S):
         "nconv_down3": lambda: fwd(d3.spec(), p3, q3, None, None, d3.weight, d3.bias, sd3),
         "nconv4": lambda: fwd(l4.spec(lib.UPCAT_SKIP_FIRST), x3, c3, x4, c4, l4.weight, l4.bias, s4, wphase=w4),
         "nconv5": lambda: fwd(l5.spec(lib.UPCAT_SKIP_FIRST), x2, c2, x34, c34, l5.weight, l5.bias, s5, wphase=w5),
-        "nconv6+7_tail": lambda: d._fused_tail(l6, l7, s6, s7, x1b, c1b, x23, c23, tail_out, w6,
-                                               comp=(S, 0.01, wt) if comp else None),
+        "nconv6+7_tail": lambda: d._fused_tail(l6, l7, s6, s7, x1b, c1b, x23, c23, tail_out, w6),
     }
 
 

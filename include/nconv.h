@@ -139,12 +139,7 @@ int nconv_phase_weights(int n, const float* const* weights, const int* cins, con
 int nconv_weight_prologue(int n, float* const* weights, const int* couts, const int* fan_ins,
                           float* const* wsums, const float* head_w1, const float* head_w2, float* w21,
                           int nphase, const float* const* phase_weights, const int* phase_cins,
-                          const int* phase_up_first, float* const* wphases, const float* tail_w6, float* tail_w,
-                          void* stream);
-/* (ABI 21: tail_w6 / tail_w) with tail_w != NULL the launch also writes the composed tail's
- * weights into tail_w (nconv_tail_weights of nconv1 head_w1, nconv2 head_w2 and nconv6 tail_w6,
- * NCONV_TAIL_WEIGHTS_FLOATS; the normalisers recomputed in-kernel with nconv_weight_prep's
- * arithmetic), bitwise what nconv_tail_weights writes. */
+                          const int* phase_up_first, float* const* wphases, void* stream);
 
 /* The training pass's weight prologue in one launch (replaces models/step1.py:190-207's EnforcePos
  * pre-hooks of DNET's nine layers, whose forward then needs the normalisers and the auxiliaries
@@ -227,46 +222,6 @@ int nconv_head_weights(const nconv_layer* L1, const nconv_layer* L2, float* w21,
 int nconv_fwd_tail(const nconv_layer* L6, const float* w7, const float* b7, const float* wsum7,
                    int cin7, int p7, float eps7, float* out, float* out_c, int out_h, int out_w, int crop0,
                    float* y6, float* cout6, void* stream);
-
-/* ABI 21. The inference fused head writing nconv2's x * c = y * cout (the product nconv6's staging
- * forms from nconv2's y and cout, models/step1.py:121 on nconv6's skip half) into xc instead of y,
- * for nconv_fwd_tail_comp with a_product = 1; cout and the pooled copies (of y and cout) as
- * nconv_fwd_head. Exact fp32 only. Replaces the same reference lines as nconv_fwd_head. */
-int nconv_fwd_head_xc(const nconv_layer* L1, const nconv_layer* L2, float* xc, float* cout, float* y_pool,
-                      float* cout_pool, void* stream);
-
-/* ABI 21. The composed tail's weights (nconv_fwd_tail_comp's comp->weights): out receives
- * NCONV_TAIL_WEIGHTS_FLOATS floats -- the composed confidence weights W621[o][U][V] = sum_i (1 / s2[i])
- * sum_{a,b} W6[o][8 + i][a][b] W21[i][U - a][V - b] (W21 = nconv2's weights composed with nconv1's,
- * nconv_head_weights' definition; s1 = L1->wsum, s2 = L2->wsum), fp64, rounded once to fp32, split
- * exactly into three bf16 parts as v_mfma_f32_16x16x32_bf16 A fragments (2048 dwords), then nconv6's
- * phase weights re-laid [i][alpha][dh][o][dw][beta] (1024 floats, bitwise nconv_phase_weights'
- * values). L1 = nconv1 (1 -> 8, 5x5), L2 = nconv2 (8 -> 8, 5x5), L6 = nconv6 (16 -> 8, 3x3, its skip
- * channels 8..15). Call after the normalisers are current. */
-#define NCONV_TAIL_WEIGHTS_FLOATS 3072
-int nconv_tail_weights(const nconv_layer* L1, const nconv_layer* L2, const nconv_layer* L6, float* out,
-                       void* stream);
-
-/* ABI 21. Fused tail (as nconv_fwd_tail) with nconv6's skip-half confidence mass composed back to
- * nconv1's thresholded input (models/step1.py:53-58 feeding :88-90): wherever nconv2's window is
- * untruncated, D6s[o] = sum_i W6[o][8+i] * c2[i] = W621[o] * c0 with c0 = (S > thresh), an 11 x 11
- * convolution of the binary mask, which runs on the bf16 matrix cores with exact products (c0 is 0
- * or 1, each composed weight the exact sum of three bf16 parts) and fp32 accumulation; the skip
- * half's data sums take one packed FMA per tap for two pixels; tiles within 5 px of the image edge
- * sum W6 * c2 on the vector ALU as nconv_fwd_tail does. L6 as nconv_fwd_tail's, restricted to DNET's
- * nconv6 (16 -> 8 = 8 upsampled + 8 skip channels, upsampled first, 3x3, padding 0, stride 1,
- * exactly-2x upsampling, exact fp32, phase weights in L6->waux; -EOPNOTSUPP otherwise), whose skip
- * source L6->a is nconv2's output on the grid of comp->s_in (B, 1, L6->H, L6->W). y6 / cout6 as
- * nconv_fwd_tail's (training: nconv6's outputs for the backward, with a_product = 0). */
-typedef struct nconv_tail_comp {
-    const float* s_in;      /* DNET's sparse input S: nconv1's c0 = (S > thresh)                       */
-    float thresh;           /* nconv1's threshold (0.01, step1.py:53)                                 */
-    const float* weights;   /* NCONV_TAIL_WEIGHTS_FLOATS from nconv_tail_weights / the prologue       */
-    int a_product;          /* 1: L6->a.x holds nconv2's y * cout (nconv_fwd_head_xc); 0: y           */
-} nconv_tail_comp;
-int nconv_fwd_tail_comp(const nconv_layer* L6, const float* w7, const float* b7, const float* wsum7, int cin7,
-                        int p7, float eps7, float* out, float* out_c, int out_h, int out_w, int crop0, float* y6,
-                        float* cout6, const nconv_tail_comp* comp, void* stream);
 
 /* Which kernels nconv_fwd (without fused pooling) and nconv_bwd run for L (enum nconv_kernel):
  * the arithmetic a descriptor selects, made observable to hosts and tests. Host-only (no device

@@ -38,9 +38,6 @@ EXPORTED = (
     "nconv_fwd_tail",
     "nconv_fwd_head",
     "nconv_head_weights",
-    "nconv_fwd_head_xc",
-    "nconv_tail_weights",
-    "nconv_fwd_tail_comp",
     "nconv_plan",
     "nconv_phase_weights_floats",
     "nconv_phase_weights",
@@ -100,11 +97,6 @@ class NconvBwdIo(ctypes.Structure):
         ("tail_w", ctypes.c_int)]
 
 
-class NconvTailComp(ctypes.Structure):
-    _fields_ = [("s_in", ctypes.c_void_p), ("thresh", ctypes.c_float), ("weights", ctypes.c_void_p),
-                ("a_product", ctypes.c_int)]
-
-
 class NconvDenseConv(ctypes.Structure):
     _fields_ = [("B", ctypes.c_int), ("x0", ctypes.c_void_p), ("C0", ctypes.c_int),
                 ("x1", ctypes.c_void_p), ("C1", ctypes.c_int), ("H", ctypes.c_int), ("W", ctypes.c_int),
@@ -159,16 +151,7 @@ def _declare(lib):
     lib.nconv_phase_weights.restype = ctypes.c_int
     lib.nconv_phase_weights.argtypes = [ctypes.c_int, P, P, P, P, P]
     lib.nconv_weight_prologue.restype = ctypes.c_int
-    lib.nconv_weight_prologue.argtypes = [ctypes.c_int, P, P, P, P, P, P, P, ctypes.c_int, P, P, P, P, P, P, P]
-    lib.nconv_fwd_head_xc.restype = ctypes.c_int
-    lib.nconv_fwd_head_xc.argtypes = [ctypes.POINTER(NconvLayer), ctypes.POINTER(NconvLayer), P, P, P, P, P]
-    lib.nconv_tail_weights.restype = ctypes.c_int
-    lib.nconv_tail_weights.argtypes = [ctypes.POINTER(NconvLayer), ctypes.POINTER(NconvLayer),
-                                       ctypes.POINTER(NconvLayer), P, P]
-    lib.nconv_fwd_tail_comp.restype = ctypes.c_int
-    lib.nconv_fwd_tail_comp.argtypes = [ctypes.POINTER(NconvLayer), P, P, P, ctypes.c_int, ctypes.c_int,
-                                        ctypes.c_float, P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P,
-                                        ctypes.POINTER(NconvTailComp), P]
+    lib.nconv_weight_prologue.argtypes = [ctypes.c_int, P, P, P, P, P, P, P, ctypes.c_int, P, P, P, P, P]
     lib.nconv_bwd_workspace_bytes.restype = ctypes.c_size_t
     lib.nconv_bwd_workspace_bytes.argtypes = [ctypes.POINTER(NconvLayer)]
     lib.nconv_bwd.restype = ctypes.c_int

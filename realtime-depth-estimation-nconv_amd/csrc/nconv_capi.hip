@@ -191,84 +191,6 @@ int nconv_head_weights(const nconv_layer* L1, const nconv_layer* L2, float* w21,
     return rc ? fail(rc, fn, why) : 0;
 }
 
-int nconv_fwd_head_xc(const nconv_layer* L1, const nconv_layer* L2, float* xc, float* cout, float* y_pool,
-                      float* cout_pool, void* stream) {
-    const char* fn = "nconv_fwd_head_xc";
-    if (!L2 || L2->math != NCONV_MATH_FP32) return fail(-95, fn, "the product head is the exact-fp32 head");
-    // validation as nconv_fwd_head's, then the same launch with the product flag
-    if (const char* why = validate(L1, false)) return fail(-22, fn, why);
-    if (!xc || !cout || !y_pool || !cout_pool) return fail(-22, fn, "null output");
-    if (L1->load_mode != NCONV_LOAD_THRESH || L1->Cin != 1 || L1->Cout != 8 || L1->KH != 5 || L1->KW != 5 ||
-        L1->PH != 2 || L1->PW != 2 || L1->SH != 1 || L1->SW != 1 || L1->DH != 1 || L1->DW != 1 || L1->groups != 1)
-        return fail(-95, fn, "nconv1 must be 1 -> 8, 5x5, padding 2, stride 1, thresholded input");
-    if (L2->B != L1->B || L2->Cin != 8 || L2->Cout != 8 || L2->KH != 5 || L2->KW != 5 || L2->PH != 2 ||
-        L2->PW != 2 || L2->SH != 1 || L2->SW != 1 || L2->DH != 1 || L2->DW != 1 || L2->groups != 1)
-        return fail(-95, fn, "nconv2 must be 8 -> 8, 5x5, padding 2, stride 1");
-    if (L2->H != L1->Ho || L2->W != L1->Wo || L2->Ho != L2->H || L2->Wo != L2->W)
-        return fail(-22, fn, "nconv2 geometry inconsistent with nconv1's output");
-    if (L2->Ho < 2 || L2->Wo < 2) return fail(-22, fn, "output too small to pool");
-    if (!L2->weight || !L2->bias || !L2->wsum) return fail(-22, fn, "null nconv2 weight/bias/wsum");
-    if (!L2->waux) return fail(-22, fn, "exact-fp32 head needs nconv2's waux = nconv_head_weights output");
-    nconv_layer l2 = *L2;
-    l2.load_mode = NCONV_LOAD_PLAIN;
-    l2.a = L1->a;
-    nconv::TailArgs t{};
-    t.py = y_pool;
-    t.pc = cout_pool;
-    t.s_in = L1->a.x;
-    t.w1 = L1->weight;
-    t.b1 = L1->bias;
-    t.s1 = L1->wsum;
-    t.eps1 = L1->eps;
-    t.thresh1 = L1->thresh;
-    t.yprod = 1;
-    const char* why = nullptr;
-    int rc = nconv::launch_fwd_head_exact(make_dev(&l2), t, xc, cout, (hipStream_t)stream, &why);
-    return rc ? fail(rc, fn, why) : 0;
-}
-
-int nconv_tail_weights(const nconv_layer* L1, const nconv_layer* L2, const nconv_layer* L6, float* out,
-                       void* stream) {
-    const char* fn = "nconv_tail_weights";
-    if (!L1 || !L2 || !L6 || !out) return fail(-22, fn, "null argument");
-    if (!L1->weight || !L1->wsum || !L2->weight || !L2->wsum || !L6->weight) return fail(-22, fn, "null weight / wsum");
-    if (L1->Cin != 1 || L1->Cout != 8 || L1->KH != 5 || L1->KW != 5 || L2->Cin != 8 || L2->Cout != 8 ||
-        L2->KH != 5 || L2->KW != 5 || L6->Cin != 16 || L6->Cout != 8 || L6->KH != 3 || L6->KW != 3 ||
-        L1->groups != 1 || L2->groups != 1 || L6->groups != 1)
-        return fail(-95, fn, "nconv1 1 -> 8 5x5, nconv2 8 -> 8 5x5 and nconv6 16 -> 8 3x3 only");
-    const char* why = nullptr;
-    int rc = nconv::launch_tail_weights(L1->weight, L1->wsum, L2->weight, L2->wsum, L6->weight, out,
-                                        (hipStream_t)stream, &why);
-    return rc ? fail(rc, fn, why) : 0;
-}
-
-int nconv_fwd_tail_comp(const nconv_layer* L6, const float* w7, const float* b7, const float* wsum7, int cin7,
-                        int p7, float eps7, float* out, float* out_c, int out_h, int out_w, int crop0, float* y6,
-                        float* cout6, const nconv_tail_comp* comp, void* stream) {
-    const char* fn = "nconv_fwd_tail_comp";
-    if (const char* why = validate(L6, true)) return fail(-22, fn, why);
-    if (!w7 || !b7 || !wsum7 || !out || !comp || !comp->s_in || !comp->weights)
-        return fail(-22, fn, "null tail pointer");
-    if (cin7 != L6->Cout) return fail(-22, fn, "nconv7 Cin must equal nconv6 Cout");
-    if (p7 < 0 || out_h < 0 || out_w < 0 || crop0 < 0) return fail(-22, fn, "bad tail geometry");
-    if (crop0 + out_h > L6->Ho + 2 * p7 || crop0 + out_w > L6->Wo + 2 * p7)
-        return fail(-22, fn, "output crop exceeds nconv7's grid");
-    if (!nconv::fwd_tail_comp_supported(*L6))
-        return fail(-95, fn, "the composed tail is built for DNET's nconv6 (16 -> 8 = up + skip, 3x3, padding 0, "
-                              "exactly-2x upsampling, exact fp32, phase weights in waux)");
-    if ((y6 == nullptr) != (cout6 == nullptr)) return fail(-22, fn, "y6 and cout6: both or neither");
-    if (y6 && (crop0 > p7 || crop0 + out_h - p7 < L6->Ho || crop0 + out_w - p7 < L6->Wo))
-        return fail(-22, fn, "y6 / cout6 need an output window covering every nconv6 pixel");
-    if (out_h == 0 || out_w == 0 || L6->B == 0) return 0;
-    nconv::TailArgs t{w7, b7, wsum7, eps7, crop0 - p7, out_h, out_w, out_c};
-    t.y6 = y6;
-    t.c6 = cout6;
-    const char* why = nullptr;
-    int rc = nconv::launch_fwd_tail_comp(make_dev(L6), t, out, comp->s_in, comp->thresh, comp->weights,
-                                         comp->a_product != 0, (hipStream_t)stream, &why);
-    return rc ? fail(rc, fn, why) : 0;
-}
-
 int nconv_fwd_tail(const nconv_layer* L6, const float* w7, const float* b7, const float* wsum7,
                    int cin7, int p7, float eps7, float* out, float* out_c, int out_h, int out_w, int crop0,
                    float* y6, float* cout6, void* stream) {
@@ -355,8 +277,7 @@ int nconv_train_prologue(int n, float* const* weights, const int* couts, const i
 int nconv_weight_prologue(int n, float* const* weights, const int* couts, const int* fan_ins,
                           float* const* wsums, const float* head_w1, const float* head_w2, float* w21,
                           int nphase, const float* const* phase_weights, const int* phase_cins,
-                          const int* phase_up_first, float* const* wphases, const float* tail_w6, float* tail_w,
-                          void* stream) {
+                          const int* phase_up_first, float* const* wphases, void* stream) {
     const char* fn = "nconv_weight_prologue";
     if (n < 0 || nphase < 0) return fail(-22, fn, "negative count");
     if (n > 0 && (!weights || !couts || !fan_ins || !wsums)) return fail(-22, fn, "null argument");
@@ -370,10 +291,9 @@ int nconv_weight_prologue(int n, float* const* weights, const int* couts, const 
         if (phase_up_first[i] < 0 || phase_up_first[i] + 8 > phase_cins[i])
             return fail(-22, fn, "upsampled channels outside [0, Cin)");
     }
-    if (tail_w && (!head_w1 || !head_w2 || !tail_w6)) return fail(-22, fn, "tail weights need head_w1, head_w2 and tail_w6");
     const char* why = nullptr;
     int rc = nconv::launch_weight_prologue(n, weights, couts, fan_ins, wsums, head_w1, head_w2, w21, nphase,
-                                           phase_weights, phase_cins, phase_up_first, wphases, tail_w6, tail_w,
+                                           phase_weights, phase_cins, phase_up_first, wphases,
                                            (hipStream_t)stream, &why);
     return rc ? fail(rc, fn, why) : 0;
 }

@@ -25,7 +25,7 @@
 //     plain convolution; those tiles sum W2 * c1 from nconv1's c1 as the unfused path does.
 // Interior-tile outputs therefore differ from the unfused exact pair only through D2's rounding;
 // N2, nconv1 and the edge tiles match it bit for bit.
-#include "nconv_tail.h"
+#include "nconv_prologue.h"
 
 namespace nconv {
 
@@ -333,9 +333,7 @@ __global__ __launch_bounds__(kHT) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
         const __amdgpu_buffer_rsrc_t rpy = plane_rsrc(t.py + pofs, ppbytes), rpc = plane_rsrc(t.pc + pofs, ppbytes);
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-            // (inference with the composed tail: y * cout, the product the tail's staging used to
-            // form from y and cout -- the same fp32 multiply, so the same bits)
-            st_f32(ry, so[h], (!TR && t.yprod) ? yv[h] * cv[h] : yv[h]);
+            st_f32(ry, so[h], yv[h]);
             st_f32(rc, so[h], cv[h]);
 #ifdef NCONV_HEAD_PROBE_NO_POOL  // timing probe only (wrong results): no pooled copies
             continue;
@@ -441,44 +439,9 @@ __global__ __launch_bounds__(64) void head_weights(const float* __restrict__ w1,
 // layer. Every block reads the weights only, so no order between the roles is needed.
 __global__ __launch_bounds__(kPrepThreads) void weight_prologue(PrepArgs prep, int nprep, const float* __restrict__ w1,
                                                                  const float* __restrict__ w2, float* __restrict__ w21,
-                                                                 PhaseArgs ph, int nphase, const float* __restrict__ w6,
-                                                                 float* __restrict__ tailw) {
+                                                                 PhaseArgs ph, int nphase) {
     const int nhead = w21 ? (kHeadUnits + 3) / 4 : 0;
-    const int ntail = tailw ? (kTailUnits + 3) / 4 : 0;
     int blk = blockIdx.x;
-    if (blk < ntail) {
-        // the composed tail's weights (nconv_tail.h) first: their units are the longest blocks of
-        // the launch. s1 / s2 recomputed with prep_block's arithmetic (row_sum_wave), so bitwise
-        // the normalisers the forward divides by
-        const int lane = threadIdx.x & 63, unit = 4 * blk + (threadIdx.x >> 6);
-        if (unit >= kTailUnits) return;
-        float v1[8], v2[8][4];
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-            v1[r] = lane < 25 ? w1[r * 25 + lane] : 0.f;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) v2[r][k] = lane + 64 * k < 200 ? w2[r * 200 + lane + 64 * k] : 0.f;
-        }
-        float s1j = 0.f, s2i = 0.f;
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-            float a = 0.f, c = 0.f;
-            if (lane < 25) a += v1[r];
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (lane + 64 * k < 200) c += v2[r][k];
-#pragma unroll
-            for (int m = 32; m > 0; m >>= 1) {
-                a += __shfl_xor(a, m);
-                c += __shfl_xor(c, m);
-            }
-            if ((lane & 7) == r) s1j = a;
-            if ((lane >> 3) == r) s2i = c;
-        }
-        tail_weights_unit(w1, w2, w6, s1j, s2i, tailw, unit, lane);
-        return;
-    }
-    blk -= ntail;
     if (blk < nprep) {
         prep_block(prep.w[blk], prep.s[blk], prep.cout[blk], prep.fan_in[blk], 0);
         return;
@@ -610,8 +573,8 @@ int launch_fwd_head_exact(const LayerDev& d2, const TailArgs& t, float* y, float
 
 int launch_weight_prologue(int n, float* const* w, const int* cout, const int* fan_in, float* const* s,
                            const float* w1, const float* w2, float* w21, int nphase, const float* const* pw,
-                           const int* pcin, const int* pup_first, float* const* pout, const float* w6, float* tailw,
-                           hipStream_t st, const char** why) {
+                           const int* pcin, const int* pup_first, float* const* pout, hipStream_t st,
+                           const char** why) {
     if (n < 0 || n > PrepArgs::kMax || nphase < 0 || nphase > PhaseArgs::kMax) {
         *why = "too many layers for one nconv_weight_prologue launch (max 32 normalisers, 8 phase layers)";
         return -22;
@@ -630,10 +593,9 @@ int launch_weight_prologue(int n, float* const* w, const int* cout, const int* f
         p.ci0[i] = pup_first[i];
         p.cin[i] = pcin[i];
     }
-    const int blocks = n + (w21 ? (kHeadUnits + 3) / 4 : 0) + nphase + (tailw ? (kTailUnits + 3) / 4 : 0);
+    const int blocks = n + (w21 ? (kHeadUnits + 3) / 4 : 0) + nphase;
     if (blocks == 0) return 0;
-    hipLaunchKernelGGL(weight_prologue, dim3(blocks), dim3(kPrepThreads), 0, st, a, n, w1, w2, w21, p, nphase, w6,
-                       tailw);
+    hipLaunchKernelGGL(weight_prologue, dim3(blocks), dim3(kPrepThreads), 0, st, a, n, w1, w2, w21, p, nphase);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         *why = hipGetErrorString(e);

@@ -26,8 +26,6 @@ struct TailArgs {
     float* c1;
     float* y6;  // optional (training): nconv6's outputs written by the fused tail (phase kernel)
     float* c6;
-    int yprod;  // inference head (nconv_fwd_head_xc): write nconv2's y * cout where y goes (the
-                // composed tail's staged product, fwd_tail_comp)
 };
 
 struct BwdArgs {
@@ -138,8 +136,8 @@ int launch_fwd_head_exact(const LayerDev& d2, const TailArgs& t, float* y, float
                           const char** why);
 int launch_weight_prologue(int n, float* const* w, const int* cout, const int* fan_in, float* const* s,
                            const float* w1, const float* w2, float* w21, int nphase, const float* const* pw,
-                           const int* pcin, const int* pup_first, float* const* pout, const float* w6, float* tailw,
-                           hipStream_t st, const char** why);
+                           const int* pcin, const int* pup_first, float* const* pout, hipStream_t st,
+                           const char** why);
 int launch_train_prologue(int n, float* const* w, const int* cout, const int* fan_in, const int* sp,
                           float* const* s, int head1, int head2, float* w21, unsigned* sync, int nphase,
                           const int* players, const int* pup_first, float* const* pout, float* const* pbox,
@@ -147,12 +145,6 @@ int launch_train_prologue(int n, float* const* w, const int* cout, const int* fa
 int launch_head_weights(const float* w1, const float* s1, const float* w2, float* out, hipStream_t st,
                         const char** why);
 int launch_fwd_tail(const LayerDev& d, const TailArgs& t, float* out, hipStream_t st, const char** why);
-// The fused tail with nconv6's skip-half confidence mass composed (nconv_fwd_tail.hip, nconv_tail.h)
-bool fwd_tail_comp_supported(const nconv_layer& L);
-int launch_fwd_tail_comp(const LayerDev& d, const TailArgs& t, float* out, const float* s_in, float thresh,
-                         const float* frag, bool a_product, hipStream_t st, const char** why);
-int launch_tail_weights(const float* w1, const float* s1, const float* w2, const float* s2, const float* w6,
-                        float* out, hipStream_t st, const char** why);
 int launch_weight_prep(int n, float* const* w, const int* cout, const int* fan_in, const int* sp,
                        float* const* s, hipStream_t st, const char** why);
 

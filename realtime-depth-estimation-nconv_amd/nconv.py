@@ -148,18 +148,13 @@ def phase_weights(weights, up_first, outs):
     _lib.check(rc, "nconv_phase_weights")
 
 
-def weight_prologue(weights, wsums, head=None, phase=None, tail=None):
+def weight_prologue(weights, wsums, head=None, phase=None):
     """nconv_weight_prologue: the eval-mode weight prologue in one launch, bitwise what
-    weight_prep(weights, [False] * n, wsums) + head_weights + phase_weights (+ tail_weights) write.
+    weight_prep(weights, [False] * n, wsums) + head_weights + phase_weights write.
     head: (w1, w2, out) -- nconv1 (8, 1, 5, 5), nconv2 (8, 8, 5, 5), HEAD_WEIGHTS_FLOATS out -- or
-    None; phase: (weights, up_first, outs) as phase_weights' arguments, or None; tail: (w6, out) --
-    nconv6 (8, 16, 3, 3) and TAIL_WEIGHTS_FLOATS out, the composed tail's weights (needs head)."""
+    None; phase: (weights, up_first, outs) as phase_weights' arguments, or None."""
     n = len(weights)
     w1, w2, w21 = head if head is not None else (None, None, None)
-    w6, wt = tail if tail is not None else (None, None)
-    if wt is not None and (w1 is None or wt.numel() < TAIL_WEIGHTS_FLOATS or not wt.is_contiguous() or
-                           wt.dtype != torch.float32):
-        raise ValueError(f"tail-weight buffer needs the head and {TAIL_WEIGHTS_FLOATS} contiguous fp32 elements")
     pw, pup, pout = phase if phase is not None else ([], [], [])
     if w21 is not None and (w21.numel() < HEAD_WEIGHTS_FLOATS or not w21.is_contiguous() or
                             w21.dtype != torch.float32):
@@ -175,8 +170,7 @@ def weight_prologue(weights, wsums, head=None, phase=None, tail=None):
         (I * max(n, 1))(*[w[0].numel() for w in weights]), (P * max(n, 1))(*[s.data_ptr() for s in wsums]),
         _lib.ptr(w1), _lib.ptr(w2), _lib.ptr(w21),
         m, (P * max(m, 1))(*[w.data_ptr() for w in pw]), (I * max(m, 1))(*[w.shape[1] for w in pw]),
-        (I * max(m, 1))(*pup), (P * max(m, 1))(*[o.data_ptr() for o in pout]), _lib.ptr(w6), _lib.ptr(wt),
-        _lib.stream_handle(dev))
+        (I * max(m, 1))(*pup), (P * max(m, 1))(*[o.data_ptr() for o in pout]), _lib.stream_handle(dev))
     _lib.check(rc, "nconv_weight_prologue")
 
 
@@ -299,40 +293,6 @@ def layer_forward_head(spec1: LayerSpec, spec2: LayerSpec, S, w1, b1, s1, w2, b2
                                    _lib.stream_handle(S.device))
     _lib.check(rc, "nconv_fwd_head")
     return (y, co, py, pc, arg, y1, c1) if train else (y, co, py, pc)
-
-
-TAIL_WEIGHTS_FLOATS = 3072  # include/nconv.h NCONV_TAIL_WEIGHTS_FLOATS
-
-
-def tail_weights(spec1: LayerSpec, spec2: LayerSpec, spec6: LayerSpec, S, w1, s1, w2, s2, w6, out=None):
-    """nconv_tail_weights: the composed tail's weights (TAIL_WEIGHTS_FLOATS: nconv6's skip-half
-    confidence weights composed with nconv2's and nconv1's as exact three-part bf16 matrix-core
-    operands, then nconv6's phase weights re-laid) from the current weights and normalisers."""
-    L1 = spec1.descriptor(S, None, None, None, w1, None, s1)
-    L2 = spec2.descriptor(S, S, None, None, w2, None, s2)
-    L6 = _lib.NconvLayer()
-    L6.Cin, L6.Cout, L6.KH, L6.KW, L6.groups = w6.shape[1], w6.shape[0], w6.shape[2], w6.shape[3], 1
-    L6.weight = w6.data_ptr()
-    if out is None:
-        out = torch.empty(TAIL_WEIGHTS_FLOATS, device=S.device, dtype=torch.float32)
-    rc = _lib.lib().nconv_tail_weights(_lib.ctypes.byref(L1), _lib.ctypes.byref(L2), _lib.ctypes.byref(L6),
-                                       _lib.ptr(out), _lib.stream_handle(S.device))
-    _lib.check(rc, "nconv_tail_weights")
-    return out
-
-
-def layer_forward_head_xc(spec1: LayerSpec, spec2: LayerSpec, S, w1, b1, s1, w2, b2, s2, w21):
-    """nconv_fwd_head_xc: the exact inference head writing nconv2's y * cout instead of y; returns
-    (xc, cout, maxpool2x2(y), maxpool2x2(cout)). No autograd."""
-    L1 = spec1.descriptor(S, None, None, None, w1, b1, s1)
-    L2 = spec2.descriptor(S, S, None, None, w2, b2, s2, w21)
-    B, H, W = S.shape[0], L1.Ho, L1.Wo
-    sh, shp = (B, 8, H, W), (B, 8, H // 2, W // 2)
-    xc, co, py, pc = _outputs(None, 4, (sh, sh, shp, shp), S.device)
-    rc = _lib.lib().nconv_fwd_head_xc(_lib.ctypes.byref(L1), _lib.ctypes.byref(L2), _lib.ptr(xc), _lib.ptr(co),
-                                      _lib.ptr(py), _lib.ptr(pc), _lib.stream_handle(S.device))
-    _lib.check(rc, "nconv_fwd_head_xc")
-    return xc, co, py, pc
 
 
 class NConvLayerFn(torch.autograd.Function):

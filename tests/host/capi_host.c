@@ -42,8 +42,6 @@ int main(void) {
     F(nconv_bwd_io, tail_cout); F(nconv_bwd_io, tail_gy); F(nconv_bwd_io, tail_workspace);
     F(nconv_bwd_io, tail_workspace_bytes); F(nconv_bwd_io, tail_gw); F(nconv_bwd_io, tail_nparts);
     F(nconv_bwd_io, box_weights); F(nconv_bwd_io, tail_crop0); F(nconv_bwd_io, tail_h); F(nconv_bwd_io, tail_w);
-    S(nconv_tail_comp);
-    F(nconv_tail_comp, s_in); F(nconv_tail_comp, thresh); F(nconv_tail_comp, weights); F(nconv_tail_comp, a_product);
     S(nconv_bn_train);
     F(nconv_bn_train, B); F(nconv_bn_train, C); F(nconv_bn_train, H); F(nconv_bn_train, W); F(nconv_bn_train, x);
     F(nconv_bn_train, gamma); F(nconv_bn_train, beta); F(nconv_bn_train, running_mean);
@@ -78,13 +76,6 @@ int main(void) {
     int kf = -1, kd = -1, kw = -1;
     rc = nconv_plan(&z, &kf, &kd, &kw);
     printf("\"plan_zero\": [%d, %d, %d, %d, %d],\n", rc, z.math == NCONV_MATH_FP32, kf, kd, kw);
-    /* the composed tail refuses a non-DNET nconv6 before any launch */
-    nconv_tail_comp tc = {fake, 0.01f, fake, 1};
-    nconv_layer l6 = L;
-    l6.Cin = 16; l6.KH = l6.KW = 3; l6.PH = l6.PW = 1; l6.Ho = 16; l6.Wo = 16;
-    l6.load_mode = NCONV_LOAD_UPCAT_UP_FIRST; l6.b = l6.a; l6.b.H = 8; l6.b.W = 8; l6.waux = fake;
-    rc = nconv_fwd_tail_comp(&l6, fake, fake, fake, 8, 2, 1e-7f, out, NULL, 16, 16, 1, NULL, NULL, &tc, NULL);
-    printf("\"rc_tail_comp_pad1\": [%d, \"%s\"],\n", rc, nconv_last_error());
     printf("\"abi\": [%d, %d]\n}\n", nconv_abi_version(), NCONV_ABI_VERSION);
     return 0;
 }

@@ -248,13 +248,12 @@ def test_weight_prologue_validation_is_host_only(nconv_amd):
     pw, po = (P * 1)(p), (P * 1)(p)
     cin, up = (I * 1)(16), (I * 1)(8)
     cases = [
-        ((-1, w, cout, fan, s, None, None, None, 0, None, None, None, None, None, None, None), "negative count"),
-        ((1, None, cout, fan, s, None, None, None, 0, None, None, None, None, None, None, None), "null argument"),
-        ((1, w, (I * 1)(0), fan, s, None, None, None, 0, None, None, None, None, None, None, None), "bad layer entry"),
-        ((1, w, cout, fan, s, None, p, p, 0, None, None, None, None, None, None, None), "head_w1 and head_w2"),
-        ((0, None, None, None, None, None, None, None, 1, None, cin, up, po, None, None, None), "null phase argument"),
-        ((0, None, None, None, None, None, None, None, 1, pw, cin, (I * 1)(9), po, None, None, None), "outside [0, Cin)"),
-        ((0, None, None, None, None, p, p, p, 0, None, None, None, None, None, p, None), "tail_w6"),
+        ((-1, w, cout, fan, s, None, None, None, 0, None, None, None, None, None), "negative count"),
+        ((1, None, cout, fan, s, None, None, None, 0, None, None, None, None, None), "null argument"),
+        ((1, w, (I * 1)(0), fan, s, None, None, None, 0, None, None, None, None, None), "bad layer entry"),
+        ((1, w, cout, fan, s, None, p, p, 0, None, None, None, None, None), "head_w1 and head_w2"),
+        ((0, None, None, None, None, None, None, None, 1, None, cin, up, po, None), "null phase argument"),
+        ((0, None, None, None, None, None, None, None, 1, pw, cin, (I * 1)(9), po, None), "outside [0, Cin)"),
     ]
     for args, msg in cases:
         assert lib.nconv_weight_prologue(*args) == -22, msg

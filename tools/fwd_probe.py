@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Inference-forward probe (developer tool, GPU): the bench's hipGraph-replayed config-2 forward
 (B=8 352x1216, exact fp32, generalized crop) with DNET attributes set from the command line, e.g.
-    python3 tools/fwd_probe.py compose_tail=0 inference_streams=1 [--steps 200] [--density 0.05]
+    python3 tools/fwd_probe.py fused_head=0 inference_streams=1 [--steps 200] [--density 0.05]
 prints frames/s; run under rocprofv3 --kernel-trace and read the replayed step's kernel timeline
 with tools/fwd_timeline.py."""
 import os
