@@ -259,9 +259,13 @@ class DNETFn(torch.autograd.Function):
             gp2 = (e(p2x), e(p2c))
             bwd(3, 0, 0, gp2, None, src_a=(p2x, p2c), spec=plain[0], pool_grad=(*gp3, a3))  # down1
             if FUSE_HEAD_BWD and not need[1]:  # nconv2's input gradient feeds nconv1's weight gradient in-tile
-                layer_bwd(sp[1], (X[1][0], X[1][1], None, None, *W[1]), X[2][0], X[2][1], *G[2],
-                          (None, None, None, None), gw[1], gb[1], pool_grad=(*gp2, a2),
-                          head=(sp[0], S, *W[0], gw[0], gb[0]))
+                args = (sp[1], (X[1][0], X[1][1], None, None, *W[1]), X[2][0], X[2][1], *G[2],
+                        (None, None, None, None), gw[1], gb[1])
+                kw = dict(pool_grad=(*gp2, a2), head=(sp[0], S, *W[0], gw[0], gb[0]))
+                if WGRAD_LAST_MAIN:  # the last layer's weight gradient after its input gradient, on this stream
+                    layer_backward(*args, defer=red, **kw)
+                else:
+                    layer_bwd(*args, **kw)
                 finish()
                 out = [None, None, None, None]
                 for i in range(9):
@@ -330,8 +334,12 @@ class CropFn(torch.autograd.Function):
 
 
 # The training backward's weight gradients on one side stream (two round-robin streams measured
-# slower: 2.20 -> 2.26 ms per graphed step, profiles/r5_ab_two_wgrad_streams.log)
+# slower: 2.20 -> 2.26 ms per graphed step, profiles/r5_ab_two_wgrad_streams.log), except the last
+# layer's (nconv2's, WGRAD_LAST_MAIN): it runs on the main stream after that layer's input
+# gradient, which is the main stream's last kernel, instead of queueing behind the side stream's
+# backlog while the main stream idles
 WGRAD_STREAM = True
+WGRAD_LAST_MAIN = True
 _WGRAD_STREAMS = {}
 
 

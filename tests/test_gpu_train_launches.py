@@ -211,3 +211,25 @@ def test_dnet_train_forward_streams_bitwise(nconv_amd, gpu, B, H, W, crop):
     assert set(ga) == set(gb) and len(ga) == 18
     for k in ga:
         assert torch.equal(ga[k], gb[k]), k
+
+
+@pytest.mark.parametrize("B,H,W,crop", [(2, 64, 96, "generalized"), (8, 352, 1216, "generalized")])
+def test_dnet_train_wgrad_stream_placement_bitwise(nconv_amd, gpu, B, H, W, crop):
+    """Where the weight gradients run (dnet.WGRAD_LAST_MAIN: nconv2's on the main stream after its
+    input gradient, or with the others on the side stream; dnet.WGRAD_STREAM off: all serial) does
+    not change a bit of any gradient: same kernels, same fixed-order reductions."""
+    D = nconv_amd.dnet
+    keep = (D.WGRAD_LAST_MAIN, D.WGRAD_STREAM)
+    runs = []
+    try:
+        for last_main, stream in ((True, True), (False, True), (True, False)):
+            D.WGRAD_LAST_MAIN, D.WGRAD_STREAM = last_main, stream
+            runs.append(_train_iteration(nconv_amd, gpu, B, H, W, crop))
+    finally:
+        D.WGRAD_LAST_MAIN, D.WGRAD_STREAM = keep
+    oa, _, ga = runs[0]
+    for ob, _, gb in runs[1:]:
+        assert torch.equal(oa, ob)
+        assert set(ga) == set(gb) and len(ga) == 18
+        for k in ga:
+            assert torch.equal(ga[k], gb[k]), k
