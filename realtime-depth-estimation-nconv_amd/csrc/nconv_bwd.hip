@@ -1625,6 +1625,325 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(GP ? NCONV_W
     }
 }
 
+// ---- wgrad_mfma over output-row pairs (8 -> 8, 5x5: nconv2 and the down layers) ------------------
+// wgrad_mfma's (kh, i) x (kw, o) tile is 40 x 40 for these layers and pads to 48 x 48 (3 x 3 MFMA
+// tiles, 69 % of the products useful). Two output rows oh, oh + 1 at once fill the tiles exactly:
+// rows M = (r, i), r = 0..K over the K + 1 staged input rows oh - PH + r (48 = 3 tiles), columns
+// N = (d, kw, o) over the two g rows oh + d (80 = 5 tiles), so
+//     C[(r, i)][(d, kw, o)] += sum_q XC[i][oh - PH + r][q - PW] * gN[o][oh + d][q - kw] (+ C * gD)
+// holds the kernel row kh = r - d of output row oh + d: gW[o][i][kh][kw] = C[(kh, i)][(0, kw, o)] +
+// C[(kh + 1, i)][(1, kw, o)] (the pairs r = K, d = 0 and r = 0, d = 1 are not taps). 15 MFMAs per
+// k-step and operand part for two rows instead of 18, and 8 operand reads instead of 12. The input
+// ring holds K + 3 rows (K + 1 in use, two being written for the next pair), the g rows are double
+// buffered per pair, the next pair staged under this pair's MFMAs; an odd last row pairs with a
+// zero row. Same products, summed in a different
+// (fixed) order: within fp32 round-off of wgrad_mfma, deterministic.
+template <int CIN, int COUT, int K>
+struct Wm2Cfg {
+    static constexpr int TW = 64;
+    static constexpr int M = (K + 1) * CIN, N = 2 * K * COUT;
+    static constexpr int MT = M / 16, NT = N / 16;
+    static_assert(M % 16 == 0 && N % 16 == 0, "row-pair tiles fill the MFMA tiles exactly");
+    static constexpr int XP = TW + 2;  // == 2 (mod 32): a kernel row's channels on banks 2i + k
+    static constexpr int SLOTS = 8;    // K + 3 <= 8: slot = input row & 7
+    static_assert(K + 3 <= SLOTS, "input ring");
+    // A: a 16-row tile holds two input rows in consecutive slots; SLOT == 16 (mod 32) puts the second
+    // on the other 16 banks (and the ring's wrap, 7 slots back, is == 16 too)
+    static constexpr int SLOT = CIN * XP + ((((2 * CIN) % 32 - CIN * XP) % 32) + 32) % 32;
+    static constexpr int GP = 68;                      // B: channel o at 4o + {kw shifts} (mod 32)
+    static constexpr int GROW = COUT * GP + ((((2 - COUT * GP) % 32) + 32) % 32);  // == 2 (mod 32):
+    // the tile straddling d = 0 / 1 reads words 4o + {0, 1} and GROW + 4o + {4, 5}: distinct banks
+    static constexpr int C_OFF = SLOTS * SLOT;         // c ring after the xc ring
+    static constexpr int G_OFF = 2 * C_OFF;
+    static constexpr int GPART = 2 * GROW;             // {gN rows d = 0, 1} then {gD rows}
+    static constexpr int GBUF = 2 * GPART;
+    static constexpr int STAGE = G_OFF + 2 * GBUF;
+    static constexpr int TILE = MT * NT * 256;         // one wave's accumulators
+    static constexpr int RED = 2 * TILE;               // waves 0 / 1 store, 2 / 3 add
+    static constexpr int LDS = STAGE > RED ? STAGE : RED;
+    static constexpr int CPW = (CIN + 3) / 4, OPW = COUT / 4;
+    static_assert(SLOT % 32 == 16 && XP % 32 == 2 && GP % 32 == 4 && GROW % 32 == 2, "bank layout");
+    static_assert(COUT % 4 == 0 && CIN % 4 == 0, "channels staged four per pass");
+};
+
+#ifndef NCONV_WM2_WAVES
+#define NCONV_WM2_WAVES 3
+#endif
+#ifndef NCONV_WM2_SCHED
+#define NCONV_WM2_SCHED 1
+#endif
+template <int CIN, int COUT, int K, int MODE, bool GP = false>
+__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(NCONV_WM2_WAVES, 8))) void wgrad_mfma2(
+    LayerDev d, BwdArgs a, float* part, int nstrip, int nseg, int seg_rows) {
+    using C = Wm2Cfg<CIN, COUT, K>;
+    __shared__ __attribute__((aligned(16))) float lds[C::LDS];
+    const nconv_layer& L = d.L;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    int blk = blockIdx.x;
+    const int strip = blk % nstrip;
+    blk /= nstrip;
+    const int seg = blk % nseg, b = blk / nseg;
+    const int ow0 = strip * C::TW;
+    const int r0 = seg * seg_rows, r1 = min(L.Ho, r0 + seg_rows);
+    constexpr unsigned OOB = 0x80000000u;
+
+    const int kq = lane >> 4, ml = lane & 15;
+    int a_r[C::MT], a_ik[C::MT], b_off[C::NT];
+#pragma unroll
+    for (int t = 0; t < C::MT; ++t) {
+        const int m = 16 * t + ml;
+        a_r[t] = m / CIN;
+        a_ik[t] = (m % CIN) * C::XP + kq;
+    }
+#pragma unroll
+    for (int u = 0; u < C::NT; ++u) {
+        const int n = 16 * u + ml, dd = n / (K * COUT), rem = n % (K * COUT);
+        b_off[u] = dd * C::GROW + (rem % COUT) * C::GP + (K - 1) - rem / COUT + kq;
+    }
+
+    // ---- staging (as wgrad_mfma, two rows per pair) ----
+    constexpr int NG = GP ? 7 : 4;  // gy, gco, y, cout (+ pooled gy, gcout, argmax code)
+    constexpr int NH = C::OPW * (K - 1);
+    static_assert(NH <= 64, "halo lanes");
+    const bool hl = lane < NH;
+    const int hkk = hl ? lane / (K - 1) : 0, hcol = 64 + lane % (K - 1), ho = w + 4 * hkk;
+    float px[1][C::CPW], pc[1][C::CPW];  // one row's loads in flight at a time (see the loop)
+    float gq[1][C::OPW][NG], gh[1][NG];
+    float gb_acc[C::OPW], gs_acc[C::OPW], gb_h = 0.f, gs_h = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < C::OPW; ++kk) gb_acc[kk] = gs_acc[kk] = 0.f;
+    const int iw_in = ow0 - L.PW + lane;
+    // input row ih (valid: a row of this pair; else zeros, so no value of another segment enters)
+    auto load_in = [&](int j, int ih, bool valid) {
+#pragma unroll
+        for (int kk = 0; kk < C::CPW; ++kk) {
+            const int i = w + 4 * kk;
+            px[j][kk] = pc[j][kk] = 0.f;
+            if (valid) load_px<MODE>(d, chan_src<MODE>(d, b, i), ih, iw_in, px[j][kk], pc[j][kk]);
+        }
+    };
+    auto store_in = [&](int j, int ih) {
+        const int slot = ih & (C::SLOTS - 1);
+#pragma unroll
+        for (int kk = 0; kk < C::CPW; ++kk) {
+            const int i = w + 4 * kk;
+            const float cv = (MODE == NCONV_LOAD_THRESH) ? (px[j][kk] > L.thresh ? 1.0f : 0.0f) : pc[j][kk];
+            lds[slot * C::SLOT + i * C::XP + lane] = px[j][kk] * cv;
+            lds[C::C_OFF + slot * C::SLOT + i * C::XP + lane] = cv;
+        }
+    };
+    const int plane = L.Ho * L.Wo;
+    const int Hp = L.Ho >> 1, Wp = L.Wo >> 1, pplane = Hp * Wp;
+    auto load_g = [&](int j, int oh, bool valid) {
+        const int ow = ow0 - (K - 1) + lane, owh = ow0 - (K - 1) + hcol;
+        const bool row_in = valid && (unsigned)oh < (unsigned)L.Ho;
+        const bool in = row_in && (unsigned)ow < (unsigned)L.Wo;
+        const bool inh = hl && row_in && (unsigned)owh < (unsigned)L.Wo;
+        const size_t base = (size_t)b * COUT * plane;
+        const int bytes = COUT * plane * 4;
+        const __amdgpu_buffer_rsrc_t rgy = plane_rsrc(a.gy + base, bytes);
+        const __amdgpu_buffer_rsrc_t rco = plane_rsrc(a.co + base, bytes);
+        const __amdgpu_buffer_rsrc_t ry = plane_rsrc(a.y + base, bytes);
+        const __amdgpu_buffer_rsrc_t rgc = plane_rsrc(a.gco ? a.gco + base : a.y, a.gco ? bytes : 0);
+        const unsigned off = in ? (unsigned)(oh * L.Wo + ow) * 4u : OOB;
+        const unsigned offh = inh ? (unsigned)((ho * L.Ho + oh) * L.Wo + owh) * 4u : OOB;
+#pragma unroll
+        for (int kk = 0; kk < C::OPW; ++kk) {
+            const int so = (w + 4 * kk) * plane * 4;
+            gq[j][kk][0] = ld_f32s(rgy, off, so);
+            gq[j][kk][1] = ld_f32s(rco, off, so);
+            gq[j][kk][2] = ld_f32s(ry, off, so);
+            gq[j][kk][3] = ld_f32s(rgc, off, so);
+        }
+        gh[j][0] = ld_f32(rgy, offh);
+        gh[j][1] = ld_f32(rco, offh);
+        gh[j][2] = ld_f32(ry, offh);
+        gh[j][3] = ld_f32(rgc, offh);
+        if constexpr (GP) {
+            const size_t pbase = (size_t)b * COUT * pplane;
+            const int pbytes = COUT * pplane * 4;
+            const __amdgpu_buffer_rsrc_t rpy = plane_rsrc(a.gpy + pbase, pbytes);
+            const __amdgpu_buffer_rsrc_t rpc = plane_rsrc(a.gpc + pbase, pbytes);
+            const __amdgpu_buffer_rsrc_t rpa = plane_rsrc((const float*)(a.parg + pbase), pbytes);
+            const unsigned po = in ? pool_elem_off(oh, ow, Hp, Wp, OOB) : OOB;
+            const unsigned pe = inh ? pool_elem_off(oh, owh, Hp, Wp, OOB) : OOB;
+            const unsigned poh = pe != OOB ? pe + (unsigned)(ho * pplane) * 4u : OOB;
+#pragma unroll
+            for (int kk = 0; kk < C::OPW; ++kk) {
+                const int so = (w + 4 * kk) * pplane * 4;
+                gq[j][kk][4] = ld_f32s(rpy, po, so);
+                gq[j][kk][5] = ld_f32s(rpc, po, so);
+                gq[j][kk][6] = ld_f32s(rpa, po, so);
+            }
+            gh[j][4] = ld_f32(rpy, poh);
+            gh[j][5] = ld_f32(rpc, poh);
+            gh[j][6] = ld_f32(rpa, poh);
+        }
+    };
+    float bias_o[C::OPW], wsum_o[C::OPW];
+#pragma unroll
+    for (int kk = 0; kk < C::OPW; ++kk) {
+        bias_o[kk] = L.bias[w + 4 * kk];
+        wsum_o[kk] = L.wsum[w + 4 * kk];
+    }
+    // g row j of the pair (output row oh_cur) into buffer buf; an invalid row (past the segment)
+    // stores zeros and adds nothing to the bias / normaliser sums
+    auto store_g = [&](int buf, int j, int dr, int oh_cur, bool valid) {
+        const unsigned sub = (unsigned)((oh_cur & 1) << 1), ow_m = (unsigned)(ow0 - (K - 1) + lane);
+        const unsigned ow_h = (unsigned)(ow0 - (K - 1) + hcol);
+        float* gb_row = lds + C::G_OFF + buf * C::GBUF + dr * C::GROW;
+#pragma unroll
+        for (int kk = 0; kk < C::OPW; ++kk) {
+            const int o = w + 4 * kk;
+            float gy = gq[j][kk][0], gco = gq[j][kk][3];
+            if constexpr (GP)
+                pool_route(gy, gco, gq[j][kk][4], gq[j][kk][5], __builtin_bit_cast(unsigned, gq[j][kk][6]), sub | (ow_m & 1u));
+            float gN, gD;
+            nconv_grad_nd(gy, gco, gq[j][kk][2], gq[j][kk][1], L.eps, bias_o[kk], wsum_o[kk], gN, gD);
+            float* g = gb_row + o * C::GP + lane;
+            g[0] = valid ? gN : 0.f;
+            g[C::GPART] = valid ? gD : 0.f;
+            if (lane >= K - 1) {  // (invalid rows loaded zeros: gy = gco = 0)
+                gb_acc[kk] += gy;
+                gs_acc[kk] = fmaf(gco, gq[j][kk][1], gs_acc[kk]);
+            }
+        }
+        {   // halo pass (columns 64 .. 64+K-2)
+            float bo = bias_o[0], so = wsum_o[0];
+#pragma unroll
+            for (int kk = 1; kk < C::OPW; ++kk) {
+                bo = hkk == kk ? bias_o[kk] : bo;
+                so = hkk == kk ? wsum_o[kk] : so;
+            }
+            float gy = gh[j][0], gco = gh[j][3];
+            if constexpr (GP) pool_route(gy, gco, gh[j][4], gh[j][5], __builtin_bit_cast(unsigned, gh[j][6]), sub | (ow_h & 1u));
+            float gN, gD;
+            nconv_grad_nd(gy, gco, gh[j][2], gh[j][1], L.eps, bo, so, gN, gD);
+            if (hl) {
+                float* g = gb_row + ho * C::GP + hcol;
+                g[0] = valid ? gN : 0.f;
+                g[C::GPART] = valid ? gD : 0.f;
+            }
+            gb_h += gy;
+            gs_h = fmaf(gco, gh[j][1], gs_h);
+        }
+    };
+
+    f4acc acc[C::MT][C::NT];
+#pragma unroll
+    for (int t = 0; t < C::MT; ++t)
+#pragma unroll
+        for (int u = 0; u < C::NT; ++u) acc[t][u] = (f4acc){0.f, 0.f, 0.f, 0.f};
+
+    // The next pair's rows are staged DURING this pair's MFMAs, one row (input + g) per half of the
+    // k-steps: its input row goes to a ring slot this pair does not read (slots ih + 6, ih + 7 of
+    // the 8), its g row to the other buffer (whose last reader, the previous pair, is behind the
+    // barrier), so only one row's loads are ever in flight and one barrier per pair suffices.
+    if (r0 < r1) {
+        for (int r = 0; r <= K; ++r) {  // prologue: the first pair's K + 1 input rows and its g rows
+            load_in(0, r0 - L.PH + r, r < K || r0 + 1 < r1);
+            store_in(0, r0 - L.PH + r);
+        }
+        for (int j = 0; j < 2; ++j) {
+            load_g(0, r0 + j, j == 0 || r0 + 1 < r1);
+            store_g(0, 0, j, r0 + j, j == 0 || r0 + 1 < r1);
+        }
+    }
+    __syncthreads();
+#pragma unroll 1
+    for (int oh = r0; oh < r1; oh += 2) {
+        const int buf = ((oh - r0) >> 1) & 1;
+        const int nx = oh + 2;  // the next pair (none past r1: its staging is skipped)
+        const bool more = nx < r1;
+        int ax[C::MT], bn[C::NT];
+#pragma unroll
+        for (int t = 0; t < C::MT; ++t) ax[t] = ((oh - L.PH + a_r[t]) & (C::SLOTS - 1)) * C::SLOT + a_ik[t];
+#pragma unroll
+        for (int u = 0; u < C::NT; ++u) bn[u] = C::G_OFF + buf * C::GBUF + b_off[u];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            if (more) {  // next pair's row j: input row r = K - 1 + j, g row d = j
+                load_in(0, nx - L.PH + K - 1 + j, j == 0 || nx + 1 < r1);
+                load_g(0, nx + j, j == 0 || nx + 1 < r1);
+            }
+#pragma unroll
+            for (int s = 2 * j; s < 2 * j + 2; ++s) {
+                const int q0 = 16 * w + 4 * s;
+#pragma unroll
+                for (int pt = 0; pt < 2; ++pt) {  // {x*c, gN} then {c, gD}
+                    float va[C::MT], vb[C::NT];
+#pragma unroll
+                    for (int t = 0; t < C::MT; ++t) va[t] = lds[ax[t] + pt * C::C_OFF + q0];
+#pragma unroll
+                    for (int u = 0; u < C::NT; ++u) vb[u] = lds[bn[u] + pt * C::GPART + q0];
+#pragma unroll
+                    for (int t = 0; t < C::MT; ++t)
+#pragma unroll
+                        for (int u = 0; u < C::NT; ++u)
+                            acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(va[t], vb[u], acc[t][u], 0, 0, 0);
+#if NCONV_WM2_SCHED
+                    __builtin_amdgcn_sched_barrier(0);  // (operand reads of the next step not hoisted above)
+#endif
+                }
+            }
+            if (more) {
+                store_in(0, nx - L.PH + K - 1 + j);
+                store_g(buf ^ 1, 0, j, nx + j, j == 0 || nx + 1 < r1);
+            }
+        }
+        __syncthreads();
+    }
+
+    // ---- the four waves' tiles summed in a fixed order ((w0 + w2) + (w1 + w3)), then each weight
+    //      as its two row-pair terms: gW[o][i][kh][kw] = C[(kh, i)][(0, kw, o)] + C[(kh+1, i)][(1, kw, o)]
+    constexpr int NW = COUT * CIN * K * K;
+    float* out = part + (size_t)blockIdx.x * (NW + 2 * COUT);
+    __syncthreads();
+    float* red = lds + (w & 1) * C::TILE;
+    if (w < 2) {
+#pragma unroll
+        for (int t = 0; t < C::MT; ++t)
+#pragma unroll
+            for (int u = 0; u < C::NT; ++u)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) red[(t * C::NT + u) * 256 + r * 64 + lane] = acc[t][u][r];
+    }
+    __syncthreads();
+    if (w >= 2) {
+#pragma unroll
+        for (int t = 0; t < C::MT; ++t)
+#pragma unroll
+            for (int u = 0; u < C::NT; ++u)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) red[(t * C::NT + u) * 256 + r * 64 + lane] += acc[t][u][r];
+    }
+    __syncthreads();
+    auto at = [&](int m, int n) {  // the summed C[m][n] (MFMA 16x16 output layout)
+        const int t = m >> 4, mm = m & 15, u = n >> 4;
+        const int idx = (t * C::NT + u) * 256 + (mm & 3) * 64 + (mm >> 2) * 16 + (n & 15);
+        return lds[idx] + lds[C::TILE + idx];
+    };
+    for (int e = tid; e < NW; e += kT) {
+        const int kw = e % K, kh = (e / K) % K, i = (e / (K * K)) % CIN, o = e / (K * K * CIN);
+        out[e] = at(kh * CIN + i, kw * COUT + o) + at((kh + 1) * CIN + i, K * COUT + kw * COUT + o);
+    }
+#pragma unroll
+    for (int kk = 0; kk < C::OPW; ++kk) {
+        const bool mine = hl && hkk == kk;
+        float sb = gb_acc[kk] + (mine ? gb_h : 0.f), ss = gs_acc[kk] + (mine ? gs_h : 0.f);
+#pragma unroll
+        for (int sh = 32; sh > 0; sh >>= 1) {
+            sb += __shfl_xor(sb, sh);
+            ss += __shfl_xor(ss, sh);
+        }
+        if (lane == 0) {
+            out[NW + w + 4 * kk] = sb;
+            out[NW + COUT + w + 4 * kk] = ss;
+        }
+    }
+}
+
 // ------------------------------------------------------------------------------------------------
 // Launchers
 // ------------------------------------------------------------------------------------------------
@@ -1696,6 +2015,15 @@ static WmGrid wm_grid(const nconv_layer& L, int target = 0) {
     if (g.nseg < 1) g.nseg = 1;
     g.nblk = (size_t)g.nstrip * g.nseg * L.B;
     return g;
+}
+// The 8 -> 8 5x5 weight gradients over output-row pairs (wgrad_mfma2); NCONV_WM_ROW_PAIRS=0: one row
+// at a time (wgrad_mfma), for A/B timing
+static bool wm_row_pairs() {
+    static const bool on = [] {
+        const char* e = getenv("NCONV_WM_ROW_PAIRS");
+        return !(e && e[0] == '0');
+    }();
+    return on;
 }
 // tiled 3x3 / 5x5 layers with several input channels (Cin = 1 has a single-row A tile and stays
 // on wgrad_tiled, which reads each g plane once per 4 x 64 tile instead of once per row segment)
@@ -1791,6 +2119,17 @@ static int go_bwd_tiled(const LayerDev& d, const BwdArgs& a, float* part, float*
             const int nw = COUT * CIN * K * K;
             return launch_wgrad_reduce(a, part, nblk, nw, COUT, CIN * K * K, L.wsum, st, why);
         } else if (a.gw || a.gb) {
+            if constexpr (CIN == 8 && COUT == 8 && K == 5 && !T7) {
+                if (wm_row_pairs()) {  // the row-pair form fills its MFMA tiles (wgrad_mfma2)
+                    const int per_cu = dev_occupancy((const void*)wgrad_mfma2<CIN, COUT, K, MODE, GP>, kT, 0);
+                    const int resident = device_cus() * (per_cu < kMfmaMaxPerCu ? per_cu : kMfmaMaxPerCu);
+                    const WmGrid g = wm_grid(L, kMfmaRounds * resident);
+                    hipLaunchKernelGGL((wgrad_mfma2<CIN, COUT, K, MODE, GP>), dim3(g.nblk), dim3(kT), 0, st, d, a,
+                                       part, g.nstrip, g.nseg, g.seg_rows);
+                    const int nw = COUT * CIN * K * K;
+                    return launch_wgrad_reduce(a, part, (int)g.nblk, nw, COUT, CIN * K * K, L.wsum, st, why);
+                }
+            }
             const int per_cu = dev_occupancy((const void*)wgrad_mfma<CIN, COUT, K, MODE, GP, T7>, kT, 0);
             const int resident = device_cus() * (per_cu < kMfmaMaxPerCu ? per_cu : kMfmaMaxPerCu);
             const WmGrid g = wm_grid(L, kMfmaRounds * resident);
