@@ -1525,25 +1525,24 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(GP ? NCONV_W
 #pragma unroll
         for (int u = 0; u < C::NT; ++u) acc[t][u] = (f4acc){0.f, 0.f, 0.f, 0.f};
 
+    // The next row is staged DURING this row's MFMAs (its loads before the first half of the k-steps,
+    // its stores after it): its input row goes to the ring slot this row does not read (K + 1 slots,
+    // K in use), its g row to the other buffer (whose last reader, the previous row, is behind the
+    // barrier) -- one barrier per row, and the staging's VALU work interleaved with the MFMAs
+    // instead of between barriers.
     if (r0 < r1) {
-        for (int kh = 0; kh < K - 1; ++kh) {  // prologue: the segment's first K-1 input rows
+        for (int kh = 0; kh < K; ++kh) {  // prologue: the segment's first K input rows and g row
             load_in(r0 - L.PH + kh);
             store_in(r0 - L.PH + kh);
         }
-        load_in(r0 - L.PH + K - 1);
         load_g(r0);
+        store_g(0, r0);
     }
+    __syncthreads();
 #pragma unroll 1
     for (int oh = r0; oh < r1; ++oh) {
         const int buf = (oh - r0) & 1;
-        store_in(oh - L.PH + K - 1);
-        store_g(buf, oh);
-        __syncthreads();
-        {   // next row's loads in flight during this row's MFMAs (re-reads the last row at the end)
-            const int nx = oh + 1 < r1 ? oh + 1 : oh;
-            load_in(nx - L.PH + K - 1);
-            load_g(nx);
-        }
+        const bool more = oh + 1 < r1;
         int ax[C::MT], bn[C::NT];
 #pragma unroll
         for (int t = 0; t < C::MT; ++t) {
@@ -1553,6 +1552,10 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(GP ? NCONV_W
         }
 #pragma unroll
         for (int u = 0; u < C::NT; ++u) bn[u] = C::G_OFF + buf * C::GBUF + b_off[u];
+        if (more) {
+            load_in(oh + 1 - L.PH + K - 1);
+            load_g(oh + 1);
+        }
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
             const int q0 = 16 * w + 4 * s;
@@ -1569,7 +1572,12 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(GP ? NCONV_W
                     for (int u = 0; u < C::NT; ++u)
                         acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(va[t], vb[u], acc[t][u], 0, 0, 0);
             }
+            if (s == 1 && more) {
+                store_in(oh + 1 - L.PH + K - 1);
+                store_g(buf ^ 1, oh + 1);
+            }
         }
+        __syncthreads();
     }
 
     // ---- the four waves' tiles summed in a fixed order -> this block's partial row ----
