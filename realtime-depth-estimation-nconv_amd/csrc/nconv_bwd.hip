@@ -1248,6 +1248,9 @@ struct WmCfg {
 #ifndef NCONV_WM_WAVES
 #define NCONV_WM_WAVES 3
 #endif
+#ifndef NCONV_WM_STORE_STEP
+#define NCONV_WM_STORE_STEP 1  // after which k-step the next row's staging is stored (its loads' latency budget)
+#endif
 #ifndef NCONV_WM_GP_WAVES
 #define NCONV_WM_GP_WAVES 3  // the pooled-gradient (training) instantiation (4: 128 VGPRs, 2 spilled)
 #endif
@@ -1572,7 +1575,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(GP ? NCONV_W
                     for (int u = 0; u < C::NT; ++u)
                         acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(va[t], vb[u], acc[t][u], 0, 0, 0);
             }
-            if (s == 1 && more) {
+            if (s == NCONV_WM_STORE_STEP && more) {
                 store_in(oh + 1 - L.PH + K - 1);
                 store_g(buf ^ 1, oh + 1);
             }
