@@ -52,6 +52,10 @@ LAYER_CASES = [
     ("nconv2_w4", PLAIN, 8, 8, 5, 2, 1, 1, 1, (8, 21, 68), None),
     ("nconv5_upcat_w4", UPCAT_SKIP_FIRST, 16, 8, 3, 1, 1, 1, 1, (8, 26, 72), (8, 13, 36)),
     ("nconv6_upfirst_w4", UPCAT_UP_FIRST, 16, 8, 3, 0, 1, 1, 1, (8, 34, 72), (8, 17, 36)),
+    # 1, 2 and 5 output rows: the row-pair weight gradient's single-row / lone-pair segments
+    ("nconv2_h1", PLAIN, 8, 8, 5, 2, 1, 1, 1, (8, 1, 70), None),
+    ("nconv2_h2", PLAIN, 8, 8, 5, 2, 1, 1, 1, (8, 2, 40), None),
+    ("down_pool_h5", POOL2, 8, 8, 5, 2, 1, 1, 1, (8, 10, 33), None),
     ("generic_3x3_plain", PLAIN, 8, 8, 3, 1, 1, 1, 1, (8, 29, 41), None),
     ("generic_stride2", PLAIN, 4, 6, 3, 1, 2, 1, 1, (4, 29, 41), None),
     ("generic_dil2_groups2", PLAIN, 4, 6, 3, 2, 1, 2, 2, (4, 29, 41), None),
