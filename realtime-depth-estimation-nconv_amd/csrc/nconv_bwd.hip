@@ -1935,9 +1935,10 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(NCONV_WM2_WA
         const int idx = (t * C::NT + u) * 256 + (mm & 3) * 64 + (mm >> 2) * 16 + (n & 15);
         return lds[idx] + lds[C::TILE + idx];
     };
-    for (int e = tid; e < NW; e += kT) {
-        const int kw = e % K, kh = (e / K) % K, i = (e / (K * K)) % CIN, o = e / (K * K * CIN);
-        out[e] = at(kh * CIN + i, kw * COUT + o) + at((kh + 1) * CIN + i, K * COUT + kw * COUT + o);
+    for (int f = tid; f < NW; f += kT) {  // o fastest: a wave's reads spread over the LDS banks
+        const int o = f % COUT, kw = (f / COUT) % K, kh = (f / (COUT * K)) % K, i = f / (COUT * K * K);
+        out[((o * CIN + i) * K + kh) * K + kw] =
+            at(kh * CIN + i, kw * COUT + o) + at((kh + 1) * CIN + i, K * COUT + kw * COUT + o);
     }
 #pragma unroll
     for (int kk = 0; kk < C::OPW; ++kk) {
