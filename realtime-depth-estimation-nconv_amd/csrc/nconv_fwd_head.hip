@@ -47,6 +47,7 @@ constexpr int kFrag = 2 * 3 * 64 * 4;
 // of each column window (mask column c + 8, rows r..r+7) at the same pitch
 constexpr int kLut = 0, kW8R = 4096, kW8C = kW8R + kSH * kSW, kTabEnd = kW8C + kHTH * kSW;
 constexpr int kDP = 8 * 64 + 16;                  // D2 transpose: channel pitch (floats)
+constexpr int kDOff = (kTabEnd + 15) & ~15;       // D2 transpose region, behind the tables (bytes)
 
 typedef const float __attribute__((address_space(4))) cfloat;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -68,7 +69,7 @@ __global__ __launch_bounds__(kHT) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
     __shared__ unsigned long long c0row[kSH];    // c0 per mask row (bits = columns)
     __shared__ unsigned c0col[kSW];              // c0 per mask column (bits = rows)
     __shared__ int tile_nan;                     // a NaN among the staged S * c0 (S NaN or -inf)
-    static_assert(kTabEnd <= (int)sizeof(hp) && 8 * kDP * 4 <= (int)sizeof(hp), "D2 tables fit the plane region");
+    static_assert(kDOff + 8 * kDP * 4 <= (int)sizeof(hp), "D2 tables and transpose fit the plane region");
     const int tid = threadIdx.x;
     const int H = L.Ho, W = L.Wo;
     const TileCoord tc = xcd_tile((W + kHTW - 1) / kHTW, (H + kHTH - 1) / kHTH, L.B);
@@ -115,53 +116,6 @@ __global__ __launch_bounds__(kHT) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
     f2 accN[8], accD[8];
 #pragma unroll
     for (int o = 0; o < 8; ++o) accN[o] = accD[o] = (f2){0.f, 0.f};
-
-    // interior D2 on the matrix cores: wave w's pixels (4w + (nb >> 1), 16 (nb & 1) + n) are the
-    // 16 columns of GEMM block nb; lane (g, n) ends with D2 of channels g (b = 0) and 4 + g (b = 1)
-    float d2v[16];
-    if (interior) {
-        unsigned char* const tb = reinterpret_cast<unsigned char*>(hp);
-        {   // table entry tid: bf16 1.0 where bit j of tid is set
-            unsigned d[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-                d[i] = ((tid >> (2 * i)) & 1u) * 0x3F80u + ((tid >> (2 * i + 1)) & 1u) * 0x3F800000u;
-            reinterpret_cast<uint4*>(tb + kLut)[tid] = make_uint4(d[0], d[1], d[2], d[3]);
-        }
-        for (int e = tid; e < kSH * kSW; e += kHT) {
-            const int r = e / kSW, c = e - r * kSW;
-            tb[kW8R + e] = (unsigned char)(c0row[r] >> c);
-            if (r < kHTH) tb[kW8C + e] = c < kHTW ? (unsigned char)(c0col[c + 8] >> r) : 0;
-        }
-        __syncthreads();
-        const int lane = tid & 63, g = lane >> 4, n = lane & 15;
-        const uint4* fr = reinterpret_cast<const uint4*>(L.waux) + lane;
-        bf16x8 A[2][3];
-#pragma unroll
-        for (int bb = 0; bb < 2; ++bb)
-#pragma unroll
-            for (int ks = 0; ks < 3; ++ks) A[bb][ks] = __builtin_bit_cast(bf16x8, fr[(bb * 3 + ks) * 64]);
-        // byte offsets of this lane's chunk octets for K step ks (pixel (4w, n) + per-block immediates)
-        const int pb = (tid >> 6) * 4 * kSW + n;
-        const int o0 = kW8R + g * kSW + pb, o1 = kW8R + (4 + g) * kSW + pb;
-        const int o2 = g == 0 ? kW8R + 8 * kSW + pb : (g == 1 ? kW8C + pb : kW8R + 8 * kSW + 8 + pb);
-#pragma unroll
-        for (int nb = 0; nb < 8; ++nb) {
-            const int po = (nb >> 1) * kSW + 16 * (nb & 1);
-            const bf16x8 B0 = __builtin_bit_cast(bf16x8, reinterpret_cast<const uint4*>(tb + kLut)[tb[o0 + po]]);
-            const bf16x8 B1 = __builtin_bit_cast(bf16x8, reinterpret_cast<const uint4*>(tb + kLut)[tb[o1 + po]]);
-            const bf16x8 B2 = __builtin_bit_cast(bf16x8, reinterpret_cast<const uint4*>(tb + kLut)[tb[o2 + po]]);
-#pragma unroll
-            for (int bb = 0; bb < 2; ++bb) {
-                f4 acc = (f4){0.f, 0.f, 0.f, 0.f};
-                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[bb][0], B0, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[bb][1], B1, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[bb][2], B2, acc, 0, 0, 0);
-                d2v[bb * 8 + nb] = (acc.x + acc.y) + acc.z;  // hi + mid, then + lo
-            }
-        }
-    }
-    __syncthreads();  // the D2 tables are dead: the region becomes nconv1's planes
 
     // ---- nconv1 on the 20 x 36 halo (origin R0 - 2, C0 - 2), nonzero taps only; writes x * c
     //      (want_c false) or c (want_c true, edge tiles' second pass) into the pair planes ----
@@ -284,14 +238,55 @@ __global__ __launch_bounds__(kHT) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
         __syncthreads();
         sum_planes(accD);
     } else {
-        // the matrix-core D2 from GEMM layout to the thread's pixels (ty, j), (ty, j + 16)
-        float* const dt = reinterpret_cast<float*>(hp);
-        const int lane = tid & 63, g = lane >> 4, n = lane & 15, w = tid >> 6;
+        // interior D2 on the matrix cores, after N2 (no D2 registers live through nconv1 and N2):
+        // the operand tables in the freed plane region, each GEMM block's results straight to the
+        // transpose region behind them, then to the thread's pixels (ty, j), (ty, j + 16). Wave w's
+        // pixels (4w + (nb >> 1), 16 (nb & 1) + n) are the 16 columns of GEMM block nb; lane (g, n)
+        // holds D2 of channels g (bb = 0) and 4 + g (bb = 1)
+        unsigned char* const tb = reinterpret_cast<unsigned char*>(hp);
+        float* const dt = reinterpret_cast<float*>(tb + kDOff);
+        {   // table entry tid: bf16 1.0 where bit j of tid is set
+            unsigned dq[4];
 #pragma unroll
-        for (int bb = 0; bb < 2; ++bb)
+            for (int i = 0; i < 4; ++i)
+                dq[i] = ((tid >> (2 * i)) & 1u) * 0x3F80u + ((tid >> (2 * i + 1)) & 1u) * 0x3F800000u;
+            reinterpret_cast<uint4*>(tb + kLut)[tid] = make_uint4(dq[0], dq[1], dq[2], dq[3]);
+        }
+        for (int e = tid; e < kSH * kSW; e += kHT) {
+            const int r = e / kSW, c = e - r * kSW;
+            tb[kW8R + e] = (unsigned char)(c0row[r] >> c);
+            if (r < kHTH) tb[kW8C + e] = c < kHTW ? (unsigned char)(c0col[c + 8] >> r) : 0;
+        }
+        __syncthreads();
+        {
+            const int lane = tid & 63, g = lane >> 4, n = lane & 15, w = tid >> 6;
+            const uint4* fr = reinterpret_cast<const uint4*>(L.waux) + lane;
+            bf16x8 A[2][3];
 #pragma unroll
-            for (int nb = 0; nb < 8; ++nb)
-                dt[(4 * bb + g) * kDP + (4 * w + (nb >> 1)) * kHTW + 16 * (nb & 1) + n] = d2v[bb * 8 + nb];
+            for (int bb = 0; bb < 2; ++bb)
+#pragma unroll
+                for (int ks = 0; ks < 3; ++ks) A[bb][ks] = __builtin_bit_cast(bf16x8, fr[(bb * 3 + ks) * 64]);
+            // byte offsets of this lane's chunk octets for K step ks (pixel (4w, n) + per-block immediates)
+            const int pb = w * 4 * kSW + n;
+            const int o0 = kW8R + g * kSW + pb, o1 = kW8R + (4 + g) * kSW + pb;
+            const int o2 = g == 0 ? kW8R + 8 * kSW + pb : (g == 1 ? kW8C + pb : kW8R + 8 * kSW + 8 + pb);
+#pragma unroll
+            for (int nb = 0; nb < 8; ++nb) {
+                const int po = (nb >> 1) * kSW + 16 * (nb & 1);
+                const bf16x8 B0 = __builtin_bit_cast(bf16x8, reinterpret_cast<const uint4*>(tb + kLut)[tb[o0 + po]]);
+                const bf16x8 B1 = __builtin_bit_cast(bf16x8, reinterpret_cast<const uint4*>(tb + kLut)[tb[o1 + po]]);
+                const bf16x8 B2 = __builtin_bit_cast(bf16x8, reinterpret_cast<const uint4*>(tb + kLut)[tb[o2 + po]]);
+#pragma unroll
+                for (int bb = 0; bb < 2; ++bb) {
+                    f4 acc = (f4){0.f, 0.f, 0.f, 0.f};
+                    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[bb][0], B0, acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[bb][1], B1, acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[bb][2], B2, acc, 0, 0, 0);
+                    dt[(4 * bb + g) * kDP + (4 * w + (nb >> 1)) * kHTW + 16 * (nb & 1) + n] =
+                        (acc.x + acc.y) + acc.z;  // hi + mid, then + lo
+                }
+            }
+        }
         __syncthreads();
 #pragma unroll
         for (int o = 0; o < 8; ++o) accD[o] = (f2){dt[o * kDP + ty * kHTW + j], dt[o * kDP + ty * kHTW + j + 16]};
