@@ -169,11 +169,15 @@ __global__ __launch_bounds__(kPT) void fwd_phase(LayerDev d, float* __restrict__
             ts.store(tile, xa, ca, 0.f);
             __syncthreads();
             ts.load(native_src<MODE>(d, b, ci + 2 < kPCA ? ci + 2 : kPCA - 1), xa, ca);
+#ifndef NCONV_PHASE_PROBE_NO_NATIVE  // timing probe only (wrong results): no native-half FMAs
             fma_native(ci, 0);
+#endif
             ts.store(tile + kStride, xb, cb, 0.f);
             __syncthreads();
             ts.load(native_src<MODE>(d, b, ci + 3 < kPCA ? ci + 3 : kPCA - 1), xb, cb);
+#ifndef NCONV_PHASE_PROBE_NO_NATIVE
             fma_native(ci + 1, 1);
+#endif
         }
     }
 #pragma unroll 1
@@ -181,11 +185,15 @@ __global__ __launch_bounds__(kPT) void fwd_phase(LayerDev d, float* __restrict__
         ls.store(low, lx0, lc0_);
         __syncthreads();
         ls.load(d, b, ci + 2 < kPCB ? ci + 2 : kPCB - 1, lx0, lc0_);
+#ifndef NCONV_PHASE_PROBE_NO_UP  // timing probe only (wrong results): no upsampled-half FMAs
         fma_up(ci, 0);
+#endif
         ls.store(low + kPLStride, lx1, lc1);
         __syncthreads();
         ls.load(d, b, ci + 3 < kPCB ? ci + 3 : kPCB - 1, lx1, lc1);
+#ifndef NCONV_PHASE_PROBE_NO_UP
         fma_up(ci + 1, 1);
+#endif
     }
 
     // ---- epilogue ----
