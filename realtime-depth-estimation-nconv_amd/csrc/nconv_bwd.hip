@@ -2005,17 +2005,28 @@ static size_t wg_blocks(const nconv_layer& L) {
 }
 
 // wgrad_mfma grid: 64-wide q strips (q = ow + kw spans Wo + K - 1 columns) x row segments x images,
-// at most `target` workgroups. The launch asks for two resident rounds of its instantiation (CUs x
-// blocks per CU x 2: a third, nearly empty round cost nconv2's weight gradient a third of its time
-// with a fixed 2048-block target); the workspace is sized for the largest possible occupancy.
-constexpr int kMfmaRounds = 2, kMfmaMaxPerCu = 4;
+// at most `target` workgroups: NCONV_WM_ROUNDS resident rounds of the instantiation (CUs x blocks
+// per CU x rounds; a third, nearly empty round once cost nconv2's weight gradient a third of its
+// time). One round (longer row segments: less per-block prologue, fewer partial rows) for the
+// weight gradients that share the CUs with the input-gradient chain, two for the tail's (T7), which
+// starts the side stream: graphed training step 2.104 -> 2.064 ms same box (one round everywhere
+// 2.093, the tail alone at one round 2.137; profiles/r6_ab_wgrad_rounds.log). The workspace is
+// sized for the larger round count at the largest possible occupancy (kMfmaRoundsMax).
+#ifndef NCONV_WM_ROUNDS
+#define NCONV_WM_ROUNDS 1
+#endif
+#ifndef NCONV_WM_T7_ROUNDS
+#define NCONV_WM_T7_ROUNDS 2
+#endif
+constexpr int kMfmaRounds = NCONV_WM_ROUNDS, kMfmaMaxPerCu = 4;
+constexpr int kMfmaRoundsMax = NCONV_WM_T7_ROUNDS > NCONV_WM_ROUNDS ? NCONV_WM_T7_ROUNDS : NCONV_WM_ROUNDS;
 struct WmGrid {
     int nstrip, nseg, seg_rows;
     size_t nblk;
 };
 static int device_cus() { return dev_cus(); }
 static WmGrid wm_grid(const nconv_layer& L, int target = 0) {
-    if (target <= 0) target = kMfmaRounds * kMfmaMaxPerCu * device_cus();  // workspace bound
+    if (target <= 0) target = kMfmaRoundsMax * kMfmaMaxPerCu * device_cus();  // workspace bound (every variant)
     WmGrid g;
     g.nstrip = (L.Wo + L.KW - 1 + 63) / 64;
     const int per_img = g.nstrip * L.B;
@@ -2144,7 +2155,7 @@ static int go_bwd_tiled(const LayerDev& d, const BwdArgs& a, float* part, float*
             }
             const int per_cu = dev_occupancy((const void*)wgrad_mfma<CIN, COUT, K, MODE, GP, T7>, kT, 0);
             const int resident = device_cus() * (per_cu < kMfmaMaxPerCu ? per_cu : kMfmaMaxPerCu);
-            const WmGrid g = wm_grid(L, kMfmaRounds * resident);
+            const WmGrid g = wm_grid(L, (T7 ? NCONV_WM_T7_ROUNDS : kMfmaRounds) * resident);
             hipLaunchKernelGGL((wgrad_mfma<CIN, COUT, K, MODE, GP, T7>), dim3(g.nblk), dim3(kT), 0, st, d, a, part,
                                g.nstrip, g.nseg, g.seg_rows);
             if constexpr (T7) {  // nconv7's weight-gradient partial rows: one per wgrad workgroup
