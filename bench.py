@@ -91,6 +91,8 @@ def parse(argv=None):
     p.add_argument("--inference-shares", default=None, type=_shares,
                    help="DNET.inference_shares: relative frames per inference stream, e.g. 5,3 (one positive "
                         "number per stream of --inference-streams, default 2)")
+    p.add_argument("--guided-alt-math", default="fp32,bf16x6", type=lambda v: [x for x in v.split(",") if x],
+                   help="also time configs 3 / 4 (graphed) with these dense maths (separately labelled)")
     p.add_argument("--guided-train-graph", type=int, default=1,
                    help="replay the config-4 guided training step from a hipGraph (1) or eager (0)")
     p.add_argument("--head-density", type=float, default=0.40,
@@ -555,6 +557,16 @@ def cpu_baseline(B, H, W, seconds):
 
 
 # ---- guided configs ---------------------------------------------------------------------------------
+# the arithmetic of the guided model's 3x3 stride-1 convolutions (dense.MATH; other kinds: fp32 MFMA)
+DENSE_ARITH = {
+    "bf16x9": "exact products on the bf16 matrix cores (three-part split operands, all nine partial "
+              "products, fp32 accumulation); other convolution kinds fp32 MFMA",
+    "fp32": "v_mfma_f32_32x32x2_f32 (exact fp32 products, fp32 accumulation) for every convolution",
+    "bf16x6": "the six largest split-bf16 partial products (each product within ~2^-23 relative), "
+              "fp32 accumulation; other convolution kinds fp32 MFMA",
+}
+
+
 def guided_forward(m, dev, B, H, W, steps, warmup, rank):
     """Config 3: SETP2 (RGB-guided, models/step2.py:80-126) forward on B/2 + B/2 frames per GPU,
     eval, hipGraph-captured; step 1 and every dense convolution on libnconv kernels. Returns the
@@ -850,9 +862,25 @@ def main():
         guided = {"frames_per_sec": round(world * B * gsteps / el, 2), "ms_per_step": round(el / gsteps * 1e3, 3),
                   "steps": gsteps, "frames_per_step": B * world,
                   "workload": "config3: SETP2_BP_EXPORT forward, B/2+B/2 frames per GPU, hipGraph",
+                  "dense_math": m.dense.MATH, "arith": DENSE_ARITH[m.dense.MATH],
                   "fp32_tflops": round(fl / (el / gsteps) / 1e12, 2),
                   "fp32_mfma_frac": round(fl / (el / gsteps) / 1e12 / FP32_PEAK_TFLOPS, 4)}
         torch.cuda.empty_cache()
+        if world == 1:  # the other dense maths, separately labelled
+            base = m.dense.MATH
+            guided["other_dense_math"] = {}
+            for mm in a.guided_alt_math:
+                if mm == base:
+                    continue
+                m.dense.MATH = mm
+                try:
+                    el2 = guided_forward(m, dev, B, H, W, gsteps, min(a.warmup, 3), rank)
+                finally:
+                    m.dense.MATH = base
+                guided["other_dense_math"][mm] = {"ms_per_step": round(el2 / gsteps * 1e3, 3),
+                                                  "frames_per_sec": round(B * gsteps / el2, 2),
+                                                  "arith": DENSE_ARITH[mm]}
+                torch.cuda.empty_cache()
 
     # ---- config 4: guided training step ----
     guided_train = None
@@ -883,6 +911,7 @@ def main():
                         "workload": "config4: SETP2_BP_TRAIN fwd+bwd+AdamW, B/2+B/2 frames per GPU, "
                                     + ("hipGraph" if gmode else "eager"),
                         "mode": "hipgraph" if gmode else "eager",
+                        "dense_math": m.dense.MATH, "arith": DENSE_ARITH[m.dense.MATH],
                         "fp32_tflops": round(fl / (tt / gts) / 1e12, 2),
                         "fp32_mfma_frac": round(fl / (tt / gts) / 1e12 / FP32_PEAK_TFLOPS, 4)}
         if gmode and world == 1:  # the eager step beside it
@@ -890,6 +919,21 @@ def main():
             te = time_guided_train(False)
             guided_train["eager"] = {"frames_per_sec": round(world * B * gts / te, 2),
                                      "ms_per_step": round(te / gts * 1e3, 3)}
+        if gmode and world == 1:  # the other dense maths (graphed), separately labelled
+            base = m.dense.MATH
+            guided_train["other_dense_math"] = {}
+            for mm in a.guided_alt_math:
+                if mm == base:
+                    continue
+                log(f"config 4 guided training step, dense math {mm}")
+                m.dense.MATH = mm
+                try:
+                    t2 = time_guided_train(True)
+                finally:
+                    m.dense.MATH = base
+                guided_train["other_dense_math"][mm] = {"ms_per_step": round(t2 / gts * 1e3, 3),
+                                                        "frames_per_sec": round(B * gts / t2, 2),
+                                                        "arith": DENSE_ARITH[mm]}
 
     # ---- per-kernel times, rooflines, CPU baseline (rank 0) ----
     if rank == 0:

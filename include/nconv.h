@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define NCONV_ABI_VERSION 21
+#define NCONV_ABI_VERSION 22
 
 /* How a layer's input (data x, confidence c) is produced from its source tensors. These are the
  * DNET glue ops fused into the layer's load stage (models/step1.py:53,61-90). */
@@ -381,9 +381,24 @@ typedef struct nconv_dense_conv {
     const float* wshort;       /* optional packed 1x1 shortcut (same stride) added after the ReLU  */
     float* out;                /* output channels [out_c0, out_c0 + Cout) of (B, out_C, Ho, Wo)    */
     int out_C, out_c0;
+    int math;                  /* enum nconv_dense_math (ABI 22; 0 = fp32 MFMA)                     */
 } nconv_dense_conv;
 
-/* Floats of a packed weight buffer for (kind, Cin, Cout). */
+/* Arithmetic of the 3x3 stride-1 convolutions without shortcut (the RGB encoder's and fusion
+ * decoder's ConvBlocks and their input gradients); every other kind runs NCONV_DENSE_MATH_FP32.
+ * Both split forms sum in fp32 on the matrix cores in another order than the fp32-MFMA kernel (an
+ * fmaf chain), so results agree with it to fp32 accumulation error, not bitwise. */
+enum nconv_dense_math {
+    NCONV_DENSE_MATH_FP32 = 0,  /* v_mfma_f32_32x32x2_f32: exact f32 products                      */
+    NCONV_DENSE_MATH_BF16X9 = 2,/* exact products on the bf16 matrix cores: both operands split into
+                                   three bf16 parts (an exact decomposition), all nine partial
+                                   products (each exact in fp32) accumulated in fp32              */
+    NCONV_DENSE_MATH_BF16X6 = 3 /* the six largest of those nine terms: each product within
+                                   ~2^-23 relative (the dropped v1*w2 + v2*w1 + v2*w2)             */
+};
+
+/* Floats of a packed weight buffer for (kind, Cin, Cout) (3x3: the fp32 image, then the
+ * pre-split bf16 image of the split-bf16 maths, ABI 22). */
 size_t nconv_dense_packed_floats(int kind, int Cin, int Cout);
 
 /* Pack w — Conv2d (Cout, Cin, k, k) or ConvTranspose2d (Cin, Cout, 4, 4) — into the kernel's

@@ -13,7 +13,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # NCONV_LIB: an alternative build of the same library (kernel-tuning experiments)
 LIB_PATH = os.environ.get("NCONV_LIB") or os.path.join(_HERE, "libnconv.so")
-ABI_VERSION = 21
+ABI_VERSION = 22
 BWD_ACCUMULATE = 1
 BWD_DEFER_REDUCE = 2
 BWD_SEPARATE = 4  # accepted and ignored since ABI 21 (include/nconv.h)
@@ -28,6 +28,8 @@ KERNEL_TILED_FP32_PHASE = 5
 KERNEL_NAMES = ("generic", "tiled_fp32", "mfma_fp32", "mfma_bf16x3", "mfma_bf16x9", "tiled_fp32_phase")
 # enum nconv_dense_kind
 DENSE_3X3, DENSE_1X1, DENSE_TRANSPOSED_4X4, DENSE_CONV4X4_S2 = 0, 1, 2, 3
+# enum nconv_dense_math
+DENSE_MATHS = {"fp32": 0, "bf16x9": 2, "bf16x6": 3}
 
 EXPORTED = (
     "nconv_abi_version",
@@ -103,7 +105,8 @@ class NconvDenseConv(ctypes.Structure):
                 ("Cout", ctypes.c_int), ("Ho", ctypes.c_int), ("Wo", ctypes.c_int),
                 ("kind", ctypes.c_int), ("stride", ctypes.c_int), ("wpack", ctypes.c_void_p),
                 ("bias", ctypes.c_void_p), ("relu", ctypes.c_int), ("wshort", ctypes.c_void_p),
-                ("out", ctypes.c_void_p), ("out_C", ctypes.c_int), ("out_c0", ctypes.c_int)]
+                ("out", ctypes.c_void_p), ("out_C", ctypes.c_int), ("out_c0", ctypes.c_int),
+                ("math", ctypes.c_int)]
 
 
 class NconvDenseWgrad(ctypes.Structure):

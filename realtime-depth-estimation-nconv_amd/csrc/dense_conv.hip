@@ -280,6 +280,199 @@ __global__ __launch_bounds__(kDT) void dense_conv_mfma(nconv_dense_conv p, int n
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// 3x3 stride-1 convolution with exact products on the bf16 matrix cores (NCONV_DENSE_MATH_BF16X9;
+// NCONV_DENSE_MATH_BF16X6: the six largest partial products).
+// Every fp32 operand v is split into three bf16 parts v = v0 + v1 + v2 (v0 = bf16(v),
+// v1 = bf16(v - v0), v2 = v - v0 - v1: at most 8 significant bits, exact), so each of the nine
+// partial products vi*wj is exact in fp32 and their sum is v*w exactly; the only rounding is the
+// fp32 accumulation, as in the fp32-MFMA kernel above (which is an fmaf chain, bitwise; this one
+// sums in another order, so results agree to fp32 accumulation error, not bitwise). Nine
+// v_mfma_f32_32x32x16_bf16 (32 cycles each) per 32x32x16 block against eight
+// v_mfma_f32_32x32x2_f32 (64 cycles each): 288 against 512 cycles.
+// GEMM as above (A = weights, B = patch, C[co][pixel]), with k = (tap pair, 8 input channels): a
+// k-step takes taps 2s (lane half 0) and 2s + 1 (lane half 1) of one 8-channel chunk; the tenth
+// tap is zero (A rows zero, B fragment zeroed). LDS images, every fragment one ds_read_b128 of 32
+// consecutive 16-byte entries:
+//   patch   [part 3][position PR x PC][8 channels]         (bf16x8 per position and part)
+//   weights [k-step 5][part 3][lane half 2][co COUT][8 ci]  (bf16x8 per row)
+// ------------------------------------------------------------------------------------------------
+typedef __bf16 dbf16x8 __attribute__((ext_vector_type(8)));
+
+template <int COUT>
+struct Db9Cfg {  // (16 rows for the 32-channel tiles, 2 waves/SIMD: not faster)
+    static constexpr int TH = 8, RW = TH / 4, TW = 32, MT = COUT / 32;
+    static constexpr int PR = TH + 2, PC = TW + 2, ROW = PC, NPOS = PR * PC;
+    static constexpr int PLANEB = NPOS * 16;                         // bytes of one part's image
+    static constexpr int DUMP = 3 * PLANEB;                          // slot of positions past the tile
+    static constexpr int WOFF = DUMP + 3 * 16;                       // weight image (bytes)
+    static constexpr int WROWS = 5 * 3 * 2 * COUT;                   // 16-byte rows per chunk
+    static constexpr int NWL = (WROWS + kDT - 1) / kDT;              // rows per thread (the last
+    static constexpr int LDSB = WOFF + NWL * kDT * 16;               //  round's excess: zeros, past the image)
+    static constexpr int NPP = (NPOS + kDT - 1) / kDT;               // positions per thread
+};
+typedef unsigned du4 __attribute__((ext_vector_type(4)));
+
+// v (8 lanes) -> three bf16x8 parts summing to v exactly
+__device__ __forceinline__ void dsplit3(const float (&v)[8], dbf16x8 (&o)[3]) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const __bf16 h0 = (__bf16)v[j];
+        const float r1 = v[j] - (float)h0;
+        const __bf16 h1 = (__bf16)r1;
+        o[0][j] = h0;
+        o[1][j] = h1;
+        o[2][j] = (__bf16)(r1 - (float)h1);
+    }
+}
+
+#ifndef NCONV_DB9_KUNROLL
+#define NCONV_DB9_KUNROLL 5  // k-steps per unrolled body (1: 4 % slower)
+#endif
+#ifndef NCONV_DB9_WAVES64
+#define NCONV_DB9_WAVES64 2
+#endif
+#ifndef NCONV_DB9_WAVES32
+#define NCONV_DB9_WAVES32 3
+#endif
+template <int COUT, int NTERM>
+__global__ __launch_bounds__(kDT) __attribute__((amdgpu_waves_per_eu(COUT == 64 ? NCONV_DB9_WAVES64 : NCONV_DB9_WAVES32)))
+void dense_conv_bf9(nconv_dense_conv p, int ntx, int nty, int ncot) {
+    using C = Db9Cfg<COUT>;
+    __shared__ __attribute__((aligned(16))) unsigned char lds[C::LDSB];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    int blk = blockIdx.x;
+    const int tx = blk % ntx;
+    blk /= ntx;
+    const int ty = blk % nty;
+    blk /= nty;
+    const int cot = blk % ncot;
+    const int b = blk / ncot;
+    const int oy0 = ty * C::TH, ox0 = tx * C::TW;
+    const int iy0 = oy0 - 1, ix0 = ox0 - 1;
+    const int Cin = p.C0 + p.C1;
+    const int nchunk = (Cin + kCK - 1) / kCK;
+    const int HW = p.H * p.W;
+
+    constexpr unsigned OOB = 0x80000000u;
+    unsigned poff[C::NPP];
+#pragma unroll
+    for (int k = 0; k < C::NPP; ++k) {
+        const int e = tid + kDT * k;
+        const int r = e / C::PC, c = e - r * C::PC;
+        const int iy = iy0 + r, ix = ix0 + c;
+        const bool in = e < C::NPOS && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
+        poff[k] = in ? (unsigned)(iy * p.W + ix) * 4u : OOB;
+    }
+    const int bytes0 = p.C0 * HW * 4, bytes1 = p.C1 * HW * 4;
+    // the pre-split weight image of (cot, chunk) behind the fp32 one (nconv_dense_pack)
+    const unsigned char* wimg = reinterpret_cast<const unsigned char*>(p.wpack + (size_t)ncot * nchunk * 9 * kCK * COUT) +
+                                (size_t)cot * nchunk * C::WROWS * 16;
+    float pv[C::NPP][8];
+    du4 wv[C::NWL];
+    auto load_chunk = [&](int ch) {
+        const int g0 = ch * kCK;
+        const bool a = g0 < p.C0;
+        const float* base = a ? p.x0 + ((size_t)b * p.C0 + g0) * HW : p.x1 + ((size_t)b * p.C1 + (g0 - p.C0)) * HW;
+        const int nbytes = a ? bytes0 - g0 * HW * 4 : bytes1 - (g0 - p.C0) * HW * 4;
+        const __amdgpu_buffer_rsrc_t rs = plane_rsrc(base, nbytes);
+#pragma unroll
+        for (int k = 0; k < C::NPP; ++k)
+#pragma unroll
+            for (int c = 0; c < 8; ++c) pv[k][c] = ld_f32s(rs, poff[k], c * HW * 4);
+        const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(wimg + (size_t)ch * C::WROWS * 16), (short)0, C::WROWS * 16, 0x00020000);
+#pragma unroll
+        for (int k = 0; k < C::NWL; ++k) wv[k] = __builtin_amdgcn_raw_buffer_load_b128(rw, (tid + kDT * k) * 16, 0, 0);
+    };
+    auto store_chunk = [&]() {
+#pragma unroll
+        for (int k = 0; k < C::NPP; ++k) {
+            const int e = tid + kDT * k;
+            dbf16x8 sp[3];
+            dsplit3(pv[k], sp);
+            const bool in = e < C::NPOS;  // past the tile: the dump slots (no branch)
+            const int a = in ? e * 16 : C::DUMP, da = in ? C::PLANEB : 16;
+#pragma unroll
+            for (int i = 0; i < 3; ++i) *reinterpret_cast<dbf16x8*>(lds + a + i * da) = sp[i];
+        }
+#pragma unroll
+        for (int k = 0; k < C::NWL; ++k) *reinterpret_cast<du4*>(lds + C::WOFF + (tid + kDT * k) * 16) = wv[k];
+    };
+
+    const int kk = lane >> 5, li = lane & 31;
+    const int abase = C::WOFF + (kk * COUT + li) * 16;
+    const int rb = w * C::RW * C::ROW + li;
+    const int bbaseA = (rb + kk) * 16;               // k-steps 0, 2, 3, 4: tap 2s+1 one column right
+    const int bbaseB = (rb + kk * (C::ROW - 2)) * 16;  // k-step 1: tap 3 = (1, 0), tap 2 = (0, 2)
+
+    f16v acc[C::MT][C::RW];
+#pragma unroll
+    for (int m = 0; m < C::MT; ++m)
+#pragma unroll
+        for (int r = 0; r < C::RW; ++r) acc[m][r] = (f16v){};
+
+    load_chunk(0);
+#pragma unroll 1
+    for (int ch = 0; ch < nchunk; ++ch) {
+        if (ch) __syncthreads();
+        store_chunk();
+        __syncthreads();
+        load_chunk(ch + 1 < nchunk ? ch + 1 : ch);
+#pragma unroll NCONV_DB9_KUNROLL
+        for (int s = 0; s < 5; ++s) {
+            const int t0 = 2 * s, dr = t0 / 3, dc = t0 % 3;
+            const int bb = s == 1 ? bbaseB : bbaseA;
+            dbf16x8 av[3][C::MT], bv[3][C::RW];
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+#pragma unroll
+                for (int m = 0; m < C::MT; ++m)
+                    av[i][m] = *reinterpret_cast<const dbf16x8*>(lds + abase + (s * 3 + i) * 2 * COUT * 16 + 32 * m * 16);
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+#pragma unroll
+                for (int r = 0; r < C::RW; ++r) {
+                    bv[i][r] = *reinterpret_cast<const dbf16x8*>(lds + bb + i * C::PLANEB + ((r + dr) * C::ROW + dc) * 16);
+                    if (s == 4 && kk) bv[i][r] = (dbf16x8){};
+                }
+            // smallest terms first; NTERM 6 (bf16x6) drops the three below 2^-25 |v w|
+            constexpr int ti[9] = {2, 2, 1, 2, 1, 0, 1, 0, 0}, tj[9] = {2, 1, 2, 0, 1, 2, 0, 1, 0};
+#pragma unroll
+            for (int q = 9 - NTERM; q < 9; ++q)
+#pragma unroll
+                for (int m = 0; m < C::MT; ++m)
+#pragma unroll
+                    for (int r = 0; r < C::RW; ++r)
+                        acc[m][r] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[ti[q]][m], bv[tj[q]][r], acc[m][r], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        __syncthreads();  // this chunk's MFMAs are done with the LDS
+    }
+    const int ox = ox0 + li;
+    const int HWo = p.Ho * p.Wo;
+    const int co0 = cot * COUT;
+    const int nco = p.Cout - co0 < COUT ? p.Cout - co0 : COUT;
+    const __amdgpu_buffer_rsrc_t ro = plane_rsrc(p.out + ((size_t)b * p.out_C + p.out_c0 + co0) * HWo, nco * HWo * 4);
+#pragma unroll
+    for (int r = 0; r < C::RW; ++r) {
+        const int oy = oy0 + w * C::RW + r;
+        const bool in = oy < p.Ho && ox < p.Wo;
+        const unsigned lo = in ? (unsigned)(4 * kk * HWo + oy * p.Wo + ox) * 4u : OOB;
+#pragma unroll
+        for (int m = 0; m < C::MT; ++m)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int cr = 32 * m + (q & 3) + 8 * (q >> 2);
+                const int co = co0 + cr + 4 * kk;
+                float v = acc[m][r][q] + ((p.bias && co < p.Cout) ? p.bias[co] : 0.f);
+                if (p.relu) v = fmaxf(v, 0.f);
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), ro, (int)lo, cr * HWo * 4, 0);
+            }
+    }
+}
+
 // ---- weight packing: (Cout, Cin, kh, kw) [conv] / (Cin, Cout, 4, 4) [transposed] ->
 //      [class][cout tile][chunk][tap][ci 8][T], times an optional per-Cout scale (eval
 //      BatchNorm); channels past Cin / Cout are zero ----------------------------------------------
@@ -800,20 +993,69 @@ __global__ __launch_bounds__(256) void dense_wgrad_tr_rows(const float* __restri
 // ------------------------------------------------------------------------------------------------
 // Launchers
 // ------------------------------------------------------------------------------------------------
-size_t dense_packed_floats(int kind, int Cin, int Cout) {
+static size_t dense_fp32_floats(int kind, int Cin, int Cout) {
     const int ncls = kind == NCONV_DENSE_TRANSPOSED_4X4 ? 4 : 1;
     const int T = dense_cout_tile(Cout);
     return (size_t)ncls * ((Cout + T - 1) / T) * ((Cin + kCK - 1) / kCK) * dense_taps(kind) * kCK * T;
 }
+// 3x3: the fp32 image, then dense_conv_bf9's pre-split one ([cot][chunk][k-step][part][half][co]
+// rows of 8 bf16: 30 T rows of 16 bytes = 120 T floats per (cot, chunk))
+static size_t dense_bf9_floats(int kind, int Cin, int Cout) {
+    if (kind != NCONV_DENSE_3X3) return 0;
+    const int T = dense_cout_tile(Cout);
+    return (size_t)((Cout + T - 1) / T) * ((Cin + kCK - 1) / kCK) * 120 * T;
+}
+size_t dense_packed_floats(int kind, int Cin, int Cout) {
+    return dense_fp32_floats(kind, Cin, Cout) + dense_bf9_floats(kind, Cin, Cout);
+}
+
+// one 16-byte row (8 input channels) of the pre-split image per thread: row = ((cot * nchunk + ch)
+// * 5 + s) * 3 + part) * 2 + half) * T + co, tap 2s + half (the tenth tap: zeros)
+__global__ __launch_bounds__(kDT) void dense_pack_bf9(int Cin, int Cout, int T, const float* w, const float* scale,
+                                                      unsigned char* img, size_t rows) {
+    const int nchunk = (Cin + kCK - 1) / kCK;
+    for (size_t e = (size_t)blockIdx.x * kDT + threadIdx.x; e < rows; e += (size_t)gridDim.x * kDT) {
+        const int co = (int)(e % T);
+        size_t r = e / T;
+        const int kk = (int)(r % 2);
+        r /= 2;
+        const int part = (int)(r % 3);
+        r /= 3;
+        const int s = (int)(r % 5);
+        r /= 5;
+        const int ch = (int)(r % nchunk);
+        const int cot = (int)(r / nchunk);
+        const int tap = 2 * s + kk, o = cot * T + co;
+        float v[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const int ci = ch * kCK + c;
+            v[c] = 0.f;
+            if (tap < 9 && ci < Cin && o < Cout) {
+                v[c] = w[((size_t)o * Cin + ci) * 9 + tap];
+                if (scale) v[c] *= scale[o];  // the fp32 image's value, then split
+            }
+        }
+        dbf16x8 sp[3];
+        dsplit3(v, sp);
+        *reinterpret_cast<dbf16x8*>(img + e * 16) = part == 0 ? sp[0] : part == 1 ? sp[1] : sp[2];
+    }
+}
 
 int launch_dense_pack(int kind, int Cin, int Cout, const float* w, const float* scale, float* wp, hipStream_t st,
                       const char** why) {
-    const size_t n = dense_packed_floats(kind, Cin, Cout);
+    const size_t n = dense_fp32_floats(kind, Cin, Cout);
     size_t blocks = (n + kDT - 1) / kDT;
     if (blocks > 4096) blocks = 4096;
     if (blocks)
         hipLaunchKernelGGL(dense_pack, dim3(blocks), dim3(kDT), 0, st, kind, Cin, Cout, dense_cout_tile(Cout), w,
                            scale, wp);
+    if (const size_t rows = dense_bf9_floats(kind, Cin, Cout) / 4) {
+        size_t b9 = (rows + kDT - 1) / kDT;
+        if (b9 > 4096) b9 = 4096;
+        hipLaunchKernelGGL(dense_pack_bf9, dim3(b9), dim3(kDT), 0, st, Cin, Cout, dense_cout_tile(Cout), w, scale,
+                           reinterpret_cast<unsigned char*>(wp + n), rows);
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         *why = hipGetErrorString(e);
@@ -837,9 +1079,34 @@ static void go_dense(const nconv_dense_conv& p, hipStream_t st) {
                            nty, ncot);
 }
 
+// p.math BF16X9 / BF16X6: the 3x3 stride-1 convolutions without shortcut (and whose chunks do
+// not straddle the two sources) on dense_conv_bf9; every other shape keeps the fp32 MFMA kernel
+template <int COUT, int NTERM>
+static void go_dense_bf9(const nconv_dense_conv& p, hipStream_t st) {
+    using C = Db9Cfg<COUT>;
+    const int ntx = (p.Wo + C::TW - 1) / C::TW, nty = (p.Ho + C::TH - 1) / C::TH;
+    const int ncot = (p.Cout + COUT - 1) / COUT;
+    hipLaunchKernelGGL((dense_conv_bf9<COUT, NTERM>), dim3(ntx * nty * ncot * p.B), dim3(kDT), 0, st, p, ntx, nty,
+                       ncot);
+}
+
 int launch_dense_conv(const nconv_dense_conv& p, hipStream_t st, const char** why) {
     const bool sc = p.wshort != nullptr;
     const int co = dense_cout_tile(p.Cout);
+    if (p.math != NCONV_DENSE_MATH_FP32 && p.kind == NCONV_DENSE_3X3 && p.stride == 1 && !sc &&
+        !(p.C1 > 0 && p.C0 % kCK != 0)) {
+        const int nt = p.math == NCONV_DENSE_MATH_BF16X9 ? 9 : 6;
+        if (co == 32)
+            nt == 9 ? go_dense_bf9<32, 9>(p, st) : go_dense_bf9<32, 6>(p, st);
+        else
+            nt == 9 ? go_dense_bf9<64, 9>(p, st) : go_dense_bf9<64, 6>(p, st);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) {
+            *why = hipGetErrorString(e);
+            return -5;
+        }
+        return 0;
+    }
 #define NCONV_DC(COUT_, KIND_, S_, SC_)                                                   \
     if (co == COUT_ && p.kind == KIND_ && p.stride == S_ && sc == SC_) {                  \
         go_dense<COUT_, KIND_, S_, SC_>(p, st);                                             \

@@ -471,6 +471,8 @@ int nconv_dense_conv_fwd(const nconv_dense_conv* c, void* stream) {
     if (c->Cout <= 0) return fail(-22, fn, "non-positive Cout");
     if (!c->wpack || !c->out) return fail(-22, fn, "null weight / output pointer");
     if (c->out_c0 < 0 || c->out_c0 + c->Cout > c->out_C) return fail(-22, fn, "output channel range exceeds out_C");
+    if (c->math != NCONV_DENSE_MATH_FP32 && c->math != NCONV_DENSE_MATH_BF16X9 && c->math != NCONV_DENSE_MATH_BF16X6)
+        return fail(-22, fn, "unknown math");
     int ho, wo;
     switch (c->kind) {
         case NCONV_DENSE_3X3:

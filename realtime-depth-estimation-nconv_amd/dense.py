@@ -21,6 +21,14 @@ from . import _lib
 from ._lib import DENSE_1X1, DENSE_3X3, DENSE_CONV4X4_S2, DENSE_TRANSPOSED_4X4  # noqa: F401  (re-exported)
 
 
+# Arithmetic of the 3x3 stride-1 convolutions (include/nconv.h enum nconv_dense_math): "bf16x9"
+# (default: exact products on the bf16 matrix cores -- three-part split operands, all nine partial
+# products, fp32 accumulation), "fp32" (v_mfma_f32_32x32x2_f32, exact products, an fmaf chain), or
+# "bf16x6" (the six largest partial products: each product within ~2^-23 relative; opt-in,
+# reported separately). Other convolution kinds always run the fp32 MFMA kernels.
+MATH = os.environ.get("NCONV_DENSE_MATH", "bf16x9")
+
+
 def bn_fold(bn, conv_bias=None):
     """Eval BatchNorm after a convolution as (scale, shift): bn(conv(x) + b) = scale*conv(x) + shift."""
     scale = bn.weight / torch.sqrt(bn.running_var + bn.eps)
@@ -73,6 +81,7 @@ def conv(x0, kind, stride, wpack, bias, relu, cout, x1=None, wshort=None, out=No
     d.relu = 1 if relu else 0
     d.wshort = wshort.data_ptr() if wshort is not None else None
     d.out, d.out_C, d.out_c0 = out.data_ptr(), out.shape[1], out_c0
+    d.math = _lib.DENSE_MATHS[MATH]
     if B == 0:
         return out
     _lib.check(_lib.lib().nconv_dense_conv_fwd(ctypes.byref(d), _lib.stream_handle(x0.device)),

@@ -28,6 +28,7 @@ int main(void) {
     F(nconv_dense_conv, Ho); F(nconv_dense_conv, Wo); F(nconv_dense_conv, kind); F(nconv_dense_conv, stride);
     F(nconv_dense_conv, wpack); F(nconv_dense_conv, bias); F(nconv_dense_conv, relu); F(nconv_dense_conv, wshort);
     F(nconv_dense_conv, out); F(nconv_dense_conv, out_C); F(nconv_dense_conv, out_c0);
+    F(nconv_dense_conv, math);
     S(nconv_dense_wgrad);
     F(nconv_dense_wgrad, B); F(nconv_dense_wgrad, kind); F(nconv_dense_wgrad, stride); F(nconv_dense_wgrad, x0);
     F(nconv_dense_wgrad, C0); F(nconv_dense_wgrad, x1); F(nconv_dense_wgrad, C1); F(nconv_dense_wgrad, H);

@@ -127,3 +127,58 @@ def test_bilinear_down_matches_cpu_interpolate(nconv_amd, gpu, H, W, k):
     assert (got - ref).abs().max().item() <= 2e-5  # two fp32 ulps at 64..80
     if (H, W) in ((352, 1216), (480, 640)):
         assert torch.equal(got, ref)
+
+
+@pytest.mark.parametrize("math", ["fp32", "bf16x9", "bf16x6"])
+@pytest.mark.parametrize("cout,c0,c1,H,W", [
+    (32, 16, 0, 13, 37),     # one source, ragged tile edges
+    (64, 64, 64, 20, 70),    # 128 -> 64 from two sources (UpCat conv)
+    (40, 24, 0, 11, 45),     # Cout padded to the 64-channel tile
+    (96, 32, 8, 9, 33),      # three 32-channel tiles
+    (32, 1, 0, 9, 33),       # depth_conv (1 input channel)
+    (64, 8, 16, 17, 65),     # source boundary on a chunk boundary
+])
+def test_dense_3x3_split_maths(nconv_amd, gpu, math, monkeypatch, cout, c0, c1, H, W):
+    """The 3x3 stride-1 convolution under each nconv_dense_math against float64, element-wise:
+    |gpu - ref| <= 1e-6 * (|x| conv |w| + |bias|)  (fp32 accumulation of exact products, and bf16x6's
+    dropped terms <= ~2^-23 of each product, both far inside; a wrong or missing term is not).
+    The split maths also agree with the fp32-MFMA kernel to the same bound."""
+    D = nconv_amd.dense
+    g = torch.Generator().manual_seed(11 + cout + c0)
+    B, cin = 2, c0 + c1
+    r32 = lambda t: t.float().double()  # the operands the GPU sees
+    x0, x1 = r32(_rand(g, B, c0, H, W)), (r32(_rand(g, B, c1, H, W)) if c1 else None)
+    x = torch.cat([x0, x1], 1) if c1 else x0
+    w = r32(_rand(g, cout, cin, 3, 3) * 0.1)
+    bias = r32(_rand(g, cout))
+    ref = F.conv2d(x, w, padding=1) + bias.view(1, -1, 1, 1)
+    bound = 1e-6 * (F.conv2d(x.abs(), w.abs(), padding=1) + bias.abs().view(1, -1, 1, 1)) + 1e-12
+    f = lambda t: None if t is None else t.to(gpu, torch.float32).contiguous()
+    outs = {}
+    for m in ("fp32", math):
+        monkeypatch.setattr(D, "MATH", m)
+        wp = D.pack(0, f(w), cin, cout)
+        outs[m] = D.conv(f(x0), 0, 1, wp, f(bias), False, cout, x1=f(x1)).double().cpu()
+    got = outs[math]
+    err = (got - ref).abs()
+    assert (err <= bound).all(), f"{math}: worst err/bound {(err / bound).max().item():.3g}"
+    assert ((got - outs["fp32"]).abs() <= 2 * bound).all()
+
+
+@pytest.mark.parametrize("math", ["bf16x9", "bf16x6"])
+def test_dense_3x3_split_maths_nan_spread(nconv_amd, gpu, math, monkeypatch):
+    """A NaN input pixel makes exactly its 3x3 neighbourhood NaN in every output channel, as in the
+    fp32 kernel: the padded tenth tap (zero weights) reads no data (its fragment is zeroed)."""
+    D = nconv_amd.dense
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(1, 16, 12, 40, generator=g)
+    x[0, 3, 5, 31] = float("nan")
+    x[0, 0, 0, 0] = float("nan")
+    w = torch.randn(32, 16, 3, 3, generator=g) * 0.1
+    nan = {}
+    for m in ("fp32", math):
+        monkeypatch.setattr(D, "MATH", m)
+        out = D.conv(x.to(gpu), 0, 1, D.pack(0, w.to(gpu), 16, 32), None, False, 32)
+        nan[m] = torch.isnan(out).cpu()
+    assert torch.equal(nan[math], nan["fp32"])
+    assert nan[math][0, :, 4:7, 30:33].all() and int(nan[math].sum()) == 32 * (9 + 4)
