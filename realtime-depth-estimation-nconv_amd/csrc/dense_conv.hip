@@ -476,6 +476,54 @@ void dense_conv_bf9(nconv_dense_conv p, int ntx, int nty, int ncot) {
 // ---- weight packing: (Cout, Cin, kh, kw) [conv] / (Cin, Cout, 4, 4) [transposed] ->
 //      [class][cout tile][chunk][tap][ci 8][T], times an optional per-Cout scale (eval
 //      BatchNorm); channels past Cin / Cout are zero ----------------------------------------------
+// 3x3: one wave per (output-channel tile, input chunk, 8 output channels): their 8 x 8 x 9
+// weights (72 contiguous floats per output channel) read coalesced into LDS, then both images'
+// entries of those channels written from there (32-byte / 128-byte runs)
+template <int T>
+__global__ __launch_bounds__(64) void dense_pack3x3(int Cin, int Cout, const float* w, const float* scale,
+                                                    float* wp) {
+    constexpr int G = 8;  // output channels per wave
+    __shared__ float wt[G * 73];
+    const int nchunk = (Cin + kCK - 1) / kCK, ncot = (Cout + T - 1) / T;
+    int blk = blockIdx.x;
+    const int sub = blk % (T / G);
+    blk /= T / G;
+    const int ch = blk % nchunk, cot = blk / nchunk;
+    const int tid = threadIdx.x, c0 = sub * G;
+    float v[G * 72 / 64], sc[G * 72 / 64];  // all loads in flight together
+#pragma unroll
+    for (int k = 0; k < G * 72 / 64; ++k) {
+        const int e = tid + 64 * k, col = e / 72, rem = e - col * 72;
+        const int o = cot * T + c0 + col, ci = ch * kCK + rem / 9;
+        const bool in = o < Cout && ci < Cin;
+        v[k] = in ? w[((size_t)o * Cin + ch * kCK) * 9 + rem] : 0.f;
+        sc[k] = in && scale ? scale[o] : 1.f;
+    }
+#pragma unroll
+    for (int k = 0; k < G * 72 / 64; ++k) {
+        const int e = tid + 64 * k, col = e / 72, rem = e - col * 72;
+        wt[col * 73 + rem] = v[k] * sc[k];
+    }
+    __syncthreads();
+    float* f = wp + ((size_t)cot * nchunk + ch) * 9 * kCK * T;  // [tap][ci][T]
+    for (int e = tid; e < 72 * G; e += 64) {
+        const int col = e % G, r = e / G, cil = r % kCK, t = r / kCK;
+        f[r * T + c0 + col] = wt[col * 73 + cil * 9 + t];
+    }
+    unsigned char* img = reinterpret_cast<unsigned char*>(wp + (size_t)ncot * nchunk * 9 * kCK * T) +
+                         ((size_t)cot * nchunk + ch) * 30 * T * 16;
+    for (int e = tid; e < 30 * G; e += 64) {
+        const int col = e % G, r = e / G, kk = r % 2, part = (r / 2) % 3, s = r / 6, tap = 2 * s + kk;
+        float v[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) v[c] = tap < 9 ? wt[col * 73 + c * 9 + tap] : 0.f;
+        dbf16x8 sp[3];
+        dsplit3(v, sp);
+        *reinterpret_cast<dbf16x8*>(img + ((size_t)r * T + c0 + col) * 16) = part == 0 ? sp[0] : part == 1 ? sp[1] : sp[2];
+    }
+}
+
+// the other kinds: one thread per element of the fp32 image
 __global__ __launch_bounds__(kDT) void dense_pack(int kind, int Cin, int Cout, int T, const float* w,
                                                   const float* scale, float* wp) {
     const int taps = dense_taps(kind);
@@ -1009,53 +1057,28 @@ size_t dense_packed_floats(int kind, int Cin, int Cout) {
     return dense_fp32_floats(kind, Cin, Cout) + dense_bf9_floats(kind, Cin, Cout);
 }
 
-// one 16-byte row (8 input channels) of the pre-split image per thread: row = ((cot * nchunk + ch)
-// * 5 + s) * 3 + part) * 2 + half) * T + co, tap 2s + half (the tenth tap: zeros)
-__global__ __launch_bounds__(kDT) void dense_pack_bf9(int Cin, int Cout, int T, const float* w, const float* scale,
-                                                      unsigned char* img, size_t rows) {
-    const int nchunk = (Cin + kCK - 1) / kCK;
-    for (size_t e = (size_t)blockIdx.x * kDT + threadIdx.x; e < rows; e += (size_t)gridDim.x * kDT) {
-        const int co = (int)(e % T);
-        size_t r = e / T;
-        const int kk = (int)(r % 2);
-        r /= 2;
-        const int part = (int)(r % 3);
-        r /= 3;
-        const int s = (int)(r % 5);
-        r /= 5;
-        const int ch = (int)(r % nchunk);
-        const int cot = (int)(r / nchunk);
-        const int tap = 2 * s + kk, o = cot * T + co;
-        float v[8];
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-            const int ci = ch * kCK + c;
-            v[c] = 0.f;
-            if (tap < 9 && ci < Cin && o < Cout) {
-                v[c] = w[((size_t)o * Cin + ci) * 9 + tap];
-                if (scale) v[c] *= scale[o];  // the fp32 image's value, then split
-            }
-        }
-        dbf16x8 sp[3];
-        dsplit3(v, sp);
-        *reinterpret_cast<dbf16x8*>(img + e * 16) = part == 0 ? sp[0] : part == 1 ? sp[1] : sp[2];
-    }
-}
-
 int launch_dense_pack(int kind, int Cin, int Cout, const float* w, const float* scale, float* wp, hipStream_t st,
                       const char** why) {
+    if (kind == NCONV_DENSE_3X3) {
+        const int T = dense_cout_tile(Cout);
+        const int nb = ((Cout + T - 1) / T) * ((Cin + kCK - 1) / kCK) * (T / 8);
+        if (T == 32)
+            hipLaunchKernelGGL(dense_pack3x3<32>, dim3(nb), dim3(64), 0, st, Cin, Cout, w, scale, wp);
+        else
+            hipLaunchKernelGGL(dense_pack3x3<64>, dim3(nb), dim3(64), 0, st, Cin, Cout, w, scale, wp);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) {
+            *why = hipGetErrorString(e);
+            return -5;
+        }
+        return 0;
+    }
     const size_t n = dense_fp32_floats(kind, Cin, Cout);
     size_t blocks = (n + kDT - 1) / kDT;
     if (blocks > 4096) blocks = 4096;
     if (blocks)
         hipLaunchKernelGGL(dense_pack, dim3(blocks), dim3(kDT), 0, st, kind, Cin, Cout, dense_cout_tile(Cout), w,
                            scale, wp);
-    if (const size_t rows = dense_bf9_floats(kind, Cin, Cout) / 4) {
-        size_t b9 = (rows + kDT - 1) / kDT;
-        if (b9 > 4096) b9 = 4096;
-        hipLaunchKernelGGL(dense_pack_bf9, dim3(b9), dim3(kDT), 0, st, Cin, Cout, dense_cout_tile(Cout), w, scale,
-                           reinterpret_cast<unsigned char*>(wp + n), rows);
-    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         *why = hipGetErrorString(e);
