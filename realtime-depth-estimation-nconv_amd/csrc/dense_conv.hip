@@ -386,7 +386,7 @@ void dense_conv_bf9(nconv_dense_conv p, int ntx, int nty, int ncot) {
 #pragma unroll
         for (int k = 0; k < C::NWL; ++k) wv[k] = __builtin_amdgcn_raw_buffer_load_b128(rw, (tid + kDT * k) * 16, 0, 0);
     };
-    auto store_chunk = [&]() {
+    auto store_chunk = [&](unsigned char* L) {
 #pragma unroll
         for (int k = 0; k < C::NPP; ++k) {
             const int e = tid + kDT * k;
@@ -395,10 +395,10 @@ void dense_conv_bf9(nconv_dense_conv p, int ntx, int nty, int ncot) {
             const bool in = e < C::NPOS;  // past the tile: the dump slots (no branch)
             const int a = in ? e * 16 : C::DUMP, da = in ? C::PLANEB : 16;
 #pragma unroll
-            for (int i = 0; i < 3; ++i) *reinterpret_cast<dbf16x8*>(lds + a + i * da) = sp[i];
+            for (int i = 0; i < 3; ++i) *reinterpret_cast<dbf16x8*>(L + a + i * da) = sp[i];
         }
 #pragma unroll
-        for (int k = 0; k < C::NWL; ++k) *reinterpret_cast<du4*>(lds + C::WOFF + (tid + kDT * k) * 16) = wv[k];
+        for (int k = 0; k < C::NWL; ++k) *reinterpret_cast<du4*>(L + C::WOFF + (tid + kDT * k) * 16) = wv[k];
     };
 
     const int kk = lane >> 5, li = lane & 31;
@@ -413,13 +413,7 @@ void dense_conv_bf9(nconv_dense_conv p, int ntx, int nty, int ncot) {
 #pragma unroll
         for (int r = 0; r < C::RW; ++r) acc[m][r] = (f16v){};
 
-    load_chunk(0);
-#pragma unroll 1
-    for (int ch = 0; ch < nchunk; ++ch) {
-        if (ch) __syncthreads();
-        store_chunk();
-        __syncthreads();
-        load_chunk(ch + 1 < nchunk ? ch + 1 : ch);
+    auto mma_chunk = [&](const unsigned char* L) {
 #pragma unroll NCONV_DB9_KUNROLL
         for (int s = 0; s < 5; ++s) {
             const int t0 = 2 * s, dr = t0 / 3, dc = t0 % 3;
@@ -429,15 +423,15 @@ void dense_conv_bf9(nconv_dense_conv p, int ntx, int nty, int ncot) {
             for (int i = 0; i < 3; ++i)
 #pragma unroll
                 for (int m = 0; m < C::MT; ++m)
-                    av[i][m] = *reinterpret_cast<const dbf16x8*>(lds + abase + (s * 3 + i) * 2 * COUT * 16 + 32 * m * 16);
+                    av[i][m] = *reinterpret_cast<const dbf16x8*>(L + abase + (s * 3 + i) * 2 * COUT * 16 + 32 * m * 16);
 #pragma unroll
             for (int i = 0; i < 3; ++i)
 #pragma unroll
                 for (int r = 0; r < C::RW; ++r) {
-                    bv[i][r] = *reinterpret_cast<const dbf16x8*>(lds + bb + i * C::PLANEB + ((r + dr) * C::ROW + dc) * 16);
+                    bv[i][r] = *reinterpret_cast<const dbf16x8*>(L + bb + i * C::PLANEB + ((r + dr) * C::ROW + dc) * 16);
                     if (s == 4 && kk) bv[i][r] = (dbf16x8){};
                 }
-            // smallest terms first; NTERM 6 (bf16x6) drops the three below 2^-25 |v w|
+            // smallest terms first; NTERM 6 (bf16x6) drops the three below ~2^-23 |v w|
             constexpr int ti[9] = {2, 2, 1, 2, 1, 0, 1, 0, 0}, tj[9] = {2, 1, 2, 0, 1, 2, 0, 1, 0};
 #pragma unroll
             for (int q = 9 - NTERM; q < 9; ++q)
@@ -448,6 +442,17 @@ void dense_conv_bf9(nconv_dense_conv p, int ntx, int nty, int ncot) {
                         acc[m][r] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[ti[q]][m], bv[tj[q]][r], acc[m][r], 0, 0, 0);
             __builtin_amdgcn_sched_barrier(0);
         }
+    };
+
+    // (two LDS images, the next chunk stored under this one's MFMAs with one barrier per chunk,
+    // measured 7-13 % slower for the 32-channel tiles: two workgroups per CU instead of three)
+    load_chunk(0);
+#pragma unroll 1
+    for (int ch = 0; ch < nchunk; ++ch) {
+        store_chunk(lds);
+        __syncthreads();
+        load_chunk(ch + 1 < nchunk ? ch + 1 : ch);  // next chunk in flight during the MFMAs
+        mma_chunk(lds);
         __syncthreads();  // this chunk's MFMAs are done with the LDS
     }
     const int ox = ox0 + li;
