@@ -299,16 +299,19 @@ __global__ __launch_bounds__(kDT) void dense_conv_mfma(nconv_dense_conv p, int n
 // ------------------------------------------------------------------------------------------------
 typedef __bf16 dbf16x8 __attribute__((ext_vector_type(8)));
 
-template <int COUT>
+template <int COUT, int S = 1, bool SC = false>
 struct Db9Cfg {  // (16 rows for the 32-channel tiles, 2 waves/SIMD: not faster)
-    static constexpr int TH = 8, RW = TH / 4, TW = 32, MT = COUT / 32;
-    static constexpr int PR = TH + 2, PC = TW + 2, ROW = PC, NPOS = PR * PC;
+    static constexpr int TH = S == 1 ? 8 : 4, RW = TH / 4, TW = 32, MT = COUT / 32;
+    static constexpr int PR = (TH - 1) * S + 3, PC = (TW - 1) * S + 3, ROW = PC, NPOS = PR * PC;
     static constexpr int PLANEB = NPOS * 16;                         // bytes of one part's image
     static constexpr int DUMP = 3 * PLANEB;                          // slot of positions past the tile
     static constexpr int WOFF = DUMP + 3 * 16;                       // weight image (bytes)
     static constexpr int WROWS = 5 * 3 * 2 * COUT;                   // 16-byte rows per chunk
     static constexpr int NWL = (WROWS + kDT - 1) / kDT;              // rows per thread (the last
-    static constexpr int LDSB = WOFF + NWL * kDT * 16;               //  round's excess: zeros, past the image)
+    static constexpr int SOFF = WOFF + NWL * kDT * 16;               //  round's excess: zeros, past the image)
+    static constexpr int SROWS = SC ? 3 * 2 * COUT : 0;              // shortcut image rows per chunk
+    static constexpr int NSL = (SROWS + kDT - 1) / kDT;
+    static constexpr int LDSB = SOFF + NSL * kDT * 16;
     static constexpr int NPP = (NPOS + kDT - 1) / kDT;               // positions per thread
 };
 typedef unsigned du4 __attribute__((ext_vector_type(4)));
@@ -329,16 +332,22 @@ __device__ __forceinline__ void dsplit3(const float (&v)[8], dbf16x8 (&o)[3]) {
 #ifndef NCONV_DB9_KUNROLL
 #define NCONV_DB9_KUNROLL 5  // k-steps per unrolled body (1: 4 % slower)
 #endif
+#ifndef NCONV_DB9_S2
+#define NCONV_DB9_S2 1  // stride-2 3x3 on the split-bf16 kernel
+#endif
+#ifndef NCONV_DB9_SC
+#define NCONV_DB9_SC 1  // the fused 1x1 shortcut on the split-bf16 kernel
+#endif
 #ifndef NCONV_DB9_WAVES64
 #define NCONV_DB9_WAVES64 2
 #endif
 #ifndef NCONV_DB9_WAVES32
 #define NCONV_DB9_WAVES32 3
 #endif
-template <int COUT, int NTERM>
+template <int COUT, int NTERM, int S, bool SC>
 __global__ __launch_bounds__(kDT) __attribute__((amdgpu_waves_per_eu(COUT == 64 ? NCONV_DB9_WAVES64 : NCONV_DB9_WAVES32)))
 void dense_conv_bf9(nconv_dense_conv p, int ntx, int nty, int ncot) {
-    using C = Db9Cfg<COUT>;
+    using C = Db9Cfg<COUT, S, SC>;
     __shared__ __attribute__((aligned(16))) unsigned char lds[C::LDSB];
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -350,7 +359,7 @@ void dense_conv_bf9(nconv_dense_conv p, int ntx, int nty, int ncot) {
     const int cot = blk % ncot;
     const int b = blk / ncot;
     const int oy0 = ty * C::TH, ox0 = tx * C::TW;
-    const int iy0 = oy0 - 1, ix0 = ox0 - 1;
+    const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;
     const int Cin = p.C0 + p.C1;
     const int nchunk = (Cin + kCK - 1) / kCK;
     const int HW = p.H * p.W;
@@ -369,8 +378,12 @@ void dense_conv_bf9(nconv_dense_conv p, int ntx, int nty, int ncot) {
     // the pre-split weight image of (cot, chunk) behind the fp32 one (nconv_dense_pack)
     const unsigned char* wimg = reinterpret_cast<const unsigned char*>(p.wpack + (size_t)ncot * nchunk * 9 * kCK * COUT) +
                                 (size_t)cot * nchunk * C::WROWS * 16;
+    // the shortcut's pre-split image (a 1x1 nconv_dense_pack: [cot][chunk][part][half][co], half 1 zero)
+    const unsigned char* simg = SC ? reinterpret_cast<const unsigned char*>(p.wshort + (size_t)ncot * nchunk * kCK * COUT) +
+                                         (size_t)cot * nchunk * C::SROWS * 16
+                                   : nullptr;
     float pv[C::NPP][8];
-    du4 wv[C::NWL];
+    du4 wv[C::NWL], sv[SC ? C::NSL : 1];
     auto load_chunk = [&](int ch) {
         const int g0 = ch * kCK;
         const bool a = g0 < p.C0;
@@ -385,6 +398,12 @@ void dense_conv_bf9(nconv_dense_conv p, int ntx, int nty, int ncot) {
             (void*)(wimg + (size_t)ch * C::WROWS * 16), (short)0, C::WROWS * 16, 0x00020000);
 #pragma unroll
         for (int k = 0; k < C::NWL; ++k) wv[k] = __builtin_amdgcn_raw_buffer_load_b128(rw, (tid + kDT * k) * 16, 0, 0);
+        if constexpr (SC) {
+            const __amdgpu_buffer_rsrc_t rsc = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)(simg + (size_t)ch * C::SROWS * 16), (short)0, C::SROWS * 16, 0x00020000);
+#pragma unroll
+            for (int k = 0; k < C::NSL; ++k) sv[k] = __builtin_amdgcn_raw_buffer_load_b128(rsc, (tid + kDT * k) * 16, 0, 0);
+        }
     };
     auto store_chunk = [&](unsigned char* L) {
 #pragma unroll
@@ -399,19 +418,27 @@ void dense_conv_bf9(nconv_dense_conv p, int ntx, int nty, int ncot) {
         }
 #pragma unroll
         for (int k = 0; k < C::NWL; ++k) *reinterpret_cast<du4*>(L + C::WOFF + (tid + kDT * k) * 16) = wv[k];
+        if constexpr (SC) {
+#pragma unroll
+            for (int k = 0; k < C::NSL; ++k) *reinterpret_cast<du4*>(L + C::SOFF + (tid + kDT * k) * 16) = sv[k];
+        }
     };
 
     const int kk = lane >> 5, li = lane & 31;
     const int abase = C::WOFF + (kk * COUT + li) * 16;
-    const int rb = w * C::RW * C::ROW + li;
+    const int sbase = C::SOFF + (kk * COUT + li) * 16;
+    const int rb = w * C::RW * S * C::ROW + li * S;
     const int bbaseA = (rb + kk) * 16;               // k-steps 0, 2, 3, 4: tap 2s+1 one column right
     const int bbaseB = (rb + kk * (C::ROW - 2)) * 16;  // k-step 1: tap 3 = (1, 0), tap 2 = (0, 2)
 
-    f16v acc[C::MT][C::RW];
+    f16v acc[C::MT][C::RW], acs[SC ? C::MT : 1][SC ? C::RW : 1];
 #pragma unroll
     for (int m = 0; m < C::MT; ++m)
 #pragma unroll
-        for (int r = 0; r < C::RW; ++r) acc[m][r] = (f16v){};
+        for (int r = 0; r < C::RW; ++r) {
+            acc[m][r] = (f16v){};
+            if constexpr (SC) acs[m][r] = (f16v){};
+        }
 
     auto mma_chunk = [&](const unsigned char* L) {
 #pragma unroll NCONV_DB9_KUNROLL
@@ -428,7 +455,7 @@ void dense_conv_bf9(nconv_dense_conv p, int ntx, int nty, int ncot) {
             for (int i = 0; i < 3; ++i)
 #pragma unroll
                 for (int r = 0; r < C::RW; ++r) {
-                    bv[i][r] = *reinterpret_cast<const dbf16x8*>(L + bb + i * C::PLANEB + ((r + dr) * C::ROW + dc) * 16);
+                    bv[i][r] = *reinterpret_cast<const dbf16x8*>(L + bb + i * C::PLANEB + ((r * S + dr) * C::ROW + dc) * 16);
                     if (s == 4 && kk) bv[i][r] = (dbf16x8){};
                 }
             // smallest terms first; NTERM 6 (bf16x6) drops the three below ~2^-23 |v w|
@@ -440,6 +467,23 @@ void dense_conv_bf9(nconv_dense_conv p, int ntx, int nty, int ncot) {
 #pragma unroll
                     for (int r = 0; r < C::RW; ++r)
                         acc[m][r] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[ti[q]][m], bv[tj[q]][r], acc[m][r], 0, 0, 0);
+            if constexpr (SC) {
+                if (s == 2) {  // the 1x1 shortcut: the centre tap (lane half 0 of k-step 2; half 1's rows zero)
+                    dbf16x8 as[3][C::MT];
+#pragma unroll
+                    for (int i = 0; i < 3; ++i)
+#pragma unroll
+                        for (int m = 0; m < C::MT; ++m)
+                            as[i][m] = *reinterpret_cast<const dbf16x8*>(L + sbase + i * 2 * COUT * 16 + 32 * m * 16);
+#pragma unroll
+                    for (int q = 9 - NTERM; q < 9; ++q)
+#pragma unroll
+                        for (int m = 0; m < C::MT; ++m)
+#pragma unroll
+                            for (int r = 0; r < C::RW; ++r)
+                                acs[m][r] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as[ti[q]][m], bv[tj[q]][r], acs[m][r], 0, 0, 0);
+                }
+            }
             __builtin_amdgcn_sched_barrier(0);
         }
     };
@@ -473,6 +517,7 @@ void dense_conv_bf9(nconv_dense_conv p, int ntx, int nty, int ncot) {
                 const int co = co0 + cr + 4 * kk;
                 float v = acc[m][r][q] + ((p.bias && co < p.Cout) ? p.bias[co] : 0.f);
                 if (p.relu) v = fmaxf(v, 0.f);
+                if constexpr (SC) v += acs[m][r][q];
                 __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), ro, (int)lo, cr * HWo * 4, 0);
             }
     }
@@ -1052,11 +1097,34 @@ static size_t dense_fp32_floats(int kind, int Cin, int Cout) {
     return (size_t)ncls * ((Cout + T - 1) / T) * ((Cin + kCK - 1) / kCK) * dense_taps(kind) * kCK * T;
 }
 // 3x3: the fp32 image, then dense_conv_bf9's pre-split one ([cot][chunk][k-step][part][half][co]
-// rows of 8 bf16: 30 T rows of 16 bytes = 120 T floats per (cot, chunk))
+// rows of 8 bf16: 30 T rows of 16 bytes = 120 T floats per (cot, chunk)); 1x1 (the shortcut of
+// the split-bf16 3x3): [cot][chunk][part][half][co], half 1 zero: 6 T rows = 24 T floats
 static size_t dense_bf9_floats(int kind, int Cin, int Cout) {
-    if (kind != NCONV_DENSE_3X3) return 0;
+    if (kind != NCONV_DENSE_3X3 && kind != NCONV_DENSE_1X1) return 0;
     const int T = dense_cout_tile(Cout);
-    return (size_t)((Cout + T - 1) / T) * ((Cin + kCK - 1) / kCK) * 120 * T;
+    return (size_t)((Cout + T - 1) / T) * ((Cin + kCK - 1) / kCK) * (kind == NCONV_DENSE_3X3 ? 120 : 24) * T;
+}
+
+// the 1x1 pre-split image, one 16-byte row per thread
+__global__ __launch_bounds__(kDT) void dense_pack1x1_bf9(int Cin, int Cout, int T, const float* w, const float* scale,
+                                                         unsigned char* img, size_t rows) {
+    const int nchunk = (Cin + kCK - 1) / kCK;
+    for (size_t e = (size_t)blockIdx.x * kDT + threadIdx.x; e < rows; e += (size_t)gridDim.x * kDT) {
+        const int co = (int)(e % T);
+        const size_t r = e / T;
+        const int kk = (int)(r % 2), part = (int)((r / 2) % 3);
+        const size_t idx = r / 6;
+        const int ch = (int)(idx % nchunk), cot = (int)(idx / nchunk), o = cot * T + co;
+        float v[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const int ci = ch * kCK + c;
+            v[c] = kk == 0 && ci < Cin && o < Cout ? w[(size_t)o * Cin + ci] * (scale ? scale[o] : 1.f) : 0.f;
+        }
+        dbf16x8 sp[3];
+        dsplit3(v, sp);
+        *reinterpret_cast<dbf16x8*>(img + e * 16) = part == 0 ? sp[0] : part == 1 ? sp[1] : sp[2];
+    }
 }
 size_t dense_packed_floats(int kind, int Cin, int Cout) {
     return dense_fp32_floats(kind, Cin, Cout) + dense_bf9_floats(kind, Cin, Cout);
@@ -1084,6 +1152,12 @@ int launch_dense_pack(int kind, int Cin, int Cout, const float* w, const float* 
     if (blocks)
         hipLaunchKernelGGL(dense_pack, dim3(blocks), dim3(kDT), 0, st, kind, Cin, Cout, dense_cout_tile(Cout), w,
                            scale, wp);
+    if (const size_t rows = dense_bf9_floats(kind, Cin, Cout) / 4) {
+        size_t b9 = (rows + kDT - 1) / kDT;
+        if (b9 > 4096) b9 = 4096;
+        hipLaunchKernelGGL(dense_pack1x1_bf9, dim3(b9), dim3(kDT), 0, st, Cin, Cout, dense_cout_tile(Cout), w, scale,
+                           reinterpret_cast<unsigned char*>(wp + n), rows);
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         *why = hipGetErrorString(e);
@@ -1107,27 +1181,35 @@ static void go_dense(const nconv_dense_conv& p, hipStream_t st) {
                            nty, ncot);
 }
 
-// p.math BF16X9 / BF16X6: the 3x3 stride-1 convolutions without shortcut (and whose chunks do
-// not straddle the two sources) on dense_conv_bf9; every other shape keeps the fp32 MFMA kernel
-template <int COUT, int NTERM>
+// p.math BF16X9 / BF16X6: the 3x3 convolutions (stride 1 or 2, with or without the 1x1 shortcut)
+// whose chunks do not straddle the two sources on dense_conv_bf9; every other shape keeps the
+// fp32 MFMA kernel
+template <int COUT, int NTERM, int S, bool SC>
 static void go_dense_bf9(const nconv_dense_conv& p, hipStream_t st) {
-    using C = Db9Cfg<COUT>;
+    using C = Db9Cfg<COUT, S, SC>;
     const int ntx = (p.Wo + C::TW - 1) / C::TW, nty = (p.Ho + C::TH - 1) / C::TH;
     const int ncot = (p.Cout + COUT - 1) / COUT;
-    hipLaunchKernelGGL((dense_conv_bf9<COUT, NTERM>), dim3(ntx * nty * ncot * p.B), dim3(kDT), 0, st, p, ntx, nty,
-                       ncot);
+    hipLaunchKernelGGL((dense_conv_bf9<COUT, NTERM, S, SC>), dim3(ntx * nty * ncot * p.B), dim3(kDT), 0, st, p, ntx,
+                       nty, ncot);
+}
+template <int COUT, int NTERM>
+static void go_dense_bf9_s(const nconv_dense_conv& p, bool sc, hipStream_t st) {
+    if (p.stride == 1)
+        sc ? go_dense_bf9<COUT, NTERM, 1, true>(p, st) : go_dense_bf9<COUT, NTERM, 1, false>(p, st);
+    else
+        sc ? go_dense_bf9<COUT, NTERM, 2, true>(p, st) : go_dense_bf9<COUT, NTERM, 2, false>(p, st);
 }
 
 int launch_dense_conv(const nconv_dense_conv& p, hipStream_t st, const char** why) {
     const bool sc = p.wshort != nullptr;
     const int co = dense_cout_tile(p.Cout);
-    if (p.math != NCONV_DENSE_MATH_FP32 && p.kind == NCONV_DENSE_3X3 && p.stride == 1 && !sc &&
-        !(p.C1 > 0 && p.C0 % kCK != 0)) {
+    if (p.math != NCONV_DENSE_MATH_FP32 && p.kind == NCONV_DENSE_3X3 && !(p.C1 > 0 && p.C0 % kCK != 0) &&
+        (p.stride == 1 || NCONV_DB9_S2) && (!sc || NCONV_DB9_SC)) {
         const int nt = p.math == NCONV_DENSE_MATH_BF16X9 ? 9 : 6;
         if (co == 32)
-            nt == 9 ? go_dense_bf9<32, 9>(p, st) : go_dense_bf9<32, 6>(p, st);
+            nt == 9 ? go_dense_bf9_s<32, 9>(p, sc, st) : go_dense_bf9_s<32, 6>(p, sc, st);
         else
-            nt == 9 ? go_dense_bf9<64, 9>(p, st) : go_dense_bf9<64, 6>(p, st);
+            nt == 9 ? go_dense_bf9_s<64, 9>(p, sc, st) : go_dense_bf9_s<64, 6>(p, sc, st);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) {
             *why = hipGetErrorString(e);

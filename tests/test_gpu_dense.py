@@ -182,3 +182,38 @@ def test_dense_3x3_split_maths_nan_spread(nconv_amd, gpu, math, monkeypatch):
         nan[m] = torch.isnan(out).cpu()
     assert torch.equal(nan[math], nan["fp32"])
     assert nan[math][0, :, 4:7, 30:33].all() and int(nan[math].sum()) == 32 * (9 + 4)
+
+
+@pytest.mark.parametrize("math", ["fp32", "bf16x9", "bf16x6"])
+@pytest.mark.parametrize("stride,shortcut,cout,cin,H,W", [
+    (2, False, 64, 32, 15, 41),   # the encoder's stride-2 3x3 (training path: no fused shortcut)
+    (2, True, 64, 32, 15, 41),    # RGBEncoder eval: stride 2 with the fused 1x1 shortcut
+    (2, True, 32, 16, 21, 70),    # 32-channel tile, odd sizes
+    (1, True, 32, 3, 9, 33),      # rgb_encoder0: 3 input channels, stride 1 with shortcut
+    (1, True, 64, 64, 12, 40),
+])
+def test_dense_3x3_split_maths_stride_shortcut(nconv_amd, gpu, math, monkeypatch, stride, shortcut, cout, cin, H, W):
+    """relu(conv3x3_s(x) + b) [+ conv1x1_s(x)] under each nconv_dense_math against float64 of the same
+    fp32 operands, element-wise at 1e-6 x (|x| conv |w| + |b| [+ |x| conv |ws|])."""
+    D = nconv_amd.dense
+    g = torch.Generator().manual_seed(31 + cout + cin + stride)
+    r32 = lambda t: t.float().double()
+    B = 2
+    x = r32(_rand(g, B, cin, H, W))
+    w = r32(_rand(g, cout, cin, 3, 3) * 0.1)
+    ws = r32(_rand(g, cout, cin, 1, 1) * 0.1) if shortcut else None
+    bias = r32(_rand(g, cout))
+    ref = torch.relu(F.conv2d(x, w, stride=stride, padding=1) + bias.view(1, -1, 1, 1))
+    bound = F.conv2d(x.abs(), w.abs(), stride=stride, padding=1) + bias.abs().view(1, -1, 1, 1)
+    if shortcut:
+        ref = ref + F.conv2d(x, ws, stride=stride)
+        bound = bound + F.conv2d(x.abs(), ws.abs(), stride=stride)
+    bound = 1e-6 * bound + 1e-12
+    f = lambda t: None if t is None else t.to(gpu, torch.float32).contiguous()
+    monkeypatch.setattr(D, "MATH", math)
+    wp = D.pack(0, f(w), cin, cout)
+    wsp = D.pack(1, f(ws), cin, cout) if shortcut else None
+    got = D.conv(f(x), 0, stride, wp, f(bias), True, cout, wshort=wsp).double().cpu()
+    assert got.shape == ref.shape
+    err = (got - ref).abs()
+    assert (err <= bound).all(), f"{math}: worst err/bound {(err / bound).max().item():.3g}"

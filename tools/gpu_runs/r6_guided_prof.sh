@@ -4,7 +4,7 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out/gprof
 tag=$1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/gprof/p_$tag -o run -- \
-    python3 tools/guided_train_driver.py 4 > gpurun_out/gprof/log_$tag.txt 2>&1 || exit $?
+    python3 tools/${DRIVER:-guided_train_driver.py} ${REPS:-4} > gpurun_out/gprof/log_$tag.txt 2>&1 || exit $?
 f=$(find gpurun_out/gprof/p_$tag -name '*kernel_stats.csv' | head -1)
 cp "$f" gpurun_out/gprof/stats_$tag.csv
 rm -rf gpurun_out/gprof/p_$tag
