@@ -560,10 +560,10 @@ def cpu_baseline(B, H, W, seconds):
 # the arithmetic of the guided model's 3x3 stride-1 convolutions (dense.MATH; other kinds: fp32 MFMA)
 DENSE_ARITH = {
     "bf16x9": "exact products on the bf16 matrix cores (three-part split operands, all nine partial "
-              "products, fp32 accumulation); other convolution kinds fp32 MFMA",
+              "products, fp32 accumulation); the 1x1 convolutions fp32 MFMA",
     "fp32": "v_mfma_f32_32x32x2_f32 (exact fp32 products, fp32 accumulation) for every convolution",
     "bf16x6": "the six largest split-bf16 partial products (each product within ~2^-23 relative), "
-              "fp32 accumulation; other convolution kinds fp32 MFMA",
+              "fp32 accumulation; the 1x1 convolutions fp32 MFMA",
 }
 
 

@@ -384,9 +384,9 @@ typedef struct nconv_dense_conv {
     int math;                  /* enum nconv_dense_math (ABI 22; 0 = fp32 MFMA)                     */
 } nconv_dense_conv;
 
-/* Arithmetic of the 3x3 convolutions, stride 1 or 2, with or without the 1x1 shortcut (the RGB
- * encoder, the fusion decoder's ConvBlocks, their stride-1 input gradients) whose 8-channel input
- * chunks do not straddle the two sources; every other kind runs NCONV_DENSE_MATH_FP32.
+/* Arithmetic of every kind but the 1x1 (3x3 stride 1 or 2 with or without the 1x1 shortcut, the
+ * transposed 4x4, the 4x4 stride 2: the RGB encoder, the fusion decoder and their input
+ * gradients); the 1x1 always runs NCONV_DENSE_MATH_FP32.
  * Both split forms sum in fp32 on the matrix cores in another order than the fp32-MFMA kernel (an
  * fmaf chain), so results agree with it to fp32 accumulation error, not bitwise. */
 enum nconv_dense_math {
@@ -398,8 +398,8 @@ enum nconv_dense_math {
                                    ~2^-23 relative (the dropped v1*w2 + v2*w1 + v2*w2)             */
 };
 
-/* Floats of a packed weight buffer for (kind, Cin, Cout) (3x3 and 1x1: the fp32 image, then the
- * pre-split bf16 image of the split-bf16 maths, ABI 22). */
+/* Floats of a packed weight buffer for (kind, Cin, Cout) (the fp32 image, then the pre-split bf16
+ * image of the split-bf16 maths, ABI 22). */
 size_t nconv_dense_packed_floats(int kind, int Cin, int Cout);
 
 /* Pack w — Conv2d (Cout, Cin, k, k) or ConvTranspose2d (Cin, Cout, 4, 4) — into the kernel's

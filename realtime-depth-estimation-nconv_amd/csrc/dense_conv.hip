@@ -299,20 +299,31 @@ __global__ __launch_bounds__(kDT) void dense_conv_mfma(nconv_dense_conv p, int n
 // ------------------------------------------------------------------------------------------------
 typedef __bf16 dbf16x8 __attribute__((ext_vector_type(8)));
 
-template <int COUT, int S = 1, bool SC = false>
+template <int COUT, int KIND = NCONV_DENSE_3X3, int S = 1, bool SC = false>
 struct Db9Cfg {  // (16 rows for the 32-channel tiles, 2 waves/SIMD: not faster)
-    static constexpr int TH = S == 1 ? 8 : 4, RW = TH / 4, TW = 32, MT = COUT / 32;
-    static constexpr int PR = (TH - 1) * S + 3, PC = (TW - 1) * S + 3, ROW = PC, NPOS = PR * PC;
+    static constexpr bool TR = KIND == NCONV_DENSE_TRANSPOSED_4X4;  // four output-parity classes
+    static constexpr int TAPS = dense_taps(KIND), NKS = (TAPS + 1) / 2;  // k-steps: tap pairs
+    static constexpr int KS = KIND == NCONV_DENSE_CONV4X4_S2 ? 4 : 3;    // patch extent per pixel
+    static constexpr int SP = TR ? 1 : S;                            // patch stride
+    static constexpr int TH = SP == 1 ? 8 : 4, RW = TH / 4, TW = 32, MT = COUT / 32;
+    static constexpr int PR = (TH - 1) * SP + KS, PC = (TW - 1) * SP + KS, ROW = PC, NPOS = PR * PC;
     static constexpr int PLANEB = NPOS * 16;                         // bytes of one part's image
     static constexpr int DUMP = 3 * PLANEB;                          // slot of positions past the tile
     static constexpr int WOFF = DUMP + 3 * 16;                       // weight image (bytes)
-    static constexpr int WROWS = 5 * 3 * 2 * COUT;                   // 16-byte rows per chunk
+    static constexpr int WROWS = NKS * 3 * 2 * COUT;                 // 16-byte rows per chunk
     static constexpr int NWL = (WROWS + kDT - 1) / kDT;              // rows per thread (the last
     static constexpr int SOFF = WOFF + NWL * kDT * 16;               //  round's excess: zeros, past the image)
     static constexpr int SROWS = SC ? 3 * 2 * COUT : 0;              // shortcut image rows per chunk
     static constexpr int NSL = (SROWS + kDT - 1) / kDT;
     static constexpr int LDSB = SOFF + NSL * kDT * 16;
     static constexpr int NPP = (NPOS + kDT - 1) / kDT;               // positions per thread
+    // tap t's patch offset (row, column) from the pixel's patch origin (transposed: the parity
+    // class's (pa, pb) added at run time)
+    static constexpr int tr_(int t) { return TR ? 1 - t / 2 : t / KS; }
+    static constexpr int tc_(int t) { return TR ? 1 - t % 2 : t % KS; }
+    static constexpr int off(int t) { return tr_(t) * ROW + tc_(t); }
+    // lane half 1's offset from lane half 0's in k-step s (the padded tenth tap of a 3x3: 0)
+    static constexpr int delta(int s) { return 2 * s + 1 < TAPS ? off(2 * s + 1) - off(2 * s) : 0; }
 };
 typedef unsigned du4 __attribute__((ext_vector_type(4)));
 
@@ -338,16 +349,19 @@ __device__ __forceinline__ void dsplit3(const float (&v)[8], dbf16x8 (&o)[3]) {
 #ifndef NCONV_DB9_SC
 #define NCONV_DB9_SC 1  // the fused 1x1 shortcut on the split-bf16 kernel
 #endif
+#ifndef NCONV_DB9_TR
+#define NCONV_DB9_TR 1  // the transposed 4x4 and the 4x4 stride 2 on the split-bf16 kernel
+#endif
 #ifndef NCONV_DB9_WAVES64
 #define NCONV_DB9_WAVES64 2
 #endif
 #ifndef NCONV_DB9_WAVES32
 #define NCONV_DB9_WAVES32 3
 #endif
-template <int COUT, int NTERM, int S, bool SC>
+template <int COUT, int NTERM, int KIND, int S, bool SC>
 __global__ __launch_bounds__(kDT) __attribute__((amdgpu_waves_per_eu(COUT == 64 ? NCONV_DB9_WAVES64 : NCONV_DB9_WAVES32)))
 void dense_conv_bf9(nconv_dense_conv p, int ntx, int nty, int ncot) {
-    using C = Db9Cfg<COUT, S, SC>;
+    using C = Db9Cfg<COUT, KIND, S, SC>;
     __shared__ __attribute__((aligned(16))) unsigned char lds[C::LDSB];
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -357,9 +371,12 @@ void dense_conv_bf9(nconv_dense_conv p, int ntx, int nty, int ncot) {
     const int ty = blk % nty;
     blk /= nty;
     const int cot = blk % ncot;
-    const int b = blk / ncot;
-    const int oy0 = ty * C::TH, ox0 = tx * C::TW;
-    const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;
+    blk /= ncot;
+    const int cls = C::TR ? blk % 4 : 0;  // output parity class (transposed)
+    const int b = C::TR ? blk / 4 : blk;
+    const int pa = cls >> 1, pb = cls & 1;
+    const int oy0 = ty * C::TH, ox0 = tx * C::TW;  // tile origin (output grid, or class grid)
+    const int iy0 = oy0 * C::SP - 1, ix0 = ox0 * C::SP - 1;
     const int Cin = p.C0 + p.C1;
     const int nchunk = (Cin + kCK - 1) / kCK;
     const int HW = p.H * p.W;
@@ -374,10 +391,15 @@ void dense_conv_bf9(nconv_dense_conv p, int ntx, int nty, int ncot) {
         const bool in = e < C::NPOS && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
         poff[k] = in ? (unsigned)(iy * p.W + ix) * 4u : OOB;
     }
-    const int bytes0 = p.C0 * HW * 4, bytes1 = p.C1 * HW * 4;
-    // the pre-split weight image of (cot, chunk) behind the fp32 one (nconv_dense_pack)
-    const unsigned char* wimg = reinterpret_cast<const unsigned char*>(p.wpack + (size_t)ncot * nchunk * 9 * kCK * COUT) +
-                                (size_t)cot * nchunk * C::WROWS * 16;
+    // each source's planes of image b behind one resource; a chunk's channel c comes from x0 or
+    // x1 by a uniform select (a chunk may straddle the two), channels past Cin read past x1's end
+    const __amdgpu_buffer_rsrc_t rs0 = plane_rsrc(p.x0 + (size_t)b * p.C0 * HW, p.C0 * HW * 4);
+    const __amdgpu_buffer_rsrc_t rs1 =
+        plane_rsrc(p.C1 > 0 ? p.x1 + (size_t)b * p.C1 * HW : p.x0, p.C1 > 0 ? p.C1 * HW * 4 : 0);
+    // the pre-split weight image of (class, cot, chunk) behind the fp32 one (nconv_dense_pack)
+    const size_t fp32_floats = (size_t)(C::TR ? 4 : 1) * ncot * nchunk * C::TAPS * kCK * COUT;
+    const unsigned char* wimg = reinterpret_cast<const unsigned char*>(p.wpack + fp32_floats) +
+                                ((size_t)cls * ncot + cot) * nchunk * C::WROWS * 16;
     // the shortcut's pre-split image (a 1x1 nconv_dense_pack: [cot][chunk][part][half][co], half 1 zero)
     const unsigned char* simg = SC ? reinterpret_cast<const unsigned char*>(p.wshort + (size_t)ncot * nchunk * kCK * COUT) +
                                          (size_t)cot * nchunk * C::SROWS * 16
@@ -386,14 +408,15 @@ void dense_conv_bf9(nconv_dense_conv p, int ntx, int nty, int ncot) {
     du4 wv[C::NWL], sv[SC ? C::NSL : 1];
     auto load_chunk = [&](int ch) {
         const int g0 = ch * kCK;
-        const bool a = g0 < p.C0;
-        const float* base = a ? p.x0 + ((size_t)b * p.C0 + g0) * HW : p.x1 + ((size_t)b * p.C1 + (g0 - p.C0)) * HW;
-        const int nbytes = a ? bytes0 - g0 * HW * 4 : bytes1 - (g0 - p.C0) * HW * 4;
-        const __amdgpu_buffer_rsrc_t rs = plane_rsrc(base, nbytes);
 #pragma unroll
-        for (int k = 0; k < C::NPP; ++k)
+        for (int c = 0; c < 8; ++c) {
+            const int g = g0 + c;
+            const bool a = g < p.C0;
+            const __amdgpu_buffer_rsrc_t rs = a ? rs0 : rs1;
+            const int so = (a ? g : g - p.C0) * HW * 4;
 #pragma unroll
-            for (int c = 0; c < 8; ++c) pv[k][c] = ld_f32s(rs, poff[k], c * HW * 4);
+            for (int k = 0; k < C::NPP; ++k) pv[k][c] = ld_f32s(rs, poff[k], so);
+        }
         const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
             (void*)(wimg + (size_t)ch * C::WROWS * 16), (short)0, C::WROWS * 16, 0x00020000);
 #pragma unroll
@@ -427,9 +450,7 @@ void dense_conv_bf9(nconv_dense_conv p, int ntx, int nty, int ncot) {
     const int kk = lane >> 5, li = lane & 31;
     const int abase = C::WOFF + (kk * COUT + li) * 16;
     const int sbase = C::SOFF + (kk * COUT + li) * 16;
-    const int rb = w * C::RW * S * C::ROW + li * S;
-    const int bbaseA = (rb + kk) * 16;               // k-steps 0, 2, 3, 4: tap 2s+1 one column right
-    const int bbaseB = (rb + kk * (C::ROW - 2)) * 16;  // k-step 1: tap 3 = (1, 0), tap 2 = (0, 2)
+    const int bbase = ((w * C::RW * C::SP + (C::TR ? pa : 0)) * C::ROW + li * C::SP + (C::TR ? pb : 0)) * 16;
 
     f16v acc[C::MT][C::RW], acs[SC ? C::MT : 1][SC ? C::RW : 1];
 #pragma unroll
@@ -442,9 +463,9 @@ void dense_conv_bf9(nconv_dense_conv p, int ntx, int nty, int ncot) {
 
     auto mma_chunk = [&](const unsigned char* L) {
 #pragma unroll NCONV_DB9_KUNROLL
-        for (int s = 0; s < 5; ++s) {
-            const int t0 = 2 * s, dr = t0 / 3, dc = t0 % 3;
-            const int bb = s == 1 ? bbaseB : bbaseA;
+        for (int s = 0; s < C::NKS; ++s) {
+            // lane half 0: tap 2s, lane half 1: tap 2s + 1 (C::delta(s) positions further)
+            const int bb = bbase + (kk ? C::delta(s) * 16 : 0) + C::off(2 * s) * 16;
             dbf16x8 av[3][C::MT], bv[3][C::RW];
 #pragma unroll
             for (int i = 0; i < 3; ++i)
@@ -455,8 +476,8 @@ void dense_conv_bf9(nconv_dense_conv p, int ntx, int nty, int ncot) {
             for (int i = 0; i < 3; ++i)
 #pragma unroll
                 for (int r = 0; r < C::RW; ++r) {
-                    bv[i][r] = *reinterpret_cast<const dbf16x8*>(L + bb + i * C::PLANEB + ((r * S + dr) * C::ROW + dc) * 16);
-                    if (s == 4 && kk) bv[i][r] = (dbf16x8){};
+                    bv[i][r] = *reinterpret_cast<const dbf16x8*>(L + bb + i * C::PLANEB + r * C::SP * C::ROW * 16);
+                    if (2 * s + 1 == C::TAPS && kk) bv[i][r] = (dbf16x8){};  // the padded tap
                 }
             // smallest terms first; NTERM 6 (bf16x6) drops the three below ~2^-23 |v w|
             constexpr int ti[9] = {2, 2, 1, 2, 1, 0, 1, 0, 0}, tj[9] = {2, 1, 2, 0, 1, 2, 0, 1, 0};
@@ -499,6 +520,7 @@ void dense_conv_bf9(nconv_dense_conv p, int ntx, int nty, int ncot) {
         mma_chunk(lds);
         __syncthreads();  // this chunk's MFMAs are done with the LDS
     }
+    const int Hc = C::TR ? p.H : p.Ho, Wc = C::TR ? p.W : p.Wo;  // (class) grid
     const int ox = ox0 + li;
     const int HWo = p.Ho * p.Wo;
     const int co0 = cot * COUT;
@@ -507,8 +529,9 @@ void dense_conv_bf9(nconv_dense_conv p, int ntx, int nty, int ncot) {
 #pragma unroll
     for (int r = 0; r < C::RW; ++r) {
         const int oy = oy0 + w * C::RW + r;
-        const bool in = oy < p.Ho && ox < p.Wo;
-        const unsigned lo = in ? (unsigned)(4 * kk * HWo + oy * p.Wo + ox) * 4u : OOB;
+        const int oyo = C::TR ? 2 * oy + pa : oy, oxo = C::TR ? 2 * ox + pb : ox;
+        const bool in = oy < Hc && ox < Wc && oyo < p.Ho && oxo < p.Wo;  // (cropped transposed output)
+        const unsigned lo = in ? (unsigned)(4 * kk * HWo + oyo * p.Wo + oxo) * 4u : OOB;
 #pragma unroll
         for (int m = 0; m < C::MT; ++m)
 #pragma unroll
@@ -1096,30 +1119,51 @@ static size_t dense_fp32_floats(int kind, int Cin, int Cout) {
     const int T = dense_cout_tile(Cout);
     return (size_t)ncls * ((Cout + T - 1) / T) * ((Cin + kCK - 1) / kCK) * dense_taps(kind) * kCK * T;
 }
-// 3x3: the fp32 image, then dense_conv_bf9's pre-split one ([cot][chunk][k-step][part][half][co]
-// rows of 8 bf16: 30 T rows of 16 bytes = 120 T floats per (cot, chunk)); 1x1 (the shortcut of
-// the split-bf16 3x3): [cot][chunk][part][half][co], half 1 zero: 6 T rows = 24 T floats
+// the fp32 image, then dense_conv_bf9's pre-split one: rows of 8 bf16 (16 bytes) in
+// [class][cot][chunk][k-step][part][half][co] order, NKS k-steps of two taps (a padded odd tap and
+// the 1x1's second half zero): 6 NKS T rows = 24 NKS T floats per (class, cot, chunk)
 static size_t dense_bf9_floats(int kind, int Cin, int Cout) {
-    if (kind != NCONV_DENSE_3X3 && kind != NCONV_DENSE_1X1) return 0;
-    const int T = dense_cout_tile(Cout);
-    return (size_t)((Cout + T - 1) / T) * ((Cin + kCK - 1) / kCK) * (kind == NCONV_DENSE_3X3 ? 120 : 24) * T;
+    const int ncls = kind == NCONV_DENSE_TRANSPOSED_4X4 ? 4 : 1;
+    const int T = dense_cout_tile(Cout), nks = (dense_taps(kind) + 1) / 2;
+    return (size_t)ncls * ((Cout + T - 1) / T) * ((Cin + kCK - 1) / kCK) * 24 * nks * T;
 }
 
-// the 1x1 pre-split image, one 16-byte row per thread
-__global__ __launch_bounds__(kDT) void dense_pack1x1_bf9(int Cin, int Cout, int T, const float* w, const float* scale,
-                                                         unsigned char* img, size_t rows) {
-    const int nchunk = (Cin + kCK - 1) / kCK;
+// the pre-split image of the other kinds (1x1, transposed 4x4, 4x4 stride 2), one row per thread
+// (3x3: dense_pack3x3); values as dense_pack's, then split
+__global__ __launch_bounds__(kDT) void dense_pack_bf9(int kind, int Cin, int Cout, int T, const float* w,
+                                                      const float* scale, unsigned char* img, size_t rows) {
+    const int taps = dense_taps(kind), nks = (taps + 1) / 2;
+    const int nchunk = (Cin + kCK - 1) / kCK, ncot = (Cout + T - 1) / T;
     for (size_t e = (size_t)blockIdx.x * kDT + threadIdx.x; e < rows; e += (size_t)gridDim.x * kDT) {
-        const int co = (int)(e % T);
-        const size_t r = e / T;
-        const int kk = (int)(r % 2), part = (int)((r / 2) % 3);
-        const size_t idx = r / 6;
-        const int ch = (int)(idx % nchunk), cot = (int)(idx / nchunk), o = cot * T + co;
+        const int col = (int)(e % T);
+        size_t r = e / T;
+        const int kk = (int)(r % 2);
+        r /= 2;
+        const int part = (int)(r % 3);
+        r /= 3;
+        const int s = (int)(r % nks);
+        r /= nks;
+        const int ch = (int)(r % nchunk);
+        r /= nchunk;
+        const int cot = (int)(r % ncot), cls = (int)(r / ncot);
+        const int t = 2 * s + kk, co = cot * T + col;
         float v[8];
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
             const int ci = ch * kCK + c;
-            v[c] = kk == 0 && ci < Cin && o < Cout ? w[(size_t)o * Cin + ci] * (scale ? scale[o] : 1.f) : 0.f;
+            float x = 0.f;
+            if (t < taps && ci < Cin && co < Cout) {
+                if (kind == NCONV_DENSE_1X1) {
+                    x = w[(size_t)co * Cin + ci];
+                } else if (kind == NCONV_DENSE_CONV4X4_S2) {
+                    x = w[((size_t)co * Cin + ci) * 16 + t];
+                } else {  // ConvTranspose2d weight (Cin, Cout, 4, 4): class (pa, pb), tap (tr, tc)
+                    const int pa = cls >> 1, pb = cls & 1, tr = t >> 1, tc = t & 1;
+                    x = w[(((size_t)ci * Cout + co) * 4 + (1 - pa + 2 * tr)) * 4 + (1 - pb + 2 * tc)];
+                }
+                if (scale) x *= scale[co];
+            }
+            v[c] = x;
         }
         dbf16x8 sp[3];
         dsplit3(v, sp);
@@ -1155,8 +1199,8 @@ int launch_dense_pack(int kind, int Cin, int Cout, const float* w, const float* 
     if (const size_t rows = dense_bf9_floats(kind, Cin, Cout) / 4) {
         size_t b9 = (rows + kDT - 1) / kDT;
         if (b9 > 4096) b9 = 4096;
-        hipLaunchKernelGGL(dense_pack1x1_bf9, dim3(b9), dim3(kDT), 0, st, Cin, Cout, dense_cout_tile(Cout), w, scale,
-                           reinterpret_cast<unsigned char*>(wp + n), rows);
+        hipLaunchKernelGGL(dense_pack_bf9, dim3(b9), dim3(kDT), 0, st, kind, Cin, Cout, dense_cout_tile(Cout), w,
+                           scale, reinterpret_cast<unsigned char*>(wp + n), rows);
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
@@ -1181,35 +1225,41 @@ static void go_dense(const nconv_dense_conv& p, hipStream_t st) {
                            nty, ncot);
 }
 
-// p.math BF16X9 / BF16X6: the 3x3 convolutions (stride 1 or 2, with or without the 1x1 shortcut)
-// whose chunks do not straddle the two sources on dense_conv_bf9; every other shape keeps the
-// fp32 MFMA kernel
-template <int COUT, int NTERM, int S, bool SC>
+// p.math BF16X9 / BF16X6: every kind but the 1x1 (3x3 stride 1 or 2 with or without the fused
+// shortcut, the transposed 4x4 and the 4x4 stride 2) on dense_conv_bf9; the 1x1 (half of each
+// k-step would be padding) keeps the fp32 MFMA kernel
+template <int COUT, int NTERM, int KIND, int S, bool SC>
 static void go_dense_bf9(const nconv_dense_conv& p, hipStream_t st) {
-    using C = Db9Cfg<COUT, S, SC>;
-    const int ntx = (p.Wo + C::TW - 1) / C::TW, nty = (p.Ho + C::TH - 1) / C::TH;
+    using C = Db9Cfg<COUT, KIND, S, SC>;
+    const int Hc = C::TR ? p.H : p.Ho, Wc = C::TR ? p.W : p.Wo;
+    const int ntx = (Wc + C::TW - 1) / C::TW, nty = (Hc + C::TH - 1) / C::TH;
     const int ncot = (p.Cout + COUT - 1) / COUT;
-    hipLaunchKernelGGL((dense_conv_bf9<COUT, NTERM, S, SC>), dim3(ntx * nty * ncot * p.B), dim3(kDT), 0, st, p, ntx,
-                       nty, ncot);
+    hipLaunchKernelGGL((dense_conv_bf9<COUT, NTERM, KIND, S, SC>), dim3(ntx * nty * ncot * p.B * (C::TR ? 4 : 1)),
+                       dim3(kDT), 0, st, p, ntx, nty, ncot);
 }
 template <int COUT, int NTERM>
-static void go_dense_bf9_s(const nconv_dense_conv& p, bool sc, hipStream_t st) {
-    if (p.stride == 1)
-        sc ? go_dense_bf9<COUT, NTERM, 1, true>(p, st) : go_dense_bf9<COUT, NTERM, 1, false>(p, st);
+static void go_dense_bf9_k(const nconv_dense_conv& p, bool sc, hipStream_t st) {
+    if (p.kind == NCONV_DENSE_TRANSPOSED_4X4)
+        go_dense_bf9<COUT, NTERM, NCONV_DENSE_TRANSPOSED_4X4, 2, false>(p, st);
+    else if (p.kind == NCONV_DENSE_CONV4X4_S2)
+        go_dense_bf9<COUT, NTERM, NCONV_DENSE_CONV4X4_S2, 2, false>(p, st);
+    else if (p.stride == 1)
+        sc ? go_dense_bf9<COUT, NTERM, NCONV_DENSE_3X3, 1, true>(p, st) : go_dense_bf9<COUT, NTERM, NCONV_DENSE_3X3, 1, false>(p, st);
     else
-        sc ? go_dense_bf9<COUT, NTERM, 2, true>(p, st) : go_dense_bf9<COUT, NTERM, 2, false>(p, st);
+        sc ? go_dense_bf9<COUT, NTERM, NCONV_DENSE_3X3, 2, true>(p, st) : go_dense_bf9<COUT, NTERM, NCONV_DENSE_3X3, 2, false>(p, st);
 }
 
 int launch_dense_conv(const nconv_dense_conv& p, hipStream_t st, const char** why) {
     const bool sc = p.wshort != nullptr;
     const int co = dense_cout_tile(p.Cout);
-    if (p.math != NCONV_DENSE_MATH_FP32 && p.kind == NCONV_DENSE_3X3 && !(p.C1 > 0 && p.C0 % kCK != 0) &&
-        (p.stride == 1 || NCONV_DB9_S2) && (!sc || NCONV_DB9_SC)) {
+    const bool bf9_kind = p.kind == NCONV_DENSE_3X3 ? (p.stride == 1 || NCONV_DB9_S2) && (!sc || NCONV_DB9_SC)
+                                                   : p.kind != NCONV_DENSE_1X1 && NCONV_DB9_TR;
+    if (p.math != NCONV_DENSE_MATH_FP32 && bf9_kind) {
         const int nt = p.math == NCONV_DENSE_MATH_BF16X9 ? 9 : 6;
         if (co == 32)
-            nt == 9 ? go_dense_bf9_s<32, 9>(p, sc, st) : go_dense_bf9_s<32, 6>(p, sc, st);
+            nt == 9 ? go_dense_bf9_k<32, 9>(p, sc, st) : go_dense_bf9_k<32, 6>(p, sc, st);
         else
-            nt == 9 ? go_dense_bf9_s<64, 9>(p, sc, st) : go_dense_bf9_s<64, 6>(p, sc, st);
+            nt == 9 ? go_dense_bf9_k<64, 9>(p, sc, st) : go_dense_bf9_k<64, 6>(p, sc, st);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) {
             *why = hipGetErrorString(e);

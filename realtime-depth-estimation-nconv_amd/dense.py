@@ -21,11 +21,11 @@ from . import _lib
 from ._lib import DENSE_1X1, DENSE_3X3, DENSE_CONV4X4_S2, DENSE_TRANSPOSED_4X4  # noqa: F401  (re-exported)
 
 
-# Arithmetic of the 3x3 convolutions (include/nconv.h enum nconv_dense_math): "bf16x9"
+# Arithmetic of the convolutions other than the 1x1 (include/nconv.h enum nconv_dense_math): "bf16x9"
 # (default: exact products on the bf16 matrix cores -- three-part split operands, all nine partial
 # products, fp32 accumulation), "fp32" (v_mfma_f32_32x32x2_f32, exact products, an fmaf chain), or
 # "bf16x6" (the six largest partial products: each product within ~2^-23 relative; opt-in,
-# reported separately). Other convolution kinds always run the fp32 MFMA kernels.
+# reported separately). The 1x1 always runs the fp32 MFMA kernel.
 MATH = os.environ.get("NCONV_DENSE_MATH", "bf16x9")
 
 

@@ -30,9 +30,13 @@ def _rand(g, *shape):
     (1, 2, 64, 16, 0, 12, 40),    # 1x1 s2
     (2, 2, 32, 32, 1, 7, 19),     # ConvTranspose 4x4 s2 from cat(features, depth)
     (2, 2, 64, 1, 64, 6, 40),     # ConvTranspose with the 1-channel source first
+    (3, 2, 33, 32, 0, 12, 40),    # Conv 4x4 s2 (the transposed convolution's input gradient)
+    (3, 2, 64, 64, 1, 14, 38),    # ... 64-channel tile, two sources (even sizes: Ho = (H - 1) // 2 + 1 = H / 2)
 ])
-def test_dense_conv_kinds(nconv_amd, gpu, kind, stride, cout, c0, c1, H, W):
+@pytest.mark.parametrize("math", ["fp32", "bf16x9", "bf16x6"])
+def test_dense_conv_kinds(nconv_amd, gpu, monkeypatch, math, kind, stride, cout, c0, c1, H, W):
     D = nconv_amd.dense
+    monkeypatch.setattr(D, "MATH", math)
     g = torch.Generator().manual_seed(7 + kind * 10 + stride)
     B, cin = 2, c0 + c1
     x0, x1 = _rand(g, B, c0, H, W), (_rand(g, B, c1, H, W) if c1 else None)
@@ -40,6 +44,9 @@ def test_dense_conv_kinds(nconv_amd, gpu, kind, stride, cout, c0, c1, H, W):
     if kind == 2:
         w = _rand(g, cin, cout, 4, 4) * 0.1
         ref = F.conv_transpose2d(x, w, stride=2, padding=1)
+    elif kind == 3:
+        w = _rand(g, cout, cin, 4, 4) * 0.1
+        ref = F.conv2d(x, w, stride=2, padding=1)
     else:
         k = 3 if kind == 0 else 1
         w = _rand(g, cout, cin, k, k) * 0.1
