@@ -446,6 +446,9 @@ typedef struct nconv_dense_wgrad {
     float* gw;                 /* OVERWRITTEN: Conv2d (Cout, Cin, k, k) / ConvTranspose2d
                                   (Cin, Cout, 4, 4). Limits: Cout <= 96 (conv), Cin <= 96
                                   (transposed), Cin <= 64 (1x1)                                   */
+    int math;                  /* enum nconv_dense_math (ABI 22): the split-bf16 maths run the 3x3
+                                  stride-1 gradient of >= 33 input channels on the bf16 matrix
+                                  cores; every other shape the fp32 MFMA kernel                   */
 } nconv_dense_wgrad;
 
 /* Workspace of nconv_dense_conv_wgrad in bytes (0 if the descriptor is invalid). */

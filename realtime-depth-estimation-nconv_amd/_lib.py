@@ -113,7 +113,7 @@ class NconvDenseWgrad(ctypes.Structure):
     _fields_ = [("B", ctypes.c_int), ("kind", ctypes.c_int), ("stride", ctypes.c_int),
                 ("x0", ctypes.c_void_p), ("C0", ctypes.c_int), ("x1", ctypes.c_void_p), ("C1", ctypes.c_int),
                 ("H", ctypes.c_int), ("W", ctypes.c_int), ("gy", ctypes.c_void_p), ("Cout", ctypes.c_int),
-                ("Ho", ctypes.c_int), ("Wo", ctypes.c_int), ("gw", ctypes.c_void_p)]
+                ("Ho", ctypes.c_int), ("Wo", ctypes.c_int), ("gw", ctypes.c_void_p), ("math", ctypes.c_int)]
 
 
 class NconvBnTrain(ctypes.Structure):

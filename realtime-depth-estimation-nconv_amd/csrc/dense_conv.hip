@@ -352,6 +352,9 @@ __device__ __forceinline__ void dsplit3(const float (&v)[8], dbf16x8 (&o)[3]) {
 #ifndef NCONV_DB9_TR
 #define NCONV_DB9_TR 1  // the transposed 4x4 and the 4x4 stride 2 on the split-bf16 kernel
 #endif
+#ifndef NCONV_WB9
+#define NCONV_WB9 1  // the 3x3 stride-1 weight gradient on the split-bf16 kernel
+#endif
 #ifndef NCONV_DB9_WAVES64
 #define NCONV_DB9_WAVES64 2
 #endif
@@ -1112,6 +1115,186 @@ __global__ __launch_bounds__(256) void dense_wgrad_tr_rows(const float* __restri
 }
 
 // ------------------------------------------------------------------------------------------------
+// Weight gradient of the 3x3 stride-1 convolution on the bf16 matrix cores (split-bf16 maths):
+//   gW[co][ci][tap] = sum over pixels p of D[co][p] * X[ci][p + tap]
+// as nine GEMMs C_tap[co][ci] (M = 32 output channels, N = 32 input channels, K = pixels) on
+// v_mfma_f32_32x32x16_bf16, both operands split into three bf16 parts (nine or six terms, as the
+// forward). A = D[co][16 pixels]: 8 consecutive pixels per lane half, one ds_read_b128 of a
+// [part][co][pixel] image. B = X[16 pixels + tap][ci]: the patch image is channel-innermost
+// ([part][position][32 channels]), so a lane's 8 pixels of one channel are a column of it, read
+// with two ds_read_b64_tr_b16 (4 rows x 16 channels per 16-lane group, delivered column-major):
+// the tap shift moves whole 64-byte rows, so every address stays aligned (pixel-contiguous
+// images would put 7 of 9 taps' fragments off the 16-byte alignment ds_read_b128 needs).
+// Tiles, split-K slices and the partial layout are dense_wgrad_mfma<3x3, 1, 9, 1, 1>'s: a workgroup
+// owns 32 output channels x 32 input channels x 9 taps and walks a contiguous range of 4 x 32
+// pixel tiles; wave w takes tile row w; the four waves' tiles are summed in LDS in a fixed order
+// and the block writes one slice (dense_wgrad_reduce adds the slices in a fixed order).
+// ------------------------------------------------------------------------------------------------
+typedef short dv4s __attribute__((ext_vector_type(4)));
+typedef short dv8s __attribute__((ext_vector_type(8)));
+struct Wb9 {
+    static constexpr int TH = 4, TW = 32, NPX = TH * TW, PR = TH + 2, PC = TW + 2, NPOS = PR * PC;
+    static constexpr int PPART = NPOS * 64;          // bytes of one part's patch image (32 channels)
+    static constexpr int PDUMP = 3 * PPART;          // slots of positions past the patch
+    static constexpr int DB = NPX * 2 + 16;          // bytes per D row (16-byte pad: conflict-free A reads)
+    static constexpr int DOFF = PDUMP + 64;
+    static constexpr int DPART = 32 * DB;
+    static constexpr int LDSB = DOFF + 3 * DPART;    // (the epilogue reuses the first 16 KB)
+    static constexpr int NPW = (NPOS + 63) / 64;     // positions per lane (wave = one 8-channel group)
+};
+
+template <int NTERM>
+__global__ __launch_bounds__(kDT, 2) void dense_wgrad_bf9(WgdArgs a, float* __restrict__ part) {
+    using C = Wb9;
+    __shared__ __attribute__((aligned(16))) unsigned char lds[C::LDSB];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    int blk = blockIdx.x;
+    const int bn = blk % a.nbn;
+    blk /= a.nbn;
+    const int bm = blk % a.nbm, ks = blk / a.nbm;
+    const int m0 = bm * 32, c_lo = bn * 32;  // first output channel, first input channel
+    const int Cp = a.pC0 + a.pC1;
+    const long long t0 = a.ntiles * ks / a.nks, t1 = a.ntiles * (ks + 1) / a.nks;
+    const int HWp = a.Hp * a.Wp, HWs = a.Hs * a.Ws;
+    constexpr unsigned OOB = 0x80000000u;
+
+    // staging registers: wave w stages input channels c_lo + 8w .. + 7 at NPW positions per lane,
+    // and 2 (output channel, 8-pixel segment) items of D per thread
+    float xv[C::NPW][8], dv[2][8];
+    int tx_c = (int)(t0 % a.ntx), ty_c = (int)((t0 / a.ntx) % a.nty), b_c = (int)(t0 / ((long long)a.ntx * a.nty));
+    auto load_tile = [&](int tx, int ty, int b) {
+        const int py0 = ty * C::TH, px0 = tx * C::TW, iy0 = py0 - 1, ix0 = px0 - 1;
+        const __amdgpu_buffer_rsrc_t rp0 = plane_rsrc(a.p0 + (size_t)b * a.pC0 * HWs, a.pC0 * HWs * 4);
+        const __amdgpu_buffer_rsrc_t rp1 =
+            plane_rsrc(a.pC1 > 0 ? a.p1 + (size_t)b * a.pC1 * HWs : a.p0, a.pC1 > 0 ? a.pC1 * HWs * 4 : 0);
+        unsigned po[C::NPW];
+#pragma unroll
+        for (int k = 0; k < C::NPW; ++k) {
+            const int pos = lane + 64 * k, r = pos / C::PC, c = pos - r * C::PC;
+            const int iy = iy0 + r, ix = ix0 + c;
+            po[k] = pos < C::NPOS && (unsigned)iy < (unsigned)a.Hs && (unsigned)ix < (unsigned)a.Ws
+                        ? (unsigned)(iy * a.Ws + ix) * 4u : OOB;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int ci = c_lo + 8 * w + j;  // wave-uniform
+            const bool s0 = ci < a.pC0;
+            const __amdgpu_buffer_rsrc_t rs = s0 ? rp0 : rp1;
+            const int so = (s0 ? ci : ci - a.pC0) * HWs * 4;  // past Cp: out of range, reads 0
+#pragma unroll
+            for (int k = 0; k < C::NPW; ++k) xv[k][j] = ld_f32s(rs, po[k], so);
+        }
+        const __amdgpu_buffer_rsrc_t rd = plane_rsrc(a.d0 + (size_t)b * a.dC0 * HWp, a.dC0 * HWp * 4);
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int it = tid + kDT * k, col = it >> 4, seg = it & 15;
+            const int py = py0 + (seg >> 2), px = px0 + (seg & 3) * 8, co = m0 + col;
+            const bool ok = co < a.M && py < a.Hp;
+            const unsigned base = (unsigned)(co * HWp + py * a.Wp + px) * 4u;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) dv[k][j] = ld_f32(rd, ok && px + j < a.Wp ? base + 4u * j : OOB);
+        }
+    };
+    auto store_tile = [&]() {
+#pragma unroll
+        for (int k = 0; k < C::NPW; ++k) {
+            const int pos = lane + 64 * k;
+            dbf16x8 sp[3];
+            dsplit3(xv[k], sp);
+            const bool in = pos < C::NPOS;
+            const int at = in ? pos * 64 + w * 16 : C::PDUMP + w * 16, da = in ? C::PPART : 0;
+#pragma unroll
+            for (int i = 0; i < 3; ++i) *reinterpret_cast<dbf16x8*>(lds + at + i * da) = sp[i];
+        }
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int it = tid + kDT * k, col = it >> 4, seg = it & 15;
+            dbf16x8 sp[3];
+            dsplit3(dv[k], sp);
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+                *reinterpret_cast<dbf16x8*>(lds + C::DOFF + i * C::DPART + col * C::DB + seg * 16) = sp[i];
+        }
+    };
+    auto next_tile = [&]() {
+        if (++tx_c == a.ntx) {
+            tx_c = 0;
+            if (++ty_c == a.nty) {
+                ty_c = 0;
+                ++b_c;
+            }
+        }
+    };
+
+    const int kk = lane >> 5, li = lane & 31;
+    const int g = lane >> 4, il = lane & 15, q = il >> 2, pq = il & 3;
+    // A: D row li, pixels (tile row w, 16 k-step columns) + 8 kk
+    const int abase = C::DOFF + li * C::DB + (w * C::TW + 8 * kk) * 2;
+    // B (transposed reads): block row q = pixel 8 kk + 4 h + q of the k-step, channels
+    // 16 (g & 1) + 4 pq .. + 3
+    const int bbase = ((w * C::PC) + 8 * kk + q) * 64 + (16 * (g & 1) + 4 * pq) * 2;
+
+    f16v acc[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[t] = (f16v){};
+    typedef __attribute__((address_space(3))) dv4s* lds4_t;
+    auto trd = [&](int off) { return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4_t)(lds + off)); };
+
+    if (t0 < t1) load_tile(tx_c, ty_c, b_c);
+#pragma unroll 1
+    for (long long t = t0; t < t1; ++t) {
+        store_tile();
+        next_tile();
+        __syncthreads();
+        if (t + 1 < t1) load_tile(tx_c, ty_c, b_c);  // the next tile's loads in flight during the MFMAs
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {  // the two 16-pixel k-steps of the wave's tile row
+            dbf16x8 av[3];
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+                av[i] = *reinterpret_cast<const dbf16x8*>(lds + abase + i * C::DPART + s2 * 32);
+#pragma unroll
+            for (int tap = 0; tap < 9; ++tap) {
+                const int kh = tap / 3, kw = tap % 3;
+                const int bo = bbase + (kh * C::PC + s2 * 16 + kw) * 64;
+                dbf16x8 bv[3];
+#pragma unroll
+                for (int i = 0; i < 3; ++i) {
+                    const dv4s lo = trd(bo + i * C::PPART), hi = trd(bo + i * C::PPART + 4 * 64);
+                    const dv8s v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+                    bv[i] = __builtin_bit_cast(dbf16x8, v);
+                }
+                constexpr int ti[9] = {2, 2, 1, 2, 1, 0, 1, 0, 0}, tj[9] = {2, 1, 2, 0, 1, 2, 0, 1, 0};
+#pragma unroll
+                for (int qq = 9 - NTERM; qq < 9; ++qq)
+                    acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[ti[qq]], bv[tj[qq]], acc[tap], 0, 0, 0);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        __syncthreads();  // this tile's MFMAs are done with the LDS
+    }
+
+    // ---- the four waves' C_tap summed in LDS (fixed order), one slice per block: C[row = co][col = ci],
+    //      col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5) for register r ----
+    float* lf = reinterpret_cast<float*>(lds);
+    float* out = part + (size_t)ks * a.M * a.N;
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < 16; ++r) lf[(w * 16 + r) * 64 + lane] = acc[tap][r];
+        __syncthreads();
+        for (int e = tid; e < 1024; e += kDT) {
+            const int r = (e >> 6) & 15, l = e & 63;
+            const float v = ((lf[r * 64 + l] + lf[(16 + r) * 64 + l]) + lf[(32 + r) * 64 + l]) + lf[(48 + r) * 64 + l];
+            const int co = m0 + (r & 3) + 8 * (r >> 2) + 4 * (l >> 5), ci = c_lo + (l & 31);
+            if (co < a.M && ci < Cp) out[(size_t)co * a.N + ci * 9 + tap] = v;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
 // Launchers
 // ------------------------------------------------------------------------------------------------
 static size_t dense_fp32_floats(int kind, int Cin, int Cout) {
@@ -1314,7 +1497,12 @@ int launch_conv3x3_c1(const float* x, int B, int Cin, int H, int W, const float*
 struct WgdPlan {
     WgdArgs a;
     int nt, gm, gn, rg;
+    bool bf9;  // dense_wgrad_bf9
 };
+// the split-bf16 weight gradient: 3x3 stride 1 with whole 32-channel n-groups (Cin >= 33)
+static bool wgrad_bf9(const nconv_dense_wgrad& g, int nt) {
+    return g.math != NCONV_DENSE_MATH_FP32 && g.kind == NCONV_DENSE_3X3 && g.stride == 1 && nt == 9 && NCONV_WB9;
+}
 
 static WgdPlan wgrad_plan(const nconv_dense_wgrad& g) {
     WgdPlan pl{};
@@ -1355,8 +1543,9 @@ static WgdPlan wgrad_plan(const nconv_dense_wgrad& g) {
     pl.nt = wgd_nt(g.kind, a.N);
     const int nmg = (a.M + 31) / 32, nng = (a.N + 32 * pl.nt - 1) / (32 * pl.nt);
     // groups per workgroup: pairs along M and N where they divide evenly; the strided 3x3
-    // stages tall patches, so it pairs along M only
-    pl.gm = (pl.nt > 1 && nmg % 2 == 0) ? 2 : 1;
+    // stages tall patches, so it pairs along M only; dense_wgrad_bf9 takes one m-tile
+    pl.bf9 = wgrad_bf9(g, pl.nt);
+    pl.gm = (pl.nt > 1 && nmg % 2 == 0 && !pl.bf9) ? 2 : 1;
     // (LDS-DMA staging: one n-group per workgroup, so two workgroups fit a CU's LDS)
     pl.gn = 1;
     pl.rg = 4 / (pl.gm * pl.gn);
@@ -1464,10 +1653,18 @@ int launch_dense_wgrad(const nconv_dense_wgrad& g, float* ws, size_t ws_bytes, h
 static int launch_dense_wgrad_main(const nconv_dense_wgrad& g, float* ws, hipStream_t st, const char** why) {
     const WgdPlan pl = wgrad_plan(g);
     bool ok = false;
+    if (pl.bf9) {
+        const dim3 grid(pl.a.nbm * pl.a.nbn * pl.a.nks), blk(kDT);
+        if (g.math == NCONV_DENSE_MATH_BF16X9)
+            hipLaunchKernelGGL(dense_wgrad_bf9<9>, grid, blk, 0, st, pl.a, ws);
+        else
+            hipLaunchKernelGGL(dense_wgrad_bf9<6>, grid, blk, 0, st, pl.a, ws);
+        ok = true;
+    }
 #define NCONV_WG(KIND_, S_)                                                                     \
     if (g.kind == KIND_ && g.stride == S_)                                                     \
         ok = pl.nt == 1 ? go_wgrad<KIND_, S_, 1>(pl, ws, st) : go_wgrad<KIND_, S_, wgd_ntb(KIND_)>(pl, ws, st);
-    NCONV_WG(NCONV_DENSE_3X3, 1)
+    if (!ok) NCONV_WG(NCONV_DENSE_3X3, 1)
     NCONV_WG(NCONV_DENSE_3X3, 2)
     NCONV_WG(NCONV_DENSE_1X1, 1)
     NCONV_WG(NCONV_DENSE_1X1, 2)

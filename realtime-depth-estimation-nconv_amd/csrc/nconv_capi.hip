@@ -60,6 +60,8 @@ const char* validate_wgrad(const nconv_dense_wgrad* g) {
     if (g->B <= 0 || g->C0 <= 0 || g->C1 < 0 || g->H <= 0 || g->W <= 0 || g->Cout <= 0)
         return "non-positive B/C0/H/W/Cout";
     if (!g->x0 || (g->C1 > 0 && !g->x1) || !g->gy || !g->gw) return "null pointer";
+    if (g->math != NCONV_DENSE_MATH_FP32 && g->math != NCONV_DENSE_MATH_BF16X9 && g->math != NCONV_DENSE_MATH_BF16X6)
+        return "unknown math";
     const int cin = g->C0 + g->C1;
     switch (g->kind) {
         case NCONV_DENSE_3X3:

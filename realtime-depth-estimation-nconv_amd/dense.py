@@ -161,6 +161,7 @@ def wgrad(x0, x1, g, kind, stride, wshape):
     d.gy, d.Cout, d.Ho, d.Wo = g.data_ptr(), g.shape[1], g.shape[2], g.shape[3]
     gw = torch.empty(wshape, device=x0.device, dtype=torch.float32)
     d.gw = gw.data_ptr()
+    d.math = _lib.DENSE_MATHS[MATH]
     nbytes = L.nconv_dense_wgrad_workspace_bytes(ctypes.byref(d))
     ws = torch.empty(max(nbytes, 4) // 4, device=x0.device, dtype=torch.float32)
     _lib.check(L.nconv_dense_conv_wgrad(ctypes.byref(d), _lib.ptr(ws), nbytes, _lib.stream_handle(x0.device)),

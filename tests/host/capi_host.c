@@ -34,6 +34,7 @@ int main(void) {
     F(nconv_dense_wgrad, C0); F(nconv_dense_wgrad, x1); F(nconv_dense_wgrad, C1); F(nconv_dense_wgrad, H);
     F(nconv_dense_wgrad, W); F(nconv_dense_wgrad, gy); F(nconv_dense_wgrad, Cout); F(nconv_dense_wgrad, Ho);
     F(nconv_dense_wgrad, Wo); F(nconv_dense_wgrad, gw);
+    F(nconv_dense_wgrad, math);
     S(nconv_bwd_io);
     F(nconv_bwd_io, y); F(nconv_bwd_io, cout); F(nconv_bwd_io, gy); F(nconv_bwd_io, gcout); F(nconv_bwd_io, gxa);
     F(nconv_bwd_io, gca); F(nconv_bwd_io, gxb); F(nconv_bwd_io, gcb); F(nconv_bwd_io, gw); F(nconv_bwd_io, gbias);

@@ -40,9 +40,14 @@ CASES = [
 ]
 
 
+@pytest.mark.parametrize("math", ["bf16x9", "fp32", "bf16x6"])
 @pytest.mark.parametrize("kind,stride,c0,c1,cout,H,W,relu,bias", CASES)
-def test_dense_conv_fn_forward_backward(nconv_amd, gpu, kind, stride, c0, c1, cout, H, W, relu, bias):
+def test_dense_conv_fn_forward_backward(nconv_amd, gpu, monkeypatch, math, kind, stride, c0, c1, cout, H, W, relu,
+                                        bias):
+    """Forward, input and weight gradients under each nconv_dense_math (the split-bf16 weight
+    gradient runs the 3x3 stride-1 cases of >= 33 input channels)."""
     D = nconv_amd.dense
+    monkeypatch.setattr(D, "MATH", math)
     g = torch.Generator().manual_seed(kind * 1000 + c0 * 10 + cout + H)
     B, cin = 2, c0 + c1
     x0 = torch.randn(B, c0, H, W, generator=g, dtype=torch.float64)
