@@ -447,7 +447,7 @@ typedef struct nconv_dense_wgrad {
                                   (Cin, Cout, 4, 4). Limits: Cout <= 96 (conv), Cin <= 96
                                   (transposed), Cin <= 64 (1x1)                                   */
     int math;                  /* enum nconv_dense_math (ABI 22): the split-bf16 maths run the 3x3
-                                  stride-1 gradient of >= 33 input channels on the bf16 matrix
+                                  gradient (stride 1 or 2, >= 4 input channels) on the bf16 matrix
                                   cores; every other shape the fp32 MFMA kernel                   */
 } nconv_dense_wgrad;
 

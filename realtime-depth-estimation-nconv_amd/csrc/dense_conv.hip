@@ -353,7 +353,10 @@ __device__ __forceinline__ void dsplit3(const float (&v)[8], dbf16x8 (&o)[3]) {
 #define NCONV_DB9_TR 1  // the transposed 4x4 and the 4x4 stride 2 on the split-bf16 kernel
 #endif
 #ifndef NCONV_WB9
-#define NCONV_WB9 1  // the 3x3 stride-1 weight gradient on the split-bf16 kernel
+#define NCONV_WB9 1  // the 3x3 weight gradient on the split-bf16 kernel
+#endif
+#ifndef NCONV_WB9_S2
+#define NCONV_WB9_S2 1  // ... its stride-2 form too
 #endif
 #ifndef NCONV_DB9_WAVES64
 #define NCONV_DB9_WAVES64 2
@@ -1132,8 +1135,12 @@ __global__ __launch_bounds__(256) void dense_wgrad_tr_rows(const float* __restri
 // ------------------------------------------------------------------------------------------------
 typedef short dv4s __attribute__((ext_vector_type(4)));
 typedef short dv8s __attribute__((ext_vector_type(8)));
-struct Wb9 {
-    static constexpr int TH = 4, TW = 32, NPX = TH * TW, PR = TH + 2, PC = TW + 2, NPOS = PR * PC;
+template <int S>
+struct Wb9 {  // tiles as dense_wgrad_mfma's: 4 x 32 pixels (stride 2: 2 x 32, its patch is twice as wide)
+    static constexpr int TH = S == 1 ? 4 : 2, TW = 32, NPX = TH * TW;
+    static constexpr int PR = (TH - 1) * S + 3, PC = (TW - 1) * S + 3, NPOS = PR * PC;
+    static constexpr int PPW = NPX / 4, NKW = PPW / 16;  // pixels and 16-pixel k-steps per wave
+    static constexpr int NDI = 32 * NPX / 8 / kDT;      // D items (channel, 8 pixels) per thread
     static constexpr int PPART = NPOS * 64;          // bytes of one part's patch image (32 channels)
     static constexpr int PDUMP = 3 * PPART;          // slots of positions past the patch
     static constexpr int DB = NPX * 2 + 16;          // bytes per D row (16-byte pad: conflict-free A reads)
@@ -1143,9 +1150,9 @@ struct Wb9 {
     static constexpr int NPW = (NPOS + 63) / 64;     // positions per lane (wave = one 8-channel group)
 };
 
-template <int NTERM>
+template <int NTERM, int S>
 __global__ __launch_bounds__(kDT, 2) void dense_wgrad_bf9(WgdArgs a, float* __restrict__ part) {
-    using C = Wb9;
+    using C = Wb9<S>;
     __shared__ __attribute__((aligned(16))) unsigned char lds[C::LDSB];
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1161,10 +1168,10 @@ __global__ __launch_bounds__(kDT, 2) void dense_wgrad_bf9(WgdArgs a, float* __re
 
     // staging registers: wave w stages input channels c_lo + 8w .. + 7 at NPW positions per lane,
     // and 2 (output channel, 8-pixel segment) items of D per thread
-    float xv[C::NPW][8], dv[2][8];
+    float xv[C::NPW][8], dv[C::NDI][8];
     int tx_c = (int)(t0 % a.ntx), ty_c = (int)((t0 / a.ntx) % a.nty), b_c = (int)(t0 / ((long long)a.ntx * a.nty));
     auto load_tile = [&](int tx, int ty, int b) {
-        const int py0 = ty * C::TH, px0 = tx * C::TW, iy0 = py0 - 1, ix0 = px0 - 1;
+        const int py0 = ty * C::TH, px0 = tx * C::TW, iy0 = py0 * S - 1, ix0 = px0 * S - 1;
         const __amdgpu_buffer_rsrc_t rp0 = plane_rsrc(a.p0 + (size_t)b * a.pC0 * HWs, a.pC0 * HWs * 4);
         const __amdgpu_buffer_rsrc_t rp1 =
             plane_rsrc(a.pC1 > 0 ? a.p1 + (size_t)b * a.pC1 * HWs : a.p0, a.pC1 > 0 ? a.pC1 * HWs * 4 : 0);
@@ -1187,8 +1194,8 @@ __global__ __launch_bounds__(kDT, 2) void dense_wgrad_bf9(WgdArgs a, float* __re
         }
         const __amdgpu_buffer_rsrc_t rd = plane_rsrc(a.d0 + (size_t)b * a.dC0 * HWp, a.dC0 * HWp * 4);
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const int it = tid + kDT * k, col = it >> 4, seg = it & 15;
+        for (int k = 0; k < C::NDI; ++k) {
+            const int it = tid + kDT * k, col = it / (C::NPX / 8), seg = it % (C::NPX / 8);
             const int py = py0 + (seg >> 2), px = px0 + (seg & 3) * 8, co = m0 + col;
             const bool ok = co < a.M && py < a.Hp;
             const unsigned base = (unsigned)(co * HWp + py * a.Wp + px) * 4u;
@@ -1208,8 +1215,8 @@ __global__ __launch_bounds__(kDT, 2) void dense_wgrad_bf9(WgdArgs a, float* __re
             for (int i = 0; i < 3; ++i) *reinterpret_cast<dbf16x8*>(lds + at + i * da) = sp[i];
         }
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const int it = tid + kDT * k, col = it >> 4, seg = it & 15;
+        for (int k = 0; k < C::NDI; ++k) {
+            const int it = tid + kDT * k, col = it / (C::NPX / 8), seg = it % (C::NPX / 8);
             dbf16x8 sp[3];
             dsplit3(dv[k], sp);
 #pragma unroll
@@ -1229,11 +1236,13 @@ __global__ __launch_bounds__(kDT, 2) void dense_wgrad_bf9(WgdArgs a, float* __re
 
     const int kk = lane >> 5, li = lane & 31;
     const int g = lane >> 4, il = lane & 15, q = il >> 2, pq = il & 3;
-    // A: D row li, pixels (tile row w, 16 k-step columns) + 8 kk
-    const int abase = C::DOFF + li * C::DB + (w * C::TW + 8 * kk) * 2;
-    // B (transposed reads): block row q = pixel 8 kk + 4 h + q of the k-step, channels
-    // 16 (g & 1) + 4 pq .. + 3
-    const int bbase = ((w * C::PC) + 8 * kk + q) * 64 + (16 * (g & 1) + 4 * pq) * 2;
+    // the wave's pixels: tile row prow, columns pcol0 .. + PPW - 1
+    const int prow = w * C::PPW / C::TW, pcol0 = w * C::PPW % C::TW;
+    // A: D row li, pixels (the k-step's 16) + 8 kk
+    const int abase = C::DOFF + li * C::DB + (w * C::PPW + 8 * kk) * 2;
+    // B (transposed reads): block row q = pixel 8 kk + 4 h + q of the k-step (patch column S x its
+    // column), channels 16 (g & 1) + 4 pq .. + 3
+    const int bbase = (prow * S * C::PC + (pcol0 + 8 * kk + q) * S) * 64 + (16 * (g & 1) + 4 * pq) * 2;
 
     f16v acc[9];
 #pragma unroll
@@ -1249,7 +1258,7 @@ __global__ __launch_bounds__(kDT, 2) void dense_wgrad_bf9(WgdArgs a, float* __re
         __syncthreads();
         if (t + 1 < t1) load_tile(tx_c, ty_c, b_c);  // the next tile's loads in flight during the MFMAs
 #pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {  // the two 16-pixel k-steps of the wave's tile row
+        for (int s2 = 0; s2 < C::NKW; ++s2) {  // the wave's 16-pixel k-steps
             dbf16x8 av[3];
 #pragma unroll
             for (int i = 0; i < 3; ++i)
@@ -1257,11 +1266,11 @@ __global__ __launch_bounds__(kDT, 2) void dense_wgrad_bf9(WgdArgs a, float* __re
 #pragma unroll
             for (int tap = 0; tap < 9; ++tap) {
                 const int kh = tap / 3, kw = tap % 3;
-                const int bo = bbase + (kh * C::PC + s2 * 16 + kw) * 64;
+                const int bo = bbase + (kh * C::PC + s2 * 16 * S + kw) * 64;
                 dbf16x8 bv[3];
 #pragma unroll
                 for (int i = 0; i < 3; ++i) {
-                    const dv4s lo = trd(bo + i * C::PPART), hi = trd(bo + i * C::PPART + 4 * 64);
+                    const dv4s lo = trd(bo + i * C::PPART), hi = trd(bo + i * C::PPART + 4 * S * 64);
                     const dv8s v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
                     bv[i] = __builtin_bit_cast(dbf16x8, v);
                 }
@@ -1499,9 +1508,10 @@ struct WgdPlan {
     int nt, gm, gn, rg;
     bool bf9;  // dense_wgrad_bf9
 };
-// the split-bf16 weight gradient: 3x3 stride 1 with whole 32-channel n-groups (Cin >= 33)
+// the split-bf16 weight gradient: 3x3 (stride 1 or 2) with 32-channel x 9-tap n-groups (Cin >= 4)
 static bool wgrad_bf9(const nconv_dense_wgrad& g, int nt) {
-    return g.math != NCONV_DENSE_MATH_FP32 && g.kind == NCONV_DENSE_3X3 && g.stride == 1 && nt == 9 && NCONV_WB9;
+    return g.math != NCONV_DENSE_MATH_FP32 && g.kind == NCONV_DENSE_3X3 && nt == 9 && (g.stride == 1 || NCONV_WB9_S2) &&
+           NCONV_WB9;
 }
 
 static WgdPlan wgrad_plan(const nconv_dense_wgrad& g) {
@@ -1655,17 +1665,22 @@ static int launch_dense_wgrad_main(const nconv_dense_wgrad& g, float* ws, hipStr
     bool ok = false;
     if (pl.bf9) {
         const dim3 grid(pl.a.nbm * pl.a.nbn * pl.a.nks), blk(kDT);
-        if (g.math == NCONV_DENSE_MATH_BF16X9)
-            hipLaunchKernelGGL(dense_wgrad_bf9<9>, grid, blk, 0, st, pl.a, ws);
+        const bool x9 = g.math == NCONV_DENSE_MATH_BF16X9;
+        if (g.stride == 1 && x9)
+            hipLaunchKernelGGL((dense_wgrad_bf9<9, 1>), grid, blk, 0, st, pl.a, ws);
+        else if (g.stride == 1)
+            hipLaunchKernelGGL((dense_wgrad_bf9<6, 1>), grid, blk, 0, st, pl.a, ws);
+        else if (x9)
+            hipLaunchKernelGGL((dense_wgrad_bf9<9, 2>), grid, blk, 0, st, pl.a, ws);
         else
-            hipLaunchKernelGGL(dense_wgrad_bf9<6>, grid, blk, 0, st, pl.a, ws);
+            hipLaunchKernelGGL((dense_wgrad_bf9<6, 2>), grid, blk, 0, st, pl.a, ws);
         ok = true;
     }
 #define NCONV_WG(KIND_, S_)                                                                     \
     if (g.kind == KIND_ && g.stride == S_)                                                     \
         ok = pl.nt == 1 ? go_wgrad<KIND_, S_, 1>(pl, ws, st) : go_wgrad<KIND_, S_, wgd_ntb(KIND_)>(pl, ws, st);
     if (!ok) NCONV_WG(NCONV_DENSE_3X3, 1)
-    NCONV_WG(NCONV_DENSE_3X3, 2)
+    if (!ok) NCONV_WG(NCONV_DENSE_3X3, 2)
     NCONV_WG(NCONV_DENSE_1X1, 1)
     NCONV_WG(NCONV_DENSE_1X1, 2)
     NCONV_WG(NCONV_DENSE_TRANSPOSED_4X4, 2)

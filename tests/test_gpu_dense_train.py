@@ -45,7 +45,7 @@ CASES = [
 def test_dense_conv_fn_forward_backward(nconv_amd, gpu, monkeypatch, math, kind, stride, c0, c1, cout, H, W, relu,
                                         bias):
     """Forward, input and weight gradients under each nconv_dense_math (the split-bf16 weight
-    gradient runs the 3x3 stride-1 cases of >= 33 input channels)."""
+    gradient runs the 3x3 cases of >= 4 input channels)."""
     D = nconv_amd.dense
     monkeypatch.setattr(D, "MATH", math)
     g = torch.Generator().manual_seed(kind * 1000 + c0 * 10 + cout + H)

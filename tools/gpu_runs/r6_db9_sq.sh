@@ -9,7 +9,7 @@ C="SQ_WAVES SQ_INSTS_MFMA SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_VM
 SHAPE=${SHAPE:-conv 128->64}
 for arm in "$@"; do
   for P in A B C; do
-    env $arm DENSE_OPS=fwd timeout -k 10 90 rocprofv3 --pmc ${!P} --output-format csv -d gpurun_out/db9sq/${arm//[= \/]/_}_$P -o run -- \
+    env $arm DENSE_OPS=${OPS:-fwd} timeout -k 10 90 rocprofv3 --pmc ${!P} --output-format csv -d gpurun_out/db9sq/${arm//[= \/]/_}_$P -o run -- \
         python3 tools/dense_microbench.py "$SHAPE" > gpurun_out/db9sq/log_$P.txt 2>&1
     rc=$?; if fatal $rc; then echo "pass $P rc=$rc"; exit $rc; fi
   done
@@ -20,7 +20,7 @@ agg = collections.defaultdict(lambda: collections.defaultdict(list))
 for P in "ABC":
     for f in glob.glob(f"{sys.argv[1]}{P}/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
-            if "dense_conv" not in r["Kernel_Name"]:
+            if "dense_" not in r["Kernel_Name"] or "reduce" in r["Kernel_Name"] or "pack" in r["Kernel_Name"]:
                 continue
             agg[r["Kernel_Name"].split("(")[0]][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, v in agg.items():
