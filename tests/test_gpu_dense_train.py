@@ -37,6 +37,9 @@ CASES = [
     (2, 2, 1, 64, 64, 7, 20, False, False),     # Basic2dTrans on cat(depth, features): 65 -> 64
     (2, 2, 1, 32, 32, 9, 19, False, True),      # 33 -> 32, with bias
     (0, 1, 32, 0, 1, 14, 37, False, False),     # 3x3 to one channel through the generic tiles
+    (0, 1, 1, 32, 32, 11, 37, True, True),      # 33 input channels, the depth channel first (a chunk
+                                                #   straddling the sources; two weight-gradient n-groups)
+    (0, 2, 33, 0, 64, 13, 29, False, True),     # stride 2, 33 input channels, odd sizes
 ]
 
 
