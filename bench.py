@@ -10,7 +10,9 @@ reference's F.conv2d; include/nconv.h NCONV_MATH_FP32). Also on the same JSON li
   config5            B=16 1024x2048 forward (BASELINE configs[4]), both arithmetics, own roofline
   train_fwd_bwd_adamw  config 4b: EnforcePos drift + calculate_loss on the whole batch
                      (train_step1.py:63) + backward + AdamW, hipGraph-replayed, with its roofline
-  guided_fwd / guided_train_fwd_bwd_adamw  configs 3 / 4 with their fp32-MFMA fraction
+  guided_fwd / guided_train_fwd_bwd_adamw  configs 3 / 4 with their fraction of the fp32 MFMA peak
+                     in reference flops, under the default dense math (bf16x9: exact products on
+                     the bf16 matrix cores) and, in other_dense_math, the fp32-MFMA and bf16x6 ones
   layer_us / roofline  per-kernel device time of the headline forward and the roofline of its
                      dominant kernel (HIP events on the launch stream; profiles/ has the rocprofv3
                      summary of the same command)
