@@ -643,12 +643,18 @@ __global__ __launch_bounds__(kDT) void dense_pack(int kind, int Cin, int Cout, i
 
 // ---- 3x3 convolution to ONE output channel + residual (the depth heads, step2.py:259,278):
 //      out = conv3x3(x, pad 1) + res. Thread = 4 adjacent pixels of a 16 x 64 tile; input
-//      channels staged one plane at a time; weights are wave-uniform (SGPR). ---------------------
+//      channels staged NCONV_C1_CB planes per barrier (the next group's loads in flight during
+//      this group's FMAs; the sums in the same channel order as one plane at a time, bitwise);
+//      weights are wave-uniform (SGPR). ---------------------------------------------------------
+#ifndef NCONV_C1_CB
+#define NCONV_C1_CB 4
+#endif
 __global__ __launch_bounds__(kDT) void conv3x3_c1(const float* __restrict__ x, int Cin, int H, int W,
                                                  const float* __restrict__ wt, const float* __restrict__ res,
                                                  float* __restrict__ out, int ntx, int nty) {
-    constexpr int TW = 64, TH = 16, PW = TW + 2, PH = TH + 2;
-    __shared__ float pl[2][PH * PW];
+    constexpr int TW = 64, TH = 16, PW = TW + 2, PH = TH + 2, CB = NCONV_C1_CB;
+    constexpr int NE = (PH * PW + kDT - 1) / kDT;
+    __shared__ float pl[2][CB][PH * PW];
     int blk = blockIdx.x;
     const int tx = blk % ntx;
     blk /= ntx;
@@ -658,38 +664,50 @@ __global__ __launch_bounds__(kDT) void conv3x3_c1(const float* __restrict__ x, i
     const int y0 = ty * TH, x0 = tx * TW;
     const size_t HW = (size_t)H * W;
     float acc[4] = {0.f, 0.f, 0.f, 0.f};
-    float st[(PH * PW + kDT - 1) / kDT];
-    auto load = [&](int ci) {
+    float st[CB][NE];
+    unsigned off[NE];  // each staged element's offset in its plane (0x80000000: outside, reads 0)
 #pragma unroll
-        for (int k = 0; k < (PH * PW + kDT - 1) / kDT; ++k) {
-            const int e = tid + kDT * k;
-            const int pr = e / PW, pc = e - pr * PW;
-            const int iy = y0 - 1 + pr, ix = x0 - 1 + pc;
-            const bool in = e < PH * PW && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
-            st[k] = in ? x[((size_t)b * Cin + ci) * HW + (size_t)iy * W + ix] : 0.f;
-        }
+    for (int k = 0; k < NE; ++k) {
+        const int e = tid + kDT * k;
+        const int pr = e / PW, pc = e - pr * PW;
+        const int iy = y0 - 1 + pr, ix = x0 - 1 + pc;
+        const bool in = e < PH * PW && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+        off[k] = in ? (unsigned)(iy * W + ix) * 4u : 0x80000000u;
+    }
+    const __amdgpu_buffer_rsrc_t rx = plane_rsrc(x + (size_t)b * Cin * HW, (int)(Cin * HW * 4));
+    auto load = [&](int c) {  // channels c .. c + CB - 1 (past Cin: out of range, 0)
+#pragma unroll
+        for (int q = 0; q < CB; ++q)
+#pragma unroll
+            for (int k = 0; k < NE; ++k) st[q][k] = ld_f32s(rx, off[k], (c + q) * (int)HW * 4);
     };
     load(0);
 #pragma unroll 1
-    for (int ci = 0; ci < Cin; ++ci) {
-        float* t = pl[ci & 1];
+    for (int cg = 0; cg < Cin; cg += CB) {
+        float(*t)[PH * PW] = pl[(cg / CB) & 1];
 #pragma unroll
-        for (int k = 0; k < (PH * PW + kDT - 1) / kDT; ++k) {
-            const int e = tid + kDT * k;
-            if (e < PH * PW) t[e] = st[k];
-        }
+        for (int q = 0; q < CB; ++q)
+#pragma unroll
+            for (int k = 0; k < NE; ++k) {
+                const int e = tid + kDT * k;
+                if (e < PH * PW) t[q][e] = st[q][k];
+            }
         __syncthreads();
-        load(ci + 1 < Cin ? ci + 1 : ci);
-        const float* wr = wt + ci * 9;
+        load(cg + CB < Cin ? cg + CB : cg);
 #pragma unroll
-        for (int kh = 0; kh < 3; ++kh) {
-            float v[6];
+        for (int q = 0; q < CB; ++q) {
+            if (cg + q >= Cin) break;
+            const float* wr = wt + (cg + q) * 9;
 #pragma unroll
-            for (int m = 0; m < 6; ++m) v[m] = t[(r + kh) * PW + c0 + m];
+            for (int kh = 0; kh < 3; ++kh) {
+                float v[6];
 #pragma unroll
-            for (int kw = 0; kw < 3; ++kw)
+                for (int m = 0; m < 6; ++m) v[m] = t[q][(r + kh) * PW + c0 + m];
 #pragma unroll
-                for (int j = 0; j < 4; ++j) acc[j] = fmaf(wr[kh * 3 + kw], v[j + kw], acc[j]);
+                for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) acc[j] = fmaf(wr[kh * 3 + kw], v[j + kw], acc[j]);
+            }
         }
     }
     const int y = y0 + r;
